@@ -1,0 +1,139 @@
+/*
+ * sst.h -- C ABI of the MI355X mass-explanation engine (libsstgpu.so).
+ *
+ * Drop-in boundary for spectrseq/spectrseqtools' per-peak combinatorial
+ * search.  The reference has no FFI (it is pure Python); these entry points
+ * are what its hot-path functions call through ctypes in
+ * spectrseqtools_amd/_native.py.  Each declaration cites the reference
+ * interface it replaces (paths relative to the reference repo root).
+ *
+ * Conventions
+ *   - plain C types only; host pointers unless the name ends in _device;
+ *   - every function returns 0 on success or a negative SST_E* code; the
+ *     message is available from sst_last_error(ctx);
+ *   - one sst_ctx per HIP device; calls on one ctx are serialised; a table
+ *     belongs to the ctx that made it;
+ *   - masses are f64 Da; windows are quantised exactly as the reference does
+ *     (mass_explanation.py:107,110-114): target = round(mass/precision) with
+ *     ties-to-even, thr = ceil((thr_abs or tolerance*mass)/precision).
+ */
+#ifndef SST_H
+#define SST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- return codes ---------------------------------------------------- */
+#define SST_OK 0
+#define SST_E_ARG (-1)      /* bad argument / shape                         */
+#define SST_E_HIP (-2)      /* HIP runtime error                            */
+#define SST_E_NOMEM (-3)    /* device allocation failed                     */
+#define SST_E_TABLE (-4)    /* packed table violates the DP recurrence      */
+#define SST_E_INTERNAL (-5) /* depth/budget guard tripped                   */
+
+/* ---- per-query status of sst_explain_batch -------------------------- */
+#define SST_NONE 0          /* reference returns MassExplanations(None)      */
+#define SST_EMPTY 1         /* reference returns MassExplanations(set())     */
+#define SST_SOME 2          /* >= 1 candidate composition                    */
+#define SST_OUT_OF_TABLE (-1) /* reference raises (NameError in explain,    */
+                              /* NotImplementedError in is_valid_mass)      */
+#define SST_OVERFLOW (-2)   /* count > cap_per_query: exact count, no payload */
+#define SST_ABORTED (-4)    /* node budget exhausted: count is a lower bound */
+
+/* ---- per-query result of sst_is_valid_batch ------------------------- */
+/*  1 = True, 0 = False, -1 = reference raises NotImplementedError          */
+
+typedef struct sst_ctx sst_ctx;
+typedef struct sst_table sst_table;
+typedef struct sst_result sst_result;
+
+/* Number of visible HIP devices (0 when none). */
+int sst_device_count(void);
+
+/* One context per GPU (one process per GPU in multi-GPU runs). */
+int sst_ctx_create(int device, sst_ctx** out);
+void sst_ctx_destroy(sst_ctx* ctx);
+const char* sst_last_error(const sst_ctx* ctx);
+/* The HIP stream all work of this ctx is queued on (hipStream_t). */
+void* sst_ctx_stream(sst_ctx* ctx);
+/* Wait for all queued work of this ctx. */
+int sst_ctx_synchronize(sst_ctx* ctx);
+
+/* Build the packed 2-bit DP reachability table on the GPU.
+ * Replaces set_up_bit_table(integer_masses, max_mass, compression_rate)
+ * (spectrseqtools/mass_table.py:207-248; settings :251-289) and therefore
+ * load_dp_table / _reduce_nucleotide_list (:319-340, :102-121).
+ * masses: sorted unique integer masses incl. the 0 sentinel (row 0),
+ * n_rows <= 120; compression in {4, 8, 16, 32}. */
+int sst_table_build(sst_ctx* ctx, const int64_t* masses, int n_rows, int64_t max_mass, int compression,
+                    sst_table** out);
+
+/* Adopt an existing packed table (e.g. the reference's .npy cache,
+ * load_dp_table mass_table.py:319-340): words are n_rows x n_cols elements
+ * of compression/4 bytes, C order.  Fails with SST_E_TABLE if the table
+ * does not satisfy the row recurrence the engine's index relies on. */
+int sst_table_upload(sst_ctx* ctx, const int64_t* masses, int n_rows, const void* words, int64_t n_cols,
+                     int compression, sst_table** out);
+
+/* Row budgets the explain DFS reads from DynamicProgrammingTable.masses:
+ * is_mod[r] = NucleotideMass.is_modification, cap[r] =
+ * round(seq.max_len * NucleotideMass.modification_rate)
+ * (mass_explanation.py:158-172, :200). */
+int sst_table_set_budgets(sst_table* t, const uint8_t* is_mod, const int64_t* cap);
+
+int sst_table_shape(const sst_table* t, int* n_rows, int64_t* n_cols, int* compression);
+/* Copy the packed table to host (n_rows*n_cols*(compression/4) bytes):
+ * the DynamicProgrammingTable.table ndarray (mass_table.py:54). */
+int sst_table_download(sst_table* t, void* words_out);
+void sst_table_destroy(sst_table* t);
+
+/* is_valid_mass (mass_explanation.py:45-89), one result per query.
+ * thr_abs may be NULL (reference default threshold = tolerance*mass). */
+int sst_is_valid_batch(sst_table* t, const double* mass, const double* thr_abs, int64_t n, double tolerance,
+                       double precision, int8_t* out);
+/* Same on device buffers, queued on the ctx stream (no synchronisation). */
+int sst_is_valid_batch_device(sst_table* t, const double* d_mass, const double* d_thr_abs, int64_t n,
+                              double tolerance, double precision, int8_t* d_out);
+
+/* explain_mass_with_table (mass_explanation.py:92-203), batched.
+ *   max_mods: per-query budget array (may be NULL) else max_mods_scalar;
+ *             a negative value means np.inf (the reference default);
+ *   with_memo: the reference's with_memo flag (memo semantics reproduced
+ *             exactly, including budget-dependent first-visit effects);
+ *   cap_per_query: candidate cap; larger sets report SST_OVERFLOW with the
+ *             exact count and no payload.
+ * Results (host copies) through sst_result_* below. */
+int sst_explain_batch(sst_table* t, const double* mass, const double* thr_abs, int64_t n, double tolerance,
+                      double precision, const int64_t* max_mods, int64_t max_mods_scalar, int with_memo,
+                      uint64_t cap_per_query, sst_result** out);
+/* Same with inputs already in HBM; results stay on the device (fetch with
+ * sst_result_device / sst_result_fetch).  Queued on the ctx stream. */
+int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d_thr_abs, int64_t n,
+                             double tolerance, double precision, const int64_t* d_max_mods, int64_t max_mods_scalar,
+                             int with_memo, uint64_t cap_per_query, sst_result** out);
+
+/* Host views of a result (valid until sst_result_free):
+ *   status[n] (SST_NONE..), count[n] candidates, offset[n] byte offset of the
+ *   query's candidates in payload; payload = per candidate one length byte k
+ *   followed by k row indices (ascending, i.e. ascending mass). */
+int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count, const uint64_t** offset,
+                    const uint8_t** payload, uint64_t* payload_bytes);
+/* Device views (no copy). */
+int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint64_t** d_offset,
+                      uint8_t** d_payload, uint64_t* payload_bytes);
+/* Copy device results to the host views (synchronises the ctx stream). */
+int sst_result_fetch(sst_result* r);
+void sst_result_free(sst_result* r);
+
+/* Counters of the last explain launch, for measurement: queries resolved by
+ * the window scan alone, by the shallow / deep / exact / no-memo kernels,
+ * index records loaded (node expansions), payload bytes. */
+int sst_result_stats(const sst_result* r, uint64_t* stats_out /* [8] */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SST_H */

@@ -1,0 +1,613 @@
+/*
+ * sst_oracle.c -- CPU restatement of the reference's mass-explanation hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in spectrseqtools_amd/ links, loads or
+ * calls this file; only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg do, and only as the checker / the timed CPU baseline.
+ *
+ * Every function restates the reference literally -- same loop order, same
+ * memo key (total_mass, row) holding the full solution LIST, same budget
+ * bookkeeping -- so that it checks the GPU engine's reformulation rather than
+ * sharing it.  Reference = spectrseq/spectrseqtools v0.1.2:
+ *   ora_build_table         mass_table.py:207-248 (+ settings :251-289)
+ *   ora_is_valid            mass_explanation.py:45-89
+ *   ora_explain_table       mass_explanation.py:92-203 (backtrack :118-188)
+ *   ora_explain_recursion   mass_explanation.py:206-284
+ *   ora_length_bound        mass_table.py:343-487
+ * Quantisation (mass_explanation.py:107,114): target = round(mass/precision)
+ * (Python round = ties-to-even on the double quotient == rint), threshold =
+ * ceil(thr/precision); thr defaults to tolerance*mass (:110-111).
+ *
+ * Pinned against tests/golden/ (reference outputs): tests/test_oracle.py.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORA_INF_BUDGET (INT64_MAX / 4) /* np.inf: never reaches 0 by decrements */
+
+/* ------------------------------------------------------------------ */
+/* packed words of width C/4 bytes (C = 4, 8, 16, 32 masses per word)   */
+/* ------------------------------------------------------------------ */
+static inline uint64_t word_get(const void* t, int C, int64_t i) {
+    switch (C) {
+        case 4: return ((const uint8_t*)t)[i];
+        case 8: return ((const uint16_t*)t)[i];
+        case 16: return ((const uint32_t*)t)[i];
+        default: return ((const uint64_t*)t)[i];
+    }
+}
+static inline void word_set(void* t, int C, int64_t i, uint64_t v) {
+    switch (C) {
+        case 4: ((uint8_t*)t)[i] = (uint8_t)v; break;
+        case 8: ((uint16_t*)t)[i] = (uint16_t)v; break;
+        case 16: ((uint32_t*)t)[i] = (uint32_t)v; break;
+        default: ((uint64_t*)t)[i] = v; break;
+    }
+}
+static inline uint64_t width_mask(int C) { return C == 32 ? ~0ull : ((1ull << (2 * C)) - 1ull); }
+/* numpy semantics for `x << s` / `x >> s` on an unsigned scalar of width 2C bits:
+ * shifts >= width give 0, results truncated to the width. */
+static inline uint64_t shl(uint64_t x, int64_t s, int C) {
+    if (s >= 2 * C || s < 0) return 0;
+    return (x << s) & width_mask(C);
+}
+static inline uint64_t shr(uint64_t x, int64_t s, int C) {
+    if (s >= 2 * C || s < 0) return 0;
+    return x >> s;
+}
+
+int64_t ora_table_cols(int64_t max_mass, int C) {
+    /* max_col = int(np.ceil((max_mass + 1) / compression_rate))  mass_table.py:214 */
+    return (int64_t)ceil((double)(max_mass + 1) / (double)C);
+}
+
+/* mass_table.py:207-248.  out: rows x max_col words of C/4 bytes, C order. */
+int ora_build_table(const int64_t* masses, int n, int64_t max_mass, int C, void* out) {
+    if (C != 4 && C != 8 && C != 16 && C != 32) return -1;
+    const uint64_t full = width_mask(C);
+    uint64_t alt_first = 0, alt_sec = 0, init = 3ull << (2 * C - 2);
+    for (int k = 0; k < C; k++) {
+        alt_first |= 2ull << (2 * k);
+        alt_sec |= 1ull << (2 * k);
+    }
+    const int64_t cols = ora_table_cols(max_mass, C);
+    memset(out, 0, (size_t)n * (size_t)cols * (size_t)(C / 4));
+    word_set(out, C, 0, init);
+    for (int i = 1; i < n; i++) {
+        int64_t ri = (int64_t)i * cols, rp = (int64_t)(i - 1) * cols;
+        for (int64_t j = 0; j < cols; j++) {
+            uint64_t val = word_get(out, C, rp + j);
+            word_set(out, C, ri + j, (val | (val >> 1)) & alt_sec);
+        }
+        int64_t step = (int64_t)((double)masses[i] / (double)C); /* int(mass / C) :226 */
+        int64_t shift = masses[i] % C;                         /* :227 */
+        for (int64_t j = 0; j < cols; j++) {
+            /* each statement re-reads dp_table[i, j]: when step == 0 (mass < C)
+             * the first one has just updated it (:233-243) */
+            uint64_t x = word_get(out, C, ri + j);
+            if (step + j < cols) {
+                uint64_t y = shr(x, 2 * shift, C);
+                uint64_t add = alt_first & ((shl(y, 1, C)) | y);
+                word_set(out, C, ri + j + step, word_get(out, C, ri + j + step) | add);
+            }
+            x = word_get(out, C, ri + j);
+            if (shift != 0 && j + step + 1 < cols) {
+                uint64_t y = shl(x, 2 * (C - shift), C);
+                uint64_t add = alt_first & (shl(y, 1, C) | y);
+                word_set(out, C, ri + j + step + 1, word_get(out, C, ri + j + step + 1) | add);
+            }
+        }
+    }
+    /* dp_table[:, -1] &= full << 2 * (max_col - (max_mass + 1) % max_col)   :246 */
+    int64_t s = 2 * (cols - (max_mass + 1) % cols);
+    uint64_t mask = shl(full, s, C);
+    for (int i = 0; i < n; i++) {
+        int64_t idx = (int64_t)i * cols + cols - 1;
+        word_set(out, C, idx, word_get(out, C, idx) & mask);
+    }
+    return 0;
+}
+
+static inline int64_t q_target(double mass, double precision) { return (int64_t)rint(mass / precision); }
+static inline int64_t q_thr(double mass, double thr, double tolerance, double precision) {
+    if (isnan(thr)) thr = tolerance * mass;
+    return (int64_t)ceil(thr / precision);
+}
+
+/* current_value = table[row, m // C] >> 2 * (C - 1 - m % C)  (numpy: high bits kept) */
+static inline uint64_t cur_value(const void* t, int64_t cols, int C, int row, int64_t m) {
+    return word_get(t, C, (int64_t)row * cols + m / C) >> (2 * (C - 1 - m % C));
+}
+
+/* mass_explanation.py:45-89.  1 True, 0 False, -1 NotImplementedError. */
+int ora_is_valid(const void* table, int nrows, int64_t cols, int C, double mass, double threshold,
+                 double tolerance, double precision) {
+    int64_t target = q_target(mass, precision);
+    int64_t thr = q_thr(mass, threshold, tolerance, precision);
+    int row = nrows - 1;
+    for (int64_t v = target - thr; v < target + thr + 1; v++) {
+        if (v <= 0) continue;
+        if (v >= cols * C) return -1;
+        uint64_t cv = cur_value(table, cols, C, row, v);
+        if (cv % (uint64_t)C == 0) continue;
+        if (cv % 2 == 1 || (cv >> 1) % 2 == 1) return 1;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* arena + open-addressing memo                                        */
+/* ------------------------------------------------------------------ */
+typedef struct Arena {
+    char** blocks;
+    size_t nblocks, cap_blocks, used, block_size;
+} Arena;
+static void* arena_alloc(Arena* a, size_t n) {
+    n = (n + 15) & ~(size_t)15;
+    if (a->nblocks == 0 || a->used + n > a->block_size) {
+        size_t bs = n > (1u << 20) ? n : (1u << 20);
+        if (a->nblocks == a->cap_blocks) {
+            a->cap_blocks = a->cap_blocks ? 2 * a->cap_blocks : 16;
+            a->blocks = (char**)realloc(a->blocks, a->cap_blocks * sizeof(char*));
+        }
+        a->blocks[a->nblocks++] = (char*)malloc(bs);
+        a->block_size = bs;
+        a->used = 0;
+    }
+    void* p = a->blocks[a->nblocks - 1] + a->used;
+    a->used += n;
+    return p;
+}
+static void arena_free(Arena* a) {
+    for (size_t i = 0; i < a->nblocks; i++) free(a->blocks[i]);
+    free(a->blocks);
+    memset(a, 0, sizeof(*a));
+}
+
+typedef struct Memo {
+    uint64_t* keys; /* 0 = empty */
+    void** vals;
+    int64_t* ivals;
+    size_t cap, n;
+} Memo;
+static inline uint64_t mix(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    return k;
+}
+static void memo_init(Memo* m) {
+    m->cap = 1024;
+    m->n = 0;
+    m->keys = (uint64_t*)calloc(m->cap, 8);
+    m->vals = (void**)calloc(m->cap, sizeof(void*));
+    m->ivals = (int64_t*)calloc(m->cap, 8);
+}
+static void memo_free(Memo* m) {
+    free(m->keys);
+    free(m->vals);
+    free(m->ivals);
+    memset(m, 0, sizeof(*m));
+}
+static long memo_find(const Memo* m, uint64_t key) {
+    size_t i = mix(key) & (m->cap - 1);
+    while (m->keys[i]) {
+        if (m->keys[i] == key) return (long)i;
+        i = (i + 1) & (m->cap - 1);
+    }
+    return -1;
+}
+static void memo_put(Memo* m, uint64_t key, void* v, int64_t iv) {
+    if (2 * (m->n + 1) > m->cap) {
+        Memo g = {0};
+        g.cap = 2 * m->cap;
+        g.keys = (uint64_t*)calloc(g.cap, 8);
+        g.vals = (void**)calloc(g.cap, sizeof(void*));
+        g.ivals = (int64_t*)calloc(g.cap, 8);
+        for (size_t i = 0; i < m->cap; i++)
+            if (m->keys[i]) memo_put(&g, m->keys[i], m->vals[i], m->ivals[i]);
+        memo_free(m);
+        *m = g;
+    }
+    size_t i = mix(key) & (m->cap - 1);
+    while (m->keys[i] && m->keys[i] != key) i = (i + 1) & (m->cap - 1);
+    if (!m->keys[i]) m->n++;
+    m->keys[i] = key;
+    m->vals[i] = v;
+    m->ivals[i] = iv;
+}
+/* key over (total_mass, row); the memo only ever stores total_mass >= 1. */
+static inline uint64_t mkey(int64_t m, int row) { return ((uint64_t)m << 9) | (uint64_t)(row + 1); }
+
+/* A solution is a persistent cons list: `entry + [w]` == new cell -> entry. */
+typedef struct Cell {
+    const struct Cell* prev;
+    int32_t row;
+    int32_t len;
+} Cell;
+typedef struct SolList {
+    int64_t n;
+    const Cell** items; /* NULL item == the empty solution [] */
+} SolList;
+
+typedef struct Ctx {
+    const void* table;
+    int nrows, C;
+    int64_t cols;
+    const int64_t* w;
+    const uint8_t* is_mod;
+    const int64_t* cap;
+    int with_memo;
+    int error; /* 1: out-of-table raise */
+    Arena arena;
+    Memo memo;
+    int64_t lookups; /* table-cell reads, for the algorithmic-bytes count */
+} Ctx;
+
+static SolList EMPTY_LIST = {0, NULL};
+
+static SolList* list_new(Ctx* c, int64_t n) {
+    SolList* l = (SolList*)arena_alloc(&c->arena, sizeof(SolList));
+    l->n = n;
+    l->items = n ? (const Cell**)arena_alloc(&c->arena, (size_t)n * sizeof(Cell*)) : NULL;
+    return l;
+}
+
+/* mass_explanation.py:118-188 */
+static SolList* backtrack(Ctx* c, int64_t total_mass, int row, int64_t A, int64_t B) {
+    if (c->error) return &EMPTY_LIST;
+    if (c->with_memo && total_mass >= 1) {
+        long i = memo_find(&c->memo, mkey(total_mass, row));
+        if (i >= 0) return (SolList*)c->memo.vals[i];
+    }
+    if (total_mass < 0) return &EMPTY_LIST;
+    if (total_mass == 0) {
+        SolList* l = list_new(c, 1);
+        l->items[0] = NULL;
+        return l;
+    }
+    if (total_mass >= c->cols * c->C) {
+        c->error = 1; /* NameError raised while formatting the NotImplementedError */
+        return &EMPTY_LIST;
+    }
+    c->lookups++;
+    uint64_t cv = cur_value(c->table, c->cols, c->C, row, total_mass);
+    if (cv % (uint64_t)c->C == 0) return &EMPTY_LIST;
+    SolList* up = &EMPTY_LIST;
+    SolList* left = &EMPTY_LIST;
+    int32_t left_row = -1;
+    if (cv % 2 == 1) up = backtrack(c, total_mass, row - 1, A, c->cap[row - 1]);
+    if ((cv >> 1) % 2 == 1) {
+        if (!c->is_mod[row] || (A > 0 && B > 0)) {
+            if (c->is_mod[row]) {
+                A -= 1;
+                B -= 1;
+            }
+            left = backtrack(c, total_mass - c->w[row], row, A, B);
+            left_row = row;
+        }
+    }
+    SolList* sols = list_new(c, up->n + left->n);
+    for (int64_t i = 0; i < up->n; i++) sols->items[i] = up->items[i];
+    for (int64_t i = 0; i < left->n; i++) {
+        Cell* cell = (Cell*)arena_alloc(&c->arena, sizeof(Cell));
+        cell->prev = left->items[i];
+        cell->row = left_row;
+        cell->len = (left->items[i] ? left->items[i]->len : 0) + 1;
+        sols->items[up->n + i] = cell;
+    }
+    if (c->with_memo) memo_put(&c->memo, mkey(total_mass, row), sols, 0);
+    return sols;
+}
+
+/* Result: status 0 = MassExplanations(None), 1 = a set (maybe empty),
+ * -1 = raise.  Solutions are returned in the reference's list order as row
+ * indices in list order (ascending mass); empty solutions are dropped like
+ * convert_nucleotide_masses_to_names (:295-296) but counted in n_empty. */
+typedef struct ora_result {
+    int status;
+    int64_t n_solutions;
+    int64_t n_empty;
+    int64_t n_items;
+    int64_t lookups;
+    int32_t* lens;
+    int16_t* rows;
+} ora_result;
+
+void ora_result_free(ora_result* r) {
+    free(r->lens);
+    free(r->rows);
+    r->lens = NULL;
+    r->rows = NULL;
+}
+
+static void emit(ora_result* out, SolList** per_v, int64_t nv, int store) {
+    int64_t ns = 0, ne = 0, ni = 0;
+    for (int64_t k = 0; k < nv; k++)
+        for (int64_t i = 0; i < per_v[k]->n; i++) {
+            const Cell* s = per_v[k]->items[i];
+            if (!s) {
+                ne++;
+                continue;
+            }
+            ns++;
+            ni += s->len;
+        }
+    out->n_solutions = ns;
+    out->n_empty = ne;
+    out->n_items = ni;
+    out->status = (ns + ne) ? 1 : 0;
+    if (!store) return;
+    out->lens = (int32_t*)malloc((size_t)(ns ? ns : 1) * 4);
+    out->rows = (int16_t*)malloc((size_t)(ni ? ni : 1) * 2);
+    int64_t si = 0, pi = 0;
+    for (int64_t k = 0; k < nv; k++)
+        for (int64_t i = 0; i < per_v[k]->n; i++) {
+            const Cell* s = per_v[k]->items[i];
+            if (!s) continue;
+            out->lens[si++] = s->len;
+            int64_t p = pi + s->len;
+            for (const Cell* q = s; q; q = q->prev) out->rows[--p] = (int16_t)q->row;
+            pi += s->len;
+        }
+}
+
+/* mass_explanation.py:92-203.  A < 0 means np.inf. */
+int ora_explain_table(const void* table, int nrows, int64_t cols, int C, const int64_t* w, const uint8_t* is_mod,
+                      const int64_t* cap, double mass, double threshold, double tolerance, double precision,
+                      int64_t A, int with_memo, int store, ora_result* out) {
+    memset(out, 0, sizeof(*out));
+    Ctx c;
+    memset(&c, 0, sizeof(c));
+    c.table = table;
+    c.nrows = nrows;
+    c.C = C;
+    c.cols = cols;
+    c.w = w;
+    c.is_mod = is_mod;
+    c.cap = cap;
+    c.with_memo = with_memo;
+    memo_init(&c.memo);
+    int64_t target = q_target(mass, precision);
+    int64_t thr = q_thr(mass, threshold, tolerance, precision);
+    int64_t nv = 2 * thr + 1 > 0 ? 2 * thr + 1 : 0;
+    SolList** per_v = (SolList**)malloc((size_t)(nv ? nv : 1) * sizeof(SolList*));
+    int64_t a0 = A < 0 ? ORA_INF_BUDGET : A;
+    for (int64_t k = 0; k < nv; k++) {
+        per_v[k] = backtrack(&c, target - thr + k, nrows - 1, a0, cap[nrows - 1]);
+        if (c.error) break;
+    }
+    if (c.error) {
+        out->status = -1;
+    } else {
+        emit(out, per_v, nv, store);
+    }
+    out->lookups = c.lookups;
+    free(per_v);
+    memo_free(&c.memo);
+    arena_free(&c.arena);
+    return out->status;
+}
+
+/* ------------------------------------------------------------------ */
+/* mass_explanation.py:206-284 (explain_mass_with_recursion)           */
+/* ------------------------------------------------------------------ */
+typedef struct RCtx {
+    int n;
+    const int64_t* w;
+    const uint8_t* is_mod;
+    const int64_t* cap;
+    int64_t max_mods, thr;
+    Arena arena;
+    Memo memo;
+} RCtx;
+
+static SolList* rdp(RCtx* c, int64_t remaining, int start, int64_t used_all, int64_t used_ind) {
+    if (used_all > c->max_mods || used_ind > c->cap[start]) return &EMPTY_LIST;
+    uint64_t key = ((uint64_t)(remaining + (1ll << 40)) << 9) | (uint64_t)(start + 1);
+    long f = memo_find(&c->memo, key);
+    if (f >= 0) return (SolList*)c->memo.vals[f];
+    if (llabs(remaining) <= c->thr || remaining == 0) {
+        SolList* l = (SolList*)arena_alloc(&c->arena, sizeof(SolList));
+        l->n = 1;
+        l->items = (const Cell**)arena_alloc(&c->arena, sizeof(Cell*));
+        l->items[0] = NULL;
+        return l;
+    }
+    if (remaining < 0) return &EMPTY_LIST;
+    /* combinations.append([w_i] + combo): build the lists front-to-back */
+    int64_t total = 0;
+    SolList** subs = (SolList**)malloc((size_t)c->n * sizeof(SolList*));
+    for (int i = start; i < c->n; i++) {
+        int64_t wi = c->w[i];
+        subs[i] = rdp(c, remaining - wi, i, used_all + (c->is_mod[i] ? 1 : 0),
+                      i != start ? 0 : used_ind + (c->is_mod[i] ? 1 : 0));
+        total += subs[i]->n;
+    }
+    SolList* l = (SolList*)arena_alloc(&c->arena, sizeof(SolList));
+    l->n = total;
+    l->items = total ? (const Cell**)arena_alloc(&c->arena, (size_t)total * sizeof(Cell*)) : NULL;
+    int64_t k = 0;
+    for (int i = start; i < c->n; i++)
+        for (int64_t j = 0; j < subs[i]->n; j++) {
+            /* prepend row i: store lists reversed (cell chain = list order) */
+            Cell* cell = (Cell*)arena_alloc(&c->arena, sizeof(Cell));
+            cell->prev = subs[i]->items[j];
+            cell->row = i;
+            cell->len = (subs[i]->items[j] ? subs[i]->items[j]->len : 0) + 1;
+            l->items[k++] = cell;
+        }
+    free(subs);
+    memo_put(&c->memo, key, l, 0);
+    return l;
+}
+
+int ora_explain_recursion(int nrows, const int64_t* w, const uint8_t* is_mod, const int64_t* cap, double mass,
+                          double threshold, double tolerance, double precision, int64_t A, ora_result* out) {
+    memset(out, 0, sizeof(*out));
+    RCtx c;
+    memset(&c, 0, sizeof(c));
+    c.n = nrows;
+    c.w = w;
+    c.is_mod = is_mod;
+    c.cap = cap;
+    c.max_mods = A < 0 ? ORA_INF_BUDGET : A;
+    int64_t target = q_target(mass, precision);
+    c.thr = q_thr(mass, threshold, tolerance, precision);
+    memo_init(&c.memo);
+    SolList* root = rdp(&c, target, 1, 0, 0);
+    /* cells are chained first-element-outermost: cell(row_first) -> rest.  Emit in
+     * list order by walking the chain forward. */
+    int64_t ns = 0, ne = 0, ni = 0;
+    for (int64_t i = 0; i < root->n; i++) {
+        if (!root->items[i]) {
+            ne++;
+            continue;
+        }
+        ns++;
+        ni += root->items[i]->len;
+    }
+    out->n_solutions = ns;
+    out->n_empty = ne;
+    out->n_items = ni;
+    out->status = (ns + ne) ? 1 : 0;
+    out->lens = (int32_t*)malloc((size_t)(ns ? ns : 1) * 4);
+    out->rows = (int16_t*)malloc((size_t)(ni ? ni : 1) * 2);
+    int64_t si = 0, pi = 0;
+    for (int64_t i = 0; i < root->n; i++) {
+        const Cell* s = root->items[i];
+        if (!s) continue;
+        out->lens[si++] = s->len;
+        for (const Cell* q = s; q; q = q->prev) out->rows[pi++] = (int16_t)q->row;
+    }
+    memo_free(&c.memo);
+    arena_free(&c.arena);
+    return out->status;
+}
+
+/* ------------------------------------------------------------------ */
+/* mass_table.py:343-487 (compute_sequence_length_bound)               */
+/* ------------------------------------------------------------------ */
+typedef struct LCtx {
+    Ctx base;
+    int dir; /* 0 lower, 1 upper */
+    int64_t dflt;
+} LCtx;
+
+static int64_t lb_backtrack(LCtx* l, int64_t total_mass, int row, int64_t A, int64_t B) {
+    Ctx* c = &l->base;
+    if (c->error) return 0;
+    if (total_mass >= 1) {
+        long i = memo_find(&c->memo, mkey(total_mass, row));
+        if (i >= 0) return c->memo.ivals[i];
+    }
+    if (total_mass < 0) return l->dflt;
+    if (total_mass == 0) return 0;
+    if (total_mass >= c->cols * c->C) {
+        c->error = 1;
+        return 0;
+    }
+    uint64_t cv = cur_value(c->table, c->cols, c->C, row, total_mass);
+    if (cv % (uint64_t)c->C == 0) return l->dflt;
+    int64_t best = l->dflt;
+    if (cv % 2 == 1) {
+        int64_t v = lb_backtrack(l, total_mass, row - 1, A, c->cap[row - 1]);
+        best = l->dir ? (v > best ? v : best) : (v < best ? v : best);
+    }
+    if ((cv >> 1) % 2 == 1) {
+        if (!c->is_mod[row] || (A > 0 && B > 0)) {
+            if (c->is_mod[row]) {
+                A -= 1;
+                B -= 1;
+            }
+            int64_t v = lb_backtrack(l, total_mass - c->w[row], row, A, B) + 1;
+            best = l->dir ? (v > best ? v : best) : (v < best ? v : best);
+        }
+    }
+    memo_put(&c->memo, mkey(total_mass, row), NULL, best);
+    return best;
+}
+
+/* returns the bound, or INT64_MIN on the NameError raise. */
+int64_t ora_length_bound(const void* table, int nrows, int64_t cols, int C, const int64_t* w, const uint8_t* is_mod,
+                         const int64_t* cap, double su_mass, double obs_mass, double tolerance, double precision,
+                         int64_t max_len, int64_t max_mods, int dir) {
+    LCtx l;
+    memset(&l, 0, sizeof(l));
+    Ctx* c = &l.base;
+    c->table = table;
+    c->nrows = nrows;
+    c->C = C;
+    c->cols = cols;
+    c->w = w;
+    c->is_mod = is_mod;
+    c->cap = cap;
+    l.dir = dir;
+    l.dflt = dir ? -1 : max_len + 1;
+    memo_init(&c->memo);
+    int64_t target = q_target(su_mass, precision);
+    int64_t thr = (int64_t)ceil(tolerance * obs_mass / precision);
+    int64_t res = dir ? INT64_MIN : INT64_MAX;
+    for (int64_t v = target - thr; v < target + thr + 1; v++) {
+        int64_t b = lb_backtrack(&l, v, nrows - 1, max_mods, cap[nrows - 1]);
+        if (c->error) break;
+        res = dir ? (b > res ? b : res) : (b < res ? b : res);
+    }
+    memo_free(&c->memo);
+    if (c->error) return INT64_MIN;
+    if (res == l.dflt) res = dir ? max_len : 1;
+    return res;
+}
+
+/* ------------------------------------------------------------------ */
+/* batch drivers for the CPU baseline (bench.py cpu_baseline leg)       */
+/* ------------------------------------------------------------------ */
+int64_t ora_is_valid_batch(const void* table, int nrows, int64_t cols, int C, const double* mass, const double* thr,
+                           int64_t n, double tolerance, double precision, int nthreads, int8_t* out) {
+    int64_t ok = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : ok)
+#endif
+    for (int64_t i = 0; i < n; i++) {
+        int r = ora_is_valid(table, nrows, cols, C, mass[i], thr ? thr[i] : NAN, tolerance, precision);
+        if (out) out[i] = (int8_t)r;
+        ok += r == 1;
+    }
+    return ok;
+}
+
+/* per query: status (0 none / 1 set / -1 raise) and candidate count. Returns sum of counts. */
+int64_t ora_explain_batch(const void* table, int nrows, int64_t cols, int C, const int64_t* w, const uint8_t* is_mod,
+                          const int64_t* cap, const double* mass, const double* thr, const int64_t* A, int64_t n,
+                          double tolerance, double precision, int with_memo, int nthreads, int8_t* status,
+                          int64_t* count, int64_t* lookups) {
+    int64_t tot = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : tot)
+#endif
+    for (int64_t i = 0; i < n; i++) {
+        ora_result r;
+        ora_explain_table(table, nrows, cols, C, w, is_mod, cap, mass[i], thr ? thr[i] : NAN, tolerance, precision,
+                          A[i], with_memo, 0, &r);
+        if (status) status[i] = (int8_t)r.status;
+        if (count) count[i] = r.n_solutions;
+        if (lookups) lookups[i] = r.lookups;
+        tot += r.n_solutions;
+    }
+    return tot;
+}
+
+int ora_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}

@@ -1,0 +1,345 @@
+"""ctypes binding of libsstgpu.so (the C ABI in include/sst.h).
+
+This is the only way the Python mirror reaches the engine.  There is no CPU
+fallback: if the library is missing or no HIP device is visible, every entry
+point raises.  ctypes releases the GIL for the duration of each call.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SST_LIBRARY", os.path.join(_HERE, "libsstgpu.so"))
+
+# status codes (include/sst.h)
+SST_NONE, SST_EMPTY, SST_SOME = 0, 1, 2
+SST_OUT_OF_TABLE, SST_OVERFLOW, SST_ABORTED = -1, -2, -4
+
+# every function include/sst.h declares (checked by tests/test_boundary.py)
+EXPORTS = (
+    "sst_device_count", "sst_ctx_create", "sst_ctx_destroy", "sst_last_error", "sst_ctx_stream",
+    "sst_ctx_synchronize", "sst_table_build", "sst_table_upload", "sst_table_set_budgets", "sst_table_shape",
+    "sst_table_download", "sst_table_destroy", "sst_is_valid_batch", "sst_is_valid_batch_device",
+    "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
+    "sst_result_free", "sst_result_stats",
+)
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_I = ctypes.c_int
+_D = ctypes.c_double
+_PP = ctypes.POINTER(ctypes.c_void_p)
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def load_library(path=LIB_PATH):
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()' "
+            "or make -C spectrseqtools_amd/csrc)")
+    lib = ctypes.CDLL(path)
+    lib.sst_device_count.restype = _I
+    lib.sst_ctx_create.argtypes = [_I, _PP]
+    lib.sst_ctx_destroy.argtypes = [_P]
+    lib.sst_ctx_destroy.restype = None
+    lib.sst_last_error.argtypes = [_P]
+    lib.sst_last_error.restype = ctypes.c_char_p
+    lib.sst_ctx_stream.argtypes = [_P]
+    lib.sst_ctx_stream.restype = _P
+    lib.sst_ctx_synchronize.argtypes = [_P]
+    lib.sst_table_build.argtypes = [_P, _P, _I, _I64, _I, _PP]
+    lib.sst_table_upload.argtypes = [_P, _P, _I, _P, _I64, _I, _PP]
+    lib.sst_table_set_budgets.argtypes = [_P, _P, _P]
+    lib.sst_table_shape.argtypes = [_P, ctypes.POINTER(_I), ctypes.POINTER(_I64), ctypes.POINTER(_I)]
+    lib.sst_table_download.argtypes = [_P, _P]
+    lib.sst_table_destroy.argtypes = [_P]
+    lib.sst_table_destroy.restype = None
+    lib.sst_is_valid_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P]
+    lib.sst_is_valid_batch_device.argtypes = [_P, _P, _P, _I64, _D, _D, _P]
+    lib.sst_explain_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
+    lib.sst_explain_batch_device.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
+    lib.sst_result_host.argtypes = [_P, _PP, _PP, _PP, _PP, ctypes.POINTER(_U64)]
+    lib.sst_result_device.argtypes = [_P, _PP, _PP, _PP, _PP, ctypes.POINTER(_U64)]
+    lib.sst_result_fetch.argtypes = [_P]
+    lib.sst_result_free.argtypes = [_P]
+    lib.sst_result_free.restype = None
+    lib.sst_result_stats.argtypes = [_P, _P]
+    return lib
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def lib():
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            _lib = load_library()
+        return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+_DT = {4: np.uint8, 8: np.uint16, 16: np.uint32, 32: np.uint64}
+
+
+class Engine:
+    """One HIP device context (one per process per GPU)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        n = L.sst_device_count()
+        if n <= 0:
+            raise EngineError("no HIP device visible: the mass-explanation engine runs on MI355X only")
+        if device >= n:
+            raise EngineError(f"HIP device {device} not present ({n} visible)")
+        h = ctypes.c_void_p()
+        rc = L.sst_ctx_create(int(device), ctypes.byref(h))
+        if rc != 0:
+            raise EngineError(f"sst_ctx_create({device}) failed with {rc}")
+        self.handle = h
+        self.device = device
+        self._lib = L
+
+    def check(self, rc, what):
+        if rc != 0:
+            msg = self._lib.sst_last_error(self.handle)
+            raise EngineError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    @property
+    def stream(self):
+        return self._lib.sst_ctx_stream(self.handle)
+
+    def synchronize(self):
+        self.check(self._lib.sst_ctx_synchronize(self.handle), "sst_ctx_synchronize")
+
+    def close(self):
+        if self.handle:
+            self._lib.sst_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_engines = {}
+_engines_lock = threading.Lock()
+
+
+def default_device():
+    for k in ("SST_DEVICE", "LOCAL_RANK"):
+        if os.environ.get(k, "").isdigit():
+            return int(os.environ[k])
+    return 0
+
+
+def get_engine(device=None):
+    device = default_device() if device is None else device
+    with _engines_lock:
+        if device not in _engines:
+            _engines[device] = Engine(device)
+        return _engines[device]
+
+
+class ExplainResult:
+    """Host (or device) views of one sst_explain_batch* call."""
+
+    def __init__(self, engine, handle, n):
+        self.engine = engine
+        self.handle = handle
+        self.n = n
+        self.status = self.count = self.offset = self.payload = None
+
+    def fetch(self):
+        L = self.engine._lib
+        if self.status is None:
+            pass
+        st, cnt, off, pay = (ctypes.c_void_p() for _ in range(4))
+        nb = _U64()
+        self.engine.check(L.sst_result_host(self.handle, ctypes.byref(st), ctypes.byref(cnt), ctypes.byref(off),
+                                            ctypes.byref(pay), ctypes.byref(nb)), "sst_result_host")
+        n = self.n
+
+        def view(p, dtype, k):
+            if k == 0 or not p.value:
+                return np.zeros(0, dtype)
+            return np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(np.ctypeslib.as_ctypes_type(dtype))),
+                                         shape=(k,)).copy()
+
+        self.status = view(st, np.int8, n)
+        self.count = view(cnt, np.uint64, n)
+        self.offset = view(off, np.uint64, n)
+        self.payload = view(pay, np.uint8, int(nb.value))
+        return self
+
+    def stats(self):
+        out = np.zeros(8, np.uint64)
+        self.engine.check(self.engine._lib.sst_result_stats(self.handle, _ptr(out)), "sst_result_stats")
+        return out
+
+    def device_views(self):
+        L = self.engine._lib
+        st, cnt, off, pay = (ctypes.c_void_p() for _ in range(4))
+        nb = _U64()
+        self.engine.check(L.sst_result_device(self.handle, ctypes.byref(st), ctypes.byref(cnt), ctypes.byref(off),
+                                              ctypes.byref(pay), ctypes.byref(nb)), "sst_result_device")
+        return st.value, cnt.value, off.value, pay.value, int(nb.value)
+
+    def fetch_device(self):
+        self.engine.check(self.engine._lib.sst_result_fetch(self.handle), "sst_result_fetch")
+        return self.fetch()
+
+    def candidates(self, i):
+        """Row-index tuples of query i (ascending rows), in engine order."""
+        k = int(self.count[i])
+        p = int(self.offset[i])
+        out = []
+        pay = self.payload
+        for _ in range(k):
+            ln = int(pay[p])
+            out.append(tuple(int(x) for x in pay[p + 1:p + 1 + ln]))
+            p += 1 + ln
+        return out
+
+    def close(self):
+        if self.handle:
+            self.engine._lib.sst_result_free(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceTable:
+    """A packed DP table plus its derived index, resident in HBM."""
+
+    def __init__(self, engine, handle, n_rows, n_cols, compression, masses):
+        self.engine = engine
+        self.handle = handle
+        self.n_rows = n_rows
+        self.n_cols = n_cols
+        self.compression = compression
+        self.masses = list(masses)
+        self._budgets = None
+
+    @classmethod
+    def build(cls, masses, max_mass, compression, engine=None):
+        engine = engine or get_engine()
+        w = np.ascontiguousarray(masses, dtype=np.int64)
+        h = ctypes.c_void_p()
+        engine.check(engine._lib.sst_table_build(engine.handle, _ptr(w), len(w), int(max_mass), int(compression),
+                                                 ctypes.byref(h)), "sst_table_build")
+        return cls._wrap(engine, h, w)
+
+    @classmethod
+    def upload(cls, masses, words, compression, engine=None):
+        engine = engine or get_engine()
+        w = np.ascontiguousarray(masses, dtype=np.int64)
+        words = np.ascontiguousarray(words, dtype=_DT[compression])
+        if words.ndim != 2 or words.shape[0] != len(w):
+            raise ValueError("packed table must have one row per integer mass")
+        h = ctypes.c_void_p()
+        engine.check(engine._lib.sst_table_upload(engine.handle, _ptr(w), len(w), _ptr(words), words.shape[1],
+                                                  int(compression), ctypes.byref(h)), "sst_table_upload")
+        return cls._wrap(engine, h, w)
+
+    @classmethod
+    def _wrap(cls, engine, h, w):
+        nr, nc, C = _I(), _I64(), _I()
+        engine._lib.sst_table_shape(h, ctypes.byref(nr), ctypes.byref(nc), ctypes.byref(C))
+        return cls(engine, h, nr.value, nc.value, C.value, w.tolist())
+
+    def set_budgets(self, is_mod, caps):
+        key = (tuple(bool(x) for x in is_mod), tuple(int(c) for c in caps))
+        if key == self._budgets:
+            return
+        m = np.ascontiguousarray(key[0], dtype=np.uint8)
+        c = np.ascontiguousarray(key[1], dtype=np.int64)
+        self.engine.check(self.engine._lib.sst_table_set_budgets(self.handle, _ptr(m), _ptr(c)),
+                          "sst_table_set_budgets")
+        self._budgets = key
+
+    def download(self):
+        out = np.empty((self.n_rows, self.n_cols), dtype=_DT[self.compression])
+        self.engine.check(self.engine._lib.sst_table_download(self.handle, _ptr(out)), "sst_table_download")
+        return out
+
+    def is_valid(self, masses, thresholds, tolerance, precision):
+        m = np.ascontiguousarray(masses, dtype=np.float64)
+        t = None if thresholds is None else np.ascontiguousarray(thresholds, dtype=np.float64)
+        out = np.zeros(len(m), np.int8)
+        self.engine.check(self.engine._lib.sst_is_valid_batch(self.handle, _ptr(m), _ptr(t), len(m), float(tolerance),
+                                                              float(precision), _ptr(out)), "sst_is_valid_batch")
+        return out
+
+    def is_valid_device(self, d_mass, d_thr, n, tolerance, precision, d_out):
+        self.engine.check(self.engine._lib.sst_is_valid_batch_device(self.handle, d_mass, d_thr, int(n),
+                                                                     float(tolerance), float(precision), d_out),
+                          "sst_is_valid_batch_device")
+
+    def explain(self, masses, thresholds, tolerance, precision, max_mods, with_memo=True, cap=2 ** 32):
+        m = np.ascontiguousarray(masses, dtype=np.float64)
+        t = None if thresholds is None else np.ascontiguousarray(thresholds, dtype=np.float64)
+        mods_arr, scalar = _mods(max_mods, len(m))
+        h = ctypes.c_void_p()
+        self.engine.check(self.engine._lib.sst_explain_batch(self.handle, _ptr(m), _ptr(t), len(m), float(tolerance),
+                                                             float(precision), _ptr(mods_arr), scalar,
+                                                             int(bool(with_memo)), int(cap), ctypes.byref(h)),
+                          "sst_explain_batch")
+        return ExplainResult(self.engine, h, len(m)).fetch()
+
+    def explain_device(self, d_mass, d_thr, n, tolerance, precision, max_mods_scalar, d_mods=None, with_memo=True,
+                       cap=2 ** 32):
+        h = ctypes.c_void_p()
+        self.engine.check(self.engine._lib.sst_explain_batch_device(self.handle, d_mass, d_thr, int(n),
+                                                                    float(tolerance), float(precision), d_mods,
+                                                                    int(max_mods_scalar), int(bool(with_memo)),
+                                                                    int(cap), ctypes.byref(h)),
+                          "sst_explain_batch_device")
+        return ExplainResult(self.engine, h, n)
+
+    def close(self):
+        if self.handle:
+            self.engine._lib.sst_table_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _mods(max_mods, n):
+    """np.inf / None -> -1 (the engine's inf); scalar or per-query array."""
+    if np.ndim(max_mods) == 0:
+        return None, _budget(max_mods)
+    arr = np.array([_budget(x) for x in max_mods], dtype=np.int64)
+    if len(arr) != n:
+        raise ValueError("max_modifications array must have one entry per mass")
+    return arr, 0
+
+
+def _budget(a):
+    if a is None:
+        return -1
+    a = float(a)
+    if np.isinf(a):
+        return -1 if a > 0 else 0
+    # the reference only ever tests `A > 0`; negative budgets behave like 0
+    return max(int(np.ceil(a)) if a != int(a) else int(a), 0)

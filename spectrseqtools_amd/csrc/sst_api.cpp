@@ -1,0 +1,655 @@
+// sst_api.cpp -- host side of libsstgpu.so: contexts, device tables, batch
+// launches and the extern "C" ABI declared in include/sst.h.
+//
+// No CPU compute path exists here: every table build, index derivation and
+// query runs in the HIP kernels of sst_kernels.hip.  The host only moves
+// buffers, sizes workspaces and retries the rare batches whose outputs did not
+// fit the first arena / hash sizing.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sst.h"
+#include "sst_internal.h"
+
+using namespace sst;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  // grow-only reallocation; returns false on OOM
+  bool ensure(size_t n) {
+    if (n <= bytes) return true;
+    release();
+    if (n == 0) return true;
+    if (hipMalloc(&p, n) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      return false;
+    }
+    bytes = n;
+    return true;
+  }
+};
+
+}  // namespace
+
+struct sst_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::recursive_mutex mu;
+  // staging for host-pointer calls
+  DevBuf in_mass, in_thr, in_mods, out_valid;
+  // persistent workspaces of the deferred explain kernels
+  DevBuf ws_deep;
+  DevBuf ws_hash, ws_frames, ws_stacks, ws_epochs;
+  uint32_t hash_cap = 0;
+  int exact_blocks = 0;
+};
+
+struct sst_table {
+  sst_ctx* ctx = nullptr;
+  int n_rows = 0;
+  int64_t n_cols = 0;
+  int C = 32;
+  int64_t M = 0;
+  std::vector<int64_t> masses;
+  std::vector<uint8_t> is_mod;
+  std::vector<int64_t> cap;
+  DevBuf packed, index, valid, w, capd, modd;
+  TableArgs args{};
+};
+
+struct sst_result {
+  sst_ctx* ctx = nullptr;
+  int64_t n = 0;
+  DevBuf status, count, offset, payload, cursor, counters, lists, stats;
+  uint64_t arena_bytes = 0;
+  std::vector<int8_t> h_status;
+  std::vector<uint64_t> h_count, h_offset;
+  std::vector<uint8_t> h_payload;
+  uint64_t payload_bytes = 0;
+  uint64_t h_stats[kNumStats] = {0};
+};
+
+namespace {
+
+int fail(sst_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+#define HIP_OK(ctx, expr)                                                                        \
+  do {                                                                                          \
+    hipError_t _e = (expr);                                                                     \
+    if (_e != hipSuccess)                                                                       \
+      return fail(ctx, SST_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
+  } while (0)
+
+int set_device(sst_ctx* c) {
+  HIP_OK(c, hipSetDevice(c->device));
+  return SST_OK;
+}
+
+uint64_t width_mask(int C) { return C == 32 ? ~0ull : ((1ull << (2 * C)) - 1ull); }
+
+// mass_table.py:246 with numpy shift semantics (shift >= width -> 0)
+uint64_t last_col_mask(int64_t max_mass, int64_t ncols, int C) {
+  int64_t s = 2 * (ncols - (max_mass + 1) % ncols);
+  if (s >= 2 * C || s < 0) return 0;
+  return (width_mask(C) << s) & width_mask(C);
+}
+
+int64_t table_cols(int64_t max_mass, int C) {
+  return (int64_t)std::ceil((double)(max_mass + 1) / (double)C);  // mass_table.py:214
+}
+
+int finish_table(sst_table* t) {
+  sst_ctx* c = t->ctx;
+  const int64_t M = t->M;
+  if (!t->index.ensure((size_t)M * sizeof(ulonglong2)) || !t->valid.ensure((size_t)((M + 63) / 64) * 8))
+    return fail(c, SST_E_NOMEM, "device allocation failed (index)");
+  HIP_OK(c, hipMemsetAsync(t->valid.p, 0, t->valid.bytes, c->stream));
+  DevBuf err;
+  if (!err.ensure(sizeof(int))) return fail(c, SST_E_NOMEM, "device allocation failed");
+  HIP_OK(c, hipMemsetAsync(err.p, 0, sizeof(int), c->stream));
+  HIP_OK(c, launch_index(t->C, t->packed.p, t->n_rows, t->n_cols, M, (ulonglong2*)t->index.p, (uint64_t*)t->valid.p,
+                         (int*)err.p, c->stream));
+  int h_err = 0;
+  HIP_OK(c, hipMemcpyAsync(&h_err, err.p, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  err.release();
+  if (h_err)
+    return fail(c, SST_E_TABLE,
+                "packed table violates the DP row recurrence (bit0(r,m) != any(r-1,m)); it was not produced by "
+                "set_up_bit_table");
+  std::vector<int> w32(t->n_rows);
+  for (int r = 0; r < t->n_rows; ++r) w32[r] = (int)t->masses[r];
+  if (!t->w.ensure(t->n_rows * sizeof(int)) || !t->capd.ensure(t->n_rows * sizeof(int)) ||
+      !t->modd.ensure(t->n_rows))
+    return fail(c, SST_E_NOMEM, "device allocation failed");
+  HIP_OK(c, hipMemcpy(t->w.p, w32.data(), t->n_rows * sizeof(int), hipMemcpyHostToDevice));
+  t->args.index = (const ulonglong2*)t->index.p;
+  t->args.valid = (const uint64_t*)t->valid.p;
+  t->args.limit = M;
+  t->args.w = (const int*)t->w.p;
+  t->args.n_rows = t->n_rows;
+  int wmin = 0;
+  for (int r = 1; r < t->n_rows; ++r)
+    if (t->masses[r] > 0 && (wmin == 0 || t->masses[r] < wmin)) wmin = (int)t->masses[r];
+  t->args.w_min = wmin > 0 ? wmin : 1;
+  // default budgets: no modification rows (callers set them)
+  std::vector<uint8_t> mod(t->n_rows, 0);
+  std::vector<int64_t> cap(t->n_rows, 0);
+  return sst_table_set_budgets(t, mod.data(), cap.data());
+}
+
+int check_masses(sst_ctx* c, const int64_t* masses, int n_rows) {
+  if (!masses || n_rows < 1 || n_rows > kMaxRows)
+    return fail(c, SST_E_ARG, "n_rows must be in [1, 120]");
+  for (int r = 0; r < n_rows; ++r)
+    if (masses[r] < 0 || masses[r] > (int64_t)INT32_MAX) return fail(c, SST_E_ARG, "integer masses must be in [0, 2^31)");
+  return SST_OK;
+}
+
+bool valid_C(int C) { return C == 4 || C == 8 || C == 16 || C == 32; }
+
+}  // namespace
+
+extern "C" {
+
+int sst_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+int sst_ctx_create(int device, sst_ctx** out) {
+  if (!out) return SST_E_ARG;
+  *out = nullptr;
+  int n = sst_device_count();
+  if (device < 0 || device >= n) return SST_E_ARG;
+  sst_ctx* c = new sst_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SST_E_HIP;
+  }
+  *out = c;
+  return SST_OK;
+}
+
+void sst_ctx_destroy(sst_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->in_mass, &c->in_thr, &c->in_mods, &c->out_valid, &c->ws_deep, &c->ws_hash, &c->ws_frames,
+                    &c->ws_stacks, &c->ws_epochs})
+    b->release();
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* sst_last_error(const sst_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void* sst_ctx_stream(sst_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int sst_ctx_synchronize(sst_ctx* c) {
+  if (!c) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  return SST_OK;
+}
+
+int sst_table_build(sst_ctx* c, const int64_t* masses, int n_rows, int64_t max_mass, int C, sst_table** out) {
+  if (!c || !out) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  *out = nullptr;
+  if (int rc = check_masses(c, masses, n_rows)) return rc;
+  if (!valid_C(C)) return fail(c, SST_E_ARG, "The compression rate is not compatible with the table setup.");
+  if (max_mass < 0) return fail(c, SST_E_ARG, "max_mass must be >= 0");
+  if (int rc = set_device(c)) return rc;
+  sst_table* t = new sst_table();
+  t->ctx = c;
+  t->n_rows = n_rows;
+  t->C = C;
+  t->n_cols = table_cols(max_mass, C);
+  t->M = t->n_cols * C;
+  t->masses.assign(masses, masses + n_rows);
+  const int64_t M = t->M, rw = (M + 63) / 64;
+  DevBuf R, tmp, wdev;
+  if (!R.ensure((size_t)n_rows * rw * 8) || !tmp.ensure((size_t)2 * rw * 8) || !wdev.ensure(n_rows * 8) ||
+      !t->packed.ensure((size_t)n_rows * t->n_cols * (C / 4))) {
+    delete t;
+    return fail(c, SST_E_NOMEM, "device allocation failed (table build)");
+  }
+  uint64_t* Rp = (uint64_t*)R.p;
+  uint64_t* T[2] = {(uint64_t*)tmp.p, (uint64_t*)tmp.p + rw};
+  HIP_OK(c, hipMemcpyAsync(wdev.p, masses, n_rows * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, launch_bits_seed(Rp, rw, c->stream));
+  // R_r = R_{r-1} closed under +w_r by doubling: after j passes all multiples
+  // 0..2^j-1 of w_r are added; stop once 2^j * w_r >= M.
+  std::vector<uint8_t> literal(n_rows, 0);
+  for (int r = 1; r < n_rows; ++r) {
+    const uint64_t* src = Rp + (int64_t)(r - 1) * rw;
+    uint64_t* dst_final = Rp + (int64_t)r * rw;
+    int64_t k = masses[r];
+    if (k > 0 && k < C) {  // step == 0: the reference's single in-place sweep
+      literal[r] = 1;
+      void* row = (char*)t->packed.p + (size_t)r * t->n_cols * (C / 4);
+      HIP_OK(c, launch_row_literal(C, src, t->n_cols, (int)k, row, rw, dst_final, c->stream));
+      continue;
+    }
+    if (k <= 0 || k >= M) {
+      HIP_OK(c, hipMemcpyAsync(dst_final, src, rw * 8, hipMemcpyDeviceToDevice, c->stream));
+      continue;
+    }
+    int passes = 0;
+    for (int64_t kk = k; kk < M; kk *= 2) ++passes;
+    int cur = 0;
+    for (int p = 0; p < passes; ++p, k *= 2) {
+      uint64_t* dst = (p == passes - 1) ? dst_final : T[cur];
+      HIP_OK(c, launch_bits_shift_or(dst, src, k, rw, M, c->stream));
+      src = dst;
+      cur ^= 1;
+    }
+  }
+  DevBuf lit;
+  if (!lit.ensure(n_rows)) return fail(c, SST_E_NOMEM, "device allocation failed");
+  HIP_OK(c, hipMemcpyAsync(lit.p, literal.data(), n_rows, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, launch_pack(C, Rp, rw, n_rows, (const int64_t*)wdev.p, t->n_cols, M, last_col_mask(max_mass, t->n_cols, C),
+                        (const uint8_t*)lit.p, t->packed.p, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  lit.release();
+  R.release();
+  tmp.release();
+  wdev.release();
+  int rc = finish_table(t);
+  if (rc) {
+    delete t;
+    return rc;
+  }
+  *out = t;
+  return SST_OK;
+}
+
+int sst_table_upload(sst_ctx* c, const int64_t* masses, int n_rows, const void* words, int64_t n_cols, int C,
+                     sst_table** out) {
+  if (!c || !out || !words) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  *out = nullptr;
+  if (int rc = check_masses(c, masses, n_rows)) return rc;
+  if (!valid_C(C) || n_cols < 1) return fail(c, SST_E_ARG, "bad compression or n_cols");
+  if (int rc = set_device(c)) return rc;
+  sst_table* t = new sst_table();
+  t->ctx = c;
+  t->n_rows = n_rows;
+  t->C = C;
+  t->n_cols = n_cols;
+  t->M = n_cols * C;
+  t->masses.assign(masses, masses + n_rows);
+  size_t bytes = (size_t)n_rows * n_cols * (C / 4);
+  if (!t->packed.ensure(bytes)) {
+    delete t;
+    return fail(c, SST_E_NOMEM, "device allocation failed (upload)");
+  }
+  hipError_t e = hipMemcpy(t->packed.p, words, bytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    delete t;
+    return fail(c, SST_E_HIP, std::string("upload: ") + hipGetErrorString(e));
+  }
+  int rc = finish_table(t);
+  if (rc) {
+    delete t;
+    return rc;
+  }
+  *out = t;
+  return SST_OK;
+}
+
+int sst_table_set_budgets(sst_table* t, const uint8_t* is_mod, const int64_t* cap) {
+  if (!t || !is_mod || !cap) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  const int N = t->n_rows;
+  t->is_mod.assign(is_mod, is_mod + N);
+  t->cap.assign(cap, cap + N);
+  std::vector<int> cap32(N);
+  uint64_t mod0 = 0, mod1 = 0, cz0 = 0, cz1 = 0;
+  int any_mod = 0;
+  int64_t wmm = 0, lim = INT64_MAX;
+  for (int r = 0; r < N; ++r) {
+    int64_t cp = cap[r];
+    cap32[r] = (int)std::max<int64_t>(std::min<int64_t>(cp, kInfBudget), -1);
+    bool m = is_mod[r] != 0;
+    if (m) {
+      (r < 64 ? mod0 : mod1) |= 1ull << (r & 63);
+      any_mod = 1;
+      int64_t w = t->masses[r];
+      if (w > 0 && (wmm == 0 || w < wmm)) wmm = w;
+      // no per-row cap can bind for window values v <= (cap+1)*w - 1
+      int64_t cpp = std::max<int64_t>(cp, 0);
+      int64_t l = (w <= 0) ? (cpp > 0 ? INT64_MAX : -1)
+                           : (cpp + 1 > INT64_MAX / std::max<int64_t>(w, 1) ? INT64_MAX : (cpp + 1) * w - 1);
+      lim = std::min(lim, l);
+    }
+    if (cp <= 0) (r < 64 ? cz0 : cz1) |= 1ull << (r & 63);
+  }
+  if (!t->capd.ensure(N * sizeof(int)) || !t->modd.ensure(N)) return fail(c, SST_E_NOMEM, "device allocation failed");
+  HIP_OK(c, hipMemcpy(t->capd.p, cap32.data(), N * sizeof(int), hipMemcpyHostToDevice));
+  HIP_OK(c, hipMemcpy(t->modd.p, is_mod, N, hipMemcpyHostToDevice));
+  t->args.cap = (const int*)t->capd.p;
+  t->args.mod = (const uint8_t*)t->modd.p;
+  t->args.mod0 = mod0;
+  t->args.mod1 = mod1;
+  t->args.capz0 = cz0;
+  t->args.capz1 = cz1;
+  t->args.any_mod = any_mod;
+  t->args.w_min_mod = (int)(wmm > 0 ? wmm : 1);
+  t->args.fast_limit_B = lim;
+  return SST_OK;
+}
+
+int sst_table_shape(const sst_table* t, int* n_rows, int64_t* n_cols, int* C) {
+  if (!t) return SST_E_ARG;
+  if (n_rows) *n_rows = t->n_rows;
+  if (n_cols) *n_cols = t->n_cols;
+  if (C) *C = t->C;
+  return SST_OK;
+}
+
+int sst_table_download(sst_table* t, void* out) {
+  if (!t || !out) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  HIP_OK(c, hipMemcpy(out, t->packed.p, (size_t)t->n_rows * t->n_cols * (t->C / 4), hipMemcpyDeviceToHost));
+  return SST_OK;
+}
+
+void sst_table_destroy(sst_table* t) {
+  if (!t) return;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&t->packed, &t->index, &t->valid, &t->w, &t->capd, &t->modd}) b->release();
+  delete t;
+}
+
+int sst_is_valid_batch_device(sst_table* t, const double* d_mass, const double* d_thr, int64_t n, double tol,
+                              double prec, int8_t* d_out) {
+  if (!t || n < 0 || (n > 0 && (!d_mass || !d_out))) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  HIP_OK(c, launch_is_valid(t->args.valid, t->args.limit, d_mass, d_thr, n, tol, prec, d_out, c->stream));
+  return SST_OK;
+}
+
+int sst_is_valid_batch(sst_table* t, const double* mass, const double* thr, int64_t n, double tol, double prec,
+                       int8_t* out) {
+  if (!t || n < 0 || (n > 0 && (!mass || !out))) return SST_E_ARG;
+  if (n == 0) return SST_OK;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (!c->in_mass.ensure(n * 8) || (thr && !c->in_thr.ensure(n * 8)) || !c->out_valid.ensure(n))
+    return fail(c, SST_E_NOMEM, "device allocation failed (staging)");
+  HIP_OK(c, hipMemcpyAsync(c->in_mass.p, mass, n * 8, hipMemcpyHostToDevice, c->stream));
+  if (thr) HIP_OK(c, hipMemcpyAsync(c->in_thr.p, thr, n * 8, hipMemcpyHostToDevice, c->stream));
+  if (int rc = sst_is_valid_batch_device(t, (const double*)c->in_mass.p, thr ? (const double*)c->in_thr.p : nullptr, n,
+                                         tol, prec, (int8_t*)c->out_valid.p))
+    return rc;
+  HIP_OK(c, hipMemcpyAsync(out, c->out_valid.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  return SST_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+constexpr int kDeepBlocks = 256;        // persistent grid of the deep / no-memo kernel
+constexpr uint32_t kHashCap0 = 1u << 14;  // exact-path hash entries per lane (first attempt)
+constexpr int kExactLanes0 = 2048;      // exact-path concurrent lanes (first attempt)
+constexpr uint64_t kNodeBudget = 1ull << 32;
+
+int ensure_exact_ws(sst_ctx* c, uint32_t hash_cap, int lanes) {
+  if (c->hash_cap == hash_cap && c->exact_blocks * 64 == lanes) return SST_OK;
+  size_t hb = (size_t)lanes * hash_cap * hash_entry_bytes();
+  c->ws_hash.release();
+  c->ws_epochs.release();
+  if (!c->ws_hash.ensure(hb) || !c->ws_epochs.ensure((size_t)lanes * 8) ||
+      !c->ws_frames.ensure((size_t)lanes * kMaxDepth * p1_frame_bytes()) ||
+      !c->ws_stacks.ensure((size_t)lanes * kMaxDepth * glob_frame_bytes()))
+    return fail(c, SST_E_NOMEM, "device allocation failed (exact workspace)");
+  HIP_OK(c, hipMemsetAsync(c->ws_hash.p, 0, hb, c->stream));
+  HIP_OK(c, hipMemsetAsync(c->ws_epochs.p, 0, (size_t)lanes * 8, c->stream));
+  c->hash_cap = hash_cap;
+  c->exact_blocks = lanes / 64;
+  return SST_OK;
+}
+
+// one pass of the explain pipeline on device buffers
+int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double* d_thr, const int64_t* d_mods,
+                 int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count) {
+  sst_ctx* c = t->ctx;
+  const int64_t n = r->n;
+  if (!r->cursor.ensure(8) || !r->counters.ensure(kNumClasses * 4) || !r->stats.ensure(kNumStats * 8) ||
+      !r->lists.ensure((size_t)kNumClasses * std::max<int64_t>(n, 1) * 4) || !r->payload.ensure(r->arena_bytes))
+    return fail(c, SST_E_NOMEM, "device allocation failed (result)");
+  HIP_OK(c, hipMemsetAsync(r->cursor.p, 0, 8, c->stream));
+  HIP_OK(c, hipMemsetAsync(r->counters.p, 0, kNumClasses * 4, c->stream));
+  HIP_OK(c, hipMemsetAsync(r->stats.p, 0, kNumStats * 8, c->stream));
+  if (!c->ws_deep.ensure((size_t)kDeepBlocks * kWG * kMaxDepth * glob_frame_bytes()))
+    return fail(c, SST_E_NOMEM, "device allocation failed (deep workspace)");
+  if (c->hash_cap == 0)
+    if (int rc = ensure_exact_ws(c, kHashCap0, kExactLanes0)) return rc;
+  QueryArgs q{d_mass, d_thr, d_mods, mods_scalar, n, tol, prec, with_memo, cap_count, kNodeBudget};
+  OutArgs o{(int8_t*)r->status.p,  (uint64_t*)r->count.p,   (uint64_t*)r->offset.p,
+            (uint8_t*)r->payload.p, r->arena_bytes,          (uint64_t*)r->cursor.p,
+            (uint32_t*)r->counters.p, (uint32_t*)r->lists.p, (unsigned long long*)r->stats.p};
+  HIP_OK(c, launch_explain_main(t->args, q, o, c->stream));
+  HIP_OK(c, launch_explain_deep(t->args, q, o, kClassDeep, c->ws_deep.p, kDeepBlocks, c->stream));
+  HIP_OK(c, launch_explain_deep(t->args, q, o, kClassNomemo, c->ws_deep.p, kDeepBlocks, c->stream));
+  ExactWs ws{(char*)c->ws_hash.p, (char*)c->ws_frames.p, (char*)c->ws_stacks.p, (uint64_t*)c->ws_epochs.p,
+             c->hash_cap};
+  HIP_OK(c, launch_explain_exact(t->args, q, o, ws, c->exact_blocks, c->stream));
+  return SST_OK;
+}
+
+int alloc_result(sst_table* t, int64_t n, sst_result** out) {
+  sst_ctx* c = t->ctx;
+  sst_result* r = new sst_result();
+  r->ctx = c;
+  r->n = n;
+  size_t nn = (size_t)std::max<int64_t>(n, 1);
+  r->arena_bytes = std::max<uint64_t>(1u << 20, 16 * (uint64_t)nn);
+  if (!r->status.ensure(nn) || !r->count.ensure(nn * 8) || !r->offset.ensure(nn * 8)) {
+    delete r;
+    return fail(c, SST_E_NOMEM, "device allocation failed (result)");
+  }
+  *out = r;
+  return SST_OK;
+}
+
+void free_result_bufs(sst_result* r) {
+  for (DevBuf* b : {&r->status, &r->count, &r->offset, &r->payload, &r->cursor, &r->counters, &r->lists, &r->stats})
+    b->release();
+}
+
+int fetch(sst_result* r) {
+  sst_ctx* c = r->ctx;
+  const int64_t n = r->n;
+  r->h_status.resize(n);
+  r->h_count.resize(n);
+  r->h_offset.resize(n);
+  uint64_t cur = 0;
+  if (n) {
+    HIP_OK(c, hipMemcpyAsync(r->h_status.data(), r->status.p, n, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(r->h_count.data(), r->count.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(r->h_offset.data(), r->offset.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  if (r->cursor.p) HIP_OK(c, hipMemcpyAsync(&cur, r->cursor.p, 8, hipMemcpyDeviceToHost, c->stream));
+  if (r->stats.p)
+    HIP_OK(c, hipMemcpyAsync(r->h_stats, r->stats.p, kNumStats * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  r->payload_bytes = std::min<uint64_t>(cur, r->arena_bytes);
+  r->h_payload.resize(r->payload_bytes);
+  if (r->payload_bytes)
+    HIP_OK(c, hipMemcpy(r->h_payload.data(), r->payload.p, r->payload_bytes, hipMemcpyDeviceToHost));
+  return SST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d_thr, int64_t n, double tol, double prec,
+                             const int64_t* d_mods, int64_t mods_scalar, int with_memo, uint64_t cap_count,
+                             sst_result** out) {
+  if (!t || !out || n < 0 || n > INT32_MAX || (n > 0 && !d_mass)) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  *out = nullptr;
+  if (int rc = set_device(c)) return rc;
+  sst_result* r = nullptr;
+  if (int rc = alloc_result(t, n, &r)) return rc;
+  int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count);
+  if (rc) {
+    free_result_bufs(r);
+    delete r;
+    return rc;
+  }
+  *out = r;
+  return SST_OK;
+}
+
+int sst_explain_batch(sst_table* t, const double* mass, const double* thr, int64_t n, double tol, double prec,
+                      const int64_t* mods, int64_t mods_scalar, int with_memo, uint64_t cap_count, sst_result** out) {
+  if (!t || !out || n < 0 || n > INT32_MAX || (n > 0 && !mass)) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  *out = nullptr;
+  if (int rc = set_device(c)) return rc;
+  size_t nn = (size_t)std::max<int64_t>(n, 1);
+  if (!c->in_mass.ensure(nn * 8) || (thr && !c->in_thr.ensure(nn * 8)) || (mods && !c->in_mods.ensure(nn * 8)))
+    return fail(c, SST_E_NOMEM, "device allocation failed (staging)");
+  if (n) {
+    HIP_OK(c, hipMemcpyAsync(c->in_mass.p, mass, n * 8, hipMemcpyHostToDevice, c->stream));
+    if (thr) HIP_OK(c, hipMemcpyAsync(c->in_thr.p, thr, n * 8, hipMemcpyHostToDevice, c->stream));
+    if (mods) HIP_OK(c, hipMemcpyAsync(c->in_mods.p, mods, n * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  const double* dm = (const double*)c->in_mass.p;
+  const double* dt = thr ? (const double*)c->in_thr.p : nullptr;
+  const int64_t* dmo = mods ? (const int64_t*)c->in_mods.p : nullptr;
+  sst_result* r = nullptr;
+  if (int rc = alloc_result(t, n, &r)) return rc;
+  int rc = SST_OK;
+  for (int attempt = 0; attempt < 6; ++attempt) {
+    rc = explain_pass(t, r, dm, dt, dmo, mods_scalar, tol, prec, with_memo, cap_count);
+    if (!rc) rc = fetch(r);
+    if (rc) break;
+    bool arena_retry = false, exact_retry = false, bad = false;
+    for (int64_t i = 0; i < n; ++i) {
+      int s = r->h_status[i];
+      arena_retry |= s == kStatusArenaRetry;
+      exact_retry |= s == kStatusExactRetry;
+      bad |= s == kStatusPending;
+    }
+    if (bad) {
+      rc = fail(c, SST_E_INTERNAL, "explain: query left pending (internal error)");
+      break;
+    }
+    if (!arena_retry && !exact_retry) break;
+    if (arena_retry) {
+      uint64_t cur = 0;
+      HIP_OK(c, hipMemcpy(&cur, r->cursor.p, 8, hipMemcpyDeviceToHost));
+      r->arena_bytes = std::max<uint64_t>(2 * r->arena_bytes, cur + (1u << 20));
+      r->payload.release();
+    }
+    if (exact_retry) {
+      uint32_t hc = c->hash_cap * 8;
+      int lanes = std::max(64, (c->exact_blocks * 64) / 8);
+      if (hc > (1u << 26)) {
+        rc = fail(c, SST_E_INTERNAL, "explain: exact-path memo exceeds 2^26 masses");
+        break;
+      }
+      if ((rc = ensure_exact_ws(c, hc, lanes))) break;
+    }
+    if (attempt == 5) rc = fail(c, SST_E_INTERNAL, "explain: retries exhausted");
+  }
+  if (rc) {
+    free_result_bufs(r);
+    delete r;
+    return rc;
+  }
+  *out = r;
+  return SST_OK;
+}
+
+int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count, const uint64_t** offset,
+                    const uint8_t** payload, uint64_t* payload_bytes) {
+  if (!r) return SST_E_ARG;
+  if (status) *status = r->h_status.data();
+  if (count) *count = r->h_count.data();
+  if (offset) *offset = r->h_offset.data();
+  if (payload) *payload = r->h_payload.data();
+  if (payload_bytes) *payload_bytes = r->payload_bytes;
+  return SST_OK;
+}
+
+int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint64_t** d_offset, uint8_t** d_payload,
+                      uint64_t* payload_bytes) {
+  if (!r) return SST_E_ARG;
+  if (d_status) *d_status = (int8_t*)r->status.p;
+  if (d_count) *d_count = (uint64_t*)r->count.p;
+  if (d_offset) *d_offset = (uint64_t*)r->offset.p;
+  if (d_payload) *d_payload = (uint8_t*)r->payload.p;
+  if (payload_bytes) *payload_bytes = r->arena_bytes;
+  return SST_OK;
+}
+
+int sst_result_fetch(sst_result* r) {
+  if (!r) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(r->ctx->mu);
+  if (int rc = set_device(r->ctx)) return rc;
+  return fetch(r);
+}
+
+void sst_result_free(sst_result* r) {
+  if (!r) return;
+  std::lock_guard<std::recursive_mutex> g(r->ctx->mu);
+  (void)hipSetDevice(r->ctx->device);
+  (void)hipStreamSynchronize(r->ctx->stream);
+  free_result_bufs(r);
+  delete r;
+}
+
+int sst_result_stats(const sst_result* r, uint64_t* s) {
+  if (!r || !s) return SST_E_ARG;
+  for (int i = 0; i < kNumStats; ++i) s[i] = r->h_stats[i];
+  return SST_OK;
+}
+
+}  // extern "C"

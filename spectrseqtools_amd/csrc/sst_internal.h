@@ -1,0 +1,100 @@
+// sst_internal.h -- shared definitions between the HIP kernels and the host
+// side of libsstgpu.so.  Not part of the public ABI (see include/sst.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sst.h"
+
+namespace sst {
+
+constexpr int kMaxRows = 120;      // rows 0..119; index record keeps lo in bits 56..63
+constexpr int kWG = 256;           // workgroup of the lane-per-query kernels (4 waves)
+constexpr int kShallowDepth = 4;   // register-stack depth of the main kernel
+constexpr int kMaxDepth = 96;      // >= max items of any multiset in a table (73 for the full alphabet)
+constexpr int kInfBudget = 1 << 30;  // np.inf budget (decremented at most kMaxDepth times)
+
+enum { kClassShallow = 0, kClassDeep = 1, kClassExact = 2, kClassNomemo = 3, kNumClasses = 4 };
+// internal statuses (never returned to callers)
+constexpr int kStatusPending = -10;
+constexpr int kStatusArenaRetry = -11;
+constexpr int kStatusExactRetry = -12;
+
+enum {
+  kStatShallow = 0,
+  kStatDeep = 1,
+  kStatExact = 2,
+  kStatNomemo = 3,
+  kStatNodes = 4,
+  kNumStats = 8
+};
+
+struct TableArgs {
+  const ulonglong2* index;  // M records
+  const uint64_t* valid;    // ceil(M/64) words
+  int64_t limit;            // M = n_cols * compression
+  const int* w;             // [n_rows] integer masses
+  const int* cap;           // [n_rows] round(max_len * rate)
+  const uint8_t* mod;       // [n_rows] is_modification
+  uint64_t mod0, mod1;      // row masks of modification rows
+  uint64_t capz0, capz1;    // row masks with cap <= 0
+  int64_t fast_limit_B;     // max window value for which no per-row cap can bind
+  int n_rows;
+  int any_mod;
+  int w_min;                // smallest positive row mass
+  int w_min_mod;            // smallest modification row mass
+};
+
+struct QueryArgs {
+  const double* mass;
+  const double* thr;        // may be null: tolerance * mass
+  const int64_t* max_mods;  // may be null: max_mods_scalar
+  int64_t max_mods_scalar;
+  int64_t n;
+  double tol, prec;
+  int with_memo;
+  uint64_t cap_count;
+  uint64_t node_budget;
+};
+
+struct OutArgs {
+  int8_t* status;
+  uint64_t* count;
+  uint64_t* offset;
+  uint8_t* payload;
+  uint64_t arena_bytes;
+  uint64_t* cursor;
+  uint32_t* counters;  // [kNumClasses]
+  uint32_t* lists;     // [kNumClasses][n]
+  unsigned long long* stats;  // [kNumStats]
+};
+
+struct ExactWs {
+  char* hash;
+  char* frames;
+  char* stacks;
+  uint64_t* epochs;
+  uint32_t hash_cap;
+};
+
+hipError_t launch_bits_seed(uint64_t* R0, int64_t nwords, hipStream_t st);
+hipError_t launch_bits_shift_or(uint64_t* dst, const uint64_t* src, int64_t k, int64_t nwords, int64_t nbits,
+                                hipStream_t st);
+hipError_t launch_pack(int C, const uint64_t* R, int64_t rw, int n_rows, const int64_t* w, int64_t ncols, int64_t M,
+                       uint64_t last_mask, const uint8_t* literal, void* out, hipStream_t st);
+hipError_t launch_row_literal(int C, const uint64_t* Rprev, int64_t ncols, int shift, void* row, int64_t rw,
+                              uint64_t* Rout, hipStream_t st);
+hipError_t launch_index(int C, const void* packed, int n_rows, int64_t ncols, int64_t M, ulonglong2* index,
+                        uint64_t* valid, int* err, hipStream_t st);
+hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, const double* mass, const double* thr, int64_t n,
+                           double tol, double prec, int8_t* out, hipStream_t st);
+hipError_t launch_explain_main(const TableArgs& t, const QueryArgs& q, const OutArgs& o, hipStream_t st);
+hipError_t launch_explain_deep(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int cls, void* ws,
+                               int n_blocks, hipStream_t st);
+hipError_t launch_explain_exact(const TableArgs& t, const QueryArgs& q, const OutArgs& o, const ExactWs& ws,
+                                int n_blocks, hipStream_t st);
+size_t glob_frame_bytes();
+size_t p1_frame_bytes();
+size_t hash_entry_bytes();
+
+}  // namespace sst

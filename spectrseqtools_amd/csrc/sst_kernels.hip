@@ -1,0 +1,1020 @@
+// sst_kernels.hip -- HIP kernels of the MI355X mass-explanation engine (gfx950).
+//
+// Data layout in HBM (one set per table, see DESIGN.md "Data layout"):
+//   packed[r][c]  the reference's packed 2-bit table (mass_table.py:207-248),
+//                 kept only to hand DynamicProgrammingTable.table back.
+//   index[m]      16-B record per integer mass m < M = n_cols*C:
+//                   .x = L bits of rows 0..63, .y = rows 64..119 | lo << 56
+//                 L bit r = pair(r, m) bit1 ("left": reachable with >= 1 copy
+//                 of row r), lo = lowest row whose pair is non-zero (0xFF: none).
+//                 For a table produced by the reference recurrence,
+//                 pair(r, m) bit0 == (r > lo) for every r, so (L, lo) is the
+//                 whole column of the packed table in one aligned load.
+//   valid[m/64]   bitset of pair(N-1, m) != 0: what is_valid_mass reads
+//                 (mass_explanation.py:62-88); 2.8 MB for the full alphabet,
+//                 L2-resident.
+//
+// The explain DFS (mass_explanation.py:118-188) is run in its chain form:
+// from (m, r) the reference walks up rows r, r-1, ... while bit0 is set, then
+// takes the left branches of those rows in ascending row order.  With the
+// memo keyed on (m, row) and budgets ignored by the key, a node's result is
+// fixed by its first visit; every visited set of rows of one mass is the
+// contiguous range [lo(m), hv(m)].  Three query classes:
+//   SHALLOW/DEEP  budgets provably never bind (fast-path theorem):
+//                 enumerate all multisets in the window directly from index.
+//   EXACT         budgets may bind: phase 1 replays the memoised DFS over
+//                 masses (per-mass high-water row hv, enabled-left mask en,
+//                 lowest non-empty row ne, in a per-lane hash), phase 2
+//                 enumerates the enabled DAG.
+//   NOMEMO        with_memo=False: enumeration carrying (A, B) budgets.
+// One lane per query ("64 peaks per wavefront"): the query working set is a
+// handful of 16-B index loads, so lane-per-query issues 64x fewer memory
+// instructions than wave-per-query; outputs are compacted with a wavefront
+// prefix sum and one arena atomic per workgroup.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sst_internal.h"
+
+namespace sst {
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+struct M128 {
+  uint64_t a, b;  // rows 0..63, rows 64..119 (bits 56..63 never set here)
+};
+__device__ __forceinline__ M128 rows_upto(int r) {  // rows 0..r inclusive
+  M128 m;
+  if (r >= 63) {
+    m.a = ~0ull;
+    int k = r - 63;  // number of rows in b
+    m.b = k >= 64 ? ~0ull : ((1ull << k) - 1ull);
+  } else {
+    m.a = r < 0 ? 0ull : ((2ull << r) - 1ull);
+    m.b = 0;
+  }
+  return m;
+}
+__device__ __forceinline__ M128 rows_from(int r) {  // rows r..119
+  M128 u = rows_upto(r - 1);
+  M128 m;
+  m.a = ~u.a;
+  m.b = ~u.b & ((1ull << 56) - 1ull);
+  return m;
+}
+__device__ __forceinline__ M128 mand(M128 x, M128 y) { return {x.a & y.a, x.b & y.b}; }
+__device__ __forceinline__ bool mzero(M128 x) { return (x.a | x.b) == 0; }
+__device__ __forceinline__ int mlow(M128 x) { return x.a ? __builtin_ctzll(x.a) : 64 + __builtin_ctzll(x.b); }
+__device__ __forceinline__ M128 mclear(M128 x, int r) {
+  if (r < 64) x.a &= ~(1ull << r);
+  else x.b &= ~(1ull << (r - 64));
+  return x;
+}
+__device__ __forceinline__ bool mtest(M128 x, int r) { return r < 64 ? (x.a >> r) & 1ull : (x.b >> (r - 64)) & 1ull; }
+
+__device__ __forceinline__ int rec_lo(ulonglong2 rec) { return (int)(rec.y >> 56); }
+__device__ __forceinline__ M128 rec_L(ulonglong2 rec) { return {rec.x, rec.y & ((1ull << 56) - 1ull)}; }
+
+__device__ __forceinline__ ulonglong2 ld_index(const ulonglong2* idx, int64_t m) { return idx[m]; }
+
+// Reference quantisation, mass_explanation.py:107,110-114.  IEEE f64 division
+// (no fast-math), rint = Python round(x, 0) ties-to-even, ceil = np.ceil.
+__device__ __forceinline__ void quantise(double mass, double thr_abs, bool thr_none, double tol, double prec,
+                                         int64_t& lo, int64_t& hi) {
+  double t = thr_none ? tol * mass : thr_abs;
+  int64_t target = (int64_t)__builtin_rint(mass / prec);
+  int64_t th = (int64_t)__builtin_ceil(t / prec);
+  lo = target - th;
+  hi = target + th;
+}
+
+// any bit of valid in [a, b] (a <= b, both < limit)
+__device__ __forceinline__ bool any_bits(const uint64_t* valid, int64_t a, int64_t b) {
+  int64_t wa = a >> 6, wb = b >> 6;
+  for (int64_t wi = wa; wi <= wb; ++wi) {
+    uint64_t x = valid[wi];
+    if (wi == wa) x &= ~0ull << (a & 63);
+    if (wi == wb) x &= ~0ull >> (63 - (b & 63));
+    if (x) return true;
+  }
+  return false;
+}
+__device__ __forceinline__ int count_bits(const uint64_t* valid, int64_t a, int64_t b) {
+  int64_t wa = a >> 6, wb = b >> 6;
+  int c = 0;
+  for (int64_t wi = wa; wi <= wb; ++wi) {
+    uint64_t x = valid[wi];
+    if (wi == wa) x &= ~0ull << (a & 63);
+    if (wi == wb) x &= ~0ull >> (63 - (b & 63));
+    c += __builtin_popcountll(x);
+  }
+  return c;
+}
+
+// is_valid_mass semantics (mass_explanation.py:63-88): ascending scan, skip
+// v <= 0, raise at the first v >= limit, True at the first reachable v.
+__device__ __forceinline__ int8_t valid_window(const uint64_t* valid, int64_t limit, int64_t lo, int64_t hi) {
+  if (hi < lo) return 0;
+  int64_t a = lo < 1 ? 1 : lo;
+  if (a > hi) return 0;
+  int64_t b = hi < limit - 1 ? hi : limit - 1;
+  if (a <= b && any_bits(valid, a, b)) return 1;
+  return hi >= limit ? (int8_t)-1 : (int8_t)0;
+}
+
+// ---------------------------------------------------------------------------
+// table build: bitsets R_r over masses [0, M), R_r = R_{r-1} closed under +w_r
+// ---------------------------------------------------------------------------
+__global__ void k_bits_seed(uint64_t* R0, int64_t nwords) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nwords) R0[i] = (i == 0) ? 1ull : 0ull;
+}
+
+// dst = src | (src << k) over an nbits-long bitset (bits >= nbits dropped).
+__global__ void k_bits_shift_or(uint64_t* __restrict__ dst, const uint64_t* __restrict__ src, int64_t k,
+                                int64_t nwords, int64_t nbits) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nwords) return;
+  int64_t q = k >> 6;
+  int s = (int)(k & 63);
+  uint64_t v = src[i];
+  int64_t j = i - q;
+  if (j >= 0) {
+    uint64_t x = src[j] << s;
+    if (s && j >= 1) x |= src[j - 1] >> (64 - s);
+    v |= x;
+  }
+  if (i == nwords - 1 && (nbits & 63)) v &= (1ull << (nbits & 63)) - 1ull;
+  dst[i] = v;
+}
+
+__device__ __forceinline__ uint64_t bits_at(const uint64_t* R, int64_t pos, int n) {
+  // n <= 32 bits starting at bit pos (pos >= 0), bit i of result = bit pos+i
+  int64_t wi = pos >> 6;
+  int s = (int)(pos & 63);
+  uint64_t x = R[wi] >> s;
+  if (s + n > 64) x |= R[wi + 1] << (64 - s);
+  return n == 64 ? x : (x & ((1ull << n) - 1ull));
+}
+__device__ __forceinline__ uint64_t spread32(uint64_t x) {  // bit i -> bit 2i (x < 2^32)
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+
+template <int C>
+__device__ __forceinline__ uint64_t pword_get(const void* p, int64_t o) {
+  if (C == 32) return ((const uint64_t*)p)[o];
+  if (C == 16) return ((const uint32_t*)p)[o];
+  if (C == 8) return ((const uint16_t*)p)[o];
+  return ((const uint8_t*)p)[o];
+}
+template <int C>
+__device__ __forceinline__ void pword_set(void* p, int64_t o, uint64_t v) {
+  if (C == 32) ((uint64_t*)p)[o] = v;
+  else if (C == 16) ((uint32_t*)p)[o] = (uint32_t)v;
+  else if (C == 8) ((uint16_t*)p)[o] = (uint16_t)v;
+  else ((uint8_t*)p)[o] = (uint8_t)v;
+}
+template <int C>
+__device__ __forceinline__ uint64_t wmask() {
+  return C == 32 ? ~0ull : ((1ull << (2 * C)) - 1ull);
+}
+
+// Rows whose mass is below C (step == 0) are not a plain closure in the
+// reference: its in-place sweep shifts each word once and spills from the
+// just-updated word (mass_table.py:230-243).  Those rows are computed
+// literally: k_row_init writes the row-init bits (:221-223), one thread runs
+// the sweep, k_unpack_any recovers the row's reachability bitset.
+template <int C>
+__global__ void k_row_init(const uint64_t* __restrict__ Rprev, int64_t ncols, void* __restrict__ row) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncols) return;
+  uint64_t b0 = bits_at(Rprev, c * C, C);
+  uint64_t rb0 = (uint64_t)(__builtin_bitreverse32((uint32_t)b0) >> (32 - C));
+  pword_set<C>(row, c, spread32(rb0));
+}
+template <int C>
+__global__ void k_row_sweep_literal(void* __restrict__ row, int64_t ncols, int shift) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  uint64_t alt_first = 0;
+  for (int k = 0; k < C; ++k) alt_first |= 2ull << (2 * k);
+  const uint64_t full = wmask<C>();
+  for (int64_t j = 0; j < ncols; ++j) {
+    uint64_t x = pword_get<C>(row, j);
+    uint64_t y = x >> (2 * shift);
+    pword_set<C>(row, j, x | (alt_first & (((y << 1) & full) | y)));
+    if (shift != 0 && j + 1 < ncols) {
+      x = pword_get<C>(row, j);
+      uint64_t z = (x << (2 * (C - shift))) & full;
+      pword_set<C>(row, j + 1, pword_get<C>(row, j + 1) | (alt_first & (((z << 1) & full) | z)));
+    }
+  }
+}
+template <int C>
+__global__ void k_unpack_any(const void* __restrict__ row, int64_t ncols, int64_t rw, uint64_t* __restrict__ R) {
+  int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one bitset word = 64 masses
+  if (wi >= rw) return;
+  uint64_t out = 0;
+  for (int k = 0; k < 64; ++k) {
+    int64_t m = wi * 64 + k;
+    int64_t c = m / C;
+    if (c >= ncols) break;
+    uint64_t pair = (pword_get<C>(row, c) >> (2 * (C - 1 - (int)(m % C)))) & 3ull;
+    if (pair) out |= 1ull << k;
+  }
+  R[wi] = out;
+}
+
+// packed[r][c] from bitsets (row 0: pair(0,0) = 3, the init 0xC0.. word),
+// last column masked with the reference's formula (mass_table.py:246).
+// Rows flagged `literal` were written by k_row_sweep_literal: mask only.
+template <int C>
+__global__ void k_pack(const uint64_t* __restrict__ R, int64_t rw, int n_rows, const int64_t* __restrict__ w,
+                       int64_t ncols, int64_t M, uint64_t last_mask, const uint8_t* __restrict__ literal,
+                       void* __restrict__ out) {
+  int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int r = blockIdx.y;
+  if (c >= ncols) return;
+  if (literal[r]) {
+    if (c == ncols - 1) {
+      int64_t o = (int64_t)r * ncols + c;
+      pword_set<C>(out, o, pword_get<C>(out, o) & last_mask);
+    }
+    return;
+  }
+  int64_t m0 = c * C;
+  uint64_t b0, b1;
+  if (r == 0) {
+    b0 = b1 = (m0 == 0) ? 1ull : 0ull;
+  } else {
+    const uint64_t* Rp = R + (int64_t)(r - 1) * rw;
+    const uint64_t* Rr = R + (int64_t)r * rw;
+    b0 = bits_at(Rp, m0, C);
+    int64_t wr = w[r];
+    // b1 bit k = R_r(m0 + k - w_r) for m0 + k >= w_r
+    int64_t s = m0 - wr;
+    if (s >= 0) {
+      b1 = bits_at(Rr, s, C);
+    } else if (s > -C) {
+      b1 = bits_at(Rr, 0, C) << (-s);
+      b1 &= (C == 64) ? ~0ull : ((1ull << C) - 1ull);
+    } else {
+      b1 = 0;
+    }
+  }
+  // mass k of the word sits at bits 2*(C-1-k): reverse the C-bit fields
+  uint64_t rb0 = (uint64_t)(__builtin_bitreverse32((uint32_t)b0) >> (32 - C));
+  uint64_t rb1 = (uint64_t)(__builtin_bitreverse32((uint32_t)b1) >> (32 - C));
+  uint64_t word = spread32(rb0) | (spread32(rb1) << 1);
+  if (c == ncols - 1) word &= last_mask;
+  int64_t o = (int64_t)r * ncols + c;
+  if (C == 32) ((uint64_t*)out)[o] = word;
+  else if (C == 16) ((uint32_t*)out)[o] = (uint32_t)word;
+  else if (C == 8) ((uint16_t*)out)[o] = (uint16_t)word;
+  else ((uint8_t*)out)[o] = (uint8_t)word;
+}
+
+// index + valid bitset from a packed table of any compression; flags tables
+// that violate bit0(r, m) == (some row < r has pair != 0).
+template <int C>
+__global__ void k_index(const void* __restrict__ packed, int n_rows, int64_t ncols, int64_t M,
+                        ulonglong2* __restrict__ index, uint64_t* __restrict__ valid, int* __restrict__ err) {
+  int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool in = m < M;
+  int64_t mm = in ? m : 0;
+  int64_t c = mm / C;
+  int sh = 2 * (C - 1 - (int)(mm % C));
+  uint64_t L0 = 0, L1 = 0;
+  int lo = 0xFF;
+  bool bad = false;
+  int pair = 0;
+  for (int r = 0; r < n_rows; ++r) {
+    int64_t o = (int64_t)r * ncols + c;
+    uint64_t word;
+    if (C == 32) word = ((const uint64_t*)packed)[o];
+    else if (C == 16) word = ((const uint32_t*)packed)[o];
+    else if (C == 8) word = ((const uint16_t*)packed)[o];
+    else word = ((const uint8_t*)packed)[o];
+    pair = (int)((word >> sh) & 3ull);
+    if (r >= 1 && (pair & 1) != (lo != 0xFF ? 1 : 0)) bad = true;
+    if (pair && lo == 0xFF) lo = r;
+    if (pair & 2) {
+      if (r < 64) L0 |= 1ull << r;
+      else L1 |= 1ull << (r - 64);
+    }
+  }
+  if (in) {
+    index[m] = make_ulonglong2(L0, L1 | ((uint64_t)lo << 56));
+    if (bad) atomicOr(err, 1);
+  }
+  // one wave = 64 consecutive masses = one valid word
+  uint64_t bal = __ballot(in && pair != 0);
+  if ((threadIdx.x & 63) == 0 && m < M) valid[m >> 6] = bal;
+}
+
+// ---------------------------------------------------------------------------
+// is_valid batch
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_is_valid(const uint64_t* __restrict__ valid, int64_t limit,
+                                                  const double* __restrict__ mass, const double* __restrict__ thr,
+                                                  int64_t n, double tol, double prec, int8_t* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t lo, hi;
+  quantise(mass[i], thr ? thr[i] : 0.0, thr == nullptr, tol, prec, lo, hi);
+  out[i] = valid_window(valid, limit, lo, hi);
+}
+
+// ---------------------------------------------------------------------------
+// explain: shared pieces
+// ---------------------------------------------------------------------------
+struct Lds {
+  int w[kMaxRows];
+  int cap[kMaxRows];
+  uint8_t mod[kMaxRows];
+};
+__device__ __forceinline__ void stage_rows(Lds& s, const TableArgs& t) {
+  for (int r = threadIdx.x; r < t.n_rows; r += blockDim.x) {
+    s.w[r] = t.w[r];
+    s.cap[r] = t.cap[r];
+    s.mod[r] = t.mod[r];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ int clamp_budget(int64_t a) {
+  if (a < 0) return kInfBudget;  // np.inf
+  return a > kInfBudget ? kInfBudget : (int)a;
+}
+
+// fast-path theorem: no budget check can fail for any window value
+// <= hi when every mod row s has cap[s] >= hi / w_s and A >= hi / w_min_mod.
+__device__ __forceinline__ bool budgets_never_bind(const TableArgs& t, int64_t hi, int A) {
+  if (!t.any_mod) return true;
+  if (hi > t.fast_limit_B) return false;
+  if (A >= kInfBudget) return true;
+  return hi < (int64_t)(A + 1) * t.w_min_mod;
+}
+
+// emit one candidate: path rows sr[0..d] were chosen top-down (descending
+// rows); the reference's list is ascending mass == ascending row.
+template <typename Stack>
+__device__ __forceinline__ void emit(uint8_t* dst, const Stack& st, int d) {
+  dst[0] = (uint8_t)(d + 1);
+  for (int k = 0; k <= d; ++k) dst[1 + k] = st.row(d - k);
+}
+
+// Per-lane DFS stack.  Reg<D>: private arrays the compiler keeps in VGPRs for
+// small D.  Glob: a per-lane slice of a global workspace (deep / exact paths).
+template <int D>
+struct RegStack {
+  uint32_t m_[D];
+  uint64_t a_[D], b_[D];
+  uint8_t r_[D];
+  int A_[D], B_[D];
+  uint8_t top_[D];
+  static constexpr int depth = D;
+  __device__ __forceinline__ uint32_t m(int d) const { return m_[d]; }
+  __device__ __forceinline__ M128 mask(int d) const { return {a_[d], b_[d]}; }
+  __device__ __forceinline__ uint8_t row(int d) const { return r_[d]; }
+  __device__ __forceinline__ void set(int d, uint32_t m, M128 k) {
+    m_[d] = m;
+    a_[d] = k.a;
+    b_[d] = k.b;
+  }
+  __device__ __forceinline__ void set_mask(int d, M128 k) {
+    a_[d] = k.a;
+    b_[d] = k.b;
+  }
+  __device__ __forceinline__ void set_row(int d, int r) { r_[d] = (uint8_t)r; }
+  __device__ __forceinline__ void set_budget(int d, int A, int B, int top) {
+    A_[d] = A;
+    B_[d] = B;
+    top_[d] = (uint8_t)top;
+  }
+  __device__ __forceinline__ int A(int d) const { return A_[d]; }
+  __device__ __forceinline__ int B(int d) const { return B_[d]; }
+  __device__ __forceinline__ int top(int d) const { return top_[d]; }
+};
+
+struct GlobFrame {
+  uint64_t a, b;
+  uint32_t m;
+  int A, B;
+  uint8_t r, top, pad0, pad1;
+};
+struct GlobStack {
+  GlobFrame* f;
+  static constexpr int depth = kMaxDepth;
+  __device__ __forceinline__ uint32_t m(int d) const { return f[d].m; }
+  __device__ __forceinline__ M128 mask(int d) const { return {f[d].a, f[d].b}; }
+  __device__ __forceinline__ uint8_t row(int d) const { return f[d].r; }
+  __device__ __forceinline__ void set(int d, uint32_t m, M128 k) {
+    f[d].m = m;
+    f[d].a = k.a;
+    f[d].b = k.b;
+  }
+  __device__ __forceinline__ void set_mask(int d, M128 k) {
+    f[d].a = k.a;
+    f[d].b = k.b;
+  }
+  __device__ __forceinline__ void set_row(int d, int r) { f[d].r = (uint8_t)r; }
+  __device__ __forceinline__ void set_budget(int d, int A, int B, int top) {
+    f[d].A = A;
+    f[d].B = B;
+    f[d].top = (uint8_t)top;
+  }
+  __device__ __forceinline__ int A(int d) const { return f[d].A; }
+  __device__ __forceinline__ int B(int d) const { return f[d].B; }
+  __device__ __forceinline__ int top(int d) const { return f[d].top; }
+};
+
+// ---------------------------------------------------------------------------
+// exact path: per-lane open-addressing hash, one 32-B entry per visited mass
+// ---------------------------------------------------------------------------
+struct HEntry {
+  uint64_t key;   // (epoch << 32) | m
+  uint32_t meta;  // hv | ne << 8 (0xFF = none)
+  uint32_t pad;
+  uint64_t en0, en1;
+};
+struct Hash {
+  HEntry* e;
+  uint32_t mask;  // capacity - 1
+  uint64_t epoch;
+  uint32_t used;
+  uint32_t limit;
+  __device__ __forceinline__ uint32_t slot(uint32_t m) const { return (m * 0x9E3779B1u) & mask; }
+  // returns entry pointer or nullptr if absent
+  __device__ __forceinline__ HEntry* find(uint32_t m) const {
+    uint64_t key = (epoch << 32) | m;
+    uint32_t i = slot(m);
+    while (true) {
+      uint64_t k = e[i].key;
+      if (k == key) return &e[i];
+      if ((k >> 32) != epoch) return nullptr;
+      i = (i + 1) & mask;
+    }
+  }
+  // returns entry (inserting a fresh one) or nullptr when full
+  __device__ __forceinline__ HEntry* get(uint32_t m) {
+    uint64_t key = (epoch << 32) | m;
+    uint32_t i = slot(m);
+    while (true) {
+      uint64_t k = e[i].key;
+      if (k == key) return &e[i];
+      if ((k >> 32) != epoch) {
+        if (used >= limit) return nullptr;
+        ++used;
+        e[i].key = key;
+        e[i].meta = 0xFFFFu;
+        e[i].en0 = 0;
+        e[i].en1 = 0;
+        return &e[i];
+      }
+      i = (i + 1) & mask;
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// enumeration over the (enabled) DAG from root v: counts candidates, adds
+// their payload bytes, writes them when dst != nullptr.
+//   MODE_FAST   enabled = L (budgets never bind)
+//   MODE_NOMEMO budgets carried along the path (with_memo=False)
+//   MODE_EXACT  enabled = en from the phase-1 hash, pruned by ne
+// ---------------------------------------------------------------------------
+enum { MODE_FAST = 0, MODE_NOMEMO = 1, MODE_EXACT = 2 };
+
+struct EnumOut {
+  uint64_t count;
+  uint64_t bytes;
+  uint64_t nodes;
+  int fail;  // 1 depth, 2 node budget
+};
+
+template <int MODE, typename Stack>
+__device__ void enumerate_root(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, uint32_t v, int A0,
+                               uint8_t* dst, uint64_t cap_count, uint64_t node_budget, EnumOut& o) {
+  const int top_row = t.n_rows - 1;
+  M128 k0;
+  if (MODE == MODE_EXACT) {
+    const HEntry* e = h->find(v);
+    if (!e) return;
+    k0 = mand(M128{e->en0, e->en1}, rows_upto(top_row));
+  } else {
+    ulonglong2 rec = ld_index(t.index, v);
+    o.nodes++;
+    k0 = mand(rec_L(rec), rows_upto(top_row));
+  }
+  st.set(0, v, k0);
+  if (MODE == MODE_NOMEMO) st.set_budget(0, A0, s.cap[top_row], top_row);
+  int d = 0;
+  while (true) {
+    M128 k = st.mask(d);
+    if (mzero(k)) {
+      if (d == 0) break;
+      --d;
+      continue;
+    }
+    int rr = mlow(k);
+    st.set_mask(d, mclear(k, rr));
+    int Bv = 0;
+    if (MODE == MODE_NOMEMO) {
+      Bv = (rr == st.top(d)) ? st.B(d) : s.cap[rr];
+      if (s.mod[rr] && !(st.A(d) > 0 && Bv > 0)) continue;
+    }
+    int64_t child = (int64_t)st.m(d) - s.w[rr];
+    st.set_row(d, rr);
+    if (child == 0) {
+      if (dst && o.count < cap_count) {
+        emit(dst + o.bytes, st, d);
+      }
+      o.bytes += (uint64_t)(d + 2);
+      o.count++;
+      continue;
+    }
+    if (child < 0) continue;
+    if (o.nodes >= node_budget) {
+      o.fail = 2;
+      return;
+    }
+    M128 kc;
+    if (MODE == MODE_EXACT) {
+      const HEntry* e = h->find((uint32_t)child);
+      if (!e) continue;
+      int ne = (int)((e->meta >> 8) & 0xFF);
+      if (ne == 0xFF || rr < ne) continue;
+      kc = mand(M128{e->en0, e->en1}, rows_upto(rr));
+      o.nodes++;
+    } else {
+      ulonglong2 rec = ld_index(t.index, child);
+      o.nodes++;
+      if (rec_lo(rec) > rr) continue;
+      kc = mand(rec_L(rec), rows_upto(rr));
+    }
+    if (d + 1 >= Stack::depth) {
+      o.fail = 1;
+      return;
+    }
+    ++d;
+    st.set(d, (uint32_t)child, kc);
+    if (MODE == MODE_NOMEMO) {
+      int md = s.mod[rr];
+      st.set_budget(d, st.A(d - 1) - md, Bv - md, rr);
+    }
+  }
+}
+
+// payload bytes/counts of a whole window [a, b] of roots
+template <int MODE, typename Stack>
+__device__ void enumerate_window(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, int64_t a, int64_t b,
+                                 int A0, uint8_t* dst, uint64_t cap_count, uint64_t node_budget, EnumOut& o) {
+  if (a > b) return;
+  int64_t wa = a >> 6, wb = b >> 6;
+  for (int64_t wi = wa; wi <= wb; ++wi) {
+    uint64_t x = t.valid[wi];
+    if (wi == wa) x &= ~0ull << (a & 63);
+    if (wi == wb) x &= ~0ull >> (63 - (b & 63));
+    while (x) {
+      int bit = __builtin_ctzll(x);
+      x &= x - 1;
+      uint32_t v = (uint32_t)((wi << 6) + bit);
+      enumerate_root<MODE>(t, s, st, h, v, A0, dst ? dst : nullptr, cap_count, node_budget, o);
+      if (o.fail) return;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// exact path phase 1: replay the memoised DFS (first-visit budgets)
+// ---------------------------------------------------------------------------
+struct P1Frame {
+  uint64_t en0, en1;  // rows newly enabled by this frame
+  HEntry* e;
+  uint32_t m;
+  int A, B;
+  uint8_t rtop, rnext, pad0, pad1;
+};
+
+// visit (m, r, A, B): returns 1 if a frame was pushed, 0 otherwise (memo hit
+// or pair == 0); *ne_child receives the child's "non-empty at row r" verdict
+// for the non-pushed case.  -1 on hash exhaustion.
+__device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int& d, uint32_t m,
+                                        int r, int A, int B, bool& nonempty, uint64_t& nodes) {
+  ulonglong2 rec = ld_index(t.index, m);
+  nodes++;
+  int lo = rec_lo(rec);
+  if (r < lo) {  // pair(r, m) == 0: [] without memo (mass_explanation.py:148-149)
+    nonempty = false;
+    return 0;
+  }
+  HEntry* e = h.get(m);
+  if (!e) return -1;
+  int hv = (int)(e->meta & 0xFF);
+  hv = hv == 0xFF ? -1 : hv;
+  if (r <= hv) {  // memo hit (mass_explanation.py:122-123)
+    int ne = (int)((e->meta >> 8) & 0xFF);
+    nonempty = ne != 0xFF && r >= ne;
+    return 0;
+  }
+  int rlo = lo > hv + 1 ? lo : hv + 1;
+  // newly visited rows [rlo, r]; left enabled iff bit1 and (not mod or A>0 && B>0),
+  // with B = cap[row] for rows reached by the up chain and B for row r itself
+  M128 rng = mand(rows_upto(r), rows_from(rlo));
+  M128 en = mand(rec_L(rec), rng);
+  if (t.any_mod) {
+    M128 blocked;
+    if (A > 0) blocked = M128{t.mod0 & t.capz0, t.mod1 & t.capz1};
+    else blocked = M128{t.mod0, t.mod1};
+    en.a &= ~blocked.a;
+    en.b &= ~blocked.b;
+    if (s.mod[r] && mtest(rec_L(rec), r)) {
+      bool ok = A > 0 && B > 0;
+      if (ok) {
+        if (r < 64) en.a |= 1ull << r;
+        else en.b |= 1ull << (r - 64);
+      } else {
+        en = mclear(en, r);
+      }
+    }
+  }
+  e->en0 |= en.a;
+  e->en1 |= en.b;
+  e->meta = (e->meta & 0xFF00u) | (uint32_t)r;
+  ++d;
+  P1Frame& f = fr[d];
+  f.en0 = en.a;
+  f.en1 = en.b;
+  f.e = e;
+  f.m = m;
+  f.A = A;
+  f.B = B;
+  f.rtop = (uint8_t)r;
+  f.rnext = (uint8_t)rlo;
+  return 1;
+}
+
+// returns 0 ok, -1 hash full, -2 depth, -3 node budget
+__device__ int phase1(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
+                      uint64_t node_budget, uint64_t& nodes) {
+  const int top = t.n_rows - 1;
+  for (int64_t v = a; v <= b; ++v) {
+    if (!((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;
+    int d = -1;
+    bool ne_dummy;
+    int pr = p1_visit(t, s, h, fr, d, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes);
+    if (pr < 0) return -1;
+    while (d >= 0) {
+      P1Frame& f = fr[d];
+      M128 rem = mand(M128{f.en0, f.en1}, rows_from(f.rnext));
+      if (mzero(rem)) {
+        // frame done; report to parent: parent's pending row = parent.rnext - 1
+        HEntry* ce = f.e;
+        --d;
+        if (d >= 0) {
+          P1Frame& p = fr[d];
+          int rr = p.rnext - 1;
+          int ne = (int)((ce->meta >> 8) & 0xFF);
+          if (ne != 0xFF && rr >= ne) {
+            if (((p.e->meta >> 8) & 0xFF) == 0xFF) p.e->meta = (p.e->meta & 0xFFu) | ((uint32_t)rr << 8);
+          }
+        }
+        continue;
+      }
+      int rr = mlow(rem);
+      f.rnext = (uint8_t)(rr + 1);
+      int md = s.mod[rr];
+      int Bv = (rr == f.rtop) ? f.B : s.cap[rr];
+      int64_t child = (int64_t)f.m - s.w[rr];
+      bool nonempty = false;
+      if (child == 0) {
+        nonempty = true;
+      } else if (child > 0) {
+        if (nodes >= node_budget) return -3;
+        if (d + 1 >= kMaxDepth) return -2;
+        int pushed = p1_visit(t, s, h, fr, d, (uint32_t)child, rr, f.A - md, Bv - md, nonempty, nodes);
+        if (pushed < 0) return -1;
+        if (pushed) continue;  // resolved when the child frame pops
+      }
+      if (nonempty) {
+        HEntry* pe = fr[d].e;
+        if (((pe->meta >> 8) & 0xFF) == 0xFF) pe->meta = (pe->meta & 0xFFu) | ((uint32_t)rr << 8);
+      }
+    }
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// workgroup output allocation: exclusive scan of per-lane byte counts, one
+// atomic per workgroup on the arena cursor.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    uint64_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  return x;
+}
+
+__device__ __forceinline__ uint64_t wg_alloc(uint64_t mine, uint64_t* cursor, uint64_t& base_out) {
+  __shared__ uint64_t wsum[kWG / 64];
+  __shared__ uint64_t base;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t incl = wave_incl_scan(mine);
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+  for (int i = 0; i < kWG / 64; ++i) {
+    if (i < wv) before += wsum[i];
+    total += wsum[i];
+  }
+  if (threadIdx.x == 0) base = total ? atomicAdd((unsigned long long*)cursor, (unsigned long long)total) : 0;
+  __syncthreads();
+  base_out = base;
+  return before + incl - mine;
+}
+
+// ---------------------------------------------------------------------------
+// main explain kernel: plan every query, resolve trivial ones, run SHALLOW
+// fast-path queries in registers, queue the rest.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWG) void k_explain_main(TableArgs t, QueryArgs q, OutArgs out) {
+  __shared__ Lds s;
+  stage_rows(s, t);
+  const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  const bool live = i < q.n;
+  int8_t status = SST_NONE;
+  uint64_t cnt = 0, bytes = 0;
+  bool shallow = false;
+  int64_t a = 0, b = -1;
+  int A0 = 0;
+  if (live) {
+    int64_t lo, hi;
+    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, lo, hi);
+    A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
+    if (hi < lo) {
+      status = SST_NONE;
+    } else if (hi >= t.limit) {
+      status = SST_OUT_OF_TABLE;  // mass_explanation.py:134-138 (raises NameError)
+    } else {
+      bool has_zero = lo <= 0 && hi >= 0;
+      a = lo < 1 ? 1 : lo;
+      b = hi;
+      bool roots = a <= b && any_bits(t.valid, a, b);
+      status = has_zero ? SST_EMPTY : SST_NONE;
+      if (roots) {
+        int cls;
+        if (!q.with_memo) cls = budgets_never_bind(t, hi, A0) ? kClassShallow : kClassNomemo;
+        else cls = budgets_never_bind(t, hi, A0) ? kClassShallow : kClassExact;
+        if (cls == kClassShallow && hi / t.w_min + 1 > kShallowDepth) cls = kClassDeep;
+        if (cls == kClassShallow) {
+          shallow = true;
+        } else {
+          // defer: wave-aggregated append to the class list
+          uint32_t slot = atomicAdd(&out.counters[cls], 1u);
+          out.lists[(int64_t)cls * q.n + slot] = (uint32_t)i;
+          status = (int8_t)kStatusPending;
+        }
+      }
+    }
+  }
+  RegStack<kShallowDepth> st;
+  EnumOut eo{0, 0, 0, 0};
+  if (shallow) {
+    enumerate_window<MODE_FAST>(t, s, st, nullptr, a, b, A0, nullptr, ~0ull, ~0ull, eo);
+    cnt = eo.count;
+    if (cnt > 0) status = SST_SOME;
+    if (cnt > q.cap_count) {
+      status = SST_OVERFLOW;
+      bytes = 0;
+    } else {
+      bytes = eo.bytes;
+    }
+  }
+  uint64_t base;
+  uint64_t off = wg_alloc(bytes, out.cursor, base);
+  off += base;
+  if (bytes && off + bytes > out.arena_bytes) {
+    status = (int8_t)kStatusArenaRetry;
+    bytes = 0;
+  }
+  if (shallow && bytes) {
+    EnumOut e2{0, 0, 0, 0};
+    enumerate_window<MODE_FAST>(t, s, st, nullptr, a, b, A0, out.payload + off, ~0ull, ~0ull, e2);
+  }
+  if (live) {
+    out.status[i] = status;
+    out.count[i] = cnt;
+    out.offset[i] = bytes ? off : 0;
+  }
+  if (shallow) {
+    atomicAdd((unsigned long long*)&out.stats[kStatShallow], 1ull);
+    atomicAdd((unsigned long long*)&out.stats[kStatNodes], (unsigned long long)eo.nodes);
+  }
+}
+
+// Deferred fast/no-memo queries with deep stacks: persistent grid, one lane per
+// query, stack in a per-lane slice of the workspace.
+template <int MODE>
+__global__ __launch_bounds__(kWG) void k_explain_deep(TableArgs t, QueryArgs q, OutArgs out, int cls,
+                                                      GlobFrame* ws) {
+  __shared__ Lds s;
+  stage_rows(s, t);
+  const uint32_t n_list = out.counters[cls];
+  const int64_t gid = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * kWG;
+  GlobStack st{ws + gid * kMaxDepth};
+  for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
+    int64_t i = out.lists[(int64_t)cls * q.n + j];
+    int64_t lo, hi;
+    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, lo, hi);
+    int A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
+    bool has_zero = lo <= 0 && hi >= 0;
+    int64_t a = lo < 1 ? 1 : lo, b = hi;
+    EnumOut eo{0, 0, 0, 0};
+    enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, nullptr, ~0ull, q.node_budget, eo);
+    int8_t status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
+    uint64_t bytes = eo.bytes;
+    if (eo.fail) {
+      status = SST_ABORTED;
+      bytes = 0;
+    } else if (eo.count > q.cap_count) {
+      status = SST_OVERFLOW;
+      bytes = 0;
+    }
+    uint64_t off = 0;
+    if (bytes) {
+      off = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
+      if (off + bytes > out.arena_bytes) {
+        status = (int8_t)kStatusArenaRetry;
+        bytes = 0;
+      } else {
+        EnumOut e2{0, 0, 0, 0};
+        enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, out.payload + off, ~0ull, ~0ull, e2);
+      }
+    }
+    out.status[i] = status;
+    out.count[i] = eo.count;
+    out.offset[i] = bytes ? off : 0;
+    atomicAdd((unsigned long long*)&out.stats[MODE == MODE_FAST ? kStatDeep : kStatNomemo], 1ull);
+    atomicAdd((unsigned long long*)&out.stats[kStatNodes], (unsigned long long)eo.nodes);
+  }
+}
+
+// Deferred budget-binding queries: exact memo replay (phase 1) + enabled-DAG
+// enumeration (phase 2).  Per lane: a hash slice and a frame slice.
+__global__ __launch_bounds__(64) void k_explain_exact(TableArgs t, QueryArgs q, OutArgs out, ExactWs ws) {
+  __shared__ Lds s;
+  stage_rows(s, t);
+  const uint32_t n_list = out.counters[kClassExact];
+  const int64_t gid = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * 64;
+  P1Frame* fr = (P1Frame*)(ws.frames + gid * kMaxDepth * sizeof(P1Frame));
+  GlobStack st{(GlobFrame*)(ws.stacks + gid * kMaxDepth * sizeof(GlobFrame))};
+  Hash h;
+  h.e = (HEntry*)(ws.hash + (size_t)gid * ws.hash_cap * sizeof(HEntry));
+  h.mask = ws.hash_cap - 1;
+  h.limit = (uint32_t)(ws.hash_cap * 0.7);
+  for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
+    int64_t i = out.lists[(int64_t)kClassExact * q.n + j];
+    int64_t lo, hi;
+    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, lo, hi);
+    int A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
+    bool has_zero = lo <= 0 && hi >= 0;
+    int64_t a = lo < 1 ? 1 : lo, b = hi;
+    h.epoch = ++ws.epochs[gid];
+    h.used = 0;
+    uint64_t nodes = 0;
+    int rc = phase1(t, s, h, fr, a, b, A0, q.node_budget, nodes);
+    int8_t status;
+    EnumOut eo{0, 0, 0, 0};
+    uint64_t bytes = 0;
+    if (rc == -1) {
+      status = (int8_t)kStatusExactRetry;
+    } else if (rc < 0) {
+      status = SST_ABORTED;
+    } else {
+      enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, nullptr, ~0ull, q.node_budget, eo);
+      status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
+      bytes = eo.bytes;
+      if (eo.fail) {
+        status = SST_ABORTED;
+        bytes = 0;
+      } else if (eo.count > q.cap_count) {
+        status = SST_OVERFLOW;
+        bytes = 0;
+      }
+    }
+    uint64_t off = 0;
+    if (bytes) {
+      off = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
+      if (off + bytes > out.arena_bytes) {
+        status = (int8_t)kStatusArenaRetry;
+        bytes = 0;
+      } else {
+        EnumOut e2{0, 0, 0, 0};
+        enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, out.payload + off, ~0ull, ~0ull, e2);
+      }
+    }
+    out.status[i] = status;
+    out.count[i] = eo.count;
+    out.offset[i] = bytes ? off : 0;
+    atomicAdd((unsigned long long*)&out.stats[kStatExact], 1ull);
+    atomicAdd((unsigned long long*)&out.stats[kStatNodes], (unsigned long long)(nodes + eo.nodes));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers (C++ linkage, used by sst_api.cpp)
+// ---------------------------------------------------------------------------
+static inline unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
+
+hipError_t launch_bits_seed(uint64_t* R0, int64_t nwords, hipStream_t st) {
+  hipLaunchKernelGGL(k_bits_seed, dim3(blocks_for(nwords, 256)), dim3(256), 0, st, R0, nwords);
+  return hipGetLastError();
+}
+hipError_t launch_bits_shift_or(uint64_t* dst, const uint64_t* src, int64_t k, int64_t nwords, int64_t nbits,
+                                hipStream_t st) {
+  hipLaunchKernelGGL(k_bits_shift_or, dim3(blocks_for(nwords, 256)), dim3(256), 0, st, dst, src, k, nwords, nbits);
+  return hipGetLastError();
+}
+hipError_t launch_pack(int C, const uint64_t* R, int64_t rw, int n_rows, const int64_t* w, int64_t ncols, int64_t M,
+                       uint64_t last_mask, const uint8_t* literal, void* out, hipStream_t st) {
+  dim3 grid(blocks_for(ncols, 256), n_rows);
+#define SST_PACK(CC) \
+  hipLaunchKernelGGL(k_pack<CC>, grid, dim3(256), 0, st, R, rw, n_rows, w, ncols, M, last_mask, literal, out)
+  switch (C) {
+    case 4: SST_PACK(4); break;
+    case 8: SST_PACK(8); break;
+    case 16: SST_PACK(16); break;
+    default: SST_PACK(32);
+  }
+#undef SST_PACK
+  return hipGetLastError();
+}
+hipError_t launch_row_literal(int C, const uint64_t* Rprev, int64_t ncols, int shift, void* row, int64_t rw,
+                              uint64_t* Rout, hipStream_t st) {
+#define SST_ROW(CC)                                                                                   \
+  hipLaunchKernelGGL(k_row_init<CC>, dim3(blocks_for(ncols, 256)), dim3(256), 0, st, Rprev, ncols, row); \
+  hipLaunchKernelGGL(k_row_sweep_literal<CC>, dim3(1), dim3(64), 0, st, row, ncols, shift);            \
+  hipLaunchKernelGGL(k_unpack_any<CC>, dim3(blocks_for(rw, 256)), dim3(256), 0, st, row, ncols, rw, Rout)
+  switch (C) {
+    case 4: SST_ROW(4); break;
+    case 8: SST_ROW(8); break;
+    case 16: SST_ROW(16); break;
+    default: SST_ROW(32);
+  }
+#undef SST_ROW
+  return hipGetLastError();
+}
+hipError_t launch_index(int C, const void* packed, int n_rows, int64_t ncols, int64_t M, ulonglong2* index,
+                        uint64_t* valid, int* err, hipStream_t st) {
+  dim3 grid(blocks_for(M, 256));
+  switch (C) {
+    case 4: hipLaunchKernelGGL(k_index<4>, grid, dim3(256), 0, st, packed, n_rows, ncols, M, index, valid, err); break;
+    case 8: hipLaunchKernelGGL(k_index<8>, grid, dim3(256), 0, st, packed, n_rows, ncols, M, index, valid, err); break;
+    case 16: hipLaunchKernelGGL(k_index<16>, grid, dim3(256), 0, st, packed, n_rows, ncols, M, index, valid, err); break;
+    default: hipLaunchKernelGGL(k_index<32>, grid, dim3(256), 0, st, packed, n_rows, ncols, M, index, valid, err);
+  }
+  return hipGetLastError();
+}
+hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, const double* mass, const double* thr, int64_t n,
+                           double tol, double prec, int8_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_is_valid, dim3(blocks_for(n, 256)), dim3(256), 0, st, valid, limit, mass, thr, n, tol, prec,
+                     out);
+  return hipGetLastError();
+}
+hipError_t launch_explain_main(const TableArgs& t, const QueryArgs& q, const OutArgs& o, hipStream_t st) {
+  if (q.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_explain_main, dim3(blocks_for(q.n, kWG)), dim3(kWG), 0, st, t, q, o);
+  return hipGetLastError();
+}
+hipError_t launch_explain_deep(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int cls, void* ws,
+                               int n_blocks, hipStream_t st) {
+  if (cls == kClassDeep)
+    hipLaunchKernelGGL(k_explain_deep<MODE_FAST>, dim3(n_blocks), dim3(kWG), 0, st, t, q, o, cls, (GlobFrame*)ws);
+  else
+    hipLaunchKernelGGL(k_explain_deep<MODE_NOMEMO>, dim3(n_blocks), dim3(kWG), 0, st, t, q, o, cls, (GlobFrame*)ws);
+  return hipGetLastError();
+}
+hipError_t launch_explain_exact(const TableArgs& t, const QueryArgs& q, const OutArgs& o, const ExactWs& ws,
+                                int n_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_explain_exact, dim3(n_blocks), dim3(64), 0, st, t, q, o, ws);
+  return hipGetLastError();
+}
+
+size_t glob_frame_bytes() { return sizeof(GlobFrame); }
+size_t p1_frame_bytes() { return sizeof(P1Frame); }
+size_t hash_entry_bytes() { return sizeof(HEntry); }
+
+}  // namespace sst
