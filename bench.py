@@ -1,0 +1,310 @@
+#!/usr/bin/env python3
+"""bench.py -- peaks explained/sec on MI355X (BASELINE.json metric).
+
+One step = the reference pipeline's hot path over one batch of synthetic
+spectra (10k spectra, ~1M peaks, full 104-mass /
+105-row alphabet, <=20-mer) with every input already resident in HBM:
+  * A7: is_valid_mass for every peak x 4 breakage weights
+        (fragment_classification.py:52-67)  -> k_is_valid
+  * A8: explain_mass_with_table for every adjacent SU-mass difference the
+        reference's sliding window emits (prediction.py:286-329), budget
+        round(0.5*max_len)                  -> k_explain_main (+ deferred kernels)
+  * N>1: per-rank results gathered to rank 0 over RCCL.
+value = peaks of all ranks / step time (max over ranks).  Spectra shard by
+rank (weak scaling: `--spectra` per GPU).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--spectra S]
+       (N>1 under torch.distributed.run, one rank per GPU)
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "peaks explained/sec (full 148-nt alphabet, <=20-mer) at 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def window_words(masses, thr, prec, limit):
+    """Bitset words spanning each query's scan range [max(lo,1), min(hi, limit-1)]
+    (the same IEEE quantisation as the kernels / mass_explanation.py:107-114)."""
+    target = np.rint(masses / prec).astype(np.int64)
+    th = np.ceil(thr / prec).astype(np.int64)
+    lo = np.maximum(target - th, 1)
+    hi = np.minimum(target + th, limit - 1)
+    w = (hi >> 6) - (lo >> 6) + 1
+    return np.where(hi >= lo, w, 0)
+
+
+def build_workload(n_spectra, seed, dp):
+    from spectrseqtools_amd.masses import build_breakage_dict
+    from spectrseqtools_amd.producers import (MAX_VARIANCE, classify_queries, diff_queries, max_nucleotide_weight,
+                                              sliding_window_pairs)
+    from spectrseqtools_amd.synthetic import make_spectra
+
+    tol, prec = dp.tolerance, dp.precision
+    batch = make_spectra(n_spectra, seed=seed)
+    brk = build_breakage_dict(555.1294, 455.1491)
+    cq = classify_queries(batch.observed, brk, prec, tol)
+    valid = dp.device_table.is_valid(cq.su_mass, cq.threshold, tol, prec)  # setup pass: selects the window inputs
+    if (valid < 0).any():
+        raise RuntimeError("synthetic peak outside the DP table")
+    n_brk = len(brk)
+    P = len(batch.observed)
+    spec = np.tile(batch.spectrum, n_brk)
+    brk_names = np.array(cq.breakage)
+    is_start = np.char.find(brk_names.astype(str), "START") >= 0
+    is_end = np.char.find(brk_names.astype(str), "END") >= 0
+    se_w = [k for k, v in brk.items() if "START_END" in v][0]
+    maxw = max_nucleotide_weight()
+    keep = valid == 1
+    order = np.lexsort((cq.su_mass, spec))
+    order = order[keep[order]]
+    d_all, t_all = [], []
+    bounds = np.searchsorted(spec[order], np.arange(n_spectra + 1))
+    for s in range(n_spectra):
+        idx = order[bounds[s]:bounds[s + 1]]
+        su_seq = batch.seq_mass[s] - se_w * prec
+        su, ob = cq.su_mass[idx], cq.observed[idx]
+        # filter_by_sequence_mass (fragment_classification.py:122-139)
+        full = is_start[idx] & is_end[idx]
+        ok = (su < su_seq + MAX_VARIANCE) & ((su > su_seq - MAX_VARIANCE) | ~full)
+        for side in (is_start, is_end):
+            sel = ok & side[idx]
+            d, t, _ = diff_queries(su[sel], ob[sel], tol, maxw)
+            d_all.append(d)
+            t_all.append(t)
+    diffs = np.concatenate(d_all)
+    dthr = np.concatenate(t_all)
+    return {
+        "peaks": P, "a7_mass": cq.su_mass, "a7_thr": cq.threshold, "a8_mass": diffs, "a8_thr": dthr,
+        "spectra": n_spectra, "a7_valid": valid,
+    }
+
+
+def cpu_baseline(wl_fn, dp, budget_s=12.0):
+    """The CPU oracle (literal C restatement of is_valid_mass /
+    explain_mass_with_table, OpenMP over the host cores) on a bounded sample
+    of the same workload."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle as oracle
+
+    ms = [m.mass for m in dp.masses]
+    table = oracle.build_table(ms, max(ms) * 35, 32)
+    alph = oracle.Alphabet(ms, [m.is_modification for m in dp.masses],
+                           [round(dp.seq.max_len * m.modification_rate) for m in dp.masses])
+    A = round(dp.seq.modification_rate * dp.seq.max_len)
+    threads = oracle.LIB.ora_num_threads()
+
+    def run(wl):
+        t0 = time.perf_counter()
+        oracle.is_valid_batch(table, 32, wl["a7_mass"], wl["a7_thr"], dp.tolerance, nthreads=threads)
+        oracle.explain_batch(table, 32, alph, wl["a8_mass"], wl["a8_thr"], A, dp.tolerance, nthreads=threads)
+        return time.perf_counter() - t0
+
+    n = 200
+    wl = wl_fn(n)
+    t = run(wl)
+    n2 = int(min(20000, max(n, n * budget_s / max(t, 1e-3))))
+    if n2 > n:
+        wl = wl_fn(n2)
+        t = run(wl)
+        n = n2
+    return {"value": wl["peaks"] / t, "unit": "peaks/s", "cores": threads, "kind": "port",
+            "sample": f"{n} synthetic spectra ({wl['peaks']} peaks, {len(wl['a7_mass'])} A7 + {len(wl['a8_mass'])} "
+                      f"A8 queries), oracle/sst_oracle.c with {threads} OpenMP threads, {t:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--spectra", type=int, default=10000, help="spectra per GPU")
+    ap.add_argument("--seed", type=int, default=1000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (profiles/), reported as roofline.traffic")
+    args = ap.parse_args()
+
+    import torch
+
+    from spectrseqtools_amd import _native
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.parallel import Gatherer, device_bytes, dist_env
+
+    rank, world, local = dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev_t = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev_t)
+
+    engine = _native.get_engine(local)
+    seq = SequenceInformation(max_len=20, su_mass=6500.0, obs_mass=6500.0, modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=engine)
+    A = round(seq.modification_rate * seq.max_len)  # calculate_explanations (common.py:55)
+    tdev = dp.device_table
+    wl = build_workload(args.spectra, args.seed + rank * 1_000_003, dp)
+    n7, n8 = len(wl["a7_mass"]), len(wl["a8_mass"])
+    a7m = torch.from_numpy(wl["a7_mass"]).to(dev_t)
+    a7t = torch.from_numpy(wl["a7_thr"]).to(dev_t)
+    a8m = torch.from_numpy(wl["a8_mass"]).to(dev_t)
+    a8t = torch.from_numpy(wl["a8_thr"]).to(dev_t)
+    out7 = torch.empty(n7, dtype=torch.int8, device=dev_t)
+    torch.cuda.synchronize()
+    ext = torch.cuda.ExternalStream(engine.stream, device=dev_t)
+
+    res = None
+    gath = Gatherer(dist, dev_t) if dist else None
+
+    def step():
+        nonlocal res
+        tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, out7.data_ptr())
+        res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=res)
+        if gath is not None:
+            torch.cuda.current_stream().wait_stream(ext)
+            st, cnt, _off, pay, _cap = res.device_views()
+            flat = torch.cat([out7.view(torch.uint8), device_bytes(st, n8, dev_t), device_bytes(cnt, 8 * n8, dev_t),
+                              device_bytes(pay, payload_bytes, dev_t)])
+            gath.gather(flat)
+
+    # untimed sizing pass: results are deterministic per rank, so the gather
+    # sizes are agreed once
+    tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, out7.data_ptr())
+    res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A)
+    engine.synchronize()
+    res.fetch_device()
+    payload_bytes = int(len(res.payload))
+    if gath is not None:
+        gath.agree(n7 + 9 * n8 + payload_bytes)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    engine.synchronize()
+
+    engine.profile(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    prof = engine.profile_read()
+    engine.profile(False)
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        pk = torch.tensor([wl["peaks"], n7, n8], dtype=torch.int64, device=dev_t)
+        dist.all_reduce(pk)
+        peaks_all, n7_all, n8_all = (int(x) for x in pk.tolist())
+    else:
+        peaks_all, n7_all, n8_all = wl["peaks"], n7, n8
+
+    # results of the last step (validation + algorithmic bytes)
+    res.fetch_device()
+    st = res.status
+    if (st < -2).any():
+        raise RuntimeError(f"internal statuses in results: {np.unique(st[st < -2])}")
+    stats = res.stats()
+    v7 = out7.cpu().numpy()
+    assert np.array_equal(v7, wl["a7_valid"]), "is_valid results changed between setup and timed runs"
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    limit = tdev.n_cols * tdev.compression
+    w7 = window_words(wl["a7_mass"], wl["a7_thr"], dp.precision, limit)
+    w8 = window_words(wl["a8_mass"], wl["a8_thr"], dp.precision, limit)
+    bytes7 = float(n7 * (16 + 1) + 8 * w7.sum())
+    bytes8 = float(n8 * (16 + 17) + 8 * w8.sum() + 16 * int(stats[4]) + len(res.payload))
+    kern = {}
+    for kid, (ms, cnt) in prof.items():
+        kern[_native.KERNEL_NAMES[kid]] = {"avg_us": 1e3 * ms / cnt, "launches": cnt}
+    k7 = kern.get("k_is_valid", {"avg_us": float("nan")})["avg_us"]
+    k8 = kern.get("k_explain_main", {"avg_us": float("nan")})["avg_us"]
+    dom, dbytes, dus = ("k_explain_main", bytes8, k8) if k8 >= k7 else ("k_is_valid", bytes7, k7)
+    achieved = dbytes / (dus * 1e-6) / 1e9
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get(dom)
+    except (OSError, ValueError):
+        pass
+    ms_step = 1e3 * elapsed / args.steps
+    value = peaks_all / (elapsed / args.steps)
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(lambda n: build_workload(n, args.seed, dp), dp)
+
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "peaks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {
+            "workload": "config3: synthetic spectra (SURVEY 8(d)), full 104-mass/105-row alphabet, <=20-mer, "
+                        "A7 (4 breakages/peak) + A8 (sliding-window differences) per step",
+            "spectra_per_gpu": args.spectra,
+            "peaks": peaks_all,
+            "a7_queries": n7_all,
+            "a8_queries": n8_all,
+            "max_len": seq.max_len,
+            "max_modifications": A,
+            "parallelism": f"spectra sharded over {world} GPU(s), RCCL gather to rank 0" if world > 1 else "1 GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": dbytes,
+            "avg_launch_us": dus,
+        },
+        "kernels": kern,
+        "engine_stats": {"shallow": int(stats[0]), "deep": int(stats[1]), "exact": int(stats[2]),
+                         "nomemo": int(stats[3]), "index_loads": int(stats[4]),
+                         "candidates": int(res.count.sum()), "payload_bytes": int(len(res.payload))},
+        "queries_per_s": (n7_all + n8_all) / (elapsed / args.steps),
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -110,7 +110,9 @@ int sst_explain_batch(sst_table* t, const double* mass, const double* thr_abs, i
                       double precision, const int64_t* max_mods, int64_t max_mods_scalar, int with_memo,
                       uint64_t cap_per_query, sst_result** out);
 /* Same with inputs already in HBM; results stay on the device (fetch with
- * sst_result_device / sst_result_fetch).  Queued on the ctx stream. */
+ * sst_result_device / sst_result_fetch).  Queued on the ctx stream, no host
+ * synchronisation.  If *out is non-NULL it must be a result of the same ctx
+ * with capacity >= n: its buffers are reused (no allocation). */
 int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d_thr_abs, int64_t n,
                              double tolerance, double precision, const int64_t* d_max_mods, int64_t max_mods_scalar,
                              int with_memo, uint64_t cap_per_query, sst_result** out);
@@ -128,10 +130,26 @@ int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint
 int sst_result_fetch(sst_result* r);
 void sst_result_free(sst_result* r);
 
-/* Counters of the last explain launch, for measurement: queries resolved by
- * the window scan alone, by the shallow / deep / exact / no-memo kernels,
- * index records loaded (node expansions), payload bytes. */
+/* Counters of the last explain launch (valid after a fetch), for measurement:
+ * [0] queries run by the shallow fast path, [1] deep fast path, [2] exact
+ * (budget-binding) path, [3] no-memo path, [4] index records loaded (node
+ * expansions of the counting pass). */
 int sst_result_stats(const sst_result* r, uint64_t* stats_out /* [8] */);
+
+/* ---- measurement ------------------------------------------------------ */
+/* Kernel ids for sst_profile_read. */
+#define SST_K_IS_VALID 0
+#define SST_K_EXPLAIN_MAIN 1
+#define SST_K_EXPLAIN_DEEP 2
+#define SST_K_EXPLAIN_NOMEMO 3
+#define SST_K_EXPLAIN_EXACT 4
+#define SST_K_COUNT 8
+/* When enabled, every kernel launch of this ctx is bracketed by hipEvents
+ * recorded on the ctx stream; sst_profile_read synchronises and returns the
+ * summed milliseconds and launch counts per kernel id since the last read
+ * (or enable), then resets them. */
+int sst_profile_enable(sst_ctx* ctx, int on);
+int sst_profile_read(sst_ctx* ctx, double* ms_total /* [SST_K_COUNT] */, int64_t* launches /* [SST_K_COUNT] */);
 
 #ifdef __cplusplus
 }

@@ -23,8 +23,13 @@ EXPORTS = (
     "sst_ctx_synchronize", "sst_table_build", "sst_table_upload", "sst_table_set_budgets", "sst_table_shape",
     "sst_table_download", "sst_table_destroy", "sst_is_valid_batch", "sst_is_valid_batch_device",
     "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
-    "sst_result_free", "sst_result_stats",
+    "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_read",
 )
+
+# kernel ids of sst_profile_read
+K_IS_VALID, K_EXPLAIN_MAIN, K_EXPLAIN_DEEP, K_EXPLAIN_NOMEMO, K_EXPLAIN_EXACT = 0, 1, 2, 3, 4
+KERNEL_NAMES = {K_IS_VALID: "k_is_valid", K_EXPLAIN_MAIN: "k_explain_main", K_EXPLAIN_DEEP: "k_explain_deep<0>",
+                K_EXPLAIN_NOMEMO: "k_explain_deep<1>", K_EXPLAIN_EXACT: "k_explain_exact"}
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -70,6 +75,8 @@ def load_library(path=LIB_PATH):
     lib.sst_result_free.argtypes = [_P]
     lib.sst_result_free.restype = None
     lib.sst_result_stats.argtypes = [_P, _P]
+    lib.sst_profile_enable.argtypes = [_P, _I]
+    lib.sst_profile_read.argtypes = [_P, _P, _P]
     return lib
 
 
@@ -121,6 +128,16 @@ class Engine:
 
     def synchronize(self):
         self.check(self._lib.sst_ctx_synchronize(self.handle), "sst_ctx_synchronize")
+
+    def profile(self, on=True):
+        self.check(self._lib.sst_profile_enable(self.handle, int(bool(on))), "sst_profile_enable")
+
+    def profile_read(self):
+        """{kernel id: (total ms, launches)} since the last read."""
+        ms = np.zeros(8, np.float64)
+        n = np.zeros(8, np.int64)
+        self.check(self._lib.sst_profile_read(self.handle, _ptr(ms), _ptr(n)), "sst_profile_read")
+        return {k: (float(ms[k]), int(n[k])) for k in range(8) if n[k]}
 
     def close(self):
         if self.handle:
@@ -304,13 +321,18 @@ class DeviceTable:
         return ExplainResult(self.engine, h, len(m)).fetch()
 
     def explain_device(self, d_mass, d_thr, n, tolerance, precision, max_mods_scalar, d_mods=None, with_memo=True,
-                       cap=2 ** 32):
-        h = ctypes.c_void_p()
+                       cap=2 ** 32, reuse=None):
+        """Queue an explain batch on device buffers (no host sync).  `reuse`: an
+        ExplainResult of this engine with capacity >= n whose buffers are reused."""
+        h = ctypes.c_void_p(reuse.handle.value if reuse is not None else None)
         self.engine.check(self.engine._lib.sst_explain_batch_device(self.handle, d_mass, d_thr, int(n),
                                                                     float(tolerance), float(precision), d_mods,
                                                                     int(max_mods_scalar), int(bool(with_memo)),
                                                                     int(cap), ctypes.byref(h)),
                           "sst_explain_batch_device")
+        if reuse is not None:
+            reuse.n = n
+            return reuse
         return ExplainResult(self.engine, h, n)
 
     def close(self):

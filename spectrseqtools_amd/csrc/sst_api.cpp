@@ -59,6 +59,16 @@ struct sst_ctx {
   DevBuf ws_hash, ws_frames, ws_stacks, ws_epochs;
   uint32_t hash_cap = 0;
   int exact_blocks = 0;
+  // measurement: hipEvents around launches on `stream`
+  bool prof = false;
+  struct Pending {
+    int kid;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
+  double prof_ms[SST_K_COUNT] = {0};
+  int64_t prof_n[SST_K_COUNT] = {0};
 };
 
 struct sst_table {
@@ -77,6 +87,7 @@ struct sst_table {
 struct sst_result {
   sst_ctx* ctx = nullptr;
   int64_t n = 0;
+  int64_t cap_n = 0;
   DevBuf status, count, offset, payload, cursor, counters, lists, stats;
   uint64_t arena_bytes = 0;
   std::vector<int8_t> h_status;
@@ -102,6 +113,55 @@ int fail(sst_ctx* c, int code, const std::string& msg) {
 int set_device(sst_ctx* c) {
   HIP_OK(c, hipSetDevice(c->device));
   return SST_OK;
+}
+
+hipEvent_t take_event(sst_ctx* c) {
+  if (!c->pool.empty()) {
+    hipEvent_t e = c->pool.back();
+    c->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return e;
+}
+
+// bracket one launch with events on the ctx stream when profiling is on
+struct Prof {
+  sst_ctx* c;
+  int kid;
+  hipEvent_t a = nullptr;
+  Prof(sst_ctx* c_, int kid_) : c(c_), kid(kid_) {
+    if (c->prof && (a = take_event(c))) (void)hipEventRecord(a, c->stream);
+  }
+  ~Prof() {
+    if (!a) return;
+    hipEvent_t b = take_event(c);
+    if (!b) {
+      c->pool.push_back(a);
+      return;
+    }
+    (void)hipEventRecord(b, c->stream);
+    c->pending.push_back({kid, a, b});
+  }
+};
+
+void prof_resolve(sst_ctx* c) {
+  for (auto& p : c->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      c->prof_ms[p.kid] += ms;
+      c->prof_n[p.kid] += 1;
+    } else {
+      (void)hipGetLastError();
+    }
+    c->pool.push_back(p.a);
+    c->pool.push_back(p.b);
+  }
+  c->pending.clear();
 }
 
 uint64_t width_mask(int C) { return C == 32 ? ~0ull : ((1ull << (2 * C)) - 1ull); }
@@ -202,6 +262,8 @@ void sst_ctx_destroy(sst_ctx* c) {
   for (DevBuf* b : {&c->in_mass, &c->in_thr, &c->in_mods, &c->out_valid, &c->ws_deep, &c->ws_hash, &c->ws_frames,
                     &c->ws_stacks, &c->ws_epochs})
     b->release();
+  prof_resolve(c);
+  for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -402,6 +464,7 @@ int sst_is_valid_batch_device(sst_table* t, const double* d_mass, const double* 
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
+  Prof p(c, SST_K_IS_VALID);
   HIP_OK(c, launch_is_valid(t->args.valid, t->args.limit, d_mass, d_thr, n, tol, prec, d_out, c->stream));
   return SST_OK;
 }
@@ -469,12 +532,24 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   OutArgs o{(int8_t*)r->status.p,  (uint64_t*)r->count.p,   (uint64_t*)r->offset.p,
             (uint8_t*)r->payload.p, r->arena_bytes,          (uint64_t*)r->cursor.p,
             (uint32_t*)r->counters.p, (uint32_t*)r->lists.p, (unsigned long long*)r->stats.p};
-  HIP_OK(c, launch_explain_main(t->args, q, o, c->stream));
-  HIP_OK(c, launch_explain_deep(t->args, q, o, kClassDeep, c->ws_deep.p, kDeepBlocks, c->stream));
-  HIP_OK(c, launch_explain_deep(t->args, q, o, kClassNomemo, c->ws_deep.p, kDeepBlocks, c->stream));
+  {
+    Prof p(c, SST_K_EXPLAIN_MAIN);
+    HIP_OK(c, launch_explain_main(t->args, q, o, c->stream));
+  }
+  {
+    Prof p(c, SST_K_EXPLAIN_DEEP);
+    HIP_OK(c, launch_explain_deep(t->args, q, o, kClassDeep, c->ws_deep.p, kDeepBlocks, c->stream));
+  }
+  {
+    Prof p(c, SST_K_EXPLAIN_NOMEMO);
+    HIP_OK(c, launch_explain_deep(t->args, q, o, kClassNomemo, c->ws_deep.p, kDeepBlocks, c->stream));
+  }
   ExactWs ws{(char*)c->ws_hash.p, (char*)c->ws_frames.p, (char*)c->ws_stacks.p, (uint64_t*)c->ws_epochs.p,
              c->hash_cap};
-  HIP_OK(c, launch_explain_exact(t->args, q, o, ws, c->exact_blocks, c->stream));
+  {
+    Prof p(c, SST_K_EXPLAIN_EXACT);
+    HIP_OK(c, launch_explain_exact(t->args, q, o, ws, c->exact_blocks, c->stream));
+  }
   return SST_OK;
 }
 
@@ -483,6 +558,7 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out) {
   sst_result* r = new sst_result();
   r->ctx = c;
   r->n = n;
+  r->cap_n = n;
   size_t nn = (size_t)std::max<int64_t>(n, 1);
   r->arena_bytes = std::max<uint64_t>(1u << 20, 16 * (uint64_t)nn);
   if (!r->status.ensure(nn) || !r->count.ensure(nn * 8) || !r->offset.ensure(nn * 8)) {
@@ -531,14 +607,21 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
   if (!t || !out || n < 0 || n > INT32_MAX || (n > 0 && !d_mass)) return SST_E_ARG;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
-  *out = nullptr;
   if (int rc = set_device(c)) return rc;
-  sst_result* r = nullptr;
-  if (int rc = alloc_result(t, n, &r)) return rc;
+  sst_result* r = *out;
+  const bool reuse = r != nullptr;
+  if (reuse) {
+    if (r->ctx != c || n > r->cap_n) return fail(c, SST_E_ARG, "result reuse: other ctx or capacity < n");
+    r->n = n;
+  } else if (int rc = alloc_result(t, n, &r)) {
+    return rc;
+  }
   int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count);
   if (rc) {
-    free_result_bufs(r);
-    delete r;
+    if (!reuse) {
+      free_result_bufs(r);
+      delete r;
+    }
     return rc;
   }
   *out = r;
@@ -649,6 +732,33 @@ void sst_result_free(sst_result* r) {
 int sst_result_stats(const sst_result* r, uint64_t* s) {
   if (!r || !s) return SST_E_ARG;
   for (int i = 0; i < kNumStats; ++i) s[i] = r->h_stats[i];
+  return SST_OK;
+}
+
+int sst_profile_enable(sst_ctx* c, int on) {
+  if (!c) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  prof_resolve(c);
+  for (int i = 0; i < SST_K_COUNT; ++i) {
+    c->prof_ms[i] = 0;
+    c->prof_n[i] = 0;
+  }
+  c->prof = on != 0;
+  return SST_OK;
+}
+
+int sst_profile_read(sst_ctx* c, double* ms, int64_t* n) {
+  if (!c) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  prof_resolve(c);
+  for (int i = 0; i < SST_K_COUNT; ++i) {
+    if (ms) ms[i] = c->prof_ms[i];
+    if (n) n[i] = c->prof_n[i];
+    c->prof_ms[i] = 0;
+    c->prof_n[i] = 0;
+  }
   return SST_OK;
 }
 

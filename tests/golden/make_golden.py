@@ -164,7 +164,7 @@ def rows_of(dp, names_set):
     return sorted(tuple(sorted(idx[n] for n in t)) for t in names_set)
 
 
-def run_explain(dp, cid, mass, threshold, A, with_memo=True, fn="table"):
+def run_explain(dp, cid, mass, threshold, A, with_memo=True, fn="table", names_limit=500):
     rec = {"ctx": cid, "fn": fn, "mass": mass, "threshold": threshold,
            "max_modifications": "inf" if A == np.inf else int(A), "with_memo": with_memo}
     t0 = time.perf_counter()
@@ -184,7 +184,8 @@ def run_explain(dp, cid, mass, threshold, A, with_memo=True, fn="table"):
         rec["status"] = "none"
     else:
         rec["status"] = "set"
-        rec["names"] = sorted(list(t) for t in r)
+        if names_limit is None or len(r) <= names_limit:  # big sets: names follow from rows via MASS_NAMES
+            rec["names"] = sorted(list(t) for t in r)
         rec["rows"] = [list(t) for t in rows_of(dp, r)]
     return rec
 
@@ -262,11 +263,11 @@ def cases():
             cid = f"tem_{''.join(seq)}_{thr:g}"
             dp = make_ctx(cid, int(m / M.TOLERANCE / MIN_INT), thr, su=m)
             A = round(0.5 * len(seq))
-            r = run_explain(dp, cid, m, None, A)
+            r = run_explain(dp, cid, m, None, A, names_limit=None)
             assert tuple(seq) in {tuple(x) for x in r["names"]}
             r["tag"] = "test_explain_masses/table"
             out.append(r)
-            r = run_explain(dp, cid, m, None, A, fn="recursion")
+            r = run_explain(dp, cid, m, None, A, fn="recursion", names_limit=None)
             r["tag"] = "test_explain_masses/recursion"
             out.append(r)
             out.append(dict(run_valid(dp, cid, m, None), tag="test_explain_masses/is_valid"))
@@ -405,6 +406,11 @@ def population():
                     e += 1
         t8 = time.perf_counter() - t0
         ctxs[cid] = CTX[cid]
+        # the spectrum itself (data of the reference's tests/testcases) so the
+        # producer chain can be replayed: observed masses, intensities, meta
+        ctxs[cid]["spectrum"] = {"observed": obs, "intensity": inten, "sequence_mass": meta["sequence_mass"],
+                                 "intensity_cutoff": cutoff, "su_seq": su_seq,
+                                 "tags": [meta.get("label_mass_5T", 555.1294), meta.get("label_mass_3T", 455.1491)]}
         print(f"  {tc}: max_len={max_len} A7={len(obs) * len(bd)} ({t7:.2f}s) A8={n8} ({t8:.2f}s)", flush=True)
         del dp
     dump("population.json.gz", {"contexts": ctxs, "a7": a7, "a8": a8}, gz=True)

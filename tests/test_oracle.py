@@ -1,0 +1,123 @@
+"""Pin the CPU oracle (oracle/sst_oracle.c) to the reference's own outputs
+(tests/golden/, produced by running spectrseq/spectrseqtools unmodified; see
+tests/golden/make_golden.py).  CPU only."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import _oracle as oracle
+from _golden_ctx import budget, ctx_alphabet, ctx_table, sha
+
+
+def test_tiny_tables_verbatim(golden_tables):
+    for tiny in golden_tables["tiny"]:
+        t = oracle.build_table(tiny["masses"], tiny["max_mass"], tiny["compression"])
+        assert list(t.shape) == tiny["shape"]
+        assert t.tolist() == tiny["words"], (tiny["masses"], tiny["max_mass"], tiny["compression"])
+
+
+def test_packed_tables_sha(golden_tables):
+    for p in golden_tables["packed"]:
+        t = oracle.build_table(p["masses"], p["max_mass"], 32)
+        assert list(t.shape) == p["shape"]
+        assert sha(t) == p["sha256"], p["what"]
+        assert [int(np.bitwise_xor.reduce(t[r])) for r in range(t.shape[0])] == p["checksums_per_row"]
+
+
+def _table_cases(golden_cases, fn):
+    return [c for c in golden_cases["cases"] if c["fn"] == fn]
+
+
+def test_explain_with_table_cases(golden_cases):
+    ctxs = golden_cases["contexts"]
+    n = 0
+    for c in _table_cases(golden_cases, "table"):
+        ctx = ctxs[c["ctx"]]
+        st, sols, n_empty, _ = oracle.explain_table(ctx_table(ctx), 32, ctx_alphabet(ctx), c["mass"], c["threshold"],
+                                                    ctx["tolerance"], budget(c["max_modifications"]),
+                                                    with_memo=c["with_memo"])
+        if c["status"] == "raise":
+            assert st == -1, c
+            continue
+        if c["status"] == "none":
+            assert st == 0 and not sols, c
+            continue
+        assert st == 1
+        assert sorted(sols) == sorted(tuple(r) for r in c["rows"]), (c["tag"], c["mass"], c["max_modifications"])
+        assert len(set(sols)) == len(sols)  # the reference's list has no duplicates either
+        n += 1
+    assert n > 1500
+
+
+def test_memo_quirk_is_exercised(golden_cases):
+    """Some golden queries differ between with_memo=True and False: the oracle
+    must reproduce the memo-on semantics, not the budget-exact one."""
+    ctxs = golden_cases["contexts"]
+    differ = 0
+    for c in _table_cases(golden_cases, "table"):
+        if c["status"] != "set" or c["ctx"] not in ("full_L2", "full_L3"):
+            continue
+        ctx = ctxs[c["ctx"]]
+        st, sols, _, _ = oracle.explain_table(ctx_table(ctx), 32, ctx_alphabet(ctx), c["mass"], c["threshold"],
+                                              ctx["tolerance"], budget(c["max_modifications"]), with_memo=False)
+        if sorted(sols) != sorted(tuple(r) for r in c["rows"]):
+            differ += 1
+    assert differ > 0
+
+
+def test_recursion_cases(golden_cases):
+    ctxs = golden_cases["contexts"]
+    for c in _table_cases(golden_cases, "recursion"):
+        ctx = ctxs[c["ctx"]]
+        st, sols, _ = oracle.explain_recursion(ctx_alphabet(ctx), c["mass"], c["threshold"], ctx["tolerance"],
+                                               budget(c["max_modifications"]))
+        assert st == 1
+        assert sorted(sols) == sorted(tuple(r) for r in c["rows"]), (c["ctx"], c["mass"])
+
+
+def test_is_valid_cases(golden_cases):
+    ctxs = golden_cases["contexts"]
+    for c in _table_cases(golden_cases, "is_valid"):
+        ctx = ctxs[c["ctx"]]
+        r = oracle.is_valid(ctx_table(ctx), 32, c["mass"], c["threshold"], ctx["tolerance"])
+        want = -1 if c["result"] == "raise" else int(c["result"])
+        assert r == want, c
+
+
+def test_length_bound_cases(golden_cases):
+    ctxs = golden_cases["contexts"]
+    cases = _table_cases(golden_cases, "length_bound")
+    assert cases
+    for c in cases:
+        ctx = ctxs[c["ctx"]]
+        su = c.get("su_mass", ctx["su_mass"])
+        obs = c.get("obs_mass", ctx["obs_mass"])
+        A = round(ctx["mod_rate"] * ctx["max_len"])
+        got = oracle.length_bound(ctx_table(ctx), 32, ctx_alphabet(ctx), su, obs, ctx["tolerance"], ctx["max_len"], A,
+                                  c["dir"])
+        assert got == c["result"], c
+
+
+def test_population_a7(golden_population):
+    ctxs = golden_population["contexts"]
+    by_ctx = {}
+    for cid, m, t, v in golden_population["a7"]:
+        by_ctx.setdefault(cid, []).append((m, t, v))
+    for cid, rows in by_ctx.items():
+        ctx = ctxs[cid]
+        m = np.array([r[0] for r in rows])
+        t = np.array([r[1] for r in rows])
+        got = oracle.is_valid_batch(ctx_table(ctx), 32, m, t, ctx["tolerance"])
+        assert got.tolist() == [int(r[2]) for r in rows], cid
+
+
+def test_population_a8(golden_population):
+    ctxs = golden_population["contexts"]
+    for cid, m, t, A, rows in golden_population["a8"][::3]:
+        ctx = ctxs[cid]
+        st, sols, n_empty, _ = oracle.explain_table(ctx_table(ctx), 32, ctx_alphabet(ctx), m, t, ctx["tolerance"], A)
+        if rows is None:
+            assert st == 0, (cid, m)
+        else:
+            assert st == 1 and sorted(sols) == sorted(tuple(r) for r in rows), (cid, m)
