@@ -238,7 +238,7 @@ def main():
     w7 = window_words(wl["a7_mass"], wl["a7_thr"], dp.precision, limit)
     w8 = window_words(wl["a8_mass"], wl["a8_thr"], dp.precision, limit)
     bytes7 = float(n7 * (16 + 1) + 8 * w7.sum())
-    bytes8 = float(n8 * (16 + 17) + 8 * w8.sum() + 16 * int(stats[4]) + len(res.payload))
+    bytes8 = float(n8 * (16 + 17) + 8 * w8.sum() + 16 * int(stats[4]) + int(stats[5]))
     kern = {}
     for kid, (ms, cnt) in prof.items():
         kern[_native.KERNEL_NAMES[kid]] = {"avg_us": 1e3 * ms / cnt, "launches": cnt}
@@ -297,7 +297,8 @@ def main():
         "kernels": kern,
         "engine_stats": {"shallow": int(stats[0]), "deep": int(stats[1]), "exact": int(stats[2]),
                          "nomemo": int(stats[3]), "index_loads": int(stats[4]),
-                         "candidates": int(res.count.sum()), "payload_bytes": int(len(res.payload))},
+                         "candidates": int(res.count.sum()), "payload_bytes": int(stats[5]),
+                         "arena_bytes_used": int(len(res.payload))},
         "queries_per_s": (n7_all + n8_all) / (elapsed / args.steps),
         "cpu_baseline": cpu,
     }

@@ -59,6 +59,8 @@ struct sst_ctx {
   DevBuf ws_hash, ws_frames, ws_stacks, ws_epochs;
   uint32_t hash_cap = 0;
   int exact_blocks = 0;
+  int n_cu = 256;       // compute units (persistent grid sizing)
+  int main_blocks = 0;  // resident workgroups of k_explain_main (occupancy x CUs)
   // measurement: hipEvents around launches on `stream`
   bool prof = false;
   struct Pending {
@@ -89,6 +91,10 @@ struct sst_result {
   int64_t n = 0;
   int64_t cap_n = 0;
   DevBuf status, count, offset, payload, cursor, counters, lists, stats;
+  DevBuf wave_used, wave_stats, prefix, dense;
+  int n_waves = 0;
+  uint64_t region_bytes = 0, spill_bytes = 0;
+  bool compacted = false;
   uint64_t arena_bytes = 0;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
@@ -211,6 +217,7 @@ int finish_table(sst_table* t) {
   for (int r = 1; r < t->n_rows; ++r)
     if (t->masses[r] > 0 && (wmin == 0 || t->masses[r] < wmin)) wmin = (int)t->masses[r];
   t->args.w_min = wmin > 0 ? wmin : 1;
+  t->args.shallow_hi = (int64_t)kShallowDepth * t->args.w_min;  // < 4 w_min: at most 3 items
   // default budgets: no modification rows (callers set them)
   std::vector<uint8_t> mod(t->n_rows, 0);
   std::vector<int64_t> cap(t->n_rows, 0);
@@ -247,6 +254,11 @@ int sst_ctx_create(int device, sst_ctx** out) {
   if (device < 0 || device >= n) return SST_E_ARG;
   sst_ctx* c = new sst_ctx();
   c->device = device;
+  {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0) c->n_cu = cu;
+    (void)hipGetLastError();
+  }
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return SST_E_HIP;
@@ -497,6 +509,30 @@ constexpr uint32_t kHashCap0 = 1u << 14;  // exact-path hash entries per lane (f
 constexpr int kExactLanes0 = 2048;      // exact-path concurrent lanes (first attempt)
 constexpr uint64_t kNodeBudget = 1ull << 32;
 
+void free_result_bufs(sst_result* r) {
+  for (DevBuf* b : {&r->status, &r->count, &r->offset, &r->payload, &r->cursor, &r->counters, &r->lists, &r->stats,
+                    &r->wave_used, &r->wave_stats, &r->prefix, &r->dense})
+    b->release();
+}
+
+OutArgs out_args(sst_result* r) {
+  OutArgs o;
+  o.status = (int8_t*)r->status.p;
+  o.count = (uint64_t*)r->count.p;
+  o.offset = (uint64_t*)r->offset.p;
+  o.payload = (uint8_t*)r->payload.p;
+  o.arena_bytes = r->arena_bytes;
+  o.region_bytes = r->region_bytes;
+  o.spill_base = (uint64_t)r->n_waves * r->region_bytes;
+  o.cursor = (uint64_t*)r->cursor.p;
+  o.wave_used = (uint64_t*)r->wave_used.p;
+  o.wave_stats = (unsigned long long*)r->wave_stats.p;
+  o.counters = (uint32_t*)r->counters.p;
+  o.lists = (uint32_t*)r->lists.p;
+  o.stats = (unsigned long long*)r->stats.p;
+  return o;
+}
+
 int ensure_exact_ws(sst_ctx* c, uint32_t hash_cap, int lanes) {
   if (c->hash_cap == hash_cap && c->exact_blocks * 64 == lanes) return SST_OK;
   size_t hb = (size_t)lanes * hash_cap * hash_entry_bytes();
@@ -518,6 +554,7 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
                  int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count) {
   sst_ctx* c = t->ctx;
   const int64_t n = r->n;
+  r->arena_bytes = (uint64_t)r->n_waves * r->region_bytes + r->spill_bytes;
   if (!r->cursor.ensure(8) || !r->counters.ensure(kNumClasses * 4) || !r->stats.ensure(kNumStats * 8) ||
       !r->lists.ensure((size_t)kNumClasses * std::max<int64_t>(n, 1) * 4) || !r->payload.ensure(r->arena_bytes))
     return fail(c, SST_E_NOMEM, "device allocation failed (result)");
@@ -528,13 +565,12 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
     return fail(c, SST_E_NOMEM, "device allocation failed (deep workspace)");
   if (c->hash_cap == 0)
     if (int rc = ensure_exact_ws(c, kHashCap0, kExactLanes0)) return rc;
+  r->compacted = false;
   QueryArgs q{d_mass, d_thr, d_mods, mods_scalar, n, tol, prec, with_memo, cap_count, kNodeBudget};
-  OutArgs o{(int8_t*)r->status.p,  (uint64_t*)r->count.p,   (uint64_t*)r->offset.p,
-            (uint8_t*)r->payload.p, r->arena_bytes,          (uint64_t*)r->cursor.p,
-            (uint32_t*)r->counters.p, (uint32_t*)r->lists.p, (unsigned long long*)r->stats.p};
+  OutArgs o = out_args(r);
   {
     Prof p(c, SST_K_EXPLAIN_MAIN);
-    HIP_OK(c, launch_explain_main(t->args, q, o, c->stream));
+    HIP_OK(c, launch_explain_main(t->args, q, o, r->n_waves / (kWG / 64), c->stream));
   }
   {
     Prof p(c, SST_K_EXPLAIN_DEEP);
@@ -555,13 +591,22 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
 
 int alloc_result(sst_table* t, int64_t n, sst_result** out) {
   sst_ctx* c = t->ctx;
+  if (c->main_blocks == 0) c->main_blocks = c->n_cu * explain_main_blocks_per_cu();
   sst_result* r = new sst_result();
   r->ctx = c;
   r->n = n;
   r->cap_n = n;
   size_t nn = (size_t)std::max<int64_t>(n, 1);
-  r->arena_bytes = std::max<uint64_t>(1u << 20, 16 * (uint64_t)nn);
-  if (!r->status.ensure(nn) || !r->count.ensure(nn * 8) || !r->offset.ensure(nn * 8)) {
+  // one arena region per main-kernel wave sized for ~16 B of payload per
+  // query, plus a spill area for overflowing regions and deferred queries
+  r->n_waves = c->main_blocks * (kWG / 64);
+  uint64_t per_wave = (nn + r->n_waves - 1) / r->n_waves;
+  r->region_bytes = std::max<uint64_t>(256, (16 * per_wave + 15) / 16 * 16);
+  r->spill_bytes = std::max<uint64_t>(1u << 20, 2 * (uint64_t)nn);
+  if (!r->status.ensure(nn) || !r->count.ensure(nn * 8) || !r->offset.ensure(nn * 8) ||
+      !r->wave_used.ensure((size_t)r->n_waves * 8) || !r->wave_stats.ensure((size_t)r->n_waves * kNumStats * 8) ||
+      !r->prefix.ensure((size_t)(r->n_waves + 2) * 8)) {
+    free_result_bufs(r);
     delete r;
     return fail(c, SST_E_NOMEM, "device allocation failed (result)");
   }
@@ -569,31 +614,42 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out) {
   return SST_OK;
 }
 
-void free_result_bufs(sst_result* r) {
-  for (DevBuf* b : {&r->status, &r->count, &r->offset, &r->payload, &r->cursor, &r->counters, &r->lists, &r->stats})
-    b->release();
+// Dense payload: per-wave regions and the spill area copied back to back,
+// offsets rewritten in place (once per explain pass).
+int compact(sst_result* r) {
+  sst_ctx* c = r->ctx;
+  if (r->compacted) return SST_OK;
+  if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, 1)))
+    return fail(c, SST_E_NOMEM, "device allocation failed (compaction)");
+  HIP_OK(c, launch_compact(out_args(r), r->n, r->n_waves, (uint64_t*)r->prefix.p, (uint8_t*)r->dense.p, c->stream));
+  r->compacted = true;
+  return SST_OK;
 }
 
 int fetch(sst_result* r) {
   sst_ctx* c = r->ctx;
   const int64_t n = r->n;
+  if (int rc = compact(r)) return rc;
   r->h_status.resize(n);
   r->h_count.resize(n);
   r->h_offset.resize(n);
-  uint64_t cur = 0;
+  uint64_t pre_tail[2] = {0, 0};
+  std::vector<unsigned long long> ws((size_t)r->n_waves * kNumStats);
   if (n) {
     HIP_OK(c, hipMemcpyAsync(r->h_status.data(), r->status.p, n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipMemcpyAsync(r->h_count.data(), r->count.p, n * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipMemcpyAsync(r->h_offset.data(), r->offset.p, n * 8, hipMemcpyDeviceToHost, c->stream));
   }
-  if (r->cursor.p) HIP_OK(c, hipMemcpyAsync(&cur, r->cursor.p, 8, hipMemcpyDeviceToHost, c->stream));
-  if (r->stats.p)
-    HIP_OK(c, hipMemcpyAsync(r->h_stats, r->stats.p, kNumStats * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipMemcpyAsync(pre_tail, (uint64_t*)r->prefix.p + r->n_waves, 16, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipMemcpyAsync(r->h_stats, r->stats.p, kNumStats * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipMemcpyAsync(ws.data(), r->wave_stats.p, ws.size() * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
-  r->payload_bytes = std::min<uint64_t>(cur, r->arena_bytes);
+  for (int w = 0; w < r->n_waves; ++w)
+    for (int k = 0; k < kNumStats; ++k) r->h_stats[k] += ws[(size_t)w * kNumStats + k];
+  r->payload_bytes = std::min<uint64_t>(pre_tail[1], r->arena_bytes);
   r->h_payload.resize(r->payload_bytes);
   if (r->payload_bytes)
-    HIP_OK(c, hipMemcpy(r->h_payload.data(), r->payload.p, r->payload_bytes, hipMemcpyDeviceToHost));
+    HIP_OK(c, hipMemcpy(r->h_payload.data(), r->dense.p, r->payload_bytes, hipMemcpyDeviceToHost));
   return SST_OK;
 }
 
@@ -665,11 +721,12 @@ int sst_explain_batch(sst_table* t, const double* mass, const double* thr, int64
       break;
     }
     if (!arena_retry && !exact_retry) break;
-    if (arena_retry) {
+    if (arena_retry) {  // the spill cursor kept counting past the arena: size the spill area to it
       uint64_t cur = 0;
       HIP_OK(c, hipMemcpy(&cur, r->cursor.p, 8, hipMemcpyDeviceToHost));
-      r->arena_bytes = std::max<uint64_t>(2 * r->arena_bytes, cur + (1u << 20));
+      r->spill_bytes = std::max<uint64_t>(2 * r->spill_bytes, cur + (1u << 20));
       r->payload.release();
+      r->dense.release();
     }
     if (exact_retry) {
       uint32_t hc = c->hash_cap * 8;
@@ -705,10 +762,13 @@ int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count
 int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint64_t** d_offset, uint8_t** d_payload,
                       uint64_t* payload_bytes) {
   if (!r) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(r->ctx->mu);
+  if (int rc = set_device(r->ctx)) return rc;
+  if (int rc = compact(r)) return rc;  // queued on the ctx stream
   if (d_status) *d_status = (int8_t*)r->status.p;
   if (d_count) *d_count = (uint64_t*)r->count.p;
   if (d_offset) *d_offset = (uint64_t*)r->offset.p;
-  if (d_payload) *d_payload = (uint8_t*)r->payload.p;
+  if (d_payload) *d_payload = (uint8_t*)r->dense.p;
   if (payload_bytes) *payload_bytes = r->arena_bytes;
   return SST_OK;
 }

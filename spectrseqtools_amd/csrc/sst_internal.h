@@ -26,6 +26,7 @@ enum {
   kStatExact = 2,
   kStatNomemo = 3,
   kStatNodes = 4,
+  kStatPayload = 5,
   kNumStats = 8
 };
 
@@ -39,6 +40,7 @@ struct TableArgs {
   uint64_t mod0, mod1;      // row masks of modification rows
   uint64_t capz0, capz1;    // row masks with cap <= 0
   int64_t fast_limit_B;     // max window value for which no per-row cap can bind
+  int64_t shallow_hi;       // window values < shallow_hi (= 4 * w_min) fit in <= 3 items
   int n_rows;
   int any_mod;
   int w_min;                // smallest positive row mass
@@ -57,16 +59,26 @@ struct QueryArgs {
   uint64_t node_budget;
 };
 
+// Arena layout of one explain pass:
+//   [0, n_waves * region)  one region per wave of the main kernel (bump
+//                          allocated by that wave alone: no atomics)
+//   [spill_base, arena)    spill area, atomically allocated (regions that
+//                          overflow, deep / exact / no-memo queries)
+// sst_result_fetch / _device compact it to a dense payload.
 struct OutArgs {
   int8_t* status;
   uint64_t* count;
   uint64_t* offset;
   uint8_t* payload;
   uint64_t arena_bytes;
-  uint64_t* cursor;
+  uint64_t region_bytes;      // per-wave region of the main kernel
+  uint64_t spill_base;        // = n_waves * region_bytes
+  uint64_t* cursor;           // spill bytes taken
+  uint64_t* wave_used;        // [n_waves] bytes used in each region
+  unsigned long long* wave_stats;  // [n_waves][kNumStats] main-kernel counters
   uint32_t* counters;  // [kNumClasses]
   uint32_t* lists;     // [kNumClasses][n]
-  unsigned long long* stats;  // [kNumStats]
+  unsigned long long* stats;  // [kNumStats] deferred-kernel counters
 };
 
 struct ExactWs {
@@ -88,7 +100,10 @@ hipError_t launch_index(int C, const void* packed, int n_rows, int64_t ncols, in
                         uint64_t* valid, int* err, hipStream_t st);
 hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, const double* mass, const double* thr, int64_t n,
                            double tol, double prec, int8_t* out, hipStream_t st);
-hipError_t launch_explain_main(const TableArgs& t, const QueryArgs& q, const OutArgs& o, hipStream_t st);
+hipError_t launch_explain_main(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks, hipStream_t st);
+int explain_main_blocks_per_cu();
+hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* wave_prefix, uint8_t* dst,
+                          hipStream_t st);
 hipError_t launch_explain_deep(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int cls, void* ws,
                                int n_blocks, hipStream_t st);
 hipError_t launch_explain_exact(const TableArgs& t, const QueryArgs& q, const OutArgs& o, const ExactWs& ws,

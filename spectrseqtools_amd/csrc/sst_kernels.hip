@@ -361,45 +361,59 @@ __device__ __forceinline__ bool budgets_never_bind(const TableArgs& t, int64_t h
   return hi < (int64_t)(A + 1) * t.w_min_mod;
 }
 
-// emit one candidate: path rows sr[0..d] were chosen top-down (descending
-// rows); the reference's list is ascending mass == ascending row.
-template <typename Stack>
-__device__ __forceinline__ void emit(uint8_t* dst, const Stack& st, int d) {
-  dst[0] = (uint8_t)(d + 1);
-  for (int k = 0; k <= d; ++k) dst[1 + k] = st.row(d - k);
-}
-
-// Per-lane DFS stack.  Reg<D>: private arrays the compiler keeps in VGPRs for
-// small D.  Glob: a per-lane slice of a global workspace (deep / exact paths).
-template <int D>
-struct RegStack {
-  uint32_t m_[D];
-  uint64_t a_[D], b_[D];
-  uint8_t r_[D];
-  int A_[D], B_[D];
-  uint8_t top_[D];
-  static constexpr int depth = D;
-  __device__ __forceinline__ uint32_t m(int d) const { return m_[d]; }
-  __device__ __forceinline__ M128 mask(int d) const { return {a_[d], b_[d]}; }
-  __device__ __forceinline__ uint8_t row(int d) const { return r_[d]; }
-  __device__ __forceinline__ void set(int d, uint32_t m, M128 k) {
-    m_[d] = m;
-    a_[d] = k.a;
-    b_[d] = k.b;
+// Candidate sinks.  A candidate is the path rows st.row(0..d), chosen top-down
+// (descending rows); the payload record is [d+1][rows ascending] (the
+// reference's solution list is ascending mass == ascending row).
+struct CountSink {
+  template <typename Stack>
+  __device__ __forceinline__ void put(const Stack&, int, uint64_t) {}
+};
+struct MemSink {  // straight to the arena (deep / exact / overflowed shallow)
+  uint8_t* dst;
+  uint64_t cap_count;
+  uint64_t written = 0;
+  template <typename Stack>
+  __device__ __forceinline__ void put(const Stack& st, int d, uint64_t pos) {
+    if (written++ >= cap_count) return;
+    dst[pos] = (uint8_t)(d + 1);
+    for (int k = 0; k <= d; ++k) dst[pos + 1 + k] = st.row(d - k);
   }
-  __device__ __forceinline__ void set_mask(int d, M128 k) {
-    a_[d] = k.a;
-    b_[d] = k.b;
+};
+// Sinks of the shallow path receive the (<= 3) rows ascending as scalars.
+struct CountSink3 {
+  __device__ __forceinline__ void put(uint64_t, int, int, int, int) {}
+};
+struct MemSink3 {
+  uint8_t* dst;
+  __device__ __forceinline__ void put(uint64_t pos, int n, int r0, int r1, int r2) {
+    dst[pos] = (uint8_t)n;
+    dst[pos + 1] = (uint8_t)r0;
+    if (n > 1) dst[pos + 2] = (uint8_t)r1;
+    if (n > 2) dst[pos + 3] = (uint8_t)r2;
   }
-  __device__ __forceinline__ void set_row(int d, int r) { r_[d] = (uint8_t)r; }
-  __device__ __forceinline__ void set_budget(int d, int A, int B, int top) {
-    A_[d] = A;
-    B_[d] = B;
-    top_[d] = (uint8_t)top;
+};
+struct RegSink {  // first 16 payload bytes of a lane kept in two VGPR pairs
+  uint64_t lo = 0, hi = 0;
+  bool over = false;
+  __device__ __forceinline__ void byte(int p, uint64_t b) {
+    uint64_t v = b << (8 * (p & 7));
+    if (p < 8) lo |= v;
+    else hi |= v;
   }
-  __device__ __forceinline__ int A(int d) const { return A_[d]; }
-  __device__ __forceinline__ int B(int d) const { return B_[d]; }
-  __device__ __forceinline__ int top(int d) const { return top_[d]; }
+  __device__ __forceinline__ void put(uint64_t pos, int n, int r0, int r1, int r2) {
+    if (pos + n + 1 > 16) {
+      over = true;
+      return;
+    }
+    int p = (int)pos;
+    byte(p, (uint64_t)n);
+    byte(p + 1, (uint64_t)r0);
+    if (n > 1) byte(p + 2, (uint64_t)r1);
+    if (n > 2) byte(p + 3, (uint64_t)r2);
+  }
+  __device__ __forceinline__ void flush(uint8_t* dst, uint64_t nbytes) const {
+    for (uint64_t p = 0; p < nbytes; ++p) dst[p] = (uint8_t)((p < 8 ? lo : hi) >> (8 * (p & 7)));
+  }
 };
 
 struct GlobFrame {
@@ -498,9 +512,9 @@ struct EnumOut {
   int fail;  // 1 depth, 2 node budget
 };
 
-template <int MODE, typename Stack>
-__device__ void enumerate_root(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, uint32_t v, int A0,
-                               uint8_t* dst, uint64_t cap_count, uint64_t node_budget, EnumOut& o) {
+template <int MODE, typename Stack, typename Sink>
+__device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, uint32_t v, int A0,
+                               Sink& sink, uint64_t node_budget, EnumOut& o) {
   const int top_row = t.n_rows - 1;
   M128 k0;
   if (MODE == MODE_EXACT) {
@@ -532,9 +546,7 @@ __device__ void enumerate_root(const TableArgs& t, const Lds& s, Stack& st, cons
     int64_t child = (int64_t)st.m(d) - s.w[rr];
     st.set_row(d, rr);
     if (child == 0) {
-      if (dst && o.count < cap_count) {
-        emit(dst + o.bytes, st, d);
-      }
+      sink.put(st, d, o.bytes);
       o.bytes += (uint64_t)(d + 2);
       o.count++;
       continue;
@@ -572,9 +584,9 @@ __device__ void enumerate_root(const TableArgs& t, const Lds& s, Stack& st, cons
 }
 
 // payload bytes/counts of a whole window [a, b] of roots
-template <int MODE, typename Stack>
-__device__ void enumerate_window(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, int64_t a, int64_t b,
-                                 int A0, uint8_t* dst, uint64_t cap_count, uint64_t node_budget, EnumOut& o) {
+template <int MODE, typename Stack, typename Sink>
+__device__ __forceinline__ void enumerate_window(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, int64_t a, int64_t b,
+                                 int A0, Sink& sink, uint64_t node_budget, EnumOut& o) {
   if (a > b) return;
   int64_t wa = a >> 6, wb = b >> 6;
   for (int64_t wi = wa; wi <= wb; ++wi) {
@@ -585,8 +597,72 @@ __device__ void enumerate_window(const TableArgs& t, const Lds& s, Stack& st, co
       int bit = __builtin_ctzll(x);
       x &= x - 1;
       uint32_t v = (uint32_t)((wi << 6) + bit);
-      enumerate_root<MODE>(t, s, st, h, v, A0, dst ? dst : nullptr, cap_count, node_budget, o);
+      enumerate_root<MODE>(t, s, st, h, v, A0, sink, node_budget, o);
       if (o.fail) return;
+    }
+  }
+}
+
+// SHALLOW fast path: budgets never bind and every window value is below
+// 4 * w_min, so a candidate has at most 3 items.  The chain-form DFS
+// (ascending rows at each level, as the reference's solution lists) becomes
+// three explicit loops with all state in registers.
+template <typename Sink>
+__device__ __forceinline__ void shallow_window(const TableArgs& t, const Lds& s, int64_t a, int64_t b, Sink& sink,
+                                               EnumOut& o) {
+  if (a > b) return;
+  const M128 top_mask = rows_upto(t.n_rows - 1);
+  const int64_t wa = a >> 6, wb = b >> 6;
+  for (int64_t wi = wa; wi <= wb; ++wi) {
+    uint64_t x = t.valid[wi];
+    if (wi == wa) x &= ~0ull << (a & 63);
+    if (wi == wb) x &= ~0ull >> (63 - (b & 63));
+    while (x) {
+      const int64_t v = (wi << 6) + __builtin_ctzll(x);
+      x &= x - 1;
+      M128 k1 = mand(rec_L(ld_index(t.index, v)), top_mask);
+      o.nodes++;
+      while (!mzero(k1)) {
+        const int r1 = mlow(k1);
+        k1 = mclear(k1, r1);
+        const int64_t c1 = v - s.w[r1];
+        if (c1 == 0) {
+          sink.put(o.bytes, 1, r1, 0, 0);
+          o.bytes += 2;
+          o.count++;
+          continue;
+        }
+        if (c1 < 0) continue;
+        const ulonglong2 rec1 = ld_index(t.index, c1);
+        o.nodes++;
+        if (rec_lo(rec1) > r1) continue;
+        M128 k2 = mand(rec_L(rec1), rows_upto(r1));
+        while (!mzero(k2)) {
+          const int r2 = mlow(k2);
+          k2 = mclear(k2, r2);
+          const int64_t c2 = c1 - s.w[r2];
+          if (c2 == 0) {
+            sink.put(o.bytes, 2, r2, r1, 0);
+            o.bytes += 3;
+            o.count++;
+            continue;
+          }
+          if (c2 < 0) continue;
+          const ulonglong2 rec2 = ld_index(t.index, c2);
+          o.nodes++;
+          if (rec_lo(rec2) > r2) continue;
+          M128 k3 = mand(rec_L(rec2), rows_upto(r2));
+          while (!mzero(k3)) {  // a 4th item cannot fit below 4 * w_min
+            const int r3 = mlow(k3);
+            k3 = mclear(k3, r3);
+            if (c2 == s.w[r3]) {
+              sink.put(o.bytes, 3, r3, r2, r1);
+              o.bytes += 4;
+              o.count++;
+            }
+          }
+        }
+      }
     }
   }
 }
@@ -725,100 +801,192 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
   return x;
 }
 
-__device__ __forceinline__ uint64_t wg_alloc(uint64_t mine, uint64_t* cursor, uint64_t& base_out) {
-  __shared__ uint64_t wsum[kWG / 64];
-  __shared__ uint64_t base;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t incl = wave_incl_scan(mine);
-  if (lane == 63) wsum[wv] = incl;
+// Sum a per-lane counter over the workgroup and add it to stats[k] with one
+// atomic (all threads of the workgroup must call it).
+__device__ __forceinline__ void wg_stat(unsigned long long* stats, int k, uint64_t v) {
+  __shared__ uint64_t red[kWG / 64];
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  uint64_t before = 0, total = 0;
-  for (int i = 0; i < kWG / 64; ++i) {
-    if (i < wv) before += wsum[i];
-    total += wsum[i];
+  if (threadIdx.x == 0) {
+    uint64_t tot = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tot += red[i];
+    if (tot) atomicAdd(&stats[k], (unsigned long long)tot);
   }
-  if (threadIdx.x == 0) base = total ? atomicAdd((unsigned long long*)cursor, (unsigned long long)total) : 0;
   __syncthreads();
-  base_out = base;
-  return before + incl - mine;
 }
 
 // ---------------------------------------------------------------------------
-// main explain kernel: plan every query, resolve trivial ones, run SHALLOW
-// fast-path queries in registers, queue the rest.
+// main explain kernel (persistent grid, independent waves): every wave takes
+// 64-query tiles in a grid stride, plans each query, resolves the trivial
+// ones, runs SHALLOW fast-path queries with all DFS state and the first 16
+// payload bytes in VGPRs, and queues the rest.  Payload goes to the wave's own
+// arena region through a bump pointer fed by a wavefront prefix sum: no
+// barriers and no atomics inside the loop (a full region spills, one atomic
+// per tile).  Counters go to per-wave slots.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kWG) void k_explain_main(TableArgs t, QueryArgs q, OutArgs out) {
   __shared__ Lds s;
   stage_rows(s, t);
-  const int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  const bool live = i < q.n;
-  int8_t status = SST_NONE;
-  uint64_t cnt = 0, bytes = 0;
-  bool shallow = false;
-  int64_t a = 0, b = -1;
-  int A0 = 0;
-  if (live) {
-    int64_t lo, hi;
-    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, lo, hi);
-    A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
-    if (hi < lo) {
-      status = SST_NONE;
-    } else if (hi >= t.limit) {
-      status = SST_OUT_OF_TABLE;  // mass_explanation.py:134-138 (raises NameError)
-    } else {
-      bool has_zero = lo <= 0 && hi >= 0;
-      a = lo < 1 ? 1 : lo;
-      b = hi;
-      bool roots = a <= b && any_bits(t.valid, a, b);
-      status = has_zero ? SST_EMPTY : SST_NONE;
-      if (roots) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+  const int64_t n_waves = (int64_t)gridDim.x * (kWG / 64);
+  const uint64_t region0 = (uint64_t)wave * out.region_bytes;
+  uint64_t used = 0;  // wave-uniform bump pointer
+  uint64_t st_shallow = 0, st_nodes = 0, st_payload = 0;
+  const int64_t ntiles = (q.n + 63) / 64;
+  for (int64_t tile = wave; tile < ntiles; tile += n_waves) {
+    const int64_t i = tile * 64 + lane;
+    const bool live = i < q.n;
+    int8_t status = SST_NONE;
+    uint64_t cnt = 0, bytes = 0;
+    bool shallow = false;
+    int64_t a = 0, b = -1;
+    if (live) {
+      int64_t lo, hi;
+      quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, lo, hi);
+      const int A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
+      if (hi < lo) {
+        status = SST_NONE;
+      } else if (hi >= t.limit) {
+        status = SST_OUT_OF_TABLE;  // mass_explanation.py:134-138 (raises NameError)
+      } else {
+        status = (lo <= 0 && hi >= 0) ? SST_EMPTY : SST_NONE;  // v == 0 -> [[]] (:130-131)
+        a = lo < 1 ? 1 : lo;
+        b = hi;
         int cls;
-        if (!q.with_memo) cls = budgets_never_bind(t, hi, A0) ? kClassShallow : kClassNomemo;
-        else cls = budgets_never_bind(t, hi, A0) ? kClassShallow : kClassExact;
-        if (cls == kClassShallow && hi / t.w_min + 1 > kShallowDepth) cls = kClassDeep;
+        if (budgets_never_bind(t, hi, A0)) cls = hi < t.shallow_hi ? kClassShallow : kClassDeep;
+        else cls = q.with_memo ? kClassExact : kClassNomemo;
         if (cls == kClassShallow) {
-          shallow = true;
-        } else {
-          // defer: wave-aggregated append to the class list
+          shallow = a <= b;
+        } else if (a <= b && any_bits(t.valid, a, b)) {
           uint32_t slot = atomicAdd(&out.counters[cls], 1u);
           out.lists[(int64_t)cls * q.n + slot] = (uint32_t)i;
           status = (int8_t)kStatusPending;
         }
       }
     }
-  }
-  RegStack<kShallowDepth> st;
-  EnumOut eo{0, 0, 0, 0};
-  if (shallow) {
-    enumerate_window<MODE_FAST>(t, s, st, nullptr, a, b, A0, nullptr, ~0ull, ~0ull, eo);
-    cnt = eo.count;
-    if (cnt > 0) status = SST_SOME;
-    if (cnt > q.cap_count) {
-      status = SST_OVERFLOW;
-      bytes = 0;
-    } else {
-      bytes = eo.bytes;
+    RegSink sink;
+    EnumOut eo{0, 0, 0, 0};
+    if (shallow) {
+      shallow_window(t, s, a, b, sink, eo);
+      cnt = eo.count;
+      if (cnt > 0) status = SST_SOME;
+      bytes = cnt > q.cap_count ? 0 : eo.bytes;
+      if (cnt > q.cap_count) status = SST_OVERFLOW;
+      st_shallow++;
+      st_nodes += eo.nodes;
     }
+    const uint64_t incl = wave_incl_scan(bytes);
+    const uint64_t total = __shfl(incl, 63, 64);
+    uint64_t base = 0;
+    if (total) {
+      if (used + total <= out.region_bytes) {
+        base = region0 + used;
+        used += total;
+      } else {
+        unsigned long long sb = 0;
+        if (lane == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
+        base = out.spill_base + __shfl(sb, 0, 64);
+      }
+    }
+    const uint64_t off = base + incl - bytes;
+    if (bytes && off + bytes > out.arena_bytes) {
+      status = (int8_t)kStatusArenaRetry;
+      bytes = 0;
+    }
+    if (bytes) {
+      if (!sink.over) {
+        sink.flush(out.payload + off, bytes);
+      } else {  // more than 16 bytes: enumerate again straight into the arena
+        MemSink3 ms{out.payload + off};
+        EnumOut e2{0, 0, 0, 0};
+        shallow_window(t, s, a, b, ms, e2);
+      }
+    }
+    if (live) {
+      out.status[i] = status;
+      out.count[i] = cnt;
+      out.offset[i] = bytes ? off : 0;
+    }
+    st_payload += bytes;
   }
-  uint64_t base;
-  uint64_t off = wg_alloc(bytes, out.cursor, base);
-  off += base;
-  if (bytes && off + bytes > out.arena_bytes) {
-    status = (int8_t)kStatusArenaRetry;
-    bytes = 0;
+  for (int o = 32; o > 0; o >>= 1) {
+    st_shallow += __shfl_down(st_shallow, o, 64);
+    st_nodes += __shfl_down(st_nodes, o, 64);
+    st_payload += __shfl_down(st_payload, o, 64);
   }
-  if (shallow && bytes) {
-    EnumOut e2{0, 0, 0, 0};
-    enumerate_window<MODE_FAST>(t, s, st, nullptr, a, b, A0, out.payload + off, ~0ull, ~0ull, e2);
+  if (lane == 0) {
+    out.wave_used[wave] = used;
+    unsigned long long* ws = out.wave_stats + wave * kNumStats;
+    for (int k = 0; k < kNumStats; ++k) ws[k] = 0;
+    ws[kStatShallow] = st_shallow;
+    ws[kStatNodes] = st_nodes;
+    ws[kStatPayload] = st_payload;
   }
-  if (live) {
-    out.status[i] = status;
-    out.count[i] = cnt;
-    out.offset[i] = bytes ? off : 0;
+}
+
+// Compaction of the arena into a dense payload (result fetch / gather only):
+// exclusive prefix over the per-wave regions, block copies, offset rewrite.
+__global__ __launch_bounds__(1024) void k_wave_prefix(const uint64_t* __restrict__ used, int n_waves,
+                                                      const uint64_t* __restrict__ cursor, uint64_t* __restrict__ pre) {
+  __shared__ uint64_t part[1024];
+  const int per = (n_waves + 1023) / 1024;
+  const int b0 = threadIdx.x * per;
+  uint64_t sum = 0;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < n_waves) sum += used[b0 + k];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
   }
-  if (shallow) {
-    atomicAdd((unsigned long long*)&out.stats[kStatShallow], 1ull);
-    atomicAdd((unsigned long long*)&out.stats[kStatNodes], (unsigned long long)eo.nodes);
+  uint64_t run = part[threadIdx.x] - sum;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < n_waves) {
+      pre[b0 + k] = run;
+      run += used[b0 + k];
+    }
+  if (threadIdx.x == 1023) {
+    pre[n_waves] = part[1023];             // bytes of all regions
+    pre[n_waves + 1] = part[1023] + *cursor;  // + spill bytes = dense payload size
+  }
+}
+
+__global__ __launch_bounds__(256) void k_compact_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                      const uint64_t* __restrict__ used,
+                                                      const uint64_t* __restrict__ pre, int n_waves, uint64_t region,
+                                                      uint64_t spill_base, const uint64_t* __restrict__ cursor) {
+  for (int w = blockIdx.x; w <= n_waves; w += gridDim.x) {
+    uint64_t len, from, to;
+    if (w < n_waves) {
+      len = used[w];
+      from = (uint64_t)w * region;
+      to = pre[w];
+    } else {
+      len = *cursor;
+      from = spill_base;
+      to = pre[n_waves];
+    }
+    for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) dst[to + k] = src[from + k];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_compact_offsets(const int8_t* __restrict__ status,
+                                                         const uint64_t* __restrict__ count, uint64_t* offset, int64_t n,
+                                                         const uint64_t* __restrict__ pre, int n_waves, uint64_t region,
+                                                         uint64_t spill_base) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (status[i] != SST_SOME) return;
+  uint64_t o = offset[i];
+  if (o >= spill_base) offset[i] = o - spill_base + pre[n_waves];
+  else {
+    uint64_t w = o / region;
+    offset[i] = o - w * region + pre[w];
   }
 }
 
@@ -833,6 +1001,7 @@ __global__ __launch_bounds__(kWG) void k_explain_deep(TableArgs t, QueryArgs q, 
   const int64_t gid = (int64_t)blockIdx.x * kWG + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * kWG;
   GlobStack st{ws + gid * kMaxDepth};
+  uint64_t st_n = 0, st_nodes = 0;
   for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
     int64_t i = out.lists[(int64_t)cls * q.n + j];
     int64_t lo, hi;
@@ -841,7 +1010,8 @@ __global__ __launch_bounds__(kWG) void k_explain_deep(TableArgs t, QueryArgs q, 
     bool has_zero = lo <= 0 && hi >= 0;
     int64_t a = lo < 1 ? 1 : lo, b = hi;
     EnumOut eo{0, 0, 0, 0};
-    enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, nullptr, ~0ull, q.node_budget, eo);
+    CountSink cs;
+    enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, cs, q.node_budget, eo);
     int8_t status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
     uint64_t bytes = eo.bytes;
     if (eo.fail) {
@@ -853,21 +1023,24 @@ __global__ __launch_bounds__(kWG) void k_explain_deep(TableArgs t, QueryArgs q, 
     }
     uint64_t off = 0;
     if (bytes) {
-      off = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
+      off = out.spill_base + atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
       if (off + bytes > out.arena_bytes) {
         status = (int8_t)kStatusArenaRetry;
         bytes = 0;
       } else {
+        MemSink ms{out.payload + off, ~0ull};
         EnumOut e2{0, 0, 0, 0};
-        enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, out.payload + off, ~0ull, ~0ull, e2);
+        enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2);
       }
     }
     out.status[i] = status;
     out.count[i] = eo.count;
     out.offset[i] = bytes ? off : 0;
-    atomicAdd((unsigned long long*)&out.stats[MODE == MODE_FAST ? kStatDeep : kStatNomemo], 1ull);
-    atomicAdd((unsigned long long*)&out.stats[kStatNodes], (unsigned long long)eo.nodes);
+    st_n++;
+    st_nodes += eo.nodes;
   }
+  wg_stat(out.stats, MODE == MODE_FAST ? kStatDeep : kStatNomemo, st_n);
+  wg_stat(out.stats, kStatNodes, st_nodes);
 }
 
 // Deferred budget-binding queries: exact memo replay (phase 1) + enabled-DAG
@@ -884,6 +1057,7 @@ __global__ __launch_bounds__(64) void k_explain_exact(TableArgs t, QueryArgs q, 
   h.e = (HEntry*)(ws.hash + (size_t)gid * ws.hash_cap * sizeof(HEntry));
   h.mask = ws.hash_cap - 1;
   h.limit = (uint32_t)(ws.hash_cap * 0.7);
+  uint64_t st_n = 0, st_nodes = 0;
   for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
     int64_t i = out.lists[(int64_t)kClassExact * q.n + j];
     int64_t lo, hi;
@@ -903,7 +1077,8 @@ __global__ __launch_bounds__(64) void k_explain_exact(TableArgs t, QueryArgs q, 
     } else if (rc < 0) {
       status = SST_ABORTED;
     } else {
-      enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, nullptr, ~0ull, q.node_budget, eo);
+      CountSink cs;
+      enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, cs, q.node_budget, eo);
       status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
       bytes = eo.bytes;
       if (eo.fail) {
@@ -916,21 +1091,24 @@ __global__ __launch_bounds__(64) void k_explain_exact(TableArgs t, QueryArgs q, 
     }
     uint64_t off = 0;
     if (bytes) {
-      off = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
+      off = out.spill_base + atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
       if (off + bytes > out.arena_bytes) {
         status = (int8_t)kStatusArenaRetry;
         bytes = 0;
       } else {
+        MemSink ms{out.payload + off, ~0ull};
         EnumOut e2{0, 0, 0, 0};
-        enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, out.payload + off, ~0ull, ~0ull, e2);
+        enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, ms, ~0ull, e2);
       }
     }
     out.status[i] = status;
     out.count[i] = eo.count;
     out.offset[i] = bytes ? off : 0;
-    atomicAdd((unsigned long long*)&out.stats[kStatExact], 1ull);
-    atomicAdd((unsigned long long*)&out.stats[kStatNodes], (unsigned long long)(nodes + eo.nodes));
+    st_n++;
+    st_nodes += nodes + eo.nodes;
   }
+  wg_stat(out.stats, kStatExact, st_n);
+  wg_stat(out.stats, kStatNodes, st_nodes);
 }
 
 // ---------------------------------------------------------------------------
@@ -994,9 +1172,26 @@ hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, const double* m
                      out);
   return hipGetLastError();
 }
-hipError_t launch_explain_main(const TableArgs& t, const QueryArgs& q, const OutArgs& o, hipStream_t st) {
+hipError_t launch_explain_main(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks, hipStream_t st) {
   if (q.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_explain_main, dim3(blocks_for(q.n, kWG)), dim3(kWG), 0, st, t, q, o);
+  hipLaunchKernelGGL(k_explain_main, dim3(n_blocks), dim3(kWG), 0, st, t, q, o);
+  return hipGetLastError();
+}
+int explain_main_blocks_per_cu() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_explain_main, kWG, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return 4;
+  }
+  return nb > 0 ? nb : 1;
+}
+hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* pre, uint8_t* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_wave_prefix, dim3(1), dim3(1024), 0, st, o.wave_used, n_waves, o.cursor, pre);
+  hipLaunchKernelGGL(k_compact_copy, dim3(2048), dim3(256), 0, st, o.payload, dst, o.wave_used, pre, n_waves,
+                     o.region_bytes, o.spill_base, o.cursor);
+  if (n > 0)
+    hipLaunchKernelGGL(k_compact_offsets, dim3(blocks_for(n, 256)), dim3(256), 0, st, o.status, o.count, o.offset, n,
+                       pre, n_waves, o.region_bytes, o.spill_base);
   return hipGetLastError();
 }
 hipError_t launch_explain_deep(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int cls, void* ws,

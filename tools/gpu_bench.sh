@@ -10,6 +10,6 @@ export TMPDIR=/tmp
 timeout -k 10 600 python bench.py $ARGS > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 rc=$?; echo "[bench] rc=$rc"; tail -c 3000 gpurun_out/${TAG}_bench.json; tail -3 gpurun_out/${TAG}_bench.err
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o trace -- python3 bench.py $ARGS --no-cpu-baseline > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof.err
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o trace -- python3 bench.py $ARGS --no-cpu-baseline > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof.err
 rc=$?; echo "[rocprof] rc=$rc"
 find gpurun_out/${TAG}_prof -name "*stats*" | head

@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU-box counter passes (one rocprofv3 --pmc pass per counter group, kernel
+# trace only, no sys/runtime trace) over a short bench run, plus the counter list.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+TAG=${1:-pmc}
+shift
+export TMPDIR=/tmp
+BENCH="bench.py --steps 5 --warmup 1 --no-cpu-baseline $@"
+timeout -k 10 120 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1 || true
+i=0
+
+while read -r grp; do
+  [ -z "$grp" ] && continue
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${TAG}_p$i -o pmc -- python3 $BENCH > gpurun_out/${TAG}_p$i.log 2>&1
+  rc=$?; echo "[pmc $i: $grp] rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+done < tools/pmc_groups.txt
