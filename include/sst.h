@@ -120,7 +120,10 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
 /* Host views of a result (valid until sst_result_free):
  *   status[n] (SST_NONE..), count[n] candidates, offset[n] byte offset of the
  *   query's candidates in payload; payload = per candidate one length byte k
- *   followed by k row indices (ascending, i.e. ascending mass). */
+ *   followed by k row indices (ascending, i.e. ascending mass).
+ *   count[i] and offset[i] are defined only when status[i] is SST_SOME,
+ *   SST_OVERFLOW or SST_ABORTED (the others carry no candidates; the engine
+ *   does not spend HBM writes on them). */
 int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count, const uint64_t** offset,
                     const uint8_t** payload, uint64_t* payload_bytes);
 /* Device views (no copy). */
@@ -143,6 +146,7 @@ int sst_result_stats(const sst_result* r, uint64_t* stats_out /* [8] */);
 #define SST_K_EXPLAIN_DEEP 2
 #define SST_K_EXPLAIN_NOMEMO 3
 #define SST_K_EXPLAIN_EXACT 4
+#define SST_K_EXPLAIN_EXPAND 5
 #define SST_K_COUNT 8
 /* When enabled, every kernel launch of this ctx is bracketed by hipEvents
  * recorded on the ctx stream; sst_profile_read synchronises and returns the

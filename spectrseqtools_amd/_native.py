@@ -27,9 +27,10 @@ EXPORTS = (
 )
 
 # kernel ids of sst_profile_read
-K_IS_VALID, K_EXPLAIN_MAIN, K_EXPLAIN_DEEP, K_EXPLAIN_NOMEMO, K_EXPLAIN_EXACT = 0, 1, 2, 3, 4
-KERNEL_NAMES = {K_IS_VALID: "k_is_valid", K_EXPLAIN_MAIN: "k_explain_main", K_EXPLAIN_DEEP: "k_explain_deep<0>",
-                K_EXPLAIN_NOMEMO: "k_explain_deep<1>", K_EXPLAIN_EXACT: "k_explain_exact"}
+K_IS_VALID, K_EXPLAIN_SCAN, K_EXPLAIN_DEEP, K_EXPLAIN_NOMEMO, K_EXPLAIN_EXACT, K_EXPLAIN_EXPAND = 0, 1, 2, 3, 4, 5
+KERNEL_NAMES = {K_IS_VALID: "k_is_valid", K_EXPLAIN_SCAN: "k_explain_scan", K_EXPLAIN_DEEP: "k_explain_deep<0>",
+                K_EXPLAIN_NOMEMO: "k_explain_deep<1>", K_EXPLAIN_EXACT: "k_explain_exact",
+                K_EXPLAIN_EXPAND: "k_explain_expand"}
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -199,6 +200,10 @@ class ExplainResult:
         self.count = view(cnt, np.uint64, n)
         self.offset = view(off, np.uint64, n)
         self.payload = view(pay, np.uint8, int(nb.value))
+        # count/offset are defined only for statuses that carry candidates (include/sst.h)
+        none = ~np.isin(self.status, (SST_SOME, SST_OVERFLOW, SST_ABORTED))
+        self.count[none] = 0
+        self.offset[none] = 0
         return self
 
     def stats(self):

@@ -60,7 +60,7 @@ struct sst_ctx {
   uint32_t hash_cap = 0;
   int exact_blocks = 0;
   int n_cu = 256;       // compute units (persistent grid sizing)
-  int main_blocks = 0;  // resident workgroups of k_explain_main (occupancy x CUs)
+  int expand_blocks = 0;  // resident workgroups of k_explain_expand
   // measurement: hipEvents around launches on `stream`
   bool prof = false;
   struct Pending {
@@ -82,7 +82,8 @@ struct sst_table {
   std::vector<int64_t> masses;
   std::vector<uint8_t> is_mod;
   std::vector<int64_t> cap;
-  DevBuf packed, index, valid, w, capd, modd;
+  DevBuf packed, index, valid, w, capd, modd, pairs, pair_bucket;
+  int scan_blocks = 0;  // resident workgroups of k_explain_scan (depends on the LDS pair list size)
   TableArgs args{};
 };
 
@@ -91,8 +92,11 @@ struct sst_result {
   int64_t n = 0;
   int64_t cap_n = 0;
   DevBuf status, count, offset, payload, cursor, counters, lists, stats;
-  DevBuf wave_used, wave_stats, prefix, dense;
-  int n_waves = 0;
+  DevBuf wave_used, wave_stats, prefix, dense, work, work_count;
+  int n_waves = 0;  // expand waves
+  int n_regions = 0;  // scan + expand waves (arena regions)
+  int64_t n_scan_waves = 0;
+  uint64_t work_region = 0;
   uint64_t region_bytes = 0, spill_bytes = 0;
   bool compacted = false;
   uint64_t arena_bytes = 0;
@@ -183,7 +187,57 @@ int64_t table_cols(int64_t max_mass, int C) {
   return (int64_t)std::ceil((double)(max_mass + 1) / (double)C);  // mass_table.py:214
 }
 
-int finish_table(sst_table* t) {
+// LDS pair list of the scan kernel: every single row mass and every sum of two
+// row masses (rows >= 1), sorted by (sum, top row), with a bucket index.  Only
+// for tables this library built from exactly these masses: then a window value
+// below 3 * w_min is reachable iff it is such a sum, and the reference's DFS
+// lists its candidates in (v, top row) order (pair fast path).
+int build_pair_list(sst_table* t, bool self_built) {
+  sst_ctx* c = t->ctx;
+  t->args.pairs_enabled = 0;
+  t->args.pair_hi = (int64_t)3 * t->args.w_min;
+  // the literal-sweep rows (mass < C) are not a closure, and the last column
+  // is masked: keep the pair path to closures strictly below the last column
+  if (!self_built || t->args.pair_hi > (t->n_cols - 1) * t->C) return SST_OK;
+  for (int r = 1; r < t->n_rows; ++r)
+    if (t->masses[r] < t->C) return SST_OK;
+  struct E {
+    uint32_t sum, rows;
+  };
+  std::vector<E> e;
+  for (int r1 = 1; r1 < t->n_rows; ++r1) {
+    if (t->masses[r1] <= 0) return SST_OK;  // zero-mass rows: leave the general path in charge
+    e.push_back({(uint32_t)t->masses[r1], ((uint32_t)r1 << 8) | 0xFFu});
+    for (int r2 = 1; r2 <= r1; ++r2) {
+      int64_t s = t->masses[r1] + t->masses[r2];
+      if (s >= t->args.pair_hi || s >= t->M) continue;  // never inside a pair-class window
+      e.push_back({(uint32_t)s, ((uint32_t)r1 << 8) | (uint32_t)r2});
+    }
+  }
+  std::sort(e.begin(), e.end(), [](const E& x, const E& y) { return x.sum != y.sum ? x.sum < y.sum : x.rows < y.rows; });
+  const int64_t max_sum = e.empty() ? 0 : e.back().sum;
+  const int64_t n_b = (max_sum >> kPairBucketShift) + 1;
+  const size_t bytes = e.size() * 8 + (size_t)(n_b + 1) * 2;
+  if (e.empty() || bytes > (size_t)kMaxPairLds || e.size() > 65535) return SST_OK;
+  std::vector<uint16_t> bst(n_b + 1);
+  size_t k = 0;
+  for (int64_t b = 0; b <= n_b; ++b) {
+    while (k < e.size() && (int64_t)(e[k].sum >> kPairBucketShift) < b) ++k;
+    bst[b] = (uint16_t)k;
+  }
+  if (!t->pairs.ensure(e.size() * 8) || !t->pair_bucket.ensure((n_b + 1) * 2))
+    return fail(c, SST_E_NOMEM, "device allocation failed (pair list)");
+  HIP_OK(c, hipMemcpy(t->pairs.p, e.data(), e.size() * 8, hipMemcpyHostToDevice));
+  HIP_OK(c, hipMemcpy(t->pair_bucket.p, bst.data(), (n_b + 1) * 2, hipMemcpyHostToDevice));
+  t->args.pairs = (const uint2*)t->pairs.p;
+  t->args.pair_bucket = (const uint16_t*)t->pair_bucket.p;
+  t->args.n_pairs = (int)e.size();
+  t->args.n_buckets = (int)n_b;
+  t->args.pairs_enabled = 1;
+  return SST_OK;
+}
+
+int finish_table(sst_table* t, bool self_built) {
   sst_ctx* c = t->ctx;
   const int64_t M = t->M;
   if (!t->index.ensure((size_t)M * sizeof(ulonglong2)) || !t->valid.ensure((size_t)((M + 63) / 64) * 8))
@@ -218,6 +272,7 @@ int finish_table(sst_table* t) {
     if (t->masses[r] > 0 && (wmin == 0 || t->masses[r] < wmin)) wmin = (int)t->masses[r];
   t->args.w_min = wmin > 0 ? wmin : 1;
   t->args.shallow_hi = (int64_t)kShallowDepth * t->args.w_min;  // < 4 w_min: at most 3 items
+  if (int rc = build_pair_list(t, self_built)) return rc;
   // default budgets: no modification rows (callers set them)
   std::vector<uint8_t> mod(t->n_rows, 0);
   std::vector<int64_t> cap(t->n_rows, 0);
@@ -355,7 +410,7 @@ int sst_table_build(sst_ctx* c, const int64_t* masses, int n_rows, int64_t max_m
   R.release();
   tmp.release();
   wdev.release();
-  int rc = finish_table(t);
+  int rc = finish_table(t, true);
   if (rc) {
     delete t;
     return rc;
@@ -389,7 +444,7 @@ int sst_table_upload(sst_ctx* c, const int64_t* masses, int n_rows, const void* 
     delete t;
     return fail(c, SST_E_HIP, std::string("upload: ") + hipGetErrorString(e));
   }
-  int rc = finish_table(t);
+  int rc = finish_table(t, false);
   if (rc) {
     delete t;
     return rc;
@@ -466,7 +521,8 @@ void sst_table_destroy(sst_table* t) {
   std::lock_guard<std::recursive_mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&t->packed, &t->index, &t->valid, &t->w, &t->capd, &t->modd}) b->release();
+  for (DevBuf* b : {&t->packed, &t->index, &t->valid, &t->w, &t->capd, &t->modd, &t->pairs, &t->pair_bucket})
+    b->release();
   delete t;
 }
 
@@ -511,7 +567,7 @@ constexpr uint64_t kNodeBudget = 1ull << 32;
 
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->count, &r->offset, &r->payload, &r->cursor, &r->counters, &r->lists, &r->stats,
-                    &r->wave_used, &r->wave_stats, &r->prefix, &r->dense})
+                    &r->wave_used, &r->wave_stats, &r->prefix, &r->dense, &r->work, &r->work_count})
     b->release();
 }
 
@@ -523,13 +579,17 @@ OutArgs out_args(sst_result* r) {
   o.payload = (uint8_t*)r->payload.p;
   o.arena_bytes = r->arena_bytes;
   o.region_bytes = r->region_bytes;
-  o.spill_base = (uint64_t)r->n_waves * r->region_bytes;
+  o.spill_base = (uint64_t)r->n_regions * r->region_bytes;
   o.cursor = (uint64_t*)r->cursor.p;
   o.wave_used = (uint64_t*)r->wave_used.p;
   o.wave_stats = (unsigned long long*)r->wave_stats.p;
   o.counters = (uint32_t*)r->counters.p;
   o.lists = (uint32_t*)r->lists.p;
   o.stats = (unsigned long long*)r->stats.p;
+  o.work = (uint4*)r->work.p;
+  o.work_count = (uint32_t*)r->work_count.p;
+  o.work_region = r->work_region;
+  o.n_scan_waves = r->n_scan_waves;
   return o;
 }
 
@@ -554,7 +614,7 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
                  int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count) {
   sst_ctx* c = t->ctx;
   const int64_t n = r->n;
-  r->arena_bytes = (uint64_t)r->n_waves * r->region_bytes + r->spill_bytes;
+  r->arena_bytes = (uint64_t)r->n_regions * r->region_bytes + r->spill_bytes;
   if (!r->cursor.ensure(8) || !r->counters.ensure(kNumClasses * 4) || !r->stats.ensure(kNumStats * 8) ||
       !r->lists.ensure((size_t)kNumClasses * std::max<int64_t>(n, 1) * 4) || !r->payload.ensure(r->arena_bytes))
     return fail(c, SST_E_NOMEM, "device allocation failed (result)");
@@ -570,7 +630,11 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   OutArgs o = out_args(r);
   {
     Prof p(c, SST_K_EXPLAIN_MAIN);
-    HIP_OK(c, launch_explain_main(t->args, q, o, r->n_waves / (kWG / 64), c->stream));
+    HIP_OK(c, launch_explain_scan(t->args, q, o, (int)(r->n_scan_waves / (kScanWG / 64)), c->stream));
+  }
+  {
+    Prof p(c, SST_K_EXPLAIN_EXPAND);
+    HIP_OK(c, launch_explain_expand(t->args, q, o, r->n_waves / (kWG / 64), c->stream));
   }
   {
     Prof p(c, SST_K_EXPLAIN_DEEP);
@@ -591,21 +655,31 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
 
 int alloc_result(sst_table* t, int64_t n, sst_result** out) {
   sst_ctx* c = t->ctx;
-  if (c->main_blocks == 0) c->main_blocks = c->n_cu * explain_main_blocks_per_cu();
+  if (t->scan_blocks == 0) t->scan_blocks = c->n_cu * explain_scan_blocks_per_cu(scan_dyn_lds(t->args));
+  if (c->expand_blocks == 0) c->expand_blocks = c->n_cu * explain_expand_blocks_per_cu();
   sst_result* r = new sst_result();
   r->ctx = c;
   r->n = n;
   r->cap_n = n;
   size_t nn = (size_t)std::max<int64_t>(n, 1);
-  // one arena region per main-kernel wave sized for ~16 B of payload per
-  // query, plus a spill area for overflowing regions and deferred queries
-  r->n_waves = c->main_blocks * (kWG / 64);
-  uint64_t per_wave = (nn + r->n_waves - 1) / r->n_waves;
+  // worklist: one region per scan wave, big enough for all its tiles
+  r->n_scan_waves = (int64_t)t->scan_blocks * (kScanWG / 64);
+  int64_t tiles = ((int64_t)nn + 63) / 64;
+  r->work_region = (uint64_t)((tiles + r->n_scan_waves - 1) / r->n_scan_waves) * 64;
+  // one arena region per scan wave and per expand wave, each sized for ~16 B
+  // of payload per query of a scan wave, then a spill area for overflowing
+  // regions and deferred queries
+  r->n_waves = c->expand_blocks * (kWG / 64);
+  r->n_regions = (int)r->n_scan_waves + r->n_waves;
+  uint64_t per_wave = (nn + r->n_scan_waves - 1) / r->n_scan_waves;
   r->region_bytes = std::max<uint64_t>(256, (16 * per_wave + 15) / 16 * 16);
   r->spill_bytes = std::max<uint64_t>(1u << 20, 2 * (uint64_t)nn);
   if (!r->status.ensure(nn) || !r->count.ensure(nn * 8) || !r->offset.ensure(nn * 8) ||
-      !r->wave_used.ensure((size_t)r->n_waves * 8) || !r->wave_stats.ensure((size_t)r->n_waves * kNumStats * 8) ||
-      !r->prefix.ensure((size_t)(r->n_waves + 2) * 8)) {
+      !r->wave_used.ensure((size_t)r->n_regions * 8) ||
+      !r->wave_stats.ensure((size_t)r->n_regions * kNumStats * 8) ||
+      !r->prefix.ensure((size_t)(r->n_regions + 2) * 8) ||
+      !r->work.ensure((size_t)r->n_scan_waves * r->work_region * 16) ||
+      !r->work_count.ensure((size_t)r->n_scan_waves * 4)) {
     free_result_bufs(r);
     delete r;
     return fail(c, SST_E_NOMEM, "device allocation failed (result)");
@@ -621,7 +695,7 @@ int compact(sst_result* r) {
   if (r->compacted) return SST_OK;
   if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, 1)))
     return fail(c, SST_E_NOMEM, "device allocation failed (compaction)");
-  HIP_OK(c, launch_compact(out_args(r), r->n, r->n_waves, (uint64_t*)r->prefix.p, (uint8_t*)r->dense.p, c->stream));
+  HIP_OK(c, launch_compact(out_args(r), r->n, r->n_regions, (uint64_t*)r->prefix.p, (uint8_t*)r->dense.p, c->stream));
   r->compacted = true;
   return SST_OK;
 }
@@ -634,17 +708,17 @@ int fetch(sst_result* r) {
   r->h_count.resize(n);
   r->h_offset.resize(n);
   uint64_t pre_tail[2] = {0, 0};
-  std::vector<unsigned long long> ws((size_t)r->n_waves * kNumStats);
+  std::vector<unsigned long long> ws((size_t)r->n_regions * kNumStats);
   if (n) {
     HIP_OK(c, hipMemcpyAsync(r->h_status.data(), r->status.p, n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipMemcpyAsync(r->h_count.data(), r->count.p, n * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipMemcpyAsync(r->h_offset.data(), r->offset.p, n * 8, hipMemcpyDeviceToHost, c->stream));
   }
-  HIP_OK(c, hipMemcpyAsync(pre_tail, (uint64_t*)r->prefix.p + r->n_waves, 16, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipMemcpyAsync(pre_tail, (uint64_t*)r->prefix.p + r->n_regions, 16, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipMemcpyAsync(r->h_stats, r->stats.p, kNumStats * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipMemcpyAsync(ws.data(), r->wave_stats.p, ws.size() * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
-  for (int w = 0; w < r->n_waves; ++w)
+  for (int w = 0; w < r->n_regions; ++w)
     for (int k = 0; k < kNumStats; ++k) r->h_stats[k] += ws[(size_t)w * kNumStats + k];
   r->payload_bytes = std::min<uint64_t>(pre_tail[1], r->arena_bytes);
   r->h_payload.resize(r->payload_bytes);

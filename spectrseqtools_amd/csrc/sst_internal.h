@@ -13,6 +13,9 @@ constexpr int kWG = 256;           // workgroup of the lane-per-query kernels (4
 constexpr int kShallowDepth = 4;   // register-stack depth of the main kernel
 constexpr int kMaxDepth = 96;      // >= max items of any multiset in a table (73 for the full alphabet)
 constexpr int kInfBudget = 1 << 30;  // np.inf budget (decremented at most kMaxDepth times)
+constexpr int kScanWG = 1024;        // scan kernel workgroup (2 per CU share the LDS pair list)
+constexpr int kPairBucketShift = 8;  // 256 masses per bucket of the pair index
+constexpr int kMaxPairLds = 96 * 1024;  // pair list + buckets must fit this many LDS bytes
 
 enum { kClassShallow = 0, kClassDeep = 1, kClassExact = 2, kClassNomemo = 3, kNumClasses = 4 };
 // internal statuses (never returned to callers)
@@ -41,6 +44,17 @@ struct TableArgs {
   uint64_t capz0, capz1;    // row masks with cap <= 0
   int64_t fast_limit_B;     // max window value for which no per-row cap can bind
   int64_t shallow_hi;       // window values < shallow_hi (= 4 * w_min) fit in <= 3 items
+  // LDS pair list: every 1- and 2-item sum of the alphabet, sorted by
+  // (sum, top row); entries {sum, top_row << 8 | low_row (0xFF: single)}.
+  // Valid only for tables known to follow the reference recurrence over
+  // exactly these masses (built here); window values < pair_hi (= 3 * w_min)
+  // have no candidate with more than 2 items.
+  const uint2* pairs;
+  const uint16_t* pair_bucket;  // [n_buckets + 1] first entry with sum >= k << kPairBucketShift
+  int64_t pair_hi;
+  int n_pairs;
+  int n_buckets;
+  int pairs_enabled;
   int n_rows;
   int any_mod;
   int w_min;                // smallest positive row mass
@@ -74,8 +88,12 @@ struct OutArgs {
   uint64_t region_bytes;      // per-wave region of the main kernel
   uint64_t spill_base;        // = n_waves * region_bytes
   uint64_t* cursor;           // spill bytes taken
-  uint64_t* wave_used;        // [n_waves] bytes used in each region
-  unsigned long long* wave_stats;  // [n_waves][kNumStats] main-kernel counters
+  uint64_t* wave_used;        // [n_waves] bytes used in each region (expand kernel waves)
+  unsigned long long* wave_stats;  // [n_waves][kNumStats] expand-kernel counters
+  uint4* work;                // [n_scan_waves][work_region] queued SHALLOW {query, a, b, has_zero}
+  uint32_t* work_count;       // [n_scan_waves]
+  uint64_t work_region;
+  int64_t n_scan_waves;
   uint32_t* counters;  // [kNumClasses]
   uint32_t* lists;     // [kNumClasses][n]
   unsigned long long* stats;  // [kNumStats] deferred-kernel counters
@@ -100,8 +118,13 @@ hipError_t launch_index(int C, const void* packed, int n_rows, int64_t ncols, in
                         uint64_t* valid, int* err, hipStream_t st);
 hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, const double* mass, const double* thr, int64_t n,
                            double tol, double prec, int8_t* out, hipStream_t st);
-hipError_t launch_explain_main(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks, hipStream_t st);
-int explain_main_blocks_per_cu();
+hipError_t launch_explain_scan(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
+                               hipStream_t st);
+hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
+                                 hipStream_t st);
+int explain_scan_blocks_per_cu(size_t dyn_lds);
+int explain_expand_blocks_per_cu();
+size_t scan_dyn_lds(const TableArgs& t);
 hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* wave_prefix, uint8_t* dst,
                           hipStream_t st);
 hipError_t launch_explain_deep(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int cls, void* ws,

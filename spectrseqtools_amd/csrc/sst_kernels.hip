@@ -613,8 +613,19 @@ __device__ __forceinline__ void shallow_window(const TableArgs& t, const Lds& s,
   if (a > b) return;
   const M128 top_mask = rows_upto(t.n_rows - 1);
   const int64_t wa = a >> 6, wb = b >> 6;
+  const int64_t nw = wb - wa + 1;
+  // the first 6 bitset words are loaded together (one round trip) and then
+  // rotated through x0 so that no private array is indexed dynamically
+  uint64_t x0 = t.valid[wa];
+  uint64_t x1 = nw > 1 ? t.valid[wa + 1] : 0, x2 = nw > 2 ? t.valid[wa + 2] : 0;
+  uint64_t x3 = nw > 3 ? t.valid[wa + 3] : 0, x4 = nw > 4 ? t.valid[wa + 4] : 0, x5 = nw > 5 ? t.valid[wa + 5] : 0;
   for (int64_t wi = wa; wi <= wb; ++wi) {
-    uint64_t x = t.valid[wi];
+    uint64_t x = wi - wa < 6 ? x0 : t.valid[wi];
+    x0 = x1;
+    x1 = x2;
+    x2 = x3;
+    x3 = x4;
+    x4 = x5;
     if (wi == wa) x &= ~0ull << (a & 63);
     if (wi == wb) x &= ~0ull >> (63 - (b & 63));
     while (x) {
@@ -817,33 +828,138 @@ __device__ __forceinline__ void wg_stat(unsigned long long* stats, int k, uint64
 }
 
 // ---------------------------------------------------------------------------
-// main explain kernel (persistent grid, independent waves): every wave takes
-// 64-query tiles in a grid stride, plans each query, resolves the trivial
-// ones, runs SHALLOW fast-path queries with all DFS state and the first 16
-// payload bytes in VGPRs, and queues the rest.  Payload goes to the wave's own
-// arena region through a bump pointer fed by a wavefront prefix sum: no
-// barriers and no atomics inside the loop (a full region spills, one atomic
-// per tile).  Counters go to per-wave slots.
+// Explain, part 1 -- k_explain_scan (persistent grid, independent waves):
+// every wave streams 64-query tiles in a grid stride: quantises the window,
+// reads its valid-bitset words with independent loads, resolves every query
+// without a reachable window value (the large majority), and appends the
+// SHALLOW rest to the wave's own worklist region (ballot + mbcnt: no atomics).
+// Budget-binding / deep / no-memo queries go to the class lists.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWG) void k_explain_main(TableArgs t, QueryArgs q, OutArgs out) {
-  __shared__ Lds s;
-  stage_rows(s, t);
+__device__ __forceinline__ uint64_t lane_mask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+
+// any reachable value in [a, b]: up to 6 bitset words loaded at once
+__device__ __forceinline__ bool window_has_roots(const uint64_t* valid, int64_t a, int64_t b) {
+  const int64_t wa = a >> 6, wb = b >> 6;
+  const int64_t nw = wb - wa + 1;
+  const uint64_t fm = ~0ull << (a & 63), lm = ~0ull >> (63 - (b & 63));
+  if (nw <= 6) {
+    uint64_t x0 = valid[wa];
+    uint64_t x1 = nw > 1 ? valid[wa + 1] : 0, x2 = nw > 2 ? valid[wa + 2] : 0;
+    uint64_t x3 = nw > 3 ? valid[wa + 3] : 0, x4 = nw > 4 ? valid[wa + 4] : 0, x5 = nw > 5 ? valid[wa + 5] : 0;
+    x0 &= fm;
+    if (nw == 1) x0 &= lm;
+    if (nw == 2) x1 &= lm;
+    if (nw == 3) x2 &= lm;
+    if (nw == 4) x3 &= lm;
+    if (nw == 5) x4 &= lm;
+    if (nw == 6) x5 &= lm;
+    return (x0 | x1 | x2 | x3 | x4 | x5) != 0;
+  }
+  return any_bits(valid, a, b);
+}
+
+// <= 2-item candidates of the window [a, b] from the LDS pair list, in the
+// reference's order (ascending v, then ascending top row).
+template <typename Sink>
+__device__ __forceinline__ void pair_window(const uint2* ent, const uint16_t* bst, int n_ent, int n_b, int64_t a,
+                                            int64_t b, Sink& sink, EnumOut& o) {
+  const int64_t ba = a >> kPairBucketShift;
+  if (ba >= n_b) return;
+  for (int k = bst[ba]; k < n_ent; ++k) {
+    const uint2 e = ent[k];
+    if ((int64_t)e.x < a) continue;
+    if ((int64_t)e.x > b) break;
+    const int lo_row = (int)(e.y & 0xFFu), top = (int)(e.y >> 8);
+    if (lo_row == 0xFF) {
+      sink.put(o.bytes, 1, top, 0, 0);
+      o.bytes += 2;
+    } else {
+      sink.put(o.bytes, 2, lo_row, top, 0);
+      o.bytes += 3;
+    }
+    o.count++;
+  }
+}
+
+// Shared tail of the scan / expand tiles: wavefront prefix sum of the payload
+// bytes, bump allocation in the wave's own region (spill when full), payload
+// write from registers (or a re-run straight into the arena).
+struct TileOut {
+  uint64_t off;
+  uint64_t bytes;
+  int8_t status;
+};
+__device__ __forceinline__ TileOut tile_alloc(const OutArgs& out, int lane, uint64_t region0, uint64_t& used,
+                                              uint64_t bytes, int8_t status) {
+  const uint64_t incl = wave_incl_scan(bytes);
+  const uint64_t total = __shfl(incl, 63, 64);
+  uint64_t base = 0;
+  if (total) {
+    if (used + total <= out.region_bytes) {
+      base = region0 + used;
+      used += total;
+    } else {
+      unsigned long long sb = 0;
+      if (lane == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
+      base = out.spill_base + __shfl(sb, 0, 64);
+    }
+  }
+  TileOut r{base + incl - bytes, bytes, status};
+  if (bytes && r.off + bytes > out.arena_bytes) {
+    r.status = (int8_t)kStatusArenaRetry;
+    r.bytes = 0;
+  }
+  return r;
+}
+
+__device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t region, int lane, uint64_t used,
+                                                 uint64_t n_q, uint64_t nodes, uint64_t payload) {
+  for (int o = 32; o > 0; o >>= 1) {
+    n_q += __shfl_down(n_q, o, 64);
+    nodes += __shfl_down(nodes, o, 64);
+    payload += __shfl_down(payload, o, 64);
+  }
+  if (lane == 0) {
+    out.wave_used[region] = used;
+    unsigned long long* ws = out.wave_stats + region * kNumStats;
+    for (int k = 0; k < kNumStats; ++k) ws[k] = 0;
+    ws[kStatShallow] = n_q;
+    ws[kStatNodes] = nodes;
+    ws[kStatPayload] = payload;
+  }
+}
+
+// 8 waves/SIMD (two 1024-lane workgroups per CU sharing the LDS pair list);
+// the compiler moves the surplus kernel-argument SGPRs into VGPR lanes.
+__global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
+  extern __shared__ uint2 lds_pairs[];
+  const uint16_t* lds_bucket = (const uint16_t*)(lds_pairs + t.n_pairs);
+  if (t.pairs_enabled) {
+    for (int k = threadIdx.x; k < t.n_pairs; k += blockDim.x) lds_pairs[k] = t.pairs[k];
+    uint16_t* bw = (uint16_t*)(lds_pairs + t.n_pairs);
+    for (int k = threadIdx.x; k <= t.n_buckets; k += blockDim.x) bw[k] = t.pair_bucket[k];
+    __syncthreads();
+  }
   const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
-  const int64_t n_waves = (int64_t)gridDim.x * (kWG / 64);
-  const uint64_t region0 = (uint64_t)wave * out.region_bytes;
-  uint64_t used = 0;  // wave-uniform bump pointer
-  uint64_t st_shallow = 0, st_nodes = 0, st_payload = 0;
+  const int64_t wave = (int64_t)blockIdx.x * (kScanWG / 64) + (threadIdx.x >> 6);
+  const int64_t n_waves = (int64_t)gridDim.x * (kScanWG / 64);
+  const uint64_t region0 = (uint64_t)wave * out.region_bytes;  // scan waves own regions [0, n_scan_waves)
+  uint64_t used = 0;                                           // wave-uniform bump pointer
+  uint64_t st_q = 0, st_payload = 0;
+  uint4* wl = out.work + (uint64_t)wave * out.work_region;
+  uint32_t n_work = 0;  // wave-uniform
   const int64_t ntiles = (q.n + 63) / 64;
   for (int64_t tile = wave; tile < ntiles; tile += n_waves) {
     const int64_t i = tile * 64 + lane;
     const bool live = i < q.n;
+    bool work = false, pair = false;
+    uint4 item = make_uint4(0, 0, 0, 0);
     int8_t status = SST_NONE;
-    uint64_t cnt = 0, bytes = 0;
-    bool shallow = false;
-    int64_t a = 0, b = -1;
+    int64_t a = 0, hi = -1;
+    CountSink3 sink;  // counting pass; the payload is written by a second LDS pass
+    EnumOut eo{0, 0, 0, 0};
     if (live) {
-      int64_t lo, hi;
+      int64_t lo;
       quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, lo, hi);
       const int A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
       if (hi < lo) {
@@ -853,83 +969,119 @@ __global__ __launch_bounds__(kWG) void k_explain_main(TableArgs t, QueryArgs q, 
       } else {
         status = (lo <= 0 && hi >= 0) ? SST_EMPTY : SST_NONE;  // v == 0 -> [[]] (:130-131)
         a = lo < 1 ? 1 : lo;
-        b = hi;
-        int cls;
-        if (budgets_never_bind(t, hi, A0)) cls = hi < t.shallow_hi ? kClassShallow : kClassDeep;
-        else cls = q.with_memo ? kClassExact : kClassNomemo;
-        if (cls == kClassShallow) {
-          shallow = a <= b;
-        } else if (a <= b && any_bits(t.valid, a, b)) {
-          uint32_t slot = atomicAdd(&out.counters[cls], 1u);
-          out.lists[(int64_t)cls * q.n + slot] = (uint32_t)i;
-          status = (int8_t)kStatusPending;
+        if (a <= hi) {
+          const bool never = budgets_never_bind(t, hi, A0);
+          if (never && t.pairs_enabled && hi < t.pair_hi) {
+            pair = true;
+            pair_window(lds_pairs, lds_bucket, t.n_pairs, t.n_buckets, a, hi, sink, eo);
+            if (eo.count) status = eo.count > q.cap_count ? SST_OVERFLOW : SST_SOME;
+            st_q++;
+          } else if (window_has_roots(t.valid, a, hi)) {
+            int cls;
+            if (never) cls = hi < t.shallow_hi ? kClassShallow : kClassDeep;
+            else cls = q.with_memo ? kClassExact : kClassNomemo;
+            if (cls == kClassShallow) {
+              work = true;  // the expand kernel writes status, count and offset
+              item = make_uint4((uint32_t)i, (uint32_t)a, (uint32_t)hi, status == SST_EMPTY ? 1u : 0u);
+            } else {
+              uint32_t slot = atomicAdd(&out.counters[cls], 1u);
+              out.lists[(int64_t)cls * q.n + slot] = (uint32_t)i;
+            }
+            status = (int8_t)kStatusPending;
+          }
         }
       }
     }
-    RegSink sink;
-    EnumOut eo{0, 0, 0, 0};
-    if (shallow) {
-      shallow_window(t, s, a, b, sink, eo);
-      cnt = eo.count;
-      if (cnt > 0) status = SST_SOME;
-      bytes = cnt > q.cap_count ? 0 : eo.bytes;
-      if (cnt > q.cap_count) status = SST_OVERFLOW;
-      st_shallow++;
-      st_nodes += eo.nodes;
+    const uint64_t want = status == SST_SOME ? eo.bytes : 0;
+    const TileOut to = tile_alloc(out, lane, region0, used, want, status);
+    if (to.bytes) {
+      MemSink3 ms{out.payload + to.off};
+      EnumOut e2{0, 0, 0, 0};
+      pair_window(lds_pairs, lds_bucket, t.n_pairs, t.n_buckets, a, hi, ms, e2);
     }
-    const uint64_t incl = wave_incl_scan(bytes);
-    const uint64_t total = __shfl(incl, 63, 64);
-    uint64_t base = 0;
-    if (total) {
-      if (used + total <= out.region_bytes) {
-        base = region0 + used;
-        used += total;
-      } else {
-        unsigned long long sb = 0;
-        if (lane == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
-        base = out.spill_base + __shfl(sb, 0, 64);
+    // NONE / EMPTY / OUT_OF_TABLE carry no candidates: count and offset stay
+    // undefined (include/sst.h), one byte per resolved query
+    if (live && !work) {
+      out.status[i] = to.status;
+      if (pair && (to.status == SST_SOME || to.status == SST_OVERFLOW)) {
+        out.count[i] = eo.count;
+        out.offset[i] = to.bytes ? to.off : 0;
       }
     }
-    const uint64_t off = base + incl - bytes;
-    if (bytes && off + bytes > out.arena_bytes) {
-      status = (int8_t)kStatusArenaRetry;
-      bytes = 0;
-    }
-    if (bytes) {
-      if (!sink.over) {
-        sink.flush(out.payload + off, bytes);
-      } else {  // more than 16 bytes: enumerate again straight into the arena
-        MemSink3 ms{out.payload + off};
-        EnumOut e2{0, 0, 0, 0};
-        shallow_window(t, s, a, b, ms, e2);
+    st_payload += to.bytes;
+    const uint64_t bal = __ballot(work);
+    if (work) wl[n_work + __builtin_popcountll(bal & lane_mask_lt(lane))] = item;
+    n_work += (uint32_t)__builtin_popcountll(bal);
+  }
+  if (lane == 0) out.work_count[wave] = n_work;
+  wave_stats_flush(out, wave, lane, used, st_q, 0, st_payload);
+}
+
+// ---------------------------------------------------------------------------
+// Explain, part 2 -- k_explain_expand: the SHALLOW fast path for the queued
+// queries (all DFS state and the first 16 payload bytes in VGPRs).  Each wave
+// takes scan-wave worklist regions in a grid stride, 64 queries at a time;
+// payload goes to the wave's own arena region through a bump pointer fed by a
+// wavefront prefix sum (a full region spills: one atomic per tile).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kWG) void k_explain_expand(TableArgs t, QueryArgs q, OutArgs out) {
+  __shared__ Lds s;
+  stage_rows(s, t);
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
+  const int64_t n_waves = (int64_t)gridDim.x * (kWG / 64);
+  const int64_t region = out.n_scan_waves + wave;  // expand regions follow the scan regions
+  const uint64_t region0 = (uint64_t)region * out.region_bytes;
+  uint64_t used = 0;  // wave-uniform bump pointer
+  uint64_t st_q = 0, st_nodes = 0, st_payload = 0;
+  for (int64_t src = wave; src < out.n_scan_waves; src += n_waves) {
+    const uint32_t nw = out.work_count[src];
+    const uint4* wl = out.work + (uint64_t)src * out.work_region;
+    for (uint32_t k0 = 0; k0 < nw; k0 += 64) {
+      const bool live = k0 + lane < nw;
+      int64_t i = 0, a = 0, b = -1;
+      int8_t status = SST_NONE;
+      RegSink sink;
+      EnumOut eo{0, 0, 0, 0};
+      if (live) {
+        const uint4 item = wl[k0 + lane];  // {query, first window value >= 1, last, v == 0 in window}
+        i = item.x;
+        a = item.y;
+        b = item.z;
+        shallow_window(t, s, a, b, sink, eo);
+        status = eo.count ? (eo.count > q.cap_count ? SST_OVERFLOW : SST_SOME) : (item.w ? SST_EMPTY : SST_NONE);
+        st_q++;
+        st_nodes += eo.nodes;
       }
+      const TileOut to = tile_alloc(out, lane, region0, used, status == SST_SOME ? eo.bytes : 0, status);
+      if (to.bytes) {
+        if (!sink.over) {
+          sink.flush(out.payload + to.off, to.bytes);
+        } else {  // more than 16 bytes: enumerate again straight into the arena
+          MemSink3 ms{out.payload + to.off};
+          EnumOut e2{0, 0, 0, 0};
+          shallow_window(t, s, a, b, ms, e2);
+        }
+      }
+      if (live) {
+        out.status[i] = to.status;
+        out.count[i] = eo.count;
+        out.offset[i] = to.bytes ? to.off : 0;
+      }
+      st_payload += to.bytes;
     }
-    if (live) {
-      out.status[i] = status;
-      out.count[i] = cnt;
-      out.offset[i] = bytes ? off : 0;
-    }
-    st_payload += bytes;
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    st_shallow += __shfl_down(st_shallow, o, 64);
-    st_nodes += __shfl_down(st_nodes, o, 64);
-    st_payload += __shfl_down(st_payload, o, 64);
-  }
-  if (lane == 0) {
-    out.wave_used[wave] = used;
-    unsigned long long* ws = out.wave_stats + wave * kNumStats;
-    for (int k = 0; k < kNumStats; ++k) ws[k] = 0;
-    ws[kStatShallow] = st_shallow;
-    ws[kStatNodes] = st_nodes;
-    ws[kStatPayload] = st_payload;
-  }
+  wave_stats_flush(out, region, lane, used, st_q, st_nodes, st_payload);
 }
 
 // Compaction of the arena into a dense payload (result fetch / gather only):
 // exclusive prefix over the per-wave regions, block copies, offset rewrite.
+// The spill cursor keeps counting past the arena when a query does not fit
+// (those queries report an arena retry): every length is clamped to what the
+// arena actually holds.
 __global__ __launch_bounds__(1024) void k_wave_prefix(const uint64_t* __restrict__ used, int n_waves,
-                                                      const uint64_t* __restrict__ cursor, uint64_t* __restrict__ pre) {
+                                                      const uint64_t* __restrict__ cursor, uint64_t spill_cap,
+                                                      uint64_t* __restrict__ pre) {
   __shared__ uint64_t part[1024];
   const int per = (n_waves + 1023) / 1024;
   const int b0 = threadIdx.x * per;
@@ -952,22 +1104,24 @@ __global__ __launch_bounds__(1024) void k_wave_prefix(const uint64_t* __restrict
     }
   if (threadIdx.x == 1023) {
     pre[n_waves] = part[1023];             // bytes of all regions
-    pre[n_waves + 1] = part[1023] + *cursor;  // + spill bytes = dense payload size
+    const uint64_t sp = *cursor < spill_cap ? *cursor : spill_cap;
+    pre[n_waves + 1] = part[1023] + sp;  // + spill bytes = dense payload size
   }
 }
 
 __global__ __launch_bounds__(256) void k_compact_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                       const uint64_t* __restrict__ used,
                                                       const uint64_t* __restrict__ pre, int n_waves, uint64_t region,
-                                                      uint64_t spill_base, const uint64_t* __restrict__ cursor) {
+                                                      uint64_t spill_base, const uint64_t* __restrict__ cursor,
+                                                      uint64_t spill_cap) {
   for (int w = blockIdx.x; w <= n_waves; w += gridDim.x) {
     uint64_t len, from, to;
     if (w < n_waves) {
-      len = used[w];
+      len = used[w] < region ? used[w] : region;
       from = (uint64_t)w * region;
       to = pre[w];
     } else {
-      len = *cursor;
+      len = *cursor < spill_cap ? *cursor : spill_cap;
       from = spill_base;
       to = pre[n_waves];
     }
@@ -1172,23 +1326,37 @@ hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, const double* m
                      out);
   return hipGetLastError();
 }
-hipError_t launch_explain_main(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks, hipStream_t st) {
+size_t scan_dyn_lds(const TableArgs& t) {
+  if (!t.pairs_enabled) return 0;
+  return ((size_t)t.n_pairs * sizeof(uint2) + (size_t)(t.n_buckets + 1) * sizeof(uint16_t) + 15) / 16 * 16;
+}
+hipError_t launch_explain_scan(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
+                               hipStream_t st) {
   if (q.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_explain_main, dim3(n_blocks), dim3(kWG), 0, st, t, q, o);
+  hipLaunchKernelGGL(k_explain_scan, dim3(n_blocks), dim3(kScanWG), scan_dyn_lds(t), st, t, q, o);
   return hipGetLastError();
 }
-int explain_main_blocks_per_cu() {
+hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
+                                 hipStream_t st) {
+  if (q.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_explain_expand, dim3(n_blocks), dim3(kWG), 0, st, t, q, o);
+  return hipGetLastError();
+}
+static int occupancy(const void* k, int threads, size_t dyn) {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_explain_main, kWG, 0) != hipSuccess) {
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, threads, dyn) != hipSuccess) {
     (void)hipGetLastError();
-    return 4;
+    return 1;
   }
   return nb > 0 ? nb : 1;
 }
+int explain_scan_blocks_per_cu(size_t dyn) { return occupancy((const void*)k_explain_scan, kScanWG, dyn); }
+int explain_expand_blocks_per_cu() { return occupancy((const void*)k_explain_expand, kWG, 0); }
 hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* pre, uint8_t* dst, hipStream_t st) {
-  hipLaunchKernelGGL(k_wave_prefix, dim3(1), dim3(1024), 0, st, o.wave_used, n_waves, o.cursor, pre);
+  const uint64_t spill_cap = o.arena_bytes > o.spill_base ? o.arena_bytes - o.spill_base : 0;
+  hipLaunchKernelGGL(k_wave_prefix, dim3(1), dim3(1024), 0, st, o.wave_used, n_waves, o.cursor, spill_cap, pre);
   hipLaunchKernelGGL(k_compact_copy, dim3(2048), dim3(256), 0, st, o.payload, dst, o.wave_used, pre, n_waves,
-                     o.region_bytes, o.spill_base, o.cursor);
+                     o.region_bytes, o.spill_base, o.cursor, spill_cap);
   if (n > 0)
     hipLaunchKernelGGL(k_compact_offsets, dim3(blocks_for(n, 256)), dim3(256), 0, st, o.status, o.count, o.offset, n,
                        pre, n_waves, o.region_bytes, o.spill_base);
