@@ -134,9 +134,11 @@ int sst_result_fetch(sst_result* r);
 void sst_result_free(sst_result* r);
 
 /* Counters of the last explain launch (valid after a fetch), for measurement:
- * [0] queries run by the shallow fast path, [1] deep fast path, [2] exact
- * (budget-binding) path, [3] no-memo path, [4] index records loaded (node
- * expansions of the counting pass). */
+ * [0] queries run by the shallow (<= 3 item) fast path, [1] deep fast path,
+ * [2] exact (budget-binding) path, [3] no-memo path, [4] index records loaded
+ * (node expansions of the counting pass), [5] payload bytes written by those
+ * paths, [6] queries answered from the on-chip pair list (<= 2 item windows),
+ * [7] payload bytes written by the pair-list path. */
 int sst_result_stats(const sst_result* r, uint64_t* stats_out /* [8] */);
 
 /* ---- measurement ------------------------------------------------------ */

@@ -215,16 +215,20 @@ int build_pair_list(sst_table* t, bool self_built) {
     }
   }
   std::sort(e.begin(), e.end(), [](const E& x, const E& y) { return x.sum != y.sum ? x.sum < y.sum : x.rows < y.rows; });
-  const int64_t max_sum = e.empty() ? 0 : e.back().sum;
-  const int64_t n_b = (max_sum >> kPairBucketShift) + 1;
-  const size_t bytes = e.size() * 8 + (size_t)(n_b + 1) * 2;
-  if (e.empty() || bytes > (size_t)kMaxPairLds || e.size() > 65535) return SST_OK;
+  if (e.empty() || e.size() > 65535) return SST_OK;
+  // finest buckets (fewest entries skipped per lookup) that still fit the LDS budget
+  const int64_t max_sum = e.back().sum;
+  int shift = 4;
+  while (shift < 16 && e.size() * 8 + (size_t)((max_sum >> shift) + 2) * 2 > (size_t)kMaxPairLds) ++shift;
+  const int64_t n_b = (max_sum >> shift) + 1;
+  if (e.size() * 8 + (size_t)(n_b + 1) * 2 > (size_t)kMaxPairLds) return SST_OK;
   std::vector<uint16_t> bst(n_b + 1);
   size_t k = 0;
   for (int64_t b = 0; b <= n_b; ++b) {
-    while (k < e.size() && (int64_t)(e[k].sum >> kPairBucketShift) < b) ++k;
+    while (k < e.size() && (int64_t)(e[k].sum >> shift) < b) ++k;
     bst[b] = (uint16_t)k;
   }
+  t->args.pair_shift = shift;
   if (!t->pairs.ensure(e.size() * 8) || !t->pair_bucket.ensure((n_b + 1) * 2))
     return fail(c, SST_E_NOMEM, "device allocation failed (pair list)");
   HIP_OK(c, hipMemcpy(t->pairs.p, e.data(), e.size() * 8, hipMemcpyHostToDevice));

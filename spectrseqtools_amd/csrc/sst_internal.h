@@ -14,8 +14,11 @@ constexpr int kShallowDepth = 4;   // register-stack depth of the main kernel
 constexpr int kMaxDepth = 96;      // >= max items of any multiset in a table (73 for the full alphabet)
 constexpr int kInfBudget = 1 << 30;  // np.inf budget (decremented at most kMaxDepth times)
 constexpr int kScanWG = 1024;        // scan kernel workgroup (2 per CU share the LDS pair list)
-constexpr int kPairBucketShift = 8;  // 256 masses per bucket of the pair index
-constexpr int kMaxPairLds = 96 * 1024;  // pair list + buckets must fit this many LDS bytes
+constexpr int kMaxPairLds = 78 * 1024;  // pair list + buckets: two scan workgroups per CU (160 KB LDS)
+// worklist item flags ({query, a, b, flags}): v == 0 lies in the window; the
+// window was not classified by the scan (the expand kernel checks the bitset
+// and routes it); budgets cannot bind (fast-path theorem)
+constexpr uint32_t kItemZero = 1u, kItemUnclassified = 2u, kItemNever = 4u;
 
 enum { kClassShallow = 0, kClassDeep = 1, kClassExact = 2, kClassNomemo = 3, kNumClasses = 4 };
 // internal statuses (never returned to callers)
@@ -30,6 +33,8 @@ enum {
   kStatNomemo = 3,
   kStatNodes = 4,
   kStatPayload = 5,
+  kStatPair = 6,         // queries answered from the LDS pair list
+  kStatPairPayload = 7,  // payload bytes of those
   kNumStats = 8
 };
 
@@ -50,10 +55,11 @@ struct TableArgs {
   // exactly these masses (built here); window values < pair_hi (= 3 * w_min)
   // have no candidate with more than 2 items.
   const uint2* pairs;
-  const uint16_t* pair_bucket;  // [n_buckets + 1] first entry with sum >= k << kPairBucketShift
+  const uint16_t* pair_bucket;  // [n_buckets + 1] first entry with sum >= k << pair_shift
   int64_t pair_hi;
   int n_pairs;
   int n_buckets;
+  int pair_shift;
   int pairs_enabled;
   int n_rows;
   int any_mod;

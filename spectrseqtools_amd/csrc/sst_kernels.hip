@@ -859,26 +859,55 @@ __device__ __forceinline__ bool window_has_roots(const uint64_t* valid, int64_t 
 }
 
 // <= 2-item candidates of the window [a, b] from the LDS pair list, in the
-// reference's order (ascending v, then ascending top row).
-template <typename Sink>
-__device__ __forceinline__ void pair_window(const uint2* ent, const uint16_t* bst, int n_ent, int n_b, int64_t a,
-                                            int64_t b, Sink& sink, EnumOut& o) {
-  const int64_t ba = a >> kPairBucketShift;
-  if (ba >= n_b) return;
-  for (int k = bst[ba]; k < n_ent; ++k) {
+// reference's order (ascending v, then ascending top row): the entries
+// [first, first + count) of the sorted list.
+struct PairHit {
+  uint32_t first, count, bytes;
+};
+__device__ __forceinline__ PairHit pair_count(const uint2* ent, const uint16_t* bst, int n_ent, int n_b, int shift,
+                                              uint32_t a, uint32_t b) {
+  PairHit h{0, 0, 0};
+  const uint32_t ba = a >> shift;
+  if (ba >= (uint32_t)n_b) return h;
+  int k = bst[ba];
+  while (k < n_ent && ent[k].x < a) ++k;
+  h.first = (uint32_t)k;
+  for (; k < n_ent; ++k) {
     const uint2 e = ent[k];
-    if ((int64_t)e.x < a) continue;
-    if ((int64_t)e.x > b) break;
-    const int lo_row = (int)(e.y & 0xFFu), top = (int)(e.y >> 8);
-    if (lo_row == 0xFF) {
-      sink.put(o.bytes, 1, top, 0, 0);
-      o.bytes += 2;
-    } else {
-      sink.put(o.bytes, 2, lo_row, top, 0);
-      o.bytes += 3;
-    }
-    o.count++;
+    if (e.x > b) break;
+    h.count++;
+    h.bytes += (e.y & 0xFFu) == 0xFFu ? 2u : 3u;  // [1][top] or [2][low][top]
   }
+  return h;
+}
+__device__ __forceinline__ void pair_write(const uint2* ent, const PairHit& h, uint8_t* dst) {
+  for (uint32_t k = h.first; k < h.first + h.count; ++k) {
+    const uint32_t y = ent[k].y;
+    const uint32_t lo_row = y & 0xFFu, top = y >> 8;
+    if (lo_row == 0xFFu) {
+      dst[0] = 1;
+      dst[1] = (uint8_t)top;
+      dst += 2;
+    } else {
+      dst[0] = 2;
+      dst[1] = (uint8_t)lo_row;
+      dst[2] = (uint8_t)top;
+      dst += 3;
+    }
+  }
+}
+
+// Inclusive wavefront prefix sum of a u32 on the DPP crossbar (no LDS
+// round trips): 16-lane row scans, then rows 1/3 and 2/3 take the running
+// totals of the rows before them through row_bcast:15 / row_bcast:31.
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
 }
 
 // Shared tail of the scan / expand tiles: wavefront prefix sum of the payload
@@ -912,8 +941,34 @@ __device__ __forceinline__ TileOut tile_alloc(const OutArgs& out, int lane, uint
   return r;
 }
 
+// tile_alloc for the scan kernel: 32-bit sizes (regions are small; a tile
+// writes < 4 GB), the prefix sum on DPP.
+__device__ __forceinline__ TileOut tile_alloc32(const OutArgs& out, uint64_t region0, uint32_t& used, uint32_t bytes,
+                                                int8_t status) {
+  const uint32_t incl = wave_incl_scan32(bytes);
+  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  uint64_t base = 0;
+  if (total) {
+    if ((uint64_t)used + total <= out.region_bytes) {
+      base = region0 + used;
+      used += total;
+    } else {
+      unsigned long long sb = 0;
+      if ((threadIdx.x & 63) == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
+      base = out.spill_base + (uint64_t)__shfl(sb, 0, 64);
+    }
+  }
+  TileOut r{base + incl - bytes, bytes, status};
+  if (bytes && r.off + bytes > out.arena_bytes) {
+    r.status = (int8_t)kStatusArenaRetry;
+    r.bytes = 0;
+  }
+  return r;
+}
+
 __device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t region, int lane, uint64_t used,
-                                                 uint64_t n_q, uint64_t nodes, uint64_t payload) {
+                                                 int q_stat, int p_stat, uint64_t n_q, uint64_t nodes,
+                                                 uint64_t payload) {
   for (int o = 32; o > 0; o >>= 1) {
     n_q += __shfl_down(n_q, o, 64);
     nodes += __shfl_down(nodes, o, 64);
@@ -923,98 +978,124 @@ __device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t reg
     out.wave_used[region] = used;
     unsigned long long* ws = out.wave_stats + region * kNumStats;
     for (int k = 0; k < kNumStats; ++k) ws[k] = 0;
-    ws[kStatShallow] = n_q;
+    ws[q_stat] = n_q;
     ws[kStatNodes] = nodes;
-    ws[kStatPayload] = payload;
+    ws[p_stat] = payload;
   }
 }
 
 // 8 waves/SIMD (two 1024-lane workgroups per CU sharing the LDS pair list);
 // the compiler moves the surplus kernel-argument SGPRs into VGPR lanes.
+// PAIRS: the table carries the LDS pair list (tables built here).  Windows
+// below 3 * w_min whose budgets cannot bind are answered from LDS; every other
+// non-empty window goes to the expand kernel unclassified, which keeps this
+// kernel's live state (and its SGPRs) to the pair path.  Without the list,
+// every non-empty window is checked against the valid bitset here.
+template <bool PAIRS>
 __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
   extern __shared__ uint2 lds_pairs[];
   const uint16_t* lds_bucket = (const uint16_t*)(lds_pairs + t.n_pairs);
-  if (t.pairs_enabled) {
+  if (PAIRS) {
     for (int k = threadIdx.x; k < t.n_pairs; k += blockDim.x) lds_pairs[k] = t.pairs[k];
     uint16_t* bw = (uint16_t*)(lds_pairs + t.n_pairs);
     for (int k = threadIdx.x; k <= t.n_buckets; k += blockDim.x) bw[k] = t.pair_bucket[k];
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)blockIdx.x * (kScanWG / 64) + (threadIdx.x >> 6);
-  const int64_t n_waves = (int64_t)gridDim.x * (kScanWG / 64);
+  const uint32_t wave = blockIdx.x * (kScanWG / 64) + (threadIdx.x >> 6);
+  const uint32_t n_waves = gridDim.x * (kScanWG / 64);
+  const uint32_t n = (uint32_t)q.n;  // < 2^32 - 64 (host checks)
+  const uint32_t ntiles = (n + 63) >> 6;
   const uint64_t region0 = (uint64_t)wave * out.region_bytes;  // scan waves own regions [0, n_scan_waves)
-  uint64_t used = 0;                                           // wave-uniform bump pointer
-  uint64_t st_q = 0, st_payload = 0;
+  uint32_t used = 0;                                           // wave-uniform bump pointer
+  uint32_t st_q = 0, st_payload = 0;
   uint4* wl = out.work + (uint64_t)wave * out.work_region;
   uint32_t n_work = 0;  // wave-uniform
-  const int64_t ntiles = (q.n + 63) / 64;
-  for (int64_t tile = wave; tile < ntiles; tile += n_waves) {
-    const int64_t i = tile * 64 + lane;
-    const bool live = i < q.n;
+  // software pipeline: the next tile's inputs are in flight while this tile
+  // does its LDS lookups (streamed once: nontemporal loads)
+  double m_nx = 0.0, t_nx = 0.0;
+  int64_t mm_nx = q.max_mods_scalar;
+  auto fetch = [&](uint32_t tl) {
+    const uint32_t j = tl * 64 + lane;
+    if (tl < ntiles && j < n) {
+      m_nx = __builtin_nontemporal_load(q.mass + j);
+      if (q.thr) t_nx = __builtin_nontemporal_load(q.thr + j);
+      if (q.max_mods) mm_nx = __builtin_nontemporal_load(q.max_mods + j);
+    }
+  };
+  fetch(wave);
+  for (uint32_t tile = wave; tile < ntiles; tile += n_waves) {
+    const uint32_t i = tile * 64 + lane;
+    const bool live = i < n;
+    const double m_cur = m_nx, t_cur = t_nx;
+    const int64_t mm_cur = mm_nx;
+    fetch(tile + n_waves);
     bool work = false, pair = false;
     uint4 item = make_uint4(0, 0, 0, 0);
     int8_t status = SST_NONE;
-    int64_t a = 0, hi = -1;
-    CountSink3 sink;  // counting pass; the payload is written by a second LDS pass
-    EnumOut eo{0, 0, 0, 0};
+    PairHit ph{0, 0, 0};  // pair path: first entry, candidates, payload bytes
     if (live) {
-      int64_t lo;
-      quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, lo, hi);
-      const int A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
+      int64_t lo, hi;
+      quantise(m_cur, t_cur, q.thr == nullptr, q.tol, q.prec, lo, hi);
       if (hi < lo) {
         status = SST_NONE;
       } else if (hi >= t.limit) {
         status = SST_OUT_OF_TABLE;  // mass_explanation.py:134-138 (raises NameError)
       } else {
-        status = (lo <= 0 && hi >= 0) ? SST_EMPTY : SST_NONE;  // v == 0 -> [[]] (:130-131)
-        a = lo < 1 ? 1 : lo;
+        const bool zero = lo <= 0 && hi >= 0;  // v == 0 -> [[]] (:130-131)
+        status = zero ? SST_EMPTY : SST_NONE;
+        const int64_t a = lo < 1 ? 1 : lo;
         if (a <= hi) {
-          const bool never = budgets_never_bind(t, hi, A0);
-          if (never && t.pairs_enabled && hi < t.pair_hi) {
-            pair = true;
-            pair_window(lds_pairs, lds_bucket, t.n_pairs, t.n_buckets, a, hi, sink, eo);
-            if (eo.count) status = eo.count > q.cap_count ? SST_OVERFLOW : SST_SOME;
-            st_q++;
+          const bool never = budgets_never_bind(t, hi, clamp_budget(mm_cur));
+          if (PAIRS) {
+            if (never && hi < t.pair_hi) {
+              pair = true;
+              ph = pair_count(lds_pairs, lds_bucket, t.n_pairs, t.n_buckets, t.pair_shift, (uint32_t)a, (uint32_t)hi);
+              if (ph.count) status = ph.count > q.cap_count ? SST_OVERFLOW : SST_SOME;
+              st_q++;
+            } else {
+              work = true;  // classified (bitset, depth, budgets) by the expand kernel
+              item = make_uint4(i, (uint32_t)a, (uint32_t)hi,
+                                (zero ? kItemZero : 0u) | kItemUnclassified | (never ? kItemNever : 0u));
+            }
           } else if (window_has_roots(t.valid, a, hi)) {
             int cls;
             if (never) cls = hi < t.shallow_hi ? kClassShallow : kClassDeep;
             else cls = q.with_memo ? kClassExact : kClassNomemo;
             if (cls == kClassShallow) {
               work = true;  // the expand kernel writes status, count and offset
-              item = make_uint4((uint32_t)i, (uint32_t)a, (uint32_t)hi, status == SST_EMPTY ? 1u : 0u);
+              item = make_uint4(i, (uint32_t)a, (uint32_t)hi, zero ? kItemZero : 0u);
             } else {
               uint32_t slot = atomicAdd(&out.counters[cls], 1u);
-              out.lists[(int64_t)cls * q.n + slot] = (uint32_t)i;
+              out.lists[(int64_t)cls * q.n + slot] = i;
+              status = (int8_t)kStatusPending;
             }
-            status = (int8_t)kStatusPending;
           }
         }
       }
     }
-    const uint64_t want = status == SST_SOME ? eo.bytes : 0;
-    const TileOut to = tile_alloc(out, lane, region0, used, want, status);
-    if (to.bytes) {
-      MemSink3 ms{out.payload + to.off};
-      EnumOut e2{0, 0, 0, 0};
-      pair_window(lds_pairs, lds_bucket, t.n_pairs, t.n_buckets, a, hi, ms, e2);
-    }
-    // NONE / EMPTY / OUT_OF_TABLE carry no candidates: count and offset stay
-    // undefined (include/sst.h), one byte per resolved query
-    if (live && !work) {
-      out.status[i] = to.status;
-      if (pair && (to.status == SST_SOME || to.status == SST_OVERFLOW)) {
-        out.count[i] = eo.count;
-        out.offset[i] = to.bytes ? to.off : 0;
+    if (PAIRS) {
+      const TileOut to = tile_alloc32(out, region0, used, status == SST_SOME ? ph.bytes : 0u, status);
+      if (to.bytes) pair_write(lds_pairs, ph, out.payload + to.off);
+      // NONE / EMPTY / OUT_OF_TABLE carry no candidates: count and offset stay
+      // undefined (include/sst.h), one byte per resolved query
+      if (live && !work) {
+        out.status[i] = to.status;
+        if (pair && (to.status == SST_SOME || to.status == SST_OVERFLOW)) {
+          out.count[i] = ph.count;
+          out.offset[i] = to.bytes ? to.off : 0;
+        }
       }
+      st_payload += (uint32_t)to.bytes;
+    } else if (live && !work) {
+      out.status[i] = status;
     }
-    st_payload += to.bytes;
     const uint64_t bal = __ballot(work);
     if (work) wl[n_work + __builtin_popcountll(bal & lane_mask_lt(lane))] = item;
     n_work += (uint32_t)__builtin_popcountll(bal);
   }
   if (lane == 0) out.work_count[wave] = n_work;
-  wave_stats_flush(out, wave, lane, used, st_q, 0, st_payload);
+  wave_stats_flush(out, wave, lane, used, kStatPair, kStatPairPayload, st_q, 0, st_payload);
 }
 
 // ---------------------------------------------------------------------------
@@ -1041,17 +1122,34 @@ __global__ __launch_bounds__(kWG) void k_explain_expand(TableArgs t, QueryArgs q
       const bool live = k0 + lane < nw;
       int64_t i = 0, a = 0, b = -1;
       int8_t status = SST_NONE;
+      bool deferred = false;
       RegSink sink;
       EnumOut eo{0, 0, 0, 0};
       if (live) {
-        const uint4 item = wl[k0 + lane];  // {query, first window value >= 1, last, v == 0 in window}
+        const uint4 item = wl[k0 + lane];  // {query, first window value >= 1, last, kItem* flags}
         i = item.x;
         a = item.y;
         b = item.z;
-        shallow_window(t, s, a, b, sink, eo);
-        status = eo.count ? (eo.count > q.cap_count ? SST_OVERFLOW : SST_SOME) : (item.w ? SST_EMPTY : SST_NONE);
-        st_q++;
-        st_nodes += eo.nodes;
+        bool run = true;
+        if (item.w & kItemUnclassified) {  // from the pair-list scan: route it here
+          if (!window_has_roots(t.valid, a, b)) {
+            run = false;
+          } else if (!(item.w & kItemNever) || b >= t.shallow_hi) {
+            const int cls = (item.w & kItemNever) ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
+            const uint32_t slot = atomicAdd(&out.counters[cls], 1u);
+            out.lists[(int64_t)cls * q.n + slot] = (uint32_t)i;
+            run = false;
+            deferred = true;
+          }
+        }
+        if (run) {
+          shallow_window(t, s, a, b, sink, eo);
+          st_q++;
+          st_nodes += eo.nodes;
+        }
+        status = eo.count ? (eo.count > q.cap_count ? SST_OVERFLOW : SST_SOME)
+                          : ((item.w & kItemZero) ? SST_EMPTY : SST_NONE);
+        if (deferred) status = (int8_t)kStatusPending;
       }
       const TileOut to = tile_alloc(out, lane, region0, used, status == SST_SOME ? eo.bytes : 0, status);
       if (to.bytes) {
@@ -1063,15 +1161,17 @@ __global__ __launch_bounds__(kWG) void k_explain_expand(TableArgs t, QueryArgs q
           shallow_window(t, s, a, b, ms, e2);
         }
       }
-      if (live) {
+      if (live) {  // deferred queries: the deep / exact kernels write all three
         out.status[i] = to.status;
-        out.count[i] = eo.count;
-        out.offset[i] = to.bytes ? to.off : 0;
+        if (!deferred) {
+          out.count[i] = eo.count;
+          out.offset[i] = to.bytes ? to.off : 0;
+        }
       }
       st_payload += to.bytes;
     }
   }
-  wave_stats_flush(out, region, lane, used, st_q, st_nodes, st_payload);
+  wave_stats_flush(out, region, lane, used, kStatShallow, kStatPayload, st_q, st_nodes, st_payload);
 }
 
 // Compaction of the arena into a dense payload (result fetch / gather only):
@@ -1333,7 +1433,10 @@ size_t scan_dyn_lds(const TableArgs& t) {
 hipError_t launch_explain_scan(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
                                hipStream_t st) {
   if (q.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_explain_scan, dim3(n_blocks), dim3(kScanWG), scan_dyn_lds(t), st, t, q, o);
+  if (t.pairs_enabled)
+    hipLaunchKernelGGL(k_explain_scan<true>, dim3(n_blocks), dim3(kScanWG), scan_dyn_lds(t), st, t, q, o);
+  else
+    hipLaunchKernelGGL(k_explain_scan<false>, dim3(n_blocks), dim3(kScanWG), 0, st, t, q, o);
   return hipGetLastError();
 }
 hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
@@ -1350,7 +1453,10 @@ static int occupancy(const void* k, int threads, size_t dyn) {
   }
   return nb > 0 ? nb : 1;
 }
-int explain_scan_blocks_per_cu(size_t dyn) { return occupancy((const void*)k_explain_scan, kScanWG, dyn); }
+int explain_scan_blocks_per_cu(size_t dyn) {
+  return dyn ? occupancy((const void*)k_explain_scan<true>, kScanWG, dyn)
+             : occupancy((const void*)k_explain_scan<false>, kScanWG, 0);
+}
 int explain_expand_blocks_per_cu() { return occupancy((const void*)k_explain_expand, kWG, 0); }
 hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* pre, uint8_t* dst, hipStream_t st) {
   const uint64_t spill_cap = o.arena_bytes > o.spill_base ? o.arena_bytes - o.spill_base : 0;

@@ -7,7 +7,6 @@ TAG=${1:-pmc}
 shift
 export TMPDIR=/tmp
 BENCH="bench.py --steps 5 --warmup 1 --no-cpu-baseline $@"
-timeout -k 10 120 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1 || true
 i=0
 
 while read -r grp; do
@@ -17,3 +16,5 @@ while read -r grp; do
   rc=$?; echo "[pmc $i: $grp] rc=$rc"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 done < tools/pmc_groups.txt
+python3 tools/pmc_summary.py gpurun_out/${TAG}_pmc.json gpurun_out/${TAG}_p* > gpurun_out/${TAG}_pmc.txt 2>&1
+echo "[pmc summary] rc=$?"
