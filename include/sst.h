@@ -155,6 +155,10 @@ int sst_result_stats(const sst_result* r, uint64_t* stats_out /* [8] */);
  * summed milliseconds and launch counts per kernel id since the last read
  * (or enable), then resets them. */
 int sst_profile_enable(sst_ctx* ctx, int on);
+/* Same, restricted to the kernel ids set in kernel_mask (bit k = id k): each
+ * bracketed launch costs two event records on the stream, so a benchmark
+ * brackets only the kernels it reports. */
+int sst_profile_select(sst_ctx* ctx, uint32_t kernel_mask);
 int sst_profile_read(sst_ctx* ctx, double* ms_total /* [SST_K_COUNT] */, int64_t* launches /* [SST_K_COUNT] */);
 
 #ifdef __cplusplus

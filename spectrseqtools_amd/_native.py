@@ -23,7 +23,8 @@ EXPORTS = (
     "sst_ctx_synchronize", "sst_table_build", "sst_table_upload", "sst_table_set_budgets", "sst_table_shape",
     "sst_table_download", "sst_table_destroy", "sst_is_valid_batch", "sst_is_valid_batch_device",
     "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
-    "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_read",
+    "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
+    "sst_profile_read",
 )
 
 # kernel ids of sst_profile_read
@@ -77,6 +78,7 @@ def load_library(path=LIB_PATH):
     lib.sst_result_free.restype = None
     lib.sst_result_stats.argtypes = [_P, _P]
     lib.sst_profile_enable.argtypes = [_P, _I]
+    lib.sst_profile_select.argtypes = [_P, ctypes.c_uint32]
     lib.sst_profile_read.argtypes = [_P, _P, _P]
     return lib
 
@@ -130,8 +132,15 @@ class Engine:
     def synchronize(self):
         self.check(self._lib.sst_ctx_synchronize(self.handle), "sst_ctx_synchronize")
 
-    def profile(self, on=True):
-        self.check(self._lib.sst_profile_enable(self.handle, int(bool(on))), "sst_profile_enable")
+    def profile(self, on=True, kernels=None):
+        """Bracket launches with HIP events: all kernels, or only the ids in `kernels`."""
+        if kernels is None or not on:
+            self.check(self._lib.sst_profile_enable(self.handle, int(bool(on))), "sst_profile_enable")
+        else:
+            mask = 0
+            for k in kernels:
+                mask |= 1 << int(k)
+            self.check(self._lib.sst_profile_select(self.handle, mask), "sst_profile_select")
 
     def profile_read(self):
         """{kernel id: (total ms, launches)} since the last read."""

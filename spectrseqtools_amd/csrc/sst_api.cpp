@@ -62,7 +62,7 @@ struct sst_ctx {
   int n_cu = 256;       // compute units (persistent grid sizing)
   int expand_blocks = 0;  // resident workgroups of k_explain_expand
   // measurement: hipEvents around launches on `stream`
-  bool prof = false;
+  uint32_t prof = 0;  // kernel ids whose launches are bracketed by events
   struct Pending {
     int kid;
     hipEvent_t a, b;
@@ -91,7 +91,12 @@ struct sst_result {
   sst_ctx* ctx = nullptr;
   int64_t n = 0;
   int64_t cap_n = 0;
-  DevBuf status, count, offset, payload, cursor, counters, lists, stats;
+  DevBuf status, count, offset, payload, ctl, lists;
+  // control block (spill cursor, class counters, stats) of the current pass;
+  // two of them: each pass's scan kernel zeroes the other for the next pass
+  // (no memsets between passes)
+  int parity = 1;
+  bool ctl_ready = false;
   DevBuf wave_used, wave_stats, prefix, dense, work, work_count;
   int n_waves = 0;  // expand waves
   int n_regions = 0;  // scan + expand waves (arena regions)
@@ -145,7 +150,7 @@ struct Prof {
   int kid;
   hipEvent_t a = nullptr;
   Prof(sst_ctx* c_, int kid_) : c(c_), kid(kid_) {
-    if (c->prof && (a = take_event(c))) (void)hipEventRecord(a, c->stream);
+    if (((c->prof >> kid) & 1u) && (a = take_event(c))) (void)hipEventRecord(a, c->stream);
   }
   ~Prof() {
     if (!a) return;
@@ -570,13 +575,19 @@ constexpr int kExactLanes0 = 2048;      // exact-path concurrent lanes (first at
 constexpr uint64_t kNodeBudget = 1ull << 32;
 
 void free_result_bufs(sst_result* r) {
-  for (DevBuf* b : {&r->status, &r->count, &r->offset, &r->payload, &r->cursor, &r->counters, &r->lists, &r->stats,
+  for (DevBuf* b : {&r->status, &r->count, &r->offset, &r->payload, &r->ctl, &r->lists,
                     &r->wave_used, &r->wave_stats, &r->prefix, &r->dense, &r->work, &r->work_count})
     b->release();
 }
 
+// control block layout (u64 words): [0] spill cursor, [1..2] class counters
+// (u32 x kNumClasses), [4..4+kNumStats) deferred-kernel stats
+constexpr int kCtlWords = 16;
+uint64_t* ctl_block(sst_result* r, int parity) { return (uint64_t*)r->ctl.p + parity * kCtlWords; }
+
 OutArgs out_args(sst_result* r) {
   OutArgs o;
+  uint64_t* ctl = ctl_block(r, r->parity);
   o.status = (int8_t*)r->status.p;
   o.count = (uint64_t*)r->count.p;
   o.offset = (uint64_t*)r->offset.p;
@@ -584,12 +595,14 @@ OutArgs out_args(sst_result* r) {
   o.arena_bytes = r->arena_bytes;
   o.region_bytes = r->region_bytes;
   o.spill_base = (uint64_t)r->n_regions * r->region_bytes;
-  o.cursor = (uint64_t*)r->cursor.p;
+  o.cursor = ctl;
+  o.ctl_next = ctl_block(r, r->parity ^ 1);
+  o.ctl_words = kCtlWords;
   o.wave_used = (uint64_t*)r->wave_used.p;
   o.wave_stats = (unsigned long long*)r->wave_stats.p;
-  o.counters = (uint32_t*)r->counters.p;
+  o.counters = (uint32_t*)(ctl + 1);
   o.lists = (uint32_t*)r->lists.p;
-  o.stats = (unsigned long long*)r->stats.p;
+  o.stats = (unsigned long long*)(ctl + 4);
   o.work = (uint4*)r->work.p;
   o.work_count = (uint32_t*)r->work_count.p;
   o.work_region = r->work_region;
@@ -619,12 +632,17 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   sst_ctx* c = t->ctx;
   const int64_t n = r->n;
   r->arena_bytes = (uint64_t)r->n_regions * r->region_bytes + r->spill_bytes;
-  if (!r->cursor.ensure(8) || !r->counters.ensure(kNumClasses * 4) || !r->stats.ensure(kNumStats * 8) ||
-      !r->lists.ensure((size_t)kNumClasses * std::max<int64_t>(n, 1) * 4) || !r->payload.ensure(r->arena_bytes))
+  static_assert(4 + kNumStats <= kCtlWords && 2 * 2 >= kNumClasses, "control block layout");
+  if (!r->ctl.ensure(2 * kCtlWords * 8) || !r->lists.ensure((size_t)kNumClasses * std::max<int64_t>(n, 1) * 4) ||
+      !r->payload.ensure(r->arena_bytes))
     return fail(c, SST_E_NOMEM, "device allocation failed (result)");
-  HIP_OK(c, hipMemsetAsync(r->cursor.p, 0, 8, c->stream));
-  HIP_OK(c, hipMemsetAsync(r->counters.p, 0, kNumClasses * 4, c->stream));
-  HIP_OK(c, hipMemsetAsync(r->stats.p, 0, kNumStats * 8, c->stream));
+  if (!r->ctl_ready) {
+    HIP_OK(c, hipMemsetAsync(r->ctl.p, 0, 2 * kCtlWords * 8, c->stream));
+    r->ctl_ready = true;
+  }
+  r->parity ^= 1;  // zeroed by the previous pass's scan (or above)
+  if (n == 0)      // no scan launch: zero the next pass's block here
+    HIP_OK(c, hipMemsetAsync(ctl_block(r, r->parity ^ 1), 0, kCtlWords * 8, c->stream));
   if (!c->ws_deep.ensure((size_t)kDeepBlocks * kWG * kMaxDepth * glob_frame_bytes()))
     return fail(c, SST_E_NOMEM, "device allocation failed (deep workspace)");
   if (c->hash_cap == 0)
@@ -719,7 +737,7 @@ int fetch(sst_result* r) {
     HIP_OK(c, hipMemcpyAsync(r->h_offset.data(), r->offset.p, n * 8, hipMemcpyDeviceToHost, c->stream));
   }
   HIP_OK(c, hipMemcpyAsync(pre_tail, (uint64_t*)r->prefix.p + r->n_regions, 16, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipMemcpyAsync(r->h_stats, r->stats.p, kNumStats * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipMemcpyAsync(r->h_stats, ctl_block(r, r->parity) + 4, kNumStats * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipMemcpyAsync(ws.data(), r->wave_stats.p, ws.size() * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   for (int w = 0; w < r->n_regions; ++w)
@@ -801,7 +819,7 @@ int sst_explain_batch(sst_table* t, const double* mass, const double* thr, int64
     if (!arena_retry && !exact_retry) break;
     if (arena_retry) {  // the spill cursor kept counting past the arena: size the spill area to it
       uint64_t cur = 0;
-      HIP_OK(c, hipMemcpy(&cur, r->cursor.p, 8, hipMemcpyDeviceToHost));
+      HIP_OK(c, hipMemcpy(&cur, ctl_block(r, r->parity), 8, hipMemcpyDeviceToHost));
       r->spill_bytes = std::max<uint64_t>(2 * r->spill_bytes, cur + (1u << 20));
       r->payload.release();
       r->dense.release();
@@ -873,7 +891,9 @@ int sst_result_stats(const sst_result* r, uint64_t* s) {
   return SST_OK;
 }
 
-int sst_profile_enable(sst_ctx* c, int on) {
+int sst_profile_enable(sst_ctx* c, int on) { return sst_profile_select(c, on ? (1u << SST_K_COUNT) - 1u : 0u); }
+
+int sst_profile_select(sst_ctx* c, uint32_t kernel_mask) {
   if (!c) return SST_E_ARG;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
@@ -882,7 +902,7 @@ int sst_profile_enable(sst_ctx* c, int on) {
     c->prof_ms[i] = 0;
     c->prof_n[i] = 0;
   }
-  c->prof = on != 0;
+  c->prof = kernel_mask & ((1u << SST_K_COUNT) - 1u);
   return SST_OK;
 }
 

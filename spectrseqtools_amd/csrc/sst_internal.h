@@ -94,6 +94,8 @@ struct OutArgs {
   uint64_t region_bytes;      // per-wave region of the main kernel
   uint64_t spill_base;        // = n_waves * region_bytes
   uint64_t* cursor;           // spill bytes taken
+  uint64_t* ctl_next;         // the next pass's control block: zeroed by the scan kernel
+  int ctl_words;
   uint64_t* wave_used;        // [n_waves] bytes used in each region (expand kernel waves)
   unsigned long long* wave_stats;  // [n_waves][kNumStats] expand-kernel counters
   uint4* work;                // [n_scan_waves][work_region] queued SHALLOW {query, a, b, has_zero}

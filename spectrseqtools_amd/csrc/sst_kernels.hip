@@ -995,6 +995,7 @@ template <bool PAIRS>
 __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
   extern __shared__ uint2 lds_pairs[];
   const uint16_t* lds_bucket = (const uint16_t*)(lds_pairs + t.n_pairs);
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
   if (PAIRS) {
     for (int k = threadIdx.x; k < t.n_pairs; k += blockDim.x) lds_pairs[k] = t.pairs[k];
     uint16_t* bw = (uint16_t*)(lds_pairs + t.n_pairs);
@@ -1094,7 +1095,10 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     if (work) wl[n_work + __builtin_popcountll(bal & lane_mask_lt(lane))] = item;
     n_work += (uint32_t)__builtin_popcountll(bal);
   }
-  if (lane == 0) out.work_count[wave] = n_work;
+  if (lane == 0) {
+    out.work_count[wave] = n_work;
+    if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle expand launch exit at once
+  }
   wave_stats_flush(out, wave, lane, used, kStatPair, kStatPairPayload, st_q, 0, st_payload);
 }
 
@@ -1107,11 +1111,16 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kWG) void k_explain_expand(TableArgs t, QueryArgs q, OutArgs out) {
   __shared__ Lds s;
-  stage_rows(s, t);
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
   const int64_t n_waves = (int64_t)gridDim.x * (kWG / 64);
   const int64_t region = out.n_scan_waves + wave;  // expand regions follow the scan regions
+  if (out.counters[kClassShallow] == 0) {  // nothing queued (block-uniform): empty regions
+    if (lane < kNumStats) out.wave_stats[region * kNumStats + lane] = 0;
+    if (lane == 0) out.wave_used[region] = 0;
+    return;
+  }
+  stage_rows(s, t);
   const uint64_t region0 = (uint64_t)region * out.region_bytes;
   uint64_t used = 0;  // wave-uniform bump pointer
   uint64_t st_q = 0, st_nodes = 0, st_payload = 0;
@@ -1250,8 +1259,9 @@ template <int MODE>
 __global__ __launch_bounds__(kWG) void k_explain_deep(TableArgs t, QueryArgs q, OutArgs out, int cls,
                                                       GlobFrame* ws) {
   __shared__ Lds s;
-  stage_rows(s, t);
   const uint32_t n_list = out.counters[cls];
+  if (n_list == 0) return;  // block-uniform: idle launch
+  stage_rows(s, t);
   const int64_t gid = (int64_t)blockIdx.x * kWG + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * kWG;
   GlobStack st{ws + gid * kMaxDepth};
@@ -1301,8 +1311,9 @@ __global__ __launch_bounds__(kWG) void k_explain_deep(TableArgs t, QueryArgs q, 
 // enumeration (phase 2).  Per lane: a hash slice and a frame slice.
 __global__ __launch_bounds__(64) void k_explain_exact(TableArgs t, QueryArgs q, OutArgs out, ExactWs ws) {
   __shared__ Lds s;
-  stage_rows(s, t);
   const uint32_t n_list = out.counters[kClassExact];
+  if (n_list == 0) return;  // block-uniform: idle launch
+  stage_rows(s, t);
   const int64_t gid = (int64_t)blockIdx.x * 64 + threadIdx.x;
   const int64_t nthreads = (int64_t)gridDim.x * 64;
   P1Frame* fr = (P1Frame*)(ws.frames + gid * kMaxDepth * sizeof(P1Frame));
