@@ -829,11 +829,11 @@ __device__ __forceinline__ void wg_stat(unsigned long long* stats, int k, uint64
 
 // ---------------------------------------------------------------------------
 // Explain, part 1 -- k_explain_scan (persistent grid, independent waves):
-// every wave streams 64-query tiles in a grid stride: quantises the window,
-// reads its valid-bitset words with independent loads, resolves every query
-// without a reachable window value (the large majority), and appends the
-// SHALLOW rest to the wave's own worklist region (ballot + mbcnt: no atomics).
-// Budget-binding / deep / no-memo queries go to the class lists.
+// every wave streams 64-query tiles in a grid stride (inputs prefetched one
+// tile ahead), quantises the window and resolves it: from the LDS pair list
+// (<= 2-item windows), or -- tables without the list -- from the valid
+// bitset, queueing the rest to the wave's own worklist region (ballot +
+// mbcnt: no atomics) or the deferred class lists.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t lane_mask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
@@ -984,8 +984,8 @@ __device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t reg
   }
 }
 
-// 8 waves/SIMD (two 1024-lane workgroups per CU sharing the LDS pair list);
-// the compiler moves the surplus kernel-argument SGPRs into VGPR lanes.
+// 8 waves/SIMD: two 1024-lane workgroups per CU, each with its LDS copy of
+// the pair list (<= 78 KB).
 // PAIRS: the table carries the LDS pair list (tables built here).  Windows
 // below 3 * w_min whose budgets cannot bind are answered from LDS; every other
 // non-empty window goes to the expand kernel unclassified, which keeps this
