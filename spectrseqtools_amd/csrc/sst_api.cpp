@@ -197,6 +197,15 @@ int64_t table_cols(int64_t max_mass, int C) {
 // for tables this library built from exactly these masses: then a window value
 // below 3 * w_min is reachable iff it is such a sum, and the reference's DFS
 // lists its candidates in (v, top row) order (pair fast path).
+// u32 fast-path limits of the scan kernel (TableArgs::never_lim / pair_lim)
+void refresh_limits(sst_table* t) {
+  TableArgs& a = t->args;
+  const int64_t u32max = (int64_t)UINT32_MAX;
+  const int64_t nl = !a.any_mod ? u32max : (a.fast_limit_B < 0 ? 0 : std::min(a.fast_limit_B, u32max - 1) + 1);
+  a.never_lim = (uint32_t)nl;
+  a.pair_lim = (uint32_t)std::min<int64_t>(std::min<int64_t>(a.pair_hi, u32max), nl);
+}
+
 int build_pair_list(sst_table* t, bool self_built) {
   sst_ctx* c = t->ctx;
   t->args.pairs_enabled = 0;
@@ -503,6 +512,7 @@ int sst_table_set_budgets(sst_table* t, const uint8_t* is_mod, const int64_t* ca
   t->args.any_mod = any_mod;
   t->args.w_min_mod = (int)(wmm > 0 ? wmm : 1);
   t->args.fast_limit_B = lim;
+  refresh_limits(t);
   return SST_OK;
 }
 
@@ -648,7 +658,7 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   if (c->hash_cap == 0)
     if (int rc = ensure_exact_ws(c, kHashCap0, kExactLanes0)) return rc;
   r->compacted = false;
-  QueryArgs q{d_mass, d_thr, d_mods, mods_scalar, n, tol, prec, with_memo, cap_count, kNodeBudget};
+  QueryArgs q{d_mass, d_thr, d_mods, mods_scalar, n, tol, prec, 1.0 / prec, with_memo, cap_count, kNodeBudget};
   OutArgs o = out_args(r);
   {
     Prof p(c, SST_K_EXPLAIN_MAIN);

@@ -60,6 +60,10 @@ struct TableArgs {
   int n_pairs;
   int n_buckets;
   int pair_shift;
+  // u32 forms of the fast-path limits (window values are < 2^31):
+  // hi < never_lim  <=>  hi <= fast_limit_B (no per-row cap binds);
+  // hi < pair_lim   <=>  pair-list window with no per-row cap binding
+  uint32_t never_lim, pair_lim;
   int pairs_enabled;
   int n_rows;
   int any_mod;
@@ -74,6 +78,7 @@ struct QueryArgs {
   int64_t max_mods_scalar;
   int64_t n;
   double tol, prec;
+  double rprec;  // 1 / prec (host-rounded): quotient fast path, see quantise()
   int with_memo;
   uint64_t cap_count;
   uint64_t node_budget;

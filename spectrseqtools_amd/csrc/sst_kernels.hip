@@ -78,13 +78,41 @@ __device__ __forceinline__ M128 rec_L(ulonglong2 rec) { return {rec.x, rec.y & (
 
 __device__ __forceinline__ ulonglong2 ld_index(const ulonglong2* idx, int64_t m) { return idx[m]; }
 
-// Reference quantisation, mass_explanation.py:107,110-114.  IEEE f64 division
-// (no fast-math), rint = Python round(x, 0) ties-to-even, ceil = np.ceil.
+// Reference quantisation, mass_explanation.py:107,110-114: target =
+// rint(mass / prec) (Python round(x, 0): ties-to-even) and thr = ceil(t / prec)
+// on the IEEE f64 quotient (no fast-math).  The quotient is taken as
+// mass * (1/prec), within 2.5 ulp of the exact one; the correctly rounded
+// division runs only when that product lies within 2^-50 (relative) of a
+// point where rint / ceil change value, so the integers are exactly the
+// reference's.
+__device__ __forceinline__ double rint_quot(double num, double den, double rden) {
+  const double q = num * rden;
+  const double f = q - __builtin_floor(q);
+  if (!(__builtin_fabs(q) < 0x1p40) || __builtin_fabs(f - 0.5) <= __builtin_fabs(q) * 0x1p-50)
+    return __builtin_rint(num / den);
+  return __builtin_rint(q);
+}
+__device__ __forceinline__ double ceil_quot(double num, double den, double rden) {
+  if (num == 0.0) return 0.0;
+  const double q = num * rden;
+  if (!(__builtin_fabs(q) < 0x1p40) || __builtin_fabs(q - __builtin_rint(q)) <= __builtin_fabs(q) * 0x1p-50)
+    return __builtin_ceil(num / den);
+  return __builtin_ceil(q);
+}
+// window [lo, hi] as exact f64 integers (|values| < 2^53)
+__device__ __forceinline__ void quantise_f(double mass, double thr_abs, bool thr_none, double tol, double prec,
+                                           double rprec, double& lo, double& hi) {
+  const double t = thr_none ? tol * mass : thr_abs;
+  const double target = rint_quot(mass, prec, rprec);
+  const double th = ceil_quot(t, prec, rprec);
+  lo = target - th;
+  hi = target + th;
+}
 __device__ __forceinline__ void quantise(double mass, double thr_abs, bool thr_none, double tol, double prec,
-                                         int64_t& lo, int64_t& hi) {
-  double t = thr_none ? tol * mass : thr_abs;
-  int64_t target = (int64_t)__builtin_rint(mass / prec);
-  int64_t th = (int64_t)__builtin_ceil(t / prec);
+                                         double rprec, int64_t& lo, int64_t& hi) {
+  const double t = thr_none ? tol * mass : thr_abs;
+  const int64_t target = (int64_t)rint_quot(mass, prec, rprec);
+  const int64_t th = (int64_t)ceil_quot(t, prec, rprec);
   lo = target - th;
   hi = target + th;
 }
@@ -322,11 +350,12 @@ __global__ void k_index(const void* __restrict__ packed, int n_rows, int64_t nco
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_is_valid(const uint64_t* __restrict__ valid, int64_t limit,
                                                   const double* __restrict__ mass, const double* __restrict__ thr,
-                                                  int64_t n, double tol, double prec, int8_t* __restrict__ out) {
+                                                  int64_t n, double tol, double prec, double rprec,
+                                                  int8_t* __restrict__ out) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int64_t lo, hi;
-  quantise(mass[i], thr ? thr[i] : 0.0, thr == nullptr, tol, prec, lo, hi);
+  quantise(mass[i], thr ? thr[i] : 0.0, thr == nullptr, tol, prec, rprec, lo, hi);
   out[i] = valid_window(valid, limit, lo, hi);
 }
 
@@ -1031,48 +1060,44 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     const double m_cur = m_nx, t_cur = t_nx;
     const int64_t mm_cur = mm_nx;
     fetch(tile + n_waves);
+    // window classification, branch-free: exact f64 integers, then u32
+    // (a window inside the table lies in [0, limit) with limit < 2^31)
+    double lof, hif;
+    quantise_f(m_cur, t_cur, q.thr == nullptr, q.tol, q.prec, q.rprec, lof, hif);
+    const bool nonempty = live && lof <= hif;
+    const bool oot = nonempty && !(hif < (double)t.limit);  // mass_explanation.py:134-138 (NameError)
+    const bool zero = nonempty && !oot && lof <= 0.0 && hif >= 0.0;  // v == 0 -> [[]] (:130-131)
+    const double af = lof < 1.0 ? 1.0 : lof;
+    const bool active = nonempty && !oot && af <= hif;
+    const uint32_t a = active ? (uint32_t)af : 0u, hi = active ? (uint32_t)hif : 0u;
+    // fast-path theorem (budgets_never_bind) on u32 window values
+    const int A0 = clamp_budget(mm_cur);
+    const bool a0ok = !t.any_mod || A0 >= kInfBudget || (uint64_t)hi < (uint64_t)(A0 + 1) * (uint64_t)t.w_min_mod;
+    const bool never = hi < t.never_lim && a0ok;
+    int8_t status = oot ? (int8_t)SST_OUT_OF_TABLE : (zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE);
     bool work = false, pair = false;
     uint4 item = make_uint4(0, 0, 0, 0);
-    int8_t status = SST_NONE;
     PairHit ph{0, 0, 0};  // pair path: first entry, candidates, payload bytes
-    if (live) {
-      int64_t lo, hi;
-      quantise(m_cur, t_cur, q.thr == nullptr, q.tol, q.prec, lo, hi);
-      if (hi < lo) {
-        status = SST_NONE;
-      } else if (hi >= t.limit) {
-        status = SST_OUT_OF_TABLE;  // mass_explanation.py:134-138 (raises NameError)
+    if (PAIRS) {
+      pair = active && a0ok && hi < t.pair_lim;
+      work = active && !pair;  // classified (bitset, depth, budgets) by the expand kernel
+      item = make_uint4(i, a, hi, (zero ? kItemZero : 0u) | kItemUnclassified | (never ? kItemNever : 0u));
+      if (pair) {
+        ph = pair_count(lds_pairs, lds_bucket, t.n_pairs, t.n_buckets, t.pair_shift, a, hi);
+        st_q++;
+      }
+      if (ph.count) status = ph.count > q.cap_count ? SST_OVERFLOW : SST_SOME;
+    } else if (active && window_has_roots(t.valid, a, hi)) {
+      int cls;
+      if (never) cls = hi < t.shallow_hi ? kClassShallow : kClassDeep;
+      else cls = q.with_memo ? kClassExact : kClassNomemo;
+      if (cls == kClassShallow) {
+        work = true;  // the expand kernel writes status, count and offset
+        item = make_uint4(i, a, hi, zero ? kItemZero : 0u);
       } else {
-        const bool zero = lo <= 0 && hi >= 0;  // v == 0 -> [[]] (:130-131)
-        status = zero ? SST_EMPTY : SST_NONE;
-        const int64_t a = lo < 1 ? 1 : lo;
-        if (a <= hi) {
-          const bool never = budgets_never_bind(t, hi, clamp_budget(mm_cur));
-          if (PAIRS) {
-            if (never && hi < t.pair_hi) {
-              pair = true;
-              ph = pair_count(lds_pairs, lds_bucket, t.n_pairs, t.n_buckets, t.pair_shift, (uint32_t)a, (uint32_t)hi);
-              if (ph.count) status = ph.count > q.cap_count ? SST_OVERFLOW : SST_SOME;
-              st_q++;
-            } else {
-              work = true;  // classified (bitset, depth, budgets) by the expand kernel
-              item = make_uint4(i, (uint32_t)a, (uint32_t)hi,
-                                (zero ? kItemZero : 0u) | kItemUnclassified | (never ? kItemNever : 0u));
-            }
-          } else if (window_has_roots(t.valid, a, hi)) {
-            int cls;
-            if (never) cls = hi < t.shallow_hi ? kClassShallow : kClassDeep;
-            else cls = q.with_memo ? kClassExact : kClassNomemo;
-            if (cls == kClassShallow) {
-              work = true;  // the expand kernel writes status, count and offset
-              item = make_uint4(i, (uint32_t)a, (uint32_t)hi, zero ? kItemZero : 0u);
-            } else {
-              uint32_t slot = atomicAdd(&out.counters[cls], 1u);
-              out.lists[(int64_t)cls * q.n + slot] = i;
-              status = (int8_t)kStatusPending;
-            }
-          }
-        }
+        uint32_t slot = atomicAdd(&out.counters[cls], 1u);
+        out.lists[(int64_t)cls * q.n + slot] = i;
+        status = (int8_t)kStatusPending;
       }
     }
     if (PAIRS) {
@@ -1269,7 +1294,7 @@ __global__ __launch_bounds__(kWG) void k_explain_deep(TableArgs t, QueryArgs q, 
   for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
     int64_t i = out.lists[(int64_t)cls * q.n + j];
     int64_t lo, hi;
-    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, lo, hi);
+    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
     int A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
     bool has_zero = lo <= 0 && hi >= 0;
     int64_t a = lo < 1 ? 1 : lo, b = hi;
@@ -1326,7 +1351,7 @@ __global__ __launch_bounds__(64) void k_explain_exact(TableArgs t, QueryArgs q, 
   for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
     int64_t i = out.lists[(int64_t)kClassExact * q.n + j];
     int64_t lo, hi;
-    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, lo, hi);
+    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
     int A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
     bool has_zero = lo <= 0 && hi >= 0;
     int64_t a = lo < 1 ? 1 : lo, b = hi;
@@ -1434,7 +1459,7 @@ hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, const double* m
                            double tol, double prec, int8_t* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_is_valid, dim3(blocks_for(n, 256)), dim3(256), 0, st, valid, limit, mass, thr, n, tol, prec,
-                     out);
+                     1.0 / prec, out);
   return hipGetLastError();
 }
 size_t scan_dyn_lds(const TableArgs& t) {

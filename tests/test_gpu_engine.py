@@ -170,3 +170,49 @@ def test_canonical_reduced_table(engine):
     seqs = [rng.choice(ms[1:], rng.integers(1, 9)) for _ in range(400)]
     masses = np.array([s.sum() * 1e-3 for s in seqs])
     _check_explain(dev, host, ms, [False] * 5, [0, 20, 20, 20, 20], masses, None, math.inf, True, tol=10e-6)
+
+
+def _boundary_queries(prec, ks, ulps=6):
+    """Masses whose quotient mass/prec sits within a few ulps of a half-integer
+    (rint ties) and thresholds whose quotient sits on an integer (ceil edge),
+    placed so that the window [target - thr, target + thr] starts exactly on
+    or next to a reachable multiple of 1000: a one-unit rounding difference
+    flips the answer."""
+    masses, thr = [], []
+    for k in ks:
+        for half in (3.5, 4.5):  # ties to even go down at 4.5, up at 3.5
+            base = (1000 * k + half) * prec
+            mb = [base]
+            for _ in range(ulps):
+                mb.append(np.nextafter(mb[-1], np.inf))
+            mb2 = [base]
+            for _ in range(ulps):
+                mb2.append(np.nextafter(mb2[-1], -np.inf))
+            tb = (3.0 if half == 3.5 else 4.0) * prec
+            tv = [tb, np.nextafter(tb, np.inf), np.nextafter(tb, -np.inf)]
+            for m in mb + mb2[1:]:
+                for t in tv:
+                    masses.append(m)
+                    thr.append(t)
+    return np.array(masses), np.array(thr)
+
+
+@pytest.mark.parametrize("prec", [1e-3, 3e-3, 7.77e-4])
+def test_quantisation_boundaries_vs_oracle(engine, prec):
+    ms = [0, 1000]
+    dev = _native.DeviceTable.build(ms, 1000 * 35, 32, engine=engine)
+    host = oracle.build_table(ms, 1000 * 35, 32)
+    masses, thr = _boundary_queries(prec, range(1, 31))
+    got = dev.is_valid(masses, thr, 1e-5, prec)
+    want = oracle.is_valid_batch(host, 32, masses, thr, 1e-5, precision=prec)
+    assert np.array_equal(got, want)
+    # the same windows through the explain scan (pair list below 3000, expand/deep above)
+    dev.set_budgets([False, False], [0, 40])
+    res = dev.explain(masses, thr, 1e-5, prec, math.inf)
+    alph = oracle.Alphabet(ms, [False, False], [0, 40])
+    for i in range(len(masses)):
+        st, sols, n_empty, _ = oracle.explain_table(host, 32, alph, masses[i], thr[i], 1e-5, math.inf, precision=prec)
+        want_st = _native.SST_SOME if sols else (_native.SST_EMPTY if n_empty else _native.SST_NONE)
+        assert int(res.status[i]) == want_st, (i, masses[i], thr[i])
+        assert res.candidates(i) == sols, (i, masses[i], thr[i])
+    dev.close()
