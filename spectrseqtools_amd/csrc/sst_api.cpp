@@ -547,7 +547,7 @@ void sst_table_destroy(sst_table* t) {
 
 int sst_is_valid_batch_device(sst_table* t, const double* d_mass, const double* d_thr, int64_t n, double tol,
                               double prec, int8_t* d_out) {
-  if (!t || n < 0 || (n > 0 && (!d_mass || !d_out))) return SST_E_ARG;
+  if (!t || n < 0 || n > INT32_MAX || (n > 0 && (!d_mass || !d_out))) return SST_E_ARG;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
@@ -558,7 +558,7 @@ int sst_is_valid_batch_device(sst_table* t, const double* d_mass, const double* 
 
 int sst_is_valid_batch(sst_table* t, const double* mass, const double* thr, int64_t n, double tol, double prec,
                        int8_t* out) {
-  if (!t || n < 0 || (n > 0 && (!mass || !out))) return SST_E_ARG;
+  if (!t || n < 0 || n > INT32_MAX || (n > 0 && (!mass || !out))) return SST_E_ARG;
   if (n == 0) return SST_OK;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
