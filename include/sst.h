@@ -141,6 +141,20 @@ void sst_result_free(sst_result* r);
  * [7] payload bytes written by the pair-list path. */
 int sst_result_stats(const sst_result* r, uint64_t* stats_out /* [8] */);
 
+/* compute_sequence_length_bound (spectrseqtools/mass_table.py:343-487),
+ * batched over (su_mass, obs_mass) pairs: window = round(su/precision) +-
+ * ceil(tolerance*obs/precision); max_mods = round(seq.modification_rate *
+ * seq.max_len) (:351); per-row caps from sst_table_set_budgets; direction 0 =
+ * "lower", 1 = "upper", optionally | SST_LB_EXACT_ONLY.  out[i] = the bound; status[i]: 0 ok, SST_OUT_OF_TABLE
+ * (the reference raises NotImplementedError), SST_LB_EMPTY_WINDOW (its
+ * min([]) raises ValueError), SST_ABORTED (DFS node budget exhausted: no
+ * bound).  Synchronous, host buffers. */
+#define SST_LB_EMPTY_WINDOW (-5)
+#define SST_LB_EXACT_ONLY 2 /* direction flag: skip the layered fast path (tests) */
+int sst_length_bound_batch(sst_table* t, const double* su_mass, const double* obs_mass, int64_t n, double tolerance,
+                           double precision, int max_len, int64_t max_mods, int direction, int64_t* out,
+                           int8_t* status);
+
 /* ---- measurement ------------------------------------------------------ */
 /* Kernel ids for sst_profile_read. */
 #define SST_K_IS_VALID 0

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("SST_LIBRARY", os.path.join(_HERE, "libsstgpu.so"))
 # status codes (include/sst.h)
 SST_NONE, SST_EMPTY, SST_SOME = 0, 1, 2
 SST_OUT_OF_TABLE, SST_OVERFLOW, SST_ABORTED = -1, -2, -4
+SST_LB_EMPTY_WINDOW = -5
 
 # every function include/sst.h declares (checked by tests/test_boundary.py)
 EXPORTS = (
@@ -24,7 +25,7 @@ EXPORTS = (
     "sst_table_download", "sst_table_destroy", "sst_is_valid_batch", "sst_is_valid_batch_device",
     "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
-    "sst_profile_read",
+    "sst_profile_read", "sst_length_bound_batch",
 )
 
 # kernel ids of sst_profile_read
@@ -80,6 +81,7 @@ def load_library(path=LIB_PATH):
     lib.sst_profile_enable.argtypes = [_P, _I]
     lib.sst_profile_select.argtypes = [_P, ctypes.c_uint32]
     lib.sst_profile_read.argtypes = [_P, _P, _P]
+    lib.sst_length_bound_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _I, _I64, _I, _P, _P]
     return lib
 
 
@@ -317,6 +319,24 @@ class DeviceTable:
         self.engine.check(self.engine._lib.sst_is_valid_batch(self.handle, _ptr(m), _ptr(t), len(m), float(tolerance),
                                                               float(precision), _ptr(out)), "sst_is_valid_batch")
         return out
+
+    def length_bound(self, su_masses, obs_masses, tolerance, precision, max_len, max_mods, direction,
+                     exact_only=False):
+        """compute_sequence_length_bound for each (su, obs) pair: (bounds int64[n], status int8[n]).
+        exact_only: skip the layered fast path (cross-checks in tests)."""
+        su = np.ascontiguousarray(su_masses, dtype=np.float64)
+        ob = np.ascontiguousarray(obs_masses, dtype=np.float64)
+        if su.shape != ob.shape:
+            raise ValueError("su_masses and obs_masses differ in length")
+        out = np.zeros(len(su), np.int64)
+        st = np.zeros(len(su), np.int8)
+        d = {"lower": 0, "upper": 1}[direction] if isinstance(direction, str) else int(direction)
+        d |= 2 if exact_only else 0  # SST_LB_EXACT_ONLY
+        self.engine.check(self.engine._lib.sst_length_bound_batch(self.handle, _ptr(su), _ptr(ob), len(su),
+                                                                  float(tolerance), float(precision), int(max_len),
+                                                                  int(max_mods), d, _ptr(out), _ptr(st)),
+                          "sst_length_bound_batch")
+        return out, st
 
     def is_valid_device(self, d_mass, d_thr, n, tolerance, precision, d_out):
         self.engine.check(self.engine._lib.sst_is_valid_batch_device(self.handle, d_mass, d_thr, int(n),

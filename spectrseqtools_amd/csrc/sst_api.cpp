@@ -84,6 +84,7 @@ struct sst_table {
   std::vector<int64_t> cap;
   DevBuf packed, index, valid, w, capd, modd, pairs, pair_bucket;
   int scan_blocks = 0;  // resident workgroups of k_explain_scan (depends on the LDS pair list size)
+  bool closure = false;  // built here from masses >= C: rows are true closures (layered fast paths valid)
   TableArgs args{};
 };
 
@@ -256,6 +257,9 @@ int build_pair_list(sst_table* t, bool self_built) {
 }
 
 int finish_table(sst_table* t, bool self_built) {
+  t->closure = self_built;
+  for (int r = 1; r < t->n_rows; ++r)
+    if (t->masses[r] < t->C) t->closure = false;  // literal-sweep rows are not closures
   sst_ctx* c = t->ctx;
   const int64_t M = t->M;
   if (!t->index.ensure((size_t)M * sizeof(ulonglong2)) || !t->valid.ensure((size_t)((M + 63) / 64) * 8))
@@ -927,6 +931,105 @@ int sst_profile_read(sst_ctx* c, double* ms, int64_t* n) {
     c->prof_ms[i] = 0;
     c->prof_n[i] = 0;
   }
+  return SST_OK;
+}
+
+constexpr uint64_t kLBNodeBudget = 1ull << 24;  // length bound: per-query DFS nodes (single lane) before ABORTED
+constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses per lane (first attempt)
+
+int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, int64_t n, double tol, double prec,
+                           int max_len, int64_t max_mods, int direction, int64_t* out, int8_t* status) {
+  const bool exact_only = (direction & SST_LB_EXACT_ONLY) != 0;
+  direction &= ~SST_LB_EXACT_ONLY;
+  if (!t || n < 0 || n > INT32_MAX || (n > 0 && (!su || !obs || !out || !status)) || (direction != 0 && direction != 1) ||
+      max_len < 0 || max_len > 120)
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (n == 0) return SST_OK;
+  const size_t nn = (size_t)n;
+  DevBuf d_su, d_obs, d_out, d_st, d_list, d_cnt, layers;
+  if (!d_su.ensure(nn * 8) || !d_obs.ensure(nn * 8) || !d_out.ensure(nn * 8) || !d_st.ensure(nn) ||
+      !d_list.ensure(nn * 4) || !d_cnt.ensure(4))
+    return fail(c, SST_E_NOMEM, "device allocation failed (length bound)");
+  HIP_OK(c, hipMemcpyAsync(d_su.p, su, nn * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, hipMemcpyAsync(d_obs.p, obs, nn * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, hipMemsetAsync(d_cnt.p, 0, 4, c->stream));
+  LBArgs q{};
+  q.su = (const double*)d_su.p;
+  q.obs = (const double*)d_obs.p;
+  q.n = n;
+  q.tol = tol;
+  q.prec = prec;
+  q.rprec = 1.0 / prec;
+  q.A0 = (int)std::max<int64_t>(0, std::min<int64_t>(max_mods, kInfBudget));  // round(rate * max_len) >= 0
+  q.dir = direction;
+  q.max_len = max_len;
+  q.out = (int64_t*)d_out.p;
+  q.status = (int8_t*)d_st.p;
+  q.exact_list = (uint32_t*)d_list.p;
+  q.exact_count = (uint32_t*)d_cnt.p;
+  q.node_budget = kLBNodeBudget;
+  // fast path: layered reachability up to the largest window (a host-side
+  // over-estimate; the kernel re-checks hi < layer_limit exactly), kept below
+  // the reference's masked last column
+  if (t->closure && t->args.w_min > 0 && !exact_only) {
+    double hmax = 0;
+    for (int64_t i = 0; i < n; ++i) hmax = std::max(hmax, (su[i] + tol * std::fabs(obs[i])) / prec + 4.0);
+    const int64_t safe = (t->n_cols - 1) * t->C;
+    const int64_t lim = std::min<int64_t>(safe, (int64_t)std::min(hmax, (double)safe));
+    if (lim > 0) {
+      const int64_t words = (lim + 63) / 64;
+      const int n_layers = (int)(lim / t->args.w_min) + 2;
+      if (!layers.ensure((size_t)n_layers * words * 8)) return fail(c, SST_E_NOMEM, "device allocation failed (layers)");
+      uint64_t* L = (uint64_t*)layers.p;
+      const uint64_t one = 1;
+      HIP_OK(c, hipMemsetAsync(L, 0, (size_t)words * 8, c->stream));
+      HIP_OK(c, hipMemcpyAsync(L, &one, 8, hipMemcpyHostToDevice, c->stream));
+      for (int k = 0; k + 1 < n_layers; ++k)
+        HIP_OK(c, launch_layer_step(L + (size_t)k * words, L + (size_t)(k + 1) * words, words, t->args.w, t->n_rows,
+                                    c->stream));
+      q.layers = L;
+      q.layer_words = words;
+      q.n_layers = n_layers;
+      q.layer_limit = lim;
+    }
+  }
+  // fast kernel (queues the rest), then the exact kernel; retried with a
+  // larger per-lane memo while any query reports hash exhaustion
+  uint32_t n_exact = 0;
+  HIP_OK(c, launch_length_bound(t->args, q, nullptr, nullptr, nullptr, 0, 0, true, c->stream));
+  HIP_OK(c, hipMemcpyAsync(&n_exact, d_cnt.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  std::vector<int8_t> st(nn);
+  if (n_exact) {
+    uint32_t cap = kLBHashCap0;
+    int lanes = (int)std::min<uint32_t>(256, (n_exact + 63) / 64 * 64);
+    for (;;) {
+      DevBuf hash, vals, frames;
+      if (!hash.ensure((size_t)lanes * cap * hash_entry_bytes()) || !vals.ensure((size_t)lanes * cap * kMaxRows) ||
+          !frames.ensure((size_t)lanes * lb_frame_bytes()))
+        return fail(c, SST_E_NOMEM, "device allocation failed (length-bound memo)");
+      HIP_OK(c, hipMemsetAsync(hash.p, 0, hash.bytes, c->stream));
+      HIP_OK(c, launch_length_bound(t->args, q, (char*)hash.p, (int8_t*)vals.p, (char*)frames.p, cap, lanes, false,
+                                    c->stream));
+      HIP_OK(c, hipMemcpyAsync(st.data(), d_st.p, nn, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(c, hipStreamSynchronize(c->stream));
+      bool retry = false;
+      for (size_t i = 0; i < nn; ++i) retry |= st[i] == kStatusExactRetry;
+      if (!retry) break;
+      if (cap >= (1u << 25)) return fail(c, SST_E_INTERNAL, "length bound: memo exceeds 2^25 masses");
+      cap *= 8;
+      lanes = std::max(64, lanes / 8);
+    }
+  }
+  HIP_OK(c, hipMemcpyAsync(out, d_out.p, nn * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipMemcpyAsync(status, d_st.p, nn, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < nn; ++i)
+    if (status[i] == kStatusPending || status[i] == kStatusExactRetry)
+      return fail(c, SST_E_INTERNAL, "length bound: query left unresolved (internal error)");
   return SST_OK;
 }
 

@@ -25,6 +25,7 @@ enum { kClassShallow = 0, kClassDeep = 1, kClassExact = 2, kClassNomemo = 3, kNu
 constexpr int kStatusPending = -10;
 constexpr int kStatusArenaRetry = -11;
 constexpr int kStatusExactRetry = -12;
+constexpr int kLBEmptyWindow = -5;  // length bound: empty window (the reference's min([]) raises ValueError)
 
 enum {
   kStatShallow = 0,
@@ -112,6 +113,25 @@ struct OutArgs {
   unsigned long long* stats;  // [kNumStats] deferred-kernel counters
 };
 
+struct LBArgs {
+  const double* su;
+  const double* obs;
+  int64_t n;
+  double tol, prec, rprec;
+  int A0;         // round(seq.modification_rate * seq.max_len)
+  int dir;        // 0 lower, 1 upper
+  int max_len;
+  int64_t* out;
+  int8_t* status;
+  uint32_t* exact_list;
+  uint32_t* exact_count;
+  const uint64_t* layers;  // [n_layers][layer_words]; null: no fast path
+  int64_t layer_words;
+  int n_layers;
+  int64_t layer_limit;     // layers cover masses [0, layer_limit)
+  uint64_t node_budget;
+};
+
 struct ExactWs {
   char* hash;
   char* frames;
@@ -145,6 +165,11 @@ hipError_t launch_explain_deep(const TableArgs& t, const QueryArgs& q, const Out
 hipError_t launch_explain_exact(const TableArgs& t, const QueryArgs& q, const OutArgs& o, const ExactWs& ws,
                                 int n_blocks, hipStream_t st);
 size_t glob_frame_bytes();
+hipError_t launch_layer_step(const uint64_t* prev, uint64_t* next, int64_t nwords, const int* w, int n_rows,
+                             hipStream_t st);
+hipError_t launch_length_bound(const TableArgs& t, const LBArgs& q, char* hash, int8_t* vals, char* frames,
+                               uint32_t hash_cap, int exact_lanes, bool fast_pass, hipStream_t st);
+size_t lb_frame_bytes();
 size_t p1_frame_bytes();
 size_t hash_entry_bytes();
 

@@ -522,6 +522,7 @@ struct Hash {
         ++used;
         e[i].key = key;
         e[i].meta = 0xFFFFu;
+        e[i].pad = 0;
         e[i].en0 = 0;
         e[i].en1 = 0;
         return &e[i];
@@ -1408,6 +1409,206 @@ __global__ __launch_bounds__(64) void k_explain_exact(TableArgs t, QueryArgs q, 
 }
 
 // ---------------------------------------------------------------------------
+// compute_sequence_length_bound (mass_table.py:343-487), batched.
+//
+// The reference's backtrack has the explain DFS's visit order, memo key
+// (m, row) and budget flow exactly (up: B = cap[row-1]; left on a mod row:
+// A-1, B-1 when A > 0 and B > 0), so the first-visit state per mass is the
+// exact path's phase 1 (hv, enabled-left mask).  A node's memoised value is
+//   value(m, r) = combine(default, value(m, r-1) [r > lo],
+//                         value(m - w_r, r) + 1 [left enabled at first visit])
+// = combine over rows s in [lo, r] of the enabled left contributions,
+// combine = min (lower, default max_len+1) or max (upper, default -1).
+//
+// Fast path (budgets provably never bind, fast-path theorem): value(v, top)
+// is the min / max item count of a multiset summing to v, i.e. the min / max
+// k with v in L_k, where L_0 = {0}, L_{k+1} = U_r (L_k + w_r) -- layered
+// bitsets built per call, one lane per query.
+// ---------------------------------------------------------------------------
+// L_{k+1} from L_k: one output word per thread, OR over the rows' shifts
+__global__ void k_layer_step(const uint64_t* __restrict__ prev, uint64_t* __restrict__ next, int64_t nwords,
+                             const int* __restrict__ w, int n_rows) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nwords) return;
+  uint64_t acc = 0;
+  for (int r = 1; r < n_rows; ++r) {
+    const int64_t q = w[r] >> 6;
+    const int sh = w[r] & 63;
+    const int64_t jj = j - q;
+    if (jj < 0) continue;
+    uint64_t x = prev[jj] << sh;
+    if (sh && jj > 0) x |= prev[jj - 1] >> (64 - sh);
+    acc |= x;
+  }
+  next[j] = acc;
+}
+
+__device__ __forceinline__ int lb_combine(int dir, int x, int y) { return dir ? (x > y ? x : y) : (x < y ? x : y); }
+
+// value arrays of the exact path: per hash slot, one int8 per row
+struct LBFrame {
+  HEntry* e;
+  uint32_t m;
+  int acc;
+  uint8_t s, lo, hv, pad;
+};
+
+// values of mass `root` (and every descendant it needs); 0 ok, -2 depth
+__device__ int lb_values(const TableArgs& t, const Lds& s, const Hash& h, int8_t* vals, LBFrame* fr, HEntry* root_e,
+                         uint32_t root, int dir, int dflt) {
+  int d = 0;
+  auto init = [&](LBFrame& f, HEntry* e, uint32_t m) {
+    f.e = e;
+    f.m = m;
+    f.acc = dflt;
+    f.lo = (uint8_t)rec_lo(ld_index(t.index, m));
+    f.hv = (uint8_t)(e->meta & 0xFF);
+    f.s = f.lo;
+  };
+  init(fr[0], root_e, root);
+  while (d >= 0) {
+    LBFrame& f = fr[d];
+    int8_t* fv = vals + (size_t)(f.e - h.e) * kMaxRows;
+    bool pushed = false;
+    while (f.s <= f.hv) {
+      const int r = f.s;
+      if (mtest(M128{f.e->en0, f.e->en1}, r)) {
+        const uint32_t c = f.m - (uint32_t)s.w[r];
+        int cv;
+        if (c == 0) {
+          cv = 0;  // total_mass == 0 -> 0 (mass_table.py:378-379)
+        } else {
+          HEntry* ce = h.find(c);  // visited by phase 1 (the edge was taken)
+          if (!ce) return -3;      // cannot happen for a consistent table; never dereference
+          if (ce->pad == 0) {
+            if (d + 1 >= kMaxDepth) return -2;
+            init(fr[d + 1], ce, c);
+            ++d;
+            pushed = true;
+            break;
+          }
+          cv = vals[(size_t)(ce - h.e) * kMaxRows + r];
+        }
+        f.acc = lb_combine(dir, f.acc, cv + 1);
+      }
+      fv[r] = (int8_t)f.acc;  // combine(default, rows lo..r)
+      f.s = (uint8_t)(r + 1);
+    }
+    if (pushed) continue;
+    f.e->pad = 1;  // values computed
+    --d;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ bool lb_window(const LBArgs& q, int64_t i, int64_t& lo, int64_t& hi) {
+  const double obs = q.obs[i];
+  quantise(q.su[i], q.tol * obs, false, q.tol, q.prec, q.rprec, lo, hi);  // mass_table.py:354-359
+  return lo <= hi;
+}
+
+__device__ __forceinline__ int64_t lb_finish(const LBArgs& q, int best) {
+  // mass_table.py:476-484: the default bound becomes 1 (lower) / max_len (upper)
+  if (q.dir == 0) return best >= q.max_len + 1 ? 1 : best;
+  return best == -1 ? q.max_len : best;
+}
+
+__global__ __launch_bounds__(256) void k_length_fast(TableArgs t, LBArgs q) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= q.n) return;
+  int64_t lo, hi;
+  if (!lb_window(q, i, lo, hi)) {
+    q.status[i] = (int8_t)kLBEmptyWindow;  // min([]) raises ValueError
+    return;
+  }
+  if (hi >= t.limit) {
+    q.status[i] = SST_OUT_OF_TABLE;  // NotImplementedError (mass_table.py:383-387)
+    return;
+  }
+  const int64_t a = lo < 0 ? 0 : lo;
+  const bool fast = q.layers && hi < q.layer_limit && budgets_never_bind(t, hi, q.A0);
+  if (!fast) {
+    const uint32_t slot = atomicAdd(q.exact_count, 1u);
+    q.exact_list[slot] = (uint32_t)i;
+    q.status[i] = (int8_t)kStatusPending;
+    return;
+  }
+  const int dflt = q.dir ? -1 : q.max_len + 1;
+  int best = dflt;
+  if (a <= hi) {
+    for (int k = 0; k < q.n_layers; ++k) {
+      if (any_bits(q.layers + (int64_t)k * q.layer_words, a, hi)) {
+        if (q.dir == 0) {
+          best = k < best ? k : best;
+          break;
+        }
+        best = k;
+      }
+    }
+  }
+  q.out[i] = lb_finish(q, best);
+  q.status[i] = 0;
+}
+
+// one lane per queued query: phase 1 (first visits) + value DP; per-lane hash
+// slice and value slice, fresh (zeroed) workspace per launch
+__global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char* hash, int8_t* vals, char* frames,
+                                                     uint32_t hash_cap) {
+  __shared__ Lds s;
+  const uint32_t n_list = *q.exact_count;
+  if (n_list == 0) return;
+  stage_rows(s, t);
+  const int64_t gid = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * 64;
+  P1Frame* fr = (P1Frame*)(frames + gid * kMaxDepth * (sizeof(P1Frame) + sizeof(LBFrame)));
+  LBFrame* lf = (LBFrame*)(fr + kMaxDepth);
+  Hash h;
+  h.e = (HEntry*)(hash + (size_t)gid * hash_cap * sizeof(HEntry));
+  h.mask = hash_cap - 1;
+  h.limit = (uint32_t)(hash_cap * 0.7);
+  int8_t* lv = vals + (size_t)gid * hash_cap * kMaxRows;
+  uint64_t epoch = 0;
+  const int top = t.n_rows - 1;
+  for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
+    const int64_t i = q.exact_list[j];
+    int64_t lo, hi;
+    lb_window(q, i, lo, hi);
+    h.epoch = ++epoch;  // the workspace was zeroed: epochs 1, 2, ... are fresh
+    h.used = 0;
+    uint64_t nodes = 0;
+    const int64_t a = lo < 1 ? 1 : lo;
+    int rc = phase1(t, s, h, fr, a, hi, q.A0, q.node_budget, nodes);
+    if (rc == -1) {
+      q.status[i] = (int8_t)kStatusExactRetry;
+      continue;
+    }
+    if (rc < 0) {
+      q.status[i] = SST_ABORTED;
+      continue;
+    }
+    const int dflt = q.dir ? -1 : q.max_len + 1;
+    int best = dflt;
+    if (lo <= 0 && hi >= 0) best = lb_combine(q.dir, best, 0);  // total_mass == 0 -> 0
+    for (int64_t v = a; v <= hi && rc == 0; ++v) {
+      if (!((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;  // pair(top, v) == 0: default
+      HEntry* e = h.find((uint32_t)v);
+      if (!e) {
+        rc = -3;
+        break;
+      }
+      if (e->pad == 0) rc = lb_values(t, s, h, lv, lf, e, (uint32_t)v, q.dir, dflt);
+      if (rc == 0) best = lb_combine(q.dir, best, lv[(size_t)(e - h.e) * kMaxRows + top]);
+    }
+    if (rc < 0) {
+      q.status[i] = SST_ABORTED;
+      continue;
+    }
+    q.out[i] = lb_finish(q, best);
+    q.status[i] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host-side launchers (C++ linkage, used by sst_api.cpp)
 // ---------------------------------------------------------------------------
 static inline unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + per - 1) / per); }
@@ -1528,4 +1729,20 @@ size_t glob_frame_bytes() { return sizeof(GlobFrame); }
 size_t p1_frame_bytes() { return sizeof(P1Frame); }
 size_t hash_entry_bytes() { return sizeof(HEntry); }
 
+hipError_t launch_layer_step(const uint64_t* prev, uint64_t* next, int64_t nwords, const int* w, int n_rows,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_layer_step, dim3(blocks_for(nwords, 256)), dim3(256), 0, st, prev, next, nwords, w, n_rows);
+  return hipGetLastError();
+}
+hipError_t launch_length_bound(const TableArgs& t, const LBArgs& q, char* hash, int8_t* vals, char* frames,
+                               uint32_t hash_cap, int exact_lanes, bool fast_pass, hipStream_t st) {
+  if (q.n <= 0) return hipSuccess;
+  if (fast_pass) hipLaunchKernelGGL(k_length_fast, dim3(blocks_for(q.n, 256)), dim3(256), 0, st, t, q);
+  if (exact_lanes >= 64)
+    hipLaunchKernelGGL(k_length_exact, dim3(exact_lanes / 64), dim3(64), 0, st, t, q, hash, vals, frames, hash_cap);
+  return hipGetLastError();
+}
+size_t lb_frame_bytes() { return kMaxDepth * (sizeof(P1Frame) + sizeof(LBFrame)); }
+
 }  // namespace sst
+

@@ -231,9 +231,32 @@ def load_dp_table(table_path, integer_masses, engine=None):
 
 
 def compute_sequence_length_bound(dp_table: DynamicProgrammingTable, dir: str) -> int:
-    """mass_table.py:343-487 (GPU implementation pending)."""
+    """Return bound on length for any sequence that could explain the given mass
+    (mass_table.py:343-487), on the GPU: the reference's memoised backtrack --
+    same first-visit budgets, same defaults and quirks -- see DESIGN.md."""
     if dir not in ("lower", "upper"):
         raise NotImplementedError(f"Support for '{dir}' is currently not given.")
-    from .length_bound import sequence_length_bound
+    seq = dp_table.seq
+    out = compute_sequence_length_bounds(dp_table, [seq.su_mass], [seq.obs_mass], dir)
+    return int(out[0])
 
-    return sequence_length_bound(dp_table, dir)
+
+def compute_sequence_length_bounds(dp_table: DynamicProgrammingTable, su_masses, obs_masses, dir: str):
+    """Batched compute_sequence_length_bound over (su_mass, obs_mass) pairs that
+    share dp_table.seq's max_len / modification_rate (one launch)."""
+    if dir not in ("lower", "upper"):
+        raise NotImplementedError(f"Support for '{dir}' is currently not given.")
+    seq = dp_table.seq
+    max_mods = round(seq.modification_rate * seq.max_len)  # mass_table.py:351
+    vals, st = dp_table.device_table.length_bound(su_masses, obs_masses, dp_table.tolerance, dp_table.precision,
+                                                  seq.max_len, max_mods, dir)
+    bad = np.flatnonzero(st != 0)
+    if len(bad):
+        s = int(st[bad[0]])
+        if s == _native.SST_OUT_OF_TABLE:
+            raise NotImplementedError("The value is not in the DP table. Extend its size if you want to compute "
+                                      "larger masses.")
+        if s == _native.SST_LB_EMPTY_WINDOW:
+            raise ValueError("min() arg is an empty sequence")
+        raise RuntimeError(f"length bound aborted: DFS node budget exhausted (status {s})")
+    return vals
