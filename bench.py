@@ -9,9 +9,12 @@ spectra (10k spectra, ~1M peaks, full 104-mass /
   * A8: explain_mass_with_table for every adjacent SU-mass difference the
         reference's sliding window emits (prediction.py:286-329), budget
         round(0.5*max_len)                  -> k_explain_main (+ deferred kernels)
-  * N>1: per-rank results gathered to rank 0 over RCCL.
-value = peaks of all ranks / step time (max over ranks).  Spectra shard by
-rank (weak scaling: `--spectra` per GPU).
+  * N>1: spectra shard by rank (weak scaling: `--spectra` per GPU); each
+        rank's results are complete for its own spectra and stay in its HBM
+        (no data-path collective in the step).  --gather adds delivery of
+        every query's result (status, count, offset, dense payload) to rank 0
+        over RCCL, timed inside the step.
+value = peaks of all ranks / step time (max over ranks).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--spectra S]
        (N>1 under torch.distributed.run, one rank per GPU)
@@ -134,6 +137,8 @@ def main():
     ap.add_argument("--spectra", type=int, default=10000, help="spectra per GPU")
     ap.add_argument("--seed", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="N>1: gather every query's result to rank 0 over RCCL inside the timed step")
     ap.add_argument("--no-events", action="store_true",
                     help="diagnostic: time the steps without the per-kernel HIP events (no roofline)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"),
@@ -175,17 +180,17 @@ def main():
     ext = torch.cuda.ExternalStream(engine.stream, device=dev_t)
 
     res = None
-    gath = Gatherer(dist, dev_t) if dist else None
+    gath = Gatherer(dist, dev_t) if (dist and args.gather) else None
 
     def step():
         nonlocal res
         tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, out7.data_ptr())
         res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=res)
         if gath is not None:
-            torch.cuda.current_stream().wait_stream(ext)
-            st, cnt, _off, pay, _cap = res.device_views()
+            st, cnt, off, pay, _cap = res.device_views()  # queues the compaction: offsets index the dense payload
+            torch.cuda.current_stream().wait_stream(ext)  # after the compaction, before torch reads the buffers
             flat = torch.cat([out7.view(torch.uint8), device_bytes(st, n8, dev_t), device_bytes(cnt, 8 * n8, dev_t),
-                              device_bytes(pay, payload_bytes, dev_t)])
+                              device_bytes(off, 8 * n8, dev_t), device_bytes(pay, payload_bytes, dev_t)])
             gath.gather(flat)
 
     # untimed sizing pass: results are deterministic per rank, so the gather
@@ -196,7 +201,7 @@ def main():
     res.fetch_device()
     payload_bytes = int(len(res.payload))
     if gath is not None:
-        gath.agree(n7 + 9 * n8 + payload_bytes)
+        gath.agree(n7 + 17 * n8 + payload_bytes)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -315,7 +320,9 @@ def main():
             "a8_queries": n8_all,
             "max_len": seq.max_len,
             "max_modifications": A,
-            "parallelism": f"spectra sharded over {world} GPU(s), RCCL gather to rank 0" if world > 1 else "1 GPU",
+            "parallelism": (f"spectra sharded over {world} GPUs, results kept per rank"
+                            + (", RCCL gather of all results to rank 0 in the step" if args.gather else "")
+                            if world > 1 else "1 GPU"),
         },
         "roofline": {
             "bound": "hbm",

@@ -117,6 +117,18 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
                              double tolerance, double precision, const int64_t* d_max_mods, int64_t max_mods_scalar,
                              int with_memo, uint64_t cap_per_query, sst_result** out);
 
+/* explain_mass_with_recursion (mass_explanation.py:206-284), batched: the
+ * table-free enumerator (target = round(mass/precision), base case
+ * |remaining| <= thr at every level, memo keyed (remaining, start) with the
+ * first visit's list, per-row caps from sst_table_set_budgets).  max_mods:
+ * per-query array or scalar; negative = np.inf; a fractional reference budget
+ * is passed floored.  Results as for sst_explain_batch (status, count,
+ * offset, payload of ascending row indices); SST_ABORTED when a query
+ * exhausts the DFS node budget.  Synchronous. */
+int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* thr_abs, int64_t n,
+                                double tolerance, double precision, const int64_t* max_mods, int64_t max_mods_scalar,
+                                uint64_t cap_per_query, sst_result** out);
+
 /* Host views of a result (valid until sst_result_free):
  *   status[n] (SST_NONE..), count[n] candidates, offset[n] byte offset of the
  *   query's candidates in payload; payload = per candidate one length byte k

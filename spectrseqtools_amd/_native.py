@@ -25,7 +25,7 @@ EXPORTS = (
     "sst_table_download", "sst_table_destroy", "sst_is_valid_batch", "sst_is_valid_batch_device",
     "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
-    "sst_profile_read", "sst_length_bound_batch",
+    "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch",
 )
 
 # kernel ids of sst_profile_read
@@ -82,6 +82,7 @@ def load_library(path=LIB_PATH):
     lib.sst_profile_select.argtypes = [_P, ctypes.c_uint32]
     lib.sst_profile_read.argtypes = [_P, _P, _P]
     lib.sst_length_bound_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _I, _I64, _I, _P, _P]
+    lib.sst_explain_recursion_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _U64, _PP]
     return lib
 
 
@@ -352,6 +353,19 @@ class DeviceTable:
                                                              float(precision), _ptr(mods_arr), scalar,
                                                              int(bool(with_memo)), int(cap), ctypes.byref(h)),
                           "sst_explain_batch")
+        return ExplainResult(self.engine, h, len(m)).fetch()
+
+    def explain_recursion(self, masses, thresholds, tolerance, precision, max_mods, cap=2 ** 32):
+        """explain_mass_with_recursion, batched; max_mods: np.inf / non-negative integers (scalar or per mass)."""
+        m = np.ascontiguousarray(masses, dtype=np.float64)
+        t = None if thresholds is None else np.ascontiguousarray(thresholds, dtype=np.float64)
+        mods_arr, scalar = _mods(max_mods, len(m))
+        h = ctypes.c_void_p()
+        self.engine.check(self.engine._lib.sst_explain_recursion_batch(self.handle, _ptr(m), _ptr(t), len(m),
+                                                                       float(tolerance), float(precision),
+                                                                       _ptr(mods_arr), scalar, int(cap),
+                                                                       ctypes.byref(h)),
+                          "sst_explain_recursion_batch")
         return ExplainResult(self.engine, h, len(m)).fetch()
 
     def explain_device(self, d_mass, d_thr, n, tolerance, precision, max_mods_scalar, d_mods=None, with_memo=True,

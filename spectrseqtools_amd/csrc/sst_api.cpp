@@ -484,7 +484,7 @@ int sst_table_set_budgets(sst_table* t, const uint8_t* is_mod, const int64_t* ca
   t->is_mod.assign(is_mod, is_mod + N);
   t->cap.assign(cap, cap + N);
   std::vector<int> cap32(N);
-  uint64_t mod0 = 0, mod1 = 0, cz0 = 0, cz1 = 0;
+  uint64_t mod0 = 0, mod1 = 0, cz0 = 0, cz1 = 0, cn0 = 0, cn1 = 0;
   int any_mod = 0;
   int64_t wmm = 0, lim = INT64_MAX;
   for (int r = 0; r < N; ++r) {
@@ -503,6 +503,7 @@ int sst_table_set_budgets(sst_table* t, const uint8_t* is_mod, const int64_t* ca
       lim = std::min(lim, l);
     }
     if (cp <= 0) (r < 64 ? cz0 : cz1) |= 1ull << (r & 63);
+    if (cp < 0) (r < 64 ? cn0 : cn1) |= 1ull << (r & 63);
   }
   if (!t->capd.ensure(N * sizeof(int)) || !t->modd.ensure(N)) return fail(c, SST_E_NOMEM, "device allocation failed");
   HIP_OK(c, hipMemcpy(t->capd.p, cap32.data(), N * sizeof(int), hipMemcpyHostToDevice));
@@ -513,6 +514,8 @@ int sst_table_set_budgets(sst_table* t, const uint8_t* is_mod, const int64_t* ca
   t->args.mod1 = mod1;
   t->args.capz0 = cz0;
   t->args.capz1 = cz1;
+  t->args.capneg0 = cn0;
+  t->args.capneg1 = cn1;
   t->args.any_mod = any_mod;
   t->args.w_min_mod = (int)(wmm > 0 ? wmm : 1);
   t->args.fast_limit_B = lim;
@@ -587,6 +590,10 @@ constexpr int kDeepBlocks = 256;        // persistent grid of the deep / no-memo
 constexpr uint32_t kHashCap0 = 1u << 14;  // exact-path hash entries per lane (first attempt)
 constexpr int kExactLanes0 = 2048;      // exact-path concurrent lanes (first attempt)
 constexpr uint64_t kNodeBudget = 1ull << 32;
+constexpr uint64_t kRecNodeBudget = 1ull << 24;  // explain_recursion: per-query DFS nodes before ABORTED
+constexpr uint32_t kRecHashCap0 = 1u << 16;       // explain_recursion: memo nodes per lane (first attempt)
+constexpr uint64_t kLBNodeBudget = 1ull << 24;  // length bound: per-query DFS nodes (single lane) before ABORTED
+constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses per lane (first attempt)
 
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->count, &r->offset, &r->payload, &r->ctl, &r->lists,
@@ -858,6 +865,85 @@ int sst_explain_batch(sst_table* t, const double* mass, const double* thr, int64
   return SST_OK;
 }
 
+int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* thr, int64_t n, double tol,
+                                double prec, const int64_t* mods, int64_t mods_scalar, uint64_t cap_count,
+                                sst_result** out) {
+  if (!t || !out || n < 0 || n > INT32_MAX || (n > 0 && !mass)) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  *out = nullptr;
+  if (int rc = set_device(c)) return rc;
+  const size_t nn = (size_t)std::max<int64_t>(n, 1);
+  if (!c->in_mass.ensure(nn * 8) || (thr && !c->in_thr.ensure(nn * 8)) || (mods && !c->in_mods.ensure(nn * 8)))
+    return fail(c, SST_E_NOMEM, "device allocation failed (staging)");
+  if (n) {
+    HIP_OK(c, hipMemcpyAsync(c->in_mass.p, mass, n * 8, hipMemcpyHostToDevice, c->stream));
+    if (thr) HIP_OK(c, hipMemcpyAsync(c->in_thr.p, thr, n * 8, hipMemcpyHostToDevice, c->stream));
+    if (mods) HIP_OK(c, hipMemcpyAsync(c->in_mods.p, mods, n * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  sst_result* r = nullptr;
+  if (int rc = alloc_result(t, n, &r)) return rc;
+  // only the spill area is used: every region is empty for the compaction
+  HIP_OK(c, hipMemsetAsync(r->wave_used.p, 0, r->wave_used.bytes, c->stream));
+  HIP_OK(c, hipMemsetAsync(r->wave_stats.p, 0, r->wave_stats.bytes, c->stream));
+  QueryArgs q{(const double*)c->in_mass.p, thr ? (const double*)c->in_thr.p : nullptr,
+              mods ? (const int64_t*)c->in_mods.p : nullptr, mods_scalar, n, tol, prec, 1.0 / prec, 1, cap_count,
+              kRecNodeBudget};
+  uint32_t cap = kRecHashCap0;
+  int lanes = (int)std::min<int64_t>(256, (n + 63) / 64 * 64);
+  int rc = SST_OK;
+  for (int attempt = 0; n > 0; ++attempt) {
+    if (attempt == 8) {
+      rc = fail(c, SST_E_INTERNAL, "explain_recursion: retries exhausted");
+      break;
+    }
+    r->arena_bytes = (uint64_t)r->n_regions * r->region_bytes + r->spill_bytes;
+    DevBuf hash, frames;
+    if (!r->ctl.ensure(2 * kCtlWords * 8) || !r->payload.ensure(r->arena_bytes) ||
+        !hash.ensure((size_t)lanes * cap * rec_entry_bytes()) || !frames.ensure((size_t)lanes * rec_frame_bytes())) {
+      rc = fail(c, SST_E_NOMEM, "device allocation failed (recursion)");
+      break;
+    }
+    r->parity = 0;  // one pass per attempt: block 0, zeroed here
+    r->ctl_ready = true;
+    HIP_OK(c, hipMemsetAsync(r->ctl.p, 0, 2 * kCtlWords * 8, c->stream));
+    HIP_OK(c, hipMemsetAsync(hash.p, 0, hash.bytes, c->stream));
+    r->compacted = false;
+    HIP_OK(c, launch_explain_recursion(t->args, q, out_args(r), (char*)hash.p, (char*)frames.p, cap, lanes,
+                                       c->stream));
+    if ((rc = fetch(r))) break;
+    bool arena_retry = false, memo_retry = false;
+    for (int64_t i = 0; i < n; ++i) {
+      arena_retry |= r->h_status[i] == kStatusArenaRetry;
+      memo_retry |= r->h_status[i] == kStatusExactRetry;
+    }
+    if (!arena_retry && !memo_retry) break;
+    if (arena_retry) {
+      uint64_t cur = 0;
+      HIP_OK(c, hipMemcpy(&cur, ctl_block(r, r->parity), 8, hipMemcpyDeviceToHost));
+      r->spill_bytes = std::max<uint64_t>(2 * r->spill_bytes, cur + (1u << 20));
+      r->payload.release();
+      r->dense.release();
+    }
+    if (memo_retry) {
+      if (cap >= (1u << 26)) {
+        rc = fail(c, SST_E_INTERNAL, "explain_recursion: memo exceeds 2^26 nodes");
+        break;
+      }
+      cap *= 8;
+      lanes = std::max(64, lanes / 8);
+    }
+  }
+  if (!rc && n == 0) rc = fetch(r);
+  if (rc) {
+    free_result_bufs(r);
+    delete r;
+    return rc;
+  }
+  *out = r;
+  return SST_OK;
+}
+
 int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count, const uint64_t** offset,
                     const uint8_t** payload, uint64_t* payload_bytes) {
   if (!r) return SST_E_ARG;
@@ -934,8 +1020,6 @@ int sst_profile_read(sst_ctx* c, double* ms, int64_t* n) {
   return SST_OK;
 }
 
-constexpr uint64_t kLBNodeBudget = 1ull << 24;  // length bound: per-query DFS nodes (single lane) before ABORTED
-constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses per lane (first attempt)
 
 int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, int64_t n, double tol, double prec,
                            int max_len, int64_t max_mods, int direction, int64_t* out, int8_t* status) {

@@ -48,6 +48,7 @@ struct TableArgs {
   const uint8_t* mod;       // [n_rows] is_modification
   uint64_t mod0, mod1;      // row masks of modification rows
   uint64_t capz0, capz1;    // row masks with cap <= 0
+  uint64_t capneg0, capneg1;  // row masks with cap < 0
   int64_t fast_limit_B;     // max window value for which no per-row cap can bind
   int64_t shallow_hi;       // window values < shallow_hi (= 4 * w_min) fit in <= 3 items
   // LDS pair list: every 1- and 2-item sum of the alphabet, sorted by
@@ -170,6 +171,10 @@ hipError_t launch_layer_step(const uint64_t* prev, uint64_t* next, int64_t nword
 hipError_t launch_length_bound(const TableArgs& t, const LBArgs& q, char* hash, int8_t* vals, char* frames,
                                uint32_t hash_cap, int exact_lanes, bool fast_pass, hipStream_t st);
 size_t lb_frame_bytes();
+hipError_t launch_explain_recursion(const TableArgs& t, const QueryArgs& q, const OutArgs& o, char* hash,
+                                   char* frames, uint32_t hash_cap, int lanes, hipStream_t st);
+size_t rec_frame_bytes();
+size_t rec_entry_bytes();
 size_t p1_frame_bytes();
 size_t hash_entry_bytes();
 

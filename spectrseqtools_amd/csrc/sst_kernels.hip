@@ -498,6 +498,7 @@ struct Hash {
   uint64_t epoch;
   uint32_t used;
   uint32_t limit;
+  uint64_t sink = 0;  // folds prefetch loads (see p1_visit)
   __device__ __forceinline__ uint32_t slot(uint32_t m) const { return (m * 0x9E3779B1u) & mask; }
   // returns entry pointer or nullptr if absent
   __device__ __forceinline__ HEntry* find(uint32_t m) const {
@@ -725,11 +726,13 @@ struct P1Frame {
   uint8_t rtop, rnext, pad0, pad1;
 };
 
-// visit (m, r, A, B): returns 1 if a frame was pushed, 0 otherwise (memo hit
-// or pair == 0); *ne_child receives the child's "non-empty at row r" verdict
-// for the non-pushed case.  -1 on hash exhaustion.
-__device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int& d, uint32_t m,
-                                        int r, int A, int B, bool& nonempty, uint64_t& nodes) {
+// visit (m, r, A, B): returns 1 if (m, r) is a first visit (its newly
+// visited rows' enabled-left mask in *en, its memo entry in *ent: the caller
+// makes it the current frame), 0 otherwise (memo hit or pair == 0; *nonempty
+// = the child's "non-empty at row r" verdict), -1 on hash exhaustion.
+// Memo entry meta: hv (bits 0-7), ne (8-15), lo (16-23).
+__device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& h, uint32_t m, int r, int A, int B,
+                                        bool& nonempty, uint64_t& nodes, M128& en_out, HEntry*& ent) {
   ulonglong2 rec = ld_index(t.index, m);
   nodes++;
   int lo = rec_lo(rec);
@@ -769,69 +772,94 @@ __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& 
   }
   e->en0 |= en.a;
   e->en1 |= en.b;
-  e->meta = (e->meta & 0xFF00u) | (uint32_t)r;
-  ++d;
-  P1Frame& f = fr[d];
-  f.en0 = en.a;
-  f.en1 = en.b;
-  f.e = e;
-  f.m = m;
-  f.A = A;
-  f.B = B;
-  f.rtop = (uint8_t)r;
-  f.rnext = (uint8_t)rlo;
+  e->meta = (e->meta & 0xFF00u) | ((uint32_t)lo << 16) | (uint32_t)r;
+  // the frame will visit (m - w_rr, rr) for every enabled row: issue their
+  // index-record and first-probe loads now, independently, so the visits
+  // that follow hit the cache instead of paying dependent HBM round trips
+  for (M128 k = en; !mzero(k);) {
+    const int rr = mlow(k);
+    k = mclear(k, rr);
+    const int64_t c = (int64_t)m - s.w[rr];
+    if (c > 0) h.sink ^= __builtin_nontemporal_load(&t.index[c].y) ^ h.e[h.slot((uint32_t)c)].key;
+  }
+  en_out = en;
+  ent = e;
   return 1;
 }
 
-// returns 0 ok, -1 hash full, -2 depth, -3 node budget
-__device__ int phase1(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
-                      uint64_t node_budget, uint64_t& nodes) {
+__device__ __forceinline__ void p1_set_ne(HEntry* e, int rr) {  // lowest non-empty row (first found wins)
+  if (((e->meta >> 8) & 0xFF) == 0xFF) e->meta = (e->meta & ~0xFF00u) | ((uint32_t)rr << 8);
+}
+
+// returns 0 ok, -1 hash full, -2 depth, -3 node budget.  The current frame
+// lives in registers; fr[] holds only the saved ancestors (touched on push
+// and pop, not per row).
+__device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
+                           uint64_t node_budget, uint64_t& nodes) {
   const int top = t.n_rows - 1;
   for (int64_t v = a; v <= b; ++v) {
     if (!((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;
-    int d = -1;
     bool ne_dummy;
-    int pr = p1_visit(t, s, h, fr, d, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes);
+    M128 rest;
+    HEntry* e;
+    int pr = p1_visit(t, s, h, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes, rest, e);
     if (pr < 0) return -1;
-    while (d >= 0) {
-      P1Frame& f = fr[d];
-      M128 rem = mand(M128{f.en0, f.en1}, rows_from(f.rnext));
-      if (mzero(rem)) {
-        // frame done; report to parent: parent's pending row = parent.rnext - 1
-        HEntry* ce = f.e;
-        --d;
-        if (d >= 0) {
-          P1Frame& p = fr[d];
-          int rr = p.rnext - 1;
-          int ne = (int)((ce->meta >> 8) & 0xFF);
-          if (ne != 0xFF && rr >= ne) {
-            if (((p.e->meta >> 8) & 0xFF) == 0xFF) p.e->meta = (p.e->meta & 0xFFu) | ((uint32_t)rr << 8);
-          }
-        }
+    if (pr == 0) continue;
+    uint32_t m = (uint32_t)v;
+    int A = A0, B = s.cap[top], rtop = top, d = 0;
+    for (;;) {
+      if (mzero(rest)) {  // frame done: report to the parent (its pending row)
+        if (d == 0) break;
+        HEntry* ce = e;
+        const P1Frame f = fr[--d];
+        rest = M128{f.en0, f.en1};
+        e = f.e;
+        m = f.m;
+        A = f.A;
+        B = f.B;
+        rtop = f.rtop;
+        const int rr = f.rnext - 1;
+        const int ne = (int)((ce->meta >> 8) & 0xFF);
+        if (ne != 0xFF && rr >= ne) p1_set_ne(e, rr);
         continue;
       }
-      int rr = mlow(rem);
-      f.rnext = (uint8_t)(rr + 1);
-      int md = s.mod[rr];
-      int Bv = (rr == f.rtop) ? f.B : s.cap[rr];
-      int64_t child = (int64_t)f.m - s.w[rr];
+      const int rr = mlow(rest);
+      rest = mclear(rest, rr);
+      const int md = s.mod[rr];
+      const int Bv = (rr == rtop) ? B : s.cap[rr];
+      const int64_t child = (int64_t)m - s.w[rr];
       bool nonempty = false;
       if (child == 0) {
         nonempty = true;
       } else if (child > 0) {
         if (nodes >= node_budget) return -3;
         if (d + 1 >= kMaxDepth) return -2;
-        int pushed = p1_visit(t, s, h, fr, d, (uint32_t)child, rr, f.A - md, Bv - md, nonempty, nodes);
+        M128 cen;
+        HEntry* cent;
+        const int pushed = p1_visit(t, s, h, (uint32_t)child, rr, A - md, Bv - md, nonempty, nodes, cen, cent);
         if (pushed < 0) return -1;
-        if (pushed) continue;  // resolved when the child frame pops
+        if (pushed) {  // descend: save this frame (its pending row is rr)
+          fr[d++] = P1Frame{rest.a, rest.b, e, m, A, B, (uint8_t)rtop, (uint8_t)(rr + 1), 0, 0};
+          rest = cen;
+          e = cent;
+          m = (uint32_t)child;
+          A -= md;
+          B = Bv - md;
+          rtop = rr;
+          continue;
+        }
       }
-      if (nonempty) {
-        HEntry* pe = fr[d].e;
-        if (((pe->meta >> 8) & 0xFF) == 0xFF) pe->meta = (pe->meta & 0xFFu) | ((uint32_t)rr << 8);
-      }
+      if (nonempty) p1_set_ne(e, rr);
     }
   }
   return 0;
+}
+
+__device__ int phase1(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
+                      uint64_t node_budget, uint64_t& nodes) {
+  h.sink = 0;
+  const int rc = phase1_body(t, s, h, fr, a, b, A0, node_budget, nodes);
+  return h.sink == 0x5bd1e9955bd1e995ull ? rc - 100 : rc;  // (never) keeps the prefetch loads alive
 }
 
 // ---------------------------------------------------------------------------
@@ -1445,60 +1473,61 @@ __global__ void k_layer_step(const uint64_t* __restrict__ prev, uint64_t* __rest
 
 __device__ __forceinline__ int lb_combine(int dir, int x, int y) { return dir ? (x > y ? x : y) : (x < y ? x : y); }
 
-// value arrays of the exact path: per hash slot, one int8 per row
+// saved ancestors of the value DP (the current frame is in registers)
 struct LBFrame {
   HEntry* e;
   uint32_t m;
   int acc;
-  uint8_t s, lo, hv, pad;
+  uint8_t r, hv, pad0, pad1;
 };
 
-// values of mass `root` (and every descendant it needs); 0 ok, -2 depth
+// values of mass `root` (and every descendant it needs), per row lo..hv in
+// vals[slot * kMaxRows + row]; 0 ok, -2 depth, -3 inconsistent memo
 __device__ int lb_values(const TableArgs& t, const Lds& s, const Hash& h, int8_t* vals, LBFrame* fr, HEntry* root_e,
                          uint32_t root, int dir, int dflt) {
+  HEntry* e = root_e;
+  uint32_t m = root;
+  int acc = dflt;
+  int r = (int)((e->meta >> 16) & 0xFF), hv = (int)(e->meta & 0xFF);
+  M128 en{e->en0, e->en1};
   int d = 0;
-  auto init = [&](LBFrame& f, HEntry* e, uint32_t m) {
-    f.e = e;
-    f.m = m;
-    f.acc = dflt;
-    f.lo = (uint8_t)rec_lo(ld_index(t.index, m));
-    f.hv = (uint8_t)(e->meta & 0xFF);
-    f.s = f.lo;
-  };
-  init(fr[0], root_e, root);
-  while (d >= 0) {
-    LBFrame& f = fr[d];
-    int8_t* fv = vals + (size_t)(f.e - h.e) * kMaxRows;
-    bool pushed = false;
-    while (f.s <= f.hv) {
-      const int r = f.s;
-      if (mtest(M128{f.e->en0, f.e->en1}, r)) {
-        const uint32_t c = f.m - (uint32_t)s.w[r];
-        int cv;
-        if (c == 0) {
-          cv = 0;  // total_mass == 0 -> 0 (mass_table.py:378-379)
-        } else {
-          HEntry* ce = h.find(c);  // visited by phase 1 (the edge was taken)
-          if (!ce) return -3;      // cannot happen for a consistent table; never dereference
-          if (ce->pad == 0) {
-            if (d + 1 >= kMaxDepth) return -2;
-            init(fr[d + 1], ce, c);
-            ++d;
-            pushed = true;
-            break;
-          }
-          cv = vals[(size_t)(ce - h.e) * kMaxRows + r];
-        }
-        f.acc = lb_combine(dir, f.acc, cv + 1);
-      }
-      fv[r] = (int8_t)f.acc;  // combine(default, rows lo..r)
-      f.s = (uint8_t)(r + 1);
+  for (;;) {
+    if (r > hv) {
+      e->pad = 1;  // values computed
+      if (d == 0) return 0;
+      const LBFrame f = fr[--d];  // resume the parent at its pending row (the child is now computed)
+      e = f.e;
+      m = f.m;
+      acc = f.acc;
+      r = f.r;
+      hv = f.hv;
+      en = M128{e->en0, e->en1};
+      continue;
     }
-    if (pushed) continue;
-    f.e->pad = 1;  // values computed
-    --d;
+    if (mtest(en, r)) {
+      const uint32_t c = m - (uint32_t)s.w[r];
+      int cv = 0;  // total_mass == 0 -> 0 (mass_table.py:378-379)
+      if (c != 0) {
+        HEntry* ce = h.find(c);  // visited by phase 1 (the edge was taken)
+        if (!ce) return -3;      // cannot happen for a consistent table; never dereference
+        if (ce->pad == 0) {
+          if (d + 1 >= kMaxDepth) return -2;
+          fr[d++] = LBFrame{e, m, acc, (uint8_t)r, (uint8_t)hv, 0, 0};
+          e = ce;
+          m = c;
+          acc = dflt;
+          r = (int)((ce->meta >> 16) & 0xFF);
+          hv = (int)(ce->meta & 0xFF);
+          en = M128{ce->en0, ce->en1};
+          continue;
+        }
+        cv = vals[(size_t)(ce - h.e) * kMaxRows + r];
+      }
+      acc = lb_combine(dir, acc, cv + 1);
+    }
+    vals[(size_t)(e - h.e) * kMaxRows + r] = (int8_t)acc;  // combine(default, rows lo..r)
+    ++r;
   }
-  return 0;
 }
 
 __device__ __forceinline__ bool lb_window(const LBArgs& q, int64_t i, int64_t& lo, int64_t& hi) {
@@ -1605,6 +1634,259 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
     }
     q.out[i] = lb_finish(q, best);
     q.status[i] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// explain_mass_with_recursion (mass_explanation.py:206-284), batched.
+//
+// dp(remaining, start, used_all, used_ind): budget check (:231-235, before
+// the memo), memo keyed (remaining, start) holding the FIRST visit's list
+// (:238-239), base cases |remaining| <= thr -> [[]] and remaining < 0 -> []
+// (not memoised), then children i = start.. in ascending order with
+// used_all + is_mod(i) and used_ind = (i != start ? 0 : used_ind + is_mod(i)).
+// Phase 1 replays the DFS and stores, per memoised node, the children that
+// passed their budget check at the node's first visit; phase 2 enumerates
+// that DAG (twice: count, then write).  One lane per query.
+// ---------------------------------------------------------------------------
+struct REntry {
+  uint64_t key;  // epoch << 40 | start << 32 | remaining
+  uint64_t en0, en1;
+  uint64_t pad;
+};
+struct RHash {
+  REntry* e;
+  uint32_t mask;
+  uint64_t epoch;
+  uint32_t used, limit;
+  __device__ __forceinline__ uint64_t key(uint32_t rem, int start) const {
+    return (epoch << 40) | ((uint64_t)start << 32) | rem;
+  }
+  __device__ __forceinline__ uint32_t slot(uint32_t rem, int start) const {
+    return ((rem * 0x9E3779B1u) ^ ((uint32_t)start * 0x85EBCA77u)) & mask;
+  }
+  __device__ __forceinline__ REntry* find(uint32_t rem, int start) const {
+    const uint64_t k = key(rem, start);
+    for (uint32_t i = slot(rem, start);; i = (i + 1) & mask) {
+      const uint64_t x = e[i].key;
+      if (x == k) return &e[i];
+      if ((x >> 40) != epoch) return nullptr;
+    }
+  }
+  __device__ __forceinline__ REntry* insert(uint32_t rem, int start) {  // caller checked absence
+    if (used >= limit) return nullptr;
+    const uint64_t k = key(rem, start);
+    for (uint32_t i = slot(rem, start);; i = (i + 1) & mask) {
+      if ((e[i].key >> 40) != epoch) {
+        ++used;
+        e[i].key = k;
+        return &e[i];
+      }
+    }
+  }
+};
+// saved (not current) DFS frames: 16 B, in LDS.  The current frame lives in
+// registers, so iterating a node's ~100 children touches no frame memory.
+struct RFrame {
+  uint32_t slot;  // memo entry
+  uint32_t rem;
+  int16_t ua, ui;
+  uint8_t start, next, pad0, pad1;
+};
+constexpr int kRecLanes = 64;  // lanes (queries) per workgroup of the recursion kernel
+
+// base case [[]]: abs(remaining) <= thr (:242-243) or remaining == 0 (:246-247)
+__device__ __forceinline__ bool rec_leaf(int64_t rem, int64_t thr) { return (rem <= thr && rem >= -thr) || rem == 0; }
+
+// children of (rem, start) that pass their budget check (:231-235)
+__device__ __forceinline__ M128 rec_enabled(const TableArgs& t, const Lds& s, int start, int ua, int ui, int A) {
+  M128 en = mand(rows_from(start), rows_upto(t.n_rows - 1));
+  if (ua + 1 > A) {  // every modification child would exceed max_modifications
+    en.a &= ~t.mod0;
+    en.b &= ~t.mod1;
+  }
+  // a fresh row i != start carries used_ind = 0: blocked only if cap[i] < 0
+  const bool keep_start = mtest(en, start) && ui + s.mod[start] <= s.cap[start];  // repeat of `start`
+  en.a &= ~t.capneg0;
+  en.b &= ~t.capneg1;
+  en = keep_start ? (start < 64 ? M128{en.a | (1ull << start), en.b} : M128{en.a, en.b | (1ull << (start - 64))})
+                  : mclear(en, start);
+  return en;
+}
+
+// Overlap the memory latency of a node's child look-ups: one independent load
+// per child's first probe slot (results folded into a sink the compiler must
+// keep), so the sequential probes that follow hit the cache instead of paying
+// one dependent HBM round trip each.
+__device__ __forceinline__ uint64_t rec_prefetch(const Lds& s, const RHash& h, uint32_t rem, M128 en, int64_t thr) {
+  uint64_t sink = 0;
+  for (M128 k = en; !mzero(k);) {
+    const int i = mlow(k);
+    k = mclear(k, i);
+    const int64_t crem = (int64_t)rem - s.w[i];
+    if (crem > thr) sink ^= __builtin_nontemporal_load(&h.e[h.slot((uint32_t)crem, i)].key) ^ 0;
+  }
+  return sink;
+}
+
+// phase 1: 0 ok, -1 memo full, -2 depth, -3 node budget.  stk: this lane's
+// kMaxDepth saved frames (LDS, stride kRecLanes).
+__device__ int rec_phase1(const TableArgs& t, const Lds& s, RHash& h, RFrame* stk, uint32_t target, int64_t thr,
+                          int A, uint64_t node_budget, uint64_t& nodes) {
+  REntry* e = h.insert(target, 1);
+  if (!e) return -1;
+  M128 rest = rec_enabled(t, s, 1, 0, 0, A);
+  e->en0 = rest.a;
+  e->en1 = rest.b;
+  uint32_t slot = (uint32_t)(e - h.e), rem = target;
+  int ua = 0, ui = 0, start = 1, d = 0;
+  uint64_t sink = rec_prefetch(s, h, rem, rest, thr);
+  for (;;) {
+    if (mzero(rest)) {
+      if (d == 0) break;
+      const RFrame f = stk[(--d) * kRecLanes];
+      const REntry* pe = h.e + f.slot;
+      slot = f.slot;
+      rem = f.rem;
+      ua = f.ua;
+      ui = f.ui;
+      start = f.start;
+      rest = mand(M128{pe->en0, pe->en1}, rows_from(f.next));
+      continue;
+    }
+    const int i = mlow(rest);
+    rest = mclear(rest, i);
+    const int64_t crem = (int64_t)rem - s.w[i];
+    if (rec_leaf(crem, thr) || crem < 0) continue;  // [[]] / []: base cases, not memoised
+    if (h.find((uint32_t)crem, i)) continue;          // memo hit: the first visit's list
+    if (++nodes > node_budget) return -3;
+    if (d + 1 >= kMaxDepth) return -2;
+    const int cua = ua + s.mod[i];
+    const int cui = i != start ? 0 : ui + s.mod[i];
+    REntry* ce = h.insert((uint32_t)crem, i);
+    if (!ce) return -1;
+    const M128 cen = rec_enabled(t, s, i, cua, cui, A);
+    ce->en0 = cen.a;
+    ce->en1 = cen.b;
+    stk[(d++) * kRecLanes] = RFrame{slot, rem, (int16_t)ua, (int16_t)ui, (uint8_t)start, (uint8_t)(i + 1), 0, 0};
+    slot = (uint32_t)(ce - h.e);
+    rem = (uint32_t)crem;
+    ua = cua;
+    ui = cui;
+    start = i;
+    rest = cen;
+    sink ^= rec_prefetch(s, h, rem, rest, thr);
+  }
+  return sink == 0x5bd1e9955bd1e995ull ? 1 : 0;  // (never) keeps the prefetch loads alive
+}
+
+// phase 2: candidates in the reference's list order; dst == nullptr counts.
+// path: this lane's row per level (LDS, stride kRecLanes).
+__device__ int rec_enumerate(const TableArgs& t, const Lds& s, const RHash& h, RFrame* stk, uint8_t* path,
+                             uint32_t target, int64_t thr, uint8_t* dst, uint64_t cap_count, uint64_t& count,
+                             uint64_t& bytes) {
+  const REntry* e = h.find(target, 1);
+  if (!e) return -3;
+  uint32_t slot = (uint32_t)(e - h.e), rem = target;
+  M128 rest = M128{e->en0, e->en1};
+  int d = 0;
+  while (true) {
+    if (mzero(rest)) {
+      if (d == 0) break;
+      const RFrame f = stk[(--d) * kRecLanes];
+      const REntry* pe = h.e + f.slot;
+      slot = f.slot;
+      rem = f.rem;
+      rest = mand(M128{pe->en0, pe->en1}, rows_from(f.next));
+      continue;
+    }
+    const int i = mlow(rest);
+    rest = mclear(rest, i);
+    path[d * kRecLanes] = (uint8_t)i;
+    const int64_t crem = (int64_t)rem - s.w[i];
+    if (rec_leaf(crem, thr)) {  // a candidate: rows path[0..d] (ascending)
+      if (dst && count < cap_count) {
+        dst[bytes] = (uint8_t)(d + 1);
+        for (int k = 0; k <= d; ++k) dst[bytes + 1 + k] = path[k * kRecLanes];
+      }
+      count++;
+      bytes += (uint64_t)d + 2;
+      continue;
+    }
+    if (crem < 0) continue;
+    const REntry* ce = h.find((uint32_t)crem, i);
+    if (!ce) return -3;  // phase 1 memoised every non-base child it reached
+    if (d + 1 >= kMaxDepth) return -2;
+    stk[(d++) * kRecLanes] = RFrame{slot, rem, 0, 0, 0, (uint8_t)(i + 1), 0, 0};
+    slot = (uint32_t)(ce - h.e);
+    rem = (uint32_t)crem;
+    rest = M128{ce->en0, ce->en1};
+  }
+  return 0;
+}
+
+__global__ __launch_bounds__(kRecLanes) void k_explain_recursion(TableArgs t, QueryArgs q, OutArgs out, char* hash,
+                                                                 uint32_t hash_cap) {
+  __shared__ Lds s;
+  __shared__ RFrame stk_all[kMaxDepth * kRecLanes];  // 96 KB
+  __shared__ uint8_t path_all[kMaxDepth * kRecLanes];
+  stage_rows(s, t);
+  const int64_t gid = (int64_t)blockIdx.x * kRecLanes + threadIdx.x;
+  const int64_t nthreads = (int64_t)gridDim.x * kRecLanes;
+  RFrame* stk = stk_all + threadIdx.x;
+  uint8_t* path = path_all + threadIdx.x;
+  RHash h;
+  h.e = (REntry*)(hash + (size_t)gid * hash_cap * sizeof(REntry));
+  h.mask = hash_cap - 1;
+  h.limit = (uint32_t)(hash_cap * 0.7);
+  uint64_t epoch = 0;
+  for (int64_t i = gid; i < q.n; i += nthreads) {
+    int64_t target, thr;
+    {
+      int64_t lo, hi;  // lo = target - thr, hi = target + thr (mass_explanation.py:218-225)
+      quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
+      target = (lo + hi) / 2;
+      thr = (hi - lo) / 2;
+    }
+    const int A = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
+    int8_t status;
+    uint64_t count = 0, bytes = 0, off = 0;
+    if (rec_leaf(target, thr)) {
+      status = SST_EMPTY;  // [[]]: the empty composition only (:242-247)
+    } else if (target < 0) {
+      status = SST_NONE;  // [] (:250-251)
+    } else if (target >= (int64_t)UINT32_MAX) {
+      status = SST_ABORTED;
+    } else {
+      h.epoch = ++epoch;  // the workspace was zeroed: epochs 1, 2, ... are fresh
+      h.used = 0;
+      uint64_t nodes = 0;
+      int rc = rec_phase1(t, s, h, stk, (uint32_t)target, thr, A, q.node_budget, nodes);
+      if (rc > 0) rc = 0;
+      if (rc == 0) rc = rec_enumerate(t, s, h, stk, path, (uint32_t)target, thr, nullptr, 0, count, bytes);
+      if (rc == -1) {
+        status = (int8_t)kStatusExactRetry;
+      } else if (rc < 0) {
+        status = SST_ABORTED;
+        count = 0;
+      } else if (count == 0) {
+        status = SST_NONE;
+      } else if (count > q.cap_count) {
+        status = SST_OVERFLOW;
+      } else {
+        status = SST_SOME;
+        off = out.spill_base + atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
+        if (off + bytes > out.arena_bytes) {
+          status = (int8_t)kStatusArenaRetry;
+        } else {
+          uint64_t c2 = 0, b2 = 0;
+          rec_enumerate(t, s, h, stk, path, (uint32_t)target, thr, out.payload + off, ~0ull, c2, b2);
+        }
+      }
+    }
+    out.status[i] = status;
+    out.count[i] = count;
+    out.offset[i] = status == SST_SOME ? off : 0;
   }
 }
 
@@ -1744,5 +2026,13 @@ hipError_t launch_length_bound(const TableArgs& t, const LBArgs& q, char* hash, 
 }
 size_t lb_frame_bytes() { return kMaxDepth * (sizeof(P1Frame) + sizeof(LBFrame)); }
 
+hipError_t launch_explain_recursion(const TableArgs& t, const QueryArgs& q, const OutArgs& o, char* hash,
+                                   char* /*frames: in LDS*/, uint32_t hash_cap, int lanes, hipStream_t st) {
+  if (q.n <= 0 || lanes < kRecLanes) return hipSuccess;
+  hipLaunchKernelGGL(k_explain_recursion, dim3(lanes / kRecLanes), dim3(kRecLanes), 0, st, t, q, o, hash, hash_cap);
+  return hipGetLastError();
+}
+size_t rec_frame_bytes() { return 64; }  // frames live in LDS; kept for the host's workspace sizing
+size_t rec_entry_bytes() { return sizeof(REntry); }
 }  // namespace sst
 

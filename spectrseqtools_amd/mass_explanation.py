@@ -134,11 +134,49 @@ def explain_masses_raw(masses, dp_table, max_modifications=np.inf, thresholds=No
 
 def explain_mass_with_recursion(mass: float, dp_table: DynamicProgrammingTable, max_modifications=np.inf,
                                 threshold=None) -> MassExplanations:
-    """mass_explanation.py:206-284 (the table-free enumerator)."""
-    from .recursion import explain_with_recursion
-
+    """mass_explanation.py:206-284: the table-free enumerator (base case
+    |remaining| <= threshold at every level, first-visit memo), on the GPU."""
     _check_finite(mass)
-    return explain_with_recursion(mass, dp_table, max_modifications, threshold)
+    return explain_masses_with_recursion([mass], dp_table, max_modifications,
+                                         None if threshold is None else [threshold])[0]
+
+
+def explain_masses_with_recursion(masses, dp_table: DynamicProgrammingTable, max_modifications=np.inf,
+                                  thresholds=None, cap_per_query=2 ** 32):
+    """Batched explain_mass_with_recursion (one engine call)."""
+    masses = np.ascontiguousarray(masses, dtype=np.float64)
+    for m in masses[~np.isfinite(masses)]:
+        _check_finite(float(m))
+    if thresholds is not None:
+        thresholds = np.ascontiguousarray(thresholds, dtype=np.float64)
+    # the reference compares used_mods_all > max_modifications: a fractional
+    # budget acts floored, a negative one rejects the root call ([] -> None)
+    def floored(x):
+        return np.inf if not np.isfinite(x) else float(np.floor(max(x, 0.0)))
+
+    if np.ndim(max_modifications) == 0:
+        negative = np.full(masses.shape, float(max_modifications) < 0)
+        engine_mods = floored(float(max_modifications))
+    else:
+        negative = np.asarray(max_modifications, dtype=np.float64) < 0
+        engine_mods = [floored(float(x)) for x in max_modifications]
+    res = dp_table.device_table.explain_recursion(masses, thresholds, dp_table.tolerance, dp_table.precision,
+                                                  engine_mods, cap=cap_per_query)
+    row_mass = [m.mass for m in dp_table.masses]
+    out = []
+    for i in range(res.n):
+        st = int(res.status[i])
+        if negative[i]:
+            out.append(MassExplanations(None))
+        elif st in (_native.SST_OVERFLOW, _native.SST_ABORTED):
+            raise OverflowError(f"query {i}: recursion enumeration exceeds the engine's caps (status {st})")
+        elif st == _native.SST_NONE:
+            out.append(MassExplanations(None))
+        elif st == _native.SST_EMPTY:
+            out.append(MassExplanations(set()))
+        else:
+            out.append(convert_nucleotide_masses_to_names([[row_mass[r] for r in c] for c in res.candidates(i)]))
+    return out
 
 
 def convert_nucleotide_masses_to_names(solutions: List[List[int]]) -> MassExplanations:

@@ -1,0 +1,87 @@
+"""Full-size parity at the benchmark's workload (10 000
+synthetic spectra, full alphabet, <= 20-mer; 4.3 M A7 + 10.7 M A8 queries):
+is_valid and explain statuses / candidate counts against the OpenMP C
+oracle, bit-exact, and every returned candidate checked by size-independent
+properties (a distinct multiset of table rows, in the reference's order,
+whose mass sum lies in the query's quantised window)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import _oracle as oracle
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def fullsize():
+    sys.path.insert(0, REPO)
+    import bench
+    from spectrseqtools_amd import _native
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+
+    seq = SequenceInformation(max_len=20, su_mass=6500.0, obs_mass=6500.0, modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=_native.get_engine(0))
+    wl = bench.build_workload(10000, 1000, dp)
+    return dp, wl
+
+
+def test_fullsize_is_valid_vs_oracle(fullsize):
+    dp, wl = fullsize
+    ms = [m.mass for m in dp.masses]
+    host = oracle.build_table(ms, max(ms) * 35, 32)
+    got = dp.device_table.is_valid(wl["a7_mass"], wl["a7_thr"], dp.tolerance, dp.precision)
+    want = oracle.is_valid_batch(host, 32, wl["a7_mass"], wl["a7_thr"], dp.tolerance, nthreads=16)
+    assert len(got) > 4_000_000
+    assert np.array_equal(got, want)
+
+
+def test_fullsize_explain_vs_oracle_and_properties(fullsize):
+    from spectrseqtools_amd import _native
+
+    dp, wl = fullsize
+    ms = np.array([m.mass for m in dp.masses], dtype=np.int64)
+    A = round(dp.seq.modification_rate * dp.seq.max_len)
+    masses, thr = wl["a8_mass"], wl["a8_thr"]
+    res = dp.device_table.explain(masses, thr, dp.tolerance, dp.precision, A)
+    assert res.n > 10_000_000
+    # statuses and counts: the C oracle (literal restatement), all queries
+    host = oracle.build_table(list(ms), int(ms.max()) * 35, 32)
+    alph = oracle.Alphabet(list(ms), [m.is_modification for m in dp.masses],
+                           [round(dp.seq.max_len * m.modification_rate) for m in dp.masses])
+    ost, ocnt, _ = oracle.explain_batch(host, 32, alph, masses, thr, A, dp.tolerance, nthreads=16)
+    want = np.where(ost < 0, _native.SST_OUT_OF_TABLE,
+                    np.where(ost == 0, _native.SST_NONE, np.where(ocnt > 0, _native.SST_SOME, _native.SST_EMPTY)))
+    assert np.array_equal(res.status.astype(np.int64), want)
+    some = res.status == _native.SST_SOME
+    assert np.array_equal(res.count[some].astype(np.int64), ocnt[some])
+    # every candidate: rows ascending, sum inside the quantised window, distinct
+    # within its query, and in the reference's order (ascending sum, then row)
+    target = np.rint(masses / dp.precision)
+    th = np.ceil(thr / dp.precision)
+    lo, hi = (target - th)[some], (target + th)[some]
+    pos = res.offset[some].astype(np.int64)
+    cnt = res.count[some].astype(np.int64)
+    pay = res.payload
+    prev_key = np.full(len(pos), -1, np.int64)
+    for j in range(int(cnt.max())):
+        act = j < cnt
+        p = pos[act]
+        k = pay[p].astype(np.int64)
+        assert ((k >= 1) & (k <= 3)).all()
+        r0 = pay[p + 1].astype(np.int64)
+        r1 = np.where(k >= 2, pay[np.minimum(p + 2, len(pay) - 1)], 0).astype(np.int64)
+        r2 = np.where(k >= 3, pay[np.minimum(p + 3, len(pay) - 1)], 0).astype(np.int64)
+        assert (r0 >= 1).all() and ((k < 2) | (r1 >= r0)).all() and ((k < 3) | (r2 >= r1)).all()
+        total = ms[r0] + np.where(k >= 2, ms[r1], 0) + np.where(k >= 3, ms[r2], 0)
+        assert ((total >= lo[act]) & (total <= hi[act])).all()
+        top = np.where(k == 1, r0, np.where(k == 2, r1, r2))
+        key = total * 128 + top
+        assert (key > prev_key[act]).all()  # strictly increasing: distinct and ordered
+        prev_key[act] = key
+        pos[act] = p + 1 + k

@@ -1,0 +1,89 @@
+"""GPU parity of explain_mass_with_recursion (mass_explanation.py:206-284):
+the reference's golden answers (tests/test_explain_masses.py masses, three
+tolerances) and the CPU oracle, candidate lists in the reference's order."""
+import math
+
+import numpy as np
+import pytest
+
+import _oracle as oracle
+from _golden_ctx import budget, ctx_alphabet
+from conftest import load_golden
+from spectrseqtools_amd import _native
+
+pytestmark = pytest.mark.gpu
+
+CANON = (305042, 306026, 329053, 345048)
+
+
+@pytest.fixture(scope="module")
+def engine():
+    return _native.get_engine(0)
+
+
+@pytest.fixture(scope="module")
+def full_dev(engine):
+    g = load_golden("alphabet.json")
+    ms = sorted({r["tolerated_integer_masses"] for r in g["rows"]} | {0})
+    return ms, _native.DeviceTable.build(ms, max(ms) * 35, 32, engine=engine)
+
+
+def test_golden_recursion(full_dev, golden_cases):
+    # one launch per budget set (contexts share the alphabet; the threshold
+    # default tolerance * mass is passed explicitly, as the reference computes it)
+    ms, dev = full_dev
+    ctxs = golden_cases["contexts"]
+    cases = [c for c in golden_cases["cases"] if c["fn"] == "recursion"]
+    assert cases
+    groups = {}
+    for c in cases:
+        ctx = ctxs[c["ctx"]]
+        assert ctx["masses"] == ms and ctx["precision"] == 1e-3
+        key = (tuple(ctx["caps"]), tuple(ctx["is_mod"]), str(c["max_modifications"]))
+        groups.setdefault(key, []).append((c, ctx))
+    for (caps, is_mod, A), items in groups.items():
+        dev.set_budgets(list(is_mod), list(caps))
+        masses = [c["mass"] for c, _ in items]
+        thr = [c["threshold"] if c["threshold"] is not None else ctx["tolerance"] * c["mass"] for c, ctx in items]
+        res = dev.explain_recursion(masses, thr, 1e-5, 1e-3, budget(items[0][0]["max_modifications"]))
+        for k, (c, ctx) in enumerate(items):
+            assert int(res.status[k]) == _native.SST_SOME, c["ctx"]
+            assert sorted(res.candidates(k)) == sorted(tuple(r) for r in c["rows"]), c["ctx"]
+
+
+def _alph(ms, max_len, rate=0.5):
+    is_mod = [m not in CANON and m != 0 for m in ms]
+    caps = [round(max_len * (rate if md else (1.0 if m else 0.0))) for m, md in zip(ms, is_mod)]
+    return is_mod, caps
+
+
+@pytest.mark.parametrize("max_len", [2, 20])
+def test_recursion_vs_oracle(full_dev, max_len):
+    ms, dev = full_dev
+    rng = np.random.default_rng(40 + max_len)
+    is_mod, caps = _alph(ms, max_len)
+    dev.set_budgets(is_mod, caps)
+    alph = oracle.Alphabet(ms, is_mod, caps)
+    k = rng.integers(1, 3, 24)
+    masses = np.array([rng.choice(ms[1:], kk).sum() * 1e-3 for kk in k]) + rng.normal(0, 0.003, 24)
+    masses = np.concatenate([masses, [0.0, 0.001, -1.0, 100.0]])
+    thr = np.concatenate([1e-5 * rng.uniform(300, 6000, 24), [0.01, 0.0, 0.01, 0.01]])
+    for A in (0, 1, math.inf):
+        res = dev.explain_recursion(masses, thr, 1e-5, 1e-3, A)
+        for i in range(len(masses)):
+            st, sols, n_empty = oracle.explain_recursion(alph, masses[i], thr[i], 1e-5, A)
+            want = _native.SST_SOME if sols else (_native.SST_EMPTY if n_empty else _native.SST_NONE)
+            assert int(res.status[i]) == want, (i, masses[i], thr[i], A)
+            assert res.candidates(i) == sols, (i, masses[i], A)  # the reference's list order
+
+
+def test_recursion_default_threshold(full_dev):
+    ms, dev = full_dev
+    is_mod, caps = _alph(ms, 6)
+    dev.set_budgets(is_mod, caps)
+    alph = oracle.Alphabet(ms, is_mod, caps)
+    masses = np.array([sum(CANON[:2]) * 1e-3, CANON[0] * 3e-3, 1285.16888])
+    res = dev.explain_recursion(masses, None, 1e-5, 1e-3, 3)
+    for i in range(len(masses)):
+        st, sols, n_empty = oracle.explain_recursion(alph, masses[i], None, 1e-5, 3)
+        assert res.candidates(i) == sols

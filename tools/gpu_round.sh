@@ -14,4 +14,4 @@ step() {  # step NAME TIMEOUT CMD...
   return 0
 }
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step gputests 1200 python -m pytest tests -x -q -m gpu -p no:cacheprovider
+step gputests 1200 python -m pytest tests -x -q -m gpu -p no:cacheprovider --durations=8
