@@ -171,9 +171,10 @@ int sst_length_bound_batch(sst_table* t, const double* su_mass, const double* ob
 /* Kernel ids for sst_profile_read. */
 #define SST_K_IS_VALID 0
 #define SST_K_EXPLAIN_MAIN 1
-#define SST_K_EXPLAIN_DEEP 2
-#define SST_K_EXPLAIN_NOMEMO 3
-#define SST_K_EXPLAIN_EXACT 4
+#define SST_K_EXPLAIN_DEFERRED 2 /* deep, no-memo and exact roles share one launch */
+#define SST_K_EXPLAIN_DEEP SST_K_EXPLAIN_DEFERRED
+#define SST_K_EXPLAIN_NOMEMO 3 /* reserved (merged into SST_K_EXPLAIN_DEFERRED) */
+#define SST_K_EXPLAIN_EXACT 4  /* reserved (merged into SST_K_EXPLAIN_DEFERRED) */
 #define SST_K_EXPLAIN_EXPAND 5
 #define SST_K_COUNT 8
 /* When enabled, every kernel launch of this ctx is bracketed by hipEvents

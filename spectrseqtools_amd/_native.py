@@ -30,9 +30,8 @@ EXPORTS = (
 
 # kernel ids of sst_profile_read
 K_IS_VALID, K_EXPLAIN_SCAN, K_EXPLAIN_DEEP, K_EXPLAIN_NOMEMO, K_EXPLAIN_EXACT, K_EXPLAIN_EXPAND = 0, 1, 2, 3, 4, 5
-KERNEL_NAMES = {K_IS_VALID: "k_is_valid", K_EXPLAIN_SCAN: "k_explain_scan", K_EXPLAIN_DEEP: "k_explain_deep<0>",
-                K_EXPLAIN_NOMEMO: "k_explain_deep<1>", K_EXPLAIN_EXACT: "k_explain_exact",
-                K_EXPLAIN_EXPAND: "k_explain_expand"}
+KERNEL_NAMES = {K_IS_VALID: "k_is_valid", K_EXPLAIN_SCAN: "k_explain_scan", K_EXPLAIN_DEEP: "k_explain_deferred",
+                K_EXPLAIN_EXPAND: "k_explain_expand"}  # ids 3, 4: reserved (merged into the deferred launch)
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64

@@ -586,7 +586,7 @@ int sst_is_valid_batch(sst_table* t, const double* mass, const double* thr, int6
 
 namespace {
 
-constexpr int kDeepBlocks = 256;        // persistent grid of the deep / no-memo kernel
+constexpr int kDeepBlocks = 512;        // 64-lane blocks per deep role (fast, no-memo) of the deferred kernel
 constexpr uint32_t kHashCap0 = 1u << 14;  // exact-path hash entries per lane (first attempt)
 constexpr int kExactLanes0 = 2048;      // exact-path concurrent lanes (first attempt)
 constexpr uint64_t kNodeBudget = 1ull << 32;
@@ -664,7 +664,7 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   r->parity ^= 1;  // zeroed by the previous pass's scan (or above)
   if (n == 0)      // no scan launch: zero the next pass's block here
     HIP_OK(c, hipMemsetAsync(ctl_block(r, r->parity ^ 1), 0, kCtlWords * 8, c->stream));
-  if (!c->ws_deep.ensure((size_t)kDeepBlocks * kWG * kMaxDepth * glob_frame_bytes()))
+  if (!c->ws_deep.ensure((size_t)2 * kDeepBlocks * 64 * kMaxDepth * glob_frame_bytes()))
     return fail(c, SST_E_NOMEM, "device allocation failed (deep workspace)");
   if (c->hash_cap == 0)
     if (int rc = ensure_exact_ws(c, kHashCap0, kExactLanes0)) return rc;
@@ -679,19 +679,11 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
     Prof p(c, SST_K_EXPLAIN_EXPAND);
     HIP_OK(c, launch_explain_expand(t->args, q, o, r->n_waves / (kWG / 64), c->stream));
   }
-  {
-    Prof p(c, SST_K_EXPLAIN_DEEP);
-    HIP_OK(c, launch_explain_deep(t->args, q, o, kClassDeep, c->ws_deep.p, kDeepBlocks, c->stream));
-  }
-  {
-    Prof p(c, SST_K_EXPLAIN_NOMEMO);
-    HIP_OK(c, launch_explain_deep(t->args, q, o, kClassNomemo, c->ws_deep.p, kDeepBlocks, c->stream));
-  }
   ExactWs ws{(char*)c->ws_hash.p, (char*)c->ws_frames.p, (char*)c->ws_stacks.p, (uint64_t*)c->ws_epochs.p,
              c->hash_cap};
   {
-    Prof p(c, SST_K_EXPLAIN_EXACT);
-    HIP_OK(c, launch_explain_exact(t->args, q, o, ws, c->exact_blocks, c->stream));
+    Prof p(c, SST_K_EXPLAIN_DEEP);  // deep, no-memo and exact roles: one launch
+    HIP_OK(c, launch_explain_deferred(t->args, q, o, c->ws_deep.p, kDeepBlocks, ws, c->exact_blocks, c->stream));
   }
   return SST_OK;
 }

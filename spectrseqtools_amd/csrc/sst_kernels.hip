@@ -1316,14 +1316,13 @@ __global__ __launch_bounds__(256) void k_compact_offsets(const int8_t* __restric
 // Deferred fast/no-memo queries with deep stacks: persistent grid, one lane per
 // query, stack in a per-lane slice of the workspace.
 template <int MODE>
-__global__ __launch_bounds__(kWG) void k_explain_deep(TableArgs t, QueryArgs q, OutArgs out, int cls,
-                                                      GlobFrame* ws) {
-  __shared__ Lds s;
+__device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs& out, int cls, GlobFrame* ws, Lds& s,
+                          int blk, int nblk) {
   const uint32_t n_list = out.counters[cls];
-  if (n_list == 0) return;  // block-uniform: idle launch
+  if (n_list == 0) return;  // block-uniform: nothing queued for this role
   stage_rows(s, t);
-  const int64_t gid = (int64_t)blockIdx.x * kWG + threadIdx.x;
-  const int64_t nthreads = (int64_t)gridDim.x * kWG;
+  const int64_t gid = (int64_t)blk * blockDim.x + threadIdx.x;
+  const int64_t nthreads = (int64_t)nblk * blockDim.x;
   GlobStack st{ws + gid * kMaxDepth};
   uint64_t st_n = 0, st_nodes = 0;
   for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
@@ -1369,13 +1368,13 @@ __global__ __launch_bounds__(kWG) void k_explain_deep(TableArgs t, QueryArgs q, 
 
 // Deferred budget-binding queries: exact memo replay (phase 1) + enabled-DAG
 // enumeration (phase 2).  Per lane: a hash slice and a frame slice.
-__global__ __launch_bounds__(64) void k_explain_exact(TableArgs t, QueryArgs q, OutArgs out, ExactWs ws) {
-  __shared__ Lds s;
+__device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs& out, ExactWs ws, Lds& s, int blk,
+                           int nblk) {
   const uint32_t n_list = out.counters[kClassExact];
-  if (n_list == 0) return;  // block-uniform: idle launch
+  if (n_list == 0) return;  // block-uniform: nothing queued for this role
   stage_rows(s, t);
-  const int64_t gid = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t nthreads = (int64_t)gridDim.x * 64;
+  const int64_t gid = (int64_t)blk * 64 + threadIdx.x;
+  const int64_t nthreads = (int64_t)nblk * 64;
   P1Frame* fr = (P1Frame*)(ws.frames + gid * kMaxDepth * sizeof(P1Frame));
   GlobStack st{(GlobFrame*)(ws.stacks + gid * kMaxDepth * sizeof(GlobFrame))};
   Hash h;
@@ -1434,6 +1433,22 @@ __global__ __launch_bounds__(64) void k_explain_exact(TableArgs t, QueryArgs q, 
   }
   wg_stat(out.stats, kStatExact, st_n);
   wg_stat(out.stats, kStatNodes, st_nodes);
+}
+
+// The three deferred roles in one launch (64-lane blocks, partitioned by
+// block index): deep fast path, deep no-memo, exact replay.  Each role exits
+// at once when its list is empty, so an idle pass costs one launch.
+__global__ __launch_bounds__(64) void k_explain_deferred(TableArgs t, QueryArgs q, OutArgs out, GlobFrame* ws_deep,
+                                                         ExactWs ws, int deep_blocks) {
+  __shared__ Lds s;
+  const int b = blockIdx.x;
+  if (b < deep_blocks)
+    deep_body<MODE_FAST>(t, q, out, kClassDeep, ws_deep, s, b, deep_blocks);
+  else if (b < 2 * deep_blocks)  // second half of the deep workspace
+    deep_body<MODE_NOMEMO>(t, q, out, kClassNomemo, ws_deep + (size_t)deep_blocks * 64 * kMaxDepth, s,
+                           b - deep_blocks, deep_blocks);
+  else
+    exact_body(t, q, out, ws, s, b - 2 * deep_blocks, (int)gridDim.x - 2 * deep_blocks);
 }
 
 // ---------------------------------------------------------------------------
@@ -1993,17 +2008,11 @@ hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* pr
                        pre, n_waves, o.region_bytes, o.spill_base);
   return hipGetLastError();
 }
-hipError_t launch_explain_deep(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int cls, void* ws,
-                               int n_blocks, hipStream_t st) {
-  if (cls == kClassDeep)
-    hipLaunchKernelGGL(k_explain_deep<MODE_FAST>, dim3(n_blocks), dim3(kWG), 0, st, t, q, o, cls, (GlobFrame*)ws);
-  else
-    hipLaunchKernelGGL(k_explain_deep<MODE_NOMEMO>, dim3(n_blocks), dim3(kWG), 0, st, t, q, o, cls, (GlobFrame*)ws);
-  return hipGetLastError();
-}
-hipError_t launch_explain_exact(const TableArgs& t, const QueryArgs& q, const OutArgs& o, const ExactWs& ws,
-                                int n_blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_explain_exact, dim3(n_blocks), dim3(64), 0, st, t, q, o, ws);
+hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const OutArgs& o, void* ws_deep,
+                                   int deep_blocks, const ExactWs& ws, int exact_blocks, hipStream_t st) {
+  if (q.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_explain_deferred, dim3(2 * deep_blocks + exact_blocks), dim3(64), 0, st, t, q, o,
+                     (GlobFrame*)ws_deep, ws, deep_blocks);
   return hipGetLastError();
 }
 
