@@ -67,7 +67,7 @@ class DynamicProgrammingTable:
     """
 
     def __init__(self, nucleotide_df, compression_rate: int, tolerance: float, precision: float,
-                 seq: SequenceInformation, engine=None):
+                 seq: SequenceInformation, engine=None, use_cache=False):
         self.compression_per_cell = compression_rate
         self.tolerance = tolerance
         self.precision = precision
@@ -80,13 +80,22 @@ class DynamicProgrammingTable:
         # Adapt individual modification rates to universal one (:76-77)
         self._adapt_individual_modification_rates_by_universal_one()
 
-        # No alphabet reduction: the full table (load_dp_table, :80-84).  Built
-        # on the GPU in milliseconds instead of read from the alphabet-blind
-        # .npy cache, so the table always matches self.masses.
+        # No alphabet reduction: the full table (load_dp_table, :80-84).  By
+        # default built on the GPU in milliseconds, so the table always matches
+        # self.masses.  use_cache=True follows the reference exactly: read (or
+        # build and write) the .npy cache at set_table_path(); the cache key
+        # ignores the alphabet, and a cached table that does not follow the
+        # recurrence for self.masses is rejected by the engine's upload check
+        # (the reference would use it silently).
         if self._device is None:
             masses = [m.mass for m in self.masses]
-            self._set_device(_native.DeviceTable.build(masses, max(masses) * MAX_SEQ_LENGTH, compression_rate,
-                                                       engine=self._engine))
+            if use_cache:
+                words = load_dp_table(set_table_path(precision, compression_rate), masses, engine=self._engine)
+                self._set_device(_native.DeviceTable.upload(masses, words, compression_rate, engine=self._engine))
+                self._table_host = words
+            else:
+                self._set_device(_native.DeviceTable.build(masses, max(masses) * MAX_SEQ_LENGTH, compression_rate,
+                                                           engine=self._engine))
 
     # -- device table ---------------------------------------------------------
     def _set_device(self, dev):
@@ -227,7 +236,7 @@ def load_dp_table(table_path, integer_masses, engine=None):
             raise NotImplementedError("compression 1 (set_up_mass_table) is not provided by the GPU engine")
         dp_table = set_up_bit_table(integer_masses, max_mass, compression_rate, engine=engine)
         np.save(table_path, dp_table)
-    return np.load(f"{table_path}.npy")
+    return np.load(f"{table_path}.npy", allow_pickle=False)
 
 
 def compute_sequence_length_bound(dp_table: DynamicProgrammingTable, dir: str) -> int:
