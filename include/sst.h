@@ -98,6 +98,18 @@ int sst_is_valid_batch(sst_table* t, const double* mass, const double* thr_abs, 
 int sst_is_valid_batch_device(sst_table* t, const double* d_mass, const double* d_thr_abs, int64_t n,
                               double tolerance, double precision, int8_t* d_out);
 
+/* is_singleton (fragment_classification.py:104-119), one result per query:
+ * 1 if some value of the quantised window [round(mass/precision) -
+ * ceil(thr/precision), ... + ...] is one of masses[0..n_masses) (the caller's
+ * integer masses; classify_fragments passes the table's rows, :73-80), else 0.
+ * n_masses <= 1024.  thr_abs may be NULL (tolerance*mass). */
+int sst_is_singleton_batch(sst_ctx* ctx, const int64_t* masses, int n_masses, const double* mass,
+                           const double* thr_abs, int64_t n, double tolerance, double precision, int8_t* out);
+/* Same on device buffers, queued on the ctx stream (masses: host array). */
+int sst_is_singleton_batch_device(sst_ctx* ctx, const int64_t* masses, int n_masses, const double* d_mass,
+                                  const double* d_thr_abs, int64_t n, double tolerance, double precision,
+                                  int8_t* d_out);
+
 /* explain_mass_with_table (mass_explanation.py:92-203), batched.
  *   max_mods: per-query budget array (may be NULL) else max_mods_scalar;
  *             a negative value means np.inf (the reference default);

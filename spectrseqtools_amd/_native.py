@@ -25,7 +25,8 @@ EXPORTS = (
     "sst_table_download", "sst_table_destroy", "sst_is_valid_batch", "sst_is_valid_batch_device",
     "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
-    "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch",
+    "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
+    "sst_is_singleton_batch_device",
 )
 
 # kernel ids of sst_profile_read
@@ -82,6 +83,8 @@ def load_library(path=LIB_PATH):
     lib.sst_profile_read.argtypes = [_P, _P, _P]
     lib.sst_length_bound_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _I, _I64, _I, _P, _P]
     lib.sst_explain_recursion_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _U64, _PP]
+    lib.sst_is_singleton_batch.argtypes = [_P, _P, _I, _P, _P, _I64, _D, _D, _P]
+    lib.sst_is_singleton_batch_device.argtypes = [_P, _P, _I, _P, _P, _I64, _D, _D, _P]
     return lib
 
 
@@ -133,6 +136,17 @@ class Engine:
 
     def synchronize(self):
         self.check(self._lib.sst_ctx_synchronize(self.handle), "sst_ctx_synchronize")
+
+    def is_singleton(self, integer_masses, masses, thresholds, tolerance, precision):
+        """fragment_classification.is_singleton for each mass: int8 {0, 1}."""
+        w = np.ascontiguousarray(integer_masses, dtype=np.int64)
+        m = np.ascontiguousarray(masses, dtype=np.float64)
+        t = None if thresholds is None else np.ascontiguousarray(thresholds, dtype=np.float64)
+        out = np.zeros(len(m), np.int8)
+        self.check(self._lib.sst_is_singleton_batch(self.handle, _ptr(w), len(w), _ptr(m), _ptr(t), len(m),
+                                                    float(tolerance), float(precision), _ptr(out)),
+                   "sst_is_singleton_batch")
+        return out
 
     def profile(self, on=True, kernels=None):
         """Bracket launches with HIP events: all kernels, or only the ids in `kernels`."""

@@ -57,6 +57,7 @@ struct sst_ctx {
   // persistent workspaces of the deferred explain kernels
   DevBuf ws_deep;
   DevBuf ws_hash, ws_frames, ws_stacks, ws_epochs;
+  DevBuf singleton_masses;  // sorted, de-duplicated integer masses of the last is_singleton call
   uint32_t hash_cap = 0;
   int exact_blocks = 0;
   int n_cu = 256;       // compute units (persistent grid sizing)
@@ -349,7 +350,7 @@ void sst_ctx_destroy(sst_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->in_mass, &c->in_thr, &c->in_mods, &c->out_valid, &c->ws_deep, &c->ws_hash, &c->ws_frames,
-                    &c->ws_stacks, &c->ws_epochs})
+                    &c->ws_stacks, &c->ws_epochs, &c->singleton_masses})
     b->release();
   prof_resolve(c);
   for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
@@ -1012,6 +1013,52 @@ int sst_profile_read(sst_ctx* c, double* ms, int64_t* n) {
   return SST_OK;
 }
 
+
+// sorted, de-duplicated copy of the caller's integer masses on the device
+static int singleton_masses(sst_ctx* c, const int64_t* masses, int n_masses, DevBuf& d, int* n_unique) {
+  if ((!masses && n_masses > 0) || n_masses < 0 || n_masses > kMaxSingletonMasses)
+    return fail(c, SST_E_ARG, "is_singleton: 0..1024 integer masses");
+  std::vector<int64_t> m(masses, masses + n_masses);
+  std::sort(m.begin(), m.end());
+  m.erase(std::unique(m.begin(), m.end()), m.end());
+  if (!d.ensure(std::max<size_t>(1, m.size()) * 8)) return fail(c, SST_E_NOMEM, "device allocation failed");
+  if (!m.empty()) HIP_OK(c, hipMemcpyAsync(d.p, m.data(), m.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));  // m is a host temporary
+  *n_unique = (int)m.size();
+  return SST_OK;
+}
+
+int sst_is_singleton_batch_device(sst_ctx* c, const int64_t* masses, int n_masses, const double* d_mass,
+                                  const double* d_thr, int64_t n, double tol, double prec, int8_t* d_out) {
+  if (!c || n < 0 || n > INT32_MAX || (n > 0 && (!d_mass || !d_out))) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  int nm = 0;
+  if (int rc = singleton_masses(c, masses, n_masses, c->singleton_masses, &nm)) return rc;
+  HIP_OK(c, launch_is_singleton((const int64_t*)c->singleton_masses.p, nm, d_mass, d_thr, n, tol, prec, d_out,
+                                c->stream));
+  return SST_OK;
+}
+
+int sst_is_singleton_batch(sst_ctx* c, const int64_t* masses, int n_masses, const double* mass, const double* thr,
+                           int64_t n, double tol, double prec, int8_t* out) {
+  if (!c || n < 0 || n > INT32_MAX || (n > 0 && (!mass || !out))) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (n == 0) return SST_OK;
+  const size_t nn = (size_t)n;
+  if (!c->in_mass.ensure(nn * 8) || (thr && !c->in_thr.ensure(nn * 8)) || !c->out_valid.ensure(nn))
+    return fail(c, SST_E_NOMEM, "device allocation failed (staging)");
+  HIP_OK(c, hipMemcpyAsync(c->in_mass.p, mass, nn * 8, hipMemcpyHostToDevice, c->stream));
+  if (thr) HIP_OK(c, hipMemcpyAsync(c->in_thr.p, thr, nn * 8, hipMemcpyHostToDevice, c->stream));
+  if (int rc = sst_is_singleton_batch_device(c, masses, n_masses, (const double*)c->in_mass.p,
+                                             thr ? (const double*)c->in_thr.p : nullptr, n, tol, prec,
+                                             (int8_t*)c->out_valid.p))
+    return rc;
+  HIP_OK(c, hipMemcpyAsync(out, c->out_valid.p, nn, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  return SST_OK;
+}
 
 int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, int64_t n, double tol, double prec,
                            int max_len, int64_t max_mods, int direction, int64_t* out, int8_t* status) {

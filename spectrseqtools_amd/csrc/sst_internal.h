@@ -14,6 +14,7 @@ constexpr int kShallowDepth = 4;   // register-stack depth of the main kernel
 constexpr int kMaxDepth = 96;      // >= max items of any multiset in a table (73 for the full alphabet)
 constexpr int kInfBudget = 1 << 30;  // np.inf budget (decremented at most kMaxDepth times)
 constexpr int kScanWG = 1024;        // scan kernel workgroup (2 per CU share the LDS pair list)
+constexpr int kMaxSingletonMasses = 1024;  // is_singleton: integer masses staged in LDS
 constexpr int kMaxPairLds = 78 * 1024;  // pair list + buckets: two scan workgroups per CU (160 KB LDS)
 // worklist item flags ({query, a, b, flags}): v == 0 lies in the window; the
 // window was not classified by the scan (the expand kernel checks the bitset
@@ -169,6 +170,8 @@ hipError_t launch_layer_step(const uint64_t* prev, uint64_t* next, int64_t nword
 hipError_t launch_length_bound(const TableArgs& t, const LBArgs& q, char* hash, int8_t* vals, char* frames,
                                uint32_t hash_cap, int exact_lanes, bool fast_pass, hipStream_t st);
 size_t lb_frame_bytes();
+hipError_t launch_is_singleton(const int64_t* masses, int n_masses, const double* mass, const double* thr, int64_t n,
+                               double tol, double prec, int8_t* out, hipStream_t st);
 hipError_t launch_explain_recursion(const TableArgs& t, const QueryArgs& q, const OutArgs& o, char* hash,
                                    char* frames, uint32_t hash_cap, int lanes, hipStream_t st);
 size_t rec_frame_bytes();

@@ -366,6 +366,32 @@ __global__ __launch_bounds__(256) void k_is_valid(const uint64_t* __restrict__ v
 }
 
 // ---------------------------------------------------------------------------
+// is_singleton (fragment_classification.py:104-119): some value of the
+// quantised window equals one of `masses` (the caller's integer masses, the
+// table's rows incl. the sentinel 0 in classify_fragments :73-80).  Sorted,
+// de-duplicated masses in LDS; one binary search per window.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_is_singleton(const int64_t* __restrict__ masses, int n_masses,
+                                                      const double* __restrict__ mass,
+                                                      const double* __restrict__ thr, int64_t n, double tol,
+                                                      double prec, double rprec, int8_t* __restrict__ out) {
+  __shared__ int64_t sm[kMaxSingletonMasses];
+  for (int k = threadIdx.x; k < n_masses; k += blockDim.x) sm[k] = masses[k];
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t lo, hi;
+  quantise(mass[i], thr ? thr[i] : 0.0, thr == nullptr, tol, prec, rprec, lo, hi);
+  int l = 0, r = n_masses;  // first index with sm[idx] >= lo
+  while (l < r) {
+    const int mid = (l + r) >> 1;
+    if (sm[mid] < lo) l = mid + 1;
+    else r = mid;
+  }
+  out[i] = (lo <= hi && l < n_masses && sm[l] <= hi) ? (int8_t)1 : (int8_t)0;
+}
+
+// ---------------------------------------------------------------------------
 // explain: shared pieces
 // ---------------------------------------------------------------------------
 struct Lds {
@@ -2043,5 +2069,12 @@ hipError_t launch_explain_recursion(const TableArgs& t, const QueryArgs& q, cons
 }
 size_t rec_frame_bytes() { return 64; }  // frames live in LDS; kept for the host's workspace sizing
 size_t rec_entry_bytes() { return sizeof(REntry); }
+hipError_t launch_is_singleton(const int64_t* masses, int n_masses, const double* mass, const double* thr, int64_t n,
+                               double tol, double prec, int8_t* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_is_singleton, dim3(blocks_for(n, 256)), dim3(256), 0, st, masses, n_masses, mass, thr, n, tol,
+                     prec, 1.0 / prec, out);
+  return hipGetLastError();
+}
 }  // namespace sst
 

@@ -150,3 +150,19 @@ def is_valid_batch(table, C, masses, thrs, tolerance, nthreads=1, precision=1e-3
     LIB.ora_is_valid_batch(_p(table), table.shape[0], table.shape[1], C, _p(masses), _p(thrs), n, float(tolerance),
                            float(precision), int(nthreads), _p(out))
     return out
+
+
+def is_singleton_batch(masses, thrs, integer_masses, tolerance, precision=1e-3):
+    """fragment_classification.py:104-119 restated (numpy, exact): target =
+    round(mass/precision) (ties-to-even on the f64 quotient), thr =
+    ceil(threshold/precision), threshold default tolerance*mass; True iff some
+    value in [target - thr, target + thr] is one of integer_masses."""
+    masses = np.asarray(masses, dtype=np.float64)
+    thrs = tolerance * masses if thrs is None else np.asarray(thrs, dtype=np.float64)
+    target = np.rint(masses / precision).astype(np.int64)
+    th = np.ceil(thrs / precision).astype(np.int64)
+    lo, hi = target - th, target + th
+    w = np.unique(np.asarray(integer_masses, dtype=np.int64))
+    k = np.searchsorted(w, lo, side="left")
+    hit = (k < len(w)) & (w[np.minimum(k, len(w) - 1)] <= hi) & (lo <= hi)
+    return hit

@@ -19,6 +19,7 @@ Outputs (all JSON, floats written with repr so they round-trip exactly):
   population.json.gz   A7 (is_valid) and A8 (adjacent-difference explain) query
                        streams of the reference's own test spectra
                        (tests/testcases/test_0[1-8]) with reference answers
+  singleton.json.gz    fragment_classification.is_singleton known answers
 
 Usage:  python tests/golden/make_golden.py [--rebuild-full-table]
 """
@@ -416,6 +417,39 @@ def population():
     dump("population.json.gz", {"contexts": ctxs, "a7": a7, "a8": a8}, gz=True)
 
 
+# --------------------------------------------------------------------------
+# 5. is_singleton (fragment_classification.py:104-119) known answers
+# --------------------------------------------------------------------------
+def singleton():
+    """The reference's own is_singleton on (a) every A7 query of its test
+    spectra (the valid fragments classify_fragments would test) and (b)
+    windows placed on / next to every row mass and the sentinel 0, with
+    thresholds from 0 to several units.  Full-alphabet table, integer_masses =
+    the table's rows as classify_fragments passes them (:73-80)."""
+    import spectrseqtools.fragment_classification as FC
+
+    dp = make_ctx("singleton_full", 20, M.MATCHING_THRESHOLD)
+    rows = [m.mass for m in dp.masses]
+    pop = json.loads(gzip.open(os.path.join(HERE, "population.json.gz")).read())
+    qs = [(q[1], q[2]) for q in pop["a7"]]
+    rng = random.Random(7)
+    for w in rows:
+        for d in (-3, -2, -1, 0, 1, 2, 3):
+            for thr_units in (0, 1, 2, 4):
+                m = (w + d) * dp.precision + rng.uniform(-0.0004, 0.0004)
+                qs.append((m, thr_units * dp.precision + rng.choice([0.0, 1e-7, -1e-7])))
+    for m in (0.0, 0.0004, -0.0004, -0.5, 0.5):
+        qs.append((m, 0.001))
+    out = []
+    t0 = time.perf_counter()
+    for m, thr in qs:
+        thr = max(thr, 0.0)
+        out.append([m, thr, bool(FC.is_singleton(m, rows, dp, threshold=thr))])
+    print(f"  is_singleton: {len(out)} queries ({time.perf_counter() - t0:.1f}s), "
+          f"{sum(o[2] for o in out)} true", flush=True)
+    dump("singleton.json.gz", {"context": CTX["singleton_full"], "queries": out}, gz=True)
+
+
 if __name__ == "__main__":
     t = time.time()
     parts = [a for a in sys.argv[1:] if not a.startswith("--")] or ["alphabet", "tables", "cases", "population"]
@@ -427,4 +461,6 @@ if __name__ == "__main__":
         cases()
     if "population" in parts:
         population()
+    if "singleton" in parts:
+        singleton()
     print(f"done in {time.time() - t:.0f}s")

@@ -8,6 +8,7 @@ import pytest
 
 import _oracle as oracle
 from _golden_ctx import budget, ctx_alphabet, ctx_table, sha
+from conftest import load_golden
 
 
 def test_tiny_tables_verbatim(golden_tables):
@@ -121,3 +122,12 @@ def test_population_a8(golden_population):
             assert st == 0, (cid, m)
         else:
             assert st == 1 and sorted(sols) == sorted(tuple(r) for r in rows), (cid, m)
+
+
+def test_is_singleton_restatement_vs_reference():
+    g = load_golden("singleton.json.gz")
+    ctx = g["context"]
+    q = np.array([[x[0], x[1]] for x in g["queries"]])
+    want = np.array([x[2] for x in g["queries"]])
+    got = oracle.is_singleton_batch(q[:, 0], q[:, 1], ctx["masses"], ctx["tolerance"], ctx["precision"])
+    assert want.sum() > 1000 and np.array_equal(got, want)
