@@ -295,6 +295,30 @@ int finish_table(sst_table* t, bool self_built) {
     if (t->masses[r] > 0 && (wmin == 0 || t->masses[r] < wmin)) wmin = (int)t->masses[r];
   t->args.w_min = wmin > 0 ? wmin : 1;
   t->args.shallow_hi = (int64_t)kShallowDepth * t->args.w_min;  // < 4 w_min: at most 3 items
+  // longest run of reachable masses (whole bitset words): every window that
+  // meets it holds a reachable value (is_valid answers without a bitset load)
+  {
+    std::vector<uint64_t> vb(t->valid.bytes / 8);
+    HIP_OK(c, hipMemcpy(vb.data(), t->valid.p, t->valid.bytes, hipMemcpyDeviceToHost));
+    int64_t best_lo = 0, best_len = 0, run_lo = 0;
+    for (int64_t k = 0; k <= (int64_t)vb.size(); ++k) {
+      if (k < (int64_t)vb.size() && vb[(size_t)k] == ~0ull) continue;
+      if (k - run_lo > best_len) {
+        best_len = k - run_lo;
+        best_lo = run_lo;
+      }
+      run_lo = k + 1;
+    }
+    t->args.full_lo = best_len ? best_lo * 64 : 1;
+    t->args.full_hi = best_len ? std::min<int64_t>((best_lo + best_len) * 64, M) : 1;  // [full_lo, full_hi)
+    // first reachable mass >= 1: windows wholly below it hold no reachable value
+    int64_t first = M;
+    for (size_t k = 0; k < vb.size() && first == M; ++k) {
+      const uint64_t x = k == 0 ? (vb[0] & ~1ull) : vb[k];
+      if (x) first = (int64_t)k * 64 + __builtin_ctzll(x);
+    }
+    t->args.first_reach = first;
+  }
   if (int rc = build_pair_list(t, self_built)) return rc;
   // default budgets: no modification rows (callers set them)
   std::vector<uint8_t> mod(t->n_rows, 0);
@@ -560,7 +584,8 @@ int sst_is_valid_batch_device(sst_table* t, const double* d_mass, const double* 
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
   Prof p(c, SST_K_IS_VALID);
-  HIP_OK(c, launch_is_valid(t->args.valid, t->args.limit, d_mass, d_thr, n, tol, prec, d_out, c->stream));
+  HIP_OK(c, launch_is_valid(t->args.valid, t->args.limit, t->args.full_lo, t->args.full_hi, t->args.first_reach, d_mass,
+                            d_thr, n, tol, prec, d_out, c->stream));
   return SST_OK;
 }
 

@@ -51,6 +51,8 @@ struct TableArgs {
   uint64_t capz0, capz1;    // row masks with cap <= 0
   uint64_t capneg0, capneg1;  // row masks with cap < 0
   int64_t fast_limit_B;     // max window value for which no per-row cap can bind
+  int64_t full_lo, full_hi;  // every mass in [full_lo, full_hi) is reachable (pair(N-1, m) != 0)
+  int64_t first_reach;       // smallest reachable mass >= 1
   int64_t shallow_hi;       // window values < shallow_hi (= 4 * w_min) fit in <= 3 items
   // LDS pair list: every 1- and 2-item sum of the alphabet, sorted by
   // (sum, top row); entries {sum, top_row << 8 | low_row (0xFF: single)}.
@@ -151,8 +153,9 @@ hipError_t launch_row_literal(int C, const uint64_t* Rprev, int64_t ncols, int s
                               uint64_t* Rout, hipStream_t st);
 hipError_t launch_index(int C, const void* packed, int n_rows, int64_t ncols, int64_t M, ulonglong2* index,
                         uint64_t* valid, int* err, hipStream_t st);
-hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, const double* mass, const double* thr, int64_t n,
-                           double tol, double prec, int8_t* out, hipStream_t st);
+hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, int64_t full_lo, int64_t full_hi, int64_t first_reach,
+                           const double* mass, const double* thr, int64_t n, double tol, double prec, int8_t* out,
+                           hipStream_t st);
 hipError_t launch_explain_scan(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
                                hipStream_t st);
 hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,

@@ -142,12 +142,14 @@ __device__ __forceinline__ int count_bits(const uint64_t* valid, int64_t a, int6
 
 // is_valid_mass semantics (mass_explanation.py:63-88): ascending scan, skip
 // v <= 0, raise at the first v >= limit, True at the first reachable v.
-__device__ __forceinline__ int8_t valid_window(const uint64_t* valid, int64_t limit, int64_t lo, int64_t hi) {
+__device__ __forceinline__ int8_t valid_window(const uint64_t* valid, int64_t limit, int64_t lo, int64_t hi,
+                                               int64_t full_lo = 1, int64_t full_hi = 1, int64_t first_reach = 0) {
   if (hi < lo) return 0;
   int64_t a = lo < 1 ? 1 : lo;
   if (a > hi) return 0;
   int64_t b = hi < limit - 1 ? hi : limit - 1;
-  if (a <= b && any_bits(valid, a, b)) return 1;
+  if (a <= b && b >= full_lo && a < full_hi) return 1;  // meets the all-reachable run: no bitset load
+  if (a <= b && b >= first_reach && any_bits(valid, a, b)) return 1;  // below first_reach: nothing reachable
   return hi >= limit ? (int8_t)-1 : (int8_t)0;
 }
 
@@ -354,15 +356,15 @@ __global__ void k_index(const void* __restrict__ packed, int n_rows, int64_t nco
 // with input prefetch, and 4 queries per lane with independent word loads,
 // were both slower -- the kernel is bound by scattered L2 requests, not by
 // dependent latency.)
-__global__ __launch_bounds__(256) void k_is_valid(const uint64_t* __restrict__ valid, int64_t limit,
-                                                  const double* __restrict__ mass, const double* __restrict__ thr,
-                                                  int64_t n, double tol, double prec, double rprec,
-                                                  int8_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_is_valid(const uint64_t* __restrict__ valid, int64_t limit, int64_t full_lo,
+                                                  int64_t full_hi, int64_t first_reach, const double* __restrict__ mass,
+                                                  const double* __restrict__ thr, int64_t n, double tol, double prec,
+                                                  double rprec, int8_t* __restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   int64_t lo, hi;
   quantise(mass[i], thr ? thr[i] : 0.0, thr == nullptr, tol, prec, rprec, lo, hi);
-  out[i] = valid_window(valid, limit, lo, hi);
+  out[i] = valid_window(valid, limit, lo, hi, full_lo, full_hi, first_reach);
 }
 
 // ---------------------------------------------------------------------------
@@ -1985,11 +1987,12 @@ hipError_t launch_index(int C, const void* packed, int n_rows, int64_t ncols, in
   }
   return hipGetLastError();
 }
-hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, const double* mass, const double* thr, int64_t n,
-                           double tol, double prec, int8_t* out, hipStream_t st) {
+hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, int64_t full_lo, int64_t full_hi, int64_t first_reach,
+                           const double* mass, const double* thr, int64_t n, double tol, double prec, int8_t* out,
+                           hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_is_valid, dim3(blocks_for(n, 256)), dim3(256), 0, st, valid, limit, mass, thr, n,
-                     tol, prec, 1.0 / prec, out);
+  hipLaunchKernelGGL(k_is_valid, dim3(blocks_for(n, 256)), dim3(256), 0, st, valid, limit, full_lo, full_hi,
+                     first_reach, mass, thr, n, tol, prec, 1.0 / prec, out);
   return hipGetLastError();
 }
 size_t scan_dyn_lds(const TableArgs& t) {
