@@ -223,14 +223,17 @@ int build_pair_list(sst_table* t, bool self_built) {
   std::vector<E> e;
   for (int r1 = 1; r1 < t->n_rows; ++r1) {
     if (t->masses[r1] <= 0) return SST_OK;  // zero-mass rows: leave the general path in charge
-    e.push_back({(uint32_t)t->masses[r1], ((uint32_t)r1 << 8) | 0xFFu});
+    // entries carry their payload record serialised: [1][top] or [2][low][top]
+    e.push_back({(uint32_t)t->masses[r1], 1u | ((uint32_t)r1 << 8)});
     for (int r2 = 1; r2 <= r1; ++r2) {
       int64_t s = t->masses[r1] + t->masses[r2];
       if (s >= t->args.pair_hi || s >= t->M) continue;  // never inside a pair-class window
-      e.push_back({(uint32_t)s, ((uint32_t)r1 << 8) | (uint32_t)r2});
+      e.push_back({(uint32_t)s, 2u | ((uint32_t)r2 << 8) | ((uint32_t)r1 << 16)});
     }
   }
-  std::sort(e.begin(), e.end(), [](const E& x, const E& y) { return x.sum != y.sum ? x.sum < y.sum : x.rows < y.rows; });
+  // the reference's order: ascending sum, then ascending top row
+  auto top = [](const E& x) { return (x.rows & 0xFFu) == 1u ? (x.rows >> 8) & 0xFFu : x.rows >> 16; };
+  std::sort(e.begin(), e.end(), [&](const E& x, const E& y) { return x.sum != y.sum ? x.sum < y.sum : top(x) < top(y); });
   if (e.empty() || e.size() > 65535) return SST_OK;
   // finest buckets (fewest entries skipped per lookup) that still fit the LDS budget
   const int64_t max_sum = e.back().sum;

@@ -55,7 +55,8 @@ struct TableArgs {
   int64_t first_reach;       // smallest reachable mass >= 1
   int64_t shallow_hi;       // window values < shallow_hi (= 4 * w_min) fit in <= 3 items
   // LDS pair list: every 1- and 2-item sum of the alphabet, sorted by
-  // (sum, top row); entries {sum, top_row << 8 | low_row (0xFF: single)}.
+  // (sum, top row); entries {sum, serialised payload record k | rows << 8,
+  // i.e. [1][top] or [2][low][top], k + 1 bytes}.
   // Valid only for tables known to follow the reference recurrence over
   // exactly these masses (built here); window values < pair_hi (= 3 * w_min)
   // have no candidate with more than 2 items.

@@ -968,24 +968,21 @@ __device__ __forceinline__ PairHit pair_count(const uint2* ent, const uint16_t* 
     const uint2 e = ent[k];
     if (e.x > b) break;
     h.count++;
-    h.bytes += (e.y & 0xFFu) == 0xFFu ? 2u : 3u;  // [1][top] or [2][low][top]
+    h.bytes += (e.y & 0xFFu) + 1u;  // [1][top] or [2][low][top]
   }
   return h;
 }
+// Records are pre-serialised in the list: per candidate a 16-bit store of
+// bytes 0-1 and a byte store of byte len-1 (for 2-byte records that rewrites
+// byte 1 with the same value) -- two stores, no branches.
 __device__ __forceinline__ void pair_write(const uint2* ent, const PairHit& h, uint8_t* dst) {
+#pragma unroll 1
   for (uint32_t k = h.first; k < h.first + h.count; ++k) {
-    const uint32_t y = ent[k].y;
-    const uint32_t lo_row = y & 0xFFu, top = y >> 8;
-    if (lo_row == 0xFFu) {
-      dst[0] = 1;
-      dst[1] = (uint8_t)top;
-      dst += 2;
-    } else {
-      dst[0] = 2;
-      dst[1] = (uint8_t)lo_row;
-      dst[2] = (uint8_t)top;
-      dst += 3;
-    }
+    const uint32_t rec = ent[k].y;
+    const uint32_t len = (rec & 0xFFu) + 1u;
+    *(uint16_t*)dst = (uint16_t)rec;
+    dst[len - 1u] = (uint8_t)(rec >> (8u * (len - 1u)));
+    dst += len;
   }
 }
 
