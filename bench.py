@@ -137,6 +137,9 @@ def main():
     ap.add_argument("--spectra", type=int, default=10000, help="spectra per GPU")
     ap.add_argument("--seed", type=int, default=1000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo: rehearsal of the "
+                         "multi-rank path, e.g. several ranks on one GPU with SST_DEVICE=0)")
     ap.add_argument("--gather", action="store_true",
                     help="N>1: gather every query's result to rank 0 over RCCL inside the timed step")
     ap.add_argument("--no-events", action="store_true",
@@ -155,15 +158,19 @@ def main():
     rank, world, local = dist_env()
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev_t = torch.device("cuda", local)
+    gpu = int(os.environ.get("SST_DEVICE", local))  # one GPU per rank (override: rehearsal on one card)
+    torch.cuda.set_device(gpu)
+    dev_t = torch.device("cuda", gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev_t)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev_t)
+        else:
+            dist.init_process_group("gloo")
 
-    engine = _native.get_engine(local)
+    engine = _native.get_engine(gpu)
     seq = SequenceInformation(max_len=20, su_mass=6500.0, obs_mass=6500.0, modification_rate=0.5)
     dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
                                  precision=TOLERANCE, seq=seq, engine=engine)
