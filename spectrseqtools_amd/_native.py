@@ -46,11 +46,32 @@ class EngineError(RuntimeError):
     pass
 
 
+def _share_hip_runtime_with_torch():
+    """One HIP runtime per process.  PyTorch-ROCm wheels bundle their own
+    libamdhip64 (same SONAME, libamdhip64.so.7, as /opt/rocm's) and load it
+    by its unversioned name: if this library loaded /opt/rocm's copy first, a
+    later torch import would load a second runtime that sees no GPU.  When
+    torch is installed, pre-load its copy (by path, without importing torch)
+    so that libsstgpu.so and torch bind to the same runtime in either order."""
+    try:
+        import importlib.util
+
+        spec = importlib.util.find_spec("torch")
+        if spec is None or not spec.origin:
+            return
+        hip = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+        if os.path.exists(hip):
+            ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+    except OSError:
+        pass
+
+
 def load_library(path=LIB_PATH):
     if not os.path.exists(path):
         raise ImportError(
             f"{path} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()' "
             "or make -C spectrseqtools_amd/csrc)")
+    _share_hip_runtime_with_torch()
     lib = ctypes.CDLL(path)
     lib.sst_device_count.restype = _I
     lib.sst_ctx_create.argtypes = [_I, _PP]
