@@ -83,7 +83,7 @@ struct sst_table {
   std::vector<int64_t> masses;
   std::vector<uint8_t> is_mod;
   std::vector<int64_t> cap;
-  DevBuf packed, index, valid, w, capd, modd, pairs, pair_bucket;
+  DevBuf packed, index, valid, w, capd, modd, pairs;
   int scan_blocks = 0;  // resident workgroups of k_explain_scan (depends on the LDS pair list size)
   bool closure = false;  // built here from masses >= C: rows are true closures (layered fast paths valid)
   TableArgs args{};
@@ -234,27 +234,40 @@ int build_pair_list(sst_table* t, bool self_built) {
   // the reference's order: ascending sum, then ascending top row
   auto top = [](const E& x) { return (x.rows & 0xFFu) == 1u ? (x.rows >> 8) & 0xFFu : x.rows >> 16; };
   std::sort(e.begin(), e.end(), [&](const E& x, const E& y) { return x.sum != y.sum ? x.sum < y.sum : top(x) < top(y); });
-  if (e.empty() || e.size() > 65535) return SST_OK;
-  // finest buckets (fewest entries skipped per lookup) that still fit the LDS budget
-  const int64_t max_sum = e.back().sum;
+  if (e.empty() || e.size() > 65533) return SST_OK;
+  const size_t n_e = e.size(), n_s = n_e + 2;  // + two sentinels: the walk reads two entries per step
+  // Buckets start at w_min (no sum below it) and cover every window start
+  // below pair_hi, so a pair-class window needs no bucket bound check; the
+  // finest buckets that fit the LDS budget.
+  const int64_t base = t->args.w_min, span = t->args.pair_hi - base;
+  if (span <= 0) return SST_OK;
   int shift = 4;
-  while (shift < 16 && e.size() * 8 + (size_t)((max_sum >> shift) + 2) * 2 > (size_t)kMaxPairLds) ++shift;
-  const int64_t n_b = (max_sum >> shift) + 1;
-  if (e.size() * 8 + (size_t)(n_b + 1) * 2 > (size_t)kMaxPairLds) return SST_OK;
-  std::vector<uint16_t> bst(n_b + 1);
+  while (shift < 16 && (2 * n_s + (size_t)(((span - 1) >> shift) + 1)) * 4 > (size_t)kMaxPairLds) ++shift;
+  const int64_t n_b = ((span - 1) >> shift) + 1;
+  if ((2 * n_s + (size_t)n_b) * 4 > (size_t)kMaxPairLds) return SST_OK;
+  std::vector<uint32_t> img(2 * n_s + n_b);
+  uint32_t* sums = img.data();
+  uint32_t* recs = sums + n_s;
+  uint32_t* bk = recs + n_s;
+  for (size_t k = 0; k < n_e; ++k) {
+    sums[k] = e[k].sum << 1 | ((e[k].rows & 0xFFu) == 2u ? 1u : 0u);
+    recs[k] = e[k].rows;
+  }
+  sums[n_e] = sums[n_e + 1] = UINT32_MAX;
+  recs[n_e] = recs[n_e + 1] = 0;
   size_t k = 0;
-  for (int64_t b = 0; b <= n_b; ++b) {
-    while (k < e.size() && (int64_t)(e[k].sum >> shift) < b) ++k;
-    bst[b] = (uint16_t)k;
+  for (int64_t b = 0; b < n_b; ++b) {
+    const int64_t start = base + (b << shift);
+    while (k < n_e && (int64_t)e[k].sum < start) ++k;
+    const int64_t delta = k < n_e ? std::min<int64_t>((int64_t)e[k].sum - start, 0xFFFF) : 0xFFFF;
+    bk[b] = (uint32_t)k | (uint32_t)delta << 16;
   }
   t->args.pair_shift = shift;
-  if (!t->pairs.ensure(e.size() * 8) || !t->pair_bucket.ensure((n_b + 1) * 2))
-    return fail(c, SST_E_NOMEM, "device allocation failed (pair list)");
-  HIP_OK(c, hipMemcpy(t->pairs.p, e.data(), e.size() * 8, hipMemcpyHostToDevice));
-  HIP_OK(c, hipMemcpy(t->pair_bucket.p, bst.data(), (n_b + 1) * 2, hipMemcpyHostToDevice));
-  t->args.pairs = (const uint2*)t->pairs.p;
-  t->args.pair_bucket = (const uint16_t*)t->pair_bucket.p;
-  t->args.n_pairs = (int)e.size();
+  if (!t->pairs.ensure(img.size() * 4)) return fail(c, SST_E_NOMEM, "device allocation failed (pair list)");
+  HIP_OK(c, hipMemcpy(t->pairs.p, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+  t->args.pair_data = (const uint32_t*)t->pairs.p;
+  t->args.pair_base = (uint32_t)base;
+  t->args.n_pairs = (int)n_e;
   t->args.n_buckets = (int)n_b;
   t->args.pairs_enabled = 1;
   return SST_OK;
@@ -411,6 +424,10 @@ int sst_table_build(sst_ctx* c, const int64_t* masses, int n_rows, int64_t max_m
   t->C = C;
   t->n_cols = table_cols(max_mass, C);
   t->M = t->n_cols * C;
+  if (t->M > (int64_t)INT32_MAX) {  // the query kernels hold window values in u32
+    delete t;
+    return fail(c, SST_E_ARG, "table would cover masses beyond 2^31 - 1");
+  }
   t->masses.assign(masses, masses + n_rows);
   const int64_t M = t->M, rw = (M + 63) / 64;
   DevBuf R, tmp, wdev;
@@ -476,6 +493,7 @@ int sst_table_upload(sst_ctx* c, const int64_t* masses, int n_rows, const void* 
   *out = nullptr;
   if (int rc = check_masses(c, masses, n_rows)) return rc;
   if (!valid_C(C) || n_cols < 1) return fail(c, SST_E_ARG, "bad compression or n_cols");
+  if (n_cols > (int64_t)INT32_MAX / C) return fail(c, SST_E_ARG, "table covers masses beyond 2^31 - 1");
   if (int rc = set_device(c)) return rc;
   sst_table* t = new sst_table();
   t->ctx = c;
@@ -575,7 +593,7 @@ void sst_table_destroy(sst_table* t) {
   std::lock_guard<std::recursive_mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&t->packed, &t->index, &t->valid, &t->w, &t->capd, &t->modd, &t->pairs, &t->pair_bucket})
+  for (DevBuf* b : {&t->packed, &t->index, &t->valid, &t->w, &t->capd, &t->modd, &t->pairs})
     b->release();
   delete t;
 }
@@ -676,6 +694,19 @@ int ensure_exact_ws(sst_ctx* c, uint32_t hash_cap, int lanes) {
   return SST_OK;
 }
 
+// The scalar budget folded into the scan's u32 limits.  With A0 =
+// clamp(max_mods_scalar), budgets_never_bind(hi, A0) holds iff
+// hi < never_lim and (no mod rows, A0 = inf, or hi < (A0 + 1) * w_min_mod);
+// window values are < 2^31, so clamping the products to u32 is exact.
+void fold_scan_limits(const TableArgs& a, QueryArgs& q) {
+  const int64_t A0 = q.max_mods_scalar < 0 ? (int64_t)kInfBudget : std::min<int64_t>(q.max_mods_scalar, kInfBudget);
+  uint64_t a0lim = UINT32_MAX;
+  if (a.any_mod && A0 < kInfBudget) a0lim = std::min<uint64_t>((uint64_t)(A0 + 1) * (uint64_t)a.w_min_mod, UINT32_MAX);
+  q.pair_hi_lim = (uint32_t)std::min<uint64_t>(a.pair_lim, a0lim);
+  q.never_hi_lim = (uint32_t)std::min<uint64_t>(a.never_lim, a0lim);
+  q.cap32 = (uint32_t)std::min<uint64_t>(q.cap_count, UINT32_MAX);
+}
+
 // one pass of the explain pipeline on device buffers
 int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double* d_thr, const int64_t* d_mods,
                  int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count) {
@@ -699,6 +730,7 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
     if (int rc = ensure_exact_ws(c, kHashCap0, kExactLanes0)) return rc;
   r->compacted = false;
   QueryArgs q{d_mass, d_thr, d_mods, mods_scalar, n, tol, prec, 1.0 / prec, with_memo, cap_count, kNodeBudget};
+  fold_scan_limits(t->args, q);
   OutArgs o = out_args(r);
   {
     Prof p(c, SST_K_EXPLAIN_MAIN);

@@ -15,7 +15,7 @@ constexpr int kMaxDepth = 96;      // >= max items of any multiset in a table (7
 constexpr int kInfBudget = 1 << 30;  // np.inf budget (decremented at most kMaxDepth times)
 constexpr int kScanWG = 1024;        // scan kernel workgroup (2 per CU share the LDS pair list)
 constexpr int kMaxSingletonMasses = 1024;  // is_singleton: integer masses staged in LDS
-constexpr int kMaxPairLds = 78 * 1024;  // pair list + buckets: two scan workgroups per CU (160 KB LDS)
+constexpr int kMaxPairLds = 78 * 1024;  // pair-list image: two scan workgroups per CU (160 KB LDS)
 // worklist item flags ({query, a, b, flags}): v == 0 lies in the window; the
 // window was not classified by the scan (the expand kernel checks the bitset
 // and routes it); budgets cannot bind (fast-path theorem)
@@ -55,17 +55,21 @@ struct TableArgs {
   int64_t first_reach;       // smallest reachable mass >= 1
   int64_t shallow_hi;       // window values < shallow_hi (= 4 * w_min) fit in <= 3 items
   // LDS pair list: every 1- and 2-item sum of the alphabet, sorted by
-  // (sum, top row); entries {sum, serialised payload record k | rows << 8,
-  // i.e. [1][top] or [2][low][top], k + 1 bytes}.
+  // (sum, top row), as one u32 image staged to LDS whole:
+  //   sums[n_pairs + 2]  sum << 1 | (record is a pair), two UINT32_MAX sentinels
+  //   recs[n_pairs + 2]  serialised payload record: [1][top] or [2][low][top]
+  //   bk[n_buckets]      bucket b covers masses pair_base + [b, b+1) << pair_shift:
+  //                      bits 0-15 first entry with sum >= the bucket start,
+  //                      bits 16-31 that sum minus the bucket start (clamped)
   // Valid only for tables known to follow the reference recurrence over
   // exactly these masses (built here); window values < pair_hi (= 3 * w_min)
   // have no candidate with more than 2 items.
-  const uint2* pairs;
-  const uint16_t* pair_bucket;  // [n_buckets + 1] first entry with sum >= k << pair_shift
+  const uint32_t* pair_data;
   int64_t pair_hi;
   int n_pairs;
   int n_buckets;
   int pair_shift;
+  uint32_t pair_base;  // = w_min: no sum lies below it
   // u32 forms of the fast-path limits (window values are < 2^31):
   // hi < never_lim  <=>  hi <= fast_limit_B (no per-row cap binds);
   // hi < pair_lim   <=>  pair-list window with no per-row cap binding
@@ -88,6 +92,10 @@ struct QueryArgs {
   int with_memo;
   uint64_t cap_count;
   uint64_t node_budget;
+  // pair-list scan, folded on the host (fold_scan_limits): with one scalar
+  // budget, hi < pair_hi_lim <=> pair-class window whose budgets cannot bind,
+  // hi < never_hi_lim <=> fast-path theorem; cap32 = min(cap_count, 2^32-1)
+  uint32_t pair_hi_lim = 0, never_hi_lim = 0, cap32 = 0;
 };
 
 // Arena layout of one explain pass:
@@ -116,6 +124,16 @@ struct OutArgs {
   uint32_t* counters;  // [kNumClasses]
   uint32_t* lists;     // [kNumClasses][n]
   unsigned long long* stats;  // [kNumStats] deferred-kernel counters
+};
+
+struct ValidArgs {  // is_valid_mass batch
+  const uint64_t* valid;
+  int64_t limit, full_lo, full_hi, first_reach;
+  const double* mass;
+  const double* thr;  // may be null: tolerance * mass
+  int64_t n;
+  double tol, prec, rprec;
+  int8_t* out;
 };
 
 struct LBArgs {

@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "sst_internal.h"
 
 namespace sst {
@@ -115,6 +117,29 @@ __device__ __forceinline__ void quantise(double mass, double thr_abs, bool thr_n
   const int64_t th = (int64_t)ceil_quot(t, prec, rprec);
   lo = target - th;
   hi = target + th;
+}
+
+// Window of one query as exact f64 integers: target = rint(mass / prec) and
+// thr = ceil(thr_abs / prec) (mass_explanation.py:107,110-114).  Both
+// quotients are taken as x * (1/prec), within 2.5 ulp of the exact one; the
+// correctly rounded division runs only when a product lies within 2^-50
+// (relative) of a point where rint / ceil change value, or is huge, so the
+// integers are exactly the reference's.  Straight-line except for that rare
+// fallback (the lean form of rint_quot / ceil_quot).
+__device__ __forceinline__ void quantise_lean(double m, double t, double prec, double rprec, double& lof,
+                                              double& hif) {
+  const double qm = m * rprec, qt = t * rprec;
+  double rm = __builtin_rint(qm), ct = __builtin_ceil(qt);
+  const double dm = qm - rm, dt = qt - __builtin_rint(qt);  // exact
+  const bool slow = !(__builtin_fabs(qm) < 0x1p40) | !(__builtin_fabs(qt) < 0x1p40) |
+                    (0.5 - __builtin_fabs(dm) <= __builtin_fabs(qm) * 0x1p-50) |
+                    (__builtin_fabs(dt) <= __builtin_fabs(qt) * 0x1p-50);
+  if (__builtin_expect(slow, 0)) {
+    rm = __builtin_rint(m / prec);
+    ct = __builtin_ceil(t / prec);
+  }
+  lof = rm - ct;
+  hif = rm + ct;
 }
 
 // any bit of valid in [a, b] (a <= b, both < limit)
@@ -350,21 +375,33 @@ __global__ void k_index(const void* __restrict__ packed, int n_rows, int64_t nco
 // ---------------------------------------------------------------------------
 // is_valid batch
 // ---------------------------------------------------------------------------
-// One query per lane.  Most A7 windows are reachable in their first bitset
-// word, so the words are scanned with an early exit (valid_window): about one
-// scattered L2 load per query.  (Measured alternatives: a persistent grid
-// with input prefetch, and 4 queries per lane with independent word loads,
-// were both slower -- the kernel is bound by scattered L2 requests, not by
-// dependent latency.)
-__global__ __launch_bounds__(256) void k_is_valid(const uint64_t* __restrict__ valid, int64_t limit, int64_t full_lo,
-                                                  int64_t full_hi, int64_t first_reach, const double* __restrict__ mass,
-                                                  const double* __restrict__ thr, int64_t n, double tol, double prec,
-                                                  double rprec, int8_t* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int64_t lo, hi;
-  quantise(mass[i], thr ? thr[i] : 0.0, thr == nullptr, tol, prec, rprec, lo, hi);
-  out[i] = valid_window(valid, limit, lo, hi, full_lo, full_hi, first_reach);
+// is_valid_mass (mass_explanation.py:45-89), one query per lane.  Windows
+// meeting the all-reachable run or lying wholly below the first reachable
+// mass need no bitset word; most others are decided by their first word
+// (the rest scan on with an early exit): about one scattered L2 load per
+// query.  (Measured alternatives, all slower: a persistent grid with the next
+// tile's inputs in flight -- with and without the bitset load ordered ahead
+// of the prefetch --, and 4 queries per lane with independent word loads.
+// The kernel is bound by its dependent load chain per wave, and a fresh wave
+// per tile overlaps those chains best.)
+template <bool THR>
+__global__ __launch_bounds__(256) void k_is_valid(ValidArgs v) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= (uint32_t)v.n) return;
+  const double m = v.mass[i];
+  const double t = THR ? v.thr[i] : v.tol * m;
+  double lof, hif;
+  quantise_lean(m, t, v.prec, v.rprec, lof, hif);
+  // ascending scan of the window (:63-88): skip v <= 0, True at the first
+  // reachable v, raise at the first v >= limit
+  const double af = __builtin_fmax(lof, 1.0);
+  const bool act = lof <= hif && af <= hif;
+  const double bf = __builtin_fmin(hif, (double)(v.limit - 1));
+  const bool inr = act && af <= bf;  // the window meets [1, limit)
+  const bool full = inr && bf >= (double)v.full_lo && af < (double)v.full_hi;
+  bool hit = full;
+  if (inr && !full && bf >= (double)v.first_reach) hit = any_bits(v.valid, (uint32_t)af, (uint32_t)bf);
+  v.out[i] = hit ? (int8_t)1 : (act && hif >= (double)v.limit ? (int8_t)-1 : (int8_t)0);
 }
 
 // ---------------------------------------------------------------------------
@@ -950,42 +987,6 @@ __device__ __forceinline__ bool window_has_roots(const uint64_t* valid, int64_t 
   return any_bits(valid, a, b);
 }
 
-// <= 2-item candidates of the window [a, b] from the LDS pair list, in the
-// reference's order (ascending v, then ascending top row): the entries
-// [first, first + count) of the sorted list.
-struct PairHit {
-  uint32_t first, count, bytes;
-};
-__device__ __forceinline__ PairHit pair_count(const uint2* ent, const uint16_t* bst, int n_ent, int n_b, int shift,
-                                              uint32_t a, uint32_t b) {
-  PairHit h{0, 0, 0};
-  const uint32_t ba = a >> shift;
-  if (ba >= (uint32_t)n_b) return h;
-  int k = bst[ba];
-  while (k < n_ent && ent[k].x < a) ++k;
-  h.first = (uint32_t)k;
-  for (; k < n_ent; ++k) {
-    const uint2 e = ent[k];
-    if (e.x > b) break;
-    h.count++;
-    h.bytes += (e.y & 0xFFu) + 1u;  // [1][top] or [2][low][top]
-  }
-  return h;
-}
-// Records are pre-serialised in the list: per candidate a 16-bit store of
-// bytes 0-1 and a byte store of byte len-1 (for 2-byte records that rewrites
-// byte 1 with the same value) -- two stores, no branches.
-__device__ __forceinline__ void pair_write(const uint2* ent, const PairHit& h, uint8_t* dst) {
-#pragma unroll 1
-  for (uint32_t k = h.first; k < h.first + h.count; ++k) {
-    const uint32_t rec = ent[k].y;
-    const uint32_t len = (rec & 0xFFu) + 1u;
-    *(uint16_t*)dst = (uint16_t)rec;
-    dst[len - 1u] = (uint8_t)(rec >> (8u * (len - 1u)));
-    dst += len;
-  }
-}
-
 // Inclusive wavefront prefix sum of a u32 on the DPP crossbar (no LDS
 // round trips): 16-lane row scans, then rows 1/3 and 2/3 take the running
 // totals of the rows before them through row_bcast:15 / row_bcast:31.
@@ -1030,31 +1031,6 @@ __device__ __forceinline__ TileOut tile_alloc(const OutArgs& out, int lane, uint
   return r;
 }
 
-// tile_alloc for the scan kernel: 32-bit sizes (regions are small; a tile
-// writes < 4 GB), the prefix sum on DPP.
-__device__ __forceinline__ TileOut tile_alloc32(const OutArgs& out, uint64_t region0, uint32_t& used, uint32_t bytes,
-                                                int8_t status) {
-  const uint32_t incl = wave_incl_scan32(bytes);
-  const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  uint64_t base = 0;
-  if (total) {
-    if ((uint64_t)used + total <= out.region_bytes) {
-      base = region0 + used;
-      used += total;
-    } else {
-      unsigned long long sb = 0;
-      if ((threadIdx.x & 63) == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
-      base = out.spill_base + (uint64_t)__shfl(sb, 0, 64);
-    }
-  }
-  TileOut r{base + incl - bytes, bytes, status};
-  if (bytes && r.off + bytes > out.arena_bytes) {
-    r.status = (int8_t)kStatusArenaRetry;
-    r.bytes = 0;
-  }
-  return r;
-}
-
 __device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t region, int lane, uint64_t used,
                                                  int q_stat, int p_stat, uint64_t n_q, uint64_t nodes,
                                                  uint64_t payload) {
@@ -1073,81 +1049,220 @@ __device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t reg
   }
 }
 
-// 8 waves/SIMD: two 1024-lane workgroups per CU, each with its LDS copy of
-// the pair list (<= 78 KB).
-// PAIRS: the table carries the LDS pair list (tables built here).  Windows
-// below 3 * w_min whose budgets cannot bind are answered from LDS; every other
-// non-empty window goes to the expand kernel unclassified, which keeps this
-// kernel's live state (and its SGPRs) to the pair path.  Without the list,
-// every non-empty window is checked against the valid bitset here.
-template <bool PAIRS>
-__global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
-  extern __shared__ uint2 lds_pairs[];
-  const uint16_t* lds_bucket = (const uint16_t*)(lds_pairs + t.n_pairs);
-  if (blockIdx.x == 0 && threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
-  if (PAIRS) {
-    for (int k = threadIdx.x; k < t.n_pairs; k += blockDim.x) lds_pairs[k] = t.pairs[k];
-    uint16_t* bw = (uint16_t*)(lds_pairs + t.n_pairs);
-    for (int k = threadIdx.x; k <= t.n_buckets; k += blockDim.x) bw[k] = t.pair_bucket[k];
-    __syncthreads();
+// Candidates of a pair-class window [a, hi] from the LDS pair list (layout:
+// TableArgs::pair_data): the entries with sums in the window, in list order
+// (= the reference's order).  The window's bucket word holds the first sum at
+// or after the bucket start, which settles most empty windows with that one
+// 4-byte read; the rest walk the sums array two entries per LDS round trip up
+// to the first sum above hi (the sentinels bound the walk).  Sums carry the
+// record kind in bit 0, so the walk compares against 2a and 2hi+1 and reads no
+// records.  Returns the count, the first entry and the payload bytes
+// ([1][top] = 2 B, [2][low][top] = 3 B).
+struct PairLds {
+  const uint32_t* sums;
+  const uint32_t* recs;
+  const uint32_t* bk;
+  uint32_t base;
+  int shift;
+};
+__device__ __forceinline__ uint32_t pair_walk(const PairLds& p, uint32_t a, uint32_t hi, uint32_t& first,
+                                              uint32_t& bytes) {
+  const uint32_t rel = a > p.base ? a - p.base : 0u;
+  const uint32_t bw = p.bk[rel >> p.shift];
+  uint32_t k = bw & 0xFFFFu, cnt = 0, nb = 0;
+  if (p.base + ((rel >> p.shift) << p.shift) + (bw >> 16) <= hi) {
+    const uint32_t a2 = a << 1, h2 = (hi << 1) | 1u;
+    for (;;) {
+      const uint32_t e0 = p.sums[k], e1 = p.sums[k + 1];
+      const bool s0 = e0 <= h2, s1 = s0 && e1 <= h2;  // sorted: still inside the walk
+      const bool in0 = s0 && e0 >= a2, in1 = s1 && e1 >= a2;
+      cnt += (in0 ? 1u : 0u) + (in1 ? 1u : 0u);
+      nb += (in0 ? 2u + (e0 & 1u) : 0u) + (in1 ? 2u + (e1 & 1u) : 0u);
+      k += (s0 ? 1u : 0u) + (s1 ? 1u : 0u);
+      if (!s1) break;
+    }
   }
+  first = k - cnt;  // the in-window entries end the walk
+  bytes = nb;
+  return cnt;
+}
+__device__ __forceinline__ void pair_store(const PairLds& p, uint32_t first, uint32_t cnt, uint8_t* dst) {
+#pragma unroll 1
+  for (uint32_t k = first; k < first + cnt; ++k) {
+    const uint32_t rec = p.recs[k];
+    const uint32_t len = (rec & 0xFFu) + 1u;
+    *(uint16_t*)dst = (uint16_t)rec;
+    dst[len - 1u] = (uint8_t)(rec >> (8u * (len - 1u)));
+    dst += len;
+  }
+}
+
+// 8 waves/SIMD: two 1024-lane workgroups per CU, each with its LDS copy of
+// the pair list (<= 78 KB).  Tables built here carry the list: a window below
+// 3 * w_min whose budgets cannot bind is answered from LDS; every other
+// non-empty window goes to the expand kernel unclassified.
+// THR: per-query thresholds given (else tol * mass).  MODS: per-query budgets
+// given (else the host folded the scalar budget into q.pair_hi_lim /
+// q.never_hi_lim, fold_scan_limits).  The classification is branch-free on
+// exact f64 integers, then u32 (a window inside the table lies in
+// [0, limit) with limit < 2^31); the per-tile cost is what bounds this kernel
+// (VALU-bound), so everything uniform is hoisted out of the loop.
+template <bool THR, bool MODS>
+__global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
+  extern __shared__ uint32_t lds_pair_img[];
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
+  const int n_img = 2 * (t.n_pairs + 2) + t.n_buckets;
+  for (int k = threadIdx.x; k < n_img; k += blockDim.x) lds_pair_img[k] = t.pair_data[k];
+  __syncthreads();
+  const PairLds pl{lds_pair_img, lds_pair_img + t.n_pairs + 2, lds_pair_img + 2 * (t.n_pairs + 2), t.pair_base,
+                   t.pair_shift};
   const int lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * (kScanWG / 64) + (threadIdx.x >> 6);
   const uint32_t n_waves = gridDim.x * (kScanWG / 64);
   const uint32_t n = (uint32_t)q.n;  // < 2^32 - 64 (host checks)
   const uint32_t ntiles = (n + 63) >> 6;
   const uint64_t region0 = (uint64_t)wave * out.region_bytes;  // scan waves own regions [0, n_scan_waves)
-  uint32_t used = 0;                                           // wave-uniform bump pointer
+  const double limitf = (double)t.limit;
+  uint32_t used = 0;  // wave-uniform bump pointer
   uint32_t st_q = 0, st_payload = 0;
   uint4* wl = out.work + (uint64_t)wave * out.work_region;
   uint32_t n_work = 0;  // wave-uniform
-  // software pipeline: the next tile's inputs are in flight while this tile
-  // does its LDS lookups (streamed once: nontemporal loads)
-  double m_nx = 0.0, t_nx = 0.0;
-  int64_t mm_nx = q.max_mods_scalar;
-  auto fetch = [&](uint32_t tl) {
-    const uint32_t j = tl * 64 + lane;
-    if (tl < ntiles && j < n) {
-      m_nx = __builtin_nontemporal_load(q.mass + j);
-      if (q.thr) t_nx = __builtin_nontemporal_load(q.thr + j);
-      if (q.max_mods) mm_nx = __builtin_nontemporal_load(q.max_mods + j);
+  // Software pipeline, two tiles deep: a tile's inputs are loaded two tiles
+  // ahead into one of two register sets that swap roles between the unrolled
+  // steps (no copies), and each load is issued AFTER the previous tile's
+  // stores.  The vmcnt counter retires in order, so the wait for a tile's
+  // inputs then covers the stores before them but never the newer prefetch.
+  // Loads are unconditional (index clamped to the last query), streamed once
+  // (nontemporal).
+  auto fetch = [&](uint32_t tl, double& m, double& tt, int64_t& mm) {
+    const uint32_t j = tl < ntiles ? min(tl * 64 + lane, n - 1) : n - 1;
+    m = __builtin_nontemporal_load(q.mass + j);
+    if (THR) tt = __builtin_nontemporal_load(q.thr + j);
+    if (MODS) mm = __builtin_nontemporal_load(q.max_mods + j);
+  };
+  auto step = [&](uint32_t tile, double m_in, double t_in, int64_t mm_cur) {
+    const uint32_t i = tile * 64 + lane;
+    const bool live = i < n;
+    const double m_cur = m_in, t_cur = THR ? t_in : q.tol * m_in;
+    double lof, hif;
+    quantise_lean(m_cur, t_cur, q.prec, q.rprec, lof, hif);
+    const bool nonempty = live && lof <= hif;
+    const bool oot = nonempty && !(hif < limitf);  // mass_explanation.py:134-138 (NameError)
+    const bool zero = nonempty && !oot && lof <= 0.0 && hif >= 0.0;  // v == 0 -> [[]] (:130-131)
+    const double af = __builtin_fmax(lof, 1.0);
+    const bool active = nonempty && !oot && af <= hif;
+    const uint32_t a = active ? (uint32_t)af : 0u, hi = active ? (uint32_t)hif : 0u;
+    bool pair, never;
+    if (MODS) {  // fast-path theorem per lane (budgets_never_bind on u32 values)
+      const int A0 = clamp_budget(mm_cur);
+      const bool a0ok =
+          !t.any_mod || A0 >= kInfBudget || (uint64_t)hi < (uint64_t)(A0 + 1) * (uint64_t)t.w_min_mod;
+      pair = active && a0ok && hi < t.pair_lim;
+      never = a0ok && hi < t.never_lim;
+    } else {
+      pair = active && hi < q.pair_hi_lim;
+      never = hi < q.never_hi_lim;
+    }
+    const bool work = active && !pair;  // classified (bitset, depth, budgets) by the expand kernel
+    uint32_t first = 0, cnt = 0, bytes = 0;
+    if (pair) cnt = pair_walk(pl, a, hi, first, bytes);
+    int8_t status = oot ? (int8_t)SST_OUT_OF_TABLE : (zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE);
+    if (cnt) status = cnt > q.cap32 ? (int8_t)SST_OVERFLOW : (int8_t)SST_SOME;
+    // payload: wavefront prefix sum, bump allocation in the wave's region
+    // (spill when full), records copied from LDS
+    uint32_t pb = status == SST_SOME ? bytes : 0u;
+    const uint32_t incl = wave_incl_scan32(pb);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    uint64_t off = 0;
+    bool retry = false;
+    if (total) {  // wave-uniform
+      uint64_t base;
+      if ((uint64_t)used + total <= out.region_bytes) {
+        base = region0 + used;
+        used += total;
+      } else {
+        unsigned long long sb = 0;
+        if (lane == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
+        base = out.spill_base + (uint64_t)__shfl(sb, 0, 64);
+      }
+      off = base + (incl - pb);
+      if (base + total > out.arena_bytes) {  // wave-uniform, rare: the arena is full, the host retries
+        retry = pb && off + pb > out.arena_bytes;
+        if (retry) pb = 0;
+      }
+      if (pb) pair_store(pl, first, cnt, out.payload + off);
+    }
+    st_payload += pb;
+    st_q += pair ? 1u : 0u;
+    // NONE / EMPTY / OUT_OF_TABLE carry no candidates: count and offset stay
+    // undefined (include/sst.h), one byte per resolved query
+    if (live && !work) {
+      out.status[i] = retry ? (int8_t)kStatusArenaRetry : status;
+      if (cnt && !retry) {  // SOME or OVERFLOW
+        out.count[i] = cnt;
+        out.offset[i] = pb ? off : 0;
+      }
+    }
+    const uint64_t bal = __ballot(work);
+    if (bal) {  // wave-uniform
+      if (work)
+        wl[n_work + __builtin_popcountll(bal & lane_mask_lt(lane))] =
+            make_uint4(i, a, hi, (zero ? kItemZero : 0u) | kItemUnclassified | (never ? kItemNever : 0u));
+      n_work += (uint32_t)__builtin_popcountll(bal);
     }
   };
-  fetch(wave);
+  double mA = 0.0, tA = 0.0, mB = 0.0, tB = 0.0;
+  int64_t mmA = q.max_mods_scalar, mmB = q.max_mods_scalar;
+  fetch(wave, mA, tA, mmA);
+  fetch(wave + n_waves, mB, tB, mmB);
+  for (uint32_t tile = wave; tile < ntiles; tile += 2 * n_waves) {
+    step(tile, mA, tA, mmA);
+    fetch(tile + 2 * n_waves, mA, tA, mmA);
+    if (tile + n_waves >= ntiles) break;
+    step(tile + n_waves, mB, tB, mmB);
+    fetch(tile + 3 * n_waves, mB, tB, mmB);
+  }
+  if (lane == 0) {
+    out.work_count[wave] = n_work;
+    if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle expand launch exit at once
+  }
+  wave_stats_flush(out, wave, lane, used, kStatPair, kStatPairPayload, st_q, 0, st_payload);
+}
+
+// Tables without the pair list (uploaded tables, literal-sweep rows): every
+// non-empty window is checked against the valid bitset here, then queued for
+// the expand kernel (<= 3 items) or the deferred class lists.
+__global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryArgs q, OutArgs out) {
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = blockIdx.x * (kScanWG / 64) + (threadIdx.x >> 6);
+  const uint32_t n_waves = gridDim.x * (kScanWG / 64);
+  const uint32_t n = (uint32_t)q.n;  // < 2^32 - 64 (host checks)
+  const uint32_t ntiles = (n + 63) >> 6;
+  uint4* wl = out.work + (uint64_t)wave * out.work_region;
+  uint32_t n_work = 0;  // wave-uniform
   for (uint32_t tile = wave; tile < ntiles; tile += n_waves) {
     const uint32_t i = tile * 64 + lane;
     const bool live = i < n;
-    const double m_cur = m_nx, t_cur = t_nx;
-    const int64_t mm_cur = mm_nx;
-    fetch(tile + n_waves);
-    // window classification, branch-free: exact f64 integers, then u32
-    // (a window inside the table lies in [0, limit) with limit < 2^31)
-    double lof, hif;
-    quantise_f(m_cur, t_cur, q.thr == nullptr, q.tol, q.prec, q.rprec, lof, hif);
+    double lof = 1.0, hif = 0.0;
+    int64_t mm = q.max_mods_scalar;
+    if (live) {
+      quantise_f(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lof, hif);
+      if (q.max_mods) mm = q.max_mods[i];
+    }
     const bool nonempty = live && lof <= hif;
     const bool oot = nonempty && !(hif < (double)t.limit);  // mass_explanation.py:134-138 (NameError)
     const bool zero = nonempty && !oot && lof <= 0.0 && hif >= 0.0;  // v == 0 -> [[]] (:130-131)
     const double af = lof < 1.0 ? 1.0 : lof;
     const bool active = nonempty && !oot && af <= hif;
     const uint32_t a = active ? (uint32_t)af : 0u, hi = active ? (uint32_t)hif : 0u;
-    // fast-path theorem (budgets_never_bind) on u32 window values
-    const int A0 = clamp_budget(mm_cur);
+    const int A0 = clamp_budget(mm);
     const bool a0ok = !t.any_mod || A0 >= kInfBudget || (uint64_t)hi < (uint64_t)(A0 + 1) * (uint64_t)t.w_min_mod;
     const bool never = hi < t.never_lim && a0ok;
     int8_t status = oot ? (int8_t)SST_OUT_OF_TABLE : (zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE);
-    bool work = false, pair = false;
+    bool work = false;
     uint4 item = make_uint4(0, 0, 0, 0);
-    PairHit ph{0, 0, 0};  // pair path: first entry, candidates, payload bytes
-    if (PAIRS) {
-      pair = active && a0ok && hi < t.pair_lim;
-      work = active && !pair;  // classified (bitset, depth, budgets) by the expand kernel
-      item = make_uint4(i, a, hi, (zero ? kItemZero : 0u) | kItemUnclassified | (never ? kItemNever : 0u));
-      if (pair) {
-        ph = pair_count(lds_pairs, lds_bucket, t.n_pairs, t.n_buckets, t.pair_shift, a, hi);
-        st_q++;
-      }
-      if (ph.count) status = ph.count > q.cap_count ? SST_OVERFLOW : SST_SOME;
-    } else if (active && window_has_roots(t.valid, a, hi)) {
+    if (active && window_has_roots(t.valid, a, hi)) {
       int cls;
       if (never) cls = hi < t.shallow_hi ? kClassShallow : kClassDeep;
       else cls = q.with_memo ? kClassExact : kClassNomemo;
@@ -1160,22 +1275,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
         status = (int8_t)kStatusPending;
       }
     }
-    if (PAIRS) {
-      const TileOut to = tile_alloc32(out, region0, used, status == SST_SOME ? ph.bytes : 0u, status);
-      if (to.bytes) pair_write(lds_pairs, ph, out.payload + to.off);
-      // NONE / EMPTY / OUT_OF_TABLE carry no candidates: count and offset stay
-      // undefined (include/sst.h), one byte per resolved query
-      if (live && !work) {
-        out.status[i] = to.status;
-        if (pair && (to.status == SST_SOME || to.status == SST_OVERFLOW)) {
-          out.count[i] = ph.count;
-          out.offset[i] = to.bytes ? to.off : 0;
-        }
-      }
-      st_payload += (uint32_t)to.bytes;
-    } else if (live && !work) {
-      out.status[i] = status;
-    }
+    if (live && !work) out.status[i] = status;
     const uint64_t bal = __ballot(work);
     if (work) wl[n_work + __builtin_popcountll(bal & lane_mask_lt(lane))] = item;
     n_work += (uint32_t)__builtin_popcountll(bal);
@@ -1184,7 +1284,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     out.work_count[wave] = n_work;
     if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle expand launch exit at once
   }
-  wave_stats_flush(out, wave, lane, used, kStatPair, kStatPairPayload, st_q, 0, st_payload);
+  wave_stats_flush(out, wave, lane, 0, kStatPair, kStatPairPayload, 0, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1988,21 +2088,32 @@ hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, int64_t full_lo
                            const double* mass, const double* thr, int64_t n, double tol, double prec, int8_t* out,
                            hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_is_valid, dim3(blocks_for(n, 256)), dim3(256), 0, st, valid, limit, full_lo, full_hi,
-                     first_reach, mass, thr, n, tol, prec, 1.0 / prec, out);
+  const int grid = (int)blocks_for(n, 256);
+  ValidArgs v{valid, limit, full_lo, full_hi, first_reach, mass, thr, n, tol, prec, 1.0 / prec, out};
+  if (thr)
+    hipLaunchKernelGGL(k_is_valid<true>, dim3(grid), dim3(256), 0, st, v);
+  else
+    hipLaunchKernelGGL(k_is_valid<false>, dim3(grid), dim3(256), 0, st, v);
   return hipGetLastError();
 }
 size_t scan_dyn_lds(const TableArgs& t) {
   if (!t.pairs_enabled) return 0;
-  return ((size_t)t.n_pairs * sizeof(uint2) + (size_t)(t.n_buckets + 1) * sizeof(uint16_t) + 15) / 16 * 16;
+  return ((size_t)(2 * (t.n_pairs + 2) + t.n_buckets) * sizeof(uint32_t) + 15) / 16 * 16;
 }
 hipError_t launch_explain_scan(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
                                hipStream_t st) {
   if (q.n <= 0) return hipSuccess;
-  if (t.pairs_enabled)
-    hipLaunchKernelGGL(k_explain_scan<true>, dim3(n_blocks), dim3(kScanWG), scan_dyn_lds(t), st, t, q, o);
+  const size_t dyn = scan_dyn_lds(t);
+  if (!t.pairs_enabled)
+    hipLaunchKernelGGL(k_bitset_scan, dim3(n_blocks), dim3(kScanWG), 0, st, t, q, o);
+  else if (q.thr && q.max_mods)
+    hipLaunchKernelGGL((k_explain_scan<true, true>), dim3(n_blocks), dim3(kScanWG), dyn, st, t, q, o);
+  else if (q.thr)
+    hipLaunchKernelGGL((k_explain_scan<true, false>), dim3(n_blocks), dim3(kScanWG), dyn, st, t, q, o);
+  else if (q.max_mods)
+    hipLaunchKernelGGL((k_explain_scan<false, true>), dim3(n_blocks), dim3(kScanWG), dyn, st, t, q, o);
   else
-    hipLaunchKernelGGL(k_explain_scan<false>, dim3(n_blocks), dim3(kScanWG), 0, st, t, q, o);
+    hipLaunchKernelGGL((k_explain_scan<false, false>), dim3(n_blocks), dim3(kScanWG), dyn, st, t, q, o);
   return hipGetLastError();
 }
 hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
@@ -2020,8 +2131,9 @@ static int occupancy(const void* k, int threads, size_t dyn) {
   return nb > 0 ? nb : 1;
 }
 int explain_scan_blocks_per_cu(size_t dyn) {
-  return dyn ? occupancy((const void*)k_explain_scan<true>, kScanWG, dyn)
-             : occupancy((const void*)k_explain_scan<false>, kScanWG, 0);
+  // every variant of the pair scan is held to 8 waves/SIMD by its launch bounds
+  return dyn ? occupancy((const void*)k_explain_scan<true, false>, kScanWG, dyn)
+             : occupancy((const void*)k_bitset_scan, kScanWG, 0);
 }
 int explain_expand_blocks_per_cu() { return occupancy((const void*)k_explain_expand, kWG, 0); }
 hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* pre, uint8_t* dst, hipStream_t st) {
