@@ -142,6 +142,8 @@ def main():
                          "multi-rank path, e.g. several ranks on one GPU with SST_DEVICE=0)")
     ap.add_argument("--gather", action="store_true",
                     help="N>1: gather every query's result to rank 0 over RCCL inside the timed step")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="bracket every n-th launch of the roofline kernel with HIP events (>= 1)")
     ap.add_argument("--no-events", action="store_true",
                     help="diagnostic: time the steps without the per-kernel HIP events (no roofline)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"),
@@ -214,10 +216,11 @@ def main():
     torch.cuda.synchronize()
     engine.synchronize()
 
-    # events bracket only the kernel the roofline reports (each bracket costs
-    # two event records, a few us, on the stream); the other kernels' times
-    # are in the rocprofv3 summaries under profiles/
-    engine.profile(not args.no_events, kernels=(_native.K_EXPLAIN_SCAN,))
+    # events bracket only the kernel the roofline reports, and only every
+    # --event-every-th launch of it: each bracket costs two event records
+    # (~6 us each on the stream), which would otherwise inflate every step;
+    # the other kernels' times are in the rocprofv3 summaries under profiles/
+    engine.profile(not args.no_events, kernels=(_native.K_EXPLAIN_SCAN,), every=args.event_every)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -341,6 +344,7 @@ def main():
             "traffic": traffic,
             "algorithmic_bytes_per_launch": dbytes,
             "avg_launch_us": dus,
+            "event_timed_launches": kern.get(dom, {}).get("launches", 0),  # every --event-every-th step
         },
         "kernels": kern,
         "engine_stats": {"pair": n_pair, "shallow": int(stats[0]), "deep": int(stats[1]), "exact": int(stats[2]),

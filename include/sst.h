@@ -198,6 +198,10 @@ int sst_profile_enable(sst_ctx* ctx, int on);
  * bracketed launch costs two event records on the stream, so a benchmark
  * brackets only the kernels it reports. */
 int sst_profile_select(sst_ctx* ctx, uint32_t kernel_mask);
+/* Bracket only every `every`-th launch of each selected kernel (default 1):
+ * the events' own cost on the stream is then spread over `every` launches
+ * while the durations are still sampled from the live launch stream. */
+int sst_profile_sample(sst_ctx* ctx, uint32_t every);
 int sst_profile_read(sst_ctx* ctx, double* ms_total /* [SST_K_COUNT] */, int64_t* launches /* [SST_K_COUNT] */);
 
 #ifdef __cplusplus

@@ -25,7 +25,7 @@ EXPORTS = (
     "sst_table_download", "sst_table_destroy", "sst_is_valid_batch", "sst_is_valid_batch_device",
     "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
-    "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
+    "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
     "sst_is_singleton_batch_device",
 )
 
@@ -101,6 +101,7 @@ def load_library(path=LIB_PATH):
     lib.sst_result_stats.argtypes = [_P, _P]
     lib.sst_profile_enable.argtypes = [_P, _I]
     lib.sst_profile_select.argtypes = [_P, ctypes.c_uint32]
+    lib.sst_profile_sample.argtypes = [_P, ctypes.c_uint32]
     lib.sst_profile_read.argtypes = [_P, _P, _P]
     lib.sst_length_bound_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _I, _I64, _I, _P, _P]
     lib.sst_explain_recursion_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _U64, _PP]
@@ -169,8 +170,10 @@ class Engine:
                    "sst_is_singleton_batch")
         return out
 
-    def profile(self, on=True, kernels=None):
-        """Bracket launches with HIP events: all kernels, or only the ids in `kernels`."""
+    def profile(self, on=True, kernels=None, every=1):
+        """Bracket launches with HIP events: all kernels, or only the ids in
+        `kernels`; only every `every`-th launch of each (sst_profile_sample)."""
+        self.check(self._lib.sst_profile_sample(self.handle, int(every)), "sst_profile_sample")
         if kernels is None or not on:
             self.check(self._lib.sst_profile_enable(self.handle, int(bool(on))), "sst_profile_enable")
         else:

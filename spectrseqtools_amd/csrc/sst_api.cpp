@@ -72,6 +72,8 @@ struct sst_ctx {
   std::vector<hipEvent_t> pool;
   double prof_ms[SST_K_COUNT] = {0};
   int64_t prof_n[SST_K_COUNT] = {0};
+  uint32_t prof_every = 1;                // bracket every n-th launch of a selected kernel
+  uint64_t prof_seen[SST_K_COUNT] = {0};  // launches of each kernel id since selection
 };
 
 struct sst_table {
@@ -152,7 +154,8 @@ struct Prof {
   int kid;
   hipEvent_t a = nullptr;
   Prof(sst_ctx* c_, int kid_) : c(c_), kid(kid_) {
-    if (((c->prof >> kid) & 1u) && (a = take_event(c))) (void)hipEventRecord(a, c->stream);
+    if (((c->prof >> kid) & 1u) && c->prof_seen[kid]++ % c->prof_every == 0 && (a = take_event(c)))
+      (void)hipEventRecord(a, c->stream);
   }
   ~Prof() {
     if (!a) return;
@@ -1054,8 +1057,17 @@ int sst_profile_select(sst_ctx* c, uint32_t kernel_mask) {
   for (int i = 0; i < SST_K_COUNT; ++i) {
     c->prof_ms[i] = 0;
     c->prof_n[i] = 0;
+    c->prof_seen[i] = 0;
   }
   c->prof = kernel_mask & ((1u << SST_K_COUNT) - 1u);
+  return SST_OK;
+}
+
+int sst_profile_sample(sst_ctx* c, uint32_t every) {
+  if (!c || every == 0) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  c->prof_every = every;
+  for (int i = 0; i < SST_K_COUNT; ++i) c->prof_seen[i] = 0;
   return SST_OK;
 }
 
