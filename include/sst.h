@@ -117,7 +117,10 @@ int sst_is_singleton_batch_device(sst_ctx* ctx, const int64_t* masses, int n_mas
  *             exactly, including budget-dependent first-visit effects);
  *   cap_per_query: candidate cap; larger sets report SST_OVERFLOW with the
  *             exact count and no payload.
+ *   n <= SST_MAX_EXPLAIN_BATCH per call (the kernels address per-query
+ *             arrays with 32-bit byte offsets; split larger batches).
  * Results (host copies) through sst_result_* below. */
+#define SST_MAX_EXPLAIN_BATCH (1ll << 29)
 int sst_explain_batch(sst_table* t, const double* mass, const double* thr_abs, int64_t n, double tolerance,
                       double precision, const int64_t* max_mods, int64_t max_mods_scalar, int with_memo,
                       uint64_t cap_per_query, sst_result** out);

@@ -833,7 +833,7 @@ extern "C" {
 int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d_thr, int64_t n, double tol, double prec,
                              const int64_t* d_mods, int64_t mods_scalar, int with_memo, uint64_t cap_count,
                              sst_result** out) {
-  if (!t || !out || n < 0 || n > INT32_MAX || (n > 0 && !d_mass)) return SST_E_ARG;
+  if (!t || !out || n < 0 || n > SST_MAX_EXPLAIN_BATCH || (n > 0 && !d_mass)) return SST_E_ARG;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
@@ -859,7 +859,7 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
 
 int sst_explain_batch(sst_table* t, const double* mass, const double* thr, int64_t n, double tol, double prec,
                       const int64_t* mods, int64_t mods_scalar, int with_memo, uint64_t cap_count, sst_result** out) {
-  if (!t || !out || n < 0 || n > INT32_MAX || (n > 0 && !mass)) return SST_E_ARG;
+  if (!t || !out || n < 0 || n > SST_MAX_EXPLAIN_BATCH || (n > 0 && !mass)) return SST_E_ARG;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   *out = nullptr;
@@ -924,7 +924,7 @@ int sst_explain_batch(sst_table* t, const double* mass, const double* thr, int64
 int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* thr, int64_t n, double tol,
                                 double prec, const int64_t* mods, int64_t mods_scalar, uint64_t cap_count,
                                 sst_result** out) {
-  if (!t || !out || n < 0 || n > INT32_MAX || (n > 0 && !mass)) return SST_E_ARG;
+  if (!t || !out || n < 0 || n > SST_MAX_EXPLAIN_BATCH || (n > 0 && !mass)) return SST_E_ARG;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   *out = nullptr;

@@ -1049,6 +1049,14 @@ __device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t reg
   }
 }
 
+// Element i of a per-query array through a 32-bit byte offset (batches are
+// capped at SST_MAX_EXPLAIN_BATCH = 2^29 queries): the compiler then
+// addresses it as SGPR base + 32-bit VGPR offset instead of 64-bit VALU math.
+template <typename T>
+__device__ __forceinline__ T* q_at(T* base, uint32_t i) {
+  return (T*)((char*)base + (uint32_t)(i * (uint32_t)sizeof(T)));
+}
+
 // Candidates of a pair-class window [a, hi] from the LDS pair list (layout:
 // TableArgs::pair_data): the entries with sums in the window, in list order
 // (= the reference's order).  The window's bucket word holds the first sum at
@@ -1136,9 +1144,9 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   // (nontemporal).
   auto fetch = [&](uint32_t tl, double& m, double& tt, int64_t& mm) {
     const uint32_t j = tl < ntiles ? min(tl * 64 + lane, n - 1) : n - 1;
-    m = __builtin_nontemporal_load(q.mass + j);
-    if (THR) tt = __builtin_nontemporal_load(q.thr + j);
-    if (MODS) mm = __builtin_nontemporal_load(q.max_mods + j);
+    m = __builtin_nontemporal_load(q_at(q.mass, j));
+    if (THR) tt = __builtin_nontemporal_load(q_at(q.thr, j));
+    if (MODS) mm = __builtin_nontemporal_load(q_at(q.max_mods, j));
   };
   auto step = [&](uint32_t tile, double m_in, double t_in, int64_t mm_cur) {
     const uint32_t i = tile * 64 + lane;
@@ -1175,7 +1183,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     uint64_t off = 0;
     bool retry = false;
-    if (total) {  // wave-uniform
+    if (total) {  // wave-uniform: the tile's chunk base stays in SGPRs
       uint64_t base;
       if ((uint64_t)used + total <= out.region_bytes) {
         base = region0 + used;
@@ -1183,10 +1191,11 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
       } else {
         unsigned long long sb = 0;
         if (lane == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
-        base = out.spill_base + (uint64_t)__shfl(sb, 0, 64);
+        base = out.spill_base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sb >> 32)) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sb));
       }
       off = base + (incl - pb);
-      if (base + total > out.arena_bytes) {  // wave-uniform, rare: the arena is full, the host retries
+      if (base + total > out.arena_bytes) {  // rare: the arena is full, the host retries these queries
         retry = pb && off + pb > out.arena_bytes;
         if (retry) pb = 0;
       }
@@ -1199,8 +1208,8 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     if (live && !work) {
       out.status[i] = retry ? (int8_t)kStatusArenaRetry : status;
       if (cnt && !retry) {  // SOME or OVERFLOW
-        out.count[i] = cnt;
-        out.offset[i] = pb ? off : 0;
+        *q_at(out.count, i) = cnt;
+        *q_at(out.offset, i) = pb ? off : 0;
       }
     }
     const uint64_t bal = __ballot(work);
