@@ -640,9 +640,18 @@ constexpr int kDeepBlocks = 512;        // 64-lane blocks per deep role (fast, n
 constexpr uint32_t kHashCap0 = 1u << 14;  // exact-path hash entries per lane (first attempt)
 constexpr int kExactLanes0 = 2048;      // exact-path concurrent lanes (first attempt)
 constexpr uint64_t kNodeBudget = 1ull << 32;
-constexpr uint64_t kRecNodeBudget = 1ull << 24;  // explain_recursion: per-query DFS nodes before ABORTED
+constexpr uint64_t kRecNodeBudget = 1ull << 34;  // explain_recursion: per-query DFS nodes before ABORTED (a guard only)
 constexpr uint32_t kRecHashCap0 = 1u << 16;       // explain_recursion: memo nodes per lane (first attempt)
-constexpr uint64_t kLBNodeBudget = 1ull << 24;  // length bound: per-query DFS nodes (single lane) before ABORTED
+constexpr uint64_t kLBNodeBudget = 1ull << 34;  // length bound: per-query DFS nodes before ABORTED (a guard only)
+constexpr size_t kMaxMemoBytes = 64ull << 30;    // largest per-launch memo workspace the retries grow to
+// first memo capacity per query in flight: 2^23 entries shared by the units
+// (one query per wave), at least `floor` each -- few queries get a large
+// memo at once instead of re-running after each exhaustion
+uint32_t memo_cap0(int units, uint32_t floor) {
+  uint32_t cap = 1u << 23;
+  while (cap > floor && (uint64_t)cap * (uint64_t)units > (1ull << 23)) cap >>= 1;
+  return cap;
+}
 constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses per lane (first attempt)
 
 void free_result_bufs(sst_result* r) {
@@ -945,8 +954,10 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
   QueryArgs q{(const double*)c->in_mass.p, thr ? (const double*)c->in_thr.p : nullptr,
               mods ? (const int64_t*)c->in_mods.p : nullptr, mods_scalar, n, tol, prec, 1.0 / prec, 1, cap_count,
               kRecNodeBudget};
-  uint32_t cap = kRecHashCap0;
-  int lanes = (int)std::min<int64_t>(256, (n + 63) / 64 * 64);
+  // one 64-lane block per query in flight (k_explain_recursion<WAVE>), each
+  // with its own memo slice
+  int units = (int)std::min<int64_t>(256, n);
+  uint32_t cap = memo_cap0(units, kRecHashCap0);
   int rc = SST_OK;
   for (int attempt = 0; n > 0; ++attempt) {
     if (attempt == 8) {
@@ -956,7 +967,7 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
     r->arena_bytes = (uint64_t)r->n_regions * r->region_bytes + r->spill_bytes;
     DevBuf hash, frames;
     if (!r->ctl.ensure(2 * kCtlWords * 8) || !r->payload.ensure(r->arena_bytes) ||
-        !hash.ensure((size_t)lanes * cap * rec_entry_bytes()) || !frames.ensure((size_t)lanes * rec_frame_bytes())) {
+        !hash.ensure((size_t)units * cap * rec_entry_bytes()) || !frames.ensure((size_t)units * rec_frame_bytes())) {
       rc = fail(c, SST_E_NOMEM, "device allocation failed (recursion)");
       break;
     }
@@ -965,7 +976,7 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
     HIP_OK(c, hipMemsetAsync(r->ctl.p, 0, 2 * kCtlWords * 8, c->stream));
     HIP_OK(c, hipMemsetAsync(hash.p, 0, hash.bytes, c->stream));
     r->compacted = false;
-    HIP_OK(c, launch_explain_recursion(t->args, q, out_args(r), (char*)hash.p, (char*)frames.p, cap, lanes,
+    HIP_OK(c, launch_explain_recursion(t->args, q, out_args(r), (char*)hash.p, (char*)frames.p, cap, units,
                                        c->stream));
     if ((rc = fetch(r))) break;
     bool arena_retry = false, memo_retry = false;
@@ -982,12 +993,12 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
       r->dense.release();
     }
     if (memo_retry) {
-      if (cap >= (1u << 26)) {
-        rc = fail(c, SST_E_INTERNAL, "explain_recursion: memo exceeds 2^26 nodes");
+      if ((size_t)std::max(1, units / 8) * cap * 8 * rec_entry_bytes() > kMaxMemoBytes) {
+        rc = fail(c, SST_E_NOMEM, "explain_recursion: memo would exceed the workspace limit");
         break;
       }
       cap *= 8;
-      lanes = std::max(64, lanes / 8);
+      units = std::max(1, units / 8);
     }
   }
   if (!rc && n == 0) rc = fetch(r);
@@ -1199,24 +1210,27 @@ int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, in
   HIP_OK(c, hipStreamSynchronize(c->stream));
   std::vector<int8_t> st(nn);
   if (n_exact) {
-    uint32_t cap = kLBHashCap0;
-    int lanes = (int)std::min<uint32_t>(256, (n_exact + 63) / 64 * 64);
+    // one 64-lane block per query in flight (k_length_exact<WAVE>), each with
+    // its own memo slice
+    int units = (int)std::min<uint32_t>(256, n_exact);
+    uint32_t cap = memo_cap0(units, kLBHashCap0);
     for (;;) {
       DevBuf hash, vals, frames;
-      if (!hash.ensure((size_t)lanes * cap * hash_entry_bytes()) || !vals.ensure((size_t)lanes * cap * kMaxRows) ||
-          !frames.ensure((size_t)lanes * lb_frame_bytes()))
+      if (!hash.ensure((size_t)units * cap * hash_entry_bytes()) || !vals.ensure((size_t)units * cap * kMaxRows) ||
+          !frames.ensure((size_t)units * lb_frame_bytes()))
         return fail(c, SST_E_NOMEM, "device allocation failed (length-bound memo)");
       HIP_OK(c, hipMemsetAsync(hash.p, 0, hash.bytes, c->stream));
-      HIP_OK(c, launch_length_bound(t->args, q, (char*)hash.p, (int8_t*)vals.p, (char*)frames.p, cap, lanes, false,
+      HIP_OK(c, launch_length_bound(t->args, q, (char*)hash.p, (int8_t*)vals.p, (char*)frames.p, cap, units, false,
                                     c->stream));
       HIP_OK(c, hipMemcpyAsync(st.data(), d_st.p, nn, hipMemcpyDeviceToHost, c->stream));
       HIP_OK(c, hipStreamSynchronize(c->stream));
       bool retry = false;
       for (size_t i = 0; i < nn; ++i) retry |= st[i] == kStatusExactRetry;
       if (!retry) break;
-      if (cap >= (1u << 25)) return fail(c, SST_E_INTERNAL, "length bound: memo exceeds 2^25 masses");
+      if ((size_t)std::max(1, units / 8) * cap * 8 * (hash_entry_bytes() + kMaxRows) > kMaxMemoBytes)
+        return fail(c, SST_E_NOMEM, "length bound: memo would exceed the workspace limit");
       cap *= 8;
-      lanes = std::max(64, lanes / 8);
+      units = std::max(1, units / 8);
     }
   }
   HIP_OK(c, hipMemcpyAsync(out, d_out.p, nn * 8, hipMemcpyDeviceToHost, c->stream));

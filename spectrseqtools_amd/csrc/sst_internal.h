@@ -190,12 +190,12 @@ size_t glob_frame_bytes();
 hipError_t launch_layer_step(const uint64_t* prev, uint64_t* next, int64_t nwords, const int* w, int n_rows,
                              hipStream_t st);
 hipError_t launch_length_bound(const TableArgs& t, const LBArgs& q, char* hash, int8_t* vals, char* frames,
-                               uint32_t hash_cap, int exact_lanes, bool fast_pass, hipStream_t st);
+                               uint32_t hash_cap, int exact_units, bool fast_pass, hipStream_t st);
 size_t lb_frame_bytes();
 hipError_t launch_is_singleton(const int64_t* masses, int n_masses, const double* mass, const double* thr, int64_t n,
                                double tol, double prec, int8_t* out, hipStream_t st);
 hipError_t launch_explain_recursion(const TableArgs& t, const QueryArgs& q, const OutArgs& o, char* hash,
-                                   char* frames, uint32_t hash_cap, int lanes, hipStream_t st);
+                                   char* frames, uint32_t hash_cap, int units, hipStream_t st);
 size_t rec_frame_bytes();
 size_t rec_entry_bytes();
 size_t p1_frame_bytes();

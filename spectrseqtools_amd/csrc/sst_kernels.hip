@@ -564,6 +564,7 @@ struct Hash {
   uint32_t used;
   uint32_t limit;
   uint64_t sink = 0;  // folds prefetch loads (see p1_visit)
+  uint32_t last_meta = 0;  // meta written by the last first visit (p1_visit)
   __device__ __forceinline__ uint32_t slot(uint32_t m) const { return (m * 0x9E3779B1u) & mask; }
   // returns entry pointer or nullptr if absent
   __device__ __forceinline__ HEntry* find(uint32_t m) const {
@@ -788,7 +789,8 @@ struct P1Frame {
   HEntry* e;
   uint32_t m;
   int A, B;
-  uint8_t rtop, rnext, pad0, pad1;
+  uint8_t rtop, rnext, ne, pad1;  // ne: the frame's lowest non-empty row so far (wave mode)
+  uint32_t meta;                  // the entry's meta as this frame wrote it (wave mode)
 };
 
 // visit (m, r, A, B): returns 1 if (m, r) is a first visit (its newly
@@ -796,21 +798,41 @@ struct P1Frame {
 // makes it the current frame), 0 otherwise (memo hit or pair == 0; *nonempty
 // = the child's "non-empty at row r" verdict), -1 on hash exhaustion.
 // Memo entry meta: hv (bits 0-7), ne (8-15), lo (16-23).
+template <bool WAVE>
 __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& h, uint32_t m, int r, int A, int B,
                                         bool& nonempty, uint64_t& nodes, M128& en_out, HEntry*& ent) {
-  ulonglong2 rec = ld_index(t.index, m);
+  // the index record and the memo's first probe slot (key, meta and the
+  // enabled mask: the whole 32-B entry) are independent: issue them together
+  // (both were prefetched by the parent frame)
+  const uint32_t sl = h.slot(m);
+  const ulonglong2 rec = ld_index(t.index, m);
+  const ulonglong2 kv = *(const ulonglong2*)&h.e[sl];
+  const ulonglong2 ev = *(const ulonglong2*)&h.e[sl].en0;
   nodes++;
   int lo = rec_lo(rec);
   if (r < lo) {  // pair(r, m) == 0: [] without memo (mass_explanation.py:148-149)
     nonempty = false;
     return 0;
   }
-  HEntry* e = h.get(m);
-  if (!e) return -1;
-  int hv = (int)(e->meta & 0xFF);
+  HEntry* e;
+  uint32_t meta;
+  uint64_t en_old0 = 0, en_old1 = 0;
+  if (kv.x == ((h.epoch << 32) | m)) {  // found in the first slot
+    e = &h.e[sl];
+    meta = (uint32_t)kv.y;
+    en_old0 = ev.x;
+    en_old1 = ev.y;
+  } else {
+    e = h.get(m);  // inserts a fresh entry when the key is absent
+    if (!e) return -1;
+    meta = e->meta;
+    en_old0 = e->en0;
+    en_old1 = e->en1;
+  }
+  int hv = (int)(meta & 0xFF);
   hv = hv == 0xFF ? -1 : hv;
   if (r <= hv) {  // memo hit (mass_explanation.py:122-123)
-    int ne = (int)((e->meta >> 8) & 0xFF);
+    int ne = (int)((meta >> 8) & 0xFF);
     nonempty = ne != 0xFF && r >= ne;
     return 0;
   }
@@ -835,17 +857,39 @@ __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& 
       }
     }
   }
-  e->en0 |= en.a;
-  e->en1 |= en.b;
-  e->meta = (e->meta & 0xFF00u) | ((uint32_t)lo << 16) | (uint32_t)r;
+  e->en0 = en_old0 | en.a;
+  e->en1 = en_old1 | en.b;
+  e->meta = (meta & 0xFF00u) | ((uint32_t)lo << 16) | (uint32_t)r;
+  h.last_meta = e->meta;
   // the frame will visit (m - w_rr, rr) for every enabled row: issue their
   // index-record and first-probe loads now, independently, so the visits
   // that follow hit the cache instead of paying dependent HBM round trips
-  for (M128 k = en; !mzero(k);) {
-    const int rr = mlow(k);
-    k = mclear(k, rr);
-    const int64_t c = (int64_t)m - s.w[rr];
-    if (c > 0) h.sink ^= __builtin_nontemporal_load(&t.index[c].y) ^ h.e[h.slot((uint32_t)c)].key;
+  if (WAVE) {
+    // one query per wave: lane L takes rows L and L + 64 -- and, speculating
+    // one level deeper, the children (c0 - w_s, s <= rr0) of the first enabled
+    // row rr0, the frame the DFS enters next, whose own records are then
+    // already in flight when it is expanded
+    const int lane = threadIdx.x & 63;
+    const int rr0 = mzero(en) ? -1 : mlow(en);
+    const int64_t c0 = rr0 >= 0 ? (int64_t)m - s.w[rr0] : 0;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int rr = lane + 64 * half;
+      if (rr < t.n_rows) {
+        const int64_t c = (int64_t)m - s.w[rr];
+        if (mtest(en, rr) && c > 0) h.sink ^= __builtin_nontemporal_load(&t.index[c].y) ^ h.e[h.slot((uint32_t)c)].key;
+        const int64_t g = c0 - s.w[rr];
+        if (rr >= 1 && rr <= rr0 && g > 0)
+          h.sink ^= __builtin_nontemporal_load(&t.index[g].y) ^ h.e[h.slot((uint32_t)g)].key;
+      }
+    }
+  } else {
+    for (M128 k = en; !mzero(k);) {
+      const int rr = mlow(k);
+      k = mclear(k, rr);
+      const int64_t c = (int64_t)m - s.w[rr];
+      if (c > 0) h.sink ^= __builtin_nontemporal_load(&t.index[c].y) ^ h.e[h.slot((uint32_t)c)].key;
+    }
   }
   en_out = en;
   ent = e;
@@ -859,6 +903,7 @@ __device__ __forceinline__ void p1_set_ne(HEntry* e, int rr) {  // lowest non-em
 // returns 0 ok, -1 hash full, -2 depth, -3 node budget.  The current frame
 // lives in registers; fr[] holds only the saved ancestors (touched on push
 // and pop, not per row).
+template <bool WAVE>
 __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
                            uint64_t node_budget, uint64_t& nodes) {
   const int top = t.n_rows - 1;
@@ -867,7 +912,7 @@ __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* f
     bool ne_dummy;
     M128 rest;
     HEntry* e;
-    int pr = p1_visit(t, s, h, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes, rest, e);
+    int pr = p1_visit<WAVE>(t, s, h, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes, rest, e);
     if (pr < 0) return -1;
     if (pr == 0) continue;
     uint32_t m = (uint32_t)v;
@@ -901,7 +946,7 @@ __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* f
         if (d + 1 >= kMaxDepth) return -2;
         M128 cen;
         HEntry* cent;
-        const int pushed = p1_visit(t, s, h, (uint32_t)child, rr, A - md, Bv - md, nonempty, nodes, cen, cent);
+        const int pushed = p1_visit<WAVE>(t, s, h, (uint32_t)child, rr, A - md, Bv - md, nonempty, nodes, cen, cent);
         if (pushed < 0) return -1;
         if (pushed) {  // descend: save this frame (its pending row is rr)
           fr[d++] = P1Frame{rest.a, rest.b, e, m, A, B, (uint8_t)rtop, (uint8_t)(rr + 1), 0, 0};
@@ -920,11 +965,89 @@ __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* f
   return 0;
 }
 
+// phase1_body for one query per wave: the same replay, with the saved frames
+// in LDS and the current frame's lowest non-empty row in a register (written
+// to its memo entry once, when the frame completes -- no other node can read
+// that entry earlier, since every node below it has a smaller mass).  That
+// leaves one memory round trip per visited node: its index record and memo
+// entry, loaded together (p1_visit).
+__device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
+                                uint64_t node_budget, uint64_t& nodes) {
+  const int top = t.n_rows - 1;
+  for (int64_t v = a; v <= b; ++v) {
+    if (!((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;
+    bool ne_dummy;
+    M128 rest;
+    HEntry* e;
+    int pr = p1_visit<true>(t, s, h, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes, rest, e);
+    if (pr < 0) return -1;
+    if (pr == 0) continue;
+    uint32_t m = (uint32_t)v, meta = h.last_meta;
+    int A = A0, B = s.cap[top], rtop = top, d = 0;
+    int ne = (int)((meta >> 8) & 0xFF);
+    for (;;) {
+      if (mzero(rest)) {  // frame done: publish its non-empty row, report to the parent
+        e->meta = (meta & ~0xFF00u) | ((uint32_t)ne << 8);
+        if (d == 0) break;
+        const int cne = ne;
+        const P1Frame f = fr[--d];
+        rest = M128{f.en0, f.en1};
+        e = f.e;
+        m = f.m;
+        A = f.A;
+        B = f.B;
+        rtop = f.rtop;
+        ne = f.ne;
+        meta = f.meta;
+        const int rr = f.rnext - 1;
+        if (cne != 0xFF && rr >= cne && ne == 0xFF) ne = rr;
+        continue;
+      }
+      const int rr = mlow(rest);
+      rest = mclear(rest, rr);
+      const int md = s.mod[rr];
+      const int Bv = (rr == rtop) ? B : s.cap[rr];
+      const int64_t child = (int64_t)m - s.w[rr];
+      bool nonempty = false;
+      if (child == 0) {
+        nonempty = true;
+      } else if (child > 0) {
+        if (nodes >= node_budget) return -3;
+        if (d + 1 >= kMaxDepth) return -2;
+        M128 cen;
+        HEntry* cent;
+        const int pushed = p1_visit<true>(t, s, h, (uint32_t)child, rr, A - md, Bv - md, nonempty, nodes, cen, cent);
+        if (pushed < 0) return -1;
+        if (pushed) {  // descend: save this frame (its pending row is rr)
+          fr[d++] = P1Frame{rest.a, rest.b, e, m, A, B, (uint8_t)rtop, (uint8_t)(rr + 1), (uint8_t)ne, 0, meta};
+          rest = cen;
+          e = cent;
+          m = (uint32_t)child;
+          A -= md;
+          B = Bv - md;
+          rtop = rr;
+          meta = h.last_meta;
+          ne = (int)((meta >> 8) & 0xFF);
+          continue;
+        }
+      }
+      if (nonempty && ne == 0xFF) ne = rr;  // lowest non-empty row (first found wins)
+    }
+  }
+  return 0;
+}
+
+// WAVE: one query per wave.  Every lane runs the same (uniform) replay --
+// identical loads and stores to the same addresses cost one transaction --
+// and the lanes split only the prefetch loads (p1_visit).
+template <bool WAVE>
 __device__ int phase1(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
                       uint64_t node_budget, uint64_t& nodes) {
   h.sink = 0;
-  const int rc = phase1_body(t, s, h, fr, a, b, A0, node_budget, nodes);
-  return h.sink == 0x5bd1e9955bd1e995ull ? rc - 100 : rc;  // (never) keeps the prefetch loads alive
+  const int rc = WAVE ? phase1_body_wave(t, s, h, fr, a, b, A0, node_budget, nodes)
+                      : phase1_body<WAVE>(t, s, h, fr, a, b, A0, node_budget, nodes);
+  // (never true) keeps every lane's prefetch loads alive; a ballot keeps rc uniform
+  return __ballot(h.sink == 0x5bd1e9955bd1e995ull) ? rc - 100 : rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -1526,7 +1649,7 @@ __device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs
     h.epoch = ++ws.epochs[gid];
     h.used = 0;
     uint64_t nodes = 0;
-    int rc = phase1(t, s, h, fr, a, b, A0, q.node_budget, nodes);
+    int rc = phase1<false>(t, s, h, fr, a, b, A0, q.node_budget, nodes);
     int8_t status;
     EnumOut eo{0, 0, 0, 0};
     uint64_t bytes = 0;
@@ -1679,6 +1802,112 @@ __device__ int lb_values(const TableArgs& t, const Lds& s, const Hash& h, int8_t
   }
 }
 
+// lb_values with one query per wave.  Values are a pure function of the
+// phase-1 DAG, so a node first computes every uncomputed child (depth first,
+// ascending rows), then all its rows at once: lane r loads child r's value
+// and a wavefront prefix min / max over rows lo..hv gives
+// vals[node][r] = combine(default, rows lo..r).  One probe round per node
+// instead of one dependent look-up per row.
+struct LBWFrame {
+  uint64_t u0, u1;  // rows whose child still has to be computed
+  HEntry* e;
+  uint32_t m;
+  uint32_t pad;
+};
+__device__ __forceinline__ int lb_scan(int dir, int x) {  // inclusive prefix combine over the 64 lanes
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x = lb_combine(dir, x, y);
+  }
+  return x;
+}
+__device__ __forceinline__ M128 lb_uncomputed(const TableArgs& t, const Lds& s, const Hash& h, const HEntry* e,
+                                              uint32_t m, bool& bad) {
+  const int lane = threadIdx.x & 63;
+  const M128 en{e->en0, e->en1};
+  bool u[2], miss = false;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lane + 64 * half;
+    u[half] = false;
+    if (r < t.n_rows && mtest(en, r) && m != (uint32_t)s.w[r]) {
+      const HEntry* ce = h.find(m - (uint32_t)s.w[r]);  // visited by phase 1 (the edge was taken)
+      miss |= ce == nullptr;
+      u[half] = ce && ce->pad == 0;
+    }
+  }
+  bad = __ballot(miss) != 0;
+  return M128{(uint64_t)__ballot(u[0]), (uint64_t)__ballot(u[1])};
+}
+__device__ int lb_values_wave(const TableArgs& t, const Lds& s, const Hash& h, int8_t* vals, LBWFrame* fr,
+                              HEntry* root_e, uint32_t root, int dir, int dflt) {
+  const int lane = threadIdx.x & 63;
+  const int neutral = dir ? -128 : 127;  // identity of max / min over int8 values
+  HEntry* e = root_e;
+  uint32_t m = root;
+  bool bad = false;
+  M128 u = lb_uncomputed(t, s, h, e, m, bad);
+  if (bad) return -3;
+  int d = 0;
+  for (;;) {
+    if (!mzero(u)) {  // compute the lowest uncomputed child first
+      const int r = mlow(u);
+      u = mclear(u, r);
+      const uint32_t c = m - (uint32_t)s.w[r];
+      HEntry* ce = h.find(c);
+      if (!ce) return -3;
+      if (ce->pad != 0) continue;  // computed meanwhile, inside an earlier sibling's subtree
+      if (d + 1 >= kMaxDepth) return -2;
+      fr[d++] = LBWFrame{u.a, u.b, e, m, 0};
+      e = ce;
+      m = c;
+      u = lb_uncomputed(t, s, h, e, m, bad);
+      if (bad) return -3;
+      continue;
+    }
+    // every child is computed: this node's rows lo..hv at once
+    const int lo = (int)((e->meta >> 16) & 0xFF), hv = (int)(e->meta & 0xFF);
+    const M128 en{e->en0, e->en1};
+    int contrib[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int r = lane + 64 * half;
+      contrib[half] = neutral;
+      if (r < t.n_rows && r >= lo && r <= hv && mtest(en, r)) {
+        const uint32_t c = m - (uint32_t)s.w[r];
+        int cv = 0;  // total_mass == 0 -> 0 (mass_table.py:378-379)
+        if (c != 0) {
+          const HEntry* ce = h.find(c);
+          cv = ce ? vals[(size_t)(ce - h.e) * kMaxRows + r] : 0;
+        }
+        contrib[half] = cv + 1;
+      }
+    }
+    const int p0 = lb_scan(dir, contrib[0]);
+    const int tot0 = __shfl(p0, 63, 64);
+    const int p1 = lb_combine(dir, lb_scan(dir, contrib[1]), tot0);
+    int8_t* row = vals + (size_t)(e - h.e) * kMaxRows;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int r = lane + 64 * half;
+      if (r < kMaxRows && r >= lo && r <= hv) row[r] = (int8_t)lb_combine(dir, dflt, half ? p1 : p0);
+    }
+    e->pad = 1;  // values computed
+    if (d == 0) return 0;
+    const LBWFrame f = fr[--d];
+    u = M128{f.u0, f.u1};
+    e = f.e;
+    m = f.m;
+  }
+}
+
+// per-query frame workspace of k_length_exact: phase-1 frames, then the value
+// DP's frames (lane or wave form)
+constexpr size_t kLBFrameBytes =
+    kMaxDepth * (sizeof(P1Frame) + (sizeof(LBFrame) > sizeof(LBWFrame) ? sizeof(LBFrame) : sizeof(LBWFrame)));
+
 __device__ __forceinline__ bool lb_window(const LBArgs& q, int64_t i, int64_t& lo, int64_t& hi) {
   const double obs = q.obs[i];
   quantise(q.su[i], q.tol * obs, false, q.tol, q.prec, q.rprec, lo, hi);  // mass_table.py:354-359
@@ -1730,20 +1959,25 @@ __global__ __launch_bounds__(256) void k_length_fast(TableArgs t, LBArgs q) {
 
 // one lane per queued query: phase 1 (first visits) + value DP; per-lane hash
 // slice and value slice, fresh (zeroed) workspace per launch
+// WAVE: one query per 64-lane block (the DFS state is wave-uniform, the
+// lanes split the prefetch); else one query per lane.
+template <bool WAVE>
 __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char* hash, int8_t* vals, char* frames,
                                                      uint32_t hash_cap) {
   __shared__ Lds s;
   const uint32_t n_list = *q.exact_count;
   if (n_list == 0) return;
   stage_rows(s, t);
-  const int64_t gid = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  const int64_t nthreads = (int64_t)gridDim.x * 64;
-  P1Frame* fr = (P1Frame*)(frames + gid * kMaxDepth * (sizeof(P1Frame) + sizeof(LBFrame)));
-  LBFrame* lf = (LBFrame*)(fr + kMaxDepth);
+  const int64_t gid = WAVE ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * 64 + threadIdx.x;
+  const int64_t nthreads = WAVE ? (int64_t)gridDim.x : (int64_t)gridDim.x * 64;
+  __shared__ P1Frame wfr[WAVE ? kMaxDepth : 1];  // wave mode: the replay's saved frames
+  P1Frame* gfr = (P1Frame*)(frames + gid * kLBFrameBytes);
+  P1Frame* fr = WAVE ? wfr : gfr;
+  LBFrame* lf = (LBFrame*)(gfr + kMaxDepth);
   Hash h;
   h.e = (HEntry*)(hash + (size_t)gid * hash_cap * sizeof(HEntry));
   h.mask = hash_cap - 1;
-  h.limit = (uint32_t)(hash_cap * 0.7);
+  h.limit = hash_cap / 4;  // load factor <= 1/4: a wave waits for its longest probe chain
   int8_t* lv = vals + (size_t)gid * hash_cap * kMaxRows;
   uint64_t epoch = 0;
   const int top = t.n_rows - 1;
@@ -1755,7 +1989,7 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
     h.used = 0;
     uint64_t nodes = 0;
     const int64_t a = lo < 1 ? 1 : lo;
-    int rc = phase1(t, s, h, fr, a, hi, q.A0, q.node_budget, nodes);
+    int rc = phase1<WAVE>(t, s, h, fr, a, hi, q.A0, q.node_budget, nodes);
     if (rc == -1) {
       q.status[i] = (int8_t)kStatusExactRetry;
       continue;
@@ -1774,7 +2008,9 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
         rc = -3;
         break;
       }
-      if (e->pad == 0) rc = lb_values(t, s, h, lv, lf, e, (uint32_t)v, q.dir, dflt);
+      if (e->pad == 0)
+        rc = WAVE ? lb_values_wave(t, s, h, lv, (LBWFrame*)lf, e, (uint32_t)v, q.dir, dflt)
+                  : lb_values(t, s, h, lv, lf, e, (uint32_t)v, q.dir, dflt);
       if (rc == 0) best = lb_combine(q.dir, best, lv[(size_t)(e - h.e) * kMaxRows + top]);
     }
     if (rc < 0) {
@@ -1867,8 +2103,29 @@ __device__ __forceinline__ M128 rec_enabled(const TableArgs& t, const Lds& s, in
 // per child's first probe slot (results folded into a sink the compiler must
 // keep), so the sequential probes that follow hit the cache instead of paying
 // one dependent HBM round trip each.
-__device__ __forceinline__ uint64_t rec_prefetch(const Lds& s, const RHash& h, uint32_t rem, M128 en, int64_t thr) {
+// WAVE (one query per wave): lane L takes children L and L + 64 and, one
+// level deeper, the children (crem0 - w_j, j >= i0) of the first enabled
+// child i0, the node the DFS most likely enters next.
+template <bool WAVE>
+__device__ __forceinline__ uint64_t rec_prefetch(const TableArgs& t, const Lds& s, const RHash& h, uint32_t rem,
+                                                 M128 en, int64_t thr) {
   uint64_t sink = 0;
+  if (WAVE) {
+    const int lane = threadIdx.x & 63;
+    const int i0 = mzero(en) ? kMaxRows : mlow(en);
+    const int64_t crem0 = i0 < kMaxRows ? (int64_t)rem - s.w[i0] : -1;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int i = lane + 64 * half;
+      if (i < t.n_rows) {
+        const int64_t crem = (int64_t)rem - s.w[i];
+        if (mtest(en, i) && crem > thr) sink ^= __builtin_nontemporal_load(&h.e[h.slot((uint32_t)crem, i)].key);
+        const int64_t g = crem0 - s.w[i];
+        if (i >= i0 && crem0 > thr && g > thr) sink ^= __builtin_nontemporal_load(&h.e[h.slot((uint32_t)g, i)].key);
+      }
+    }
+    return sink;
+  }
   for (M128 k = en; !mzero(k);) {
     const int i = mlow(k);
     k = mclear(k, i);
@@ -1880,6 +2137,7 @@ __device__ __forceinline__ uint64_t rec_prefetch(const Lds& s, const RHash& h, u
 
 // phase 1: 0 ok, -1 memo full, -2 depth, -3 node budget.  stk: this lane's
 // kMaxDepth saved frames (LDS, stride kRecLanes).
+template <bool WAVE>
 __device__ int rec_phase1(const TableArgs& t, const Lds& s, RHash& h, RFrame* stk, uint32_t target, int64_t thr,
                           int A, uint64_t node_budget, uint64_t& nodes) {
   REntry* e = h.insert(target, 1);
@@ -1889,11 +2147,11 @@ __device__ int rec_phase1(const TableArgs& t, const Lds& s, RHash& h, RFrame* st
   e->en1 = rest.b;
   uint32_t slot = (uint32_t)(e - h.e), rem = target;
   int ua = 0, ui = 0, start = 1, d = 0;
-  uint64_t sink = rec_prefetch(s, h, rem, rest, thr);
+  uint64_t sink = rec_prefetch<WAVE>(t, s, h, rem, rest, thr);
   for (;;) {
     if (mzero(rest)) {
       if (d == 0) break;
-      const RFrame f = stk[(--d) * kRecLanes];
+      const RFrame f = stk[(--d) * (WAVE ? 1 : kRecLanes)];
       const REntry* pe = h.e + f.slot;
       slot = f.slot;
       rem = f.rem;
@@ -1917,20 +2175,207 @@ __device__ int rec_phase1(const TableArgs& t, const Lds& s, RHash& h, RFrame* st
     const M128 cen = rec_enabled(t, s, i, cua, cui, A);
     ce->en0 = cen.a;
     ce->en1 = cen.b;
-    stk[(d++) * kRecLanes] = RFrame{slot, rem, (int16_t)ua, (int16_t)ui, (uint8_t)start, (uint8_t)(i + 1), 0, 0};
+    stk[(d++) * (WAVE ? 1 : kRecLanes)] = RFrame{slot, rem, (int16_t)ua, (int16_t)ui, (uint8_t)start, (uint8_t)(i + 1), 0, 0};
     slot = (uint32_t)(ce - h.e);
     rem = (uint32_t)crem;
     ua = cua;
     ui = cui;
     start = i;
     rest = cen;
-    sink ^= rec_prefetch(s, h, rem, rest, thr);
+    sink ^= rec_prefetch<WAVE>(t, s, h, rem, rest, thr);
   }
-  return sink == 0x5bd1e9955bd1e995ull ? 1 : 0;  // (never) keeps the prefetch loads alive
+  return __ballot(sink == 0x5bd1e9955bd1e995ull) ? 1 : 0;  // (never) keeps every lane's prefetch loads alive
+}
+
+// Phase 1 with one query per wave.  A node's children (rem - w_i, i) have
+// pairwise distinct keys, and no node inside child i's subtree can carry a
+// later sibling's key (its start row would be that sibling's row j with
+// w_i + ... = w_j over rows i <= ... <= j, impossible for positive masses).
+// So every sibling's memo state at the moment the reference reaches it equals
+// its state when the parent is first entered: the lanes probe all children at
+// once (lane L: rows L and L + 64) and the DFS then walks only the children
+// that need a first visit, in ascending row order -- the reference's order.
+struct RWFrame {
+  uint64_t d0, d1;  // children still to descend into
+  uint32_t slot, rem;
+  int16_t ua, ui;
+  uint8_t start, pad0, pad1, pad2;
+};
+__device__ __forceinline__ M128 rec_descend_mask(const TableArgs& t, const Lds& s, const RHash& h, uint32_t rem,
+                                                 M128 en, int64_t thr, uint64_t& sink) {
+  const int lane = threadIdx.x & 63;
+  bool need[2];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int i = lane + 64 * half;
+    need[half] = false;
+    if (i < t.n_rows && mtest(en, i)) {
+      const int64_t crem = (int64_t)rem - s.w[i];
+      // [[]] / [] base cases are not memoised; otherwise a memo miss is a first visit
+      if (!rec_leaf(crem, thr) && crem >= 0) need[half] = h.find((uint32_t)crem, i) == nullptr;
+    }
+  }
+  const M128 d{(uint64_t)__ballot(need[0]), (uint64_t)__ballot(need[1])};
+  // prefetch the memo slots of the first descendant's children
+  if (!mzero(d)) {
+    const int i0 = mlow(d);
+    const int64_t crem0 = (int64_t)rem - s.w[i0];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int j = lane + 64 * half;
+      if (j < t.n_rows && j >= i0) {
+        const int64_t g = crem0 - s.w[j];
+        if (g > thr) sink ^= __builtin_nontemporal_load(&h.e[h.slot((uint32_t)g, j)].key);
+      }
+    }
+  }
+  return d;
+}
+// Whether the node's memoised list (its first visit's) is non-empty: some
+// enabled child is a [[]] base case or a memo node whose own list is non-empty
+// (REntry::pad bit 0, set when that node completed -- children complete before
+// their parents, and memo hits were completed earlier).  Lanes probe the
+// children in one round.  Phase 2 then walks only non-empty subtrees.
+__device__ __forceinline__ void rec_complete(const TableArgs& t, const Lds& s, const RHash& h, REntry* e,
+                                             uint32_t rem, int64_t thr) {
+  const int lane = threadIdx.x & 63;
+  const M128 en{e->en0, e->en1};
+  bool ne = false;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int i = lane + 64 * half;
+    if (i < t.n_rows && mtest(en, i)) {
+      const int64_t crem = (int64_t)rem - s.w[i];
+      if (rec_leaf(crem, thr)) {
+        ne = true;
+      } else if (crem > 0) {
+        const REntry* ce = h.find((uint32_t)crem, i);
+        ne |= ce && (ce->pad & 1u);
+      }
+    }
+  }
+  if (__ballot(ne)) e->pad = 1;
+}
+__device__ int rec_phase1_wave(const TableArgs& t, const Lds& s, RHash& h, RWFrame* stk, uint32_t target,
+                               int64_t thr, int A, uint64_t node_budget, uint64_t& nodes) {
+  REntry* e = h.insert(target, 1);
+  if (!e) return -1;
+  uint64_t sink = 0;
+  M128 en = rec_enabled(t, s, 1, 0, 0, A);
+  e->en0 = en.a;
+  e->en1 = en.b;
+  e->pad = 0;
+  uint32_t slot = (uint32_t)(e - h.e), rem = target;
+  int ua = 0, ui = 0, start = 1, d = 0;
+  M128 rest = rec_descend_mask(t, s, h, rem, en, thr, sink);
+  for (;;) {
+    if (mzero(rest)) {
+      rec_complete(t, s, h, h.e + slot, rem, thr);  // every child of this node is done
+      if (d == 0) break;
+      const RWFrame f = stk[--d];
+      slot = f.slot;
+      rem = f.rem;
+      ua = f.ua;
+      ui = f.ui;
+      start = f.start;
+      rest = M128{f.d0, f.d1};
+      continue;
+    }
+    const int i = mlow(rest);
+    rest = mclear(rest, i);
+    const uint32_t crem = rem - (uint32_t)s.w[i];
+    if (++nodes > node_budget) return -3;
+    if (d + 1 >= kMaxDepth) return -2;
+    const int cua = ua + s.mod[i];
+    const int cui = i != start ? 0 : ui + s.mod[i];
+    REntry* ce = h.insert(crem, i);
+    if (!ce) return -1;
+    const M128 cen = rec_enabled(t, s, i, cua, cui, A);
+    ce->en0 = cen.a;
+    ce->en1 = cen.b;
+    ce->pad = 0;
+    stk[d++] = RWFrame{rest.a, rest.b, slot, rem, (int16_t)ua, (int16_t)ui, (uint8_t)start, 0, 0, 0};
+    slot = (uint32_t)(ce - h.e);
+    rem = crem;
+    ua = cua;
+    ui = cui;
+    start = i;
+    rest = rec_descend_mask(t, s, h, rem, cen, thr, sink);
+  }
+  return __ballot(sink == 0x5bd1e9955bd1e995ull) ? 1 : 0;  // (never) keeps every lane's prefetch loads alive
+}
+
+// Phase 2 with one query per wave: the candidates in the reference's list
+// order (children ascending, each child's list in its own order), walking
+// only the non-empty subtrees marked by phase 1.  At each node the lanes
+// classify every enabled child in one probe round; a candidate's record is
+// written with one byte per lane.  dst == nullptr counts.
+struct RPFrame {
+  uint64_t t0, t1;  // children still to emit / enter
+  uint32_t rem;
+  uint32_t pad;
+};
+__device__ __forceinline__ M128 rec_todo(const TableArgs& t, const Lds& s, const RHash& h, uint32_t rem,
+                                         const REntry* e, int64_t thr) {
+  const int lane = threadIdx.x & 63;
+  const M128 en{e->en0, e->en1};
+  bool go[2];
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int i = lane + 64 * half;
+    go[half] = false;
+    if (i < t.n_rows && mtest(en, i)) {
+      const int64_t crem = (int64_t)rem - s.w[i];
+      if (rec_leaf(crem, thr)) {
+        go[half] = true;
+      } else if (crem > 0) {
+        const REntry* ce = h.find((uint32_t)crem, i);
+        go[half] = ce && (ce->pad & 1u);
+      }
+    }
+  }
+  return M128{(uint64_t)__ballot(go[0]), (uint64_t)__ballot(go[1])};
+}
+__device__ int rec_enumerate_wave(const TableArgs& t, const Lds& s, const RHash& h, RPFrame* stk, uint8_t* path,
+                                  uint32_t target, int64_t thr, uint8_t* dst, uint64_t& count, uint64_t& bytes) {
+  const int lane = threadIdx.x & 63;
+  const REntry* e = h.find(target, 1);
+  if (!e) return -3;
+  if (!(e->pad & 1u)) return 0;
+  uint32_t rem = target;
+  M128 todo = rec_todo(t, s, h, rem, e, thr);
+  int d = 0;
+  for (;;) {
+    if (mzero(todo)) {
+      if (d == 0) break;
+      const RPFrame f = stk[--d];
+      rem = f.rem;
+      todo = M128{f.t0, f.t1};
+      continue;
+    }
+    const int i = mlow(todo);
+    todo = mclear(todo, i);
+    path[d] = (uint8_t)i;
+    const int64_t crem = (int64_t)rem - s.w[i];
+    if (rec_leaf(crem, thr)) {  // a candidate: rows path[0..d] (ascending)
+      if (dst && lane <= d + 1) dst[bytes + lane] = lane == 0 ? (uint8_t)(d + 1) : path[lane - 1];
+      count++;
+      bytes += (uint64_t)d + 2;
+      continue;
+    }
+    const REntry* ce = h.find((uint32_t)crem, i);  // non-empty memo node (rec_todo)
+    if (!ce) return -3;
+    if (d + 1 >= kMaxDepth) return -2;
+    stk[d++] = RPFrame{todo.a, todo.b, rem, 0};
+    rem = (uint32_t)crem;
+    todo = rec_todo(t, s, h, rem, ce, thr);
+  }
+  return 0;
 }
 
 // phase 2: candidates in the reference's list order; dst == nullptr counts.
 // path: this lane's row per level (LDS, stride kRecLanes).
+template <bool WAVE>
 __device__ int rec_enumerate(const TableArgs& t, const Lds& s, const RHash& h, RFrame* stk, uint8_t* path,
                              uint32_t target, int64_t thr, uint8_t* dst, uint64_t cap_count, uint64_t& count,
                              uint64_t& bytes) {
@@ -1942,7 +2387,7 @@ __device__ int rec_enumerate(const TableArgs& t, const Lds& s, const RHash& h, R
   while (true) {
     if (mzero(rest)) {
       if (d == 0) break;
-      const RFrame f = stk[(--d) * kRecLanes];
+      const RFrame f = stk[(--d) * (WAVE ? 1 : kRecLanes)];
       const REntry* pe = h.e + f.slot;
       slot = f.slot;
       rem = f.rem;
@@ -1951,12 +2396,12 @@ __device__ int rec_enumerate(const TableArgs& t, const Lds& s, const RHash& h, R
     }
     const int i = mlow(rest);
     rest = mclear(rest, i);
-    path[d * kRecLanes] = (uint8_t)i;
+    path[d * (WAVE ? 1 : kRecLanes)] = (uint8_t)i;
     const int64_t crem = (int64_t)rem - s.w[i];
     if (rec_leaf(crem, thr)) {  // a candidate: rows path[0..d] (ascending)
       if (dst && count < cap_count) {
         dst[bytes] = (uint8_t)(d + 1);
-        for (int k = 0; k <= d; ++k) dst[bytes + 1 + k] = path[k * kRecLanes];
+        for (int k = 0; k <= d; ++k) dst[bytes + 1 + k] = path[k * (WAVE ? 1 : kRecLanes)];
       }
       count++;
       bytes += (uint64_t)d + 2;
@@ -1966,7 +2411,7 @@ __device__ int rec_enumerate(const TableArgs& t, const Lds& s, const RHash& h, R
     const REntry* ce = h.find((uint32_t)crem, i);
     if (!ce) return -3;  // phase 1 memoised every non-base child it reached
     if (d + 1 >= kMaxDepth) return -2;
-    stk[(d++) * kRecLanes] = RFrame{slot, rem, 0, 0, 0, (uint8_t)(i + 1), 0, 0};
+    stk[(d++) * (WAVE ? 1 : kRecLanes)] = RFrame{slot, rem, 0, 0, 0, (uint8_t)(i + 1), 0, 0};
     slot = (uint32_t)(ce - h.e);
     rem = (uint32_t)crem;
     rest = M128{ce->en0, ce->en1};
@@ -1974,20 +2419,26 @@ __device__ int rec_enumerate(const TableArgs& t, const Lds& s, const RHash& h, R
   return 0;
 }
 
+// WAVE: one query per 64-lane block; the DFS state (and its LDS stack) is
+// wave-uniform, the lanes split the prefetch loads.  Else one query per lane.
+template <bool WAVE>
 __global__ __launch_bounds__(kRecLanes) void k_explain_recursion(TableArgs t, QueryArgs q, OutArgs out, char* hash,
                                                                  uint32_t hash_cap) {
+  constexpr int kLanesPerStack = WAVE ? 1 : kRecLanes;
   __shared__ Lds s;
-  __shared__ RFrame stk_all[kMaxDepth * kRecLanes];  // 96 KB
-  __shared__ uint8_t path_all[kMaxDepth * kRecLanes];
+  __shared__ RFrame stk_all[kMaxDepth * kLanesPerStack];  // 96 KB per block in lane mode
+  __shared__ uint8_t path_all[kMaxDepth * kLanesPerStack];
+  __shared__ RWFrame wstk[WAVE ? kMaxDepth : 1];           // phase 1 of the wave mode
+  __shared__ RPFrame pstk[WAVE ? kMaxDepth : 1];           // phase 2 of the wave mode
   stage_rows(s, t);
-  const int64_t gid = (int64_t)blockIdx.x * kRecLanes + threadIdx.x;
-  const int64_t nthreads = (int64_t)gridDim.x * kRecLanes;
-  RFrame* stk = stk_all + threadIdx.x;
-  uint8_t* path = path_all + threadIdx.x;
+  const int64_t gid = WAVE ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * kRecLanes + threadIdx.x;
+  const int64_t nthreads = WAVE ? (int64_t)gridDim.x : (int64_t)gridDim.x * kRecLanes;
+  RFrame* stk = stk_all + (WAVE ? 0 : threadIdx.x);
+  uint8_t* path = path_all + (WAVE ? 0 : threadIdx.x);
   RHash h;
   h.e = (REntry*)(hash + (size_t)gid * hash_cap * sizeof(REntry));
   h.mask = hash_cap - 1;
-  h.limit = (uint32_t)(hash_cap * 0.7);
+  h.limit = hash_cap / 4;  // load factor <= 1/4: a wave waits for its longest probe chain
   uint64_t epoch = 0;
   for (int64_t i = gid; i < q.n; i += nthreads) {
     int64_t target, thr;
@@ -2010,9 +2461,12 @@ __global__ __launch_bounds__(kRecLanes) void k_explain_recursion(TableArgs t, Qu
       h.epoch = ++epoch;  // the workspace was zeroed: epochs 1, 2, ... are fresh
       h.used = 0;
       uint64_t nodes = 0;
-      int rc = rec_phase1(t, s, h, stk, (uint32_t)target, thr, A, q.node_budget, nodes);
+      int rc = WAVE ? rec_phase1_wave(t, s, h, wstk, (uint32_t)target, thr, A, q.node_budget, nodes)
+                    : rec_phase1<WAVE>(t, s, h, stk, (uint32_t)target, thr, A, q.node_budget, nodes);
       if (rc > 0) rc = 0;
-      if (rc == 0) rc = rec_enumerate(t, s, h, stk, path, (uint32_t)target, thr, nullptr, 0, count, bytes);
+      if (rc == 0)
+        rc = WAVE ? rec_enumerate_wave(t, s, h, pstk, path, (uint32_t)target, thr, nullptr, count, bytes)
+                  : rec_enumerate<WAVE>(t, s, h, stk, path, (uint32_t)target, thr, nullptr, 0, count, bytes);
       if (rc == -1) {
         status = (int8_t)kStatusExactRetry;
       } else if (rc < 0) {
@@ -2024,12 +2478,22 @@ __global__ __launch_bounds__(kRecLanes) void k_explain_recursion(TableArgs t, Qu
         status = SST_OVERFLOW;
       } else {
         status = SST_SOME;
-        off = out.spill_base + atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
+        if (WAVE) {  // one allocation per wave, broadcast
+          unsigned long long sb = 0;
+          if ((threadIdx.x & 63) == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
+          off = out.spill_base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sb >> 32)) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sb));
+        } else {
+          off = out.spill_base + atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
+        }
         if (off + bytes > out.arena_bytes) {
           status = (int8_t)kStatusArenaRetry;
         } else {
           uint64_t c2 = 0, b2 = 0;
-          rec_enumerate(t, s, h, stk, path, (uint32_t)target, thr, out.payload + off, ~0ull, c2, b2);
+          if (WAVE)
+            rec_enumerate_wave(t, s, h, pstk, path, (uint32_t)target, thr, out.payload + off, c2, b2);
+          else
+            rec_enumerate<WAVE>(t, s, h, stk, path, (uint32_t)target, thr, out.payload + off, ~0ull, c2, b2);
         }
       }
     }
@@ -2173,19 +2637,19 @@ hipError_t launch_layer_step(const uint64_t* prev, uint64_t* next, int64_t nword
   return hipGetLastError();
 }
 hipError_t launch_length_bound(const TableArgs& t, const LBArgs& q, char* hash, int8_t* vals, char* frames,
-                               uint32_t hash_cap, int exact_lanes, bool fast_pass, hipStream_t st) {
+                               uint32_t hash_cap, int exact_units, bool fast_pass, hipStream_t st) {
   if (q.n <= 0) return hipSuccess;
   if (fast_pass) hipLaunchKernelGGL(k_length_fast, dim3(blocks_for(q.n, 256)), dim3(256), 0, st, t, q);
-  if (exact_lanes >= 64)
-    hipLaunchKernelGGL(k_length_exact, dim3(exact_lanes / 64), dim3(64), 0, st, t, q, hash, vals, frames, hash_cap);
+  if (exact_units >= 1)  // one 64-lane block per query in flight
+    hipLaunchKernelGGL(k_length_exact<true>, dim3(exact_units), dim3(64), 0, st, t, q, hash, vals, frames, hash_cap);
   return hipGetLastError();
 }
-size_t lb_frame_bytes() { return kMaxDepth * (sizeof(P1Frame) + sizeof(LBFrame)); }
+size_t lb_frame_bytes() { return kLBFrameBytes; }
 
 hipError_t launch_explain_recursion(const TableArgs& t, const QueryArgs& q, const OutArgs& o, char* hash,
-                                   char* /*frames: in LDS*/, uint32_t hash_cap, int lanes, hipStream_t st) {
-  if (q.n <= 0 || lanes < kRecLanes) return hipSuccess;
-  hipLaunchKernelGGL(k_explain_recursion, dim3(lanes / kRecLanes), dim3(kRecLanes), 0, st, t, q, o, hash, hash_cap);
+                                   char* /*frames: in LDS*/, uint32_t hash_cap, int units, hipStream_t st) {
+  if (q.n <= 0 || units < 1) return hipSuccess;  // one 64-lane block per query in flight
+  hipLaunchKernelGGL(k_explain_recursion<true>, dim3(units), dim3(kRecLanes), 0, st, t, q, o, hash, hash_cap);
   return hipGetLastError();
 }
 size_t rec_frame_bytes() { return 64; }  // frames live in LDS; kept for the host's workspace sizing
