@@ -965,6 +965,52 @@ __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* f
   return 0;
 }
 
+// Classification of a fresh frame's children in one probe round (wave mode).
+// For child (c = m - w_r, r) two of the three outcomes of its visit are
+// settled now and cannot change before the replay reaches row r:
+//   r < lo(c): pair(r, c) == 0, [] without memo (static);
+//   hv(c) >= r: memo hit, non-empty iff ne(c) <= r (hv only grows, and an ne
+//     <= hv is final: an ne set later lies above the hv of that time);
+// and the third, hv(c) < r, stays a first visit: the nodes inside an earlier
+// sibling's subtree have rows r' < r and raise hv(c) to at most r' < r.
+// Only those children are descended (ascending rows, as the reference).  The
+// frame's lowest non-empty row is the minimum over its rows (the sequential
+// replay meets them in ascending order, so "first found" is the minimum).
+__device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, const Hash& h, uint32_t m, M128 rows,
+                                            int& ne) {
+  const int lane = threadIdx.x & 63;
+  bool desc[2];
+  int nrow = 0xFF;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lane + 64 * half;
+    desc[half] = false;
+    if (r < t.n_rows && mtest(rows, r)) {
+      const int64_t c = (int64_t)m - s.w[r];
+      if (c == 0) {
+        nrow = nrow < r ? nrow : r;
+      } else if (c > 0 && r >= rec_lo(ld_index(t.index, c))) {
+        const HEntry* ce = h.find((uint32_t)c);
+        const uint32_t meta = ce ? ce->meta : 0xFFFFu;
+        const int hv = (meta & 0xFF) == 0xFF ? -1 : (int)(meta & 0xFF);
+        if (r <= hv) {
+          const int nec = (int)((meta >> 8) & 0xFF);
+          if (nec != 0xFF && r >= nec) nrow = nrow < r ? nrow : r;
+        } else {
+          desc[half] = true;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const int o = __shfl_xor(nrow, off, 64);
+    nrow = nrow < o ? nrow : o;
+  }
+  ne = ne < nrow ? ne : nrow;
+  return M128{(uint64_t)__ballot(desc[0]), (uint64_t)__ballot(desc[1])};
+}
+
 // phase1_body for one query per wave: the same replay, with the saved frames
 // in LDS and the current frame's lowest non-empty row in a register (written
 // to its memo entry once, when the frame completes -- no other node can read
@@ -985,6 +1031,7 @@ __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Fra
     uint32_t m = (uint32_t)v, meta = h.last_meta;
     int A = A0, B = s.cap[top], rtop = top, d = 0;
     int ne = (int)((meta >> 8) & 0xFF);
+    rest = p1_classify(t, s, h, m, rest, ne);
     for (;;) {
       if (mzero(rest)) {  // frame done: publish its non-empty row, report to the parent
         e->meta = (meta & ~0xFF00u) | ((uint32_t)ne << 8);
@@ -1000,7 +1047,7 @@ __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Fra
         ne = f.ne;
         meta = f.meta;
         const int rr = f.rnext - 1;
-        if (cne != 0xFF && rr >= cne && ne == 0xFF) ne = rr;
+        if (cne != 0xFF && rr >= cne) ne = ne < rr ? ne : rr;
         continue;
       }
       const int rr = mlow(rest);
@@ -1028,10 +1075,11 @@ __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Fra
           rtop = rr;
           meta = h.last_meta;
           ne = (int)((meta >> 8) & 0xFF);
+          rest = p1_classify(t, s, h, m, rest, ne);
           continue;
         }
       }
-      if (nonempty && ne == 0xFF) ne = rr;  // lowest non-empty row (first found wins)
+      if (nonempty) ne = ne < rr ? ne : rr;  // lowest non-empty row
     }
   }
   return 0;
