@@ -120,3 +120,12 @@ def test_length_bound_errors(engine, alphabet_rows):
     assert int(st[0]) == _native.SST_OUT_OF_TABLE
     assert int(st[1]) == _native.SST_LB_EMPTY_WINDOW
     assert int(st[2]) == 0 and int(got[2]) == 1  # only negative values: default -> 1
+
+
+def test_full_alphabet_6mer_vs_oracle(engine, alphabet_rows):
+    # whole 6-mers over the full alphabet: budgets bind (A = 3 < 6 items), so
+    # the exact replay's first-visit classification is exercised at depth
+    rng = np.random.default_rng(6)
+    ms = alphabet_rows
+    su = np.array([rng.choice(ms[1:], 6).sum() * 1e-3 for _ in range(2)])
+    _check(engine, ms, 6, su, su)

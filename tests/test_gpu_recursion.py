@@ -87,3 +87,21 @@ def test_recursion_default_threshold(full_dev):
     for i in range(len(masses)):
         st, sols, n_empty = oracle.explain_recursion(alph, masses[i], None, 1e-5, 3)
         assert res.candidates(i) == sols
+
+
+def test_recursion_whole_masses_ordered_vs_oracle(full_dev):
+    # deep DAGs (the reference's CCUAGG 6-mer and random 4/5-mers with mods):
+    # the wave-mode first-visit replay and enumeration give the reference's
+    # candidate list in its order
+    ms, dev = full_dev
+    is_mod, caps = _alph(ms, 6)
+    dev.set_budgets(is_mod, caps)
+    alph = oracle.Alphabet(ms, is_mod, caps)
+    rng = np.random.default_rng(3)
+    masses = [1935.25876] + [rng.choice(ms[1:], k).sum() * 1e-3 for k in (4, 5, 5)]
+    for A in (3, 2):
+        res = dev.explain_recursion(masses, None, 1e-5, 1e-3, A)
+        for i, m in enumerate(masses):
+            st, sols, n_empty = oracle.explain_recursion(alph, m, None, 1e-5, A)
+            assert int(res.status[i]) == (_native.SST_SOME if sols else _native.SST_NONE), (i, m, A)
+            assert res.candidates(i) == sols, (i, m, A)
