@@ -41,7 +41,7 @@ extern "C" {
 #define SST_OUT_OF_TABLE (-1) /* reference raises (NameError in explain,    */
                               /* NotImplementedError in is_valid_mass)      */
 #define SST_OVERFLOW (-2)   /* count > cap_per_query: exact count, no payload */
-#define SST_ABORTED (-4)    /* node budget exhausted: count is a lower bound */
+#define SST_ABORTED (-4)    /* DFS node guard (2^34 nodes) exhausted: count is a lower bound */
 
 /* ---- per-query result of sst_is_valid_batch ------------------------- */
 /*  1 = True, 0 = False, -1 = reference raises NotImplementedError          */
