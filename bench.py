@@ -144,6 +144,8 @@ def main():
                     help="N>1: gather every query's result to rank 0 over RCCL inside the timed step")
     ap.add_argument("--event-every", type=int, default=4,
                     help="bracket every n-th launch of the roofline kernel with HIP events (>= 1)")
+    ap.add_argument("--no-validate", action="store_true",
+                    help="diagnostic builds only: skip the result checks after the timed region")
     ap.add_argument("--no-events", action="store_true",
                     help="diagnostic: time the steps without the per-kernel HIP events (no roofline)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"),
@@ -247,7 +249,7 @@ def main():
     # results of the last step (validation + algorithmic bytes)
     res.fetch_device()
     st = res.status
-    if (st < -2).any():
+    if (st < -2).any() and not args.no_validate:
         raise RuntimeError(f"internal statuses in results: {np.unique(st[st < -2])}")
     stats = res.stats()
     v7 = out7.cpu().numpy()
@@ -267,7 +269,7 @@ def main():
     w_min = min(m.mass for m in dp.masses if m.mass > 0)
     pair = (w8 > 0) & (hi8 < 3 * w_min)
     n_pair, n_work, nodes = int(stats[6]), int(stats[0]), int(stats[4])
-    if int(pair.sum()) != n_pair:
+    if int(pair.sum()) != n_pair and not args.no_validate:
         raise RuntimeError(f"pair-path partition {int(pair.sum())} != engine counter {n_pair}")
     some = (st == 2) | (st == -2)
     # algorithmic HBM bytes per launch (DESIGN.md "Measurement"); the LDS pair
