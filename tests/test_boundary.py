@@ -59,6 +59,7 @@ def test_null_arguments_rejected():
     assert lib.sst_is_valid_batch(None, None, None, 0, 1e-5, 1e-3, None) < 0
     assert lib.sst_explain_batch(None, None, None, 0, 1e-5, 1e-3, None, 0, 1, 1, None) < 0
     assert lib.sst_result_stats(None, None) < 0
+    assert lib.sst_profile_sample(None, 1) < 0
     assert lib.sst_last_error(None) == b"null context"
 
 

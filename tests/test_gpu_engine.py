@@ -216,3 +216,19 @@ def test_quantisation_boundaries_vs_oracle(engine, prec):
         assert int(res.status[i]) == want_st, (i, masses[i], thr[i])
         assert res.candidates(i) == sols, (i, masses[i], thr[i])
     dev.close()
+
+
+def test_profile_sampling(full_dev, alphabet_rows):
+    # sst_profile_sample: only every n-th launch of a selected kernel is
+    # bracketed with events (bench.py --event-every)
+    eng = full_dev.engine
+    rng = np.random.default_rng(2)
+    masses, thr = _random_queries(rng, alphabet_rows, 512, kmax=2)
+    eng.profile(True, kernels=(_native.K_EXPLAIN_SCAN,), every=3)
+    for _ in range(7):
+        full_dev.explain(masses, thr, 1e-5, 1e-3, 10)
+    prof = eng.profile_read()
+    eng.profile(False)
+    assert set(prof) == {_native.K_EXPLAIN_SCAN}
+    assert prof[_native.K_EXPLAIN_SCAN][1] == 3  # launches 0, 3 and 6
+    assert prof[_native.K_EXPLAIN_SCAN][0] > 0
