@@ -144,6 +144,9 @@ def main():
                     help="N>1: gather every query's result to rank 0 over RCCL inside the timed step")
     ap.add_argument("--event-every", type=int, default=4,
                     help="bracket every n-th launch of the roofline kernel with HIP events (>= 1)")
+    ap.add_argument("--a7-stream", type=int, default=0,
+                    help="1: queue the A7 batch on a second HIP stream, concurrent with the A8 chain "
+                         "(sst_ctx_set_stream); 0: both on the engine stream, one after the other")
     ap.add_argument("--no-validate", action="store_true",
                     help="diagnostic builds only: skip the result checks after the timed region")
     ap.add_argument("--no-events", action="store_true",
@@ -193,13 +196,28 @@ def main():
     res = None
     gath = Gatherer(dist, dev_t) if (dist and args.gather) else None
 
+    side = torch.cuda.Stream(device=dev_t) if args.a7_stream else None
+
     def step():
         nonlocal res
+        # A8 chain first (its persistent scan grid fills the chip), then A7 on
+        # the side stream: its blocks take the CUs the scan's waves leave and
+        # run through the A8 tail launches.  The two touch disjoint buffers;
+        # the timed region ends with a device-wide synchronize.
+        if args.a7_stream != 2:
+            res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=res)
+        if side is not None:
+            engine.set_stream(side.cuda_stream)
         tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, out7.data_ptr())
-        res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=res)
+        if side is not None:
+            engine.set_stream(None)
+        if args.a7_stream == 2:
+            res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=res)
         if gath is not None:
             st, cnt, off, pay, _cap = res.device_views()  # queues the compaction: offsets index the dense payload
             torch.cuda.current_stream().wait_stream(ext)  # after the compaction, before torch reads the buffers
+            if side is not None:
+                torch.cuda.current_stream().wait_stream(side)  # A7 results
             flat = torch.cat([out7.view(torch.uint8), device_bytes(st, n8, dev_t), device_bytes(cnt, 8 * n8, dev_t),
                               device_bytes(off, 8 * n8, dev_t), device_bytes(pay, payload_bytes, dev_t)])
             gath.gather(flat)
@@ -332,6 +350,7 @@ def main():
             "a8_queries": n8_all,
             "max_len": seq.max_len,
             "max_modifications": A,
+            "a7_stream": ("side stream, concurrent with the A8 chain" if args.a7_stream else "engine stream"),
             "parallelism": (f"spectra sharded over {world} GPUs, results kept per rank"
                             + (", RCCL gather of all results to rank 0 in the step" if args.gather else "")
                             if world > 1 else "1 GPU"),

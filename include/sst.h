@@ -59,6 +59,14 @@ void sst_ctx_destroy(sst_ctx* ctx);
 const char* sst_last_error(const sst_ctx* ctx);
 /* The HIP stream all work of this ctx is queued on (hipStream_t). */
 void* sst_ctx_stream(sst_ctx* ctx);
+/* Queue this ctx's subsequent work on `stream` (a hipStream_t of the ctx's
+ * device, owned by the caller), or on the ctx's own stream again when NULL.
+ * Set-stream semantics as in rocBLAS: nothing is ordered across the switch,
+ * the caller orders work on different streams (events).  A result's later
+ * operations (compaction, fetch, free) go to the ctx's stream at that time.  Used to overlap the A7
+ * batch with the A8 chain (bench.py).  No reference equivalent (the
+ * reference is single-threaded Python). */
+int sst_ctx_set_stream(sst_ctx* ctx, void* stream);
 /* Wait for all queued work of this ctx. */
 int sst_ctx_synchronize(sst_ctx* ctx);
 

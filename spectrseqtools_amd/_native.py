@@ -26,7 +26,7 @@ EXPORTS = (
     "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
-    "sst_is_singleton_batch_device",
+    "sst_is_singleton_batch_device", "sst_ctx_set_stream",
 )
 
 # kernel ids of sst_profile_read
@@ -81,6 +81,8 @@ def load_library(path=LIB_PATH):
     lib.sst_last_error.restype = ctypes.c_char_p
     lib.sst_ctx_stream.argtypes = [_P]
     lib.sst_ctx_stream.restype = _P
+    lib.sst_ctx_set_stream.argtypes = [_P, _P]
+    lib.sst_ctx_set_stream.restype = _I
     lib.sst_ctx_synchronize.argtypes = [_P]
     lib.sst_table_build.argtypes = [_P, _P, _I, _I64, _I, _PP]
     lib.sst_table_upload.argtypes = [_P, _P, _I, _P, _I64, _I, _PP]
@@ -155,6 +157,12 @@ class Engine:
     @property
     def stream(self):
         return self._lib.sst_ctx_stream(self.handle)
+
+    def set_stream(self, stream=None):
+        """Queue subsequent work on `stream` (a hipStream_t handle, e.g.
+        torch.cuda.Stream().cuda_stream), or on the engine's own stream when
+        None.  The caller orders work across streams (sst_ctx_set_stream)."""
+        self.check(self._lib.sst_ctx_set_stream(self.handle, stream), "sst_ctx_set_stream")
 
     def synchronize(self):
         self.check(self._lib.sst_ctx_synchronize(self.handle), "sst_ctx_synchronize")

@@ -49,7 +49,8 @@ struct DevBuf {
 
 struct sst_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // where work is queued: `own`, or the caller's (sst_ctx_set_stream)
+  hipStream_t own = nullptr;
   std::string err;
   std::recursive_mutex mu;
   // staging for host-pointer calls
@@ -108,6 +109,7 @@ struct sst_result {
   uint64_t work_region = 0;
   uint64_t region_bytes = 0, spill_bytes = 0;
   bool compacted = false;
+  bool hits = false;  // the last pass's scan left hit lists (k_explain_scan) for the compaction to scatter
   uint64_t arena_bytes = 0;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
@@ -380,10 +382,11 @@ int sst_ctx_create(int device, sst_ctx** out) {
     if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0) c->n_cu = cu;
     (void)hipGetLastError();
   }
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return SST_E_HIP;
   }
+  c->stream = c->own;
   *out = c;
   return SST_OK;
 }
@@ -392,18 +395,26 @@ void sst_ctx_destroy(sst_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->own);
   for (DevBuf* b : {&c->in_mass, &c->in_thr, &c->in_mods, &c->out_valid, &c->ws_deep, &c->ws_hash, &c->ws_frames,
                     &c->ws_stacks, &c->ws_epochs, &c->singleton_masses})
     b->release();
   prof_resolve(c);
   for (hipEvent_t e : c->pool) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(c->stream);
+  (void)hipStreamDestroy(c->own);
   delete c;
 }
 
 const char* sst_last_error(const sst_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 void* sst_ctx_stream(sst_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int sst_ctx_set_stream(sst_ctx* c, void* stream) {
+  if (!c) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  c->stream = stream ? (hipStream_t)stream : c->own;
+  return SST_OK;
+}
 
 int sst_ctx_synchronize(sst_ctx* c) {
   if (!c) return SST_E_ARG;
@@ -747,6 +758,7 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   {
     Prof p(c, SST_K_EXPLAIN_MAIN);
     HIP_OK(c, launch_explain_scan(t->args, q, o, (int)(r->n_scan_waves / (kScanWG / 64)), c->stream));
+    r->hits = n > 0;  // every scan wave writes its hit-list length (0 for k_bitset_scan)
   }
   {
     Prof p(c, SST_K_EXPLAIN_EXPAND);
@@ -787,7 +799,7 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out) {
       !r->wave_stats.ensure((size_t)r->n_regions * kNumStats * 8) ||
       !r->prefix.ensure((size_t)(r->n_regions + 2) * 8) ||
       !r->work.ensure((size_t)r->n_scan_waves * r->work_region * 16) ||
-      !r->work_count.ensure((size_t)r->n_scan_waves * 4)) {
+      !r->work_count.ensure((size_t)r->n_scan_waves * 2 * 4)) {  // worklist lengths, then hit-list lengths
     free_result_bufs(r);
     delete r;
     return fail(c, SST_E_NOMEM, "device allocation failed (result)");
@@ -803,7 +815,8 @@ int compact(sst_result* r) {
   if (r->compacted) return SST_OK;
   if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, 1)))
     return fail(c, SST_E_NOMEM, "device allocation failed (compaction)");
-  HIP_OK(c, launch_compact(out_args(r), r->n, r->n_regions, (uint64_t*)r->prefix.p, (uint8_t*)r->dense.p, c->stream));
+  HIP_OK(c, launch_compact(out_args(r), r->n, r->n_regions, (uint64_t*)r->prefix.p, (uint8_t*)r->dense.p, r->hits,
+                           c->stream));
   r->compacted = true;
   return SST_OK;
 }

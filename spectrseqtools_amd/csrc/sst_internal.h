@@ -117,8 +117,9 @@ struct OutArgs {
   int ctl_words;
   uint64_t* wave_used;        // [n_waves] bytes used in each region (expand kernel waves)
   unsigned long long* wave_stats;  // [n_waves][kNumStats] expand-kernel counters
-  uint4* work;                // [n_scan_waves][work_region] queued SHALLOW {query, a, b, has_zero}
-  uint32_t* work_count;       // [n_scan_waves]
+  uint4* work;                // [n_scan_waves][work_region] queued SHALLOW {query, a, b, has_zero} from the
+                              // front, hit records {query, count, offset lo, hi} from the back
+  uint32_t* work_count;       // [2][n_scan_waves]: worklist lengths, then hit-list lengths (k_explain_scan)
   uint64_t work_region;
   int64_t n_scan_waves;
   uint32_t* counters;  // [kNumClasses]
@@ -182,7 +183,7 @@ hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const O
 int explain_scan_blocks_per_cu(size_t dyn_lds);
 int explain_expand_blocks_per_cu();
 size_t scan_dyn_lds(const TableArgs& t);
-hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* wave_prefix, uint8_t* dst,
+hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* wave_prefix, uint8_t* dst, bool hits,
                           hipStream_t st);
 hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const OutArgs& o, void* ws_deep,
                                    int deep_blocks, const ExactWs& ws, int exact_blocks, hipStream_t st);

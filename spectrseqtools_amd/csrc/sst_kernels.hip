@@ -1306,6 +1306,12 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   uint32_t st_q = 0, st_payload = 0;
   uint4* wl = out.work + (uint64_t)wave * out.work_region;
   uint32_t n_work = 0;  // wave-uniform
+  // hit list: one {query, count, offset} record per SOME / OVERFLOW query,
+  // filled from the END of the wave's worklist region (a query is either
+  // queued or a hit, so the two never meet); k_scatter_hits turns it into the
+  // per-query count / offset arrays at compaction
+  uint4* hits = wl + out.work_region - 1;
+  uint32_t n_hit = 0;  // wave-uniform
   // Software pipeline, two tiles deep: a tile's inputs are loaded two tiles
   // ahead into one of two register sets that swap roles between the unrolled
   // steps (no copies), and each load is issued AFTER the previous tile's
@@ -1375,13 +1381,19 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     st_payload += pb;
     st_q += pair ? 1u : 0u;
     // NONE / EMPTY / OUT_OF_TABLE carry no candidates: count and offset stay
-    // undefined (include/sst.h), one byte per resolved query
-    if (live && !work) {
-      out.status[i] = retry ? (int8_t)kStatusArenaRetry : status;
-      if (cnt && !retry) {  // SOME or OVERFLOW
-        *q_at(out.count, i) = cnt;
-        *q_at(out.offset, i) = pb ? off : 0;
+    // undefined (include/sst.h), one byte per resolved query.  SOME and
+    // OVERFLOW append a 16-B hit record instead of two scattered 8-B stores
+    // (those were partial-line writes: 3x write amplification in the PMC)
+    if (live && !work) out.status[i] = retry ? (int8_t)kStatusArenaRetry : status;
+    const bool hit = cnt && !retry;  // pair path only: cnt == 0 off it
+    const uint64_t hbal = __ballot(hit);
+    if (hbal) {  // wave-uniform
+      if (hit) {
+        const uint64_t o = pb ? off : 0;
+        *(hits - (n_hit + (uint32_t)__builtin_popcountll(hbal & lane_mask_lt(lane)))) =
+            make_uint4(i, cnt, (uint32_t)o, (uint32_t)(o >> 32));
       }
+      n_hit += (uint32_t)__builtin_popcountll(hbal);
     }
     const uint64_t bal = __ballot(work);
     if (bal) {  // wave-uniform
@@ -1404,6 +1416,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   }
   if (lane == 0) {
     out.work_count[wave] = n_work;
+    out.work_count[out.n_scan_waves + wave] = n_hit;
     if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle expand launch exit at once
   }
   wave_stats_flush(out, wave, lane, used, kStatPair, kStatPairPayload, st_q, 0, st_payload);
@@ -1462,6 +1475,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryAr
   }
   if (lane == 0) {
     out.work_count[wave] = n_work;
+    out.work_count[out.n_scan_waves + wave] = 0;  // no hit list: the expand kernel writes count / offset
     if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle expand launch exit at once
   }
   wave_stats_flush(out, wave, lane, 0, kStatPair, kStatPairPayload, 0, 0, 0);
@@ -1600,6 +1614,23 @@ __global__ __launch_bounds__(256) void k_compact_copy(const uint8_t* __restrict_
       to = pre[n_waves];
     }
     for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) dst[to + k] = src[from + k];
+  }
+}
+
+// The scan's hit lists -> count[i] and (arena) offset[i]; runs before
+// k_compact_offsets rewrites the offsets into the dense payload.
+__global__ __launch_bounds__(256) void k_scatter_hits(const uint4* __restrict__ work,
+                                                      const uint32_t* __restrict__ hit_count, uint64_t region,
+                                                      int64_t n_scan_waves, uint64_t* __restrict__ count,
+                                                      uint64_t* __restrict__ offset) {
+  for (int64_t w = blockIdx.x; w < n_scan_waves; w += gridDim.x) {
+    const uint32_t nh = hit_count[w];
+    const uint4* top = work + (uint64_t)(w + 1) * region - 1;
+    for (uint32_t k = threadIdx.x; k < nh; k += blockDim.x) {
+      const uint4 h = *(top - k);
+      count[h.x] = h.y;
+      offset[h.x] = ((uint64_t)h.w << 32) | h.z;
+    }
   }
 }
 
@@ -2657,11 +2688,16 @@ int explain_scan_blocks_per_cu(size_t dyn) {
              : occupancy((const void*)k_bitset_scan, kScanWG, 0);
 }
 int explain_expand_blocks_per_cu() { return occupancy((const void*)k_explain_expand, kWG, 0); }
-hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* pre, uint8_t* dst, hipStream_t st) {
+hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* pre, uint8_t* dst, bool hits,
+                          hipStream_t st) {
   const uint64_t spill_cap = o.arena_bytes > o.spill_base ? o.arena_bytes - o.spill_base : 0;
   hipLaunchKernelGGL(k_wave_prefix, dim3(1), dim3(1024), 0, st, o.wave_used, n_waves, o.cursor, spill_cap, pre);
   hipLaunchKernelGGL(k_compact_copy, dim3(2048), dim3(256), 0, st, o.payload, dst, o.wave_used, pre, n_waves,
                      o.region_bytes, o.spill_base, o.cursor, spill_cap);
+  if (n > 0 && hits)
+    hipLaunchKernelGGL(k_scatter_hits, dim3(2048), dim3(256), 0, st, (const uint4*)o.work,
+                       (const uint32_t*)o.work_count + o.n_scan_waves, o.work_region, o.n_scan_waves, o.count,
+                       o.offset);
   if (n > 0)
     hipLaunchKernelGGL(k_compact_offsets, dim3(blocks_for(n, 256)), dim3(256), 0, st, o.status, o.count, o.offset, n,
                        pre, n_waves, o.region_bytes, o.spill_base);
