@@ -161,7 +161,11 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
  *   does not spend HBM writes on them). */
 int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count, const uint64_t** offset,
                     const uint8_t** payload, uint64_t* payload_bytes);
-/* Device views (no copy). */
+/* Device views (no copy).  The first view or fetch after a pass queues the
+ * compaction on the ctx stream: the pair scan's hit lists ({query, count,
+ * offset} records written instead of scattered count/offset stores) are
+ * scattered into count[] / offset[], and the per-wave payload regions are
+ * packed into one dense payload that offset[] then indexes. */
 int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint64_t** d_offset,
                       uint8_t** d_payload, uint64_t* payload_bytes);
 /* Copy device results to the host views (synchronises the ctx stream). */
