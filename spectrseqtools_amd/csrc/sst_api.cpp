@@ -110,6 +110,9 @@ struct sst_result {
   uint64_t region_bytes = 0, spill_bytes = 0;
   bool compacted = false;
   bool hits = false;  // the last pass's scan left hit lists (k_explain_scan) for the compaction to scatter
+  // the expand waves' arena regions hold data of an earlier pass (k_explain_expand ran); fresh results
+  // start with them zeroed (alloc_result)
+  bool expand_regions_dirty = false;
   uint64_t arena_bytes = 0;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
@@ -760,15 +763,24 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
     HIP_OK(c, launch_explain_scan(t->args, q, o, (int)(r->n_scan_waves / (kScanWG / 64)), c->stream));
     r->hits = n > 0;  // every scan wave writes its hit-list length (0 for k_bitset_scan)
   }
-  {
+  if (!t->args.pairs_enabled) {  // the pair scan runs its queued windows itself
     Prof p(c, SST_K_EXPLAIN_EXPAND);
     HIP_OK(c, launch_explain_expand(t->args, q, o, r->n_waves / (kWG / 64), c->stream));
+    r->expand_regions_dirty = true;
+  } else if (r->expand_regions_dirty) {  // an earlier pass of this result launched it: empty its regions
+    HIP_OK(c, hipMemsetAsync((uint64_t*)r->wave_used.p + r->n_scan_waves, 0, (size_t)r->n_waves * 8, c->stream));
+    HIP_OK(c, hipMemsetAsync((unsigned long long*)r->wave_stats.p + r->n_scan_waves * kNumStats, 0,
+                             (size_t)r->n_waves * kNumStats * 8, c->stream));
+    r->expand_regions_dirty = false;
   }
   ExactWs ws{(char*)c->ws_hash.p, (char*)c->ws_frames.p, (char*)c->ws_stacks.p, (uint64_t*)c->ws_epochs.p,
              c->hash_cap};
   {
     Prof p(c, SST_K_EXPLAIN_DEEP);  // deep, no-memo and exact roles: one launch
-    HIP_OK(c, launch_explain_deferred(t->args, q, o, c->ws_deep.p, kDeepBlocks, ws, c->exact_blocks, c->stream));
+    // after the pair scan this launch also runs the SHALLOW windows (one wave per block, expand regions)
+    const int shallow_blocks = t->args.pairs_enabled ? std::min(r->n_waves, 4 * c->n_cu) : 0;
+    HIP_OK(c, launch_explain_deferred(t->args, q, o, c->ws_deep.p, shallow_blocks, kDeepBlocks, ws, c->exact_blocks,
+                                      c->stream));
   }
   return SST_OK;
 }
@@ -803,6 +815,13 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out) {
     free_result_bufs(r);
     delete r;
     return fail(c, SST_E_NOMEM, "device allocation failed (result)");
+  }
+  // the expand waves' regions stay empty unless k_explain_expand runs (tables without the pair list)
+  if (hipMemsetAsync(r->wave_used.p, 0, r->wave_used.bytes, c->stream) != hipSuccess ||
+      hipMemsetAsync(r->wave_stats.p, 0, r->wave_stats.bytes, c->stream) != hipSuccess) {
+    free_result_bufs(r);
+    delete r;
+    return fail(c, SST_E_HIP, "hipMemsetAsync failed (result)");
   }
   *out = r;
   return SST_OK;

@@ -186,7 +186,8 @@ size_t scan_dyn_lds(const TableArgs& t);
 hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* wave_prefix, uint8_t* dst, bool hits,
                           hipStream_t st);
 hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const OutArgs& o, void* ws_deep,
-                                   int deep_blocks, const ExactWs& ws, int exact_blocks, hipStream_t st);
+                                   int shallow_blocks, int deep_blocks, const ExactWs& ws, int exact_blocks,
+                                   hipStream_t st);
 size_t glob_frame_bytes();
 hipError_t launch_layer_step(const uint64_t* prev, uint64_t* next, int64_t nwords, const int* w, int n_rows,
                              hipStream_t st);

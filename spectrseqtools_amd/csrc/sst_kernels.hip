@@ -1202,6 +1202,10 @@ __device__ __forceinline__ TileOut tile_alloc(const OutArgs& out, int lane, uint
   return r;
 }
 
+// counters of the SHALLOW windows one wave ran (shallow_chunk)
+struct ShallowStats {
+  uint64_t q, nodes, payload;
+};
 __device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t region, int lane, uint64_t used,
                                                  int q_stat, int p_stat, uint64_t n_q, uint64_t nodes,
                                                  uint64_t payload) {
@@ -1274,6 +1278,66 @@ __device__ __forceinline__ void pair_store(const PairLds& p, uint32_t first, uin
     dst[len - 1u] = (uint8_t)(rec >> (8u * (len - 1u)));
     dst += len;
   }
+}
+
+// One 64-item chunk of a worklist: route unclassified windows (no reachable
+// value -> NONE / EMPTY; deeper than SHALLOW or budget-binding -> the deferred
+// class lists, status pending), run the SHALLOW fast path on the rest (all
+// DFS state and the first 16 payload bytes in VGPRs), allocate payload in the
+// wave's region and write status / count / offset.
+__device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArgs& q, const OutArgs& out, const Lds& s,
+                                              const uint4* wl, uint32_t k0, uint32_t nw, int lane, uint64_t region0,
+                                              uint64_t& used, ShallowStats& st) {
+  const bool live = k0 + lane < nw;
+  int64_t i = 0, a = 0, b = -1;
+  int8_t status = SST_NONE;
+  bool deferred = false;
+  RegSink sink;
+  EnumOut eo{0, 0, 0, 0};
+  if (live) {
+    const uint4 item = wl[k0 + lane];  // {query, first window value >= 1, last, kItem* flags}
+    i = item.x;
+    a = item.y;
+    b = item.z;
+    bool run = true;
+    if (item.w & kItemUnclassified) {  // from the pair-list scan: route it here
+      if (!window_has_roots(t.valid, a, b)) {
+        run = false;
+      } else if (!(item.w & kItemNever) || b >= t.shallow_hi) {
+        const int cls = (item.w & kItemNever) ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
+        const uint32_t slot = atomicAdd(&out.counters[cls], 1u);
+        out.lists[(int64_t)cls * q.n + slot] = (uint32_t)i;
+        run = false;
+        deferred = true;
+      }
+    }
+    if (run) {
+      shallow_window(t, s, a, b, sink, eo);
+      st.q++;
+      st.nodes += eo.nodes;
+    }
+    status = eo.count ? (eo.count > q.cap_count ? SST_OVERFLOW : SST_SOME)
+                      : ((item.w & kItemZero) ? SST_EMPTY : SST_NONE);
+    if (deferred) status = (int8_t)kStatusPending;
+  }
+  const TileOut to = tile_alloc(out, lane, region0, used, status == SST_SOME ? eo.bytes : 0, status);
+  if (to.bytes) {
+    if (!sink.over) {
+      sink.flush(out.payload + to.off, to.bytes);
+    } else {  // more than 16 bytes: enumerate again straight into the arena
+      MemSink3 ms{out.payload + to.off};
+      EnumOut e2{0, 0, 0, 0};
+      shallow_window(t, s, a, b, ms, e2);
+    }
+  }
+  if (live) {  // deferred queries: the deep / exact kernels write all three
+    out.status[i] = to.status;
+    if (!deferred) {
+      out.count[i] = eo.count;
+      out.offset[i] = to.bytes ? to.off : 0;
+    }
+  }
+  st.payload += to.bytes;
 }
 
 // 8 waves/SIMD: two 1024-lane workgroups per CU, each with its LDS copy of
@@ -1395,12 +1459,26 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
       }
       n_hit += (uint32_t)__builtin_popcountll(hbal);
     }
-    const uint64_t bal = __ballot(work);
-    if (bal) {  // wave-uniform
-      if (work)
-        wl[n_work + __builtin_popcountll(bal & lane_mask_lt(lane))] =
-            make_uint4(i, a, hi, (zero ? kItemZero : 0u) | kItemUnclassified | (never ? kItemNever : 0u));
-      n_work += (uint32_t)__builtin_popcountll(bal);
+    if (__ballot(work)) {  // wave-uniform, rare here: route the window now, so that the deferred class lists
+                           // are complete when the scan ends (one tail launch runs every class)
+      bool shallow = false;
+      if (work) {
+        int8_t st2 = zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;  // no reachable value in the window
+        if (window_has_roots(t.valid, a, hi)) {
+          if (never && hi < t.shallow_hi) {
+            shallow = true;  // <= 3 items, budgets cannot bind: the SHALLOW role writes all three
+          } else {
+            const int cls = never ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
+            const uint32_t slot = atomicAdd(&out.counters[cls], 1u);
+            out.lists[(int64_t)cls * q.n + slot] = i;
+            st2 = (int8_t)kStatusPending;
+          }
+        }
+        if (!shallow) out.status[i] = st2;
+      }
+      const uint64_t sb = __ballot(shallow);
+      if (shallow) wl[n_work + __builtin_popcountll(sb & lane_mask_lt(lane))] = make_uint4(i, a, hi, zero ? kItemZero : 0u);
+      n_work += (uint32_t)__builtin_popcountll(sb);
     }
   };
   double mA = 0.0, tA = 0.0, mB = 0.0, tB = 0.0;
@@ -1417,7 +1495,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   if (lane == 0) {
     out.work_count[wave] = n_work;
     out.work_count[out.n_scan_waves + wave] = n_hit;
-    if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle expand launch exit at once
+    if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle SHALLOW role exit at once
   }
   wave_stats_flush(out, wave, lane, used, kStatPair, kStatPairPayload, st_q, 0, st_payload);
 }
@@ -1482,17 +1560,16 @@ __global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryAr
 }
 
 // ---------------------------------------------------------------------------
-// Explain, part 2 -- k_explain_expand: the SHALLOW fast path for the queued
-// queries (all DFS state and the first 16 payload bytes in VGPRs).  Each wave
-// takes scan-wave worklist regions in a grid stride, 64 queries at a time;
-// payload goes to the wave's own arena region through a bump pointer fed by a
+// Explain, part 2 -- the SHALLOW fast path for queued windows: k_explain_expand
+// after k_bitset_scan (tables without the pair list), the first role of
+// k_explain_deferred after the pair scan (which routed every window).  Each wave takes
+// scan-wave worklist regions in a grid stride, 64 queries at a time; payload
+// goes to the wave's own arena region through a bump pointer fed by a
 // wavefront prefix sum (a full region spills: one atomic per tile).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kWG) void k_explain_expand(TableArgs t, QueryArgs q, OutArgs out) {
-  __shared__ Lds s;
+__device__ __forceinline__ void expand_body(const TableArgs& t, const QueryArgs& q, const OutArgs& out, Lds& s,
+                                            int64_t wave, int64_t n_waves) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6);
-  const int64_t n_waves = (int64_t)gridDim.x * (kWG / 64);
   const int64_t region = out.n_scan_waves + wave;  // expand regions follow the scan regions
   if (out.counters[kClassShallow] == 0) {  // nothing queued (block-uniform): empty regions
     if (lane < kNumStats) out.wave_stats[region * kNumStats + lane] = 0;
@@ -1502,64 +1579,17 @@ __global__ __launch_bounds__(kWG) void k_explain_expand(TableArgs t, QueryArgs q
   stage_rows(s, t);
   const uint64_t region0 = (uint64_t)region * out.region_bytes;
   uint64_t used = 0;  // wave-uniform bump pointer
-  uint64_t st_q = 0, st_nodes = 0, st_payload = 0;
+  ShallowStats st{0, 0, 0};
   for (int64_t src = wave; src < out.n_scan_waves; src += n_waves) {
     const uint32_t nw = out.work_count[src];
     const uint4* wl = out.work + (uint64_t)src * out.work_region;
-    for (uint32_t k0 = 0; k0 < nw; k0 += 64) {
-      const bool live = k0 + lane < nw;
-      int64_t i = 0, a = 0, b = -1;
-      int8_t status = SST_NONE;
-      bool deferred = false;
-      RegSink sink;
-      EnumOut eo{0, 0, 0, 0};
-      if (live) {
-        const uint4 item = wl[k0 + lane];  // {query, first window value >= 1, last, kItem* flags}
-        i = item.x;
-        a = item.y;
-        b = item.z;
-        bool run = true;
-        if (item.w & kItemUnclassified) {  // from the pair-list scan: route it here
-          if (!window_has_roots(t.valid, a, b)) {
-            run = false;
-          } else if (!(item.w & kItemNever) || b >= t.shallow_hi) {
-            const int cls = (item.w & kItemNever) ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
-            const uint32_t slot = atomicAdd(&out.counters[cls], 1u);
-            out.lists[(int64_t)cls * q.n + slot] = (uint32_t)i;
-            run = false;
-            deferred = true;
-          }
-        }
-        if (run) {
-          shallow_window(t, s, a, b, sink, eo);
-          st_q++;
-          st_nodes += eo.nodes;
-        }
-        status = eo.count ? (eo.count > q.cap_count ? SST_OVERFLOW : SST_SOME)
-                          : ((item.w & kItemZero) ? SST_EMPTY : SST_NONE);
-        if (deferred) status = (int8_t)kStatusPending;
-      }
-      const TileOut to = tile_alloc(out, lane, region0, used, status == SST_SOME ? eo.bytes : 0, status);
-      if (to.bytes) {
-        if (!sink.over) {
-          sink.flush(out.payload + to.off, to.bytes);
-        } else {  // more than 16 bytes: enumerate again straight into the arena
-          MemSink3 ms{out.payload + to.off};
-          EnumOut e2{0, 0, 0, 0};
-          shallow_window(t, s, a, b, ms, e2);
-        }
-      }
-      if (live) {  // deferred queries: the deep / exact kernels write all three
-        out.status[i] = to.status;
-        if (!deferred) {
-          out.count[i] = eo.count;
-          out.offset[i] = to.bytes ? to.off : 0;
-        }
-      }
-      st_payload += to.bytes;
-    }
+    for (uint32_t k0 = 0; k0 < nw; k0 += 64) shallow_chunk(t, q, out, s, wl, k0, nw, lane, region0, used, st);
   }
-  wave_stats_flush(out, region, lane, used, kStatShallow, kStatPayload, st_q, st_nodes, st_payload);
+  wave_stats_flush(out, region, lane, used, kStatShallow, kStatPayload, st.q, st.nodes, st.payload);
+}
+__global__ __launch_bounds__(kWG) void k_explain_expand(TableArgs t, QueryArgs q, OutArgs out) {
+  __shared__ Lds s;
+  expand_body(t, q, out, s, (int64_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6), (int64_t)gridDim.x * (kWG / 64));
 }
 
 // Compaction of the arena into a dense payload (result fetch / gather only):
@@ -1771,20 +1801,28 @@ __device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs
   wg_stat(out.stats, kStatNodes, st_nodes);
 }
 
-// The three deferred roles in one launch (64-lane blocks, partitioned by
-// block index): deep fast path, deep no-memo, exact replay.  Each role exits
-// at once when its list is empty, so an idle pass costs one launch.
+// The pair scan's tail in one launch (64-lane blocks, partitioned by block
+// index): SHALLOW windows (the scan waves' worklists), deep fast path, deep
+// no-memo, exact replay.  The scan routed every window, so the roles are
+// independent; each exits at once when its list is empty, so an idle pass
+// costs one launch.  shallow_blocks = 0 after k_bitset_scan (its windows go to
+// k_explain_expand, which routes them).
 __global__ __launch_bounds__(64) void k_explain_deferred(TableArgs t, QueryArgs q, OutArgs out, GlobFrame* ws_deep,
-                                                         ExactWs ws, int deep_blocks) {
+                                                         ExactWs ws, int shallow_blocks, int deep_blocks) {
   __shared__ Lds s;
-  const int b = blockIdx.x;
+  int b = blockIdx.x;
+  if (b < shallow_blocks) {
+    expand_body(t, q, out, s, b, shallow_blocks);
+    return;
+  }
+  b -= shallow_blocks;
   if (b < deep_blocks)
     deep_body<MODE_FAST>(t, q, out, kClassDeep, ws_deep, s, b, deep_blocks);
   else if (b < 2 * deep_blocks)  // second half of the deep workspace
     deep_body<MODE_NOMEMO>(t, q, out, kClassNomemo, ws_deep + (size_t)deep_blocks * 64 * kMaxDepth, s,
                            b - deep_blocks, deep_blocks);
   else
-    exact_body(t, q, out, ws, s, b - 2 * deep_blocks, (int)gridDim.x - 2 * deep_blocks);
+    exact_body(t, q, out, ws, s, b - 2 * deep_blocks, (int)gridDim.x - shallow_blocks - 2 * deep_blocks);
 }
 
 // ---------------------------------------------------------------------------
@@ -2704,10 +2742,11 @@ hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* pr
   return hipGetLastError();
 }
 hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const OutArgs& o, void* ws_deep,
-                                   int deep_blocks, const ExactWs& ws, int exact_blocks, hipStream_t st) {
+                                   int shallow_blocks, int deep_blocks, const ExactWs& ws, int exact_blocks,
+                                   hipStream_t st) {
   if (q.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_explain_deferred, dim3(2 * deep_blocks + exact_blocks), dim3(64), 0, st, t, q, o,
-                     (GlobFrame*)ws_deep, ws, deep_blocks);
+  hipLaunchKernelGGL(k_explain_deferred, dim3(shallow_blocks + 2 * deep_blocks + exact_blocks), dim3(64), 0, st, t, q,
+                     o, (GlobFrame*)ws_deep, ws, shallow_blocks, deep_blocks);
   return hipGetLastError();
 }
 
