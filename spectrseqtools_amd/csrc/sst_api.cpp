@@ -113,6 +113,18 @@ struct sst_result {
   // the expand waves' arena regions hold data of an earlier pass (k_explain_expand ran); fresh results
   // start with them zeroed (alloc_result)
   bool expand_regions_dirty = false;
+  // the last pass came from sst_explain_batch_device and has not been checked
+  // for arena / memo retries yet (settle, at the first view or fetch)
+  bool unsettled = false;
+  struct {
+    sst_table* t;
+    const double *mass, *thr;
+    const int64_t* mods;
+    int64_t mods_scalar;
+    double tol, prec;
+    int with_memo;
+    uint64_t cap;
+  } pass{};
   uint64_t arena_bytes = 0;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
@@ -690,6 +702,7 @@ OutArgs out_args(sst_result* r) {
   o.region_bytes = r->region_bytes;
   o.spill_base = (uint64_t)r->n_regions * r->region_bytes;
   o.cursor = ctl;
+  o.exact_retries = (unsigned long long*)(ctl + 3);
   o.ctl_next = ctl_block(r, r->parity ^ 1);
   o.ctl_words = kCtlWords;
   o.wave_used = (uint64_t*)r->wave_used.p;
@@ -717,6 +730,25 @@ int ensure_exact_ws(sst_ctx* c, uint32_t hash_cap, int lanes) {
   HIP_OK(c, hipMemsetAsync(c->ws_epochs.p, 0, (size_t)lanes * 8, c->stream));
   c->hash_cap = hash_cap;
   c->exact_blocks = lanes / 64;
+  return SST_OK;
+}
+
+// Workspaces for a retry pass: the spill area sized to what the spill cursor
+// counted (it keeps counting past the arena), the exact path's memo 8x larger
+// per lane over 8x fewer lanes.
+int grow_for_retry(sst_result* r, bool arena, bool exact, uint64_t cursor) {
+  sst_ctx* c = r->ctx;
+  if (arena) {
+    r->spill_bytes = std::max<uint64_t>(2 * r->spill_bytes, cursor + (1u << 20));
+    r->payload.release();
+    r->dense.release();
+  }
+  if (exact) {
+    const uint32_t hc = c->hash_cap * 8;
+    const int lanes = std::max(64, (c->exact_blocks * 64) / 8);
+    if (hc > (1u << 26)) return fail(c, SST_E_INTERNAL, "explain: exact-path memo exceeds 2^26 masses");
+    if (int rc = ensure_exact_ws(c, hc, lanes)) return rc;
+  }
   return SST_OK;
 }
 
@@ -829,9 +861,34 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out) {
 
 // Dense payload: per-wave regions and the spill area copied back to back,
 // offsets rewritten in place (once per explain pass).
+// A device-path pass may leave queries that did not fit the arena or the
+// exact path's memo (internal statuses).  The host path retries them at once;
+// here the first view / fetch checks two counters of the control block (8+8
+// bytes) and re-runs the pass with larger workspaces from the caller's device
+// inputs, which must still hold the batch (include/sst.h).
+int settle(sst_result* r) {
+  if (!r->unsettled) return SST_OK;
+  sst_ctx* c = r->ctx;
+  for (int attempt = 0;; ++attempt) {
+    uint64_t h[4] = {0, 0, 0, 0};
+    HIP_OK(c, hipMemcpyAsync(h, ctl_block(r, r->parity), sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    const bool arena = h[0] > r->spill_bytes, exact = h[3] > 0;
+    if (!arena && !exact) break;
+    if (attempt == 6) return fail(c, SST_E_INTERNAL, "explain: retries exhausted");
+    if (int rc = grow_for_retry(r, arena, exact, h[0])) return rc;
+    const auto& p = r->pass;
+    if (int rc = explain_pass(p.t, r, p.mass, p.thr, p.mods, p.mods_scalar, p.tol, p.prec, p.with_memo, p.cap))
+      return rc;
+  }
+  r->unsettled = false;
+  return SST_OK;
+}
+
 int compact(sst_result* r) {
   sst_ctx* c = r->ctx;
   if (r->compacted) return SST_OK;
+  if (int rc = settle(r)) return rc;
   if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, 1)))
     return fail(c, SST_E_NOMEM, "device allocation failed (compaction)");
   HIP_OK(c, launch_compact(out_args(r), r->n, r->n_regions, (uint64_t*)r->prefix.p, (uint8_t*)r->dense.p, r->hits,
@@ -887,6 +944,8 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
     return rc;
   }
   int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count);
+  r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count};
+  r->unsettled = rc == SST_OK;
   if (rc) {
     if (!reuse) {
       free_result_bufs(r);
@@ -935,22 +994,9 @@ int sst_explain_batch(sst_table* t, const double* mass, const double* thr, int64
       break;
     }
     if (!arena_retry && !exact_retry) break;
-    if (arena_retry) {  // the spill cursor kept counting past the arena: size the spill area to it
-      uint64_t cur = 0;
-      HIP_OK(c, hipMemcpy(&cur, ctl_block(r, r->parity), 8, hipMemcpyDeviceToHost));
-      r->spill_bytes = std::max<uint64_t>(2 * r->spill_bytes, cur + (1u << 20));
-      r->payload.release();
-      r->dense.release();
-    }
-    if (exact_retry) {
-      uint32_t hc = c->hash_cap * 8;
-      int lanes = std::max(64, (c->exact_blocks * 64) / 8);
-      if (hc > (1u << 26)) {
-        rc = fail(c, SST_E_INTERNAL, "explain: exact-path memo exceeds 2^26 masses");
-        break;
-      }
-      if ((rc = ensure_exact_ws(c, hc, lanes))) break;
-    }
+    uint64_t cur = 0;
+    HIP_OK(c, hipMemcpy(&cur, ctl_block(r, r->parity), 8, hipMemcpyDeviceToHost));
+    if ((rc = grow_for_retry(r, arena_retry, exact_retry, cur))) break;
     if (attempt == 5) rc = fail(c, SST_E_INTERNAL, "explain: retries exhausted");
   }
   if (rc) {

@@ -112,7 +112,8 @@ struct OutArgs {
   uint64_t arena_bytes;
   uint64_t region_bytes;      // per-wave region of the main kernel
   uint64_t spill_base;        // = n_waves * region_bytes
-  uint64_t* cursor;           // spill bytes taken
+  uint64_t* cursor;           // spill bytes taken (keeps counting past the arena: > spill area = arena retries)
+  unsigned long long* exact_retries;  // queries the exact path left for a retry with a larger memo
   uint64_t* ctl_next;         // the next pass's control block: zeroed by the scan kernel
   int ctl_words;
   uint64_t* wave_used;        // [n_waves] bytes used in each region (expand kernel waves)

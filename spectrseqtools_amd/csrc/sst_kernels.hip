@@ -1764,6 +1764,7 @@ __device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs
     uint64_t bytes = 0;
     if (rc == -1) {
       status = (int8_t)kStatusExactRetry;
+      atomicAdd(out.exact_retries, 1ull);  // lets the host see it without a status scan (settle)
     } else if (rc < 0) {
       status = SST_ABORTED;
     } else {

@@ -1,0 +1,137 @@
+"""GPU tests of the result path (through the C ABI): candidate caps (SST_OVERFLOW
+with the exact count), the device entry points with result reuse (the pair
+scan's hit lists are rebuilt every pass and scattered into count/offset at the
+first view), and queueing on a caller's stream (sst_ctx_set_stream).
+Checked against the CPU oracle and against the host-buffer entry points."""
+import numpy as np
+import pytest
+
+import _oracle as oracle
+from conftest import load_golden
+from spectrseqtools_amd import _native
+
+pytestmark = pytest.mark.gpu
+
+TOL, PREC = 1e-5, 1e-3
+CANONICAL = (305042, 306026, 329053, 345048)
+
+
+@pytest.fixture(scope="module")
+def engine():
+    return _native.get_engine(0)
+
+
+@pytest.fixture(scope="module")
+def rows():
+    g = load_golden("alphabet.json")
+    return sorted({r["tolerated_integer_masses"] for r in g["rows"]} | {0})
+
+
+@pytest.fixture(scope="module")
+def dev(engine, rows):
+    t = _native.DeviceTable.build(rows, max(rows) * 35, 32, engine=engine)
+    is_mod = [m not in CANONICAL and m != 0 for m in rows]
+    t.set_budgets(is_mod, [round(20 * (0.5 if md else (1.0 if m else 0.0))) for m, md in zip(rows, is_mod)])
+    return t
+
+
+@pytest.fixture(scope="module")
+def host(rows):
+    return oracle.build_table(rows, max(rows) * 35, 32)
+
+
+def _queries(rng, rows, n, kmax, thr_hi=14000, noise=0.004):
+    ints = np.array(rows[1:])
+    k = rng.integers(1, kmax + 1, n)
+    masses = np.array([ints[rng.integers(0, len(ints), kk)].sum() for kk in k]) * 1e-3
+    return masses + rng.normal(0, noise, n), 1e-5 * rng.uniform(300, thr_hi, n)
+
+
+def _same(a, b, n):
+    """Two ExplainResults hold the same answers (status, counts, candidates)."""
+    assert np.array_equal(a.status[:n], b.status[:n])
+    for i in range(n):
+        if int(a.status[i]) in (_native.SST_SOME, _native.SST_OVERFLOW):
+            assert int(a.count[i]) == int(b.count[i]), i
+        if int(a.status[i]) == _native.SST_SOME:
+            assert a.candidates(i) == b.candidates(i), i
+
+
+def test_explain_cap_overflow(dev, host, rows):
+    """cap_per_query: sets larger than the cap report OVERFLOW with the exact
+    count and no payload, on the pair path (<= 2 items) and beyond it."""
+    rng = np.random.default_rng(11)
+    m2, t2 = _queries(rng, rows, 400, 2)
+    m3, t3 = _queries(rng, rows, 80, 3)
+    masses, thr = np.concatenate([m2, m3]), np.concatenate([t2, t3])
+    is_mod = [m not in CANONICAL and m != 0 for m in rows]
+    alph = oracle.Alphabet(rows, is_mod, [round(20 * (0.5 if md else (1.0 if m else 0.0)))
+                                          for m, md in zip(rows, is_mod)])
+    want = [oracle.explain_table(host, 32, alph, masses[i], thr[i], TOL, 10) for i in range(len(masses))]
+    for cap in (1, 2, 3):
+        res = dev.explain(masses, thr, TOL, PREC, 10, cap=cap)
+        n_over = n_some = 0
+        for i, (st, sols, n_empty, _) in enumerate(want):
+            if st < 0:
+                assert int(res.status[i]) == _native.SST_OUT_OF_TABLE, i
+            elif len(sols) > cap:
+                assert int(res.status[i]) == _native.SST_OVERFLOW, (cap, i, int(res.status[i]), len(sols))
+                assert int(res.count[i]) == len(sols), (cap, i)
+                n_over += 1
+            else:
+                ws = _native.SST_SOME if sols else (_native.SST_EMPTY if n_empty else _native.SST_NONE)
+                assert int(res.status[i]) == ws, (cap, i)
+                if sols:
+                    assert res.candidates(i) == sols, (cap, i)
+                    n_some += 1
+        assert n_over > 0 and n_some > 0, (cap, n_over, n_some)
+
+
+def test_device_entry_points_with_reuse(engine, dev, rows):
+    """explain_device / is_valid_device on HBM inputs, one result object reused
+    over passes with many, few and many hits again: every pass matches the
+    host-buffer entry points (stale hit lists or offsets would not)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(12)
+    n = 3000
+    many = _queries(rng, rows, n, 2)
+    few = (rng.uniform(0.2, 0.9, n), 1e-5 * rng.uniform(300, 2000, n))  # masses below the first reachable one
+    mixed = _queries(rng, rows, n, 3)
+    dev_t = torch.device("cuda", engine.device)
+    res = None
+    out = torch.empty(n, dtype=torch.int8, device=dev_t)
+    for masses, thr in (many, few, many, mixed):
+        dm = torch.from_numpy(np.ascontiguousarray(masses)).to(dev_t)
+        dt = torch.from_numpy(np.ascontiguousarray(thr)).to(dev_t)
+        torch.cuda.synchronize()  # the engine queues on its own stream
+        res = dev.explain_device(dm.data_ptr(), dt.data_ptr(), n, TOL, PREC, 10, reuse=res)
+        dev.is_valid_device(dm.data_ptr(), dt.data_ptr(), n, TOL, PREC, out.data_ptr())
+        res.fetch_device()
+        _same(res, dev.explain(masses, thr, TOL, PREC, 10), n)
+        engine.synchronize()
+        assert np.array_equal(out.cpu().numpy(), dev.is_valid(masses, thr, TOL, PREC))
+
+
+def test_side_stream(engine, dev, rows):
+    """sst_ctx_set_stream: A7 on a caller's stream beside A8 on the engine
+    stream; results equal the one-stream results."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(13)
+    n = 5000
+    masses, thr = _queries(rng, rows, n, 2)
+    dev_t = torch.device("cuda", engine.device)
+    dm = torch.from_numpy(masses).to(dev_t)
+    dt = torch.from_numpy(thr).to(dev_t)
+    out = torch.full((n,), 7, dtype=torch.int8, device=dev_t)
+    side = torch.cuda.Stream(device=dev_t)
+    torch.cuda.synchronize()
+    res = dev.explain_device(dm.data_ptr(), dt.data_ptr(), n, TOL, PREC, 10)
+    try:
+        engine.set_stream(side.cuda_stream)
+        dev.is_valid_device(dm.data_ptr(), dt.data_ptr(), n, TOL, PREC, out.data_ptr())
+    finally:
+        engine.set_stream(None)
+    torch.cuda.synchronize()
+    res.fetch_device()
+    assert np.array_equal(out.cpu().numpy(), dev.is_valid(masses, thr, TOL, PREC))
+    _same(res, dev.explain(masses, thr, TOL, PREC, 10), n)
