@@ -15,7 +15,7 @@ constexpr int kMaxDepth = 96;      // >= max items of any multiset in a table (7
 constexpr int kInfBudget = 1 << 30;  // np.inf budget (decremented at most kMaxDepth times)
 constexpr int kScanWG = 1024;        // scan kernel workgroup (2 per CU share the LDS pair list)
 constexpr int kMaxSingletonMasses = 1024;  // is_singleton: integer masses staged in LDS
-constexpr int kMaxPairLds = 78 * 1024;  // pair-list image: two scan workgroups per CU (160 KB LDS)
+constexpr int kMaxPairLds = 44 * 1024;  // pair-list image per scan workgroup (staged at launch; 78 KB: 2 us slower)
 // worklist item flags ({query, a, b, flags}): v == 0 lies in the window; the
 // window was not classified by the scan (the expand kernel checks the bitset
 // and routes it); budgets cannot bind (fast-path theorem)
