@@ -283,6 +283,7 @@ int build_pair_list(sst_table* t, bool self_built) {
     bk[b] = (uint32_t)k | (uint32_t)delta << 16;
   }
   t->args.pair_shift = shift;
+  img.resize((img.size() + 3) / 4 * 4, 0u);  // the scan stages it in 16-B pieces
   if (!t->pairs.ensure(img.size() * 4)) return fail(c, SST_E_NOMEM, "device allocation failed (pair list)");
   HIP_OK(c, hipMemcpy(t->pairs.p, img.data(), img.size() * 4, hipMemcpyHostToDevice));
   t->args.pair_data = (const uint32_t*)t->pairs.p;

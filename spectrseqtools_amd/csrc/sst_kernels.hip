@@ -1355,7 +1355,9 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   extern __shared__ uint32_t lds_pair_img[];
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
   const int n_img = 2 * (t.n_pairs + 2) + t.n_buckets;
-  for (int k = threadIdx.x; k < n_img; k += blockDim.x) lds_pair_img[k] = t.pair_data[k];
+  // 16-B copies (the image is padded to 16 B; 4-B copies: scan +2.5 us)
+  for (int k = threadIdx.x; k < ((n_img + 3) >> 2); k += blockDim.x)
+    ((uint4*)lds_pair_img)[k] = ((const uint4*)t.pair_data)[k];
   __syncthreads();
   const PairLds pl{lds_pair_img, lds_pair_img + t.n_pairs + 2, lds_pair_img + 2 * (t.n_pairs + 2), t.pair_base,
                    t.pair_shift};
