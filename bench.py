@@ -316,11 +316,12 @@ def main():
     dbytes, dus = bytes_k[dom], kern.get(dom, {"avg_us": float("nan")})["avg_us"]
     achieved = dbytes / (dus * 1e-6) / 1e9
     traffic = None
-    try:
-        with open(args.traffic_json) as f:
-            traffic = json.load(f).get(dom)
-    except (OSError, ValueError):
-        pass
+    if args.spectra == 10000 and args.seed == 1000:  # the workload the PMC passes in profiles/ measured
+        try:
+            with open(args.traffic_json) as f:
+                traffic = json.load(f).get(dom)
+        except (OSError, ValueError):
+            pass
     ms_step = 1e3 * elapsed / args.steps
     value = peaks_all / (elapsed / args.steps)
 
