@@ -13,7 +13,8 @@ spectra (10k spectra, ~1M peaks, full 104-mass /
         rank's results are complete for its own spectra and stay in its HBM
         (no data-path collective in the step).  --gather adds delivery of
         every query's result (status, count, offset, dense payload) to rank 0
-        over RCCL, timed inside the step.
+        over RCCL, timed inside the step (status bytes + dense hit list +
+        dense payload, sst_result_hit_list).
 value = peaks of all ranks / step time (max over ranks).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--spectra S]
@@ -214,12 +215,16 @@ def main():
         if args.a7_stream == 2:
             res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=res)
         if gath is not None:
-            st, cnt, off, pay, _cap = res.device_views()  # queues the compaction: offsets index the dense payload
-            torch.cuda.current_stream().wait_stream(ext)  # after the compaction, before torch reads the buffers
+            # wire format: A7 bytes, A8 status bytes, the dense hit list
+            # ({query, count, offset} per query with candidates) and the dense
+            # payload -- ~1 B/query + 16 B/hit instead of 17 B/query
+            hits, n_hits = res.hit_list_device()  # compaction + hit list (synchronises the engine stream)
+            st, _cnt, _off, pay, _cap = res.device_views()  # compacted already: pointers only
+            torch.cuda.current_stream().wait_stream(ext)
             if side is not None:
                 torch.cuda.current_stream().wait_stream(side)  # A7 results
-            flat = torch.cat([out7.view(torch.uint8), device_bytes(st, n8, dev_t), device_bytes(cnt, 8 * n8, dev_t),
-                              device_bytes(off, 8 * n8, dev_t), device_bytes(pay, payload_bytes, dev_t)])
+            flat = torch.cat([out7.view(torch.uint8), device_bytes(st, n8, dev_t), device_bytes(hits, 16 * n_hits, dev_t),
+                              device_bytes(pay, payload_bytes, dev_t)])
             gath.gather(flat)
 
     # untimed sizing pass: results are deterministic per rank, so the gather
@@ -230,7 +235,7 @@ def main():
     res.fetch_device()
     payload_bytes = int(len(res.payload))
     if gath is not None:
-        gath.agree(n7 + 17 * n8 + payload_bytes)
+        gath.agree(n7 + n8 + 16 * res.hit_list_device()[1] + payload_bytes)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

@@ -172,6 +172,15 @@ int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count
  * packed into one dense payload that offset[] then indexes. */
 int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint64_t** d_offset,
                       uint8_t** d_payload, uint64_t* payload_bytes);
+/* Dense hit list of a result, on the device: one 16-B record
+ * {u32 query, u32 count (saturated), u64 offset into the dense payload as
+ * u32 lo, hi} per query with candidates (SOME, OVERFLOW, ABORTED), in no
+ * particular order -- with the status bytes and the payload, the whole
+ * result in ~1 B/query + 16 B per hit (the wire format bench.py --gather
+ * sends over RCCL instead of 17 B/query).  Compacts the result first and
+ * synchronises the ctx stream to report *n_hits.  Valid until the next pass
+ * on this result or its free.  No reference equivalent. */
+int sst_result_hit_list(sst_result* r, void** d_hits, uint64_t* n_hits);
 /* Copy device results to the host views (synchronises the ctx stream). */
 int sst_result_fetch(sst_result* r);
 void sst_result_free(sst_result* r);

@@ -26,7 +26,7 @@ EXPORTS = (
     "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
-    "sst_is_singleton_batch_device", "sst_ctx_set_stream",
+    "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list",
 )
 
 # kernel ids of sst_profile_read
@@ -97,6 +97,8 @@ def load_library(path=LIB_PATH):
     lib.sst_explain_batch_device.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
     lib.sst_result_host.argtypes = [_P, _PP, _PP, _PP, _PP, ctypes.POINTER(_U64)]
     lib.sst_result_device.argtypes = [_P, _PP, _PP, _PP, _PP, ctypes.POINTER(_U64)]
+    lib.sst_result_hit_list.argtypes = [_P, _PP, ctypes.POINTER(_U64)]
+    lib.sst_result_hit_list.restype = _I
     lib.sst_result_fetch.argtypes = [_P]
     lib.sst_result_free.argtypes = [_P]
     lib.sst_result_free.restype = None
@@ -275,6 +277,16 @@ class ExplainResult:
         self.engine.check(L.sst_result_device(self.handle, ctypes.byref(st), ctypes.byref(cnt), ctypes.byref(off),
                                               ctypes.byref(pay), ctypes.byref(nb)), "sst_result_device")
         return st.value, cnt.value, off.value, pay.value, int(nb.value)
+
+    def hit_list_device(self):
+        """(device pointer, n_hits) of the dense hit list: u32x4 records
+        {query, count, offset lo, offset hi}, in no particular order
+        (sst_result_hit_list)."""
+        p = ctypes.c_void_p()
+        nh = _U64()
+        self.engine.check(self.engine._lib.sst_result_hit_list(self.handle, ctypes.byref(p), ctypes.byref(nh)),
+                          "sst_result_hit_list")
+        return p.value, int(nh.value)
 
     def fetch_device(self):
         self.engine.check(self.engine._lib.sst_result_fetch(self.handle), "sst_result_fetch")

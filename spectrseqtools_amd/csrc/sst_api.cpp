@@ -103,6 +103,7 @@ struct sst_result {
   int parity = 1;
   bool ctl_ready = false;
   DevBuf wave_used, wave_stats, prefix, dense, work, work_count;
+  DevBuf hit_list, hit_ctr;  // sst_result_hit_list
   int n_waves = 0;  // expand waves
   int n_regions = 0;  // scan + expand waves (arena regions)
   int64_t n_scan_waves = 0;
@@ -683,7 +684,8 @@ constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses pe
 
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->count, &r->offset, &r->payload, &r->ctl, &r->lists,
-                    &r->wave_used, &r->wave_stats, &r->prefix, &r->dense, &r->work, &r->work_count})
+                    &r->wave_used, &r->wave_stats, &r->prefix, &r->dense, &r->work, &r->work_count,
+                    &r->hit_list, &r->hit_ctr})
     b->release();
 }
 
@@ -1112,6 +1114,26 @@ int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint
   if (d_offset) *d_offset = (uint64_t*)r->offset.p;
   if (d_payload) *d_payload = (uint8_t*)r->dense.p;
   if (payload_bytes) *payload_bytes = r->arena_bytes;
+  return SST_OK;
+}
+
+int sst_result_hit_list(sst_result* r, void** d_hits, uint64_t* n_hits) {
+  if (!r || !d_hits || !n_hits) return SST_E_ARG;
+  sst_ctx* c = r->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = compact(r)) return rc;  // final count / offset arrays
+  if (!r->hit_list.ensure((size_t)std::max<int64_t>(r->n, 1) * 16) || !r->hit_ctr.ensure(8))
+    return fail(c, SST_E_NOMEM, "device allocation failed (hit list)");
+  HIP_OK(c, hipMemsetAsync(r->hit_ctr.p, 0, 8, c->stream));
+  HIP_OK(c, launch_pack_hit_list((const int8_t*)r->status.p, (const uint64_t*)r->count.p,
+                                 (const uint64_t*)r->offset.p, r->n, r->hit_list.p,
+                                 (unsigned long long*)r->hit_ctr.p, c->stream));
+  uint64_t nh = 0;
+  HIP_OK(c, hipMemcpyAsync(&nh, r->hit_ctr.p, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  *d_hits = r->hit_list.p;
+  *n_hits = nh;
   return SST_OK;
 }
 

@@ -184,6 +184,8 @@ hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const O
 int explain_scan_blocks_per_cu(size_t dyn_lds);
 int explain_expand_blocks_per_cu();
 size_t scan_dyn_lds(const TableArgs& t);
+hipError_t launch_pack_hit_list(const int8_t* status, const uint64_t* count, const uint64_t* offset, int64_t n,
+                                void* out, unsigned long long* ctr, hipStream_t st);
 hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* wave_prefix, uint8_t* dst, bool hits,
                           hipStream_t st);
 hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const OutArgs& o, void* ws_deep,

@@ -1672,6 +1672,33 @@ __global__ __launch_bounds__(256) void k_scatter_hits(const uint4* __restrict__ 
   }
 }
 
+// Dense hit list of a compacted result (sst_result_hit_list): one
+// {query, count (saturated to u32), offset lo, offset hi} record per query
+// with candidates, appended per wavefront (ballot + one atomic), so records
+// come in no particular order.
+__global__ __launch_bounds__(256) void k_pack_hit_list(const int8_t* __restrict__ status,
+                                                       const uint64_t* __restrict__ count,
+                                                       const uint64_t* __restrict__ offset, int64_t n,
+                                                       uint4* __restrict__ out, unsigned long long* ctr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  bool hit = false;
+  if (i < n) {
+    const int8_t st = status[i];
+    hit = st == SST_SOME || st == SST_OVERFLOW || st == SST_ABORTED;
+  }
+  const uint64_t b = __ballot(hit);
+  if (!b) return;  // wave-uniform
+  unsigned long long base = 0;
+  if (lane == 0) base = atomicAdd(ctr, (unsigned long long)__builtin_popcountll(b));
+  base = __shfl(base, 0, 64);
+  if (hit) {
+    const uint64_t c = count[i], o = offset[i];
+    out[base + __builtin_popcountll(b & lane_mask_lt(lane))] =
+        make_uint4((uint32_t)i, c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c, (uint32_t)o, (uint32_t)(o >> 32));
+  }
+}
+
 __global__ __launch_bounds__(256) void k_compact_offsets(const int8_t* __restrict__ status,
                                                          const uint64_t* __restrict__ count, uint64_t* offset, int64_t n,
                                                          const uint64_t* __restrict__ pre, int n_waves, uint64_t region,
@@ -2756,6 +2783,14 @@ hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const
   if (q.n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_explain_deferred, dim3(shallow_blocks + 2 * deep_blocks + exact_blocks), dim3(64), 0, st, t, q,
                      o, (GlobFrame*)ws_deep, ws, shallow_blocks, deep_blocks);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_hit_list(const int8_t* status, const uint64_t* count, const uint64_t* offset, int64_t n,
+                                void* out, unsigned long long* ctr, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pack_hit_list, dim3(blocks_for(n, 256)), dim3(256), 0, st, status, count, offset, n,
+                     (uint4*)out, ctr);
   return hipGetLastError();
 }
 

@@ -135,3 +135,33 @@ def test_side_stream(engine, dev, rows):
     res.fetch_device()
     assert np.array_equal(out.cpu().numpy(), dev.is_valid(masses, thr, TOL, PREC))
     _same(res, dev.explain(masses, thr, TOL, PREC, 10), n)
+
+
+def test_hit_list_matches_result_arrays(engine, dev, rows):
+    """sst_result_hit_list: one {query, count, offset} record per query with
+    candidates, equal to the compacted count / offset arrays (the --gather
+    wire format)."""
+    torch = pytest.importorskip("torch")
+    from spectrseqtools_amd.parallel import device_bytes
+
+    rng = np.random.default_rng(14)
+    n = 4000
+    masses, thr = _queries(rng, rows, n, 3)
+    dev_t = torch.device("cuda", engine.device)
+    dm = torch.from_numpy(masses).to(dev_t)
+    dt = torch.from_numpy(thr).to(dev_t)
+    torch.cuda.synchronize()
+    res = dev.explain_device(dm.data_ptr(), dt.data_ptr(), n, TOL, PREC, 10, cap=50)
+    ptr, n_hits = res.hit_list_device()
+    recs = device_bytes(ptr, 16 * n_hits, dev_t).cpu().numpy().view(np.uint32).reshape(-1, 4)
+    res.fetch_device()
+    has = np.isin(res.status, (_native.SST_SOME, _native.SST_OVERFLOW, _native.SST_ABORTED))
+    assert n_hits == int(has.sum()) and n_hits > 0
+    q = recs[:, 0].astype(np.int64)
+    assert len(np.unique(q)) == n_hits and has[q].all()
+    assert np.array_equal(recs[:, 1].astype(np.uint64), res.count[q])
+    st = res.status[q]
+    some = st == _native.SST_SOME
+    off = recs[:, 2].astype(np.uint64) | (recs[:, 3].astype(np.uint64) << np.uint64(32))
+    assert np.array_equal(off[some], res.offset[q][some])
+    assert (st == _native.SST_OVERFLOW).any()  # cap=50 leaves some queries over the cap
