@@ -143,8 +143,9 @@ def main():
                          "multi-rank path, e.g. several ranks on one GPU with SST_DEVICE=0)")
     ap.add_argument("--gather", action="store_true",
                     help="N>1: gather every query's result to rank 0 over RCCL inside the timed step")
-    ap.add_argument("--event-every", type=int, default=4,
-                    help="bracket every n-th launch of the roofline kernel with HIP events (>= 1)")
+    ap.add_argument("--event-every", type=int, default=0,
+                    help="bracket every n-th launch of the roofline kernel with HIP events (0: about five "
+                         "brackets over the timed steps, at least every 4th launch)")
     ap.add_argument("--a7-stream", type=int, default=0,
                     help="1: queue the A7 batch on a second HIP stream, concurrent with the A8 chain "
                          "(sst_ctx_set_stream); 0: both on the engine stream, one after the other")
@@ -245,7 +246,8 @@ def main():
     # --event-every-th launch of it: each bracket costs two event records
     # (~6 us each on the stream), which would otherwise inflate every step;
     # the other kernels' times are in the rocprofv3 summaries under profiles/
-    engine.profile(not args.no_events, kernels=(_native.K_EXPLAIN_SCAN,), every=args.event_every)
+    every = args.event_every if args.event_every > 0 else max(4, args.steps // 5)
+    engine.profile(not args.no_events, kernels=(_native.K_EXPLAIN_SCAN,), every=every)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
