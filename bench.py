@@ -200,6 +200,8 @@ def main():
 
     side = torch.cuda.Stream(device=dev_t) if args.a7_stream else None
 
+    routed = False  # set by the sizing pass below
+
     def step():
         nonlocal res
         # A8 chain first (its persistent scan grid fills the chip), then A7 on
@@ -215,6 +217,11 @@ def main():
             engine.set_stream(None)
         if args.a7_stream == 2:
             res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=res)
+        if routed and gath is None:
+            # the scan routed windows to the deferred classes: run them (and the
+            # compaction) inside the step -- the device path starts them only at
+            # the first view of a result (sst_explain_batch_device)
+            res.device_views()
         if gath is not None:
             # wire format: A7 bytes, A8 status bytes, the dense hit list
             # ({query, count, offset} per query with candidates) and the dense
@@ -235,6 +242,8 @@ def main():
     engine.synchronize()
     res.fetch_device()
     payload_bytes = int(len(res.payload))
+    st0 = res.stats()
+    routed = int(st0[0] + st0[1] + st0[2] + st0[3]) > 0  # windows beyond the pair list (config 3: none)
     if gath is not None:
         gath.agree(n7 + n8 + 16 * res.hit_list_device()[1] + payload_bytes)
     for _ in range(args.warmup):

@@ -137,9 +137,11 @@ int sst_explain_batch(sst_table* t, const double* mass, const double* thr_abs, i
  * synchronisation.  If *out is non-NULL it must be a result of the same ctx
  * with capacity >= n: its buffers are reused (no allocation).  The inputs
  * (and the table) must stay valid and unchanged until the result's first
- * view or fetch: that call checks whether any query outgrew the payload
- * arena or the exact path's memo (16 bytes read back) and, if so, runs the
- * pass again with larger workspaces before it returns. */
+ * view or fetch: that call reads the pass's control block back (32 bytes),
+ * runs the deferred window classes if the scan routed any (deep, exact,
+ * no-memo and > 2-item windows; the pass itself launches only the scan on
+ * tables with the pair list), and re-runs the pass with larger workspaces
+ * if a query outgrew the payload arena or the exact path's memo. */
 int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d_thr_abs, int64_t n,
                              double tolerance, double precision, const int64_t* d_max_mods, int64_t max_mods_scalar,
                              int with_memo, uint64_t cap_per_query, sst_result** out);

@@ -117,6 +117,10 @@ struct sst_result {
   // the last pass came from sst_explain_batch_device and has not been checked
   // for arena / memo retries yet (settle, at the first view or fetch)
   bool unsettled = false;
+  // the device path's tail launch (k_explain_deferred) waits for the first
+  // view / fetch, which launches it only if the scan routed any window to it
+  bool tail_deferred = false;
+  bool tail_regions_used = false;  // a tail launch wrote the expand regions since they were last zeroed
   struct {
     sst_table* t;
     const double *mass, *thr;
@@ -769,9 +773,32 @@ void fold_scan_limits(const TableArgs& a, QueryArgs& q) {
 }
 
 // one pass of the explain pipeline on device buffers
-int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double* d_thr, const int64_t* d_mods,
-                 int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count) {
+// the deferred-class launch of a pass (after the pair scan it also runs the
+// SHALLOW windows, one wave per block, in the expand regions)
+int launch_tail(sst_table* t, sst_result* r) {
   sst_ctx* c = t->ctx;
+  const auto& ps = r->pass;
+  QueryArgs q{ps.mass, ps.thr, ps.mods, ps.mods_scalar, r->n, ps.tol, ps.prec, 1.0 / ps.prec, ps.with_memo, ps.cap,
+              kNodeBudget};
+  fold_scan_limits(t->args, q);
+  OutArgs o = out_args(r);
+  ExactWs ws{(char*)c->ws_hash.p, (char*)c->ws_frames.p, (char*)c->ws_stacks.p, (uint64_t*)c->ws_epochs.p,
+             c->hash_cap};
+  Prof p(c, SST_K_EXPLAIN_DEEP);  // deep, no-memo and exact roles: one launch
+  const int shallow_blocks = t->args.pairs_enabled ? std::min(r->n_waves, 4 * c->n_cu) : 0;
+  HIP_OK(c, launch_explain_deferred(t->args, q, o, c->ws_deep.p, shallow_blocks, kDeepBlocks, ws, c->exact_blocks,
+                                    c->stream));
+  if (shallow_blocks) r->tail_regions_used = true;
+  r->tail_deferred = false;
+  return SST_OK;
+}
+
+// lazy_tail (device path, pair scan): the tail launch waits for settle()
+int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double* d_thr, const int64_t* d_mods,
+                 int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count,
+                 bool lazy_tail = false) {
+  sst_ctx* c = t->ctx;
+  r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count};
   const int64_t n = r->n;
   r->arena_bytes = (uint64_t)r->n_regions * r->region_bytes + r->spill_bytes;
   static_assert(4 + kNumStats <= kCtlWords && 2 * 2 >= kNumClasses, "control block layout");
@@ -808,16 +835,11 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
                              (size_t)r->n_waves * kNumStats * 8, c->stream));
     r->expand_regions_dirty = false;
   }
-  ExactWs ws{(char*)c->ws_hash.p, (char*)c->ws_frames.p, (char*)c->ws_stacks.p, (uint64_t*)c->ws_epochs.p,
-             c->hash_cap};
-  {
-    Prof p(c, SST_K_EXPLAIN_DEEP);  // deep, no-memo and exact roles: one launch
-    // after the pair scan this launch also runs the SHALLOW windows (one wave per block, expand regions)
-    const int shallow_blocks = t->args.pairs_enabled ? std::min(r->n_waves, 4 * c->n_cu) : 0;
-    HIP_OK(c, launch_explain_deferred(t->args, q, o, c->ws_deep.p, shallow_blocks, kDeepBlocks, ws, c->exact_blocks,
-                                      c->stream));
+  if (lazy_tail && t->args.pairs_enabled && n > 0) {
+    r->tail_deferred = true;
+    return SST_OK;
   }
-  return SST_OK;
+  return launch_tail(t, r);
 }
 
 int alloc_result(sst_table* t, int64_t n, sst_result** out) {
@@ -876,6 +898,20 @@ int settle(sst_result* r) {
     uint64_t h[4] = {0, 0, 0, 0};
     HIP_OK(c, hipMemcpyAsync(h, ctl_block(r, r->parity), sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (r->tail_deferred) {  // the class counters (h[1], h[2]) say whether the scan routed any window
+      if (h[1] | h[2]) {
+        if (int rc = launch_tail(r->pass.t, r)) return rc;
+        --attempt;  // read the counters again after the tail
+        continue;
+      }
+      r->tail_deferred = false;
+      if (r->tail_regions_used) {  // an earlier pass's tail left data in the expand regions
+        HIP_OK(c, hipMemsetAsync((uint64_t*)r->wave_used.p + r->n_scan_waves, 0, (size_t)r->n_waves * 8, c->stream));
+        HIP_OK(c, hipMemsetAsync((unsigned long long*)r->wave_stats.p + r->n_scan_waves * kNumStats, 0,
+                                 (size_t)r->n_waves * kNumStats * 8, c->stream));
+        r->tail_regions_used = false;
+      }
+    }
     const bool arena = h[0] > r->spill_bytes, exact = h[3] > 0;
     if (!arena && !exact) break;
     if (attempt == 6) return fail(c, SST_E_INTERNAL, "explain: retries exhausted");
@@ -946,8 +982,7 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
   } else if (int rc = alloc_result(t, n, &r)) {
     return rc;
   }
-  int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count);
-  r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count};
+  int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count, true);
   r->unsettled = rc == SST_OK;
   if (rc) {
     if (!reuse) {
