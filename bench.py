@@ -369,7 +369,8 @@ def main():
             "max_modifications": A,
             "a7_stream": ("side stream, concurrent with the A8 chain" if args.a7_stream else "engine stream"),
             "parallelism": (f"spectra sharded over {world} GPUs, results kept per rank"
-                            + (", RCCL gather of all results to rank 0 in the step" if args.gather else "")
+                            + ((", RCCL" if args.backend == "nccl" else ", gloo") +
+                               " gather of all results to rank 0 in the step" if args.gather else "")
                             if world > 1 else "1 GPU"),
         },
         "roofline": {
