@@ -161,7 +161,8 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
 /* Host views of a result (valid until sst_result_free):
  *   status[n] (SST_NONE..), count[n] candidates, offset[n] byte offset of the
  *   query's candidates in payload; payload = per candidate one length byte k
- *   followed by k row indices (ascending, i.e. ascending mass).
+ *   followed by k row indices (ascending, i.e. ascending mass); a query's
+ *   candidates may be followed by unused bytes (count delimits them).
  *   count[i] and offset[i] are defined only when status[i] is SST_SOME,
  *   SST_OVERFLOW or SST_ABORTED (the others carry no candidates; the engine
  *   does not spend HBM writes on them). */

@@ -1269,14 +1269,17 @@ __device__ __forceinline__ uint32_t pair_walk(const PairLds& p, uint32_t a, uint
   bytes = nb;
   return cnt;
 }
+// One (unaligned) dword store per record: the 1-2 bytes past a record are
+// rewritten by the lane's next record, or land in the 2 pad bytes allocated
+// after the query's last one (never referenced: offsets and counts delimit
+// the candidates).  Two stores per record (short + byte): scan +1 us.
+typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 __device__ __forceinline__ void pair_store(const PairLds& p, uint32_t first, uint32_t cnt, uint8_t* dst) {
 #pragma unroll 1
   for (uint32_t k = first; k < first + cnt; ++k) {
-    const uint32_t rec = p.recs[k];
-    const uint32_t len = (rec & 0xFFu) + 1u;
-    *(uint16_t*)dst = (uint16_t)rec;
-    dst[len - 1u] = (uint8_t)(rec >> (8u * (len - 1u)));
-    dst += len;
+    const uint32_t rec = p.recs[k];  // [k][rows] in the low 2-3 bytes, zero above
+    *(u32_unaligned*)dst = rec;
+    dst += (rec & 0xFFu) + 1u;
   }
 }
 
@@ -1421,7 +1424,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     if (cnt) status = cnt > q.cap32 ? (int8_t)SST_OVERFLOW : (int8_t)SST_SOME;
     // payload: wavefront prefix sum, bump allocation in the wave's region
     // (spill when full), records copied from LDS
-    uint32_t pb = status == SST_SOME ? bytes : 0u;
+    uint32_t pb = status == SST_SOME ? bytes + 2u : 0u;  // + 2 pad bytes (pair_store)
     const uint32_t incl = wave_incl_scan32(pb);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     uint64_t off = 0;
