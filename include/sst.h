@@ -38,8 +38,9 @@ extern "C" {
 #define SST_NONE 0          /* reference returns MassExplanations(None)      */
 #define SST_EMPTY 1         /* reference returns MassExplanations(set())     */
 #define SST_SOME 2          /* >= 1 candidate composition                    */
-#define SST_OUT_OF_TABLE (-1) /* reference raises (NameError in explain,    */
-                              /* NotImplementedError in is_valid_mass)      */
+#define SST_OUT_OF_TABLE (-1) /* reference raises NotImplementedError naming */
+                              /* its window value (mass_explanation.py:68-72, */
+                              /* :134-138 with `value` bound at :192)        */
 #define SST_OVERFLOW (-2)   /* count > cap_per_query: exact count, no payload */
 #define SST_ABORTED (-4)    /* DFS node guard (2^34 nodes) exhausted: count is a lower bound */
 

@@ -44,9 +44,28 @@ def _check_finite(mass):
             raise OverflowError("cannot convert float infinity to integer")
 
 
-def _not_in_table(mass, dp_table):
+def _not_in_table(value):
+    """The reference's out-of-table message (mass_explanation.py:68-72,
+    :134-138; mass_table.py:383-387)."""
+    return f"The value {value} is not in the DP table. Extend its size if you want to compute larger masses."
+
+
+def _table_limit(dp_table):
+    return dp_table.device_table.n_cols * dp_table.compression_per_cell
+
+
+def first_value_beyond(mass, threshold, dp_table, tolerance_mass=None):
+    """The `value` the reference's raise formats: its window loop runs
+    ascending over [target - thr, target + thr] (mass_explanation.py:110-114,
+    :189-192), and a DFS only moves to smaller masses, so the first root that
+    meets a mass beyond the table is the first window value >= the table end
+    (n_cols * compression).  tolerance_mass: the mass the default threshold
+    scales (the length bound passes obs_mass, mass_table.py:357-359)."""
     target = int(round(mass / dp_table.precision, 0))
-    return f"The value {target} is not in the DP table. Extend its size if you want to compute larger masses."
+    if threshold is None:
+        threshold = dp_table.tolerance * (mass if tolerance_mass is None else tolerance_mass)
+    thr = int(np.ceil(threshold / dp_table.precision))
+    return max(target - thr, _table_limit(dp_table))
 
 
 def is_valid_mass(mass: float, dp_table: DynamicProgrammingTable, threshold: float = None) -> bool:
@@ -54,7 +73,7 @@ def is_valid_mass(mass: float, dp_table: DynamicProgrammingTable, threshold: flo
     _check_finite(mass)
     r = is_valid_masses([mass], dp_table, None if threshold is None else [threshold], errors="status")[0]
     if r < 0:
-        raise NotImplementedError(_not_in_table(mass, dp_table))
+        raise NotImplementedError(_not_in_table(first_value_beyond(mass, threshold, dp_table)))
     return bool(r)
 
 
@@ -71,7 +90,9 @@ def is_valid_masses(masses, dp_table: DynamicProgrammingTable, thresholds=None, 
         return out
     bad = np.nonzero(out < 0)[0]
     if len(bad):
-        raise NotImplementedError(_not_in_table(float(masses[bad[0]]), dp_table))
+        k = bad[0]
+        thr = None if thresholds is None else float(thresholds[k])
+        raise NotImplementedError(_not_in_table(first_value_beyond(float(masses[k]), thr, dp_table)))
     return out.astype(bool)
 
 
@@ -94,8 +115,9 @@ def explain_masses(masses, dp_table: DynamicProgrammingTable, max_modifications=
 
     max_modifications: scalar (np.inf default) or one budget per mass.
     Returns a list of MassExplanations.  A query that the reference would
-    raise on (window beyond the table) raises NameError like the reference
-    (errors="raise") or yields None in the list (errors="none").  Queries with
+    raise on (window beyond the table) raises the reference's
+    NotImplementedError, naming the same window value (errors="raise"), or
+    yields None in the list (errors="none").  Queries with
     more than cap_per_query candidates raise OverflowError."""
     res = explain_masses_raw(masses, dp_table, max_modifications, thresholds, with_memo, cap_per_query)
     row_mass = [m.mass for m in dp_table.masses]
@@ -104,7 +126,8 @@ def explain_masses(masses, dp_table: DynamicProgrammingTable, max_modifications=
         st = int(res.status[i])
         if st == _native.SST_OUT_OF_TABLE:
             if errors == "raise":
-                raise NameError("name 'value' is not defined")
+                thr = None if thresholds is None else float(np.asarray(thresholds, dtype=np.float64)[i])
+                raise NotImplementedError(_not_in_table(first_value_beyond(float(masses[i]), thr, dp_table)))
             out.append(None)
             continue
         if st in (_native.SST_OVERFLOW, _native.SST_ABORTED):

@@ -263,8 +263,14 @@ def compute_sequence_length_bounds(dp_table: DynamicProgrammingTable, su_masses,
     if len(bad):
         s = int(st[bad[0]])
         if s == _native.SST_OUT_OF_TABLE:
-            raise NotImplementedError("The value is not in the DP table. Extend its size if you want to compute "
-                                      "larger masses.")
+            # the reference formats its window-loop variable `value` (mass_table.py:383-387, :461): the first
+            # window value at or beyond the table end (the DFS only moves to smaller masses)
+            k = bad[0]
+            target = int(round(float(su_masses[k]) / dp_table.precision, 0))
+            thr = int(np.ceil(dp_table.tolerance * float(obs_masses[k]) / dp_table.precision))
+            value = max(target - thr, dp_table.device_table.n_cols * dp_table.compression_per_cell)
+            raise NotImplementedError(f"The value {value} is not in the DP table. Extend its size if you want to "
+                                      f"compute larger masses.")
         if s == _native.SST_LB_EMPTY_WINDOW:
             raise ValueError("min() arg is an empty sequence")
         raise RuntimeError(f"length bound aborted: DFS node budget exhausted (status {s})")

@@ -41,3 +41,8 @@ def golden_cases():
 @pytest.fixture(scope="session")
 def golden_population():
     return load_golden("population.json.gz")
+
+
+@pytest.fixture(scope="session")
+def golden_raise_cases():
+    return load_golden("raise_cases.json")

@@ -128,11 +128,15 @@ def test_mirror_errors_like_reference():
 
     seq = SequenceInformation(max_len=20, su_mass=1000.0, obs_mass=1000.0, modification_rate=0.5)
     dp = DynamicProgrammingTable(EXPLANATION_MASSES, 32, MATCHING_THRESHOLD, TOLERANCE, seq)
-    beyond = dp.device_table.n_cols * 32 * 1e-3 + 10
-    with pytest.raises(NameError):
+    limit = dp.device_table.n_cols * 32
+    beyond = limit * 1e-3 + 10
+    msg = f"The value {limit + 10000 - 10} is not in the DP table. Extend its size if you want to compute larger masses."
+    with pytest.raises(NotImplementedError) as e:
         explain_mass_with_table(beyond, dp, threshold=0.01)
-    with pytest.raises(NotImplementedError):
+    assert str(e.value) == msg
+    with pytest.raises(NotImplementedError) as e:
         is_valid_mass(beyond, dp, threshold=0.01)
+    assert str(e.value) == msg
     with pytest.raises(ValueError):
         is_valid_mass(float("nan"), dp)
     assert explain_mass_with_table(0.0001, dp, threshold=0.01).explanations == set()
@@ -155,3 +159,83 @@ def test_alphabet_reduction_rebuilds_on_gpu(golden_cases):
 
     assert hashlib.sha256(dp.table.tobytes()).hexdigest() == ctx["table_sha256"]
     assert [round(20 * m.modification_rate) for m in dp.masses] == ctx["caps"]
+
+
+def _mirror_table(keep, max_len):
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
+
+    frame = EXPLANATION_MASSES.filter_rows(lambda r: r["nucleoside"] in keep)
+    seq = SequenceInformation(max_len=max_len, su_mass=0.0, obs_mass=0.0, modification_rate=0.5)
+    return DynamicProgrammingTable(frame, 32, MATCHING_THRESHOLD, TOLERANCE, seq)
+
+
+def test_raise_cases_type_and_message(golden_raise_cases):
+    """Every out-of-table case of tests/golden/raise_cases.json (the reference
+    run by make_raise_golden.py): same exception type, same message (the
+    reference formats its window-loop `value`), same non-raising results."""
+    from spectrseqtools_amd.mass_explanation import explain_mass_with_table, is_valid_mass
+    from spectrseqtools_amd.mass_table import compute_sequence_length_bound
+
+    g = golden_raise_cases
+    dp = _mirror_table(set(g["keep"]), g["max_len"])
+    assert [m.mass for m in dp.masses] == g["masses"]
+    assert dp.device_table.n_cols * 32 == g["limit"]
+    n_raise = 0
+    for c in g["cases"]:
+        if c["fn"] == "explain":
+            call = lambda: explain_mass_with_table(c["mass"], dp, threshold=c["threshold"])  # noqa: E731
+        elif c["fn"] == "is_valid":
+            call = lambda: is_valid_mass(c["mass"], dp, threshold=c["threshold"])  # noqa: E731
+        else:
+            dp.seq.su_mass, dp.seq.obs_mass = c["su_mass"], c["obs_mass"]
+            call = lambda: compute_sequence_length_bound(dp, c["dir"])  # noqa: E731
+        if c["status"] == "raise":
+            with pytest.raises(Exception) as e:
+                call()
+            assert type(e.value).__name__ == c["error"], c
+            assert str(e.value) == c["message"], c
+            n_raise += 1
+        else:
+            got = call()
+            if c["fn"] == "explain":
+                got = None if got.explanations is None else sorted(list(t) for t in got.explanations)
+            assert got == c["result"], c
+    assert n_raise >= 15
+
+
+def test_golden_raise_cases_through_mirror(golden_cases):
+    """Every explain_cases.json.gz case with status "raise" through the
+    mirror's explain_mass_with_table / is_valid_mass: the reference's
+    exception type (NotImplementedError), never NameError."""
+    from spectrseqtools_amd.mass_explanation import explain_mass_with_table, is_valid_mass
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, TOLERANCE
+
+    ctxs = golden_cases["contexts"]
+    dps = {}
+    n = 0
+    for c in golden_cases["cases"]:
+        raising = c.get("status") == "raise" or c.get("result") == "raise"
+        if not raising or c["fn"] not in ("table", "is_valid"):
+            continue
+        ctx = ctxs[c["ctx"]]
+        if c["ctx"] not in dps:
+            seq = SequenceInformation(max_len=ctx["max_len"], su_mass=ctx["su_mass"], obs_mass=ctx["obs_mass"],
+                                      modification_rate=ctx["mod_rate"])
+            dps[c["ctx"]] = DynamicProgrammingTable(EXPLANATION_MASSES, 32, ctx["tolerance"], TOLERANCE, seq)
+        dp = dps[c["ctx"]]
+        assert [m.mass for m in dp.masses] == ctx["masses"]
+        limit = dp.device_table.n_cols * 32
+        with pytest.raises(Exception) as e:
+            if c["fn"] == "table":
+                explain_mass_with_table(c["mass"], dp, max_modifications=budget(c["max_modifications"]),
+                                        threshold=c["threshold"], with_memo=c["with_memo"])
+            else:
+                is_valid_mass(c["mass"], dp, threshold=c["threshold"])
+        assert type(e.value).__name__ == c["error"], c
+        target = int(round(c["mass"] / TOLERANCE, 0))
+        thr = int(np.ceil(c["threshold"] / TOLERANCE))
+        assert str(e.value).startswith(f"The value {max(target - thr, limit)} is not in the DP table."), c
+        n += 1
+    assert n >= 8
