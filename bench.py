@@ -48,6 +48,17 @@ def windows(masses, thr, prec, limit):
     return lo, hi, np.where(ok, (hi >> 6) - (lo >> 6) + 1, 0)
 
 
+def result_digest(r):
+    """SHA-256 over a fetched result: status bytes, per-query counts and
+    offsets (from the hit list) and the dense payload."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for a in (r.status, r.count, r.offset, r.payload):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
 def build_workload(n_spectra, seed, dp):
     from spectrseqtools_amd.masses import build_breakage_dict
     from spectrseqtools_amd.producers import (MAX_VARIANCE, classify_queries, diff_queries, max_nucleotide_weight,
@@ -94,10 +105,11 @@ def build_workload(n_spectra, seed, dp):
     }
 
 
-def cpu_baseline(wl_fn, dp, budget_s=12.0):
+def cpu_baseline(wl_fn, dp, budget_s=10.0, single_budget_s=8.0):
     """The CPU oracle (literal C restatement of is_valid_mass /
-    explain_mass_with_table, OpenMP over the host cores) on a bounded sample
-    of the same workload."""
+    explain_mass_with_table) on a bounded sample of the same workload, with
+    OpenMP over all the host threads the box grants, and single-threaded
+    (per-core parity against BASELINE.md's reference-Python rates)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle as oracle
 
@@ -106,28 +118,33 @@ def cpu_baseline(wl_fn, dp, budget_s=12.0):
     alph = oracle.Alphabet(ms, [m.is_modification for m in dp.masses],
                            [round(dp.seq.max_len * m.modification_rate) for m in dp.masses])
     A = round(dp.seq.modification_rate * dp.seq.max_len)
-    threads = oracle.LIB.ora_num_threads()
+    all_threads = oracle.LIB.ora_num_threads()
 
-    def run(wl):
-        t0 = time.perf_counter()
-        oracle.is_valid_batch(table, 32, wl["a7_mass"], wl["a7_thr"], dp.tolerance, nthreads=threads)
-        oracle.explain_batch(table, 32, alph, wl["a8_mass"], wl["a8_thr"], A, dp.tolerance, nthreads=threads)
-        return time.perf_counter() - t0
+    def leg(threads, budget, n_max):
+        def run(wl):
+            t0 = time.perf_counter()
+            oracle.is_valid_batch(table, 32, wl["a7_mass"], wl["a7_thr"], dp.tolerance, nthreads=threads)
+            oracle.explain_batch(table, 32, alph, wl["a8_mass"], wl["a8_thr"], A, dp.tolerance, nthreads=threads)
+            return time.perf_counter() - t0
 
-    # size the sample from a small probe, then repeat it until ~budget_s of CPU
-    # work has been timed (the same sample each time: identical results)
-    n = 200
-    t = run(wl_fn(n))
-    n = int(min(20000, max(n, n * budget_s / 4 / max(t, 1e-3))))
-    wl = wl_fn(n)
-    reps, total = 0, 0.0
-    while total < budget_s:
-        total += run(wl)
-        reps += 1
-    return {"value": reps * wl["peaks"] / total, "unit": "peaks/s", "cores": threads, "kind": "port",
-            "sample": f"{n} synthetic spectra ({wl['peaks']} peaks, {len(wl['a7_mass'])} A7 + {len(wl['a8_mass'])} "
-                      f"A8 queries) x {reps} repetitions, oracle/sst_oracle.c with {threads} OpenMP threads, "
-                      f"{total:.1f} s"}
+        # size the sample from a small probe, then repeat it until ~budget s of
+        # CPU work has been timed (the same sample each time: identical results)
+        n = 100
+        t = run(wl_fn(n))
+        n = int(min(n_max, max(n, n * budget / 4 / max(t, 1e-3))))
+        wl = wl_fn(n)
+        reps, total = 0, 0.0
+        while total < budget:
+            total += run(wl)
+            reps += 1
+        return {"value": reps * wl["peaks"] / total, "unit": "peaks/s", "cores": threads, "kind": "port",
+                "sample": f"{n} synthetic spectra ({wl['peaks']} peaks, {len(wl['a7_mass'])} A7 + "
+                          f"{len(wl['a8_mass'])} A8 queries) x {reps} repetitions, oracle/sst_oracle.c with "
+                          f"{threads} OpenMP thread{'s' if threads > 1 else ''}, {total:.1f} s"}
+
+    out = leg(all_threads, budget_s, 20000)
+    out["single_core"] = leg(1, single_budget_s, 2000)
+    return out
 
 
 def main():
@@ -191,63 +208,74 @@ def main():
     a7t = torch.from_numpy(wl["a7_thr"]).to(dev_t)
     a8m = torch.from_numpy(wl["a8_mass"]).to(dev_t)
     a8t = torch.from_numpy(wl["a8_thr"]).to(dev_t)
-    out7 = torch.empty(n7, dtype=torch.int8, device=dev_t)
+    # two result sets used in turn: while step k runs on the GPU, the host
+    # settles step k-1 (waits for its pass, reads its header, runs any routed
+    # deferred windows or retries) -- the pipelined consumer loop of a serving
+    # deployment; every step's result is complete and checked inside the
+    # timed region
+    outs7 = [torch.empty(n7, dtype=torch.int8, device=dev_t) for _ in range(2)]
     torch.cuda.synchronize()
     ext = torch.cuda.ExternalStream(engine.stream, device=dev_t)
 
-    res = None
+    results = [None, None]
     gath = Gatherer(dist, dev_t) if (dist and args.gather) else None
-
     side = torch.cuda.Stream(device=dev_t) if args.a7_stream else None
+    settled = {"n": 0}
 
-    routed = False  # set by the sizing pass below
+    def settle(r):
+        nh, nb = r.settle()
+        if nh != n_hits0 or nb != payload0:
+            raise RuntimeError(f"step result differs from the reference pass: {nh} hits / {nb} B "
+                               f"vs {n_hits0} / {payload0}")
+        settled["n"] += 1
 
-    def step():
-        nonlocal res
-        # A8 chain first (its persistent scan grid fills the chip), then A7 on
-        # the side stream: its blocks take the CUs the scan's waves leave and
-        # run through the A8 tail launches.  The two touch disjoint buffers;
-        # the timed region ends with a device-wide synchronize.
+    def step(k):
+        cur = k & 1
+        out7 = outs7[cur]
+        # A8 first (its persistent scan grid fills the chip), then A7; the two
+        # touch disjoint buffers
         if args.a7_stream != 2:
-            res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=res)
+            results[cur] = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A,
+                                               reuse=results[cur])
         if side is not None:
             engine.set_stream(side.cuda_stream)
         tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, out7.data_ptr())
         if side is not None:
             engine.set_stream(None)
         if args.a7_stream == 2:
-            res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=res)
-        if routed and gath is None:
-            # the scan routed windows to the deferred classes: run them (and the
-            # compaction) inside the step -- the device path starts them only at
-            # the first view of a result (sst_explain_batch_device)
-            res.device_views()
+            results[cur] = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A,
+                                               reuse=results[cur])
         if gath is not None:
             # wire format: A7 bytes, A8 status bytes, the dense hit list
-            # ({query, count, offset} per query with candidates) and the dense
+            # ({query, count, word} per query with candidates) and the dense
             # payload -- ~1 B/query + 16 B/hit instead of 17 B/query
-            hits, n_hits = res.hit_list_device()  # compaction + hit list (synchronises the engine stream)
-            st, _cnt, _off, pay, _cap = res.device_views()  # compacted already: pointers only
+            settle(results[cur])
+            hits, n_hits = results[cur].hit_list_device()
+            st, _c, _o, pay, nb = results[cur].device_views(arrays=False)
             torch.cuda.current_stream().wait_stream(ext)
             if side is not None:
                 torch.cuda.current_stream().wait_stream(side)  # A7 results
             flat = torch.cat([out7.view(torch.uint8), device_bytes(st, n8, dev_t), device_bytes(hits, 16 * n_hits, dev_t),
-                              device_bytes(pay, payload_bytes, dev_t)])
+                              device_bytes(pay, nb, dev_t)])
             gath.gather(flat)
+        elif k > 0:
+            settle(results[cur ^ 1])  # the previous step's result, while this one runs
 
-    # untimed sizing pass: results are deterministic per rank, so the gather
-    # sizes are agreed once
-    tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, out7.data_ptr())
-    res = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A)
-    engine.synchronize()
-    res.fetch_device()
-    payload_bytes = int(len(res.payload))
-    st0 = res.stats()
-    routed = int(st0[0] + st0[1] + st0[2] + st0[3]) > 0  # windows beyond the pair list (config 3: none)
+    def drain(k_last):
+        if gath is None and results[k_last & 1] is not None:
+            settle(results[k_last & 1])
+
+    # untimed reference pass: sizes for the gather and the expected result
+    tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, outs7[0].data_ptr())
+    ref = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A)
+    ref.fetch_device()
+    n_hits0, payload0 = ref.settle()
+    ref_digest = result_digest(ref)
     if gath is not None:
-        gath.agree(n7 + n8 + 16 * res.hit_list_device()[1] + payload_bytes)
-    for _ in range(args.warmup):
-        step()
+        gath.agree(n7 + n8 + 16 * n_hits0 + payload0)
+    for k in range(args.warmup):
+        step(k)
+    drain(args.warmup - 1)
     torch.cuda.synchronize()
     engine.synchronize()
 
@@ -256,13 +284,15 @@ def main():
     # (~6 us each on the stream), which would otherwise inflate every step;
     # the other kernels' times are in the rocprofv3 summaries under profiles/
     every = args.event_every if args.event_every > 0 else max(4, args.steps // 5)
-    engine.profile(not args.no_events, kernels=(_native.K_EXPLAIN_SCAN,), every=every)
+    engine.profile(not args.no_events, kernels=(_native.K_EXPLAIN_SCAN, _native.K_RESULT_PACK), every=every)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    settled["n"] = 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        step(k)
+    drain(args.steps - 1)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -280,14 +310,23 @@ def main():
     else:
         peaks_all, n7_all, n8_all = wl["peaks"], n7, n8
 
-    # results of the last step (validation + algorithmic bytes)
-    res.fetch_device()
+    # every timed step was settled in the loop; the last two steps' results
+    # must equal the reference pass bit for bit (status bytes, hit list,
+    # payload), and A7 the setup pass
+    if settled["n"] != args.steps and not args.no_validate:
+        raise RuntimeError(f"{settled['n']} of {args.steps} steps settled")
+    for r in results:
+        if r is not None:
+            r.fetch_device()
+            if result_digest(r) != ref_digest and not args.no_validate:
+                raise RuntimeError("a timed step's result differs from the reference pass")
+    res = results[(args.steps - 1) & 1]
     st = res.status
     if (st < -2).any() and not args.no_validate:
         raise RuntimeError(f"internal statuses in results: {np.unique(st[st < -2])}")
     stats = res.stats()
-    v7 = out7.cpu().numpy()
-    assert np.array_equal(v7, wl["a7_valid"]), "is_valid results changed between setup and timed runs"
+    for o in outs7:
+        assert np.array_equal(o.cpu().numpy(), wl["a7_valid"]), "is_valid results changed between setup and timed runs"
 
     if rank != 0:
         if dist:
@@ -311,16 +350,21 @@ def main():
     # counted at 8 B per word touched:
     #   k_is_valid:       mass+thr (16) + result (1) + the window's bitset words (8 each)
     #   k_explain_scan:   mass+thr (16) + status (1) of every query it resolves;
-    #                     pair path: count+offset (16) + payload of each SOME;
+    #                     pair path: 8-B hit record + payload of each SOME / OVERFLOW;
     #                     other windows: bitset words (8 each); 16 B worklist item per queued query
     #   k_explain_expand: worklist item (16) + status/count/offset (17) + 16 B per
     #                     index record expanded + payload (its bitset words are not counted)
+    #   k_result_pack:    8-B hit record in + 16-B dense record out per hit, the
+    #                     candidate payload read and written once (pad bytes not counted)
+    n_some_pair = int(((st == 2) & pair).sum())
+    cand_bytes = int(stats[7]) - 2 * n_some_pair + int(stats[5])
     bytes_k = {
         "k_is_valid": float(n7 * (16 + 1) + 8 * w7.sum()),
         # (stats[7] counts the 2 pad bytes per SOME query of the dword record stores: not algorithmic)
-        "k_explain_scan": float(n8 * 16 + (n8 - n_work) + 16 * int((some & pair).sum())
-                                + int(stats[7]) - 2 * int(((st == 2) & pair).sum())
+        "k_explain_scan": float(n8 * 16 + (n8 - n_work) + 8 * int((some & pair).sum())
+                                + int(stats[7]) - 2 * n_some_pair
                                 + 8 * int(w8[~pair].sum()) + 16 * n_work),
+        "k_result_pack": float(24 * n_hits0 + 2 * cand_bytes),
         "k_explain_expand": float(n_work * (16 + 17) + 16 * nodes + int(stats[5])),
     }
     kern = {}
@@ -391,7 +435,9 @@ def main():
         "engine_stats": {"pair": n_pair, "shallow": int(stats[0]), "deep": int(stats[1]), "exact": int(stats[2]),
                          "nomemo": int(stats[3]), "index_loads": int(stats[4]),
                          "candidates": int(res.count[some].sum()), "payload_bytes": int(stats[5] + stats[7]),
-                         "arena_bytes_used": int(len(res.payload))},
+                         "hits": n_hits0, "dense_payload_bytes": int(len(res.payload))},
+        "step": "k_is_valid + k_explain_scan + k_result_pack per step (status bytes, dense hit list and dense "
+                "payload of every query: the complete result); the host settles step k-1 while step k runs",
         "queries_per_s": (n7_all + n8_all) / (elapsed / args.steps),
         "cpu_baseline": cpu,
     }

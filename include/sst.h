@@ -133,17 +133,21 @@ int sst_is_singleton_batch_device(sst_ctx* ctx, const int64_t* masses, int n_mas
 int sst_explain_batch(sst_table* t, const double* mass, const double* thr_abs, int64_t n, double tolerance,
                       double precision, const int64_t* max_mods, int64_t max_mods_scalar, int with_memo,
                       uint64_t cap_per_query, sst_result** out);
-/* Same with inputs already in HBM; results stay on the device (fetch with
- * sst_result_device / sst_result_fetch).  Queued on the ctx stream, no host
- * synchronisation.  If *out is non-NULL it must be a result of the same ctx
- * with capacity >= n: its buffers are reused (no allocation).  The inputs
- * (and the table) must stay valid and unchanged until the result's first
- * view or fetch: that call reads the pass's control block back (32 bytes),
- * runs the deferred window classes if the scan routed any (deep, exact,
- * no-memo and > 2-item windows; the pass itself launches only the scan on
- * tables with the pair list), and re-runs the pass with larger workspaces
- * if a query outgrew the payload arena or the exact path's memo. */
-int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d_thr_abs, int64_t n,
+/* Same with inputs already in HBM; results stay on the device.  Queued on
+ * the ctx stream, no host synchronisation: the pass is the scan kernel and
+ * k_result_pack, which writes the complete result (status bytes, dense hit
+ * list, dense payload; see sst_result_hit_list) plus a small header into
+ * host-mapped memory.  If *out is non-NULL it must be a result of the same
+ * ctx with capacity >= n: its buffers are reused (no allocation).  The inputs
+ * (and the table) must stay valid and unchanged until the pass is settled
+ * (sst_result_settle, or the first view / fetch, which settle implicitly):
+ * settling waits for the pass and reads its header; only if the scan routed
+ * windows to the deferred classes (deep, exact, no-memo and > 2-item windows;
+ * the pass launches only the scan and the pack on tables with the pair list)
+ * does it launch them and pack again, and only if a query outgrew a payload
+ * region, the spill area or the exact path's memo does it re-run the pass
+ * with larger workspaces. */
+int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d_thr, int64_t n,
                              double tolerance, double precision, const int64_t* d_max_mods, int64_t max_mods_scalar,
                              int with_memo, uint64_t cap_per_query, sst_result** out);
 
@@ -159,31 +163,38 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
                                 double tolerance, double precision, const int64_t* max_mods, int64_t max_mods_scalar,
                                 uint64_t cap_per_query, sst_result** out);
 
-/* Host views of a result (valid until sst_result_free):
+/* Wait for a result's pass and complete it (see sst_explain_batch_device);
+ * reports the dense hit list's length and the dense payload's size.  Other
+ * work queued on the ctx stream after the pass keeps running.  No reference
+ * equivalent. */
+int sst_result_settle(sst_result* r, uint64_t* n_hits, uint64_t* payload_bytes);
+
+/* Host views of a result (valid until sst_result_free; filled by
+ * sst_result_fetch, which sst_explain_batch calls):
  *   status[n] (SST_NONE..), count[n] candidates, offset[n] byte offset of the
  *   query's candidates in payload; payload = per candidate one length byte k
  *   followed by k row indices (ascending, i.e. ascending mass); a query's
  *   candidates may be followed by unused bytes (count delimits them).
- *   count[i] and offset[i] are defined only when status[i] is SST_SOME,
- *   SST_OVERFLOW or SST_ABORTED (the others carry no candidates; the engine
- *   does not spend HBM writes on them). */
+ *   count[i] and offset[i] are 0 unless status[i] is SST_SOME, SST_OVERFLOW
+ *   or SST_ABORTED (the host builds them from the hit list). */
 int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count, const uint64_t** offset,
                     const uint8_t** payload, uint64_t* payload_bytes);
-/* Device views (no copy).  The first view or fetch after a pass queues the
- * compaction on the ctx stream: the pair scan's hit lists ({query, count,
- * offset} records written instead of scattered count/offset stores) are
- * scattered into count[] / offset[], and the per-wave payload regions are
- * packed into one dense payload that offset[] then indexes. */
+/* Device views (no copy; settle the result first).  d_status and d_payload
+ * (the dense payload) are the pass's own output.  d_count / d_offset are
+ * per-query u64 arrays built from the hit list only when asked for (pass
+ * NULL to skip them: 16 B per query of extra HBM traffic); their entries are
+ * undefined for queries without candidates. */
 int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint64_t** d_offset,
                       uint8_t** d_payload, uint64_t* payload_bytes);
-/* Dense hit list of a result, on the device: one 16-B record
- * {u32 query, u32 count (saturated), u64 offset into the dense payload as
- * u32 lo, hi} per query with candidates (SOME, OVERFLOW, ABORTED), in no
- * particular order -- with the status bytes and the payload, the whole
- * result in ~1 B/query + 16 B per hit (the wire format bench.py --gather
- * sends over RCCL instead of 17 B/query).  Compacts the result first and
- * synchronises the ctx stream to report *n_hits.  Valid until the next pass
- * on this result or its free.  No reference equivalent. */
+/* The dense hit list of a result, on the device (settles it first): one
+ * 16-B record {u32 query, u32 count (saturated), u32 word lo, u32 word hi}
+ * per query with candidates (SOME, OVERFLOW, ABORTED), where word is the
+ * byte offset of the query's candidates in the dense payload (SOME) or the
+ * exact candidate count (OVERFLOW, ABORTED: no payload).  Records come in the
+ * engine's order (per scan wave, then the deferred paths).  With the status
+ * bytes and the payload this is the whole result in ~1 B/query + 16 B per hit
+ * (the wire format bench.py --gather sends over RCCL).  Valid until the next
+ * pass on this result or its free.  No reference equivalent. */
 int sst_result_hit_list(sst_result* r, void** d_hits, uint64_t* n_hits);
 /* Copy device results to the host views (synchronises the ctx stream). */
 int sst_result_fetch(sst_result* r);
@@ -220,6 +231,7 @@ int sst_length_bound_batch(sst_table* t, const double* su_mass, const double* ob
 #define SST_K_EXPLAIN_NOMEMO 3 /* reserved (merged into SST_K_EXPLAIN_DEFERRED) */
 #define SST_K_EXPLAIN_EXACT 4  /* reserved (merged into SST_K_EXPLAIN_DEFERRED) */
 #define SST_K_EXPLAIN_EXPAND 5
+#define SST_K_RESULT_PACK 6 /* k_result_pack: dense hit list + payload of a pass */
 #define SST_K_COUNT 8
 /* When enabled, every kernel launch of this ctx is bracketed by hipEvents
  * recorded on the ctx stream; sst_profile_read synchronises and returns the

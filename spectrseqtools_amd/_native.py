@@ -26,13 +26,15 @@ EXPORTS = (
     "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
-    "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list",
+    "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
 )
 
 # kernel ids of sst_profile_read
 K_IS_VALID, K_EXPLAIN_SCAN, K_EXPLAIN_DEEP, K_EXPLAIN_NOMEMO, K_EXPLAIN_EXACT, K_EXPLAIN_EXPAND = 0, 1, 2, 3, 4, 5
+K_RESULT_PACK = 6
 KERNEL_NAMES = {K_IS_VALID: "k_is_valid", K_EXPLAIN_SCAN: "k_explain_scan", K_EXPLAIN_DEEP: "k_explain_deferred",
-                K_EXPLAIN_EXPAND: "k_explain_expand"}  # ids 3, 4: reserved (merged into the deferred launch)
+                K_EXPLAIN_EXPAND: "k_explain_expand",
+                K_RESULT_PACK: "k_result_pack"}  # ids 3, 4: reserved (merged into the deferred launch)
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -99,6 +101,8 @@ def load_library(path=LIB_PATH):
     lib.sst_result_device.argtypes = [_P, _PP, _PP, _PP, _PP, ctypes.POINTER(_U64)]
     lib.sst_result_hit_list.argtypes = [_P, _PP, ctypes.POINTER(_U64)]
     lib.sst_result_hit_list.restype = _I
+    lib.sst_result_settle.argtypes = [_P, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]
+    lib.sst_result_settle.restype = _I
     lib.sst_result_fetch.argtypes = [_P]
     lib.sst_result_free.argtypes = [_P]
     lib.sst_result_free.restype = None
@@ -240,9 +244,10 @@ class ExplainResult:
         self.status = self.count = self.offset = self.payload = None
 
     def fetch(self):
+        """Host views of the fetched result (sst_result_host): status,
+        count / offset (0 for queries without candidates) and the dense
+        payload."""
         L = self.engine._lib
-        if self.status is None:
-            pass
         st, cnt, off, pay = (ctypes.c_void_p() for _ in range(4))
         nb = _U64()
         self.engine.check(L.sst_result_host(self.handle, ctypes.byref(st), ctypes.byref(cnt), ctypes.byref(off),
@@ -259,29 +264,37 @@ class ExplainResult:
         self.count = view(cnt, np.uint64, n)
         self.offset = view(off, np.uint64, n)
         self.payload = view(pay, np.uint8, int(nb.value))
-        # count/offset are defined only for statuses that carry candidates (include/sst.h)
-        none = ~np.isin(self.status, (SST_SOME, SST_OVERFLOW, SST_ABORTED))
-        self.count[none] = 0
-        self.offset[none] = 0
         return self
+
+    def settle(self):
+        """Wait for the pass and complete it (sst_result_settle):
+        (hit records, dense payload bytes)."""
+        nh, nb = _U64(), _U64()
+        self.engine.check(self.engine._lib.sst_result_settle(self.handle, ctypes.byref(nh), ctypes.byref(nb)),
+                          "sst_result_settle")
+        return int(nh.value), int(nb.value)
 
     def stats(self):
         out = np.zeros(8, np.uint64)
         self.engine.check(self.engine._lib.sst_result_stats(self.handle, _ptr(out)), "sst_result_stats")
         return out
 
-    def device_views(self):
+    def device_views(self, arrays=True):
+        """(status, count, offset, payload, payload bytes) device pointers;
+        arrays=False skips building the per-query count / offset arrays
+        (their pointers are then None)."""
         L = self.engine._lib
         st, cnt, off, pay = (ctypes.c_void_p() for _ in range(4))
         nb = _U64()
-        self.engine.check(L.sst_result_device(self.handle, ctypes.byref(st), ctypes.byref(cnt), ctypes.byref(off),
-                                              ctypes.byref(pay), ctypes.byref(nb)), "sst_result_device")
+        self.engine.check(L.sst_result_device(self.handle, ctypes.byref(st), ctypes.byref(cnt) if arrays else None,
+                                              ctypes.byref(off) if arrays else None, ctypes.byref(pay),
+                                              ctypes.byref(nb)), "sst_result_device")
         return st.value, cnt.value, off.value, pay.value, int(nb.value)
 
     def hit_list_device(self):
         """(device pointer, n_hits) of the dense hit list: u32x4 records
-        {query, count, offset lo, offset hi}, in no particular order
-        (sst_result_hit_list)."""
+        {query, count, word lo, word hi}; word = payload offset (SOME) or the
+        exact count (OVERFLOW / ABORTED) (sst_result_hit_list)."""
         p = ctypes.c_void_p()
         nh = _U64()
         self.engine.check(self.engine._lib.sst_result_hit_list(self.handle, ctypes.byref(p), ctypes.byref(nh)),

@@ -6,10 +6,13 @@
 // buffers, sizes workspaces and retries the rare batches whose outputs did not
 // fit the first arena / hash sizing.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -96,31 +99,31 @@ struct sst_result {
   sst_ctx* ctx = nullptr;
   int64_t n = 0;
   int64_t cap_n = 0;
-  DevBuf status, count, offset, payload, ctl, lists;
+  // the result a consumer reads (include/sst.h): status[n], the dense hit
+  // list and the dense payload, all written on the device by the pass
+  DevBuf status, hits, dense;
+  // pass workspaces: the arena (scan-wave regions + spill area), control
+  // blocks, class lists, scan worklists / hit records, tallies, deferred hits
+  DevBuf payload, ctl, lists, wave_stats, work, work_count, tally, wg_tally, dhits, hdr;
+  DevBuf count, offset;  // per-query arrays: only built for sst_result_device callers that ask for them
+  uint64_t* hdr_host = nullptr;  // host-mapped copy of the pack kernel's header (host address)
+  uint64_t* hdr_host_dev = nullptr;  // its device address
   // control block (spill cursor, class counters, stats) of the current pass;
   // two of them: each pass's scan kernel zeroes the other for the next pass
   // (no memsets between passes)
   int parity = 1;
   bool ctl_ready = false;
-  DevBuf wave_used, wave_stats, prefix, dense, work, work_count;
-  DevBuf hit_list, hit_ctr;  // sst_result_hit_list
-  int n_waves = 0;  // expand waves
-  int n_regions = 0;  // scan + expand waves (arena regions)
+  int n_expand_waves = 0;  // waves of k_explain_expand / the SHALLOW role
   int64_t n_scan_waves = 0;
+  int n_wg = 0;             // scan workgroups (= k_result_pack blocks)
   uint64_t work_region = 0;
   uint64_t region_bytes = 0, spill_bytes = 0;
-  bool compacted = false;
-  bool hits = false;  // the last pass's scan left hit lists (k_explain_scan) for the compaction to scatter
-  // the expand waves' arena regions hold data of an earlier pass (k_explain_expand ran); fresh results
-  // start with them zeroed (alloc_result)
-  bool expand_regions_dirty = false;
-  // the last pass came from sst_explain_batch_device and has not been checked
-  // for arena / memo retries yet (settle, at the first view or fetch)
-  bool unsettled = false;
-  // the device path's tail launch (k_explain_deferred) waits for the first
-  // view / fetch, which launches it only if the scan routed any window to it
-  bool tail_deferred = false;
-  bool tail_regions_used = false;  // a tail launch wrote the expand regions since they were last zeroed
+  uint64_t pass_id = 0;
+  uint64_t pack_seq = 0;  // k_result_pack launches of this result: the header carries the latest
+  bool tail_ran = false;   // the deferred-class launch ran for the current pass
+  bool settled = true;     // the current pass has been checked (routed windows run, retries done)
+  bool arrays_ready = false;  // count[] / offset[] built from the hit list for the current pass
+  bool bitset_scan = false;   // the pass ran k_bitset_scan + k_explain_expand (tables without the pair list)
   struct {
     sst_table* t;
     const double *mass, *thr;
@@ -131,10 +134,10 @@ struct sst_result {
     uint64_t cap;
   } pass{};
   uint64_t arena_bytes = 0;
+  uint64_t n_hits = 0, payload_bytes = 0;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
   std::vector<uint8_t> h_payload;
-  uint64_t payload_bytes = 0;
   uint64_t h_stats[kNumStats] = {0};
 };
 
@@ -259,7 +262,8 @@ int build_pair_list(sst_table* t, bool self_built) {
   // the reference's order: ascending sum, then ascending top row
   auto top = [](const E& x) { return (x.rows & 0xFFu) == 1u ? (x.rows >> 8) & 0xFFu : x.rows >> 16; };
   std::sort(e.begin(), e.end(), [&](const E& x, const E& y) { return x.sum != y.sum ? x.sum < y.sum : top(x) < top(y); });
-  if (e.empty() || e.size() > 65533) return SST_OK;
+  // the scan's 8-B hit records carry a window's count and payload bytes (<= 3 per entry + 2) as u16
+  if (e.empty() || e.size() > 21000) return SST_OK;
   const size_t n_e = e.size(), n_s = n_e + 2;  // + two sentinels: the walk reads two entries per step
   // Buckets start at w_min (no sum below it) and cover every window start
   // below pair_hi, so a pair-class window needs no bucket bound check; the
@@ -687,40 +691,43 @@ uint32_t memo_cap0(int units, uint32_t floor) {
 constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses per lane (first attempt)
 
 void free_result_bufs(sst_result* r) {
-  for (DevBuf* b : {&r->status, &r->count, &r->offset, &r->payload, &r->ctl, &r->lists,
-                    &r->wave_used, &r->wave_stats, &r->prefix, &r->dense, &r->work, &r->work_count,
-                    &r->hit_list, &r->hit_ctr})
+  for (DevBuf* b : {&r->status, &r->hits, &r->dense, &r->payload, &r->ctl, &r->lists, &r->wave_stats, &r->work,
+                    &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->count, &r->offset})
     b->release();
+  if (r->hdr_host) (void)hipHostFree(r->hdr_host);
+  r->hdr_host = nullptr;
 }
 
-// control block layout (u64 words): [0] spill cursor, [1..2] class counters
-// (u32 x kNumClasses), [4..4+kNumStats) deferred-kernel stats
-constexpr int kCtlWords = 16;
 uint64_t* ctl_block(sst_result* r, int parity) { return (uint64_t*)r->ctl.p + parity * kCtlWords; }
 
 OutArgs out_args(sst_result* r) {
-  OutArgs o;
+  static_assert(kCtlArenaRetries < kCtlWords && kCtlStats + kNumStats <= kCtlDhits && 2 * 2 >= kNumClasses,
+                "control block layout");
+  OutArgs o{};
   uint64_t* ctl = ctl_block(r, r->parity);
   o.status = (int8_t*)r->status.p;
-  o.count = (uint64_t*)r->count.p;
-  o.offset = (uint64_t*)r->offset.p;
   o.payload = (uint8_t*)r->payload.p;
   o.arena_bytes = r->arena_bytes;
   o.region_bytes = r->region_bytes;
-  o.spill_base = (uint64_t)r->n_regions * r->region_bytes;
-  o.cursor = ctl;
-  o.exact_retries = (unsigned long long*)(ctl + 3);
+  o.spill_base = (uint64_t)r->n_scan_waves * r->region_bytes;
+  o.cursor = ctl + kCtlCursor;
+  o.exact_retries = (unsigned long long*)(ctl + kCtlExactRetries);
+  o.arena_retries = (unsigned long long*)(ctl + kCtlArenaRetries);
+  o.region_need = (unsigned long long*)(ctl + kCtlRegionNeed);
   o.ctl_next = ctl_block(r, r->parity ^ 1);
   o.ctl_words = kCtlWords;
-  o.wave_used = (uint64_t*)r->wave_used.p;
   o.wave_stats = (unsigned long long*)r->wave_stats.p;
-  o.counters = (uint32_t*)(ctl + 1);
-  o.lists = (uint32_t*)r->lists.p;
-  o.stats = (unsigned long long*)(ctl + 4);
   o.work = (uint4*)r->work.p;
   o.work_count = (uint32_t*)r->work_count.p;
+  o.tally = (uint2*)r->tally.p;
+  o.wg_tally = (uint2*)r->wg_tally.p;
   o.work_region = r->work_region;
   o.n_scan_waves = r->n_scan_waves;
+  o.counters = (uint32_t*)(ctl + kCtlCounters);
+  o.lists = (uint32_t*)r->lists.p;
+  o.stats = (unsigned long long*)(ctl + kCtlStats);
+  o.dhits = (uint4*)r->dhits.p;
+  o.dhit_count = (uint32_t*)(ctl + kCtlDhits);
   return o;
 }
 
@@ -740,13 +747,17 @@ int ensure_exact_ws(sst_ctx* c, uint32_t hash_cap, int lanes) {
   return SST_OK;
 }
 
-// Workspaces for a retry pass: the spill area sized to what the spill cursor
-// counted (it keeps counting past the arena), the exact path's memo 8x larger
-// per lane over 8x fewer lanes.
-int grow_for_retry(sst_result* r, bool arena, bool exact, uint64_t cursor) {
+uint64_t round16(uint64_t x) { return (x + 15u) & ~15ull; }
+
+// Workspaces for a retry pass: scan-wave regions 4x larger when a wave's
+// region overflowed, the spill area sized to what the spill cursor counted
+// (it keeps counting past the arena), the exact path's memo 8x larger per
+// lane over 8x fewer lanes.
+int grow_for_retry(sst_result* r, bool regions, bool spill, bool exact, uint64_t cursor, uint64_t region_need) {
   sst_ctx* c = r->ctx;
-  if (arena) {
-    r->spill_bytes = std::max<uint64_t>(2 * r->spill_bytes, cursor + (1u << 20));
+  if (regions) r->region_bytes = round16(std::max<uint64_t>(2 * r->region_bytes, region_need + region_need / 4));
+  if (spill) r->spill_bytes = round16(std::max<uint64_t>(2 * r->spill_bytes, cursor + (1u << 20)));
+  if (regions || spill) {
     r->payload.release();
     r->dense.release();
   }
@@ -772,9 +783,8 @@ void fold_scan_limits(const TableArgs& a, QueryArgs& q) {
   q.cap32 = (uint32_t)std::min<uint64_t>(q.cap_count, UINT32_MAX);
 }
 
-// one pass of the explain pipeline on device buffers
 // the deferred-class launch of a pass (after the pair scan it also runs the
-// SHALLOW windows, one wave per block, in the expand regions)
+// SHALLOW windows, one wave per block)
 int launch_tail(sst_table* t, sst_result* r) {
   sst_ctx* c = t->ctx;
   const auto& ps = r->pass;
@@ -785,61 +795,92 @@ int launch_tail(sst_table* t, sst_result* r) {
   ExactWs ws{(char*)c->ws_hash.p, (char*)c->ws_frames.p, (char*)c->ws_stacks.p, (uint64_t*)c->ws_epochs.p,
              c->hash_cap};
   Prof p(c, SST_K_EXPLAIN_DEEP);  // deep, no-memo and exact roles: one launch
-  const int shallow_blocks = t->args.pairs_enabled ? std::min(r->n_waves, 4 * c->n_cu) : 0;
+  const int shallow_blocks = r->bitset_scan ? 0 : std::min(r->n_expand_waves, 4 * c->n_cu);
   HIP_OK(c, launch_explain_deferred(t->args, q, o, c->ws_deep.p, shallow_blocks, kDeepBlocks, ws, c->exact_blocks,
                                     c->stream));
-  if (shallow_blocks) r->tail_regions_used = true;
-  r->tail_deferred = false;
+  r->tail_ran = true;
   return SST_OK;
 }
 
-// lazy_tail (device path, pair scan): the tail launch waits for settle()
+// k_result_pack: dense hit list + dense payload + header of the current pass
+int launch_pack(sst_result* r) {
+  sst_ctx* c = r->ctx;
+  PackArgs pa{};
+  pa.tally = (const uint2*)r->tally.p;
+  pa.wg_tally = (const uint2*)r->wg_tally.p;
+  pa.work = (const uint4*)r->work.p;
+  pa.work_region = r->work_region;
+  pa.arena = (const uint8_t*)r->payload.p;
+  pa.region_bytes = r->region_bytes;
+  pa.spill_base = (uint64_t)r->n_scan_waves * r->region_bytes;
+  pa.spill_cap = r->spill_bytes;
+  pa.ctl = ctl_block(r, r->parity);
+  pa.dhits = (const uint4*)r->dhits.p;
+  pa.hits = (uint4*)r->hits.p;
+  pa.payload = (uint8_t*)r->dense.p;
+  pa.hdr = (uint64_t*)r->hdr.p;
+  pa.hdr_host = r->hdr_host_dev;
+  pa.pass_id = ++r->pack_seq;
+  pa.n_wg = r->n_wg;
+  {
+    static const char* dbg = getenv("SST_PACK_DBG");
+    pa.dbg = dbg ? atoi(dbg) : 0;
+  }
+  {
+    Prof p(c, SST_K_RESULT_PACK);
+    HIP_OK(c, launch_result_pack(pa, c->stream));
+  }
+  return SST_OK;
+}
+
+// One pass of the explain pipeline on device buffers: the scan, the
+// deferred-class launch (eager_tail; otherwise settle() launches it only if
+// the scan routed a window to it) and the result pack.  Tables without the
+// pair list run k_bitset_scan + k_explain_expand and always the tail.
 int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double* d_thr, const int64_t* d_mods,
-                 int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count,
-                 bool lazy_tail = false) {
+                 int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count, bool eager_tail) {
   sst_ctx* c = t->ctx;
   r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count};
   const int64_t n = r->n;
-  r->arena_bytes = (uint64_t)r->n_regions * r->region_bytes + r->spill_bytes;
-  static_assert(4 + kNumStats <= kCtlWords && 2 * 2 >= kNumClasses, "control block layout");
+  r->arena_bytes = (uint64_t)r->n_scan_waves * r->region_bytes + r->spill_bytes;
   if (!r->ctl.ensure(2 * kCtlWords * 8) || !r->lists.ensure((size_t)kNumClasses * std::max<int64_t>(n, 1) * 4) ||
-      !r->payload.ensure(r->arena_bytes))
+      !r->payload.ensure(r->arena_bytes) || !r->dense.ensure(r->arena_bytes))
     return fail(c, SST_E_NOMEM, "device allocation failed (result)");
   if (!r->ctl_ready) {
     HIP_OK(c, hipMemsetAsync(r->ctl.p, 0, 2 * kCtlWords * 8, c->stream));
     r->ctl_ready = true;
   }
   r->parity ^= 1;  // zeroed by the previous pass's scan (or above)
-  if (n == 0)      // no scan launch: zero the next pass's block here
+  ++r->pass_id;
+  r->tail_ran = false;
+  r->arrays_ready = false;
+  r->bitset_scan = !t->args.pairs_enabled;
+  if (n == 0) {  // nothing to launch: an empty, settled result
     HIP_OK(c, hipMemsetAsync(ctl_block(r, r->parity ^ 1), 0, kCtlWords * 8, c->stream));
+    r->n_hits = r->payload_bytes = 0;
+    r->settled = true;
+    return SST_OK;
+  }
+  r->settled = false;
   if (!c->ws_deep.ensure((size_t)2 * kDeepBlocks * 64 * kMaxDepth * glob_frame_bytes()))
     return fail(c, SST_E_NOMEM, "device allocation failed (deep workspace)");
   if (c->hash_cap == 0)
     if (int rc = ensure_exact_ws(c, kHashCap0, kExactLanes0)) return rc;
-  r->compacted = false;
   QueryArgs q{d_mass, d_thr, d_mods, mods_scalar, n, tol, prec, 1.0 / prec, with_memo, cap_count, kNodeBudget};
   fold_scan_limits(t->args, q);
   OutArgs o = out_args(r);
   {
     Prof p(c, SST_K_EXPLAIN_MAIN);
-    HIP_OK(c, launch_explain_scan(t->args, q, o, (int)(r->n_scan_waves / (kScanWG / 64)), c->stream));
-    r->hits = n > 0;  // every scan wave writes its hit-list length (0 for k_bitset_scan)
+    HIP_OK(c, launch_explain_scan(t->args, q, o, r->n_wg, c->stream));
   }
-  if (!t->args.pairs_enabled) {  // the pair scan runs its queued windows itself
+  if (r->bitset_scan) {  // the expand kernel routes the windows the bitset scan queued
     Prof p(c, SST_K_EXPLAIN_EXPAND);
-    HIP_OK(c, launch_explain_expand(t->args, q, o, r->n_waves / (kWG / 64), c->stream));
-    r->expand_regions_dirty = true;
-  } else if (r->expand_regions_dirty) {  // an earlier pass of this result launched it: empty its regions
-    HIP_OK(c, hipMemsetAsync((uint64_t*)r->wave_used.p + r->n_scan_waves, 0, (size_t)r->n_waves * 8, c->stream));
-    HIP_OK(c, hipMemsetAsync((unsigned long long*)r->wave_stats.p + r->n_scan_waves * kNumStats, 0,
-                             (size_t)r->n_waves * kNumStats * 8, c->stream));
-    r->expand_regions_dirty = false;
+    HIP_OK(c, launch_explain_expand(t->args, q, o, r->n_expand_waves / (kWG / 64), c->stream));
+    eager_tail = true;
   }
-  if (lazy_tail && t->args.pairs_enabled && n > 0) {
-    r->tail_deferred = true;
-    return SST_OK;
-  }
-  return launch_tail(t, r);
+  if (eager_tail)
+    if (int rc = launch_tail(t, r)) return rc;
+  return launch_pack(r);
 }
 
 int alloc_result(sst_table* t, int64_t n, sst_result** out) {
@@ -851,115 +892,140 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out) {
   r->n = n;
   r->cap_n = n;
   size_t nn = (size_t)std::max<int64_t>(n, 1);
-  // worklist: one region per scan wave, big enough for all its tiles
-  r->n_scan_waves = (int64_t)t->scan_blocks * (kScanWG / 64);
+  // the scan grid: every resident workgroup, or fewer for small batches (16
+  // tiles of 64 queries per workgroup at least); worklist: one region per
+  // scan wave, big enough for all its tiles
   int64_t tiles = ((int64_t)nn + 63) / 64;
+  r->n_wg = (int)std::max<int64_t>(1, std::min<int64_t>(t->scan_blocks, (tiles + 15) / 16));
+  r->n_scan_waves = (int64_t)r->n_wg * (kScanWG / 64);
   r->work_region = (uint64_t)((tiles + r->n_scan_waves - 1) / r->n_scan_waves) * 64;
-  // one arena region per scan wave and per expand wave, each sized for ~16 B
-  // of payload per query of a scan wave, then a spill area for overflowing
-  // regions and deferred queries
-  r->n_waves = c->expand_blocks * (kWG / 64);
-  r->n_regions = (int)r->n_scan_waves + r->n_waves;
-  uint64_t per_wave = (nn + r->n_scan_waves - 1) / r->n_scan_waves;
-  r->region_bytes = std::max<uint64_t>(256, (16 * per_wave + 15) / 16 * 16);
-  r->spill_bytes = std::max<uint64_t>(1u << 20, 2 * (uint64_t)nn);
-  if (!r->status.ensure(nn) || !r->count.ensure(nn * 8) || !r->offset.ensure(nn * 8) ||
-      !r->wave_used.ensure((size_t)r->n_regions * 8) ||
-      !r->wave_stats.ensure((size_t)r->n_regions * kNumStats * 8) ||
-      !r->prefix.ensure((size_t)(r->n_regions + 2) * 8) ||
-      !r->work.ensure((size_t)r->n_scan_waves * r->work_region * 16) ||
-      !r->work_count.ensure((size_t)r->n_scan_waves * 2 * 4)) {  // worklist lengths, then hit-list lengths
+  // one arena region per scan wave, sized for 16 B of payload per query slot
+  // of the wave (2 KB at least), then a spill area for the deferred paths
+  r->n_expand_waves = c->expand_blocks * (kWG / 64);
+  r->region_bytes = std::max<uint64_t>(2048, round16(16 * r->work_region));
+  r->spill_bytes = round16(std::max<uint64_t>(1u << 20, 2 * (uint64_t)nn));
+  void* hh = nullptr;
+  bool ok = r->status.ensure(nn) && r->hits.ensure(nn * 16) && r->dhits.ensure(nn * 16) &&
+            r->wave_stats.ensure((size_t)r->n_scan_waves * kNumStats * 8) &&
+            r->work.ensure((size_t)r->n_scan_waves * r->work_region * 16) &&
+            r->work_count.ensure((size_t)r->n_scan_waves * 4) && r->tally.ensure((size_t)r->n_scan_waves * 16) &&
+            r->wg_tally.ensure((size_t)r->n_wg * 16) && r->hdr.ensure(kHdrWords * 8);
+  if (ok && hipHostMalloc(&hh, kHdrWords * 8, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+    r->hdr_host = (uint64_t*)hh;
+    void* dp = nullptr;
+    ok = hipHostGetDevicePointer(&dp, hh, 0) == hipSuccess && dp != nullptr;
+    r->hdr_host_dev = (uint64_t*)dp;
+    memset(hh, 0, kHdrWords * 8);
+  } else {
+    ok = false;
+  }
+  if (!ok) {
+    (void)hipGetLastError();
     free_result_bufs(r);
     delete r;
     return fail(c, SST_E_NOMEM, "device allocation failed (result)");
-  }
-  // the expand waves' regions stay empty unless k_explain_expand runs (tables without the pair list)
-  if (hipMemsetAsync(r->wave_used.p, 0, r->wave_used.bytes, c->stream) != hipSuccess ||
-      hipMemsetAsync(r->wave_stats.p, 0, r->wave_stats.bytes, c->stream) != hipSuccess) {
-    free_result_bufs(r);
-    delete r;
-    return fail(c, SST_E_HIP, "hipMemsetAsync failed (result)");
   }
   *out = r;
   return SST_OK;
 }
 
-// Dense payload: per-wave regions and the spill area copied back to back,
-// offsets rewritten in place (once per explain pass).
-// A device-path pass may leave queries that did not fit the arena or the
-// exact path's memo (internal statuses).  The host path retries them at once;
-// here the first view / fetch checks two counters of the control block (8+8
-// bytes) and re-runs the pass with larger workspaces from the caller's device
-// inputs, which must still hold the batch (include/sst.h).
+// Wait for the current pass's last pack to publish its header and read it.
+// The header lives in host-mapped memory, written by the pack kernel as soon
+// as its sums are known: the host polls it (no event on the stream); the
+// pack's remaining stores complete in stream order before any later work of
+// this ctx (fetch copies, a re-run, the caller's next kernels).
+int wait_header(sst_result* r, uint64_t* h) {
+  sst_ctx* c = r->ctx;
+  volatile uint64_t* hv = r->hdr_host;
+  auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 0; __atomic_load_n(&hv[kHdrPass], __ATOMIC_ACQUIRE) != r->pack_seq; ++spin) {
+    if (spin < 4096) continue;
+    sched_yield();
+    if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      // a long pass (or a lost write): wait for the stream itself, then insist
+      HIP_OK(c, hipStreamSynchronize(c->stream));
+      if (__atomic_load_n(&hv[kHdrPass], __ATOMIC_ACQUIRE) != r->pack_seq)
+        return fail(c, SST_E_INTERNAL, "explain: the result header was not written");
+      break;
+    }
+  }
+  for (int k = 0; k < kHdrWords; ++k) h[k] = __atomic_load_n(&hv[k], __ATOMIC_ACQUIRE);
+  if (h[kHdrPass] != r->pack_seq) return fail(c, SST_E_INTERNAL, "explain: result header of another pass");
+  return SST_OK;
+}
+
+// Settle the current pass: wait for it, launch the deferred classes if the
+// scan routed windows to them (then pack again), and re-run the pass with
+// larger workspaces if a query outgrew a payload region, the spill area or
+// the exact path's memo -- from the caller's device inputs, which must still
+// hold the batch (include/sst.h).
 int settle(sst_result* r) {
-  if (!r->unsettled) return SST_OK;
+  if (r->settled) return SST_OK;
   sst_ctx* c = r->ctx;
   for (int attempt = 0;; ++attempt) {
-    uint64_t h[4] = {0, 0, 0, 0};
-    HIP_OK(c, hipMemcpyAsync(h, ctl_block(r, r->parity), sizeof h, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(c, hipStreamSynchronize(c->stream));
-    if (r->tail_deferred) {  // the class counters (h[1], h[2]) say whether the scan routed any window
-      if (h[1] | h[2]) {
-        if (int rc = launch_tail(r->pass.t, r)) return rc;
-        --attempt;  // read the counters again after the tail
-        continue;
-      }
-      r->tail_deferred = false;
-      if (r->tail_regions_used) {  // an earlier pass's tail left data in the expand regions
-        HIP_OK(c, hipMemsetAsync((uint64_t*)r->wave_used.p + r->n_scan_waves, 0, (size_t)r->n_waves * 8, c->stream));
-        HIP_OK(c, hipMemsetAsync((unsigned long long*)r->wave_stats.p + r->n_scan_waves * kNumStats, 0,
-                                 (size_t)r->n_waves * kNumStats * 8, c->stream));
-        r->tail_regions_used = false;
-      }
+    uint64_t h[kHdrWords];
+    if (int rc = wait_header(r, h)) return rc;
+    if (h[kHdrRouted] && !r->tail_ran) {
+      if (int rc = launch_tail(r->pass.t, r)) return rc;
+      if (int rc = launch_pack(r)) return rc;
+      --attempt;
+      continue;
     }
-    const bool arena = h[0] > r->spill_bytes, exact = h[3] > 0;
-    if (!arena && !exact) break;
+    const bool regions = h[kHdrArenaRetries] > 0, spill = h[kHdrCursor] > r->spill_bytes;
+    const bool exact = h[kHdrExactRetries] > 0;
+    if (!regions && !spill && !exact) {
+      r->n_hits = h[kHdrHits];
+      r->payload_bytes = h[kHdrPayload];
+      break;
+    }
     if (attempt == 6) return fail(c, SST_E_INTERNAL, "explain: retries exhausted");
-    if (int rc = grow_for_retry(r, arena, exact, h[0])) return rc;
+    HIP_OK(c, hipStreamSynchronize(c->stream));  // the pack may still run: buffers are about to be replaced
+    if (int rc = grow_for_retry(r, regions, spill, exact, h[kHdrCursor], h[kHdrRegionNeed])) return rc;
     const auto& p = r->pass;
-    if (int rc = explain_pass(p.t, r, p.mass, p.thr, p.mods, p.mods_scalar, p.tol, p.prec, p.with_memo, p.cap))
+    if (int rc = explain_pass(p.t, r, p.mass, p.thr, p.mods, p.mods_scalar, p.tol, p.prec, p.with_memo, p.cap, true))
       return rc;
   }
-  r->unsettled = false;
+  r->settled = true;
   return SST_OK;
 }
 
-int compact(sst_result* r) {
-  sst_ctx* c = r->ctx;
-  if (r->compacted) return SST_OK;
-  if (int rc = settle(r)) return rc;
-  if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, 1)))
-    return fail(c, SST_E_NOMEM, "device allocation failed (compaction)");
-  HIP_OK(c, launch_compact(out_args(r), r->n, r->n_regions, (uint64_t*)r->prefix.p, (uint8_t*)r->dense.p, r->hits,
-                           c->stream));
-  r->compacted = true;
-  return SST_OK;
-}
-
+// Host copies: status, the dense hit list (-> count[] / offset[] on the host)
+// and the dense payload.
 int fetch(sst_result* r) {
   sst_ctx* c = r->ctx;
   const int64_t n = r->n;
-  if (int rc = compact(r)) return rc;
+  if (int rc = settle(r)) return rc;
   r->h_status.resize(n);
-  r->h_count.resize(n);
-  r->h_offset.resize(n);
-  uint64_t pre_tail[2] = {0, 0};
-  std::vector<unsigned long long> ws((size_t)r->n_regions * kNumStats);
+  r->h_count.assign(n, 0);
+  r->h_offset.assign(n, 0);
+  std::vector<uint4> hv(r->n_hits);
+  std::vector<unsigned long long> ws((size_t)r->n_scan_waves * kNumStats);
   if (n) {
     HIP_OK(c, hipMemcpyAsync(r->h_status.data(), r->status.p, n, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(c, hipMemcpyAsync(r->h_count.data(), r->count.p, n * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_OK(c, hipMemcpyAsync(r->h_offset.data(), r->offset.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(r->h_stats, ctl_block(r, r->parity) + kCtlStats, kNumStats * 8, hipMemcpyDeviceToHost,
+                             c->stream));
+    HIP_OK(c, hipMemcpyAsync(ws.data(), r->wave_stats.p, ws.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    for (auto& x : r->h_stats) x = 0;
   }
-  HIP_OK(c, hipMemcpyAsync(pre_tail, (uint64_t*)r->prefix.p + r->n_regions, 16, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipMemcpyAsync(r->h_stats, ctl_block(r, r->parity) + 4, kNumStats * 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipMemcpyAsync(ws.data(), r->wave_stats.p, ws.size() * 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
-  for (int w = 0; w < r->n_regions; ++w)
-    for (int k = 0; k < kNumStats; ++k) r->h_stats[k] += ws[(size_t)w * kNumStats + k];
-  r->payload_bytes = std::min<uint64_t>(pre_tail[1], r->arena_bytes);
+  if (r->n_hits) HIP_OK(c, hipMemcpyAsync(hv.data(), r->hits.p, r->n_hits * 16, hipMemcpyDeviceToHost, c->stream));
   r->h_payload.resize(r->payload_bytes);
   if (r->payload_bytes)
-    HIP_OK(c, hipMemcpy(r->h_payload.data(), r->dense.p, r->payload_bytes, hipMemcpyDeviceToHost));
+    HIP_OK(c, hipMemcpyAsync(r->h_payload.data(), r->dense.p, r->payload_bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (n && !r->bitset_scan)  // k_bitset_scan's waves write zero counters
+    for (int64_t w = 0; w < r->n_scan_waves; ++w)
+      for (int k = 0; k < kNumStats; ++k) r->h_stats[k] += ws[(size_t)w * kNumStats + k];
+  for (const uint4& h : hv) {
+    if (h.x >= (uint32_t)n) return fail(c, SST_E_INTERNAL, "explain: hit record out of range");
+    const uint64_t word = ((uint64_t)h.w << 32) | h.z;
+    if (r->h_status[h.x] == SST_SOME) {
+      r->h_count[h.x] = h.y;
+      r->h_offset[h.x] = word;
+    } else {
+      r->h_count[h.x] = word;
+    }
+  }
   return SST_OK;
 }
 
@@ -982,8 +1048,7 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
   } else if (int rc = alloc_result(t, n, &r)) {
     return rc;
   }
-  int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count, true);
-  r->unsettled = rc == SST_OK;
+  int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count, false);
   if (rc) {
     if (!reuse) {
       free_result_bufs(r);
@@ -1015,28 +1080,10 @@ int sst_explain_batch(sst_table* t, const double* mass, const double* thr, int64
   const int64_t* dmo = mods ? (const int64_t*)c->in_mods.p : nullptr;
   sst_result* r = nullptr;
   if (int rc = alloc_result(t, n, &r)) return rc;
-  int rc = SST_OK;
-  for (int attempt = 0; attempt < 6; ++attempt) {
-    rc = explain_pass(t, r, dm, dt, dmo, mods_scalar, tol, prec, with_memo, cap_count);
-    if (!rc) rc = fetch(r);
-    if (rc) break;
-    bool arena_retry = false, exact_retry = false, bad = false;
-    for (int64_t i = 0; i < n; ++i) {
-      int s = r->h_status[i];
-      arena_retry |= s == kStatusArenaRetry;
-      exact_retry |= s == kStatusExactRetry;
-      bad |= s == kStatusPending;
-    }
-    if (bad) {
-      rc = fail(c, SST_E_INTERNAL, "explain: query left pending (internal error)");
-      break;
-    }
-    if (!arena_retry && !exact_retry) break;
-    uint64_t cur = 0;
-    HIP_OK(c, hipMemcpy(&cur, ctl_block(r, r->parity), 8, hipMemcpyDeviceToHost));
-    if ((rc = grow_for_retry(r, arena_retry, exact_retry, cur))) break;
-    if (attempt == 5) rc = fail(c, SST_E_INTERNAL, "explain: retries exhausted");
-  }
+  int rc = explain_pass(t, r, dm, dt, dmo, mods_scalar, tol, prec, with_memo, cap_count, true);
+  if (!rc) rc = fetch(r);  // settles: retries with larger workspaces happen there
+  for (int64_t i = 0; !rc && i < n; ++i)
+    if (r->h_status[i] <= kStatusPending) rc = fail(c, SST_E_INTERNAL, "explain: query left unresolved (internal error)");
   if (rc) {
     free_result_bufs(r);
     delete r;
@@ -1064,9 +1111,10 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
   }
   sst_result* r = nullptr;
   if (int rc = alloc_result(t, n, &r)) return rc;
-  // only the spill area is used: every region is empty for the compaction
-  HIP_OK(c, hipMemsetAsync(r->wave_used.p, 0, r->wave_used.bytes, c->stream));
-  HIP_OK(c, hipMemsetAsync(r->wave_stats.p, 0, r->wave_stats.bytes, c->stream));
+  // no scan: the pack finds empty scan tallies and takes the kernel's hit
+  // records and spill bytes
+  HIP_OK(c, hipMemsetAsync(r->tally.p, 0, r->tally.bytes, c->stream));
+  HIP_OK(c, hipMemsetAsync(r->wg_tally.p, 0, r->wg_tally.bytes, c->stream));
   QueryArgs q{(const double*)c->in_mass.p, thr ? (const double*)c->in_thr.p : nullptr,
               mods ? (const int64_t*)c->in_mods.p : nullptr, mods_scalar, n, tol, prec, 1.0 / prec, 1, cap_count,
               kRecNodeBudget};
@@ -1080,31 +1128,36 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
       rc = fail(c, SST_E_INTERNAL, "explain_recursion: retries exhausted");
       break;
     }
-    r->arena_bytes = (uint64_t)r->n_regions * r->region_bytes + r->spill_bytes;
+    r->arena_bytes = (uint64_t)r->n_scan_waves * r->region_bytes + r->spill_bytes;
     DevBuf hash, frames;
     if (!r->ctl.ensure(2 * kCtlWords * 8) || !r->payload.ensure(r->arena_bytes) ||
-        !hash.ensure((size_t)units * cap * rec_entry_bytes()) || !frames.ensure((size_t)units * rec_frame_bytes())) {
+        !r->dense.ensure(r->arena_bytes) || !hash.ensure((size_t)units * cap * rec_entry_bytes()) ||
+        !frames.ensure((size_t)units * rec_frame_bytes())) {
       rc = fail(c, SST_E_NOMEM, "device allocation failed (recursion)");
       break;
     }
     r->parity = 0;  // one pass per attempt: block 0, zeroed here
     r->ctl_ready = true;
+    ++r->pass_id;
+    r->bitset_scan = true;  // no scan-wave counters
     HIP_OK(c, hipMemsetAsync(r->ctl.p, 0, 2 * kCtlWords * 8, c->stream));
     HIP_OK(c, hipMemsetAsync(hash.p, 0, hash.bytes, c->stream));
-    r->compacted = false;
     HIP_OK(c, launch_explain_recursion(t->args, q, out_args(r), (char*)hash.p, (char*)frames.p, cap, units,
                                        c->stream));
+    if ((rc = launch_pack(r))) break;
+    uint64_t h[kHdrWords];
+    if ((rc = wait_header(r, h))) break;
+    r->n_hits = h[kHdrHits];
+    r->payload_bytes = h[kHdrPayload];
+    r->settled = true;
+    r->tail_ran = true;
     if ((rc = fetch(r))) break;
-    bool arena_retry = false, memo_retry = false;
-    for (int64_t i = 0; i < n; ++i) {
-      arena_retry |= r->h_status[i] == kStatusArenaRetry;
-      memo_retry |= r->h_status[i] == kStatusExactRetry;
-    }
+    bool memo_retry = false;
+    for (int64_t i = 0; i < n; ++i) memo_retry |= r->h_status[i] == kStatusExactRetry;
+    const bool arena_retry = h[kHdrCursor] > r->spill_bytes;
     if (!arena_retry && !memo_retry) break;
     if (arena_retry) {
-      uint64_t cur = 0;
-      HIP_OK(c, hipMemcpy(&cur, ctl_block(r, r->parity), 8, hipMemcpyDeviceToHost));
-      r->spill_bytes = std::max<uint64_t>(2 * r->spill_bytes, cur + (1u << 20));
+      r->spill_bytes = round16(std::max<uint64_t>(2 * r->spill_bytes, h[kHdrCursor] + (1u << 20)));
       r->payload.release();
       r->dense.release();
     }
@@ -1117,13 +1170,26 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
       units = std::max(1, units / 8);
     }
   }
-  if (!rc && n == 0) rc = fetch(r);
+  if (!rc && n == 0) {
+    r->settled = true;
+    rc = fetch(r);
+  }
   if (rc) {
     free_result_bufs(r);
     delete r;
     return rc;
   }
   *out = r;
+  return SST_OK;
+}
+
+int sst_result_settle(sst_result* r, uint64_t* n_hits, uint64_t* payload_bytes) {
+  if (!r) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(r->ctx->mu);
+  if (int rc = set_device(r->ctx)) return rc;
+  if (int rc = settle(r)) return rc;
+  if (n_hits) *n_hits = r->n_hits;
+  if (payload_bytes) *payload_bytes = r->payload_bytes;
   return SST_OK;
 }
 
@@ -1134,21 +1200,30 @@ int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count
   if (count) *count = r->h_count.data();
   if (offset) *offset = r->h_offset.data();
   if (payload) *payload = r->h_payload.data();
-  if (payload_bytes) *payload_bytes = r->payload_bytes;
+  if (payload_bytes) *payload_bytes = r->h_payload.size();
   return SST_OK;
 }
 
 int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint64_t** d_offset, uint8_t** d_payload,
                       uint64_t* payload_bytes) {
   if (!r) return SST_E_ARG;
-  std::lock_guard<std::recursive_mutex> g(r->ctx->mu);
-  if (int rc = set_device(r->ctx)) return rc;
-  if (int rc = compact(r)) return rc;  // queued on the ctx stream
+  sst_ctx* c = r->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = settle(r)) return rc;
+  if ((d_count || d_offset) && !r->arrays_ready) {  // per-query arrays: built from the hit list on request
+    const size_t nn = (size_t)std::max<int64_t>(r->n, 1);
+    if (!r->count.ensure(nn * 8) || !r->offset.ensure(nn * 8))
+      return fail(c, SST_E_NOMEM, "device allocation failed (count / offset arrays)");
+    HIP_OK(c, launch_hits_to_arrays((const uint4*)r->hits.p, r->n_hits, (const int8_t*)r->status.p,
+                                    (uint64_t*)r->count.p, (uint64_t*)r->offset.p, c->stream));
+    r->arrays_ready = true;
+  }
   if (d_status) *d_status = (int8_t*)r->status.p;
   if (d_count) *d_count = (uint64_t*)r->count.p;
   if (d_offset) *d_offset = (uint64_t*)r->offset.p;
   if (d_payload) *d_payload = (uint8_t*)r->dense.p;
-  if (payload_bytes) *payload_bytes = r->arena_bytes;
+  if (payload_bytes) *payload_bytes = r->payload_bytes;
   return SST_OK;
 }
 
@@ -1157,18 +1232,9 @@ int sst_result_hit_list(sst_result* r, void** d_hits, uint64_t* n_hits) {
   sst_ctx* c = r->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
-  if (int rc = compact(r)) return rc;  // final count / offset arrays
-  if (!r->hit_list.ensure((size_t)std::max<int64_t>(r->n, 1) * 16) || !r->hit_ctr.ensure(8))
-    return fail(c, SST_E_NOMEM, "device allocation failed (hit list)");
-  HIP_OK(c, hipMemsetAsync(r->hit_ctr.p, 0, 8, c->stream));
-  HIP_OK(c, launch_pack_hit_list((const int8_t*)r->status.p, (const uint64_t*)r->count.p,
-                                 (const uint64_t*)r->offset.p, r->n, r->hit_list.p,
-                                 (unsigned long long*)r->hit_ctr.p, c->stream));
-  uint64_t nh = 0;
-  HIP_OK(c, hipMemcpyAsync(&nh, r->hit_ctr.p, 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(c, hipStreamSynchronize(c->stream));
-  *d_hits = r->hit_list.p;
-  *n_hits = nh;
+  if (int rc = settle(r)) return rc;
+  *d_hits = r->hits.p;
+  *n_hits = r->n_hits;
   return SST_OK;
 }
 

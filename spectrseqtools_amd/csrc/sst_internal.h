@@ -99,33 +99,90 @@ struct QueryArgs {
 };
 
 // Arena layout of one explain pass:
-//   [0, n_waves * region)  one region per wave of the main kernel (bump
-//                          allocated by that wave alone: no atomics)
-//   [spill_base, arena)    spill area, atomically allocated (regions that
-//                          overflow, deep / exact / no-memo queries)
-// sst_result_fetch / _device compact it to a dense payload.
+//   [0, spill_base)        one region per scan wave (bump allocated by that
+//                          wave alone: no atomics), spill_base =
+//                          n_scan_waves * region_bytes
+//   [spill_base, arena)    spill area, atomically allocated (the deferred
+//                          paths: SHALLOW worklists, deep / exact / no-memo,
+//                          recursion)
+// k_result_pack turns the pass's output into the result every consumer
+// reads: status[n] (written in place by the kernels), a dense hit list (one
+// 16-B record {query, count, word} per query with candidates) and a dense
+// payload (see include/sst.h, sst_result_hit_list).
 struct OutArgs {
   int8_t* status;
-  uint64_t* count;
-  uint64_t* offset;
-  uint8_t* payload;
+  uint8_t* payload;           // the arena
   uint64_t arena_bytes;
-  uint64_t region_bytes;      // per-wave region of the main kernel
-  uint64_t spill_base;        // = n_waves * region_bytes
+  uint64_t region_bytes;      // per-wave region of the scan kernel (multiple of 16)
+  uint64_t spill_base;        // = n_scan_waves * region_bytes
   uint64_t* cursor;           // spill bytes taken (keeps counting past the arena: > spill area = arena retries)
   unsigned long long* exact_retries;  // queries the exact path left for a retry with a larger memo
+  unsigned long long* arena_retries;  // SOME queries whose scan-wave region was full (retried with larger regions)
+  unsigned long long* region_need;    // atomicMax: payload bytes a wave with a full region would have needed
   uint64_t* ctl_next;         // the next pass's control block: zeroed by the scan kernel
   int ctl_words;
-  uint64_t* wave_used;        // [n_waves] bytes used in each region (expand kernel waves)
-  unsigned long long* wave_stats;  // [n_waves][kNumStats] expand-kernel counters
+  unsigned long long* wave_stats;  // [n_scan_waves][kNumStats] scan-wave counters
   uint4* work;                // [n_scan_waves][work_region] queued SHALLOW {query, a, b, has_zero} from the
-                              // front, hit records {query, count, offset lo, hi} from the back
-  uint32_t* work_count;       // [2][n_scan_waves]: worklist lengths, then hit-list lengths (k_explain_scan)
+                              // front; the scan's hit records {query, count | bytes << 16} (uint2) from the back
+  uint32_t* work_count;       // [n_scan_waves] worklist lengths (k_explain_scan)
+  uint2* tally;               // [n_scan_waves] {hit records, region bytes used in 16-B units}
+  uint2* wg_tally;            // [scan workgroups] the sums over its 16 waves
   uint64_t work_region;
   int64_t n_scan_waves;
   uint32_t* counters;  // [kNumClasses]
   uint32_t* lists;     // [kNumClasses][n]
   unsigned long long* stats;  // [kNumStats] deferred-kernel counters
+  uint4* dhits;        // [n] hit records of the deferred paths (final format; kHitOffsetFlag: word = arena offset)
+  uint32_t* dhit_count;
+};
+
+// hit records: {query | flags, count (saturated to u32), word lo, word hi};
+// word = the byte offset of the query's candidates (SOME) or its exact
+// candidate count (OVERFLOW / ABORTED, no payload).  The deferred paths set
+// kHitOffsetFlag on SOME records (word = arena offset, rebased by the pack).
+constexpr uint32_t kHitOffsetFlag = 1u << 31;
+
+// control block layout (u64 words of one pass)
+enum {
+  kCtlCursor = 0,       // spill cursor
+  kCtlCounters = 1,     // [1..2]: u32 class counters x kNumClasses
+  kCtlExactRetries = 3,
+  kCtlStats = 4,        // [4..12): deferred-kernel stats
+  kCtlDhits = 12,       // u32 deferred hit records
+  kCtlArenaRetries = 13,
+  kCtlRegionNeed = 14,  // largest region a scan wave would have needed (when one overflowed)
+  kCtlWords = 16
+};
+
+// result header written by k_result_pack (u64 words)
+enum {
+  kHdrHits = 0,         // dense hit records
+  kHdrPayload = 1,      // dense payload bytes
+  kHdrRouted = 2,       // windows the scan queued for the deferred kernel (SHALLOW items + class lists)
+  kHdrExactRetries = 3,
+  kHdrArenaRetries = 4, // SOME queries whose scan-wave region was full
+  kHdrCursor = 5,       // raw spill cursor (sizes a retry's spill area)
+  kHdrPass = 6,         // pass id the header belongs to
+  kHdrRegionNeed = 7,   // largest region a scan wave would have needed (sizes a retry's regions)
+  kHdrWords = 8
+};
+
+struct PackArgs {
+  const uint2* tally;
+  const uint2* wg_tally;
+  const uint4* work;
+  uint64_t work_region;
+  const uint8_t* arena;
+  uint64_t region_bytes, spill_base, spill_cap;
+  const uint64_t* ctl;
+  const uint4* dhits;
+  uint4* hits;         // dense hit list out
+  uint8_t* payload;    // dense payload out
+  uint64_t* hdr;       // device copy of the header
+  uint64_t* hdr_host;  // host-mapped copy (may be null)
+  uint64_t pass_id;
+  int n_wg;
+  int dbg;  // DIAGNOSTIC (SST_PACK_DBG): 1 no hit stores, 2 no payload copy, 4 no host header, 8 only round 1
 };
 
 struct ValidArgs {  // is_valid_mass batch
@@ -184,10 +241,9 @@ hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const O
 int explain_scan_blocks_per_cu(size_t dyn_lds);
 int explain_expand_blocks_per_cu();
 size_t scan_dyn_lds(const TableArgs& t);
-hipError_t launch_pack_hit_list(const int8_t* status, const uint64_t* count, const uint64_t* offset, int64_t n,
-                                void* out, unsigned long long* ctr, hipStream_t st);
-hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* wave_prefix, uint8_t* dst, bool hits,
-                          hipStream_t st);
+hipError_t launch_result_pack(const PackArgs& p, hipStream_t st);
+hipError_t launch_hits_to_arrays(const uint4* hits, uint64_t n_hits, const int8_t* status, uint64_t* count,
+                                 uint64_t* offset, hipStream_t st);
 hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const OutArgs& o, void* ws_deep,
                                    int shallow_blocks, int deep_blocks, const ExactWs& ws, int exact_blocks,
                                    hipStream_t st);

@@ -1137,6 +1137,31 @@ __device__ __forceinline__ void wg_stat(unsigned long long* stats, int k, uint64
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t lane_mask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
 
+// One query's final result on the deferred paths: its status byte, and for a
+// query with candidates one hit record appended to the deferred hit list
+// (k_result_pack moves the list behind the scan's hits and rebases its
+// payload offsets).  Appends are wavefront-aggregated: one atomic per wave
+// instruction over its active lanes.
+__device__ __forceinline__ void emit_result(const OutArgs& out, bool live, uint32_t i, int8_t status,
+                                            uint64_t count, uint64_t off, bool lane_owns = true) {
+  if (live) out.status[i] = status;
+  const bool hit = live && lane_owns && (status == SST_SOME || status == SST_OVERFLOW || status == SST_ABORTED);
+  const uint64_t b = __ballot(hit);
+  if (!b) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __builtin_ctzll(b);
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(out.dhit_count, (uint32_t)__builtin_popcountll(b));
+  base = (uint32_t)__shfl((int)base, leader, 64);
+  if (hit) {
+    const bool some = status == SST_SOME;
+    const uint64_t word = some ? off : count;
+    out.dhits[base + __builtin_popcountll(b & lane_mask_lt(lane))] =
+        make_uint4(i | (some ? kHitOffsetFlag : 0u), count > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)count,
+                   (uint32_t)word, (uint32_t)(word >> 32));
+  }
+}
+
 // any reachable value in [a, b]: up to 6 bitset words loaded at once
 __device__ __forceinline__ bool window_has_roots(const uint64_t* valid, int64_t a, int64_t b) {
   const int64_t wa = a >> 6, wb = b >> 6;
@@ -1171,28 +1196,21 @@ __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
   return x;
 }
 
-// Shared tail of the scan / expand tiles: wavefront prefix sum of the payload
-// bytes, bump allocation in the wave's own region (spill when full), payload
-// write from registers (or a re-run straight into the arena).
+// Payload allocation of one 64-query chunk of the SHALLOW role: wavefront
+// prefix sum of the per-lane byte counts, one atomic on the spill cursor.
 struct TileOut {
   uint64_t off;
   uint64_t bytes;
   int8_t status;
 };
-__device__ __forceinline__ TileOut tile_alloc(const OutArgs& out, int lane, uint64_t region0, uint64_t& used,
-                                              uint64_t bytes, int8_t status) {
+__device__ __forceinline__ TileOut spill_alloc(const OutArgs& out, int lane, uint64_t bytes, int8_t status) {
   const uint64_t incl = wave_incl_scan(bytes);
   const uint64_t total = __shfl(incl, 63, 64);
   uint64_t base = 0;
   if (total) {
-    if (used + total <= out.region_bytes) {
-      base = region0 + used;
-      used += total;
-    } else {
-      unsigned long long sb = 0;
-      if (lane == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
-      base = out.spill_base + __shfl(sb, 0, 64);
-    }
+    unsigned long long sb = 0;
+    if (lane == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
+    base = out.spill_base + __shfl(sb, 0, 64);
   }
   TileOut r{base + incl - bytes, bytes, status};
   if (bytes && r.off + bytes > out.arena_bytes) {
@@ -1206,20 +1224,17 @@ __device__ __forceinline__ TileOut tile_alloc(const OutArgs& out, int lane, uint
 struct ShallowStats {
   uint64_t q, nodes, payload;
 };
-__device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t region, int lane, uint64_t used,
-                                                 int q_stat, int p_stat, uint64_t n_q, uint64_t nodes,
-                                                 uint64_t payload) {
+// a scan wave's counters into its own wave_stats slot (no atomics)
+__device__ __forceinline__ void wave_stats_flush(const OutArgs& out, int64_t wave, int lane, int q_stat, int p_stat,
+                                                 uint64_t n_q, uint64_t payload) {
   for (int o = 32; o > 0; o >>= 1) {
     n_q += __shfl_down(n_q, o, 64);
-    nodes += __shfl_down(nodes, o, 64);
     payload += __shfl_down(payload, o, 64);
   }
   if (lane == 0) {
-    out.wave_used[region] = used;
-    unsigned long long* ws = out.wave_stats + region * kNumStats;
+    unsigned long long* ws = out.wave_stats + wave * kNumStats;
     for (int k = 0; k < kNumStats; ++k) ws[k] = 0;
     ws[q_stat] = n_q;
-    ws[kStatNodes] = nodes;
     ws[p_stat] = payload;
   }
 }
@@ -1287,10 +1302,9 @@ __device__ __forceinline__ void pair_store(const PairLds& p, uint32_t first, uin
 // value -> NONE / EMPTY; deeper than SHALLOW or budget-binding -> the deferred
 // class lists, status pending), run the SHALLOW fast path on the rest (all
 // DFS state and the first 16 payload bytes in VGPRs), allocate payload in the
-// wave's region and write status / count / offset.
+// spill area and write the status byte and hit record.
 __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArgs& q, const OutArgs& out, const Lds& s,
-                                              const uint4* wl, uint32_t k0, uint32_t nw, int lane, uint64_t region0,
-                                              uint64_t& used, ShallowStats& st) {
+                                              const uint4* wl, uint32_t k0, uint32_t nw, int lane, ShallowStats& st) {
   const bool live = k0 + lane < nw;
   int64_t i = 0, a = 0, b = -1;
   int8_t status = SST_NONE;
@@ -1323,7 +1337,7 @@ __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArg
                       : ((item.w & kItemZero) ? SST_EMPTY : SST_NONE);
     if (deferred) status = (int8_t)kStatusPending;
   }
-  const TileOut to = tile_alloc(out, lane, region0, used, status == SST_SOME ? eo.bytes : 0, status);
+  const TileOut to = spill_alloc(out, lane, status == SST_SOME ? eo.bytes : 0, status);
   if (to.bytes) {
     if (!sink.over) {
       sink.flush(out.payload + to.off, to.bytes);
@@ -1333,13 +1347,8 @@ __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArg
       shallow_window(t, s, a, b, ms, e2);
     }
   }
-  if (live) {  // deferred queries: the deep / exact kernels write all three
-    out.status[i] = to.status;
-    if (!deferred) {
-      out.count[i] = eo.count;
-      out.offset[i] = to.bytes ? to.off : 0;
-    }
-  }
+  // deferred queries: pending here, the deep / exact roles write their result
+  emit_result(out, live, (uint32_t)i, to.status, eo.count, to.off, !deferred);
   st.payload += to.bytes;
 }
 
@@ -1371,16 +1380,20 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   const uint32_t ntiles = (n + 63) >> 6;
   const uint64_t region0 = (uint64_t)wave * out.region_bytes;  // scan waves own regions [0, n_scan_waves)
   const double limitf = (double)t.limit;
+  const uint32_t region_cap = (uint32_t)min(out.region_bytes, (uint64_t)UINT32_MAX);
   uint32_t used = 0;  // wave-uniform bump pointer
   uint32_t st_q = 0, st_payload = 0;
   uint4* wl = out.work + (uint64_t)wave * out.work_region;
   uint32_t n_work = 0;  // wave-uniform
-  // hit list: one {query, count, offset} record per SOME / OVERFLOW query,
-  // filled from the END of the wave's worklist region (a query is either
-  // queued or a hit, so the two never meet); k_scatter_hits turns it into the
-  // per-query count / offset arrays at compaction
-  uint4* hits = wl + out.work_region - 1;
+  // hit records: one 8-B {query, count | payload bytes << 16} per SOME /
+  // OVERFLOW query, filled from the END of the wave's worklist region (a query
+  // is either queued or a hit, and 16 * items + 8 * hits <= the region).  The
+  // wave's payload lies in its region in the same order, so k_result_pack
+  // derives every offset from a prefix sum of the byte counts.
+  uint2* hits = (uint2*)(wl + out.work_region) - 1;
   uint32_t n_hit = 0;  // wave-uniform
+  uint32_t n_retry = 0;  // wave-uniform: SOME queries that found the region full
+  uint64_t want = 0;     // wave-uniform: payload bytes of all the wave's tiles (sizes a retry)
   // Software pipeline, two tiles deep: a tile's inputs are loaded two tiles
   // ahead into one of two register sets that swap roles between the unrolled
   // steps (no copies), and each load is issued AFTER the previous tile's
@@ -1422,46 +1435,35 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     if (pair) cnt = pair_walk(pl, a, hi, first, bytes);
     int8_t status = oot ? (int8_t)SST_OUT_OF_TABLE : (zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE);
     if (cnt) status = cnt > q.cap32 ? (int8_t)SST_OVERFLOW : (int8_t)SST_SOME;
-    // payload: wavefront prefix sum, bump allocation in the wave's region
-    // (spill when full), records copied from LDS
+    // payload: wavefront prefix sum, bump allocation in the wave's region,
+    // records copied from LDS.  A full region (rare: > 16 B of payload per
+    // query of the wave) sends the tile's SOME queries to a host retry with
+    // larger regions.
     uint32_t pb = status == SST_SOME ? bytes + 2u : 0u;  // + 2 pad bytes (pair_store)
     const uint32_t incl = wave_incl_scan32(pb);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    uint64_t off = 0;
     bool retry = false;
+    want += total;
     if (total) {  // wave-uniform: the tile's chunk base stays in SGPRs
-      uint64_t base;
-      if ((uint64_t)used + total <= out.region_bytes) {
-        base = region0 + used;
+      if (used + total <= region_cap) {
+        if (pb) pair_store(pl, first, cnt, out.payload + (region0 + used + (incl - pb)));  // OVERFLOW: no payload
         used += total;
       } else {
-        unsigned long long sb = 0;
-        if (lane == 0) sb = atomicAdd((unsigned long long*)out.cursor, (unsigned long long)total);
-        base = out.spill_base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sb >> 32)) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sb));
+        retry = pb != 0;
+        n_retry += (uint32_t)__builtin_popcountll(__ballot(retry));
+        pb = 0;
       }
-      off = base + (incl - pb);
-      if (base + total > out.arena_bytes) {  // rare: the arena is full, the host retries these queries
-        retry = pb && off + pb > out.arena_bytes;
-        if (retry) pb = 0;
-      }
-      if (pb) pair_store(pl, first, cnt, out.payload + off);
     }
     st_payload += pb;
     st_q += pair ? 1u : 0u;
-    // NONE / EMPTY / OUT_OF_TABLE carry no candidates: count and offset stay
-    // undefined (include/sst.h), one byte per resolved query.  SOME and
-    // OVERFLOW append a 16-B hit record instead of two scattered 8-B stores
-    // (those were partial-line writes: 3x write amplification in the PMC)
+    // NONE / EMPTY / OUT_OF_TABLE carry no candidates: one byte per resolved
+    // query.  SOME and OVERFLOW append an 8-B hit record
     if (live && !work) out.status[i] = retry ? (int8_t)kStatusArenaRetry : status;
     const bool hit = cnt && !retry;  // pair path only: cnt == 0 off it
     const uint64_t hbal = __ballot(hit);
     if (hbal) {  // wave-uniform
-      if (hit) {
-        const uint64_t o = pb ? off : 0;
-        *(hits - (n_hit + (uint32_t)__builtin_popcountll(hbal & lane_mask_lt(lane)))) =
-            make_uint4(i, cnt, (uint32_t)o, (uint32_t)(o >> 32));
-      }
+      if (hit)
+        *(hits - (n_hit + (uint32_t)__builtin_popcountll(hbal & lane_mask_lt(lane)))) = make_uint2(i, cnt | (pb << 16));
       n_hit += (uint32_t)__builtin_popcountll(hbal);
     }
     if (__ballot(work)) {  // wave-uniform, rare here: route the window now, so that the deferred class lists
@@ -1505,10 +1507,27 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   }
   if (lane == 0) {
     out.work_count[wave] = n_work;
-    out.work_count[out.n_scan_waves + wave] = n_hit;
+    out.tally[wave] = make_uint2(n_hit, (used + 15u) >> 4);
     if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle SHALLOW role exit at once
+    if (n_retry) {
+      atomicAdd(out.arena_retries, (unsigned long long)n_retry);
+      atomicMax(out.region_need, (unsigned long long)want);
+    }
   }
-  wave_stats_flush(out, wave, lane, used, kStatPair, kStatPairPayload, st_q, 0, st_payload);
+  wave_stats_flush(out, wave, lane, kStatPair, kStatPairPayload, st_q, st_payload);
+  // the workgroup's totals for k_result_pack's prefix: {hit records, region
+  // 16-B units (the dense payload keeps 16-B aligned wave pieces)}
+  __shared__ uint2 wg_part[kScanWG / 64];
+  if (lane == 0) wg_part[w_in] = make_uint2(n_hit, (used + 15u) >> 4);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t h = 0, u = 0;
+    for (int k = 0; k < kScanWG / 64; ++k) {
+      h += wg_part[k].x;
+      u += wg_part[k].y;
+    }
+    out.wg_tally[blockIdx.x] = make_uint2(h, u);
+  }
 }
 
 // Tables without the pair list (uploaded tables, literal-sweep rows): every
@@ -1564,10 +1583,11 @@ __global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryAr
   }
   if (lane == 0) {
     out.work_count[wave] = n_work;
-    out.work_count[out.n_scan_waves + wave] = 0;  // no hit list: the expand kernel writes count / offset
+    out.tally[wave] = make_uint2(0, 0);  // no hit records: the expand kernel emits them
     if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle expand launch exit at once
   }
-  wave_stats_flush(out, wave, lane, 0, kStatPair, kStatPairPayload, 0, 0, 0);
+  if (threadIdx.x == 0) out.wg_tally[blockIdx.x] = make_uint2(0, 0);
+  wave_stats_flush(out, wave, lane, kStatPair, kStatPairPayload, 0, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1581,139 +1601,195 @@ __global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryAr
 __device__ __forceinline__ void expand_body(const TableArgs& t, const QueryArgs& q, const OutArgs& out, Lds& s,
                                             int64_t wave, int64_t n_waves) {
   const int lane = threadIdx.x & 63;
-  const int64_t region = out.n_scan_waves + wave;  // expand regions follow the scan regions
-  if (out.counters[kClassShallow] == 0) {  // nothing queued (block-uniform): empty regions
-    if (lane < kNumStats) out.wave_stats[region * kNumStats + lane] = 0;
-    if (lane == 0) out.wave_used[region] = 0;
-    return;
-  }
+  if (out.counters[kClassShallow] == 0) return;  // nothing queued (block-uniform)
   stage_rows(s, t);
-  const uint64_t region0 = (uint64_t)region * out.region_bytes;
-  uint64_t used = 0;  // wave-uniform bump pointer
   ShallowStats st{0, 0, 0};
   for (int64_t src = wave; src < out.n_scan_waves; src += n_waves) {
     const uint32_t nw = out.work_count[src];
     const uint4* wl = out.work + (uint64_t)src * out.work_region;
-    for (uint32_t k0 = 0; k0 < nw; k0 += 64) shallow_chunk(t, q, out, s, wl, k0, nw, lane, region0, used, st);
+    for (uint32_t k0 = 0; k0 < nw; k0 += 64) shallow_chunk(t, q, out, s, wl, k0, nw, lane, st);
   }
-  wave_stats_flush(out, region, lane, used, kStatShallow, kStatPayload, st.q, st.nodes, st.payload);
+  for (int o = 32; o > 0; o >>= 1) {
+    st.q += __shfl_down(st.q, o, 64);
+    st.nodes += __shfl_down(st.nodes, o, 64);
+    st.payload += __shfl_down(st.payload, o, 64);
+  }
+  if (lane == 0 && st.q) {
+    atomicAdd(&out.stats[kStatShallow], (unsigned long long)st.q);
+    atomicAdd(&out.stats[kStatNodes], (unsigned long long)st.nodes);
+    atomicAdd(&out.stats[kStatPayload], (unsigned long long)st.payload);
+  }
 }
 __global__ __launch_bounds__(kWG) void k_explain_expand(TableArgs t, QueryArgs q, OutArgs out) {
   __shared__ Lds s;
   expand_body(t, q, out, s, (int64_t)blockIdx.x * (kWG / 64) + (threadIdx.x >> 6), (int64_t)gridDim.x * (kWG / 64));
 }
 
-// Compaction of the arena into a dense payload (result fetch / gather only):
-// exclusive prefix over the per-wave regions, block copies, offset rewrite.
-// The spill cursor keeps counting past the arena when a query does not fit
-// (those queries report an arena retry): every length is clamped to what the
-// arena actually holds.
-__global__ __launch_bounds__(1024) void k_wave_prefix(const uint64_t* __restrict__ used, int n_waves,
-                                                      const uint64_t* __restrict__ cursor, uint64_t spill_cap,
-                                                      uint64_t* __restrict__ pre) {
-  __shared__ uint64_t part[1024];
-  const int per = (n_waves + 1023) / 1024;
-  const int b0 = threadIdx.x * per;
-  uint64_t sum = 0;
-  for (int k = 0; k < per; ++k)
-    if (b0 + k < n_waves) sum += used[b0 + k];
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
+// ---------------------------------------------------------------------------
+// Result materialisation -- k_result_pack, once per pass (and again after a
+// deferred-class launch): the dense hit list and the dense payload every
+// consumer reads (include/sst.h, sst_result_hit_list).
+//   * block b packs scan workgroup b's 16 waves: its place in the dense
+//     output is the prefix of the workgroup tallies before it plus the
+//     prefix of its own waves' tallies; each wave turns its scan wave's 8-B
+//     hit records into 16-B dense records (payload offsets from a wavefront
+//     prefix sum of the byte counts) and copies the wave's payload region in
+//     16-B pieces;
+//   * the deferred paths' hit records and spill bytes follow the scan's,
+//     spread over the whole grid;
+//   * block 0 writes the header (sizes, routed windows, retry counters) to
+//     HBM and to host-mapped memory, so that the host can settle the pass
+//     without a copy.
+// ---------------------------------------------------------------------------
+
+// Latency shape: every load the block needs in the common case -- the
+// workgroup tallies, its waves' tallies, the first 4 x 64 hit records and the
+// first 2 KB of payload of each wave -- is issued in one round before any of
+// them is used (the record and payload loads speculatively, with clamped
+// indices: the worklist and arena regions are always allocated that far), so
+// a block costs one memory round trip plus one workgroup reduction; larger
+// waves loop.  Sums are u32: hit records (< 2^32 queries) and 16-B units.
+constexpr int kPackRec = 4;  // hit records per lane in the first round
+constexpr int kPackPay = 2;  // 16-B payload pieces per lane in the first round
+
+// 64 scan hit records -> dense records; returns the running payload offset
+__device__ __forceinline__ uint64_t pack_hits(uint4* __restrict__ out, uint32_t k, uint32_t nh, uint2 rr, uint64_t run) {
+  const bool live = k < nh;
+  const uint32_t cnt = rr.y & 0xFFFFu, bytes = live ? rr.y >> 16 : 0u;
+  const uint32_t incl = wave_incl_scan32(bytes);
+  const uint64_t word = bytes ? run + (incl - bytes) : (uint64_t)cnt;  // offset, or OVERFLOW's count
+  if (live) out[k] = make_uint4(rr.x, cnt, (uint32_t)word, (uint32_t)(word >> 32));
+  return run + (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(x), 63);
+}
+
+__global__ __launch_bounds__(1024, 8) void k_result_pack(PackArgs p) {  // 2 blocks per CU
+  const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int b = blockIdx.x;
+  const bool scan_part = b < p.n_wg;
+  const uint64_t w = (uint64_t)b * 16 + wv;  // wave-uniform: region bases stay in SGPRs
+  // ---- round 1: issue every load (no barrier: each wave sums the workgroup
+  // tallies itself, 8 B per scan workgroup from L2)
+  const uint32_t nd = *(const uint32_t*)(p.ctl + kCtlDhits);  // deferred hit records
+  const uint64_t cursor = p.ctl[kCtlCursor];
+  const uint2 wtv = scan_part ? p.tally[(int64_t)b * 16 + (lane & 15)] : make_uint2(0, 0);
+  // (plain variables, not arrays: an array here is promoted to LDS)
+  uint2 r0 = make_uint2(0, 0), r1 = r0, r2 = r0, r3 = r0;
+  uint4 pay0 = make_uint4(0, 0, 0, 0), pay1 = pay0;
+  // record k of the wave sits at rec[top - k] (filled from the region's end)
+  const uint2* rec = (const uint2*)(p.work + w * p.work_region);
+  const uint32_t top = (uint32_t)(2 * p.work_region - 1);  // work_region < 2^31 (host checks)
+  const uint4* src = (const uint4*)(p.arena + w * p.region_bytes);
+  if (scan_part) {
+    const uint32_t last_pay = (uint32_t)min<uint64_t>(p.region_bytes >> 4, 0xFFFFFFFFull) - 1;
+    r0 = rec[top - min((uint32_t)lane, top)];
+    r1 = rec[top - min((uint32_t)(64 + lane), top)];
+    r2 = rec[top - min((uint32_t)(128 + lane), top)];
+    r3 = rec[top - min((uint32_t)(192 + lane), top)];
+    pay0 = src[min((uint32_t)lane, last_pay)];
+    pay1 = src[min((uint32_t)(64 + lane), last_pay)];
   }
-  uint64_t run = part[threadIdx.x] - sum;
-  for (int k = 0; k < per; ++k)
-    if (b0 + k < n_waves) {
-      pre[b0 + k] = run;
-      run += used[b0 + k];
+  // ---- workgroup prefix (< b) and totals of the scan's hit records / units
+  uint32_t ph = 0, pu = 0, th = 0, tu = 0;
+  for (int k0 = 0; k0 < p.n_wg; k0 += 8 * 64) {
+    uint2 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j * 64 + lane;
+      v[j] = k < p.n_wg ? p.wg_tally[k] : make_uint2(0, 0);
     }
-  if (threadIdx.x == 1023) {
-    pre[n_waves] = part[1023];             // bytes of all regions
-    const uint64_t sp = *cursor < spill_cap ? *cursor : spill_cap;
-    pre[n_waves + 1] = part[1023] + sp;  // + spill bytes = dense payload size
-  }
-}
-
-__global__ __launch_bounds__(256) void k_compact_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                      const uint64_t* __restrict__ used,
-                                                      const uint64_t* __restrict__ pre, int n_waves, uint64_t region,
-                                                      uint64_t spill_base, const uint64_t* __restrict__ cursor,
-                                                      uint64_t spill_cap) {
-  for (int w = blockIdx.x; w <= n_waves; w += gridDim.x) {
-    uint64_t len, from, to;
-    if (w < n_waves) {
-      len = used[w] < region ? used[w] : region;
-      from = (uint64_t)w * region;
-      to = pre[w];
-    } else {
-      len = *cursor < spill_cap ? *cursor : spill_cap;
-      from = spill_base;
-      to = pre[n_waves];
-    }
-    for (uint64_t k = threadIdx.x; k < len; k += blockDim.x) dst[to + k] = src[from + k];
-  }
-}
-
-// The scan's hit lists -> count[i] and (arena) offset[i]; runs before
-// k_compact_offsets rewrites the offsets into the dense payload.
-__global__ __launch_bounds__(256) void k_scatter_hits(const uint4* __restrict__ work,
-                                                      const uint32_t* __restrict__ hit_count, uint64_t region,
-                                                      int64_t n_scan_waves, uint64_t* __restrict__ count,
-                                                      uint64_t* __restrict__ offset) {
-  for (int64_t w = blockIdx.x; w < n_scan_waves; w += gridDim.x) {
-    const uint32_t nh = hit_count[w];
-    const uint4* top = work + (uint64_t)(w + 1) * region - 1;
-    for (uint32_t k = threadIdx.x; k < nh; k += blockDim.x) {
-      const uint4 h = *(top - k);
-      count[h.x] = h.y;
-      offset[h.x] = ((uint64_t)h.w << 32) | h.z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + j * 64 + lane;
+      th += v[j].x;
+      tu += v[j].y;
+      ph += k < b ? v[j].x : 0u;
+      pu += k < b ? v[j].y : 0u;
     }
   }
+  ph = wave_sum32(ph);
+  pu = wave_sum32(pu);
+  th = wave_sum32(th);
+  tu = wave_sum32(tu);
+  const uint64_t tb = (uint64_t)tu << 4;  // scan payload bytes (16-B pieces)
+  if (p.dbg & 8) {
+    if (b == 0 && t == 0) p.hdr[0] = th + pu + ph + tu + r0.x + r1.x + r2.x + r3.x + pay0.x + pay1.x;
+    return;
+  }
+  // ---- this wave's scan wave: dense hit records, then its payload region
+  if (scan_part) {
+    const uint32_t eh = wave_sum32(lane < wv ? wtv.x : 0u);
+    const uint32_t eu = wave_sum32(lane < wv ? wtv.y : 0u);
+    const uint32_t nh = (uint32_t)__builtin_amdgcn_readlane((int)wtv.x, wv);
+    uint32_t n16 = (uint32_t)__builtin_amdgcn_readlane((int)wtv.y, wv);
+    const uint64_t hbase = (uint64_t)ph + eh, pbase = ((uint64_t)pu + eu) << 4;
+    uint64_t run = pbase;
+    const uint32_t nhs = (p.dbg & 1) ? 0 : nh;
+    if (nh > 0) run = pack_hits(p.hits + hbase, lane, nhs, r0, run);
+    if (nh > 64) run = pack_hits(p.hits + hbase, 64 + lane, nhs, r1, run);
+    if (nh > 128) run = pack_hits(p.hits + hbase, 128 + lane, nhs, r2, run);
+    if (nh > 192) run = pack_hits(p.hits + hbase, 192 + lane, nhs, r3, run);
+    for (uint32_t k0 = kPackRec * 64; k0 < nh; k0 += 64)
+      run = pack_hits(p.hits + hbase, k0 + lane, nh, rec[top - min(k0 + lane, nh - 1)], run);
+    uint4* dst = (uint4*)(p.payload + pbase);
+    if (p.dbg & 2) n16 = 0;
+    if ((uint32_t)lane < n16) dst[lane] = pay0;
+    if ((uint32_t)(64 + lane) < n16) dst[64 + lane] = pay1;
+    for (uint32_t c = kPackPay * 64 + lane; c < n16; c += 64) dst[c] = src[c];
+  }
+  // ---- the deferred paths' records and spill bytes, behind the scan's
+  const uint64_t spill_used = cursor < p.spill_cap ? cursor : p.spill_cap;
+  const uint64_t gt = (uint64_t)b * 1024 + t, G = (uint64_t)gridDim.x * 1024;
+  for (uint64_t k = gt; k < nd; k += G) {
+    uint4 r = p.dhits[k];
+    if (r.x & kHitOffsetFlag) {
+      const uint64_t o = (((uint64_t)r.w << 32) | r.z) - p.spill_base + tb;
+      r = make_uint4(r.x & ~kHitOffsetFlag, r.y, (uint32_t)o, (uint32_t)(o >> 32));
+    }
+    p.hits[(uint64_t)th + k] = r;
+  }
+  const uint64_t n16s = (spill_used + 15u) >> 4;
+  const uint4* ssrc = (const uint4*)(p.arena + p.spill_base);
+  uint4* sdst = (uint4*)(p.payload + tb);
+  for (uint64_t c = gt; c < n16s; c += G) sdst[c] = ssrc[c];
+  // ---- header
+  if (b == 0 && t == 0) {
+    const uint32_t* ctr = (const uint32_t*)(p.ctl + kCtlCounters);
+    uint64_t h[kHdrWords];
+    for (int k = 0; k < kHdrWords; ++k) h[k] = 0;
+    h[kHdrHits] = (uint64_t)th + nd;
+    h[kHdrPayload] = tb + spill_used;
+    h[kHdrRouted] = (uint64_t)ctr[0] + ctr[1] + ctr[2] + ctr[3];
+    h[kHdrExactRetries] = p.ctl[kCtlExactRetries];
+    h[kHdrArenaRetries] = p.ctl[kCtlArenaRetries];  // spill overflows: the host compares the cursor
+    h[kHdrCursor] = cursor;
+    h[kHdrPass] = p.pass_id;
+    h[kHdrRegionNeed] = p.ctl[kCtlRegionNeed];
+    for (int k = 0; k < kHdrWords; ++k) p.hdr[k] = h[k];
+    if (p.hdr_host && !(p.dbg & 4))
+      for (int k = 0; k < kHdrWords; ++k)
+        __hip_atomic_store(p.hdr_host + k, h[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
-// Dense hit list of a compacted result (sst_result_hit_list): one
-// {query, count (saturated to u32), offset lo, offset hi} record per query
-// with candidates, appended per wavefront (ballot + one atomic), so records
-// come in no particular order.
-__global__ __launch_bounds__(256) void k_pack_hit_list(const int8_t* __restrict__ status,
-                                                       const uint64_t* __restrict__ count,
-                                                       const uint64_t* __restrict__ offset, int64_t n,
-                                                       uint4* __restrict__ out, unsigned long long* ctr) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  bool hit = false;
-  if (i < n) {
-    const int8_t st = status[i];
-    hit = st == SST_SOME || st == SST_OVERFLOW || st == SST_ABORTED;
-  }
-  const uint64_t b = __ballot(hit);
-  if (!b) return;  // wave-uniform
-  unsigned long long base = 0;
-  if (lane == 0) base = atomicAdd(ctr, (unsigned long long)__builtin_popcountll(b));
-  base = __shfl(base, 0, 64);
-  if (hit) {
-    const uint64_t c = count[i], o = offset[i];
-    out[base + __builtin_popcountll(b & lane_mask_lt(lane))] =
-        make_uint4((uint32_t)i, c > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)c, (uint32_t)o, (uint32_t)(o >> 32));
-  }
-}
-
-__global__ __launch_bounds__(256) void k_compact_offsets(const int8_t* __restrict__ status,
-                                                         const uint64_t* __restrict__ count, uint64_t* offset, int64_t n,
-                                                         const uint64_t* __restrict__ pre, int n_waves, uint64_t region,
-                                                         uint64_t spill_base) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (status[i] != SST_SOME) return;
-  uint64_t o = offset[i];
-  if (o >= spill_base) offset[i] = o - spill_base + pre[n_waves];
-  else {
-    uint64_t w = o / region;
-    offset[i] = o - w * region + pre[w];
+// Per-query count[] / offset[] arrays from the dense hit list (only for
+// callers that ask for them: sst_result_device).  Queries without candidates
+// keep undefined entries (include/sst.h).
+__global__ __launch_bounds__(256) void k_hits_to_arrays(const uint4* __restrict__ hits, uint64_t n_hits,
+                                                        const int8_t* __restrict__ status, uint64_t* __restrict__ count,
+                                                        uint64_t* __restrict__ offset) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n_hits) return;
+  const uint4 r = hits[k];
+  const uint64_t word = ((uint64_t)r.w << 32) | r.z;
+  if (status[r.x] == SST_SOME) {
+    count[r.x] = r.y;
+    offset[r.x] = word;
+  } else {
+    count[r.x] = word;
+    offset[r.x] = 0;
   }
 }
 
@@ -1760,9 +1836,7 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
         enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2);
       }
     }
-    out.status[i] = status;
-    out.count[i] = eo.count;
-    out.offset[i] = bytes ? off : 0;
+    emit_result(out, true, (uint32_t)i, status, eo.count, off);
     st_n++;
     st_nodes += eo.nodes;
   }
@@ -1830,9 +1904,7 @@ __device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs
         enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, ms, ~0ull, e2);
       }
     }
-    out.status[i] = status;
-    out.count[i] = eo.count;
-    out.offset[i] = bytes ? off : 0;
+    emit_result(out, true, (uint32_t)i, status, eo.count, off);
     st_n++;
     st_nodes += nodes + eo.nodes;
   }
@@ -2653,9 +2725,8 @@ __global__ __launch_bounds__(kRecLanes) void k_explain_recursion(TableArgs t, Qu
         }
       }
     }
-    out.status[i] = status;
-    out.count[i] = count;
-    out.offset[i] = status == SST_SOME ? off : 0;
+    // WAVE: every lane holds the same query; lane 0 owns its hit record
+    emit_result(out, true, (uint32_t)i, status, count, off, !WAVE || (threadIdx.x & 63) == 0);
   }
 }
 
@@ -2765,19 +2836,15 @@ int explain_scan_blocks_per_cu(size_t dyn) {
              : occupancy((const void*)k_bitset_scan, kScanWG, 0);
 }
 int explain_expand_blocks_per_cu() { return occupancy((const void*)k_explain_expand, kWG, 0); }
-hipError_t launch_compact(const OutArgs& o, int64_t n, int n_waves, uint64_t* pre, uint8_t* dst, bool hits,
-                          hipStream_t st) {
-  const uint64_t spill_cap = o.arena_bytes > o.spill_base ? o.arena_bytes - o.spill_base : 0;
-  hipLaunchKernelGGL(k_wave_prefix, dim3(1), dim3(1024), 0, st, o.wave_used, n_waves, o.cursor, spill_cap, pre);
-  hipLaunchKernelGGL(k_compact_copy, dim3(2048), dim3(256), 0, st, o.payload, dst, o.wave_used, pre, n_waves,
-                     o.region_bytes, o.spill_base, o.cursor, spill_cap);
-  if (n > 0 && hits)
-    hipLaunchKernelGGL(k_scatter_hits, dim3(2048), dim3(256), 0, st, (const uint4*)o.work,
-                       (const uint32_t*)o.work_count + o.n_scan_waves, o.work_region, o.n_scan_waves, o.count,
-                       o.offset);
-  if (n > 0)
-    hipLaunchKernelGGL(k_compact_offsets, dim3(blocks_for(n, 256)), dim3(256), 0, st, o.status, o.count, o.offset, n,
-                       pre, n_waves, o.region_bytes, o.spill_base);
+hipError_t launch_result_pack(const PackArgs& p, hipStream_t st) {
+  hipLaunchKernelGGL(k_result_pack, dim3(p.n_wg > 0 ? p.n_wg : 1), dim3(1024), 0, st, p);
+  return hipGetLastError();
+}
+hipError_t launch_hits_to_arrays(const uint4* hits, uint64_t n_hits, const int8_t* status, uint64_t* count,
+                                 uint64_t* offset, hipStream_t st) {
+  if (n_hits == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hits_to_arrays, dim3(blocks_for((int64_t)n_hits, 256)), dim3(256), 0, st, hits, n_hits, status,
+                     count, offset);
   return hipGetLastError();
 }
 hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const OutArgs& o, void* ws_deep,
@@ -2786,14 +2853,6 @@ hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const
   if (q.n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_explain_deferred, dim3(shallow_blocks + 2 * deep_blocks + exact_blocks), dim3(64), 0, st, t, q,
                      o, (GlobFrame*)ws_deep, ws, shallow_blocks, deep_blocks);
-  return hipGetLastError();
-}
-
-hipError_t launch_pack_hit_list(const int8_t* status, const uint64_t* count, const uint64_t* offset, int64_t n,
-                                void* out, unsigned long long* ctr, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pack_hit_list, dim3(blocks_for(n, 256)), dim3(256), 0, st, status, count, offset, n,
-                     (uint4*)out, ctr);
   return hipGetLastError();
 }
 
