@@ -358,11 +358,16 @@ def main():
     #                     candidate payload read and written once (pad bytes not counted)
     n_some_pair = int(((st == 2) & pair).sum())
     cand_bytes = int(stats[7]) - 2 * n_some_pair + int(stats[5])
+    # the device path's pair scan packs its own result (fused: no k_result_pack
+    # launch): its algorithmic bytes are then the inputs, the status bytes and
+    # the dense result (16-B hit record + candidate bytes per query with
+    # candidates); the wave-local records and payload it re-reads are not
+    fused = _native.K_RESULT_PACK not in prof
     bytes_k = {
         "k_is_valid": float(n7 * (16 + 1) + 8 * w7.sum()),
         # (stats[7] counts the 2 pad bytes per SOME query of the dword record stores: not algorithmic)
-        "k_explain_scan": float(n8 * 16 + (n8 - n_work) + 8 * int((some & pair).sum())
-                                + int(stats[7]) - 2 * n_some_pair
+        "k_explain_scan": float(n8 * 16 + (n8 - n_work) + (16 * n_hits0 + cand_bytes if fused else
+                                                            8 * int((some & pair).sum()) + int(stats[7]) - 2 * n_some_pair)
                                 + 8 * int(w8[~pair].sum()) + 16 * n_work),
         "k_result_pack": float(24 * n_hits0 + 2 * cand_bytes),
         "k_explain_expand": float(n_work * (16 + 17) + 16 * nodes + int(stats[5])),
@@ -436,8 +441,10 @@ def main():
                          "nomemo": int(stats[3]), "index_loads": int(stats[4]),
                          "candidates": int(res.count[some].sum()), "payload_bytes": int(stats[5] + stats[7]),
                          "hits": n_hits0, "dense_payload_bytes": int(len(res.payload))},
-        "step": "k_is_valid + k_explain_scan + k_result_pack per step (status bytes, dense hit list and dense "
-                "payload of every query: the complete result); the host settles step k-1 while step k runs",
+        "step": ("k_is_valid + k_explain_scan (packing its own dense result)" if fused else
+                 "k_is_valid + k_explain_scan + k_result_pack") +
+                " per step: status bytes, dense hit list and dense payload of every query (the complete "
+                "result); the host settles step k-1 while step k runs",
         "queries_per_s": (n7_all + n8_all) / (elapsed / args.steps),
         "cpu_baseline": cpu,
     }

@@ -104,7 +104,7 @@ struct sst_result {
   DevBuf status, hits, dense;
   // pass workspaces: the arena (scan-wave regions + spill area), control
   // blocks, class lists, scan worklists / hit records, tallies, deferred hits
-  DevBuf payload, ctl, lists, wave_stats, work, work_count, tally, wg_tally, dhits, hdr;
+  DevBuf payload, ctl, lists, wave_stats, work, work_count, tally, wg_tally, dhits, hdr, agg;
   DevBuf count, offset;  // per-query arrays: only built for sst_result_device callers that ask for them
   uint64_t* hdr_host = nullptr;  // host-mapped copy of the pack kernel's header (host address)
   uint64_t* hdr_host_dev = nullptr;  // its device address
@@ -692,7 +692,7 @@ constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses pe
 
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->hits, &r->dense, &r->payload, &r->ctl, &r->lists, &r->wave_stats, &r->work,
-                    &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->count, &r->offset})
+                    &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->count, &r->offset})
     b->release();
   if (r->hdr_host) (void)hipHostFree(r->hdr_host);
   r->hdr_host = nullptr;
@@ -728,6 +728,14 @@ OutArgs out_args(sst_result* r) {
   o.stats = (unsigned long long*)(ctl + kCtlStats);
   o.dhits = (uint4*)r->dhits.p;
   o.dhit_count = (uint32_t*)(ctl + kCtlDhits);
+  o.fused = 0;
+  o.agg = (uint64_t*)r->agg.p + (size_t)r->parity * r->n_wg;
+  o.agg_next = (uint64_t*)r->agg.p + (size_t)(r->parity ^ 1) * r->n_wg;
+  o.hits_out = (uint4*)r->hits.p;
+  o.dense = (uint8_t*)r->dense.p;
+  o.hdr = (uint64_t*)r->hdr.p;
+  o.hdr_host = r->hdr_host_dev;
+  o.pass_id = 0;
   return o;
 }
 
@@ -869,10 +877,20 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   QueryArgs q{d_mass, d_thr, d_mods, mods_scalar, n, tol, prec, 1.0 / prec, with_memo, cap_count, kNodeBudget};
   fold_scan_limits(t->args, q);
   OutArgs o = out_args(r);
+  // the pair scan packs its own result (and writes the header) when no
+  // deferred-class launch follows it in this pass
+  const bool fused = !eager_tail && !r->bitset_scan;
+  if (fused) {
+    o.fused = 1;
+    o.pass_id = ++r->pack_seq;
+    static const char* dbg = getenv("SST_PACK_DBG");
+    o.dbg = dbg ? atoi(dbg) : 0;
+  }
   {
     Prof p(c, SST_K_EXPLAIN_MAIN);
     HIP_OK(c, launch_explain_scan(t->args, q, o, r->n_wg, c->stream));
   }
+  if (fused) return SST_OK;
   if (r->bitset_scan) {  // the expand kernel routes the windows the bitset scan queued
     Prof p(c, SST_K_EXPLAIN_EXPAND);
     HIP_OK(c, launch_explain_expand(t->args, q, o, r->n_expand_waves / (kWG / 64), c->stream));
@@ -908,8 +926,10 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out) {
   bool ok = r->status.ensure(nn) && r->hits.ensure(nn * 16) && r->dhits.ensure(nn * 16) &&
             r->wave_stats.ensure((size_t)r->n_scan_waves * kNumStats * 8) &&
             r->work.ensure((size_t)r->n_scan_waves * r->work_region * 16) &&
-            r->work_count.ensure((size_t)r->n_scan_waves * 4) && r->tally.ensure((size_t)r->n_scan_waves * 16) &&
-            r->wg_tally.ensure((size_t)r->n_wg * 16) && r->hdr.ensure(kHdrWords * 8);
+            r->work_count.ensure((size_t)r->n_scan_waves * 4) && r->tally.ensure((size_t)r->n_scan_waves * 8) &&
+            r->wg_tally.ensure((size_t)r->n_wg * 8) && r->hdr.ensure(kHdrWords * 8) &&
+            r->agg.ensure((size_t)2 * r->n_wg * 8) &&
+            hipMemsetAsync(r->agg.p, 0, (size_t)2 * r->n_wg * 8, c->stream) == hipSuccess;
   if (ok && hipHostMalloc(&hh, kHdrWords * 8, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
     r->hdr_host = (uint64_t*)hh;
     void* dp = nullptr;

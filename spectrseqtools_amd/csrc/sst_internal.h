@@ -134,6 +134,19 @@ struct OutArgs {
   unsigned long long* stats;  // [kNumStats] deferred-kernel counters
   uint4* dhits;        // [n] hit records of the deferred paths (final format; kHitOffsetFlag: word = arena offset)
   uint32_t* dhit_count;
+  // fused result pack (k_explain_scan on the device path): each workgroup
+  // publishes its {hits, 16-B units} in agg[] (bit 63 = published), sums its
+  // predecessors' and writes its waves' dense records and payload; the last
+  // workgroup writes the header
+  int fused;
+  uint64_t* agg;       // [n_wg] this pass
+  uint64_t* agg_next;  // [n_wg] the next pass's: zeroed by block 0
+  uint4* hits_out;     // dense hit list
+  uint8_t* dense;      // dense payload
+  uint64_t* hdr;       // device header
+  uint64_t* hdr_host;  // host-mapped header (device address)
+  uint64_t pass_id;
+  int dbg;  // DIAGNOSTIC (SST_PACK_DBG): 1 no record copy, 2 no payload copy, 4 no look-back wait
 };
 
 // hit records: {query | flags, count (saturated to u32), word lo, word hi};
@@ -151,6 +164,7 @@ enum {
   kCtlDhits = 12,       // u32 deferred hit records
   kCtlArenaRetries = 13,
   kCtlRegionNeed = 14,  // largest region a scan wave would have needed (when one overflowed)
+  kCtlSpare = 15,
   kCtlWords = 16
 };
 

@@ -1352,6 +1352,31 @@ __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArg
   st.payload += to.bytes;
 }
 
+// 64 scan hit records -> dense records; returns the running payload offset
+__device__ __forceinline__ uint64_t pack_hits(uint4* __restrict__ out, uint32_t k, uint32_t nh, uint2 rr, uint64_t run) {
+  const bool live = k < nh;
+  const uint32_t cnt = rr.y & 0xFFFFu, bytes = live ? rr.y >> 16 : 0u;
+  const uint32_t incl = wave_incl_scan32(bytes);
+  const uint64_t word = bytes ? run + (incl - bytes) : (uint64_t)cnt;  // offset, or OVERFLOW's count
+  if (live) out[k] = make_uint4(rr.x, cnt, (uint32_t)word, (uint32_t)(word >> 32));
+  return run + (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+}
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(x), 63);
+}
+
+// The result header (u64 words, include order kHdr*): HBM copy and the
+// host-mapped copy the host polls (system-scope stores, one lane)
+__device__ __forceinline__ void write_header(uint64_t* hdr, uint64_t* hdr_host, const uint64_t* h) {
+  for (int k = 0; k < kHdrWords; ++k) hdr[k] = h[k];
+  if (hdr_host)
+    for (int k = 0; k < kHdrWords; ++k)
+      __hip_atomic_store(hdr_host + k, h[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ctl_read(uint64_t* ctl, int k) {  // counters other workgroups added to
+  return __hip_atomic_fetch_add(ctl + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // 8 waves/SIMD: two 1024-lane workgroups per CU, each with its LDS copy of
 // the pair list (<= 78 KB).  Tables built here carry the list: a window below
 // 3 * w_min whose budgets cannot bind is answered from LDS; every other
@@ -1365,7 +1390,10 @@ __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArg
 template <bool THR, bool MODS>
 __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
   extern __shared__ uint32_t lds_pair_img[];
-  if (blockIdx.x == 0 && threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
+    for (uint32_t k = threadIdx.x; k < gridDim.x; k += blockDim.x) out.agg_next[k] = 0;
+  }
   const int n_img = 2 * (t.n_pairs + 2) + t.n_buckets;
   // 16-B copies (the image is padded to 16 B; 4-B copies: scan +2.5 us)
   for (int k = threadIdx.x; k < ((n_img + 3) >> 2); k += blockDim.x)
@@ -1515,26 +1543,95 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     }
   }
   wave_stats_flush(out, wave, lane, kStatPair, kStatPairPayload, st_q, st_payload);
-  // the workgroup's totals for k_result_pack's prefix: {hit records, region
+  // the workgroup's totals for the result pack's prefix: {hit records, region
   // 16-B units (the dense payload keeps 16-B aligned wave pieces)}
   __shared__ uint2 wg_part[kScanWG / 64];
-  if (lane == 0) wg_part[w_in] = make_uint2(n_hit, (used + 15u) >> 4);
+  __shared__ uint32_t wg_pre[2];
+  const uint32_t units = (used + 15u) >> 4;
+  if (out.fused) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's records, payload, counter adds landed
+  if (lane == 0) wg_part[w_in] = make_uint2(n_hit, units);
   __syncthreads();
+  uint32_t wg_h = 0, wg_u = 0;
   if (threadIdx.x == 0) {
-    uint32_t h = 0, u = 0;
     for (int k = 0; k < kScanWG / 64; ++k) {
-      h += wg_part[k].x;
-      u += wg_part[k].y;
+      wg_h += wg_part[k].x;
+      wg_u += wg_part[k].y;
     }
-    out.wg_tally[blockIdx.x] = make_uint2(h, u);
+    out.wg_tally[blockIdx.x] = make_uint2(wg_h, wg_u);
+    if (out.fused)  // publish (8-B agent-scope store: flag and sums in one word)
+      __hip_atomic_store(out.agg + blockIdx.x, (1ull << 63) | ((uint64_t)wg_u << 32) | wg_h, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (!out.fused) return;
+  // ---- fused result pack.  Wave 0 sums the aggregates of the workgroups
+  // before this one (decoupled look-back over workgroups: each publishes once,
+  // when its tiles are done); the last workgroup also has every total and
+  // writes the header
+  if (w_in == 0) {
+    const uint32_t b = blockIdx.x;
+    uint32_t ph = 0, pu = 0;
+    for (uint32_t k0 = 0; k0 < b; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      uint64_t v = 0;
+      if (k < b && !(out.dbg & 4))
+        for (;;) {
+          v = __hip_atomic_load(out.agg + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (v >> 63) break;
+          __builtin_amdgcn_s_sleep(16);
+        }
+      ph += (uint32_t)v;
+      pu += (uint32_t)(v >> 32) & 0x7FFFFFFFu;
+    }
+    ph = wave_sum32(ph);
+    pu = wave_sum32(pu);
+    if (lane == 0) {
+      wg_pre[0] = ph;
+      wg_pre[1] = pu;
+      if (b == gridDim.x - 1) {  // every workgroup before this one has published: the totals
+        uint64_t* ctl = out.cursor;  // the pass's control block
+        const uint64_t ctr01 = ctl_read(ctl, kCtlCounters), ctr23 = ctl_read(ctl, kCtlCounters + 1);
+        uint64_t h[kHdrWords];
+        h[kHdrHits] = (uint64_t)ph + wg_h;
+        h[kHdrPayload] = ((uint64_t)pu + wg_u) << 4;
+        h[kHdrRouted] = (ctr01 & 0xFFFFFFFFu) + (ctr01 >> 32) + (ctr23 & 0xFFFFFFFFu) + (ctr23 >> 32);
+        h[kHdrExactRetries] = 0;
+        h[kHdrArenaRetries] = ctl_read(ctl, kCtlArenaRetries);
+        h[kHdrCursor] = 0;
+        h[kHdrPass] = out.pass_id;
+        h[kHdrRegionNeed] = ctl_read(ctl, kCtlRegionNeed);
+        write_header(out.hdr, out.hdr_host, h);
+      }
+    }
+  }
+  __syncthreads();
+  // each wave: its scan wave's dense records, then its payload region (data
+  // this wave wrote itself: served from this XCD's L2)
+  uint32_t eh = 0, eu = 0;
+  for (uint32_t k = 0; k < w_in; ++k) {
+    eh += wg_part[k].x;
+    eu += wg_part[k].y;
+  }
+  const uint64_t hbase = (uint64_t)wg_pre[0] + eh, pbase = ((uint64_t)wg_pre[1] + eu) << 4;
+  uint64_t run = pbase;
+  const uint2* rec = hits + 1;  // record k at rec[-1 - k]
+  const uint32_t nh_copy = (out.dbg & 1) ? 0 : n_hit, u_copy = (out.dbg & 2) ? 0 : units;
+  for (uint32_t k0 = 0; k0 < nh_copy; k0 += 64) {
+    const uint32_t k = k0 + lane;
+    run = pack_hits(out.hits_out + hbase, k, n_hit, k < n_hit ? *(rec - 1 - k) : make_uint2(0, 0), run);
+  }
+  const uint4* src = (const uint4*)(out.payload + region0);
+  uint4* dst = (uint4*)(out.dense + pbase);
+  for (uint32_t c = lane; c < u_copy; c += 64) dst[c] = src[c];
 }
 
 // Tables without the pair list (uploaded tables, literal-sweep rows): every
 // non-empty window is checked against the valid bitset here, then queued for
 // the expand kernel (<= 3 items) or the deferred class lists.
 __global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryArgs q, OutArgs out) {
-  if (blockIdx.x == 0 && threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
+    for (uint32_t k = threadIdx.x; k < gridDim.x; k += blockDim.x) out.agg_next[k] = 0;
+  }
   const int lane = threadIdx.x & 63;
   const uint32_t wave = blockIdx.x * (kScanWG / 64) + (threadIdx.x >> 6);
   const uint32_t n_waves = gridDim.x * (kScanWG / 64);
@@ -1652,19 +1749,6 @@ __global__ __launch_bounds__(kWG) void k_explain_expand(TableArgs t, QueryArgs q
 constexpr int kPackRec = 4;  // hit records per lane in the first round
 constexpr int kPackPay = 2;  // 16-B payload pieces per lane in the first round
 
-// 64 scan hit records -> dense records; returns the running payload offset
-__device__ __forceinline__ uint64_t pack_hits(uint4* __restrict__ out, uint32_t k, uint32_t nh, uint2 rr, uint64_t run) {
-  const bool live = k < nh;
-  const uint32_t cnt = rr.y & 0xFFFFu, bytes = live ? rr.y >> 16 : 0u;
-  const uint32_t incl = wave_incl_scan32(bytes);
-  const uint64_t word = bytes ? run + (incl - bytes) : (uint64_t)cnt;  // offset, or OVERFLOW's count
-  if (live) out[k] = make_uint4(rr.x, cnt, (uint32_t)word, (uint32_t)(word >> 32));
-  return run + (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-}
-__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(x), 63);
-}
-
 __global__ __launch_bounds__(1024, 8) void k_result_pack(PackArgs p) {  // 2 blocks per CU
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int b = blockIdx.x;
@@ -1767,10 +1851,7 @@ __global__ __launch_bounds__(1024, 8) void k_result_pack(PackArgs p) {  // 2 blo
     h[kHdrCursor] = cursor;
     h[kHdrPass] = p.pass_id;
     h[kHdrRegionNeed] = p.ctl[kCtlRegionNeed];
-    for (int k = 0; k < kHdrWords; ++k) p.hdr[k] = h[k];
-    if (p.hdr_host && !(p.dbg & 4))
-      for (int k = 0; k < kHdrWords; ++k)
-        __hip_atomic_store(p.hdr_host + k, h[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    write_header(p.hdr, (p.dbg & 4) ? nullptr : p.hdr_host, h);
   }
 }
 
