@@ -124,6 +124,7 @@ struct sst_result {
   bool settled = true;     // the current pass has been checked (routed windows run, retries done)
   bool arrays_ready = false;  // count[] / offset[] built from the hit list for the current pass
   bool bitset_scan = false;   // the pass ran k_bitset_scan + k_explain_expand (tables without the pair list)
+  bool fused_pass = false;    // the pass's scan packed its own queries' result (dense records + payload)
   struct {
     sst_table* t;
     const double *mass, *thr;
@@ -811,9 +812,14 @@ int launch_tail(sst_table* t, sst_result* r) {
 }
 
 // k_result_pack: dense hit list + dense payload + header of the current pass
-int launch_pack(sst_result* r) {
+int launch_pack(sst_result* r, const uint64_t* scan_hdr = nullptr) {
   sst_ctx* c = r->ctx;
   PackArgs pa{};
+  if (scan_hdr) {  // after a fused scan: its part of the result is in place
+    pa.scan_packed = 1;
+    pa.scan_hits = scan_hdr[kHdrHits];
+    pa.scan_bytes = scan_hdr[kHdrPayload];
+  }
   pa.tally = (const uint2*)r->tally.p;
   pa.wg_tally = (const uint2*)r->wg_tally.p;
   pa.work = (const uint4*)r->work.p;
@@ -880,6 +886,7 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   // the pair scan packs its own result (and writes the header) when no
   // deferred-class launch follows it in this pass
   const bool fused = !eager_tail && !r->bitset_scan;
+  r->fused_pass = fused;
   if (fused) {
     o.fused = 1;
     o.pass_id = ++r->pack_seq;
@@ -987,7 +994,7 @@ int settle(sst_result* r) {
     if (int rc = wait_header(r, h)) return rc;
     if (h[kHdrRouted] && !r->tail_ran) {
       if (int rc = launch_tail(r->pass.t, r)) return rc;
-      if (int rc = launch_pack(r)) return rc;
+      if (int rc = launch_pack(r, r->fused_pass ? h : nullptr)) return rc;
       --attempt;
       continue;
     }

@@ -197,6 +197,11 @@ struct PackArgs {
   uint64_t pass_id;
   int n_wg;
   int dbg;  // DIAGNOSTIC (SST_PACK_DBG): 1 no hit stores, 2 no payload copy, 4 no host header, 8 only round 1
+  // after a fused scan (which wrote the dense records and payload of its own
+  // queries): only the deferred paths' records and spill bytes are packed,
+  // behind the scan's totals
+  int scan_packed;
+  uint64_t scan_hits, scan_bytes;
 };
 
 struct ValidArgs {  // is_valid_mass batch

@@ -1377,16 +1377,47 @@ __device__ __forceinline__ uint64_t ctl_read(uint64_t* ctl, int k) {  // counter
   return __hip_atomic_fetch_add(ctl + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Raw buffer resource over [base, base + bytes): a lane whose offset is past
+// the end is dropped by the hardware (no memory access), so a masked store is
+// one unconditional instruction.  The scan's tiles issue a fixed number of
+// vector-memory instructions this way, which lets the compiler's vmcnt waits
+// for the next tile's inputs be exact: the in-order counter then never makes
+// a tile wait for the stores of the tile just before it.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kBufSkip = 0x80000000u;  // an offset past every buffer the scan addresses
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // set bits of m below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// payload bytes of `cnt` pair-list records from entry `first` (LDS)
+__device__ __forceinline__ uint32_t pair_bytes(const PairLds& p, uint32_t first, uint32_t cnt) {
+  uint32_t b = 0;
+#pragma unroll 1
+  for (uint32_t k = first; k < first + cnt; ++k) b += (p.recs[k] & 0xFFu) + 1u;
+  return b;
+}
+
 // 8 waves/SIMD: two 1024-lane workgroups per CU, each with its LDS copy of
-// the pair list (<= 78 KB).  Tables built here carry the list: a window below
+// the pair list (<= 44 KB).  Tables built here carry the list: a window below
 // 3 * w_min whose budgets cannot bind is answered from LDS; every other
-// non-empty window goes to the expand kernel unclassified.
-// THR: per-query thresholds given (else tol * mass).  MODS: per-query budgets
-// given (else the host folded the scalar budget into q.pair_hi_lim /
+// non-empty window is routed (bitset check, SHALLOW worklist or deferred class
+// lists).  THR: per-query thresholds given (else tol * mass).  MODS: per-query
+// budgets given (else the host folded the scalar budget into q.pair_hi_lim /
 // q.never_hi_lim, fold_scan_limits).  The classification is branch-free on
-// exact f64 integers, then u32 (a window inside the table lies in
-// [0, limit) with limit < 2^31); the per-tile cost is what bounds this kernel
-// (VALU-bound), so everything uniform is hoisted out of the loop.
+// exact f64 integers, then u32 (a window inside the table lies in [0, limit)
+// with limit < 2^31).
+//
+// A tile (64 queries) issues exactly its input loads and two masked stores:
+// the status bytes and one 8-B hit record {query, first entry | count << 16}
+// per SOME / OVERFLOW query, at the back of the wave's worklist region.  The
+// candidates' bytes are not written in the loop: after its tiles each wave
+// turns its hit records into the result (payload bytes from the LDS pair
+// list): on the device path (fused) the dense hit list and the dense payload,
+// placed by a decoupled look-back over the workgroups' totals (the last
+// workgroup writes the header); otherwise its payload region and 8-B records
+// {query, count | bytes << 16} for k_result_pack.
 template <bool THR, bool MODS>
 __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
   extern __shared__ uint32_t lds_pair_img[];
@@ -1402,31 +1433,25 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   const PairLds pl{lds_pair_img, lds_pair_img + t.n_pairs + 2, lds_pair_img + 2 * (t.n_pairs + 2), t.pair_base,
                    t.pair_shift};
   const int lane = threadIdx.x & 63;
-  const uint32_t wave = blockIdx.x * (kScanWG / 64) + (threadIdx.x >> 6);
+  // wave-uniform in SGPRs (the buffer resources below must be scalar)
+  const uint32_t w_in = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wave = blockIdx.x * (kScanWG / 64) + w_in;
   const uint32_t n_waves = gridDim.x * (kScanWG / 64);
   const uint32_t n = (uint32_t)q.n;  // < 2^32 - 64 (host checks)
   const uint32_t ntiles = (n + 63) >> 6;
-  const uint64_t region0 = (uint64_t)wave * out.region_bytes;  // scan waves own regions [0, n_scan_waves)
   const double limitf = (double)t.limit;
-  const uint32_t region_cap = (uint32_t)min(out.region_bytes, (uint64_t)UINT32_MAX);
-  uint32_t used = 0;  // wave-uniform bump pointer
-  uint32_t st_q = 0, st_payload = 0;
+  uint32_t st_q = 0, st_payload = 0;  // per lane: pair-path queries, their payload bytes (+ 2 pad bytes each)
   uint4* wl = out.work + (uint64_t)wave * out.work_region;
   uint32_t n_work = 0;  // wave-uniform
-  // hit records: one 8-B {query, count | payload bytes << 16} per SOME /
-  // OVERFLOW query, filled from the END of the wave's worklist region (a query
-  // is either queued or a hit, and 16 * items + 8 * hits <= the region).  The
-  // wave's payload lies in its region in the same order, so k_result_pack
-  // derives every offset from a prefix sum of the byte counts.
-  uint2* hits = (uint2*)(wl + out.work_region) - 1;
+  // hit records fill the wave's worklist region from its END (a query is
+  // either queued or a hit, and 16 * items + 8 * hits <= the region)
+  const uint32_t wl_bytes = (uint32_t)(out.work_region * 16);  // < 2^32 (host checks)
+  const __amdgpu_buffer_rsrc_t wl_rsrc = buf_rsrc(wl, wl_bytes);
+  const __amdgpu_buffer_rsrc_t st_rsrc = buf_rsrc(out.status, n);
   uint32_t n_hit = 0;  // wave-uniform
-  uint32_t n_retry = 0;  // wave-uniform: SOME queries that found the region full
-  uint64_t want = 0;     // wave-uniform: payload bytes of all the wave's tiles (sizes a retry)
   // Software pipeline, two tiles deep: a tile's inputs are loaded two tiles
   // ahead into one of two register sets that swap roles between the unrolled
-  // steps (no copies), and each load is issued AFTER the previous tile's
-  // stores.  The vmcnt counter retires in order, so the wait for a tile's
-  // inputs then covers the stores before them but never the newer prefetch.
+  // steps (no copies), each load issued after the previous tile's two stores.
   // Loads are unconditional (index clamped to the last query), streamed once
   // (nontemporal).
   auto fetch = [&](uint32_t tl, double& m, double& tt, int64_t& mm) {
@@ -1442,7 +1467,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     double lof, hif;
     quantise_lean(m_cur, t_cur, q.prec, q.rprec, lof, hif);
     const bool nonempty = live && lof <= hif;
-    const bool oot = nonempty && !(hif < limitf);  // mass_explanation.py:134-138 (NameError)
+    const bool oot = nonempty && !(hif < limitf);  // mass_explanation.py:134-138 (NotImplementedError)
     const bool zero = nonempty && !oot && lof <= 0.0 && hif >= 0.0;  // v == 0 -> [[]] (:130-131)
     const double af = __builtin_fmax(lof, 1.0);
     const bool active = nonempty && !oot && af <= hif;
@@ -1458,42 +1483,21 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
       pair = active && hi < q.pair_hi_lim;
       never = hi < q.never_hi_lim;
     }
-    const bool work = active && !pair;  // classified (bitset, depth, budgets) by the expand kernel
+    const bool work = active && !pair;  // routed below (bitset, depth, budgets)
     uint32_t first = 0, cnt = 0, bytes = 0;
     if (pair) cnt = pair_walk(pl, a, hi, first, bytes);
     int8_t status = oot ? (int8_t)SST_OUT_OF_TABLE : (zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE);
     if (cnt) status = cnt > q.cap32 ? (int8_t)SST_OVERFLOW : (int8_t)SST_SOME;
-    // payload: wavefront prefix sum, bump allocation in the wave's region,
-    // records copied from LDS.  A full region (rare: > 16 B of payload per
-    // query of the wave) sends the tile's SOME queries to a host retry with
-    // larger regions.
-    uint32_t pb = status == SST_SOME ? bytes + 2u : 0u;  // + 2 pad bytes (pair_store)
-    const uint32_t incl = wave_incl_scan32(pb);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    bool retry = false;
-    want += total;
-    if (total) {  // wave-uniform: the tile's chunk base stays in SGPRs
-      if (used + total <= region_cap) {
-        if (pb) pair_store(pl, first, cnt, out.payload + (region0 + used + (incl - pb)));  // OVERFLOW: no payload
-        used += total;
-      } else {
-        retry = pb != 0;
-        n_retry += (uint32_t)__builtin_popcountll(__ballot(retry));
-        pb = 0;
-      }
-    }
-    st_payload += pb;
+    st_payload += status == SST_SOME ? bytes + 2u : 0u;  // + 2 pad bytes (pair_store)
     st_q += pair ? 1u : 0u;
-    // NONE / EMPTY / OUT_OF_TABLE carry no candidates: one byte per resolved
-    // query.  SOME and OVERFLOW append an 8-B hit record
-    if (live && !work) out.status[i] = retry ? (int8_t)kStatusArenaRetry : status;
-    const bool hit = cnt && !retry;  // pair path only: cnt == 0 off it
-    const uint64_t hbal = __ballot(hit);
-    if (hbal) {  // wave-uniform
-      if (hit)
-        *(hits - (n_hit + (uint32_t)__builtin_popcountll(hbal & lane_mask_lt(lane)))) = make_uint2(i, cnt | (pb << 16));
-      n_hit += (uint32_t)__builtin_popcountll(hbal);
-    }
+    // the tile's two stores (masked lanes dropped): NONE / EMPTY / OUT_OF_TABLE /
+    // SOME / OVERFLOW status bytes; the hit records (pair path only: cnt == 0 off it)
+    const uint64_t hbal = __ballot(cnt != 0);
+    const uint32_t hpos = n_hit + mbcnt(hbal);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)status, st_rsrc, (live && !work) ? i : kBufSkip, 0, 0);
+    const u32x2 rv = {i, first | (cnt << 16)};
+    __builtin_amdgcn_raw_buffer_store_b64(rv, wl_rsrc, cnt ? wl_bytes - 8u * (hpos + 1u) : kBufSkip, 0, 0);
+    n_hit += (uint32_t)__builtin_popcountll(hbal);
     if (__ballot(work)) {  // wave-uniform, rare here: route the window now, so that the deferred class lists
                            // are complete when the scan ends (one tail launch runs every class)
       bool shallow = false;
@@ -1512,7 +1516,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
         if (!shallow) out.status[i] = st2;
       }
       const uint64_t sb = __ballot(shallow);
-      if (shallow) wl[n_work + __builtin_popcountll(sb & lane_mask_lt(lane))] = make_uint4(i, a, hi, zero ? kItemZero : 0u);
+      if (shallow) wl[n_work + mbcnt(sb)] = make_uint4(i, a, hi, zero ? kItemZero : 0u);
       n_work += (uint32_t)__builtin_popcountll(sb);
     }
   };
@@ -1522,9 +1526,13 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   // partial round of tiles is spread over all CUs (not over the first few
   // workgroups) while tiles 2j, 2j+1 -- one 128-B line of status bytes --
   // stay in one workgroup, i.e. one XCD's L2 (A/B: -0.8 us)
-  const uint32_t w_in = threadIdx.x >> 6;
   const uint32_t vw = (((w_in >> 1) * gridDim.x + blockIdx.x) << 1) | (w_in & 1u);
   fetch(vw, mA, tA, mmA);
+  // two dropped stores where a tile's stores would be: the loop entry then has
+  // the same VMEM count between the two prefetches as every later round, so
+  // the compiler's waits at the loop head are exact on both paths into it
+  __builtin_amdgcn_raw_buffer_store_b8(0, st_rsrc, kBufSkip, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b8(1, st_rsrc, kBufSkip + 64u, 0, 0);
   fetch(vw + n_waves, mB, tB, mmB);
   for (uint32_t tile = vw; tile < ntiles; tile += 2 * n_waves) {
     step(tile, mA, tA, mmA);
@@ -1533,22 +1541,26 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     step(tile + n_waves, mB, tB, mmB);
     fetch(tile + 3 * n_waves, mB, tB, mmB);
   }
+  // ---- the wave's totals: hit records, payload bytes (16-B units per wave
+  // piece of the payload)
+  const uint32_t pay = wave_sum32(st_payload);
+  const uint64_t region0 = (uint64_t)wave * out.region_bytes;  // non-fused: the wave's payload region
+  const bool fits = out.fused || pay <= min(out.region_bytes, (uint64_t)UINT32_MAX);
+  const uint32_t units = fits ? (pay + 15u) >> 4 : 0u;
   if (lane == 0) {
     out.work_count[wave] = n_work;
-    out.tally[wave] = make_uint2(n_hit, (used + 15u) >> 4);
+    out.tally[wave] = make_uint2(n_hit, units);
     if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle SHALLOW role exit at once
-    if (n_retry) {
-      atomicAdd(out.arena_retries, (unsigned long long)n_retry);
-      atomicMax(out.region_need, (unsigned long long)want);
+    if (!fits) {  // the host re-runs the pass with larger regions
+      atomicAdd(out.arena_retries, (unsigned long long)max(n_hit, 1u));
+      atomicMax(out.region_need, (unsigned long long)pay);
     }
   }
   wave_stats_flush(out, wave, lane, kStatPair, kStatPairPayload, st_q, st_payload);
-  // the workgroup's totals for the result pack's prefix: {hit records, region
-  // 16-B units (the dense payload keeps 16-B aligned wave pieces)}
   __shared__ uint2 wg_part[kScanWG / 64];
   __shared__ uint32_t wg_pre[2];
-  const uint32_t units = (used + 15u) >> 4;
-  if (out.fused) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's records, payload, counter adds landed
+  // this wave's hit records, counter adds and routed lists have landed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0) wg_part[w_in] = make_uint2(n_hit, units);
   __syncthreads();
   uint32_t wg_h = 0, wg_u = 0;
@@ -1562,66 +1574,89 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
       __hip_atomic_store(out.agg + blockIdx.x, (1ull << 63) | ((uint64_t)wg_u << 32) | wg_h, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (!out.fused) return;
-  // ---- fused result pack.  Wave 0 sums the aggregates of the workgroups
-  // before this one (decoupled look-back over workgroups: each publishes once,
-  // when its tiles are done); the last workgroup also has every total and
-  // writes the header
-  if (w_in == 0) {
-    const uint32_t b = blockIdx.x;
-    uint32_t ph = 0, pu = 0;
-    for (uint32_t k0 = 0; k0 < b; k0 += 64) {
-      const uint32_t k = k0 + lane;
-      uint64_t v = 0;
-      if (k < b && !(out.dbg & 4))
-        for (;;) {
-          v = __hip_atomic_load(out.agg + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (v >> 63) break;
-          __builtin_amdgcn_s_sleep(16);
+  uint64_t hbase = 0, pbase = region0;
+  if (out.fused) {
+    // Wave 0 sums the aggregates of the workgroups before this one (decoupled
+    // look-back over workgroups: each publishes once, when its tiles are
+    // done); the last workgroup also has every total and writes the header
+    if (w_in == 0) {
+      const uint32_t b = blockIdx.x;
+      uint32_t ph = 0, pu = 0;
+      for (uint32_t k0 = 0; k0 < b; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        uint64_t v = 0;
+        if (k < b && !(out.dbg & 4))
+          for (;;) {
+            v = __hip_atomic_load(out.agg + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v >> 63) break;
+            __builtin_amdgcn_s_sleep(16);
+          }
+        ph += (uint32_t)v;
+        pu += (uint32_t)(v >> 32) & 0x7FFFFFFFu;
+      }
+      ph = wave_sum32(ph);
+      pu = wave_sum32(pu);
+      if (lane == 0) {
+        wg_pre[0] = ph;
+        wg_pre[1] = pu;
+        if (b == gridDim.x - 1) {  // every workgroup before this one has published: the totals
+          uint64_t* ctl = out.cursor;  // the pass's control block
+          const uint64_t ctr01 = ctl_read(ctl, kCtlCounters), ctr23 = ctl_read(ctl, kCtlCounters + 1);
+          const uint64_t total = ((uint64_t)pu + wg_u) << 4;
+          // the scan's part of the dense payload is bounded by the regions part of the
+          // arena (a tail pack appends the spill bytes behind it): re-run with larger regions
+          const bool over = total > out.spill_base;
+          uint64_t h[kHdrWords];
+          h[kHdrHits] = (uint64_t)ph + wg_h;
+          h[kHdrPayload] = total;
+          h[kHdrRouted] = (ctr01 & 0xFFFFFFFFu) + (ctr01 >> 32) + (ctr23 & 0xFFFFFFFFu) + (ctr23 >> 32);
+          h[kHdrExactRetries] = 0;
+          if (over) atomicAdd(out.arena_retries, 1ull);  // also seen by a later tail pack's header
+          h[kHdrArenaRetries] = ctl_read(ctl, kCtlArenaRetries);
+          h[kHdrCursor] = 0;
+          h[kHdrPass] = out.pass_id;
+          h[kHdrRegionNeed] = ctl_read(ctl, kCtlRegionNeed);
+          write_header(out.hdr, out.hdr_host, h);
         }
-      ph += (uint32_t)v;
-      pu += (uint32_t)(v >> 32) & 0x7FFFFFFFu;
-    }
-    ph = wave_sum32(ph);
-    pu = wave_sum32(pu);
-    if (lane == 0) {
-      wg_pre[0] = ph;
-      wg_pre[1] = pu;
-      if (b == gridDim.x - 1) {  // every workgroup before this one has published: the totals
-        uint64_t* ctl = out.cursor;  // the pass's control block
-        const uint64_t ctr01 = ctl_read(ctl, kCtlCounters), ctr23 = ctl_read(ctl, kCtlCounters + 1);
-        uint64_t h[kHdrWords];
-        h[kHdrHits] = (uint64_t)ph + wg_h;
-        h[kHdrPayload] = ((uint64_t)pu + wg_u) << 4;
-        h[kHdrRouted] = (ctr01 & 0xFFFFFFFFu) + (ctr01 >> 32) + (ctr23 & 0xFFFFFFFFu) + (ctr23 >> 32);
-        h[kHdrExactRetries] = 0;
-        h[kHdrArenaRetries] = ctl_read(ctl, kCtlArenaRetries);
-        h[kHdrCursor] = 0;
-        h[kHdrPass] = out.pass_id;
-        h[kHdrRegionNeed] = ctl_read(ctl, kCtlRegionNeed);
-        write_header(out.hdr, out.hdr_host, h);
       }
     }
+    __syncthreads();
+    uint32_t eh = 0, eu = 0;
+    for (uint32_t k = 0; k < w_in; ++k) {
+      eh += wg_part[k].x;
+      eu += wg_part[k].y;
+    }
+    hbase = (uint64_t)wg_pre[0] + eh;
+    pbase = ((uint64_t)wg_pre[1] + eu) << 4;
   }
-  __syncthreads();
-  // each wave: its scan wave's dense records, then its payload region (data
-  // this wave wrote itself: served from this XCD's L2)
-  uint32_t eh = 0, eu = 0;
-  for (uint32_t k = 0; k < w_in; ++k) {
-    eh += wg_part[k].x;
-    eu += wg_part[k].y;
-  }
-  const uint64_t hbase = (uint64_t)wg_pre[0] + eh, pbase = ((uint64_t)wg_pre[1] + eu) << 4;
+  // ---- the wave's hit records -> result: payload bytes from the LDS pair
+  // list (one dword store per record, pair_store), dense 16-B records (fused)
+  // or the k_result_pack records in place
+  const bool write_pay = out.fused ? pbase + pay <= out.spill_base : fits;
+  uint8_t* pdst = out.fused ? out.dense : out.payload;
+  uint2* rec = (uint2*)(wl + out.work_region);  // record k at rec[-1 - k]
   uint64_t run = pbase;
-  const uint2* rec = hits + 1;  // record k at rec[-1 - k]
-  const uint32_t nh_copy = (out.dbg & 1) ? 0 : n_hit, u_copy = (out.dbg & 2) ? 0 : units;
+  const uint32_t nh_copy = (out.dbg & 1) ? 0 : n_hit;
   for (uint32_t k0 = 0; k0 < nh_copy; k0 += 64) {
     const uint32_t k = k0 + lane;
-    run = pack_hits(out.hits_out + hbase, k, n_hit, k < n_hit ? *(rec - 1 - k) : make_uint2(0, 0), run);
+    const bool live = k < n_hit;
+    const uint2 rr = live ? *(rec - 1 - k) : make_uint2(0, 0);
+    const uint32_t cnt = rr.y >> 16, first = rr.y & 0xFFFFu;
+    const bool some = live && cnt <= q.cap32;
+    const uint32_t pb = some ? pair_bytes(pl, first, cnt) + 2u : 0u;
+    const uint32_t incl = wave_incl_scan32(pb);
+    const uint64_t off = run + (incl - pb);
+    if (pb && write_pay && !(out.dbg & 2)) pair_store(pl, first, cnt, pdst + off);
+    if (live) {
+      if (out.fused) {
+        const uint64_t word = some ? off : (uint64_t)cnt;  // OVERFLOW: the exact count, no payload
+        out.hits_out[hbase + k] = make_uint4(rr.x, cnt, (uint32_t)word, (uint32_t)(word >> 32));
+      } else {
+        *(rec - 1 - k) = make_uint2(rr.x, cnt | (pb << 16));
+      }
+    }
+    run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   }
-  const uint4* src = (const uint4*)(out.payload + region0);
-  uint4* dst = (uint4*)(out.dense + pbase);
-  for (uint32_t c = lane; c < u_copy; c += 64) dst[c] = src[c];
 }
 
 // Tables without the pair list (uploaded tables, literal-sweep rows): every
@@ -1752,7 +1787,7 @@ constexpr int kPackPay = 2;  // 16-B payload pieces per lane in the first round
 __global__ __launch_bounds__(1024, 8) void k_result_pack(PackArgs p) {  // 2 blocks per CU
   const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
   const int b = blockIdx.x;
-  const bool scan_part = b < p.n_wg;
+  const bool scan_part = b < p.n_wg && !p.scan_packed;  // a fused scan placed its own part already
   const uint64_t w = (uint64_t)b * 16 + wv;  // wave-uniform: region bases stay in SGPRs
   // ---- round 1: issue every load (no barrier: each wave sums the workgroup
   // tallies itself, 8 B per scan workgroup from L2)
@@ -1797,7 +1832,11 @@ __global__ __launch_bounds__(1024, 8) void k_result_pack(PackArgs p) {  // 2 blo
   pu = wave_sum32(pu);
   th = wave_sum32(th);
   tu = wave_sum32(tu);
-  const uint64_t tb = (uint64_t)tu << 4;  // scan payload bytes (16-B pieces)
+  uint64_t tb = (uint64_t)tu << 4;  // scan payload bytes (16-B pieces)
+  if (p.scan_packed) {  // the fused scan's totals (its header, read by the host)
+    th = (uint32_t)p.scan_hits;
+    tb = p.scan_bytes;
+  }
   if (p.dbg & 8) {
     if (b == 0 && t == 0) p.hdr[0] = th + pu + ph + tu + r0.x + r1.x + r2.x + r3.x + pay0.x + pay1.x;
     return;
