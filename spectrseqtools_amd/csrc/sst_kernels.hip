@@ -1384,7 +1384,8 @@ __device__ __forceinline__ uint64_t ctl_read(uint64_t* ctl, int k) {  // counter
 // for the next tile's inputs be exact: the in-order counter then never makes
 // a tile wait for the stores of the tile just before it.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-constexpr uint32_t kBufSkip = 0x80000000u;  // an offset past every buffer the scan addresses
+constexpr uint32_t kBufSkip = 0x80000000u;
+constexpr int kPreChunks = 4;  // hit-record chunks a scan wave prepares before its look-back wait  // an offset past every buffer the scan addresses
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
 }
@@ -1574,6 +1575,26 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
       __hip_atomic_store(out.agg + blockIdx.x, (1ull << 63) | ((uint64_t)wg_u << 32) | wg_h, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
+  // The first kPreChunks x 64 hit records, their payload sizes (LDS) and
+  // wave-relative offsets are taken after this workgroup published its totals and before its
+  // look-back, so that this work overlaps the wait for the workgroups before this one
+  const uint2* rec = (const uint2*)(wl + out.work_region);  // record k at rec[-1 - k]
+  const uint32_t nh_copy = (out.dbg & 1) ? 0 : n_hit;
+  uint2 rr[kPreChunks];
+  uint32_t pbv[kPreChunks], inclv[kPreChunks], rel[kPreChunks + 1];
+  rel[0] = 0;
+#pragma unroll
+  for (int c = 0; c < kPreChunks; ++c) {
+    const uint32_t k = c * 64 + lane;
+    rr[c] = k < nh_copy ? *(rec - 1 - k) : make_uint2(0, 0);
+  }
+#pragma unroll
+  for (int c = 0; c < kPreChunks; ++c) {
+    const uint32_t k = c * 64 + lane, cnt = rr[c].y >> 16;
+    pbv[c] = (k < nh_copy && cnt <= q.cap32) ? pair_bytes(pl, rr[c].y & 0xFFFFu, cnt) + 2u : 0u;
+    inclv[c] = wave_incl_scan32(pbv[c]);
+    rel[c + 1] = rel[c] + (uint32_t)__builtin_amdgcn_readlane((int)inclv[c], 63);
+  }
   uint64_t hbase = 0, pbase = region0;
   if (out.fused) {
     // Wave 0 sums the aggregates of the workgroups before this one (decoupled
@@ -1589,7 +1610,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
           for (;;) {
             v = __hip_atomic_load(out.agg + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (v >> 63) break;
-            __builtin_amdgcn_s_sleep(16);
+            __builtin_amdgcn_s_sleep(4);
           }
         ph += (uint32_t)v;
         pu += (uint32_t)(v >> 32) & 0x7FFFFFFFu;
@@ -1634,27 +1655,29 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   // or the k_result_pack records in place
   const bool write_pay = out.fused ? pbase + pay <= out.spill_base : fits;
   uint8_t* pdst = out.fused ? out.dense : out.payload;
-  uint2* rec = (uint2*)(wl + out.work_region);  // record k at rec[-1 - k]
-  uint64_t run = pbase;
-  const uint32_t nh_copy = (out.dbg & 1) ? 0 : n_hit;
-  for (uint32_t k0 = 0; k0 < nh_copy; k0 += 64) {
-    const uint32_t k = k0 + lane;
-    const bool live = k < n_hit;
-    const uint2 rr = live ? *(rec - 1 - k) : make_uint2(0, 0);
-    const uint32_t cnt = rr.y >> 16, first = rr.y & 0xFFFFu;
-    const bool some = live && cnt <= q.cap32;
-    const uint32_t pb = some ? pair_bytes(pl, first, cnt) + 2u : 0u;
-    const uint32_t incl = wave_incl_scan32(pb);
-    const uint64_t off = run + (incl - pb);
+  auto emit = [&](uint32_t k, uint2 r, uint32_t pb, uint64_t off) {
+    const uint32_t cnt = r.y >> 16, first = r.y & 0xFFFFu;
     if (pb && write_pay && !(out.dbg & 2)) pair_store(pl, first, cnt, pdst + off);
-    if (live) {
+    if (k < n_hit) {
       if (out.fused) {
-        const uint64_t word = some ? off : (uint64_t)cnt;  // OVERFLOW: the exact count, no payload
-        out.hits_out[hbase + k] = make_uint4(rr.x, cnt, (uint32_t)word, (uint32_t)(word >> 32));
+        const uint64_t word = pb ? off : (uint64_t)cnt;  // OVERFLOW: the exact count, no payload
+        out.hits_out[hbase + k] = make_uint4(r.x, cnt, (uint32_t)word, (uint32_t)(word >> 32));
       } else {
-        *(rec - 1 - k) = make_uint2(rr.x, cnt | (pb << 16));
+        *((uint2*)rec - 1 - k) = make_uint2(r.x, cnt | (pb << 16));
       }
     }
+  };
+#pragma unroll
+  for (int c = 0; c < kPreChunks; ++c)
+    if (c * 64 < nh_copy) emit(c * 64 + lane, rr[c], pbv[c], pbase + rel[c] + (inclv[c] - pbv[c]));
+  uint64_t run = pbase + rel[kPreChunks];
+  for (uint32_t k0 = kPreChunks * 64; k0 < nh_copy; k0 += 64) {
+    const uint32_t k = k0 + lane;
+    const uint2 r = k < n_hit ? *(rec - 1 - k) : make_uint2(0, 0);
+    const uint32_t cnt = r.y >> 16;
+    const uint32_t pb = (k < n_hit && cnt <= q.cap32) ? pair_bytes(pl, r.y & 0xFFFFu, cnt) + 2u : 0u;
+    const uint32_t incl = wave_incl_scan32(pb);
+    emit(k, r, pb, run + (incl - pb));
     run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   }
 }
