@@ -222,6 +222,18 @@ int sst_length_bound_batch(sst_table* t, const double* su_mass, const double* ob
                            double precision, int max_len, int64_t max_mods, int direction, int64_t* out,
                            int8_t* status);
 
+/* ---- query producers (host code, no device) --------------------------- */
+/* The sliding window of collect_explanations_per_side
+ * (spectrseqtools/prediction.py:286-329) over many sides at once: side j is
+ * su[offsets[j] .. offsets[j+1]) (SU masses sorted ascending); every (start,
+ * end) pair whose difference the reference explains, in its order (including
+ * its quirk: once `end` reaches the last fragment, later starts pair only with
+ * it until a difference exceeds max_weight), as indices into su.  cap: room in
+ * start_out / end_out; the return value is the number of pairs (> cap: nothing
+ * beyond cap written, call again with more room) or a negative SST_E* code. */
+int64_t sst_window_pairs(const double* su, const int64_t* offsets, int64_t n_sides, double max_weight,
+                         int64_t* start_out, int64_t* end_out, int64_t cap);
+
 /* ---- measurement ------------------------------------------------------ */
 /* Kernel ids for sst_profile_read. */
 #define SST_K_IS_VALID 0

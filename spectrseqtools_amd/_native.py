@@ -27,6 +27,7 @@ EXPORTS = (
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
     "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
+    "sst_window_pairs",
 )
 
 # kernel ids of sst_profile_read
@@ -115,6 +116,8 @@ def load_library(path=LIB_PATH):
     lib.sst_explain_recursion_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _U64, _PP]
     lib.sst_is_singleton_batch.argtypes = [_P, _P, _I, _P, _P, _I64, _D, _D, _P]
     lib.sst_is_singleton_batch_device.argtypes = [_P, _P, _I, _P, _P, _I64, _D, _D, _P]
+    lib.sst_window_pairs.argtypes = [_P, _P, _I64, _D, _P, _P, _I64]
+    lib.sst_window_pairs.restype = _I64
     return lib
 
 
@@ -132,6 +135,25 @@ def lib():
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def window_pairs(su, offsets, max_weight):
+    """sst_window_pairs: the (start, end) index pairs of the reference's
+    sliding window (prediction.py:286-329) over every side su[offsets[j]:
+    offsets[j+1]] (host code in libsstgpu.so; no device needed)."""
+    su = np.ascontiguousarray(su, dtype=np.float64)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    L = lib()
+    cap = max(16, 4 * len(su))
+    while True:
+        s = np.empty(cap, np.int64)
+        e = np.empty(cap, np.int64)
+        k = L.sst_window_pairs(_ptr(su), _ptr(offsets), len(offsets) - 1, float(max_weight), _ptr(s), _ptr(e), cap)
+        if k < 0:
+            raise EngineError(f"sst_window_pairs failed ({k})")
+        if k <= cap:
+            return s[:k], e[:k]
+        cap = int(k)
 
 
 _DT = {4: np.uint8, 8: np.uint16, 16: np.uint32, 32: np.uint64}

@@ -1472,3 +1472,41 @@ int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, in
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Query producers (host): the sliding window of collect_explanations_per_side
+// (prediction.py:286-329), the same state machine over every side.
+// ---------------------------------------------------------------------------
+int64_t sst_window_pairs(const double* su, const int64_t* offsets, int64_t n_sides, double max_weight,
+                         int64_t* start_out, int64_t* end_out, int64_t cap) {
+  if (n_sides < 0 || (n_sides > 0 && (!su || !offsets)) || cap < 0 || (cap > 0 && (!start_out || !end_out)))
+    return SST_E_ARG;
+  int64_t k = 0;
+  for (int64_t j = 0; j < n_sides; ++j) {
+    const int64_t b = offsets[j], n = offsets[j + 1] - offsets[j];
+    if (n < 0) return SST_E_ARG;
+    int64_t start = 0, end = 1;
+    while (end < n) {
+      if (end - start <= 0) {  // :297-300
+        ++end;
+        continue;
+      }
+      const double diff = su[b + end] - su[b + start];  // :303
+      if (diff > max_weight) {  // :306-309
+        ++start;
+        end = start + 1;
+        continue;
+      }
+      if (k < cap) {
+        start_out[k] = b + start;
+        end_out[k] = b + end;
+      }
+      ++k;
+      if (end == n - 1)  // :324-327
+        ++start;
+      else
+        ++end;
+    }
+  }
+  return k;
+}

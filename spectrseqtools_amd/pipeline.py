@@ -1,0 +1,194 @@
+"""Columnar, many-spectrum form of the prediction pipeline's explanation
+stages (SURVEY config 5), on the GPU engine.
+
+The reference runs its pipeline one spectrum at a time and one query at a
+time (cli.py:192-207 -> classify_fragments, Predictor.predict).  Here the
+stages that issue hot-path queries run over a whole batch of spectra at once,
+in flat arrays (spectrum id per row) instead of per-spectrum frames:
+
+  1. classify   (fragment_classification.py:17-101): every peak x breakage
+                 weight -> one is_valid batch, valid rows -> one is_singleton
+                 batch, then the intensity / mass / sequence-mass filters and
+                 the per-spectrum SU-mass sort (lexsort);
+  2. su_diffs   (prediction.py:261-329, the first filter_by_explanation
+                 round): every side's sliding-window pairs (sst_window_pairs,
+                 host-native) and the singleton masses -> one explain batch;
+  3. bins       (skeleton_building.py:114-196, 372-421): every side's bins
+                 (neighbouring SU differences within tolerance) and the
+                 speculative bin-pair queries -> one explain batch; the first
+                 bin of a side explains whole fragment masses (deep windows:
+                 the engine's deferred DFS kernels).
+
+Every stage's rows equal what the per-spectrum mirrors produce
+(tests/test_pipeline.py).  Budgets follow each spectrum's max_len (the cli
+derives it from the sequence mass, cli.py:158-177): spectra are grouped by
+max_len and each group is one engine call with that group's row caps.
+Alphabet reduction (a per-spectrum table rebuild) and the MILP are not
+batched stages.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._native import window_pairs
+from .masses import MATCHING_THRESHOLD, PHOSPHATE_LINK_MASS, TOLERANCE
+
+MAX_VARIANCE = 1  # fragment_classification.py:8
+
+
+@dataclass
+class Classified:
+    """classify_fragments' rows of all spectra, spectrum-major, each spectrum
+    sorted by SU mass (its frame's row order)."""
+    spec: np.ndarray        # spectrum id
+    su: np.ndarray          # standard_unit_mass
+    obs: np.ndarray         # observed_mass
+    frag: np.ndarray        # fragment_index (peak position within its spectrum)
+    brk: np.ndarray         # breakage code: index into `names`
+    singleton: np.ndarray   # is_singleton
+    names: list             # breakage label per code
+    offsets: np.ndarray     # [S+1] row ranges per spectrum
+    n_valid_queries: int    # is_valid queries issued
+    n_singleton_queries: int
+
+
+def max_len_of(su_seq, precision=TOLERANCE, min_int_mass=None):
+    """cli.py:158-170: int(su_mass / precision / min(integer masses with rate > 0))."""
+    return (np.asarray(su_seq, dtype=np.float64) / precision / min_int_mass).astype(np.int64)
+
+
+def classify(obs, offsets, su_seq, dp_table, breakage_dict, intensity=None, intensity_cutoff=0.5e6,
+             mass_cutoff=50000):
+    """Stage 1 over S spectra: obs[offsets[s]:offsets[s+1]] are spectrum s's
+    observed masses; su_seq[s] its SU sequence mass (dp_table.seq.su_mass of
+    its own pipeline run)."""
+    from .fragment_classification import is_singletons
+    from .mass_explanation import is_valid_masses
+
+    obs = np.asarray(obs, dtype=np.float64)
+    offsets = np.asarray(offsets, dtype=np.int64)
+    S = len(offsets) - 1
+    n_peaks = np.diff(offsets)
+    spec_p = np.repeat(np.arange(S), n_peaks)
+    frag_p = np.arange(len(obs)) - offsets[spec_p]
+    inten = (np.full(len(obs), intensity_cutoff * 1.1) if intensity is None
+             else np.asarray(intensity, dtype=np.float64))
+    weights = list(breakage_dict.keys())
+    names = [breakage_dict[w][0] for w in weights]
+    B = len(weights)
+    # breakage-major within each spectrum (the reference's pl.concat order)
+    spec = np.tile(spec_p, B)
+    frag = np.tile(frag_p, B)
+    brk = np.repeat(np.arange(B), len(obs))
+    ob = np.tile(obs, B)
+    su = ob - np.repeat(np.asarray(weights, dtype=np.float64) * dp_table.precision, len(obs))
+    valid = is_valid_masses(su, dp_table, thresholds=dp_table.tolerance * ob)
+    keep = np.flatnonzero(valid)
+    sing = is_singletons(su[keep], [m.mass for m in dp_table.masses], dp_table,
+                         thresholds=dp_table.tolerance * ob[keep]) if len(keep) else np.zeros(0, bool)
+    # filters (:84-95), then per spectrum: SU order, ties in concat order
+    it = np.tile(inten, B)[keep]
+    full = np.array([("START" in n) and ("END" in n) for n in names], dtype=bool)[brk[keep]]
+    seq = np.asarray(su_seq, dtype=np.float64)[spec[keep]]
+    ok = (it > intensity_cutoff) & (ob[keep] < mass_cutoff) & (su[keep] < seq + MAX_VARIANCE) & \
+         ((su[keep] > seq - MAX_VARIANCE) | ~full)
+    rows, sing = keep[ok], sing[ok]
+    # the expanded position orders each spectrum's rows as its own concat (breakage, fragment)
+    order = np.lexsort((rows, su[rows], spec[rows]))
+    rows, sing = rows[order], sing[order]
+    off = np.searchsorted(spec[rows], np.arange(S + 1))
+    return Classified(spec[rows], su[rows], ob[rows], frag[rows], brk[rows], sing, names, off, len(su), len(keep))
+
+
+def _sides(c: Classified, side):
+    """Rows of one side per spectrum (SU order kept): row ids and offsets."""
+    m = np.array([side in n for n in c.names], dtype=bool)[c.brk]
+    rows = np.flatnonzero(m)
+    return rows, np.searchsorted(c.spec[rows], np.arange(len(c.offsets)))
+
+
+@dataclass
+class Queries:
+    diff: np.ndarray
+    thr: np.ndarray
+    spec: np.ndarray
+    kind: np.ndarray  # stage-specific tag (su_diffs: 0 START pair, 1 END pair, 2 singleton; bins: bin id)
+    side: np.ndarray = None  # bins: 0 START, 1 END
+
+
+def su_diff_queries(c: Classified, explanation_masses, tolerance=MATCHING_THRESHOLD):
+    """Stage 2's queries: per spectrum the START-side pairs, the END-side
+    pairs, then the singletons (collect_diff_explanations_for_su's order)."""
+    max_w = max(explanation_masses.get_column("monoisotopic_mass").to_list()) + PHOSPHATE_LINK_MASS
+    parts = []
+    for k, side in enumerate(("START", "END")):
+        rows, off = _sides(c, side)
+        s, e = window_pairs(c.su[rows], off, max_w)
+        a, b = rows[s], rows[e]
+        parts.append((c.su[b] - c.su[a], tolerance * (c.obs[a] + c.obs[b]), c.spec[a], np.full(len(a), k)))
+    sg = np.flatnonzero(c.singleton)
+    parts.append((c.su[sg], tolerance * c.obs[sg], c.spec[sg], np.full(len(sg), 2)))
+    spec = np.concatenate([p[2] for p in parts])
+    kind = np.concatenate([p[3] for p in parts])
+    order = np.lexsort((kind, spec))  # stable: pairs keep their window order
+    return Queries(np.concatenate([p[0] for p in parts])[order], np.concatenate([p[1] for p in parts])[order],
+                   spec[order], kind[order])
+
+
+def bin_queries(c: Classified, tolerance=MATCHING_THRESHOLD):
+    """Stage 3's speculative queries: per side, its bins as
+    SkeletonBuilder._predict_skeleton forms them, the first bin's whole
+    masses and every later bin against the bin before it (kind = the bin's
+    global id; bins of a spectrum's START side, then END side)."""
+    d_all, t_all, s_all, k_all, sd_all = [], [], [], [], []
+    bin_base = 0
+    for side_k, side in enumerate(("START", "END")):
+        rows, off = _sides(c, side)
+        su, ob = c.su[rows], c.obs[rows]
+        n = len(rows)
+        if n == 0:
+            continue
+        first = np.zeros(n, dtype=bool)
+        first[off[:-1][np.diff(off) > 0]] = True  # first row of each side
+        joins = np.zeros(n, dtype=bool)  # row i joins row i-1's bin
+        joins[1:] = (su[1:] - su[:-1]) <= tolerance * (ob[:-1] + ob[1:])
+        joins &= ~first
+        bin_id = np.cumsum(~joins) - 1  # a bin per run
+        nb = int(bin_id[-1]) + 1 if n else 0
+        # a bin is explained when a later row of its side closes it, or its last
+        # row is the side's last row and joined it (:150-153); the side's own
+        # first bin has no predecessor
+        last_of_side = np.zeros(n, dtype=bool)
+        last_of_side[off[1:][np.diff(off) > 0] - 1] = True
+        bstart = np.flatnonzero(~joins)
+        bend = np.append(bstart[1:], n)  # exclusive
+        closed = ~last_of_side[bend - 1] | (joins[bend - 1] & (bend - bstart > 1))
+        side_first = first[bstart]
+        # first bins: whole masses against 0.0
+        fb = np.flatnonzero(side_first & closed)
+        mem = np.concatenate([np.arange(bstart[b], bend[b]) for b in fb]) if len(fb) else np.zeros(0, np.int64)
+        d_all.append(su[mem])
+        t_all.append(tolerance * (0.0 + ob[mem]))
+        s_all.append(c.spec[rows[mem]])
+        k_all.append(bin_base + bin_id[mem])
+        sd_all.append(np.full(len(mem), side_k))
+        # later bins against their predecessor: |prev| x |cur| pairs
+        lb = np.flatnonzero(~side_first & closed)
+        if len(lb):
+            psz = (bend - bstart)[lb - 1]
+            csz = (bend - bstart)[lb]
+            reps = psz * csz
+            tot = int(reps.sum())
+            grp = np.repeat(np.arange(len(lb)), reps)
+            local = np.arange(tot) - np.repeat(np.cumsum(reps) - reps, reps)
+            p = bstart[lb - 1][grp] + local // csz[grp]
+            q = bstart[lb][grp] + local % csz[grp]
+            d_all.append(su[q] - su[p])
+            t_all.append(tolerance * (ob[p] + ob[q]))
+            s_all.append(c.spec[rows[q]])
+            k_all.append(bin_base + bin_id[q])
+            sd_all.append(np.full(len(q), side_k))
+        bin_base += nb
+    cat = (lambda x: np.concatenate(x)) if d_all else (lambda x: np.zeros(0))
+    return Queries(cat(d_all), cat(t_all), cat(s_all).astype(np.int64), cat(k_all).astype(np.int64),
+                   cat(sd_all).astype(np.int8))

@@ -73,6 +73,14 @@ def sliding_window_pairs(su_sorted, max_weight):
     return pairs
 
 
+def window_pairs(su_sorted, max_weight):
+    """sliding_window_pairs as index arrays, by the library's host-native
+    producer (sst_window_pairs)."""
+    from ._native import window_pairs as _wp
+
+    return _wp(su_sorted, [0, len(su_sorted)], max_weight)
+
+
 def diff_queries(su_sorted, obs_sorted, tolerance, max_weight):
     """Adjacent-difference explain queries of one side (prediction.py:286-329):
     diff = su[end] - su[start], threshold = tolerance*(obs[start]+obs[end])

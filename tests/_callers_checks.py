@@ -1,0 +1,172 @@
+"""Parity checks of the callers' mirrors (classify_fragments, Predictor,
+SkeletonBuilder) against the reference-run fixtures; shared by the CPU suite
+(oracle-backed tables, tests/_fake_engine.py) and the GPU suite (the HIP
+engine).  TEST INFRASTRUCTURE."""
+import numpy as np
+
+from spectrseqtools_amd.frame import Frame
+from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+from spectrseqtools_amd.masses import EXPLANATION_MASSES, build_breakage_dict
+
+
+def make_dp(ctx, engine=None):
+    seq = SequenceInformation(max_len=ctx["max_len"], su_mass=ctx["su_mass"], obs_mass=ctx["obs_mass"],
+                              modification_rate=ctx["mod_rate"])
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=ctx["tolerance"],
+                                 precision=ctx["precision"], seq=seq, engine=engine)
+    assert [m.mass for m in dp.masses] == ctx["masses"]
+    return dp
+
+
+def frame_of(d):
+    return Frame({c: [r[i] for r in d["rows"]] for i, c in enumerate(d["columns"])})
+
+
+def check_classify(rec, dp):
+    from spectrseqtools_amd.fragment_classification import classify_fragments
+
+    bd = build_breakage_dict(*rec["tags"])
+    got = classify_fragments(frame_of(rec["input"]), dp, bd, intensity_cutoff=rec["intensity_cutoff"])
+    want = rec["classify"]
+    assert got.columns == want["columns"]
+    rows = [list(r) for r in got.rows()]
+    assert len(rows) == len(want["rows"])
+    for a, b in zip(rows, want["rows"]):
+        assert a == b, (a, b)
+    return got
+
+
+def prepared(classified):
+    """Predictor.predict's framing (prediction.py:68-80)."""
+    f = classified.with_row_index("orig_index").sort("standard_unit_mass").with_row_index("index")
+    return f.with_columns(min_end=[0] * len(f), max_end=[-1] * len(f))
+
+
+def rows_of_expl(dp, expl):
+    """Explanation list -> sorted row-index tuples of dp's alphabet."""
+    if expl is None:
+        return None
+    idx = {}
+    for i, m in enumerate(dp.masses):
+        for n in m.names:
+            idx[n] = i
+    return sorted(tuple(sorted(idx[n] for n in e.nucleosides)) for e in expl)
+
+
+def check_filter(rec, dp):
+    from spectrseqtools_amd.prediction import Predictor
+
+    pred = Predictor(dp, EXPLANATION_MASSES)
+    frags, expl = pred.filter_by_explanation(prepared(frame_of(rec["classify"])))
+    last = rec["filter"]["rounds"][-1]
+    assert [m.mass for m in dp.masses] == last["masses"]
+    assert frags.get_column("index").to_list() == last["kept_index"]
+    want = rec["filter"]["explanations"]
+    assert sorted(map(repr, expl)) == sorted(want)
+    for k, v in expl.items():
+        w = want[repr(k)]
+        assert rows_of_expl(dp, v) == (None if w is None else sorted(tuple(x) for x in w)), k
+    return frags, expl
+
+
+def predict_skeleton_sequential(builder, fragments, skeleton_seq):
+    """skeleton_building.py:114-196 restated literally (one
+    explain_bin_differences call per bin): the reference's loop the batched
+    SkeletonBuilder._predict_skeleton must reproduce."""
+    from spectrseqtools_amd.common import calculate_error_threshold
+
+    pos = {0}
+    last_valid_bin = None
+    invalid_list = []
+    current_bin = [0]
+    n = len(fragments)
+    for frag_idx in range(1, n):
+        if len(pos) == 0:
+            invalid_list.append(fragments.item(frag_idx, "index"))
+            continue
+        neighbour_diff = fragments.item(frag_idx, "standard_unit_mass") - fragments.item(frag_idx - 1,
+                                                                                          "standard_unit_mass")
+        neighbour_threshold = calculate_error_threshold(fragments.item(frag_idx - 1, "observed_mass"),
+                                                        fragments.item(frag_idx, "observed_mass"),
+                                                        builder.dp_table.tolerance)
+        if neighbour_diff <= neighbour_threshold:
+            current_bin.append(frag_idx)
+            if frag_idx + 1 < n:
+                continue
+        explanations = builder.explain_bin_differences(prev_bin=last_valid_bin, current_bin=current_bin,
+                                                       fragments=fragments)
+        if explanations is None:
+            for idx in current_bin:
+                invalid_list.append(fragments.item(idx, "index"))
+        else:
+            pos, skeleton_seq = builder.update_skeleton_for_given_explanations(explanations=explanations, pos=pos,
+                                                                               skeleton_seq=skeleton_seq)
+            for idx in current_bin:
+                fragments[idx, "min_end"] = min(pos, default=1)
+                fragments[idx, "max_end"] = max(pos, default=0)
+            last_valid_bin = current_bin
+        current_bin = [frag_idx]
+    keep = [i for i in range(n) if fragments.item(i, "index") not in set(invalid_list)]
+    return skeleton_seq, fragments.take(keep)
+
+
+def check_skeleton(dp, frags, expl):
+    """Batched _predict_skeleton == the literal loop, per side, with the same
+    answers (both use this engine's explain)."""
+    from spectrseqtools_amd.skeleton_building import SkeletonBuilder
+
+    calls = []
+    for side in ("START", "END"):
+        sub = frags.filter_mask([side in b for b in frags.get_column("breakage").to_list()])
+        b1 = SkeletonBuilder(explanations=expl, dp_table=dp)
+        sk1, f1 = b1._predict_skeleton(Frame(sub.to_dict()), [set() for _ in range(dp.seq.max_len)])
+        b2 = SkeletonBuilder(explanations=expl, dp_table=dp)
+        sk2, f2 = predict_skeleton_sequential(b2, Frame(sub.to_dict()), [set() for _ in range(dp.seq.max_len)])
+        assert sk1 == sk2, side
+        assert f1.to_dict() == f2.to_dict(), side
+        calls.append((b1.engine_calls, b2.engine_calls))
+    return calls
+
+
+def check_per_side(pop, ctx_id, dp):
+    """Predictor.collect_explanations_per_side on the START and END fragments
+    of a reference test spectrum (classified here) == the dict the reference
+    builds from its own answers (population.json.gz, queries in order: START
+    side, then END side; {**start, **end} keeps that order and overwrite)."""
+    from spectrseqtools_amd.fragment_classification import classify_fragments
+    from spectrseqtools_amd.prediction import Predictor
+
+    sp = pop["contexts"][ctx_id]["spectrum"]
+    cols = {"observed_mass": sp["observed"]}
+    if sp["intensity"][0] is not None:
+        cols["intensity"] = sp["intensity"]
+    bd = build_breakage_dict(*sp["tags"])
+    fr = classify_fragments(Frame(cols), dp, bd, intensity_cutoff=sp["intensity_cutoff"])
+    pred = Predictor(dp, EXPLANATION_MASSES)
+    got = {}
+    for side in ("START", "END"):
+        sub = fr.filter_mask([side in b for b in fr.get_column("breakage").to_list()])
+        got = {**got, **pred.collect_explanations_per_side(sub)}
+    want = {}
+    for rec in pop["a8"]:
+        if rec[0] == ctx_id and rec[4] is not None and len(rec[4]) >= 1:
+            want[rec[1]] = sorted(tuple(x) for x in rec[4])
+    assert list(got) == list(want)
+    for k, v in got.items():
+        assert rows_of_expl(dp, v) == want[k], k
+    return len(want)
+
+
+def check_classify_batch(recs, dps_by_ctx):
+    """classify_fragments_batch == per-spectrum classify_fragments for spectra
+    sharing one table (grouped by context)."""
+    from spectrseqtools_amd.fragment_classification import classify_fragments, classify_fragments_batch
+
+    for cid, (dp, group) in dps_by_ctx.items():
+        bd = build_breakage_dict(*group[0]["tags"])
+        frames = [frame_of(r["input"]) for r in group]
+        cuts = [r["intensity_cutoff"] for r in group]
+        batch = classify_fragments_batch(frames, dp, bd, intensity_cutoff=cuts)
+        for f, c, b in zip(frames, cuts, batch):
+            assert classify_fragments(f, dp, bd, intensity_cutoff=c).to_dict() == b.to_dict()
+    return np.int64(0)

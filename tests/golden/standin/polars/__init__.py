@@ -1,6 +1,8 @@
 """Minimal pandas-backed stand-in for the subset of `polars` that the reference's
 hot-path modules (masses.py, mass_table.py, mass_explanation.py) touch at import
-time and in `DynamicProgrammingTable`.
+time and in `DynamicProgrammingTable`, plus the frame plumbing of
+fragment_classification.classify_fragments (lit, struct.map_elements, concat,
+with_row_index, rename, drop, comparisons, str.contains).
 
 TEST INFRASTRUCTURE ONLY.  polars is not installed in this image and there is no
 network.  This module is put on sys.path solely by tests/golden/make_golden.py
@@ -51,6 +53,31 @@ class Expr:
     def __gt__(self, v):
         return self._map(lambda x: x > v)
 
+    def __lt__(self, v):
+        return self._map(lambda x: x < v)
+
+    def __and__(self, o):
+        return Expr(lambda df: self.fn(df) & o.fn(df), self.name)
+
+    def __or__(self, o):
+        return Expr(lambda df: self.fn(df) | o.fn(df), self.name)
+
+    def __invert__(self):
+        return self._map(lambda x: ~x)
+
+    @property
+    def str(self):
+        outer = self
+
+        class _Str:
+            def contains(self, pat):
+                return outer._map(lambda x: x.astype(str).str.contains(pat, regex=True))
+
+        return _Str()
+
+    def map_elements(self, fn, return_dtype=None):
+        return self._map(lambda rows: pd.Series([fn(r) for r in rows]))
+
     __hash__ = object.__hash__
 
     def alias(self, name):
@@ -76,6 +103,18 @@ class Expr:
 
 def col(name):
     return Expr(lambda df: df._d[name], name)
+
+
+def lit(value, dtype=None):
+    return Expr(lambda df: pd.Series([value] * len(df._d)), "literal")
+
+
+def struct(*names):
+    return Expr(lambda df: [dict(zip(names, r)) for r in df._d[list(names)].itertuples(index=False)], names[0])
+
+
+def concat(frames):
+    return DataFrame(pd.concat([f._d for f in frames], ignore_index=True))
 
 
 class Series(list):
@@ -132,8 +171,23 @@ class DataFrame:
     def with_columns(self, *exprs):
         d = self._d.copy()
         for e in exprs:
-            d[e.name] = e.fn(self).values
+            v = e.fn(self)
+            d[e.name] = v.values if hasattr(v, "values") else v
         return DataFrame(d)
+
+    def with_row_index(self, name="index"):
+        d = self._d.copy()
+        d.insert(0, name, range(len(d)))
+        return DataFrame(d)
+
+    def rename(self, mapping):
+        return DataFrame(self._d.rename(columns=mapping))
+
+    def drop(self, name):
+        return DataFrame(self._d.drop(columns=[name]))
+
+    def write_csv(self, path, separator=","):
+        self._d.to_csv(path, sep=separator, index=False)
 
     def group_by(self, key, maintain_order=True):
         return _GroupBy(self, key)
@@ -156,10 +210,10 @@ class DataFrame:
         return DataFrame(self._d.merge(other._d, on=on, how=how))
 
     def filter(self, e):
-        return DataFrame(self._d[e.fn(self).values])
+        return DataFrame(self._d[np.asarray(e.fn(self), dtype=bool)])
 
     def sort(self, c):
-        return DataFrame(self._d.sort_values(c, kind="stable"))
+        return DataFrame(self._d.sort_values(c.name if isinstance(c, Expr) else c, kind="stable"))
 
     def __len__(self):
         return len(self._d)

@@ -1,0 +1,113 @@
+"""CPU suite for the hot path's callers (A12 calculate_explanations, A14
+classify_fragments / Predictor / SkeletonBuilder mirrors), with the device
+tables routed to the CPU oracle (tests/_fake_engine.py) so the host logic is
+checked without a GPU.  The same checks run on the HIP engine in
+tests/test_gpu_callers.py.  Fixtures: tests/golden/callers.json.gz (the
+reference's own classify_fragments output and filter_by_explanation results,
+make_callers_golden.py) and population.json.gz (the reference's answers to
+the sliding-window queries)."""
+import gc
+
+import pytest
+
+import _callers_checks as C
+import _fake_engine
+from conftest import load_golden
+from spectrseqtools_amd import common
+from spectrseqtools_amd.common import Explanation, calculate_error_threshold, calculate_explanations
+
+SPECTRA = ["test_01", "test_02", "test_03", "test_04", "test_05", "test_06", "test_07", "test_08"]
+
+
+@pytest.fixture(scope="module")
+def callers():
+    return load_golden("callers.json.gz")
+
+
+@pytest.fixture()
+def fake(monkeypatch):
+    _fake_engine.install(monkeypatch)
+    yield
+    gc.collect()
+
+
+def test_calculate_error_threshold(monkeypatch):
+    """common.py:37-44: l1 (the live method), l2, anything else raises."""
+    assert calculate_error_threshold(1000.0, 2000.0, 1e-5) == 1e-5 * (1000.0 + 2000.0)
+    monkeypatch.setattr(common, "ERROR_METHOD", "l2_norm")
+    assert calculate_error_threshold(3.0, 4.0, 0.5) == 0.5 * 5.0
+    monkeypatch.setattr(common, "ERROR_METHOD", "other")
+    with pytest.raises(NotImplementedError, match="This error method is not implemented."):
+        calculate_error_threshold(1.0, 1.0, 1.0)
+
+
+def test_explanation_value_semantics():
+    """common.py:20-35: nucleosides sorted; equality against tuples and
+    Explanations; no __hash__ (callers de-duplicate with `in` on lists)."""
+    e = Explanation("U", "C", "9A")
+    assert e.nucleosides == ("9A", "C", "U") and len(e) == 3 and list(e) == ["9A", "C", "U"]
+    assert repr(e) == "{9A,C,U}"
+    assert e == ("9A", "C", "U") and e == Explanation("C", "U", "9A") and not e == Explanation("C")
+    with pytest.raises(TypeError):
+        hash(e)
+
+
+@pytest.mark.parametrize("tc", ["test_01", "test_05"])
+def test_calculate_explanations_vs_population(fake, tc):
+    """calculate_explanations (common.py:47-65) and its batched form on the
+    reference's own sliding-window queries: None stays None, a set becomes a
+    list of Explanations naming the same compositions."""
+    pop = load_golden("population.json.gz")
+    cid = f"pop_{tc}"
+    dp = C.make_dp(pop["contexts"][cid])
+    recs = [r for r in pop["a8"] if r[0] == cid][:300]
+    batch = common.calculate_explanations_batch([r[1] for r in recs], [r[2] for r in recs], dp)
+    for r, b in zip(recs, batch):
+        one = calculate_explanations(r[1], r[2], dp)
+        want = None if r[4] is None else sorted(tuple(x) for x in r[4])
+        assert C.rows_of_expl(dp, one) == want
+        assert C.rows_of_expl(dp, b) == want
+        if one is not None:
+            assert all(isinstance(x, Explanation) for x in one)
+
+
+@pytest.mark.parametrize("tc", SPECTRA)
+def test_classify_fragments_matches_reference(fake, callers, tc):
+    """fragment_classification.classify_fragments: columns, row order and
+    values identical to the reference's own output on its test spectra."""
+    rec = callers[tc]
+    C.check_classify(rec, C.make_dp(rec["ctx"]))
+
+
+@pytest.mark.parametrize("tc", SPECTRA)
+def test_filter_by_explanation_matches_reference(fake, callers, tc):
+    """Predictor.filter_by_explanation: final alphabet, kept fragments and the
+    explanation dict (keys, None values, compositions) as the reference."""
+    rec = callers[tc]
+    C.check_filter(rec, C.make_dp(rec["ctx"]))
+
+
+@pytest.mark.parametrize("tc", ["test_01", "test_03", "test_07"])
+def test_collect_explanations_per_side_population(fake, tc):
+    pop = load_golden("population.json.gz")
+    cid = f"pop_{tc}"
+    assert C.check_per_side(pop, cid, C.make_dp(pop["contexts"][cid])) > 0
+
+
+@pytest.mark.parametrize("tc", ["test_01", "test_02", "test_06"])
+def test_predict_skeleton_batched_equals_loop(fake, callers, tc):
+    """SkeletonBuilder._predict_skeleton (speculative batch per side) gives
+    the reference loop's skeleton, end indices and rejected fragments."""
+    rec = callers[tc]
+    dp = C.make_dp(rec["ctx"])
+    frags, expl = C.check_filter(rec, dp)
+    calls = C.check_skeleton(dp, frags, expl)
+    assert all(b <= max(2, s) for b, s in calls), calls
+
+
+def test_classify_batch_equals_single(fake, callers):
+    groups = {}
+    for tc in ("test_01", "test_02"):
+        rec = callers[tc]
+        groups.setdefault(tc, (C.make_dp(rec["ctx"]), [rec]))
+    C.check_classify_batch(None, groups)

@@ -1,0 +1,86 @@
+"""CPU suite for the columnar many-spectrum stages (spectrseqtools_amd/
+pipeline.py, the config-5 harness tools/pipeline_bench.py): every stage's
+rows and queries equal what the per-spectrum mirrors (classify_fragments,
+Predictor, SkeletonBuilder -- pinned to the reference in test_callers.py)
+produce for each spectrum.  Device tables are oracle-backed
+(tests/_fake_engine.py)."""
+import numpy as np
+import pytest
+
+import _fake_engine
+from spectrseqtools_amd import pipeline
+from spectrseqtools_amd.fragment_classification import classify_fragments
+from spectrseqtools_amd.frame import Frame
+from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+from spectrseqtools_amd.masses import (EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict)
+from spectrseqtools_amd.prediction import Predictor, _side_mask
+from spectrseqtools_amd.skeleton_building import SkeletonBuilder
+from spectrseqtools_amd.synthetic import make_spectra
+
+
+@pytest.fixture(scope="module")
+def setup():
+    mp = pytest.MonkeyPatch()
+    _fake_engine.install(mp)
+    batch = make_spectra(24, seed=5)
+    bd = build_breakage_dict(555.1294, 455.1491)
+    w_full = [k for k, v in bd.items() if "START_END" in v][0]
+    su_seq = batch.seq_mass - w_full * TOLERANCE
+    seq = SequenceInformation(max_len=20, su_mass=float(su_seq[0]), obs_mass=float(batch.seq_mass[0]),
+                              modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq)
+    c = pipeline.classify(batch.observed, batch.offsets, su_seq, dp, bd)
+    frames = []
+    for s in range(len(su_seq)):
+        dp.seq.su_mass = float(su_seq[s])
+        obs = batch.observed[batch.offsets[s]:batch.offsets[s + 1]]
+        frames.append(classify_fragments(Frame({"observed_mass": obs.tolist()}), dp, bd))
+    yield batch, dp, c, frames
+    mp.undo()
+
+
+def test_classify_rows_equal_per_spectrum(setup):
+    batch, dp, c, frames = setup
+    for s, f in enumerate(frames):
+        r = slice(c.offsets[s], c.offsets[s + 1])
+        assert c.su[r].tolist() == f.get_column("standard_unit_mass").to_list()
+        assert c.obs[r].tolist() == f.get_column("observed_mass").to_list()
+        assert c.frag[r].tolist() == f.get_column("fragment_index").to_list()
+        assert [c.names[b] for b in c.brk[r]] == f.get_column("breakage").to_list()
+        assert c.singleton[r].tolist() == f.get_column("is_singleton").to_list()
+    assert c.offsets[-1] > 0
+
+
+def test_su_diff_queries_equal_per_spectrum(setup):
+    batch, dp, c, frames = setup
+    q = pipeline.su_diff_queries(c, EXPLANATION_MASSES)
+    pred = Predictor(dp, EXPLANATION_MASSES)
+    for s, f in enumerate(frames):
+        su = np.asarray(f.get_column("standard_unit_mass").to_list())
+        obs = np.asarray(f.get_column("observed_mass").to_list())
+        brk = f.get_column("breakage").to_list()
+        parts = [pred._side_queries(su[_side_mask(brk, side)], obs[_side_mask(brk, side)]) for side in ("START", "END")]
+        sing = np.asarray(f.get_column("is_singleton").to_list(), dtype=bool)
+        want_d = np.concatenate([parts[0][1], parts[1][1], su[sing]])
+        want_t = np.concatenate([parts[0][2], parts[1][2], MATCHING_THRESHOLD * obs[sing]])
+        m = q.spec == s
+        assert q.diff[m].tolist() == want_d.tolist()
+        assert q.thr[m].tolist() == want_t.tolist()
+
+
+def test_bin_queries_equal_per_spectrum(setup):
+    batch, dp, c, frames = setup
+    q = pipeline.bin_queries(c)
+    sk = SkeletonBuilder(explanations={}, dp_table=dp)
+    n_total = 0
+    for s, f in enumerate(frames):
+        for side_k, side in enumerate(("START", "END")):
+            sub = f.filter_mask([side in b for b in f.get_column("breakage").to_list()])
+            _, qs = sk.speculative_bin_queries(sub)
+            want = [(d, MATCHING_THRESHOLD * (pm + cm)) for ql in qs for (d, pm, cm) in ql]
+            m = (q.spec == s) & (q.side == side_k)
+            got = list(zip(q.diff[m].tolist(), q.thr[m].tolist()))
+            assert got == want, (s, side)
+            n_total += len(want)
+    assert n_total > 0
