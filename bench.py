@@ -170,6 +170,10 @@ def main():
                     help="diagnostic builds only: skip the result checks after the timed region")
     ap.add_argument("--no-events", action="store_true",
                     help="diagnostic: time the steps without the per-kernel HIP events (no roofline)")
+    ap.add_argument("--workload", default="config3", choices=("config3", "config1"),
+                    help="config3 (default): the headline A7 + A8 step; config1: whole-mass explain of random "
+                         "canonical <=8-mers on the canonical table (the deferred DFS kernels, SURVEY 8(d))")
+    ap.add_argument("--queries", type=int, default=200000, help="config1: queries per step per GPU")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/), reported as roofline.traffic")
     args = ap.parse_args()
@@ -197,6 +201,8 @@ def main():
             dist.init_process_group("gloo")
 
     engine = _native.get_engine(gpu)
+    if args.workload == "config1":
+        return main_config1(args, engine, dist, rank, world, dev_t)
     seq = SequenceInformation(max_len=20, su_mass=6500.0, obs_mass=6500.0, modification_rate=0.5)
     dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
                                  precision=TOLERANCE, seq=seq, engine=engine)
@@ -449,6 +455,157 @@ def main():
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+CONFIG1_TEST_SEQ = ["A", "AA", "GG", "CC", "UU", "CUAG", "CCUAGG"]  # tests/test_explain_masses.py:34-42
+CONFIG1_PPM = (10e-6, 5e-6, 2e-6)  # :51
+
+
+def config1_queries(n, seed):
+    """the reference test's 7 masses x 3 tolerances, then
+    random canonical 1..8-mers (masses as get_seq_weight, test_explain_masses.py:
+    16-31: round(len * PHOSPHATE_LINK_MASS + sum of monoisotopic masses, 5)),
+    tolerance cycling over the test's three; budget round(0.5 * len) (:92)."""
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, PHOSPHATE_LINK_MASS
+
+    mono = dict(zip(EXPLANATION_MASSES.get_column("nucleoside").to_list(),
+                    EXPLANATION_MASSES.get_column("monoisotopic_mass").to_list()))
+    seqs = [s for s in CONFIG1_TEST_SEQ for _ in CONFIG1_PPM]
+    ppm = [p for _ in CONFIG1_TEST_SEQ for p in CONFIG1_PPM]
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(1, 9, max(0, n - len(seqs)))
+    letters = np.array(list("ACGU"))
+    seqs += ["".join(letters[rng.integers(0, 4, L)]) for L in lens]
+    ppm += [CONFIG1_PPM[k % 3] for k in range(len(lens))]
+    mass = np.array([round(len(q) * PHOSPHATE_LINK_MASS + sum(mono[c] for c in q), 5) for q in seqs])
+    return mass, np.asarray(ppm) * mass, np.array([round(0.5 * len(q)) for q in seqs], dtype=np.int64)
+
+
+def main_config1(args, engine, dist, rank, world, dev_t):
+    """Config 1 step: one explain pass over whole canonical masses (windows of
+    up to 8 items: the scan routes them to the deferred DFS kernel), settled
+    inside the step (deferred launch + result pack), with inputs in HBM."""
+    import torch
+
+    from spectrseqtools_amd import _native
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, TOLERANCE, UNMODIFIED_BASES
+
+    seq = SequenceInformation(max_len=8, su_mass=0.0, obs_mass=0.0, modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=10e-6, precision=TOLERANCE,
+                                 seq=seq, engine=engine)
+    dp.adapt_individual_modification_rates_by_alphabet_reduction(set(UNMODIFIED_BASES))  # 5 x 377 397 table
+    tdev = dp.device_table
+    mass, thr, mods = config1_queries(args.queries, args.seed + rank * 1_000_003)
+    n = len(mass)
+    dm = torch.from_numpy(mass).to(dev_t)
+    dt = torch.from_numpy(thr).to(dev_t)
+    dmods = torch.from_numpy(mods).to(dev_t)
+    torch.cuda.synchronize()
+
+    def step(res):
+        res = tdev.explain_device(dm.data_ptr(), dt.data_ptr(), n, dp.tolerance, dp.precision, 0,
+                                  d_mods=dmods.data_ptr(), reuse=res)
+        res.settle()  # routed windows: the deferred DFS launch and the result pack, inside the step
+        return res
+
+    res = step(None)
+    res.fetch_device()
+    ref_st, ref_cnt = res.status.copy(), res.count.copy()
+    for k in range(args.warmup):
+        res = step(res)
+    engine.synchronize()
+    engine.profile(not args.no_events, kernels=(_native.K_EXPLAIN_SCAN, _native.K_EXPLAIN_DEEP,
+                                                 _native.K_RESULT_PACK), every=1)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        res = step(res)
+    engine.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = engine.profile_read() if not args.no_events else {}
+    engine.profile(False)
+    res.fetch_device()
+    if not (np.array_equal(res.status, ref_st) and np.array_equal(res.count, ref_cnt)):
+        raise RuntimeError("a timed config-1 step's result differs from the reference pass")
+    # parity sample against the CPU oracle (the checker, outside the timed region)
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle as oracle
+
+    ms = [m.mass for m in dp.masses]
+    table = oracle.build_table(ms, max(ms) * 35, 32)
+    alph = oracle.Alphabet(ms, [m.is_modification for m in dp.masses],
+                           [round(seq.max_len * m.modification_rate) for m in dp.masses])
+    sample = np.unique(np.concatenate([np.arange(min(n, 21)), np.random.default_rng(3).integers(0, n, 400)]))
+    for i in sample:
+        st, sols, n_empty, _ = oracle.explain_table(table, 32, alph, mass[i], thr[i], dp.tolerance, int(mods[i]))
+        if sorted(res.candidates(i)) != sorted(sols):
+            raise RuntimeError(f"config-1 query {i} differs from the oracle")
+    stats = res.stats()
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+    n_def = int(stats[1] + stats[2] + stats[3])
+    nodes = int(stats[4])
+    some = res.status == _native.SST_SOME
+    # algorithmic bytes of the deferred launch: each routed query's window
+    # bounds (16) and status byte, 16 B per index record the DFS loads, its
+    # payload and 16-B hit record per query with candidates
+    limit = tdev.n_cols * tdev.compression
+    _, hi, w = windows(mass, thr, dp.precision, limit)
+    pair = (w > 0) & (hi < 3 * min(m.mass for m in dp.masses if m.mass > 0))  # answered by the scan
+    if int(pair.sum()) != int(stats[6]):
+        raise RuntimeError(f"pair-path partition {int(pair.sum())} != engine counter {int(stats[6])}")
+    n_hit_def = int((some & ~pair).sum())
+    bytes_def = float(n_def * 17 + 16 * nodes + int(stats[5]) + 16 * n_hit_def)
+    kern = {}
+    for kid, (ms_, cnt) in prof.items():
+        kern[_native.KERNEL_NAMES[kid]] = {"avg_us": 1e3 * ms_ / cnt, "launches": cnt}
+    dus = kern.get("k_explain_deferred", {"avg_us": float("nan")})["avg_us"]
+    achieved = bytes_def / (dus * 1e-6) / 1e9
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        sub = np.arange(min(n, 20000))
+        out = {}
+        for threads in (oracle.LIB.ora_num_threads(), 1):
+            k = len(sub) if threads > 1 else min(len(sub), 4000)
+            t1 = time.perf_counter()
+            oracle.explain_batch(table, 32, alph, mass[:k], thr[:k], mods[:k], dp.tolerance, nthreads=threads)
+            dt_ = time.perf_counter() - t1
+            out[threads] = {"value": k / dt_, "unit": "peaks/s", "cores": threads, "kind": "port",
+                            "sample": f"first {k} config-1 queries, oracle/sst_oracle.c, {threads} thread(s), "
+                                      f"{dt_:.1f} s"}
+        cpu = out[max(out)]
+        cpu["single_core"] = out[1]
+        cpu["reference_python_single_core"] = {"value": 904.0, "unit": "peaks/s", "source": "BASELINE.md config 1"}
+    print(json.dumps({
+        "metric": METRIC, "value": n * world / (elapsed / args.steps), "unit": "peaks/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+        "config": {"workload": "config1: whole masses of random canonical 1..8-mers (+ the reference test's 7 x 3), "
+                               "canonical 5-row table, budget round(0.5 len) per query", "queries_per_gpu": n},
+        "roofline": {"bound": "hbm", "kernel": "k_explain_deferred", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "algorithmic_bytes_per_launch": bytes_def, "avg_launch_us": dus},
+        "kernels": kern,
+        "engine_stats": {"pair": int(stats[6]), "deep": int(stats[1]), "exact": int(stats[2]),
+                         "nomemo": int(stats[3]), "index_loads": nodes, "candidates": int(res.count[some].sum()),
+                         "payload_bytes": int(stats[5] + stats[7])},
+        "step": "explain pass (scan routes deep windows) + settle: deferred DFS launch + result pack",
+        "cpu_baseline": cpu,
+    }), flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -522,30 +522,35 @@ struct GlobFrame {
   int A, B;
   uint8_t r, top, pad0, pad1;
 };
+// A lane's DFS stack in global memory, interleaved over the role's lanes:
+// frame d of lane g at f0[d * stride + g], so the lanes of a wave at equal
+// depth touch consecutive frames (coalesced) instead of lines 3 KB apart.
 struct GlobStack {
-  GlobFrame* f;
+  GlobFrame* f;       // this lane's frame 0
+  uint32_t stride;    // lanes of the role (frames per depth level)
   static constexpr int depth = kMaxDepth;
-  __device__ __forceinline__ uint32_t m(int d) const { return f[d].m; }
-  __device__ __forceinline__ M128 mask(int d) const { return {f[d].a, f[d].b}; }
-  __device__ __forceinline__ uint8_t row(int d) const { return f[d].r; }
+  __device__ __forceinline__ GlobFrame& at(int d) const { return f[(size_t)d * stride]; }
+  __device__ __forceinline__ uint32_t m(int d) const { return at(d).m; }
+  __device__ __forceinline__ M128 mask(int d) const { return {at(d).a, at(d).b}; }
+  __device__ __forceinline__ uint8_t row(int d) const { return at(d).r; }
   __device__ __forceinline__ void set(int d, uint32_t m, M128 k) {
-    f[d].m = m;
-    f[d].a = k.a;
-    f[d].b = k.b;
+    at(d).m = m;
+    at(d).a = k.a;
+    at(d).b = k.b;
   }
   __device__ __forceinline__ void set_mask(int d, M128 k) {
-    f[d].a = k.a;
-    f[d].b = k.b;
+    at(d).a = k.a;
+    at(d).b = k.b;
   }
-  __device__ __forceinline__ void set_row(int d, int r) { f[d].r = (uint8_t)r; }
+  __device__ __forceinline__ void set_row(int d, int r) { at(d).r = (uint8_t)r; }
   __device__ __forceinline__ void set_budget(int d, int A, int B, int top) {
-    f[d].A = A;
-    f[d].B = B;
-    f[d].top = (uint8_t)top;
+    at(d).A = A;
+    at(d).B = B;
+    at(d).top = (uint8_t)top;
   }
-  __device__ __forceinline__ int A(int d) const { return f[d].A; }
-  __device__ __forceinline__ int B(int d) const { return f[d].B; }
-  __device__ __forceinline__ int top(int d) const { return f[d].top; }
+  __device__ __forceinline__ int A(int d) const { return at(d).A; }
+  __device__ __forceinline__ int B(int d) const { return at(d).B; }
+  __device__ __forceinline__ int top(int d) const { return at(d).top; }
 };
 
 // ---------------------------------------------------------------------------
@@ -1136,6 +1141,27 @@ __device__ __forceinline__ void wg_stat(unsigned long long* stats, int k, uint64
 // mbcnt: no atomics) or the deferred class lists.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t lane_mask_lt(int lane) { return lane ? (~0ull >> (64 - lane)) : 0ull; }
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // set bits of m below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Append query i to deferred class list `cls` (kClassDeep / kClassExact /
+// kClassNomemo; -1: none) with one atomic per class per wave instruction:
+// per-lane atomics on one counter serialise in L2 (125 k routed windows cost
+// the scan 1.4 ms that way).  Call with every lane that may append active.
+__device__ __forceinline__ void route_append(const OutArgs& out, int64_t n, int cls, uint32_t i) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = kClassDeep; c <= kClassNomemo; ++c) {
+    const uint64_t m = __ballot(cls == c);
+    if (!m) continue;
+    const int leader = __builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&out.counters[c], (uint32_t)__builtin_popcountll(m));
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    if (cls == c) out.lists[(int64_t)c * n + base + mbcnt(m)] = i;
+  }
+}
 
 // One query's final result on the deferred paths: its status byte, and for a
 // query with candidates one hit record appended to the deferred hit list
@@ -1311,6 +1337,7 @@ __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArg
   bool deferred = false;
   RegSink sink;
   EnumOut eo{0, 0, 0, 0};
+  int cls = -1;
   if (live) {
     const uint4 item = wl[k0 + lane];  // {query, first window value >= 1, last, kItem* flags}
     i = item.x;
@@ -1321,9 +1348,7 @@ __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArg
       if (!window_has_roots(t.valid, a, b)) {
         run = false;
       } else if (!(item.w & kItemNever) || b >= t.shallow_hi) {
-        const int cls = (item.w & kItemNever) ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
-        const uint32_t slot = atomicAdd(&out.counters[cls], 1u);
-        out.lists[(int64_t)cls * q.n + slot] = (uint32_t)i;
+        cls = (item.w & kItemNever) ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
         run = false;
         deferred = true;
       }
@@ -1337,6 +1362,7 @@ __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArg
                       : ((item.w & kItemZero) ? SST_EMPTY : SST_NONE);
     if (deferred) status = (int8_t)kStatusPending;
   }
+  route_append(out, q.n, cls, (uint32_t)i);
   const TileOut to = spill_alloc(out, lane, status == SST_SOME ? eo.bytes : 0, status);
   if (to.bytes) {
     if (!sink.over) {
@@ -1388,9 +1414,6 @@ constexpr uint32_t kBufSkip = 0x80000000u;
 constexpr int kPreChunks = 4;  // hit-record chunks a scan wave prepares before its look-back wait  // an offset past every buffer the scan addresses
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {  // set bits of m below this lane
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 // payload bytes of `cnt` pair-list records from entry `first` (LDS)
 __device__ __forceinline__ uint32_t pair_bytes(const PairLds& p, uint32_t first, uint32_t cnt) {
@@ -1502,20 +1525,20 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     if (__ballot(work)) {  // wave-uniform, rare here: route the window now, so that the deferred class lists
                            // are complete when the scan ends (one tail launch runs every class)
       bool shallow = false;
+      int cls = -1;
       if (work) {
         int8_t st2 = zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;  // no reachable value in the window
         if (window_has_roots(t.valid, a, hi)) {
           if (never && hi < t.shallow_hi) {
             shallow = true;  // <= 3 items, budgets cannot bind: the SHALLOW role writes all three
           } else {
-            const int cls = never ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
-            const uint32_t slot = atomicAdd(&out.counters[cls], 1u);
-            out.lists[(int64_t)cls * q.n + slot] = i;
+            cls = never ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
             st2 = (int8_t)kStatusPending;
           }
         }
         if (!shallow) out.status[i] = st2;
       }
+      route_append(out, q.n, cls, i);
       const uint64_t sb = __ballot(shallow);
       if (shallow) wl[n_work + mbcnt(sb)] = make_uint4(i, a, hi, zero ? kItemZero : 0u);
       n_work += (uint32_t)__builtin_popcountll(sb);
@@ -1718,6 +1741,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryAr
     int8_t status = oot ? (int8_t)SST_OUT_OF_TABLE : (zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE);
     bool work = false;
     uint4 item = make_uint4(0, 0, 0, 0);
+    int route = -1;
     if (active && window_has_roots(t.valid, a, hi)) {
       int cls;
       if (never) cls = hi < t.shallow_hi ? kClassShallow : kClassDeep;
@@ -1726,11 +1750,11 @@ __global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryAr
         work = true;  // the expand kernel writes status, count and offset
         item = make_uint4(i, a, hi, zero ? kItemZero : 0u);
       } else {
-        uint32_t slot = atomicAdd(&out.counters[cls], 1u);
-        out.lists[(int64_t)cls * q.n + slot] = i;
+        route = cls;
         status = (int8_t)kStatusPending;
       }
     }
+    route_append(out, q.n, route, i);
     if (live && !work) out.status[i] = status;
     const uint64_t bal = __ballot(work);
     if (work) wl[n_work + __builtin_popcountll(bal & lane_mask_lt(lane))] = item;
@@ -1946,42 +1970,50 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
   stage_rows(s, t);
   const int64_t gid = (int64_t)blk * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)nblk * blockDim.x;
-  GlobStack st{ws + gid * kMaxDepth};
+  GlobStack st{ws + gid, (uint32_t)nthreads};
   uint64_t st_n = 0, st_nodes = 0;
-  for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
-    int64_t i = out.lists[(int64_t)cls * q.n + j];
-    int64_t lo, hi;
-    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
-    int A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
-    bool has_zero = lo <= 0 && hi >= 0;
-    int64_t a = lo < 1 ? 1 : lo, b = hi;
+  const int lane = threadIdx.x & 63;
+  // wave-uniform trip count (one wave per block): the payload allocation and
+  // the hit records then take one atomic per wave, not one per query
+  for (int64_t j0 = gid - lane; j0 < (int64_t)n_list; j0 += nthreads) {
+    const int64_t j = j0 + lane;
+    const bool live = j < (int64_t)n_list;
+    int64_t i = 0, a = 1, b = 0;
+    int A0 = 0;
     EnumOut eo{0, 0, 0, 0};
-    CountSink cs;
-    enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, cs, q.node_budget, eo);
-    int8_t status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
-    uint64_t bytes = eo.bytes;
-    if (eo.fail) {
-      status = SST_ABORTED;
-      bytes = 0;
-    } else if (eo.count > q.cap_count) {
-      status = SST_OVERFLOW;
-      bytes = 0;
-    }
-    uint64_t off = 0;
-    if (bytes) {
-      off = out.spill_base + atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
-      if (off + bytes > out.arena_bytes) {
-        status = (int8_t)kStatusArenaRetry;
+    int8_t status = SST_NONE;
+    uint64_t bytes = 0;
+    if (live) {
+      i = out.lists[(int64_t)cls * q.n + j];
+      int64_t lo, hi;
+      quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
+      A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
+      const bool has_zero = lo <= 0 && hi >= 0;
+      a = lo < 1 ? 1 : lo;
+      b = hi;
+      CountSink cs;
+      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, cs, q.node_budget, eo);
+      status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
+      bytes = eo.bytes;
+      if (eo.fail) {
+        status = SST_ABORTED;
         bytes = 0;
-      } else {
-        MemSink ms{out.payload + off, ~0ull};
-        EnumOut e2{0, 0, 0, 0};
-        enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2);
+      } else if (eo.count > q.cap_count) {
+        status = SST_OVERFLOW;
+        bytes = 0;
       }
     }
-    emit_result(out, true, (uint32_t)i, status, eo.count, off);
-    st_n++;
-    st_nodes += eo.nodes;
+    const TileOut to = spill_alloc(out, lane, bytes, status);
+    if (to.bytes) {
+      MemSink ms{out.payload + to.off, ~0ull};
+      EnumOut e2{0, 0, 0, 0};
+      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2);
+    }
+    emit_result(out, live, (uint32_t)i, to.status, eo.count, to.off);
+    if (live) {
+      st_n++;
+      st_nodes += eo.nodes;
+    }
   }
   wg_stat(out.stats, MODE == MODE_FAST ? kStatDeep : kStatNomemo, st_n);
   wg_stat(out.stats, kStatNodes, st_nodes);
@@ -1997,59 +2029,62 @@ __device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs
   const int64_t gid = (int64_t)blk * 64 + threadIdx.x;
   const int64_t nthreads = (int64_t)nblk * 64;
   P1Frame* fr = (P1Frame*)(ws.frames + gid * kMaxDepth * sizeof(P1Frame));
-  GlobStack st{(GlobFrame*)(ws.stacks + gid * kMaxDepth * sizeof(GlobFrame))};
+  GlobStack st{(GlobFrame*)ws.stacks + gid, (uint32_t)nthreads};
   Hash h;
   h.e = (HEntry*)(ws.hash + (size_t)gid * ws.hash_cap * sizeof(HEntry));
   h.mask = ws.hash_cap - 1;
   h.limit = (uint32_t)(ws.hash_cap * 0.7);
   uint64_t st_n = 0, st_nodes = 0;
-  for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
-    int64_t i = out.lists[(int64_t)kClassExact * q.n + j];
-    int64_t lo, hi;
-    quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
-    int A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
-    bool has_zero = lo <= 0 && hi >= 0;
-    int64_t a = lo < 1 ? 1 : lo, b = hi;
-    h.epoch = ++ws.epochs[gid];
-    h.used = 0;
-    uint64_t nodes = 0;
-    int rc = phase1<false>(t, s, h, fr, a, b, A0, q.node_budget, nodes);
-    int8_t status;
+  const int lane = threadIdx.x & 63;
+  for (int64_t j0 = gid - lane; j0 < (int64_t)n_list; j0 += nthreads) {  // wave-uniform (see deep_body)
+    const int64_t j = j0 + lane;
+    const bool live = j < (int64_t)n_list;
+    int64_t i = 0, a = 1, b = 0;
+    int A0 = 0;
+    int8_t status = SST_NONE;
     EnumOut eo{0, 0, 0, 0};
-    uint64_t bytes = 0;
-    if (rc == -1) {
-      status = (int8_t)kStatusExactRetry;
-      atomicAdd(out.exact_retries, 1ull);  // lets the host see it without a status scan (settle)
-    } else if (rc < 0) {
-      status = SST_ABORTED;
-    } else {
-      CountSink cs;
-      enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, cs, q.node_budget, eo);
-      status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
-      bytes = eo.bytes;
-      if (eo.fail) {
+    uint64_t bytes = 0, nodes = 0;
+    if (live) {
+      i = out.lists[(int64_t)kClassExact * q.n + j];
+      int64_t lo, hi;
+      quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
+      A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
+      const bool has_zero = lo <= 0 && hi >= 0;
+      a = lo < 1 ? 1 : lo;
+      b = hi;
+      h.epoch = ++ws.epochs[gid];
+      h.used = 0;
+      const int rc = phase1<false>(t, s, h, fr, a, b, A0, q.node_budget, nodes);
+      if (rc == -1) {
+        status = (int8_t)kStatusExactRetry;
+        atomicAdd(out.exact_retries, 1ull);  // lets the host see it without a status scan (settle)
+      } else if (rc < 0) {
         status = SST_ABORTED;
-        bytes = 0;
-      } else if (eo.count > q.cap_count) {
-        status = SST_OVERFLOW;
-        bytes = 0;
-      }
-    }
-    uint64_t off = 0;
-    if (bytes) {
-      off = out.spill_base + atomicAdd((unsigned long long*)out.cursor, (unsigned long long)bytes);
-      if (off + bytes > out.arena_bytes) {
-        status = (int8_t)kStatusArenaRetry;
-        bytes = 0;
       } else {
-        MemSink ms{out.payload + off, ~0ull};
-        EnumOut e2{0, 0, 0, 0};
-        enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, ms, ~0ull, e2);
+        CountSink cs;
+        enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, cs, q.node_budget, eo);
+        status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
+        bytes = eo.bytes;
+        if (eo.fail) {
+          status = SST_ABORTED;
+          bytes = 0;
+        } else if (eo.count > q.cap_count) {
+          status = SST_OVERFLOW;
+          bytes = 0;
+        }
       }
     }
-    emit_result(out, true, (uint32_t)i, status, eo.count, off);
-    st_n++;
-    st_nodes += nodes + eo.nodes;
+    const TileOut to = spill_alloc(out, lane, bytes, status);
+    if (to.bytes) {
+      MemSink ms{out.payload + to.off, ~0ull};
+      EnumOut e2{0, 0, 0, 0};
+      enumerate_window<MODE_EXACT>(t, s, st, &h, a, b, A0, ms, ~0ull, e2);
+    }
+    emit_result(out, live, (uint32_t)i, to.status, eo.count, to.off);
+    if (live) {
+      st_n++;
+      st_nodes += nodes + eo.nodes;
+    }
   }
   wg_stat(out.stats, kStatExact, st_n);
   wg_stat(out.stats, kStatNodes, st_nodes);
