@@ -10,11 +10,10 @@ spectra (10k spectra, ~1M peaks, full 104-mass /
         reference's sliding window emits (prediction.py:286-329), budget
         round(0.5*max_len)                  -> k_explain_main (+ deferred kernels)
   * N>1: spectra shard by rank (weak scaling: `--spectra` per GPU); each
-        rank's results are complete for its own spectra and stay in its HBM
-        (no data-path collective in the step).  --gather adds delivery of
-        every query's result (status, count, offset, dense payload) to rank 0
-        over RCCL, timed inside the step (status bytes + dense hit list +
-        dense payload, sst_result_hit_list).
+        step's complete result of every rank (A7 bytes, A8 status bytes, dense
+        hit list, dense payload: parallel.wire_pack) is gathered to rank 0 over
+        RCCL on a second stream while the next step computes (--no-gather:
+        results stay in each rank's HBM).
 value = peaks of all ranks / step time (max over ranks).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--spectra S]
@@ -158,8 +157,9 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo: rehearsal of the "
                          "multi-rank path, e.g. several ranks on one GPU with SST_DEVICE=0)")
-    ap.add_argument("--gather", action="store_true",
-                    help="N>1: gather every query's result to rank 0 over RCCL inside the timed step")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: keep every rank's results in its own HBM (default: each step's complete result of "
+                         "every rank is gathered to rank 0 over RCCL, overlapped with the next step)")
     ap.add_argument("--event-every", type=int, default=0,
                     help="bracket every n-th launch of the roofline kernel with HIP events (0: about five "
                          "brackets over the timed steps, at least every 4th launch)")
@@ -183,7 +183,7 @@ def main():
     from spectrseqtools_amd import _native
     from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
     from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
-    from spectrseqtools_amd.parallel import Gatherer, device_bytes, dist_env
+    from spectrseqtools_amd.parallel import Gatherer, decode_hits, device_bytes, dist_env, wire_pack, wire_unpack
 
     rank, world, local = dist_env()
     if world != args.gpus:
@@ -224,9 +224,16 @@ def main():
     ext = torch.cuda.ExternalStream(engine.stream, device=dev_t)
 
     results = [None, None]
-    gath = Gatherer(dist, dev_t) if (dist and args.gather) else None
+    gath = Gatherer(dist, dev_t) if (dist and not args.no_gather) else None
     side = torch.cuda.Stream(device=dev_t) if args.a7_stream else None
-    settled = {"n": 0}
+    settled = {"n": 0, "sent": 0}
+    # N>1 delivery: step j's result goes to rank 0 on a second stream while
+    # step j+1 computes.  pass_done[j&1]: step j's kernels (engine stream);
+    # copied[j&1]: its wire copy (comm stream), which the engine stream waits
+    # for before step j+2 reuses the same result buffers
+    comm = torch.cuda.Stream(device=dev_t) if gath is not None else None
+    pass_done = [torch.cuda.Event(), torch.cuda.Event()]
+    copied = [None, None]
 
     def settle(r):
         nh, nb = r.settle()
@@ -235,9 +242,31 @@ def main():
                                f"vs {n_hits0} / {payload0}")
         settled["n"] += 1
 
+    def send(j):
+        """Step j's complete result of this rank -> rank 0 (wire format:
+        parallel.wire_pack -- A7 bytes, A8 status bytes, dense hit list, dense
+        payload; ~1 B/query + 16 B/hit)."""
+        r = results[j & 1]
+        settle(r)  # host: the pass's header (routed windows / retries handled)
+        hits, n_hits = r.hit_list_device()
+        st, _c, _o, pay, nb = r.device_views(arrays=False)
+        with torch.cuda.stream(comm):
+            comm.wait_event(pass_done[j & 1])
+            if side is not None:
+                comm.wait_stream(side)
+            wire = wire_pack(outs7[j & 1], device_bytes(st, n8, dev_t), device_bytes(hits, 16 * n_hits, dev_t),
+                             device_bytes(pay, nb, dev_t))
+            ev = torch.cuda.Event()
+            ev.record(comm)
+            copied[j & 1] = ev
+            gath.gather(wire)
+        settled["sent"] += 1
+
     def step(k):
         cur = k & 1
         out7 = outs7[cur]
+        if copied[cur] is not None:  # step k-2's wire copy read these buffers
+            ext.wait_event(copied[cur])
         # A8 first (its persistent scan grid fills the chip), then A7; the two
         # touch disjoint buffers
         if args.a7_stream != 2:
@@ -252,24 +281,19 @@ def main():
             results[cur] = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A,
                                                reuse=results[cur])
         if gath is not None:
-            # wire format: A7 bytes, A8 status bytes, the dense hit list
-            # ({query, count, word} per query with candidates) and the dense
-            # payload -- ~1 B/query + 16 B/hit instead of 17 B/query
-            settle(results[cur])
-            hits, n_hits = results[cur].hit_list_device()
-            st, _c, _o, pay, nb = results[cur].device_views(arrays=False)
-            torch.cuda.current_stream().wait_stream(ext)
-            if side is not None:
-                torch.cuda.current_stream().wait_stream(side)  # A7 results
-            flat = torch.cat([out7.view(torch.uint8), device_bytes(st, n8, dev_t), device_bytes(hits, 16 * n_hits, dev_t),
-                              device_bytes(pay, nb, dev_t)])
-            gath.gather(flat)
-        elif k > 0:
-            settle(results[cur ^ 1])  # the previous step's result, while this one runs
+            pass_done[cur].record(ext)
+        if k > 0:  # the previous step's result, while this one runs: settled, and delivered for N>1
+            if gath is not None:
+                send(k - 1)
+            else:
+                settle(results[cur ^ 1])
 
     def drain(k_last):
-        if gath is None and results[k_last & 1] is not None:
-            settle(results[k_last & 1])
+        if results[k_last & 1] is not None:
+            if gath is not None:
+                send(k_last)
+            else:
+                settle(results[k_last & 1])
 
     # untimed reference pass: sizes for the gather and the expected result
     tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, outs7[0].data_ptr())
@@ -278,7 +302,7 @@ def main():
     n_hits0, payload0 = ref.settle()
     ref_digest = result_digest(ref)
     if gath is not None:
-        gath.agree(n7 + n8 + 16 * n_hits0 + payload0)
+        gath.agree(32 + n7 + n8 + 16 * n_hits0 + payload0)
     for k in range(args.warmup):
         step(k)
     drain(args.warmup - 1)
@@ -294,7 +318,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    settled["n"] = 0
+    settled["n"] = settled["sent"] = 0
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(k)
@@ -321,6 +345,8 @@ def main():
     # payload), and A7 the setup pass
     if settled["n"] != args.steps and not args.no_validate:
         raise RuntimeError(f"{settled['n']} of {args.steps} steps settled")
+    if gath is not None and settled["sent"] != args.steps:
+        raise RuntimeError(f"{settled['sent']} of {args.steps} steps delivered to rank 0")
     for r in results:
         if r is not None:
             r.fetch_device()
@@ -328,6 +354,23 @@ def main():
                 raise RuntimeError("a timed step's result differs from the reference pass")
     res = results[(args.steps - 1) & 1]
     st = res.status
+    if gath is not None:
+        # rank 0 decodes what it received from every rank in the last step:
+        # each rank's result digest must match (and its A7 bytes)
+        import hashlib
+
+        mine = torch.tensor(np.frombuffer(bytes.fromhex(ref_digest), dtype=np.uint8).copy(), device=dev_t)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        if rank == 0 and not args.no_validate:
+            for r_, (buf, want) in enumerate(zip(gath.last, allr)):
+                v_, st_, hits_, pay_ = wire_unpack(buf.cpu().numpy())
+                cnt_, off_ = decode_hits(st_, hits_)
+                h = hashlib.sha256()
+                for a_ in (st_, cnt_, off_, pay_):
+                    h.update(np.ascontiguousarray(a_).tobytes())
+                if h.digest() != bytes(want.cpu().numpy()):
+                    raise RuntimeError(f"rank {r_}'s gathered result does not decode to its own result")
     if (st < -2).any() and not args.no_validate:
         raise RuntimeError(f"internal statuses in results: {np.unique(st[st < -2])}")
     stats = res.stats()
@@ -425,9 +468,10 @@ def main():
             "max_len": seq.max_len,
             "max_modifications": A,
             "a7_stream": ("side stream, concurrent with the A8 chain" if args.a7_stream else "engine stream"),
-            "parallelism": (f"spectra sharded over {world} GPUs, results kept per rank"
-                            + ((", RCCL" if args.backend == "nccl" else ", gloo") +
-                               " gather of all results to rank 0 in the step" if args.gather else "")
+            "parallelism": ((f"spectra sharded over {world} GPUs; every step's complete result of every rank "
+                             f"gathered to rank 0 ({'RCCL' if args.backend == 'nccl' else 'gloo'}, wire format "
+                             f"parallel.wire_pack), overlapped with the next step"
+                             if gath is not None else f"spectra sharded over {world} GPUs, results kept per rank")
                             if world > 1 else "1 GPU"),
         },
         "roofline": {

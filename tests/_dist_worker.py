@@ -1,6 +1,9 @@
 """One rank of the world-size-2 gloo test (tests/test_parallel.py): the
 multi-GPU layer's host logic on CPU -- sharding, the agreed-size gather of
-per-rank result buffers to rank 0, and the max-over-ranks step time that
+per-rank result buffers to rank 0, the engine's result wire format (each
+rank encodes oracle answers to its own queries exactly as the engine lays out
+a result: status bytes, dense hit list, dense payload; rank 0 decodes every
+query of every rank and checks it), and the max-over-ranks step time that
 bench.py reports."""
 import os
 import sys
@@ -9,8 +12,52 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
-from spectrseqtools_amd.parallel import Gatherer, dist_env, shard_by_weight, shard_range  # noqa: E402
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(HERE, ".."), HERE]
+import _oracle as oracle  # noqa: E402  (test infrastructure: the answers each rank encodes)
+from spectrseqtools_amd.parallel import (Gatherer, candidates, decode_hits, dist_env, shard_by_weight,  # noqa: E402
+                                         shard_range, wire_pack, wire_unpack)
+
+ROWS = [0, 305042, 306026, 329053, 345048]  # canonical alphabet (a 5 x 377 397 table)
+TOL, PREC, CAP = 1e-5, 1e-3, 1
+
+
+def rank_queries(rank, n=600):
+    rng = np.random.default_rng(1000 + rank)
+    k = rng.integers(1, 5, n)
+    m = np.array([sum(ROWS[1:][j] for j in rng.integers(0, 4, kk)) for kk in k]) * PREC
+    m = m + rng.normal(0, 0.003, n)
+    m[:20] = rng.uniform(0.0, 0.2, 20)  # below the first reachable mass: NONE / EMPTY
+    t = TOL * rng.uniform(300, 3000, n)
+    t[20:120] = rng.uniform(1.0, 3.0, 100)  # wide windows: several candidates (OVERFLOW past CAP)
+    return m, t
+
+
+def oracle_answers(table, alph, masses, thr):
+    out = []
+    for m, t in zip(masses, thr):
+        st, sols, n_empty, _ = oracle.explain_table(table, 32, alph, float(m), float(t), TOL, -1)
+        out.append((st, sorted(sols), n_empty))
+    return out
+
+
+def engine_layout(answers):
+    """An engine result (include/sst.h) built from oracle answers: status
+    bytes, dense hit records {query, count, word lo, word hi}, dense payload."""
+    status, hits, payload = [], [], []
+    for i, (st, sols, n_empty) in enumerate(answers):
+        if st == 1 and sols and len(sols) > CAP:
+            status.append(-2)  # SST_OVERFLOW: exact count, no payload
+            hits.append([i, len(sols), len(sols), 0])
+        elif st == 1 and sols:
+            status.append(2)
+            hits.append([i, len(sols), len(payload), 0])
+            for c in sols:
+                payload += [len(c)] + list(c)
+        else:
+            status.append(1 if (st == 1 and n_empty) else 0)
+    return (np.array(status, np.int8), np.array(hits, np.uint32).reshape(-1, 4),
+            np.array(payload, np.uint8))
 
 
 def main():
@@ -47,6 +94,40 @@ def main():
         for r, buf in enumerate(got):
             want = np.random.default_rng(100 + r).integers(0, 256, 1000 + 37 * r, dtype=np.uint8)
             assert np.array_equal(buf.numpy(), want), r
+    else:
+        assert got is None
+
+    # the engine's wire format: every rank's answers decode on rank 0
+    table = oracle.build_table(ROWS, max(ROWS) * 35, 32)
+    alph = oracle.Alphabet(ROWS, [0] * 5, [20] * 5)
+    masses, thr = rank_queries(rank)
+    ans = oracle_answers(table, alph, masses, thr)
+    st, hits, pay = engine_layout(ans)
+    valid = np.array([oracle.is_valid(table, 32, m, t, TOL) for m, t in zip(masses, thr)], np.int8)
+    wire = wire_pack(torch.from_numpy(valid), torch.from_numpy(st), torch.from_numpy(hits.view(np.uint8).ravel()),
+                     torch.from_numpy(pay))
+    g2 = Gatherer(dist, torch.device("cpu"))
+    g2.agree(wire.numel())
+    got = g2.gather(wire)
+    if rank == 0:
+        n_checked = n_some = n_over = 0
+        for r, buf in enumerate(got):
+            v_r, st_r, hits_r, pay_r = wire_unpack(buf.numpy())
+            m_r, t_r = rank_queries(r)
+            want = oracle_answers(table, alph, m_r, t_r)
+            assert np.array_equal(v_r, [oracle.is_valid(table, 32, m, t, TOL) for m, t in zip(m_r, t_r)])
+            cnt, off = decode_hits(st_r, hits_r)
+            for i, (s0, sols, n_empty) in enumerate(want):
+                if s0 == 1 and len(sols) > CAP:
+                    assert st_r[i] == -2 and int(cnt[i]) == len(sols), (r, i)
+                    n_over += 1
+                elif s0 == 1 and sols:
+                    assert st_r[i] == 2 and candidates(pay_r, cnt, off, i) == sols, (r, i)
+                    n_some += 1
+                else:
+                    assert st_r[i] == (1 if (s0 == 1 and n_empty) else 0), (r, i)
+                n_checked += 1
+        assert n_checked == 1200 and n_some > 0 and n_over > 0, (n_checked, n_some, n_over)
     else:
         assert got is None
 
