@@ -1441,8 +1441,9 @@ int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, in
   std::vector<int8_t> st(nn);
   if (n_exact) {
     // one 64-lane block per query in flight (k_length_exact<WAVE>), each with
-    // its own memo slice
-    int units = (int)std::min<uint32_t>(256, n_exact);
+    // its own memo slice: up to 1 024 at once (4 waves per CU; the memo slices
+    // then take ~10 GB of HBM), batches of many spectra keep the chip busy
+    int units = (int)std::min<uint32_t>(1024, n_exact);
     uint32_t cap = memo_cap0(units, kLBHashCap0);
     for (;;) {
       DevBuf hash, vals, frames;
