@@ -302,7 +302,7 @@ def main():
     n_hits0, payload0 = ref.settle()
     ref_digest = result_digest(ref)
     if gath is not None:
-        gath.agree(32 + n7 + n8 + 16 * n_hits0 + payload0)
+        gath.agree(64 + (n7 + 3) // 4 + (n8 + 3) // 4 + 12 * n_hits0 + payload0)
     for k in range(args.warmup):
         step(k)
     drain(args.warmup - 1)

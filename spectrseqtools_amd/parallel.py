@@ -10,13 +10,19 @@ candidate payload) to the rank that drives the Python pipeline.  RCCL has no
 gatherv: sizes are agreed once (all_gather of lengths), then one padded
 torch.distributed.gather moves the bytes (send/recv over xGMI).
 
-Wire format of one rank's result (wire_pack / wire_unpack): a 32-B header
-{u64 n_valid, n_explain, n_hits, payload_bytes}, the is_valid bytes, the
-explain status bytes, the dense hit list (16-B records {u32 query, u32 count,
-u64 word}: word = the candidates' payload offset (SOME) or the exact count
-(OVERFLOW / ABORTED), include/sst.h sst_result_hit_list) and the dense
-payload ([k][row_0..row_{k-1}] per candidate).  decode_hits turns it back
-into per-query counts / offsets.
+Wire format of one rank's result (wire_pack / wire_unpack), packed on the
+device with a few tensor ops (no host round trip):
+  header   8 x i64: magic, n_valid, n_explain, n_hits, payload_bytes, 0, 0, 0
+  valid    2-bit codes (is_valid + 1: 0 raise, 1 False, 2 True), 4 per byte
+  status   2-bit codes: 0 NONE, 1 EMPTY, 2 a hit record follows, 3 OUT_OF_TABLE
+  hits     12-B records {u32 query | kind << 30, u32 a, u32 b}: kind 0 SOME
+           (a = candidates, b = their payload offset), 1 OVERFLOW / 2 ABORTED
+           (a, b = the exact count's low / high word, no payload)
+  payload  the dense payload ([k][row_0..row_{k-1}] per candidate)
+About 0.5 B per query + 12 B per query with candidates + payload: 33 MB per
+rank per config-3 step instead of the 51 MB of the engine's own layout
+(1 B status, 16-B hit records).  wire_unpack + decode_hits + candidates read
+it back with numpy alone.
 """
 import os
 
@@ -109,40 +115,88 @@ def device_bytes(ptr, nbytes, device):
     return torch.as_tensor(_Iface(), device=device)
 
 
-WIRE_HEADER = 32
-SST_SOME = 2
+WIRE_HEADER = 64
+WIRE_MAGIC = 0x3257545353  # "SSTW2"
+SST_NONE, SST_EMPTY, SST_SOME, SST_OUT_OF_TABLE, SST_OVERFLOW, SST_ABORTED = 0, 1, 2, -1, -2, -4
+
+
+def _pack2(codes):
+    """uint8 codes in {0..3} -> 4 per byte (torch, on the codes' device)."""
+    import torch
+
+    n = codes.numel()
+    pad = (-n) % 4
+    if pad:
+        codes = torch.cat([codes, torch.zeros(pad, dtype=torch.uint8, device=codes.device)])
+    c = codes.view(-1, 4)
+    return c[:, 0] | (c[:, 1] << 2) | (c[:, 2] << 4) | (c[:, 3] << 6)
+
+
+def _unpack2(b, n):
+    b = np.asarray(b, dtype=np.uint8)
+    c = np.stack([b & 3, (b >> 2) & 3, (b >> 4) & 3, b >> 6], axis=1).ravel()
+    return c[:n]
 
 
 def wire_pack(valid, status, hits, payload):
-    """One rank's result as a flat uint8 tensor (same device as the parts):
-    header, is_valid bytes, status bytes, hit records, payload.  The parts
-    are uint8 tensors (views of the engine's buffers on the device path)."""
+    """One rank's result in the wire format above, as a flat uint8 tensor on
+    the parts' device.  valid / status: int8 tensors (is_valid results,
+    explain statuses); hits: the engine's dense hit list as a uint8 tensor
+    (16-B records, include/sst.h sst_result_hit_list); payload: uint8."""
     import torch
 
     dev = status.device
-    hdr = torch.tensor([valid.numel(), status.numel(), hits.numel() // 16, payload.numel()], dtype=torch.int64,
-                       device=dev).view(torch.uint8)
-    return torch.cat([hdr, valid.view(torch.uint8), status.view(torch.uint8), hits.view(torch.uint8),
-                      payload.view(torch.uint8)])
+    st = status.view(torch.int8)
+    code8 = torch.where(st == SST_NONE, 0, torch.where(st == SST_EMPTY, 1, torch.where(st == SST_OUT_OF_TABLE, 3, 2)))
+    code7 = (valid.view(torch.int8) + 1).to(torch.uint8)
+    r = hits.view(torch.int32).view(-1, 4)
+    if payload.numel() >= (1 << 32):
+        raise ValueError("wire format: payload offsets are 32-bit")
+    if r.shape[0]:
+        kind = st[r[:, 0].long()]
+        kind = torch.where(kind == SST_OVERFLOW, 1, torch.where(kind == SST_ABORTED, 2, 0)).to(torch.int32)
+        some = kind == 0
+        rec = torch.stack([r[:, 0] | (kind << 30), torch.where(some, r[:, 1], r[:, 2]),
+                           torch.where(some, r[:, 2], r[:, 3])], dim=1)
+    else:
+        rec = torch.zeros((0, 3), dtype=torch.int32, device=dev)
+    hdr = torch.tensor([WIRE_MAGIC, valid.numel(), status.numel(), r.shape[0], payload.numel(), 0, 0, 0],
+                       dtype=torch.int64, device=dev)
+    return torch.cat([hdr.view(torch.uint8), _pack2(code7), _pack2(code8.to(torch.uint8)),
+                      rec.contiguous().view(torch.uint8).view(-1), payload.view(torch.uint8)])
 
 
 def wire_unpack(buf):
-    """numpy views of a wire buffer: (valid i8, status i8, hits u32[n,4], payload u8)."""
+    """numpy form of a wire buffer: (valid i8, status i8, hits u32[n,4] in
+    the engine's record layout {query, count, word lo, word hi}, payload u8)."""
     b = np.ascontiguousarray(np.asarray(buf, dtype=np.uint8))
-    n7, n8, nh, nb = (int(x) for x in b[:WIRE_HEADER].view(np.int64))
+    magic, n7, n8, nh, nb = (int(x) for x in b[:40].view(np.int64))
+    if magic != WIRE_MAGIC:
+        raise ValueError("not a wire buffer")
     o = WIRE_HEADER
-    valid = b[o:o + n7].view(np.int8)
-    o += n7
-    status = b[o:o + n8].view(np.int8)
-    o += n8
-    hits = b[o:o + 16 * nh].view(np.uint32).reshape(nh, 4)
-    o += 16 * nh
+    k7, k8 = (n7 + 3) // 4, (n8 + 3) // 4
+    valid = _unpack2(b[o:o + k7], n7).astype(np.int8) - 1
+    o += k7
+    code = _unpack2(b[o:o + k8], n8)
+    o += k8
+    rec = b[o:o + 12 * nh].view(np.uint32).reshape(nh, 3)
+    o += 12 * nh
     payload = b[o:o + nb]
     if o + nb != len(b):
         raise ValueError(f"wire buffer of {len(b)} B, header says {o + nb} B")
+    status = np.select([code == 0, code == 1, code == 3], [SST_NONE, SST_EMPTY, SST_OUT_OF_TABLE], SST_SOME)
+    status = status.astype(np.int8)
+    q = (rec[:, 0] & 0x3FFFFFFF).astype(np.int64)
+    kind = rec[:, 0] >> 30
+    status[q] = np.select([kind == 1, kind == 2], [SST_OVERFLOW, SST_ABORTED], SST_SOME)
+    hits = np.zeros((nh, 4), np.uint32)
+    hits[:, 0] = q
+    some = kind == 0
+    hits[:, 1] = np.where(some, rec[:, 1], np.minimum(rec[:, 1].astype(np.uint64) | (rec[:, 2].astype(np.uint64) << 32),
+                                                         0xFFFFFFFF)).astype(np.uint32)
+    hits[:, 2] = np.where(some, rec[:, 2], rec[:, 1])
+    hits[:, 3] = np.where(some, 0, rec[:, 2])
     return valid, status, hits, payload
-
-
 def decode_hits(status, hits):
     """Per-query (count, offset) from the hit list: SOME -> its payload
     offset, OVERFLOW / ABORTED -> the exact count (no payload); 0 elsewhere."""
