@@ -134,10 +134,11 @@ int sst_explain_batch(sst_table* t, const double* mass, const double* thr_abs, i
                       double precision, const int64_t* max_mods, int64_t max_mods_scalar, int with_memo,
                       uint64_t cap_per_query, sst_result** out);
 /* Same with inputs already in HBM; results stay on the device.  Queued on
- * the ctx stream, no host synchronisation: the pass is the scan kernel and
- * k_result_pack, which writes the complete result (status bytes, dense hit
+ * the ctx stream, no host synchronisation: on tables built here the pass is
+ * one scan launch that writes the complete result (status bytes, dense hit
  * list, dense payload; see sst_result_hit_list) plus a small header into
- * host-mapped memory.  If *out is non-NULL it must be a result of the same
+ * host-mapped memory (uploaded tables: scan, expand, deferred and pack
+ * launches).  If *out is non-NULL it must be a result of the same
  * ctx with capacity >= n: its buffers are reused (no allocation).  The inputs
  * (and the table) must stay valid and unchanged until the pass is settled
  * (sst_result_settle, or the first view / fetch, which settle implicitly):
