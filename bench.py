@@ -5,7 +5,8 @@ One step = the reference pipeline's hot path over one batch of synthetic
 spectra (10k spectra, ~1M peaks, full 104-mass /
 105-row alphabet, <=20-mer) with every input already resident in HBM:
   * A7: is_valid_mass for every peak x 4 breakage weights
-        (fragment_classification.py:52-67)  -> k_is_valid
+        (fragment_classification.py:52-67)  -> k_is_valid_peaks (one lane per
+        peak, the peak's mass read once for its 4 windows)
   * A8: explain_mass_with_table for every adjacent SU-mass difference the
         reference's sliding window emits (prediction.py:286-329), budget
         round(0.5*max_len)                  -> k_explain_main (+ deferred kernels)
@@ -100,7 +101,8 @@ def build_workload(n_spectra, seed, dp):
     dthr = np.concatenate(t_all)
     return {
         "peaks": P, "a7_mass": cq.su_mass, "a7_thr": cq.threshold, "a8_mass": diffs, "a8_thr": dthr,
-        "spectra": n_spectra, "a7_valid": valid,
+        "spectra": n_spectra, "a7_valid": valid, "obs": np.ascontiguousarray(batch.observed, dtype=np.float64),
+        "shifts": np.array([w * prec for w in brk], dtype=np.float64),  # classify_fragments' su = obs - w * prec
     }
 
 
@@ -210,8 +212,8 @@ def main():
     tdev = dp.device_table
     wl = build_workload(args.spectra, args.seed + rank * 1_000_003, dp)
     n7, n8 = len(wl["a7_mass"]), len(wl["a8_mass"])
-    a7m = torch.from_numpy(wl["a7_mass"]).to(dev_t)
-    a7t = torch.from_numpy(wl["a7_thr"]).to(dev_t)
+    obs_d = torch.from_numpy(wl["obs"]).to(dev_t)  # A7 reads the peaks (sst_is_valid_peaks: 4 windows per peak)
+    P_peaks, shifts = len(wl["obs"]), wl["shifts"]
     a8m = torch.from_numpy(wl["a8_mass"]).to(dev_t)
     a8t = torch.from_numpy(wl["a8_thr"]).to(dev_t)
     # two result sets used in turn: while step k runs on the GPU, the host
@@ -274,7 +276,7 @@ def main():
                                                reuse=results[cur])
         if side is not None:
             engine.set_stream(side.cuda_stream)
-        tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, out7.data_ptr())
+        tdev.is_valid_peaks_device(obs_d.data_ptr(), P_peaks, shifts, dp.tolerance, dp.precision, out7.data_ptr())
         if side is not None:
             engine.set_stream(None)
         if args.a7_stream == 2:
@@ -296,7 +298,7 @@ def main():
                 settle(results[k_last & 1])
 
     # untimed reference pass: sizes for the gather and the expected result
-    tdev.is_valid_device(a7m.data_ptr(), a7t.data_ptr(), n7, dp.tolerance, dp.precision, outs7[0].data_ptr())
+    tdev.is_valid_peaks_device(obs_d.data_ptr(), P_peaks, shifts, dp.tolerance, dp.precision, outs7[0].data_ptr())
     ref = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A)
     ref.fetch_device()
     n_hits0, payload0 = ref.settle()
@@ -397,7 +399,8 @@ def main():
     # algorithmic HBM bytes per launch (DESIGN.md "Measurement"); the LDS pair
     # list and the L2-resident bitset are on-chip after first touch but are
     # counted at 8 B per word touched:
-    #   k_is_valid:       mass+thr (16) + result (1) + the window's bitset words (8 each)
+    #   k_is_valid:       the peak's mass (8, once for its 4 windows) + result (1 per window) + the
+    #                     window's bitset words (8 each)
     #   k_explain_scan:   mass+thr (16) + status (1) of every query it resolves;
     #                     pair path: 8-B hit record + payload of each SOME / OVERFLOW;
     #                     other windows: bitset words (8 each); 16 B worklist item per queued query
@@ -413,7 +416,7 @@ def main():
     # candidates); the wave-local records and payload it re-reads are not
     fused = _native.K_RESULT_PACK not in prof
     bytes_k = {
-        "k_is_valid": float(n7 * (16 + 1) + 8 * w7.sum()),
+        "k_is_valid": float(8 * P_peaks + n7 + 8 * w7.sum()),
         # (stats[7] counts the 2 pad bytes per SOME query of the dword record stores: not algorithmic)
         "k_explain_scan": float(n8 * 16 + (n8 - n_work) + (16 * n_hits0 + cand_bytes if fused else
                                                             8 * int((some & pair).sum()) + int(stats[7]) - 2 * n_some_pair)

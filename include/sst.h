@@ -107,6 +107,17 @@ int sst_is_valid_batch(sst_table* t, const double* mass, const double* thr_abs, 
 int sst_is_valid_batch_device(sst_table* t, const double* d_mass, const double* d_thr_abs, int64_t n,
                               double tolerance, double precision, int8_t* d_out);
 
+/* is_valid_mass over peaks x breakage weights, as classify_fragments maps it
+ * over its concatenated frame (fragment_classification.py:39-67): for every
+ * peak p and shift k, mass = obs[p] - shifts[k] and threshold = tolerance *
+ * obs[p] (shifts[k] = breakage weight x precision, computed by the caller as
+ * the reference does); out[k * n_peaks + p] as sst_is_valid_batch
+ * (breakage-major, the reference's row order).  Reads each peak once. */
+int sst_is_valid_peaks(sst_table* t, const double* obs, int64_t n_peaks, const double* shifts, int n_shifts,
+                       double tolerance, double precision, int8_t* out);
+int sst_is_valid_peaks_device(sst_table* t, const double* d_obs, int64_t n_peaks, const double* shifts, int n_shifts,
+                              double tolerance, double precision, int8_t* d_out);
+
 /* is_singleton (fragment_classification.py:104-119), one result per query:
  * 1 if some value of the quantised window [round(mass/precision) -
  * ceil(thr/precision), ... + ...] is one of masses[0..n_masses) (the caller's

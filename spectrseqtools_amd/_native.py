@@ -27,7 +27,7 @@ EXPORTS = (
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
     "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
-    "sst_window_pairs",
+    "sst_window_pairs", "sst_is_valid_peaks", "sst_is_valid_peaks_device",
 )
 
 # kernel ids of sst_profile_read
@@ -116,6 +116,8 @@ def load_library(path=LIB_PATH):
     lib.sst_explain_recursion_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _U64, _PP]
     lib.sst_is_singleton_batch.argtypes = [_P, _P, _I, _P, _P, _I64, _D, _D, _P]
     lib.sst_is_singleton_batch_device.argtypes = [_P, _P, _I, _P, _P, _I64, _D, _D, _P]
+    lib.sst_is_valid_peaks.argtypes = [_P, _P, _I64, _P, _I, _D, _D, _P]
+    lib.sst_is_valid_peaks_device.argtypes = [_P, _P, _I64, _P, _I, _D, _D, _P]
     lib.sst_window_pairs.argtypes = [_P, _P, _I64, _D, _P, _P, _I64]
     lib.sst_window_pairs.restype = _I64
     return lib
@@ -430,6 +432,23 @@ class DeviceTable:
                                                                   int(max_mods), d, _ptr(out), _ptr(st)),
                           "sst_length_bound_batch")
         return out, st
+
+    def is_valid_peaks(self, observed, shifts, tolerance, precision):
+        """is_valid over peaks x breakage shifts (sst_is_valid_peaks): int8
+        [len(shifts) * n_peaks], breakage-major."""
+        o = np.ascontiguousarray(observed, dtype=np.float64)
+        sh = np.ascontiguousarray(shifts, dtype=np.float64)
+        out = np.zeros(len(o) * len(sh), np.int8)
+        self.engine.check(self.engine._lib.sst_is_valid_peaks(self.handle, _ptr(o), len(o), _ptr(sh), len(sh),
+                                                              float(tolerance), float(precision), _ptr(out)),
+                          "sst_is_valid_peaks")
+        return out
+
+    def is_valid_peaks_device(self, d_obs, n_peaks, shifts, tolerance, precision, d_out):
+        sh = np.ascontiguousarray(shifts, dtype=np.float64)
+        self.engine.check(self.engine._lib.sst_is_valid_peaks_device(self.handle, d_obs, int(n_peaks), _ptr(sh),
+                                                                     len(sh), float(tolerance), float(precision),
+                                                                     d_out), "sst_is_valid_peaks_device")
 
     def is_valid_device(self, d_mass, d_thr, n, tolerance, precision, d_out):
         self.engine.check(self.engine._lib.sst_is_valid_batch_device(self.handle, d_mass, d_thr, int(n),

@@ -214,6 +214,10 @@ struct ValidArgs {  // is_valid_mass batch
   int8_t* out;
 };
 
+struct PeakShifts {  // breakage weight x precision per output block (k_is_valid_peaks)
+  double shift[4];
+};
+
 struct LBArgs {
   const double* su;
   const double* obs;
@@ -253,6 +257,9 @@ hipError_t launch_index(int C, const void* packed, int n_rows, int64_t ncols, in
 hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, int64_t full_lo, int64_t full_hi, int64_t first_reach,
                            const double* mass, const double* thr, int64_t n, double tol, double prec, int8_t* out,
                            hipStream_t st);
+hipError_t launch_is_valid_peaks(const uint64_t* valid, int64_t limit, int64_t full_lo, int64_t full_hi,
+                                 int64_t first_reach, const double* obs, int64_t n, const double* shifts, int n_w,
+                                 double tol, double prec, int8_t* out, hipStream_t st);
 hipError_t launch_explain_scan(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
                                hipStream_t st);
 hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,

@@ -404,6 +404,35 @@ __global__ __launch_bounds__(256) void k_is_valid(ValidArgs v) {
   v.out[i] = hit ? (int8_t)1 : (act && hif >= (double)v.limit ? (int8_t)-1 : (int8_t)0);
 }
 
+// is_valid_mass over peaks x breakage weights, as classify_fragments issues
+// it (fragment_classification.py:39-67): su = obs - shift[k] (shift[k] =
+// breakage weight x precision, the host's f64 product), threshold = tolerance
+// x obs; out[k * n + p], breakage-major like the reference's pl.concat.  One
+// lane per peak: the peak's mass is read once (8 B instead of 16 B per
+// query) and its NW windows are quantised together, so their bitset loads
+// are in flight at once.
+template <int NW>
+__global__ __launch_bounds__(256) void k_is_valid_peaks(ValidArgs v, PeakShifts sh) {
+  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= (uint32_t)v.n) return;
+  const double obs = __builtin_nontemporal_load(v.mass + p);
+  const double t = v.tol * obs;
+  const double bmax = (double)(v.limit - 1);
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    double lof, hif;
+    quantise_lean(obs - sh.shift[k], t, v.prec, v.rprec, lof, hif);
+    const double af = __builtin_fmax(lof, 1.0);
+    const bool act = lof <= hif && af <= hif;
+    const double bf = __builtin_fmin(hif, bmax);
+    const bool inr = act && af <= bf;
+    const bool full = inr && bf >= (double)v.full_lo && af < (double)v.full_hi;
+    bool hit = full;
+    if (inr && !full && bf >= (double)v.first_reach) hit = any_bits(v.valid, (uint32_t)af, (uint32_t)bf);
+    v.out[(size_t)k * v.n + p] = hit ? (int8_t)1 : (act && hif >= (double)v.limit ? (int8_t)-1 : (int8_t)0);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // is_singleton (fragment_classification.py:104-119): some value of the
 // quantised window equals one of `masses` (the caller's integer masses, the
@@ -2972,6 +3001,34 @@ hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, int64_t full_lo
     hipLaunchKernelGGL(k_is_valid<true>, dim3(grid), dim3(256), 0, st, v);
   else
     hipLaunchKernelGGL(k_is_valid<false>, dim3(grid), dim3(256), 0, st, v);
+  return hipGetLastError();
+}
+hipError_t launch_is_valid_peaks(const uint64_t* valid, int64_t limit, int64_t full_lo, int64_t full_hi,
+                                 int64_t first_reach, const double* obs, int64_t n, const double* shifts, int n_w,
+                                 double tol, double prec, int8_t* out, hipStream_t st) {
+  if (n <= 0 || n_w <= 0) return hipSuccess;
+  const int grid = (int)blocks_for(n, 256);
+  ValidArgs v{valid, limit, full_lo, full_hi, first_reach, obs, nullptr, n, tol, prec, 1.0 / prec, out};
+  PeakShifts sh{};
+  for (int k = 0; k < n_w; ++k) sh.shift[k] = shifts[k];
+  switch (n_w) {  // the reference's breakage dicts: 4 weights (FULL_BREAKAGE_DICT: up to 16)
+    case 1: hipLaunchKernelGGL(k_is_valid_peaks<1>, dim3(grid), dim3(256), 0, st, v, sh); break;
+    case 2: hipLaunchKernelGGL(k_is_valid_peaks<2>, dim3(grid), dim3(256), 0, st, v, sh); break;
+    case 3: hipLaunchKernelGGL(k_is_valid_peaks<3>, dim3(grid), dim3(256), 0, st, v, sh); break;
+    case 4: hipLaunchKernelGGL(k_is_valid_peaks<4>, dim3(grid), dim3(256), 0, st, v, sh); break;
+    default:
+      for (int k0 = 0; k0 < n_w; k0 += 4) {  // four weights per launch, output block k0 on
+        const int m = n_w - k0 < 4 ? n_w - k0 : 4;
+        PeakShifts s2{};
+        for (int k = 0; k < m; ++k) s2.shift[k] = shifts[k0 + k];
+        ValidArgs v2 = v;
+        v2.out = out + (size_t)k0 * n;
+        if (m == 4) hipLaunchKernelGGL(k_is_valid_peaks<4>, dim3(grid), dim3(256), 0, st, v2, s2);
+        if (m == 3) hipLaunchKernelGGL(k_is_valid_peaks<3>, dim3(grid), dim3(256), 0, st, v2, s2);
+        if (m == 2) hipLaunchKernelGGL(k_is_valid_peaks<2>, dim3(grid), dim3(256), 0, st, v2, s2);
+        if (m == 1) hipLaunchKernelGGL(k_is_valid_peaks<1>, dim3(grid), dim3(256), 0, st, v2, s2);
+      }
+  }
   return hipGetLastError();
 }
 size_t scan_dyn_lds(const TableArgs& t) {

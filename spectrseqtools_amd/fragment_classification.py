@@ -11,7 +11,6 @@ for all of them (the config-5 pipeline harness, tools/pipeline_bench.py).
 import numpy as np
 
 from .frame import as_columns, like
-from .mass_explanation import is_valid_masses
 from .mass_table import DynamicProgrammingTable
 
 MAX_VARIANCE = 1  # fragment_classification.py:8
@@ -29,6 +28,24 @@ def is_singletons(masses, integer_masses, dp_table: DynamicProgrammingTable, thr
     eng = dp_table.device_table.engine
     out = eng.is_singleton(integer_masses, masses, thresholds, dp_table.tolerance, dp_table.precision)
     return np.asarray(out).astype(bool)
+
+
+def valid_peaks(observed, breakage_dict, dp_table: DynamicProgrammingTable):
+    """is_valid_mass over every peak x breakage weight (:52-67) in one engine
+    call reading each peak once (sst_is_valid_peaks): bool[len(dict) * n],
+    breakage-major.  Raises the reference's NotImplementedError for the first
+    row whose window leaves the table."""
+    from .mass_explanation import _not_in_table, first_value_beyond
+
+    obs = np.ascontiguousarray(observed, dtype=np.float64)
+    shifts = np.array([w * dp_table.precision for w in breakage_dict], dtype=np.float64)
+    out = dp_table.device_table.is_valid_peaks(obs, shifts, dp_table.tolerance, dp_table.precision)
+    bad = np.flatnonzero(out < 0)
+    if len(bad):
+        k, p = divmod(int(bad[0]), len(obs))
+        raise NotImplementedError(_not_in_table(first_value_beyond(float(obs[p] - shifts[k]),
+                                                                   float(dp_table.tolerance * obs[p]), dp_table)))
+    return out.astype(bool)
 
 
 def _expand(fragment_masses, breakage_dict, precision, intensity_cutoff):
@@ -94,7 +111,8 @@ def classify_fragments(fragment_masses, dp_table: DynamicProgrammingTable, break
     cols = _expand(fragment_masses, breakage_dict, dp_table.precision, intensity_cutoff)
     su = cols["standard_unit_mass"]
     obs = np.asarray(cols["observed_mass"], dtype=np.float64)
-    valid = is_valid_masses(su, dp_table, thresholds=dp_table.tolerance * obs)
+    n = len(obs) // max(1, len(breakage_dict))
+    valid = valid_peaks(obs[:n], breakage_dict, dp_table)  # the concat repeats the peaks per weight
     keep = np.flatnonzero(valid)
     singleton = is_singletons(su[keep], [m.mass for m in dp_table.masses], dp_table,
                               thresholds=dp_table.tolerance * obs[keep]) if len(keep) else np.zeros(0, bool)
@@ -115,7 +133,15 @@ def classify_fragments_batch(spectra, dp_table: DynamicProgrammingTable, breakag
     parts = [_expand(f, breakage_dict, dp_table.precision, float(c)) for f, c in zip(spectra, cuts)]
     su = np.concatenate([p["standard_unit_mass"] for p in parts]) if parts else np.zeros(0)
     obs = np.concatenate([np.asarray(p["observed_mass"], dtype=np.float64) for p in parts]) if parts else np.zeros(0)
-    valid = is_valid_masses(su, dp_table, thresholds=dp_table.tolerance * obs)
+    # one engine call for every spectrum's peaks (each spectrum's rows are
+    # breakage-major over its own peaks: regroup the peaks-major answers)
+    B = len(breakage_dict)
+    peaks = [np.asarray(p["observed_mass"][:len(p["observed_mass"]) // max(1, B)], dtype=np.float64) for p in parts]
+    allp = np.concatenate(peaks) if peaks else np.zeros(0)
+    v = valid_peaks(allp, breakage_dict, dp_table).reshape(B, len(allp)) if len(allp) else np.zeros((B, 0), bool)
+    cuts_p = np.concatenate([[0], np.cumsum([len(x) for x in peaks])]).astype(np.int64)
+    valid = np.concatenate([v[:, cuts_p[j]:cuts_p[j + 1]].ravel() for j in range(len(peaks))]) if peaks else \
+        np.zeros(0, bool)
     keep = np.flatnonzero(valid)
     singleton = is_singletons(su[keep], [m.mass for m in dp_table.masses], dp_table,
                               thresholds=dp_table.tolerance * obs[keep]) if len(keep) else np.zeros(0, bool)

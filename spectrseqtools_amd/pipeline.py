@@ -62,8 +62,7 @@ def classify(obs, offsets, su_seq, dp_table, breakage_dict, intensity=None, inte
     """Stage 1 over S spectra: obs[offsets[s]:offsets[s+1]] are spectrum s's
     observed masses; su_seq[s] its SU sequence mass (dp_table.seq.su_mass of
     its own pipeline run)."""
-    from .fragment_classification import is_singletons
-    from .mass_explanation import is_valid_masses
+    from .fragment_classification import is_singletons, valid_peaks
 
     obs = np.asarray(obs, dtype=np.float64)
     offsets = np.asarray(offsets, dtype=np.int64)
@@ -82,7 +81,7 @@ def classify(obs, offsets, su_seq, dp_table, breakage_dict, intensity=None, inte
     brk = np.repeat(np.arange(B), len(obs))
     ob = np.tile(obs, B)
     su = ob - np.repeat(np.asarray(weights, dtype=np.float64) * dp_table.precision, len(obs))
-    valid = is_valid_masses(su, dp_table, thresholds=dp_table.tolerance * ob)
+    valid = valid_peaks(obs, breakage_dict, dp_table)  # one lane per peak, breakage-major like `su`
     keep = np.flatnonzero(valid)
     sing = is_singletons(su[keep], [m.mass for m in dp_table.masses], dp_table,
                          thresholds=dp_table.tolerance * ob[keep]) if len(keep) else np.zeros(0, bool)

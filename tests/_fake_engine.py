@@ -50,6 +50,13 @@ class FakeDeviceTable:
         self.calls += 1
         return oracle.is_valid_batch(self.table, 32, masses, thresholds, tolerance, precision=precision)
 
+    def is_valid_peaks(self, observed, shifts, tolerance, precision):
+        self.calls += 1
+        o = np.asarray(observed, dtype=np.float64)
+        su = np.concatenate([o - s for s in shifts]) if len(shifts) else np.zeros(0)
+        return oracle.is_valid_batch(self.table, 32, su, tolerance * np.tile(o, len(shifts)), tolerance,
+                                     precision=precision)
+
     def explain(self, masses, thresholds, tolerance, precision, max_mods, with_memo=True, cap=2 ** 32):
         self.calls += 1
         masses = np.asarray(masses, dtype=np.float64)
