@@ -11,8 +11,9 @@ spectra (10k spectra, ~1M peaks, full 104-mass /
         reference's sliding window emits (prediction.py:286-329), budget
         round(0.5*max_len)                  -> k_explain_main (+ deferred kernels)
   * N>1: spectra shard by rank (weak scaling: `--spectra` per GPU); each
-        step's complete result of every rank (A7 bytes, A8 status bytes, dense
-        hit list, dense payload: parallel.wire_pack) is gathered to rank 0 over
+        step's complete result of every rank (wire format v3, parallel.wire_pack:
+        2-bit A7 / A8 codes, 4 B per pair-path hit, the deferred hits' records
+        and payload; ~10 MB per rank per config-3 step) is gathered to rank 0 over
         RCCL on a second stream while the next step computes (--no-gather:
         results stay in each rank's HBM).
 value = peaks of all ranks / step time (max over ranks).
@@ -185,7 +186,8 @@ def main():
     from spectrseqtools_amd import _native
     from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
     from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
-    from spectrseqtools_amd.parallel import Gatherer, decode_hits, device_bytes, dist_env, wire_pack, wire_unpack
+    from spectrseqtools_amd.parallel import (Gatherer, canonical_digest, decode_hits, device_bytes, dist_env, pair_key,
+                                             wire_pack, wire_size, wire_unpack)
 
     rank, world, local = dist_env()
     if world != args.gpus:
@@ -245,19 +247,22 @@ def main():
         settled["n"] += 1
 
     def send(j):
-        """Step j's complete result of this rank -> rank 0 (wire format:
-        parallel.wire_pack -- A7 bytes, A8 status bytes, dense hit list, dense
-        payload; ~1 B/query + 16 B/hit)."""
+        """Step j's complete result of this rank -> rank 0 (wire format v3:
+        parallel.wire_pack -- 2-bit A7 and A8 codes, 4 B per pair-path hit,
+        which rank 0 expands from its own copy of the table's pair list, and
+        records + payload of the deferred paths' hits)."""
         r = results[j & 1]
         settle(r)  # host: the pass's header (routed windows / retries handled)
         hits, n_hits = r.hit_list_device()
+        refs, n_pair, pair_bytes, n_wg = r.pair_hits_device()
         st, _c, _o, pay, nb = r.device_views(arrays=False)
         with torch.cuda.stream(comm):
             comm.wait_event(pass_done[j & 1])
             if side is not None:
                 comm.wait_stream(side)
             wire = wire_pack(outs7[j & 1], device_bytes(st, n8, dev_t), device_bytes(hits, 16 * n_hits, dev_t),
-                             device_bytes(pay, nb, dev_t))
+                             device_bytes(pay, nb, dev_t), device_bytes(refs, 2 * n_pair, dev_t), n_pair, pair_bytes,
+                             n_wg, pkey)
             ev = torch.cuda.Event()
             ev.record(comm)
             copied[j & 1] = ev
@@ -304,7 +309,11 @@ def main():
     n_hits0, payload0 = ref.settle()
     ref_digest = result_digest(ref)
     if gath is not None:
-        gath.agree(64 + (n7 + 3) // 4 + (n8 + 3) // 4 + 12 * n_hits0 + payload0)
+        precs = tdev.pair_records()
+        pkey = pair_key(precs)
+        _r, n_pair0, pair_bytes0, _w = ref.pair_hits_device()
+        gath.agree(wire_size(n7, n8, n_hits0, payload0, n_pair0, pair_bytes0))
+        ref_canon = canonical_digest(ref.status, ref.count, ref.offset, ref.payload)
     for k in range(args.warmup):
         step(k)
     drain(args.warmup - 1)
@@ -359,19 +368,15 @@ def main():
     if gath is not None:
         # rank 0 decodes what it received from every rank in the last step:
         # each rank's result digest must match (and its A7 bytes)
-        import hashlib
 
-        mine = torch.tensor(np.frombuffer(bytes.fromhex(ref_digest), dtype=np.uint8).copy(), device=dev_t)
+        mine = torch.tensor(np.frombuffer(bytes.fromhex(ref_canon), dtype=np.uint8).copy(), device=dev_t)
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         if rank == 0 and not args.no_validate:
             for r_, (buf, want) in enumerate(zip(gath.last, allr)):
-                v_, st_, hits_, pay_ = wire_unpack(buf.cpu().numpy())
+                v_, st_, hits_, pay_ = wire_unpack(buf.cpu().numpy(), precs)
                 cnt_, off_ = decode_hits(st_, hits_)
-                h = hashlib.sha256()
-                for a_ in (st_, cnt_, off_, pay_):
-                    h.update(np.ascontiguousarray(a_).tobytes())
-                if h.digest() != bytes(want.cpu().numpy()):
+                if bytes.fromhex(canonical_digest(st_, cnt_, off_, pay_)) != bytes(want.cpu().numpy()):
                     raise RuntimeError(f"rank {r_}'s gathered result does not decode to its own result")
     if (st < -2).any() and not args.no_validate:
         raise RuntimeError(f"internal statuses in results: {np.unique(st[st < -2])}")
@@ -476,6 +481,7 @@ def main():
                              f"parallel.wire_pack), overlapped with the next step"
                              if gath is not None else f"spectra sharded over {world} GPUs, results kept per rank")
                             if world > 1 else "1 GPU"),
+            "wire_bytes_per_rank_step": (gath.sizes if gath is not None else None),
         },
         "roofline": {
             "bound": "hbm",

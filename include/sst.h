@@ -208,6 +208,25 @@ int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint
  * (the wire format bench.py --gather sends over RCCL).  Valid until the next
  * pass on this result or its free.  No reference equivalent. */
 int sst_result_hit_list(sst_result* r, void** d_hits, uint64_t* n_hits);
+/* The pair-path part of a device-path result (settles it first): its first
+ * *n_pair_hits dense records are the hits the scan answered from the pair
+ * list, and their candidates occupy the first *pair_bytes of the dense
+ * payload.  d_refs (u16, one per such record): the first pair-list entry of
+ * the query's candidates (entries first .. first + count - 1, records as
+ * sst_table_pair_records returns them), | 0x8000 for OVERFLOW.  The records
+ * come in the scan's order: workgroup b < *n_scan_wg, its wave w < 16, then
+ * that wave's tiles (64 queries each; wave w of workgroup b takes tiles
+ * v, v + 16 * n_scan_wg, ... with v = ((w >> 1) * n_scan_wg + b) * 2 + (w & 1)),
+ * ascending query within a tile.  0 pair hits after passes that were not
+ * fused (host entry points, retries, tables without the pair list).  With
+ * the status codes this is the whole pair-path result in ~4 B per hit and
+ * no payload (parallel.wire_pack).  No reference equivalent. */
+int sst_result_pair_hits(sst_result* r, void** d_refs, uint64_t* n_pair_hits, uint64_t* pair_bytes, int* n_scan_wg);
+/* The table's pair list: payload record of entry e (u32: [k][row..] in its
+ * low 2-3 bytes, the bytes sst_result_host's payload holds for that
+ * candidate); *n = 0 for tables without the list.  recs may be NULL (size
+ * query). */
+int sst_table_pair_records(sst_table* t, uint32_t* recs, int64_t cap, int64_t* n);
 /* Copy device results to the host views (synchronises the ctx stream). */
 int sst_result_fetch(sst_result* r);
 void sst_result_free(sst_result* r);

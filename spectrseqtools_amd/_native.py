@@ -27,7 +27,8 @@ EXPORTS = (
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
     "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
-    "sst_window_pairs", "sst_is_valid_peaks", "sst_is_valid_peaks_device",
+    "sst_window_pairs", "sst_is_valid_peaks", "sst_is_valid_peaks_device", "sst_result_pair_hits",
+    "sst_table_pair_records",
 )
 
 # kernel ids of sst_profile_read
@@ -120,6 +121,10 @@ def load_library(path=LIB_PATH):
     lib.sst_is_valid_peaks_device.argtypes = [_P, _P, _I64, _P, _I, _D, _D, _P]
     lib.sst_window_pairs.argtypes = [_P, _P, _I64, _D, _P, _P, _I64]
     lib.sst_window_pairs.restype = _I64
+    lib.sst_result_pair_hits.argtypes = [_P, _PP, ctypes.POINTER(_U64), ctypes.POINTER(_U64), ctypes.POINTER(_I)]
+    lib.sst_result_pair_hits.restype = _I
+    lib.sst_table_pair_records.argtypes = [_P, _P, _I64, ctypes.POINTER(_I64)]
+    lib.sst_table_pair_records.restype = _I
     return lib
 
 
@@ -325,6 +330,16 @@ class ExplainResult:
                           "sst_result_hit_list")
         return p.value, int(nh.value)
 
+    def pair_hits_device(self):
+        """(refs device pointer, n_pair_hits, pair_bytes, n_scan_wg): the
+        pair-path part of the dense hit list (sst_result_pair_hits)."""
+        p = ctypes.c_void_p()
+        nh, nb, wg = _U64(), _U64(), _I()
+        self.engine.check(self.engine._lib.sst_result_pair_hits(self.handle, ctypes.byref(p), ctypes.byref(nh),
+                                                                ctypes.byref(nb), ctypes.byref(wg)),
+                          "sst_result_pair_hits")
+        return p.value, int(nh.value), int(nb.value), int(wg.value)
+
     def fetch_device(self):
         self.engine.check(self.engine._lib.sst_result_fetch(self.handle), "sst_result_fetch")
         return self.fetch()
@@ -401,6 +416,18 @@ class DeviceTable:
         self.engine.check(self.engine._lib.sst_table_set_budgets(self.handle, _ptr(m), _ptr(c)),
                           "sst_table_set_budgets")
         self._budgets = key
+
+    def pair_records(self):
+        """u32 payload record per pair-list entry (sst_table_pair_records);
+        empty for tables without the list."""
+        L = self.engine._lib
+        n = _I64()
+        self.engine.check(L.sst_table_pair_records(self.handle, None, 0, ctypes.byref(n)), "sst_table_pair_records")
+        out = np.zeros(n.value, np.uint32)
+        if n.value:
+            self.engine.check(L.sst_table_pair_records(self.handle, _ptr(out), n.value, ctypes.byref(n)),
+                              "sst_table_pair_records")
+        return out
 
     def download(self):
         out = np.empty((self.n_rows, self.n_cols), dtype=_DT[self.compression])

@@ -90,6 +90,7 @@ struct sst_table {
   std::vector<uint8_t> is_mod;
   std::vector<int64_t> cap;
   DevBuf packed, index, valid, w, capd, modd, pairs;
+  std::vector<uint32_t> pair_recs;  // the pair list's payload records (host copy)
   int scan_blocks = 0;  // resident workgroups of k_explain_scan (depends on the LDS pair list size)
   bool closure = false;  // built here from masses >= C: rows are true closures (layered fast paths valid)
   TableArgs args{};
@@ -104,7 +105,7 @@ struct sst_result {
   DevBuf status, hits, dense;
   // pass workspaces: the arena (scan-wave regions + spill area), control
   // blocks, class lists, scan worklists / hit records, tallies, deferred hits
-  DevBuf payload, ctl, lists, wave_stats, work, work_count, tally, wg_tally, dhits, hdr, agg;
+  DevBuf payload, ctl, lists, wave_stats, work, work_count, tally, wg_tally, dhits, hdr, agg, refs;
   DevBuf count, offset;  // per-query arrays: only built for sst_result_device callers that ask for them
   uint64_t* hdr_host = nullptr;  // host-mapped copy of the pack kernel's header (host address)
   uint64_t* hdr_host_dev = nullptr;  // its device address
@@ -136,6 +137,11 @@ struct sst_result {
   } pass{};
   uint64_t arena_bytes = 0;
   uint64_t n_hits = 0, payload_bytes = 0;
+  // the fused scan's part of the result (its header): the first scan_hits
+  // dense records are pair-path hits with refs[], their payload the first
+  // scan_bytes of the dense payload (0 / 0 after an unfused pass)
+  bool scan_hdr_pending = false;
+  uint64_t scan_hits = 0, scan_bytes = 0;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
   std::vector<uint8_t> h_payload;
@@ -295,6 +301,7 @@ int build_pair_list(sst_table* t, bool self_built) {
     const int64_t delta = k < n_e ? std::min<int64_t>((int64_t)e[k].sum - start, 0xFFFF) : 0xFFFF;
     bk[b] = (uint32_t)k | (uint32_t)delta << 16;
   }
+  t->pair_recs.assign(recs, recs + n_e);  // host copy (sst_table_pair_records)
   t->args.pair_shift = shift;
   img.resize((img.size() + 3) / 4 * 4, 0u);  // the scan stages it in 16-B pieces
   if (!t->pairs.ensure(img.size() * 4)) return fail(c, SST_E_NOMEM, "device allocation failed (pair list)");
@@ -731,7 +738,7 @@ constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses pe
 
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->hits, &r->dense, &r->payload, &r->ctl, &r->lists, &r->wave_stats, &r->work,
-                    &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->count, &r->offset})
+                    &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->refs, &r->count, &r->offset})
     b->release();
   if (r->hdr_host) (void)hipHostFree(r->hdr_host);
   r->hdr_host = nullptr;
@@ -771,6 +778,7 @@ OutArgs out_args(sst_result* r) {
   o.agg = (uint64_t*)r->agg.p + (size_t)r->parity * r->n_wg;
   o.agg_next = (uint64_t*)r->agg.p + (size_t)(r->parity ^ 1) * r->n_wg;
   o.hits_out = (uint4*)r->hits.p;
+  o.hit_refs = (uint16_t*)r->refs.p;
   o.dense = (uint8_t*)r->dense.p;
   o.hdr = (uint64_t*)r->hdr.p;
   o.hdr_host = r->hdr_host_dev;
@@ -925,6 +933,8 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   // deferred-class launch follows it in this pass
   const bool fused = !eager_tail && !r->bitset_scan;
   r->fused_pass = fused;
+  r->scan_hdr_pending = fused;
+  r->scan_hits = r->scan_bytes = 0;
   if (fused) {
     o.fused = 1;
     o.pass_id = ++r->pack_seq;
@@ -968,7 +978,7 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out) {
   r->region_bytes = std::max<uint64_t>(2048, round16(16 * r->work_region));
   r->spill_bytes = round16(std::max<uint64_t>(1u << 20, 2 * (uint64_t)nn));
   void* hh = nullptr;
-  bool ok = r->status.ensure(nn) && r->hits.ensure(nn * 16) && r->dhits.ensure(nn * 16) &&
+  bool ok = r->status.ensure(nn) && r->hits.ensure(nn * 16) && r->refs.ensure(nn * 2) && r->dhits.ensure(nn * 16) &&
             r->wave_stats.ensure((size_t)r->n_scan_waves * kNumStats * 8) &&
             r->work.ensure((size_t)r->n_scan_waves * r->work_region * 16) &&
             r->work_count.ensure((size_t)r->n_scan_waves * 4) && r->tally.ensure((size_t)r->n_scan_waves * 8) &&
@@ -1030,6 +1040,11 @@ int settle(sst_result* r) {
   for (int attempt = 0;; ++attempt) {
     uint64_t h[kHdrWords];
     if (int rc = wait_header(r, h)) return rc;
+    if (r->scan_hdr_pending) {  // the fused scan's own header
+      r->scan_hits = h[kHdrHits];
+      r->scan_bytes = h[kHdrPayload];
+      r->scan_hdr_pending = false;
+    }
     if (h[kHdrRouted] && !r->tail_ran) {
       if (int rc = launch_tail(r->pass.t, r)) return rc;
       if (int rc = launch_pack(r, r->fused_pass ? h : nullptr)) return rc;
@@ -1300,6 +1315,28 @@ int sst_result_hit_list(sst_result* r, void** d_hits, uint64_t* n_hits) {
   if (int rc = settle(r)) return rc;
   *d_hits = r->hits.p;
   *n_hits = r->n_hits;
+  return SST_OK;
+}
+
+int sst_result_pair_hits(sst_result* r, void** d_refs, uint64_t* n_pair_hits, uint64_t* pair_bytes, int* n_scan_wg) {
+  if (!r) return SST_E_ARG;
+  sst_ctx* c = r->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = settle(r)) return rc;
+  if (d_refs) *d_refs = r->refs.p;
+  if (n_pair_hits) *n_pair_hits = r->scan_hits;
+  if (pair_bytes) *pair_bytes = r->scan_bytes;
+  if (n_scan_wg) *n_scan_wg = r->n_wg;
+  return SST_OK;
+}
+
+int sst_table_pair_records(sst_table* t, uint32_t* recs, int64_t cap, int64_t* n) {
+  if (!t || !n) return SST_E_ARG;
+  *n = t->args.pairs_enabled ? (int64_t)t->pair_recs.size() : 0;
+  if (!recs || *n == 0) return SST_OK;
+  if (cap < *n) return fail(t->ctx, SST_E_ARG, "pair records: buffer too small");
+  memcpy(recs, t->pair_recs.data(), (size_t)*n * 4);
   return SST_OK;
 }
 

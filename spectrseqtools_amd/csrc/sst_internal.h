@@ -142,6 +142,7 @@ struct OutArgs {
   uint64_t* agg;       // [n_wg] this pass
   uint64_t* agg_next;  // [n_wg] the next pass's: zeroed by block 0
   uint4* hits_out;     // dense hit list
+  uint16_t* hit_refs;  // per scan hit: its first pair-list entry | 0x8000 for OVERFLOW (sst_result_pair_hits)
   uint8_t* dense;      // dense payload
   uint64_t* hdr;       // device header
   uint64_t* hdr_host;  // host-mapped header (device address)

@@ -1714,6 +1714,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
       if (out.fused) {
         const uint64_t word = pb ? off : (uint64_t)cnt;  // OVERFLOW: the exact count, no payload
         out.hits_out[hbase + k] = make_uint4(r.x, cnt, (uint32_t)word, (uint32_t)(word >> 32));
+        out.hit_refs[hbase + k] = (uint16_t)(first | (pb ? 0u : 0x8000u));  // sst_result_pair_hits
       } else {
         *((uint2*)rec - 1 - k) = make_uint2(r.x, cnt | (pb << 16));
       }

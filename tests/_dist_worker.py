@@ -2,9 +2,10 @@
 multi-GPU layer's host logic on CPU -- sharding, the agreed-size gather of
 per-rank result buffers to rank 0, the engine's result wire format (each
 rank encodes oracle answers to its own queries exactly as the engine lays out
-a result: status bytes, dense hit list, dense payload; rank 0 decodes every
-query of every rank and checks it), and the max-over-ranks step time that
-bench.py reports."""
+a result: status bytes, dense hit list -- the pair-path hits first, in the
+scan's order, with their pair-list refs --, dense payload; rank 0 decodes
+every query of every rank from the wire and its copy of the pair list and
+checks it), and the max-over-ranks step time that bench.py reports."""
 import os
 import sys
 
@@ -15,8 +16,8 @@ import torch.distributed as dist
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(HERE, ".."), HERE]
 import _oracle as oracle  # noqa: E402  (test infrastructure: the answers each rank encodes)
-from spectrseqtools_amd.parallel import (Gatherer, candidates, decode_hits, dist_env, shard_by_weight,  # noqa: E402
-                                         shard_range, wire_pack, wire_unpack)
+from spectrseqtools_amd.parallel import (Gatherer, candidates, decode_hits, dist_env, pair_key,  # noqa: E402
+                                         scan_order_key, shard_by_weight, shard_range, wire_pack, wire_unpack)
 
 ROWS = [0, 305042, 306026, 329053, 345048]  # canonical alphabet (a 5 x 377 397 table)
 TOL, PREC, CAP = 1e-5, 1e-3, 1
@@ -41,23 +42,72 @@ def oracle_answers(table, alph, masses, thr):
     return out
 
 
-def engine_layout(answers):
-    """An engine result (include/sst.h) built from oracle answers: status
-    bytes, dense hit records {query, count, word lo, word hi}, dense payload."""
-    status, hits, payload = [], [], []
+def pair_list(rows):
+    """The scan's pair list for these row masses (sst_api.cpp build_pair_list):
+    every single row and every two-row sum below 3 * w_min, by (sum, top
+    row); (sums, payload records [k][rows] as u32)."""
+    w_min, e = min(rows[1:]), []
+    for r1 in range(1, len(rows)):
+        e.append((rows[r1], r1, 1 | (r1 << 8)))
+        for r2 in range(1, r1 + 1):
+            if rows[r1] + rows[r2] < 3 * w_min:
+                e.append((rows[r1] + rows[r2], r1, 2 | (r2 << 8) | (r1 << 16)))
+    e.sort(key=lambda x: (x[0], x[1]))
+    return np.array([x[0] for x in e], np.int64), np.array([x[2] for x in e], np.uint32)
+
+
+def rec_bytes(rec):
+    k = int(rec) & 0xFF
+    return [k] + [(int(rec) >> (8 * (j + 1))) & 0xFF for j in range(k)]
+
+
+def engine_layout(answers, masses, thr, sums, recs, n_wg):
+    """An engine result (include/sst.h) built from oracle answers, as a fused
+    device pass lays it out: status bytes; the dense hit list -- first the
+    pair-path hits (windows below 3 * w_min whose candidates are the pair-list
+    entries with sums in the window), in the scan's order, with their refs
+    (first entry | 0x8000 for OVERFLOW, sst_result_pair_hits), then the other
+    hits --; the dense payload (pair-path candidates + 2 pad bytes per query,
+    then the others').  Returns (status, hits, payload, refs, n_pair, pair_bytes)."""
+    n = len(answers)
+    w_min = min(ROWS[1:])
+    status = np.zeros(n, np.int8)
+    pair, other = [], []
     for i, (st, sols, n_empty) in enumerate(answers):
-        if st == 1 and sols and len(sols) > CAP:
-            status.append(-2)  # SST_OVERFLOW: exact count, no payload
+        if st == 1 and sols:
+            over = len(sols) > CAP
+            status[i] = -2 if over else 2  # SST_OVERFLOW: exact count, no payload
+            lo = int(np.rint(masses[i] / PREC)) - int(np.ceil(thr[i] / PREC))
+            hi = int(np.rint(masses[i] / PREC)) + int(np.ceil(thr[i] / PREC))
+            a, b = np.searchsorted(sums, max(lo, 1), "left"), np.searchsorted(sums, hi, "right")
+            ents = sorted(tuple(rec_bytes(r)[1:]) for r in recs[a:b])
+            if hi < 3 * w_min and ents == sorted(tuple(c) for c in sols):
+                pair.append((i, int(a), int(b - a), over))
+            else:
+                other.append((i, sols, over))
+        else:
+            status[i] = 1 if (st == 1 and n_empty) else 0
+    pair.sort(key=lambda x: int(scan_order_key([x[0]], n, n_wg)[0]))
+    hits, refs, payload = [], [], []
+    for i, first, cnt, over in pair:
+        refs.append(first | (0x8000 if over else 0))
+        if over:
+            hits.append([i, cnt, cnt, 0])
+        else:
+            hits.append([i, cnt, len(payload), 0])
+            for r in recs[first:first + cnt]:
+                payload += rec_bytes(r)
+            payload += [0, 0]  # the scan's 2 pad bytes after a query's candidates
+    pair_bytes = len(payload)
+    for i, sols, over in other:
+        if over:
             hits.append([i, len(sols), len(sols), 0])
-        elif st == 1 and sols:
-            status.append(2)
+        else:
             hits.append([i, len(sols), len(payload), 0])
             for c in sols:
                 payload += [len(c)] + list(c)
-        else:
-            status.append(1 if (st == 1 and n_empty) else 0)
-    return (np.array(status, np.int8), np.array(hits, np.uint32).reshape(-1, 4),
-            np.array(payload, np.uint8))
+    return (status, np.array(hits, np.uint32).reshape(-1, 4), np.array(payload, np.uint8),
+            np.array(refs, np.uint16), len(pair), pair_bytes)
 
 
 def main():
@@ -102,17 +152,21 @@ def main():
     alph = oracle.Alphabet(ROWS, [0] * 5, [20] * 5)
     masses, thr = rank_queries(rank)
     ans = oracle_answers(table, alph, masses, thr)
-    st, hits, pay = engine_layout(ans)
+    sums, recs = pair_list(ROWS)
+    n_wg = 1 + rank  # the scan grid differs per rank: each buffer carries its own
+    st, hits, pay, refs, n_pair, pair_bytes = engine_layout(ans, masses, thr, sums, recs, n_wg)
+    assert 0 < n_pair < len(hits)  # both kinds of hit records travel
     valid = np.array([oracle.is_valid(table, 32, m, t, TOL) for m, t in zip(masses, thr)], np.int8)
     wire = wire_pack(torch.from_numpy(valid), torch.from_numpy(st), torch.from_numpy(hits.view(np.uint8).ravel()),
-                     torch.from_numpy(pay))
+                     torch.from_numpy(pay), torch.from_numpy(refs.view(np.uint8)), n_pair, pair_bytes, n_wg,
+                     pair_key(recs))
     g2 = Gatherer(dist, torch.device("cpu"))
     g2.agree(wire.numel())
     got = g2.gather(wire)
     if rank == 0:
         n_checked = n_some = n_over = 0
         for r, buf in enumerate(got):
-            v_r, st_r, hits_r, pay_r = wire_unpack(buf.numpy())
+            v_r, st_r, hits_r, pay_r = wire_unpack(buf.numpy(), recs)
             m_r, t_r = rank_queries(r)
             want = oracle_answers(table, alph, m_r, t_r)
             assert np.array_equal(v_r, [oracle.is_valid(table, 32, m, t, TOL) for m, t in zip(m_r, t_r)])
@@ -122,7 +176,7 @@ def main():
                     assert st_r[i] == -2 and int(cnt[i]) == len(sols), (r, i)
                     n_over += 1
                 elif s0 == 1 and sols:
-                    assert st_r[i] == 2 and candidates(pay_r, cnt, off, i) == sols, (r, i)
+                    assert st_r[i] == 2 and sorted(candidates(pay_r, cnt, off, i)) == sols, (r, i)
                     n_some += 1
                 else:
                     assert st_r[i] == (1 if (s0 == 1 and n_empty) else 0), (r, i)

@@ -165,3 +165,55 @@ def test_hit_list_matches_result_arrays(engine, dev, rows):
     off = recs[:, 2].astype(np.uint64) | (recs[:, 3].astype(np.uint64) << np.uint64(32))
     assert np.array_equal(off[some], res.offset[q][some])
     assert (st == _native.SST_OVERFLOW).any()  # cap=50 leaves some queries over the cap
+
+
+def test_wire_pair_hits_roundtrip(engine, dev, rows):
+    """sst_result_pair_hits + parallel.wire_pack / wire_unpack (the N>1
+    gather's wire format v3) on a real device pass: the pair-path hits come
+    in the documented scan order (several tile rounds per wave), their refs
+    name the pair-list entries of their candidates (SOME and OVERFLOW), and
+    the decoded wire holds exactly the result's answers (canonical digest:
+    status, counts, every query's candidate bytes)."""
+    torch = pytest.importorskip("torch")
+    from spectrseqtools_amd.parallel import (canonical_digest, decode_hits, device_bytes, pair_key, scan_order_key,
+                                             wire_pack, wire_size, wire_unpack)
+
+    rng = np.random.default_rng(15)
+    m2, t2 = _queries(rng, rows, 600_000, 2)
+    m3, t3 = _queries(rng, rows, 3000, 3)
+    masses, thr = np.concatenate([m2, m3]), np.concatenate([t2, t3])
+    perm = rng.permutation(len(masses))
+    masses, thr = masses[perm], thr[perm]
+    n = len(masses)
+    dev_t = torch.device("cuda", engine.device)
+    dm = torch.from_numpy(masses).to(dev_t)
+    dt = torch.from_numpy(thr).to(dev_t)
+    torch.cuda.synchronize()
+    res = dev.explain_device(dm.data_ptr(), dt.data_ptr(), n, TOL, PREC, 10, cap=3)
+    hits_p, n_hits = res.hit_list_device()
+    refs_p, n_pair, pair_bytes, n_wg = res.pair_hits_device()
+    assert 0 < n_pair < n_hits and n_wg > 1
+    assert -(-((n + 63) // 64) // (16 * n_wg)) > 1  # several tile rounds per scan wave
+    st_p, _c, _o, pay_p, nb = res.device_views(arrays=False)
+    hits = device_bytes(hits_p, 16 * n_hits, dev_t)
+    recs = dev.pair_records()
+    wire = wire_pack(torch.zeros(5, dtype=torch.int8, device=dev_t), device_bytes(st_p, n, dev_t), hits,
+                     device_bytes(pay_p, nb, dev_t), device_bytes(refs_p, 2 * n_pair, dev_t), n_pair, pair_bytes,
+                     n_wg, pair_key(recs))
+    assert wire.numel() == wire_size(5, n, n_hits, nb, n_pair, pair_bytes)
+    res.fetch_device()
+    h = hits.cpu().numpy().view(np.uint32).reshape(-1, 4)
+    q = h[:n_pair, 0].astype(np.int64)
+    key = scan_order_key(q, n, n_wg)
+    assert (np.diff(key) > 0).all()  # the scan's order
+    refs = device_bytes(refs_p, 2 * n_pair, dev_t).cpu().numpy().view(np.uint16)
+    ovf = (refs >> 15).astype(bool)
+    assert np.array_equal(ovf, res.status[q] == _native.SST_OVERFLOW) and ovf.any()
+    for j in np.flatnonzero(~ovf)[:200]:  # refs name the candidates' pair-list entries
+        first, cnt = int(refs[j] & 0x7FFF), int(h[j, 1])
+        want = [tuple((int(r) >> (8 * (k + 1))) & 0xFF for k in range(int(r) & 0xFF)) for r in recs[first:first + cnt]]
+        assert res.candidates(int(q[j])) == want, j
+    v_, st_, hits_, pay_ = wire_unpack(wire.cpu().numpy(), recs)
+    cnt_, off_ = decode_hits(st_, hits_)
+    assert np.array_equal(st_, res.status)
+    assert canonical_digest(st_, cnt_, off_, pay_) == canonical_digest(res.status, res.count, res.offset, res.payload)
