@@ -105,7 +105,7 @@ struct sst_result {
   DevBuf status, hits, dense;
   // pass workspaces: the arena (scan-wave regions + spill area), control
   // blocks, class lists, scan worklists / hit records, tallies, deferred hits
-  DevBuf payload, ctl, lists, wave_stats, work, work_count, tally, wg_tally, dhits, hdr, agg, refs;
+  DevBuf payload, ctl, lists, wave_stats, work, work_count, tally, wg_tally, dhits, hdr, agg, refs, stage;
   DevBuf count, offset;  // per-query arrays: only built for sst_result_device callers that ask for them
   uint64_t* hdr_host = nullptr;  // host-mapped copy of the pack kernel's header (host address)
   uint64_t* hdr_host_dev = nullptr;  // its device address
@@ -738,7 +738,7 @@ constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses pe
 
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->hits, &r->dense, &r->payload, &r->ctl, &r->lists, &r->wave_stats, &r->work,
-                    &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->refs, &r->count, &r->offset})
+                    &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->refs, &r->stage, &r->count, &r->offset})
     b->release();
   if (r->hdr_host) (void)hipHostFree(r->hdr_host);
   r->hdr_host = nullptr;
@@ -765,6 +765,7 @@ OutArgs out_args(sst_result* r) {
   o.wave_stats = (unsigned long long*)r->wave_stats.p;
   o.work = (uint4*)r->work.p;
   o.work_count = (uint32_t*)r->work_count.p;
+  o.stage = (uint32_t*)r->stage.p;
   o.tally = (uint2*)r->tally.p;
   o.wg_tally = (uint2*)r->wg_tally.p;
   o.work_region = r->work_region;
@@ -981,6 +982,7 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out) {
   bool ok = r->status.ensure(nn) && r->hits.ensure(nn * 16) && r->refs.ensure(nn * 2) && r->dhits.ensure(nn * 16) &&
             r->wave_stats.ensure((size_t)r->n_scan_waves * kNumStats * 8) &&
             r->work.ensure((size_t)r->n_scan_waves * r->work_region * 16) &&
+            r->stage.ensure((size_t)r->n_scan_waves * r->work_region * 4) &&
             r->work_count.ensure((size_t)r->n_scan_waves * 4) && r->tally.ensure((size_t)r->n_scan_waves * 8) &&
             r->wg_tally.ensure((size_t)r->n_wg * 8) && r->hdr.ensure(kHdrWords * 8) &&
             r->agg.ensure((size_t)2 * r->n_wg * 8) &&

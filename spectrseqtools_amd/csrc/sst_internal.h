@@ -125,6 +125,7 @@ struct OutArgs {
   uint4* work;                // [n_scan_waves][work_region] queued SHALLOW {query, a, b, has_zero} from the
                               // front; the scan's hit records {query, count | bytes << 16} (uint2) from the back
   uint32_t* work_count;       // [n_scan_waves] worklist lengths (k_explain_scan)
+  uint32_t* stage;            // [n_scan_waves][work_region] the pair scan's deferred-class windows (query | class << 30)
   uint2* tally;               // [n_scan_waves] {hit records, region bytes used in 16-B units}
   uint2* wg_tally;            // [scan workgroups] the sums over its 16 waves
   uint64_t work_region;

@@ -1502,6 +1502,12 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   const __amdgpu_buffer_rsrc_t wl_rsrc = buf_rsrc(wl, wl_bytes);
   const __amdgpu_buffer_rsrc_t st_rsrc = buf_rsrc(out.status, n);
   uint32_t n_hit = 0;  // wave-uniform
+  // deferred-class windows (deep / exact / no-memo): staged in the wave's own
+  // slots during the tiles, copied to the class lists after them with one
+  // atomic per class per workgroup -- atomics of every wave on the shared
+  // class counters serialise (config 1: scan 80 -> 44 us without them)
+  uint32_t* const stage = out.stage + (uint64_t)wave * out.work_region;
+  uint32_t n_staged = 0, n_cls1 = 0, n_cls2 = 0, n_cls3 = 0;  // wave-uniform
   // Software pipeline, two tiles deep: a tile's inputs are loaded two tiles
   // ahead into one of two register sets that swap roles between the unrolled
   // steps (no copies), each load issued after the previous tile's two stores.
@@ -1567,7 +1573,12 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
         }
         if (!shallow) out.status[i] = st2;
       }
-      route_append(out, q.n, cls, i);
+      const uint64_t cb = __ballot(cls >= 0);
+      if (cls >= 0) stage[n_staged + mbcnt(cb)] = i | ((uint32_t)cls << 30);
+      n_staged += (uint32_t)__builtin_popcountll(cb);
+      n_cls1 += (uint32_t)__builtin_popcountll(__ballot(cls == 1));
+      n_cls2 += (uint32_t)__builtin_popcountll(__ballot(cls == 2));
+      n_cls3 += (uint32_t)__builtin_popcountll(__ballot(cls == 3));
       const uint64_t sb = __ballot(shallow);
       if (shallow) wl[n_work + mbcnt(sb)] = make_uint4(i, a, hi, zero ? kItemZero : 0u);
       n_work += (uint32_t)__builtin_popcountll(sb);
@@ -1603,7 +1614,6 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   if (lane == 0) {
     out.work_count[wave] = n_work;
     out.tally[wave] = make_uint2(n_hit, units);
-    if (n_work) atomicAdd(&out.counters[kClassShallow], n_work);  // lets an idle SHALLOW role exit at once
     if (!fits) {  // the host re-runs the pass with larger regions
       atomicAdd(out.arena_retries, (unsigned long long)max(n_hit, 1u));
       atomicMax(out.region_need, (unsigned long long)pay);
@@ -1612,12 +1622,26 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   wave_stats_flush(out, wave, lane, kStatPair, kStatPairPayload, st_q, st_payload);
   __shared__ uint2 wg_part[kScanWG / 64];
   __shared__ uint32_t wg_pre[2];
-  // this wave's hit records, counter adds and routed lists have landed
+  __shared__ uint32_t wg_cls[kScanWG / 64][kNumClasses];  // per wave: SHALLOW items, staged class windows
+  __shared__ uint32_t wg_cls_base[kNumClasses];
+  // this wave's hit records, staged windows and counter adds have landed
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) wg_part[w_in] = make_uint2(n_hit, units);
+  if (lane == 0) {
+    wg_part[w_in] = make_uint2(n_hit, units);
+    wg_cls[w_in][kClassShallow] = n_work;
+    wg_cls[w_in][1] = n_cls1;
+    wg_cls[w_in][2] = n_cls2;
+    wg_cls[w_in][3] = n_cls3;
+  }
   __syncthreads();
   uint32_t wg_h = 0, wg_u = 0;
+  if (threadIdx.x < kNumClasses) {  // the workgroup's class totals: one atomic each (SHALLOW: lets an idle role exit)
+    uint32_t tot = 0;
+    for (int k = 0; k < kScanWG / 64; ++k) tot += wg_cls[k][threadIdx.x];
+    wg_cls_base[threadIdx.x] = tot ? atomicAdd(&out.counters[threadIdx.x], tot) : 0u;
+  }
   if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the class adds are done before the totals are published
     for (int k = 0; k < kScanWG / 64; ++k) {
       wg_h += wg_part[k].x;
       wg_u += wg_part[k].y;
@@ -1701,6 +1725,26 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     }
     hbase = (uint64_t)wg_pre[0] + eh;
     pbase = ((uint64_t)wg_pre[1] + eu) << 4;
+  }
+  if (!out.fused) __syncthreads();  // wg_cls_base (the fused path synchronised after its look-back)
+  if (n_staged) {  // this wave's staged class windows -> the class lists, behind the waves before it
+    uint32_t run1 = wg_cls_base[1], run2 = wg_cls_base[2], run3 = wg_cls_base[3];
+    for (uint32_t k = 0; k < w_in; ++k) {
+      run1 += wg_cls[k][1];
+      run2 += wg_cls[k][2];
+      run3 += wg_cls[k][3];
+    }
+    for (uint32_t k0 = 0; k0 < n_staged; k0 += 64) {
+      const uint32_t k = k0 + lane;
+      const uint32_t item = k < n_staged ? stage[k] : 0u;
+      const uint32_t c = item >> 30;  // 0: no item
+      const uint64_t b1 = __ballot(c == 1), b2 = __ballot(c == 2), b3 = __ballot(c == 3);
+      const uint32_t slot = c == 1 ? run1 + mbcnt(b1) : (c == 2 ? run2 + mbcnt(b2) : run3 + mbcnt(b3));
+      if (c) out.lists[(int64_t)c * q.n + slot] = item & 0x3FFFFFFFu;
+      run1 += (uint32_t)__builtin_popcountll(b1);
+      run2 += (uint32_t)__builtin_popcountll(b2);
+      run3 += (uint32_t)__builtin_popcountll(b3);
+    }
   }
   // ---- the wave's hit records -> result: payload bytes from the LDS pair
   // list (one dword store per record, pair_store), dense 16-B records (fused)
