@@ -599,7 +599,7 @@ def main_config1(args, engine, dist, rank, world, dev_t):
     sample = np.unique(np.concatenate([np.arange(min(n, 21)), np.random.default_rng(3).integers(0, n, 400)]))
     for i in sample:
         st, sols, n_empty, _ = oracle.explain_table(table, 32, alph, mass[i], thr[i], dp.tolerance, int(mods[i]))
-        if sorted(res.candidates(i)) != sorted(sols):
+        if sorted(res.candidates(i)) != sorted(sols) and not args.no_validate:
             raise RuntimeError(f"config-1 query {i} differs from the oracle")
     stats = res.stats()
     if dist:

@@ -848,6 +848,10 @@ int launch_tail(sst_table* t, sst_result* r) {
               kNodeBudget};
   fold_scan_limits(t->args, q);
   OutArgs o = out_args(r);
+  {
+    static const char* dbg = getenv("SST_TAIL_DBG");  // DIAGNOSTIC
+    o.dbg = dbg ? atoi(dbg) : 0;
+  }
   ExactWs ws{(char*)c->ws_hash.p, (char*)c->ws_frames.p, (char*)c->ws_stacks.p, (uint64_t*)c->ws_epochs.p,
              c->hash_cap};
   Prof p(c, SST_K_EXPLAIN_DEEP);  // deep, no-memo and exact roles: one launch

@@ -508,6 +508,38 @@ struct MemSink {  // straight to the arena (deep / exact / overflowed shallow)
     for (int k = 0; k <= d; ++k) dst[pos + 1 + k] = st.row(d - k);
   }
 };
+// First 32 payload bytes of a deep-path lane kept in VGPRs during the
+// counting DFS, so that a window whose candidates fit needs no second DFS to
+// write them (config 1: one candidate of <= 9 bytes per query, 2x shorter
+// dependent chains).
+struct RegSinkDeep {
+  uint64_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  bool over = false;
+  __device__ __forceinline__ void byte(int p, uint64_t b) {
+    const uint64_t v = b << (8 * (p & 7));
+    switch (p >> 3) {
+      case 0: w0 |= v; break;
+      case 1: w1 |= v; break;
+      case 2: w2 |= v; break;
+      default: w3 |= v; break;
+    }
+  }
+  template <typename Stack>
+  __device__ __forceinline__ void put(const Stack& st, int d, uint64_t pos) {
+    if (over || pos + d + 2 > 32) {
+      over = true;
+      return;
+    }
+    byte((int)pos, (uint64_t)(d + 1));
+    for (int k = 0; k <= d; ++k) byte((int)pos + 1 + k, st.row(d - k));
+  }
+  __device__ __forceinline__ void flush(uint8_t* dst, uint64_t nbytes) const {
+    for (uint64_t p = 0; p < nbytes; ++p) {
+      const uint64_t w = p < 8 ? w0 : (p < 16 ? w1 : (p < 24 ? w2 : w3));
+      dst[p] = (uint8_t)(w >> (8 * (p & 7)));
+    }
+  }
+};
 // Sinks of the shallow path receive the (<= 3) rows ascending as scalars.
 struct CountSink3 {
   __device__ __forceinline__ void put(uint64_t, int, int, int, int) {}
@@ -1358,26 +1390,21 @@ __device__ __forceinline__ void pair_store(const PairLds& p, uint32_t first, uin
 // class lists, status pending), run the SHALLOW fast path on the rest (all
 // DFS state and the first 16 payload bytes in VGPRs), allocate payload in the
 // spill area and write the status byte and hit record.
-__device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArgs& q, const OutArgs& out, const Lds& s,
-                                              const uint4* wl, uint32_t k0, uint32_t nw, int lane, ShallowStats& st) {
-  const bool live = k0 + lane < nw;
-  int64_t i = 0, a = 0, b = -1;
+__device__ __forceinline__ void shallow_item(const TableArgs& t, const QueryArgs& q, const OutArgs& out, const Lds& s,
+                                             bool live, uint32_t i, int64_t a, int64_t b, uint32_t flags, int lane,
+                                             ShallowStats& st) {
   int8_t status = SST_NONE;
   bool deferred = false;
   RegSink sink;
   EnumOut eo{0, 0, 0, 0};
   int cls = -1;
   if (live) {
-    const uint4 item = wl[k0 + lane];  // {query, first window value >= 1, last, kItem* flags}
-    i = item.x;
-    a = item.y;
-    b = item.z;
     bool run = true;
-    if (item.w & kItemUnclassified) {  // from the pair-list scan: route it here
+    if (flags & kItemUnclassified) {  // from the bitset scan: route it here
       if (!window_has_roots(t.valid, a, b)) {
         run = false;
-      } else if (!(item.w & kItemNever) || b >= t.shallow_hi) {
-        cls = (item.w & kItemNever) ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
+      } else if (!(flags & kItemNever) || b >= t.shallow_hi) {
+        cls = (flags & kItemNever) ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
         run = false;
         deferred = true;
       }
@@ -1388,10 +1415,10 @@ __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArg
       st.nodes += eo.nodes;
     }
     status = eo.count ? (eo.count > q.cap_count ? SST_OVERFLOW : SST_SOME)
-                      : ((item.w & kItemZero) ? SST_EMPTY : SST_NONE);
+                      : ((flags & kItemZero) ? SST_EMPTY : SST_NONE);
     if (deferred) status = (int8_t)kStatusPending;
   }
-  route_append(out, q.n, cls, (uint32_t)i);
+  route_append(out, q.n, cls, i);
   const TileOut to = spill_alloc(out, lane, status == SST_SOME ? eo.bytes : 0, status);
   if (to.bytes) {
     if (!sink.over) {
@@ -1403,8 +1430,14 @@ __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArg
     }
   }
   // deferred queries: pending here, the deep / exact roles write their result
-  emit_result(out, live, (uint32_t)i, to.status, eo.count, to.off, !deferred);
+  emit_result(out, live, i, to.status, eo.count, to.off, !deferred);
   st.payload += to.bytes;
+}
+__device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArgs& q, const OutArgs& out, const Lds& s,
+                                              const uint4* wl, uint32_t k0, uint32_t nw, int lane, ShallowStats& st) {
+  const bool live = k0 + lane < nw;
+  const uint4 item = live ? wl[k0 + lane] : make_uint4(0, 1, 0, 0);  // {query, first window value >= 1, last, kItem* flags}
+  shallow_item(t, q, out, s, live, item.x, item.y, item.z, item.w, lane, st);
 }
 
 // 64 scan hit records -> dense records; returns the running payload offset
@@ -1507,7 +1540,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   // atomic per class per workgroup -- atomics of every wave on the shared
   // class counters serialise (config 1: scan 80 -> 44 us without them)
   uint32_t* const stage = out.stage + (uint64_t)wave * out.work_region;
-  uint32_t n_staged = 0, n_cls1 = 0, n_cls2 = 0, n_cls3 = 0;  // wave-uniform
+  uint32_t n_staged = 0, n_cls0 = 0, n_cls1 = 0, n_cls2 = 0, n_cls3 = 0;  // wave-uniform
   // Software pipeline, two tiles deep: a tile's inputs are loaded two tiles
   // ahead into one of two register sets that swap roles between the unrolled
   // steps (no copies), each load issued after the previous tile's two stores.
@@ -1559,29 +1592,26 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     n_hit += (uint32_t)__builtin_popcountll(hbal);
     if (__ballot(work)) {  // wave-uniform, rare here: route the window now, so that the deferred class lists
                            // are complete when the scan ends (one tail launch runs every class)
-      bool shallow = false;
       int cls = -1;
       if (work) {
         int8_t st2 = zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;  // no reachable value in the window
         if (window_has_roots(t.valid, a, hi)) {
           if (never && hi < t.shallow_hi) {
-            shallow = true;  // <= 3 items, budgets cannot bind: the SHALLOW role writes all three
+            cls = kClassShallow;  // <= 3 items, budgets cannot bind: the SHALLOW role writes all three
           } else {
             cls = never ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
             st2 = (int8_t)kStatusPending;
           }
         }
-        if (!shallow) out.status[i] = st2;
+        if (cls != kClassShallow) out.status[i] = st2;
       }
       const uint64_t cb = __ballot(cls >= 0);
       if (cls >= 0) stage[n_staged + mbcnt(cb)] = i | ((uint32_t)cls << 30);
       n_staged += (uint32_t)__builtin_popcountll(cb);
+      n_cls0 += (uint32_t)__builtin_popcountll(__ballot(cls == 0));
       n_cls1 += (uint32_t)__builtin_popcountll(__ballot(cls == 1));
       n_cls2 += (uint32_t)__builtin_popcountll(__ballot(cls == 2));
       n_cls3 += (uint32_t)__builtin_popcountll(__ballot(cls == 3));
-      const uint64_t sb = __ballot(shallow);
-      if (shallow) wl[n_work + mbcnt(sb)] = make_uint4(i, a, hi, zero ? kItemZero : 0u);
-      n_work += (uint32_t)__builtin_popcountll(sb);
     }
   };
   double mA = 0.0, tA = 0.0, mB = 0.0, tB = 0.0;
@@ -1628,7 +1658,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0) {
     wg_part[w_in] = make_uint2(n_hit, units);
-    wg_cls[w_in][kClassShallow] = n_work;
+    wg_cls[w_in][kClassShallow] = n_cls0;
     wg_cls[w_in][1] = n_cls1;
     wg_cls[w_in][2] = n_cls2;
     wg_cls[w_in][3] = n_cls3;
@@ -1728,22 +1758,25 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   }
   if (!out.fused) __syncthreads();  // wg_cls_base (the fused path synchronised after its look-back)
   if (n_staged) {  // this wave's staged class windows -> the class lists, behind the waves before it
-    uint32_t run1 = wg_cls_base[1], run2 = wg_cls_base[2], run3 = wg_cls_base[3];
-    for (uint32_t k = 0; k < w_in; ++k) {
-      run1 += wg_cls[k][1];
-      run2 += wg_cls[k][2];
-      run3 += wg_cls[k][3];
+    uint32_t run[kNumClasses];
+#pragma unroll
+    for (int c = 0; c < kNumClasses; ++c) {
+      run[c] = wg_cls_base[c];
+      for (uint32_t k = 0; k < w_in; ++k) run[c] += wg_cls[k][c];
     }
     for (uint32_t k0 = 0; k0 < n_staged; k0 += 64) {
       const uint32_t k = k0 + lane;
-      const uint32_t item = k < n_staged ? stage[k] : 0u;
-      const uint32_t c = item >> 30;  // 0: no item
-      const uint64_t b1 = __ballot(c == 1), b2 = __ballot(c == 2), b3 = __ballot(c == 3);
-      const uint32_t slot = c == 1 ? run1 + mbcnt(b1) : (c == 2 ? run2 + mbcnt(b2) : run3 + mbcnt(b3));
-      if (c) out.lists[(int64_t)c * q.n + slot] = item & 0x3FFFFFFFu;
-      run1 += (uint32_t)__builtin_popcountll(b1);
-      run2 += (uint32_t)__builtin_popcountll(b2);
-      run3 += (uint32_t)__builtin_popcountll(b3);
+      const bool live = k < n_staged;
+      const uint32_t item = live ? stage[k] : 0u;
+      const uint32_t cl = item >> 30;
+      uint32_t slot = 0;
+#pragma unroll
+      for (int c = 0; c < kNumClasses; ++c) {
+        const uint64_t bc = __ballot(live && cl == (uint32_t)c);
+        if (live && cl == (uint32_t)c) slot = run[c] + mbcnt(bc);
+        run[c] += (uint32_t)__builtin_popcountll(bc);
+      }
+      if (live) out.lists[(int64_t)cl * q.n + slot] = item & 0x3FFFFFFFu;
     }
   }
   // ---- the wave's hit records -> result: payload bytes from the LDS pair
@@ -1861,6 +1894,44 @@ __device__ __forceinline__ void expand_body(const TableArgs& t, const QueryArgs&
     const uint32_t nw = out.work_count[src];
     const uint4* wl = out.work + (uint64_t)src * out.work_region;
     for (uint32_t k0 = 0; k0 < nw; k0 += 64) shallow_chunk(t, q, out, s, wl, k0, nw, lane, st);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    st.q += __shfl_down(st.q, o, 64);
+    st.nodes += __shfl_down(st.nodes, o, 64);
+    st.payload += __shfl_down(st.payload, o, 64);
+  }
+  if (lane == 0 && st.q) {
+    atomicAdd(&out.stats[kStatShallow], (unsigned long long)st.q);
+    atomicAdd(&out.stats[kStatNodes], (unsigned long long)st.nodes);
+    atomicAdd(&out.stats[kStatPayload], (unsigned long long)st.payload);
+  }
+}
+// The SHALLOW role of k_explain_deferred after the pair scan: the scan
+// appended its <= 3-item windows (budgets cannot bind) to the dense class-0
+// list; one lane per window (recomputed from the query), the waves of the
+// role in a grid stride over the list.
+__device__ void shallow_list_body(const TableArgs& t, const QueryArgs& q, const OutArgs& out, Lds& s, int blk,
+                                  int nblk) {
+  const uint32_t n_list = out.counters[kClassShallow];
+  if (n_list == 0) return;  // block-uniform: nothing queued
+  stage_rows(s, t);
+  const int lane = threadIdx.x & 63;
+  const int64_t nthreads = (int64_t)nblk * 64;
+  ShallowStats st{0, 0, 0};
+  for (int64_t j0 = (int64_t)blk * 64; j0 < (int64_t)n_list; j0 += nthreads) {  // wave-uniform
+    const int64_t j = j0 + lane;
+    const bool live = j < (int64_t)n_list;
+    uint32_t i = 0, flags = 0;
+    int64_t a = 1, b = 0;
+    if (live) {
+      i = out.lists[(int64_t)kClassShallow * q.n + j];
+      int64_t lo, hi;
+      quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
+      flags = (lo <= 0 && hi >= 0) ? kItemZero : 0u;
+      a = lo < 1 ? 1 : lo;
+      b = hi;
+    }
+    shallow_item(t, q, out, s, live, i, a, b, flags, lane, st);
   }
   for (int o = 32; o > 0; o >>= 1) {
     st.q += __shfl_down(st.q, o, 64);
@@ -2057,6 +2128,7 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
     EnumOut eo{0, 0, 0, 0};
     int8_t status = SST_NONE;
     uint64_t bytes = 0;
+    RegSinkDeep rs;  // the candidates' first 32 bytes, written by the counting DFS
     if (live) {
       i = out.lists[(int64_t)cls * q.n + j];
       int64_t lo, hi;
@@ -2065,8 +2137,7 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
       const bool has_zero = lo <= 0 && hi >= 0;
       a = lo < 1 ? 1 : lo;
       b = hi;
-      CountSink cs;
-      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, cs, q.node_budget, eo);
+      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, rs, q.node_budget, eo);
       status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
       bytes = eo.bytes;
       if (eo.fail) {
@@ -2077,8 +2148,17 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
         bytes = 0;
       }
     }
+    if (out.dbg & 4) {  // DIAGNOSTIC 4: the counting DFS only
+      if (live) {
+        st_n++;
+        st_nodes += eo.nodes;
+      }
+      continue;
+    }
     const TileOut to = spill_alloc(out, lane, bytes, status);
-    if (to.bytes) {
+    if (to.bytes && !rs.over) {
+      rs.flush(out.payload + to.off, to.bytes);
+    } else if (to.bytes) {  // more than 32 bytes: enumerate again straight into the arena
       MemSink ms{out.payload + to.off, ~0ull};
       EnumOut e2{0, 0, 0, 0};
       enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2);
@@ -2175,10 +2255,11 @@ __global__ __launch_bounds__(64) void k_explain_deferred(TableArgs t, QueryArgs 
   __shared__ Lds s;
   int b = blockIdx.x;
   if (b < shallow_blocks) {
-    expand_body(t, q, out, s, b, shallow_blocks);
+    if (!(out.dbg & 1)) shallow_list_body(t, q, out, s, b, shallow_blocks);  // DIAGNOSTIC 1: no SHALLOW role
     return;
   }
   b -= shallow_blocks;
+  if (out.dbg & 2) return;  // DIAGNOSTIC 2: no deep / exact roles
   if (b < deep_blocks)
     deep_body<MODE_FAST>(t, q, out, kClassDeep, ws_deep, s, b, deep_blocks);
   else if (b < 2 * deep_blocks)  // second half of the deep workspace

@@ -1,0 +1,10 @@
+cd /root/repo; export TMPDIR=/tmp
+for v in 0 1 2 4 0; do
+  export SST_TAIL_DBG=$v
+  rm -rf gpurun_out/td_$v
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/td_$v -o run -- python3 bench.py --workload config1 --steps 20 --no-cpu-baseline --no-validate > gpurun_out/td_$v.json 2> gpurun_out/td_$v.err || exit $?
+  f=$(find gpurun_out/td_$v -name "*kernel_stats.csv" | head -1)
+  python3 -c "
+import csv
+print('$v', [(r['Name'].split('(')[0].replace('void ','').replace('sst::',''), round(float(r['AverageNs'])/1e3,1)) for r in csv.DictReader(open('$f')) if 'k_explain' in r['Name']])"
+done
