@@ -1540,7 +1540,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   // atomic per class per workgroup -- atomics of every wave on the shared
   // class counters serialise (config 1: scan 80 -> 44 us without them)
   uint32_t* const stage = out.stage + (uint64_t)wave * out.work_region;
-  uint32_t n_staged = 0, n_cls0 = 0, n_cls1 = 0, n_cls2 = 0, n_cls3 = 0;  // wave-uniform
+  uint32_t n_staged = 0;  // wave-uniform (one SGPR in the tile loop: the per-class counts are taken after it)
   // Software pipeline, two tiles deep: a tile's inputs are loaded two tiles
   // ahead into one of two register sets that swap roles between the unrolled
   // steps (no copies), each load issued after the previous tile's two stores.
@@ -1592,26 +1592,21 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     n_hit += (uint32_t)__builtin_popcountll(hbal);
     if (__ballot(work)) {  // wave-uniform, rare here: route the window now, so that the deferred class lists
                            // are complete when the scan ends (one tail launch runs every class)
+      // (the class's role reads the window's bitset words itself: a window
+      // without reachable values costs it one look; none here keeps the
+      // tile loop free of scattered loads)
       int cls = -1;
       if (work) {
-        int8_t st2 = zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;  // no reachable value in the window
-        if (window_has_roots(t.valid, a, hi)) {
-          if (never && hi < t.shallow_hi) {
-            cls = kClassShallow;  // <= 3 items, budgets cannot bind: the SHALLOW role writes all three
-          } else {
-            cls = never ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
-            st2 = (int8_t)kStatusPending;
-          }
+        if (never && hi < t.shallow_hi) {
+          cls = kClassShallow;  // <= 3 items, budgets cannot bind: the SHALLOW role writes the result
+        } else {
+          cls = never ? kClassDeep : (q.with_memo ? kClassExact : kClassNomemo);
+          out.status[i] = (int8_t)kStatusPending;
         }
-        if (cls != kClassShallow) out.status[i] = st2;
       }
       const uint64_t cb = __ballot(cls >= 0);
       if (cls >= 0) stage[n_staged + mbcnt(cb)] = i | ((uint32_t)cls << 30);
       n_staged += (uint32_t)__builtin_popcountll(cb);
-      n_cls0 += (uint32_t)__builtin_popcountll(__ballot(cls == 0));
-      n_cls1 += (uint32_t)__builtin_popcountll(__ballot(cls == 1));
-      n_cls2 += (uint32_t)__builtin_popcountll(__ballot(cls == 2));
-      n_cls3 += (uint32_t)__builtin_popcountll(__ballot(cls == 3));
     }
   };
   double mA = 0.0, tA = 0.0, mB = 0.0, tB = 0.0;
@@ -1656,12 +1651,17 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   __shared__ uint32_t wg_cls_base[kNumClasses];
   // this wave's hit records, staged windows and counter adds have landed
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint32_t n_cls[kNumClasses] = {0u, 0u, 0u, 0u};
+  for (uint32_t k0 = 0; k0 < n_staged; k0 += 64) {  // its staged windows per class
+    const uint32_t k = k0 + lane;
+    const uint32_t cl = k < n_staged ? stage[k] >> 30 : 4u;
+#pragma unroll
+    for (int c = 0; c < kNumClasses; ++c) n_cls[c] += (uint32_t)__builtin_popcountll(__ballot(cl == (uint32_t)c));
+  }
   if (lane == 0) {
     wg_part[w_in] = make_uint2(n_hit, units);
-    wg_cls[w_in][kClassShallow] = n_cls0;
-    wg_cls[w_in][1] = n_cls1;
-    wg_cls[w_in][2] = n_cls2;
-    wg_cls[w_in][3] = n_cls3;
+#pragma unroll
+    for (int c = 0; c < kNumClasses; ++c) wg_cls[w_in][c] = n_cls[c];
   }
   __syncthreads();
   uint32_t wg_h = 0, wg_u = 0;
