@@ -264,6 +264,23 @@ int sst_length_bound_batch(sst_table* t, const double* su_mass, const double* ob
  * beyond cap written, call again with more room) or a negative SST_E* code. */
 int64_t sst_window_pairs(const double* su, const int64_t* offsets, int64_t n_sides, double max_weight,
                          int64_t* start_out, int64_t* end_out, int64_t cap);
+/* The first filter_by_explanation round's queries over many spectra
+ * (spectrseqtools/prediction.py:261-329, collect_diff_explanations_for_su):
+ * spectrum g's rows su/obs[offsets[g] .. offsets[g+1]) (classify_fragments'
+ * rows, ascending SU mass); flags per row: 1 START side, 2 END side, 4
+ * singleton.  Per spectrum, in the reference's order: the START side's
+ * sliding-window pairs, the END side's, then the singletons: diff = su[end] -
+ * su[start] (a singleton: its su), thr = tolerance * (obs[start] + obs[end])
+ * (a singleton: tolerance * obs), spec = g, kind = 0 / 1 / 2.  Returns the
+ * number of queries (> cap: nothing beyond cap written) or SST_E*. */
+int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* flags, const int64_t* offsets,
+                            int64_t n_spec, double max_weight, double tolerance, double* diff, double* thr,
+                            int64_t* spec, int8_t* kind, int64_t cap);
+/* order[0..n): the row permutation that sorts by group (0 <= group < n_groups)
+ * then key ascending, ties in row order -- classify_fragments' per-spectrum
+ * sort by standard_unit_mass (fragment_classification.py:84), for many
+ * spectra (numpy.lexsort((rows, key, group))). */
+int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_groups, int64_t* order);
 
 /* ---- measurement ------------------------------------------------------ */
 /* Kernel ids for sst_profile_read. */

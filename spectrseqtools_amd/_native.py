@@ -28,7 +28,7 @@ EXPORTS = (
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
     "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
     "sst_window_pairs", "sst_is_valid_peaks", "sst_is_valid_peaks_device", "sst_result_pair_hits",
-    "sst_table_pair_records",
+    "sst_table_pair_records", "sst_su_diff_queries", "sst_sort_rows",
 )
 
 # kernel ids of sst_profile_read
@@ -125,6 +125,10 @@ def load_library(path=LIB_PATH):
     lib.sst_result_pair_hits.restype = _I
     lib.sst_table_pair_records.argtypes = [_P, _P, _I64, ctypes.POINTER(_I64)]
     lib.sst_table_pair_records.restype = _I
+    lib.sst_su_diff_queries.argtypes = [_P, _P, _P, _P, _I64, _D, _D, _P, _P, _P, _P, _I64]
+    lib.sst_su_diff_queries.restype = _I64
+    lib.sst_sort_rows.argtypes = [_P, _P, _I64, _I64, _P]
+    lib.sst_sort_rows.restype = _I
     return lib
 
 
@@ -142,6 +146,39 @@ def lib():
 
 def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def su_diff_queries(su, obs, flags, offsets, max_weight, tolerance):
+    """sst_su_diff_queries: (diff, thr, spec, kind) of the first
+    filter_by_explanation round over many spectra (host code)."""
+    su = np.ascontiguousarray(su, dtype=np.float64)
+    obs = np.ascontiguousarray(obs, dtype=np.float64)
+    flags = np.ascontiguousarray(flags, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    L = lib()
+    cap = max(16, 8 * len(su))
+    while True:
+        d, t = np.empty(cap, np.float64), np.empty(cap, np.float64)
+        g, k = np.empty(cap, np.int64), np.empty(cap, np.int8)
+        n = L.sst_su_diff_queries(_ptr(su), _ptr(obs), _ptr(flags), _ptr(offsets), len(offsets) - 1,
+                                  float(max_weight), float(tolerance), _ptr(d), _ptr(t), _ptr(g), _ptr(k), cap)
+        if n < 0:
+            raise EngineError(f"sst_su_diff_queries failed ({n})")
+        if n <= cap:
+            return d[:n], t[:n], g[:n], k[:n]
+        cap = int(n)
+
+
+def sort_rows(group, key, n_groups):
+    """sst_sort_rows: permutation sorting by group, then key, ties in row
+    order (numpy.lexsort((rows, key, group)); host code)."""
+    group = np.ascontiguousarray(group, dtype=np.int64)
+    key = np.ascontiguousarray(key, dtype=np.float64)
+    order = np.empty(len(group), np.int64)
+    rc = lib().sst_sort_rows(_ptr(group), _ptr(key), len(group), int(n_groups), _ptr(order))
+    if rc:
+        raise EngineError(f"sst_sort_rows failed ({rc})")
+    return order
 
 
 def window_pairs(su, offsets, max_weight):

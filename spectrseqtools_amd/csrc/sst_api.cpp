@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "sst.h"
@@ -1591,4 +1592,99 @@ int64_t sst_window_pairs(const double* su, const int64_t* offsets, int64_t n_sid
     }
   }
   return k;
+}
+
+// One side's sliding window (the state machine above) over rows idx[0..n):
+// emits the pairs through f(a, b) in the reference's order.
+template <typename F>
+static void window_side(const double* su, const int64_t* idx, int64_t n, double max_weight, F&& f) {
+  int64_t start = 0, end = 1;
+  while (end < n) {
+    if (end - start <= 0) {
+      ++end;
+      continue;
+    }
+    if (su[idx[end]] - su[idx[start]] > max_weight) {
+      ++start;
+      end = start + 1;
+      continue;
+    }
+    f(idx[start], idx[end]);
+    if (end == n - 1)
+      ++start;
+    else
+      ++end;
+  }
+}
+
+int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* flags, const int64_t* offsets,
+                            int64_t n_spec, double max_weight, double tolerance, double* diff, double* thr,
+                            int64_t* spec, int8_t* kind, int64_t cap) {
+  if (n_spec < 0 || (n_spec > 0 && (!su || !obs || !flags || !offsets)) || cap < 0 ||
+      (cap > 0 && (!diff || !thr || !spec || !kind)))
+    return SST_E_ARG;
+  int64_t k = 0;
+  std::vector<int64_t> side;
+  for (int64_t g = 0; g < n_spec; ++g) {
+    const int64_t lo = offsets[g], hi = offsets[g + 1];
+    if (hi < lo) return SST_E_ARG;
+    for (int sd = 0; sd < 2; ++sd) {  // START pairs, then END pairs (prediction.py:261-329)
+      side.clear();
+      for (int64_t r = lo; r < hi; ++r)
+        if (flags[r] & (1u << sd)) side.push_back(r);
+      window_side(su, side.data(), (int64_t)side.size(), max_weight, [&](int64_t a, int64_t b) {
+        if (k < cap) {
+          diff[k] = su[b] - su[a];
+          thr[k] = tolerance * (obs[a] + obs[b]);
+          spec[k] = g;
+          kind[k] = (int8_t)sd;
+        }
+        ++k;
+      });
+    }
+    for (int64_t r = lo; r < hi; ++r)  // then the singletons' own masses
+      if (flags[r] & 4u) {
+        if (k < cap) {
+          diff[k] = su[r];
+          thr[k] = tolerance * obs[r];
+          spec[k] = g;
+          kind[k] = 2;
+        }
+        ++k;
+      }
+  }
+  return k;
+}
+
+int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_groups, int64_t* order) {
+  if (n < 0 || n_groups < 0 || (n > 0 && (!group || !key || !order))) return SST_E_ARG;
+  std::vector<int64_t> start((size_t)n_groups + 1, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    if (group[i] < 0 || group[i] >= n_groups) return SST_E_ARG;
+    ++start[(size_t)group[i] + 1];
+  }
+  for (int64_t g = 0; g < n_groups; ++g) start[(size_t)g + 1] += start[(size_t)g];
+  {
+    std::vector<int64_t> pos(start.begin(), start.end() - 1);
+    for (int64_t i = 0; i < n; ++i) order[pos[(size_t)group[i]]++] = i;  // stable: input order per group
+  }
+  // each group by key, ties in input order; groups split over a few threads
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const int64_t per = (n_groups + hw - 1) / hw;
+  auto work = [&](int64_t g0, int64_t g1) {
+    for (int64_t g = g0; g < g1; ++g)
+      std::stable_sort(order + start[(size_t)g], order + start[(size_t)g + 1],
+                       [&](int64_t a, int64_t b) { return key[a] < key[b]; });
+  };
+  if (n < (1 << 16) || hw == 1) {
+    work(0, n_groups);
+  } else {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < hw; ++t) {
+      const int64_t g0 = std::min<int64_t>(n_groups, (int64_t)t * per), g1 = std::min<int64_t>(n_groups, g0 + per);
+      if (g0 < g1) th.emplace_back(work, g0, g1);
+    }
+    for (auto& x : th) x.join();
+  }
+  return SST_OK;
 }

@@ -9,9 +9,9 @@ in flat arrays (spectrum id per row) instead of per-spectrum frames:
   1. classify   (fragment_classification.py:17-101): every peak x breakage
                  weight -> one is_valid batch, valid rows -> one is_singleton
                  batch, then the intensity / mass / sequence-mass filters and
-                 the per-spectrum SU-mass sort (lexsort);
+                 the per-spectrum SU-mass sort (sst_sort_rows, host-native);
   2. su_diffs   (prediction.py:261-329, the first filter_by_explanation
-                 round): every side's sliding-window pairs (sst_window_pairs,
+                 round): every side's sliding-window pairs (sst_su_diff_queries,
                  host-native) and the singleton masses -> one explain batch;
   3. bins       (skeleton_building.py:114-196, 372-421): every side's bins
                  (neighbouring SU differences within tolerance) and the
@@ -30,7 +30,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._native import window_pairs
+from ._native import sort_rows, su_diff_queries as _su_diff_queries
 from .masses import MATCHING_THRESHOLD, PHOSPHATE_LINK_MASS, TOLERANCE
 
 MAX_VARIANCE = 1  # fragment_classification.py:8
@@ -92,8 +92,9 @@ def classify(obs, offsets, su_seq, dp_table, breakage_dict, intensity=None, inte
     ok = (it > intensity_cutoff) & (ob[keep] < mass_cutoff) & (su[keep] < seq + MAX_VARIANCE) & \
          ((su[keep] > seq - MAX_VARIANCE) | ~full)
     rows, sing = keep[ok], sing[ok]
-    # the expanded position orders each spectrum's rows as its own concat (breakage, fragment)
-    order = np.lexsort((rows, su[rows], spec[rows]))
+    # the expanded position orders each spectrum's rows as its own concat (breakage,
+    # fragment): per spectrum by SU mass, ties in that order (host-native sort)
+    order = sort_rows(spec[rows], su[rows], S)
     rows, sing = rows[order], sing[order]
     off = np.searchsorted(spec[rows], np.arange(S + 1))
     return Classified(spec[rows], su[rows], ob[rows], frag[rows], brk[rows], sing, names, off, len(su), len(keep))
@@ -117,21 +118,13 @@ class Queries:
 
 def su_diff_queries(c: Classified, explanation_masses, tolerance=MATCHING_THRESHOLD):
     """Stage 2's queries: per spectrum the START-side pairs, the END-side
-    pairs, then the singletons (collect_diff_explanations_for_su's order)."""
+    pairs, then the singletons (collect_diff_explanations_for_su's order),
+    produced by host-native code in one pass (sst_su_diff_queries)."""
     max_w = max(explanation_masses.get_column("monoisotopic_mass").to_list()) + PHOSPHATE_LINK_MASS
-    parts = []
-    for k, side in enumerate(("START", "END")):
-        rows, off = _sides(c, side)
-        s, e = window_pairs(c.su[rows], off, max_w)
-        a, b = rows[s], rows[e]
-        parts.append((c.su[b] - c.su[a], tolerance * (c.obs[a] + c.obs[b]), c.spec[a], np.full(len(a), k)))
-    sg = np.flatnonzero(c.singleton)
-    parts.append((c.su[sg], tolerance * c.obs[sg], c.spec[sg], np.full(len(sg), 2)))
-    spec = np.concatenate([p[2] for p in parts])
-    kind = np.concatenate([p[3] for p in parts])
-    order = np.lexsort((kind, spec))  # stable: pairs keep their window order
-    return Queries(np.concatenate([p[0] for p in parts])[order], np.concatenate([p[1] for p in parts])[order],
-                   spec[order], kind[order])
+    side = np.array([("START" in n) | (("END" in n) << 1) for n in c.names], dtype=np.uint8)
+    flags = side[c.brk] | (np.asarray(c.singleton, dtype=np.uint8) << 2)
+    d, t, g, k = _su_diff_queries(c.su, c.obs, flags, c.offsets, max_w, tolerance)
+    return Queries(d, t, g, k.astype(np.int64))
 
 
 def bin_queries(c: Classified, tolerance=MATCHING_THRESHOLD):
