@@ -272,7 +272,8 @@ int64_t sst_window_pairs(const double* su, const int64_t* offsets, int64_t n_sid
  * sliding-window pairs, the END side's, then the singletons: diff = su[end] -
  * su[start] (a singleton: its su), thr = tolerance * (obs[start] + obs[end])
  * (a singleton: tolerance * obs), spec = g, kind = 0 / 1 / 2.  Returns the
- * number of queries (> cap: nothing beyond cap written) or SST_E*. */
+ * number of queries (> cap: nothing written) or SST_E*.  Spectra are split
+ * over up to 16 host threads. */
 int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* flags, const int64_t* offsets,
                             int64_t n_spec, double max_weight, double tolerance, double* diff, double* thr,
                             int64_t* spec, int8_t* kind, int64_t cap);

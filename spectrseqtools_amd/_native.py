@@ -156,7 +156,7 @@ def su_diff_queries(su, obs, flags, offsets, max_weight, tolerance):
     flags = np.ascontiguousarray(flags, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.int64)
     L = lib()
-    cap = max(16, 8 * len(su))
+    cap = 0  # the first call counts (cheap: no output), the second fills
     while True:
         d, t = np.empty(cap, np.float64), np.empty(cap, np.float64)
         g, k = np.empty(cap, np.int64), np.empty(cap, np.int8)

@@ -1617,43 +1617,72 @@ static void window_side(const double* su, const int64_t* idx, int64_t n, double 
   }
 }
 
+// the host producers' worker threads: at most 16 (the GPU box's CPU share)
+static unsigned host_threads() { return std::max(1u, std::min(16u, std::thread::hardware_concurrency())); }
+template <typename F>
+static void parallel_ranges(int64_t n, int64_t grain, F&& f) {  // f(lo, hi) over [0, n) in contiguous pieces
+  const unsigned hw = host_threads();
+  if (n < grain || hw == 1) {
+    f((int64_t)0, n);
+    return;
+  }
+  const int64_t per = (n + hw - 1) / hw;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < hw; ++t) {
+    const int64_t lo = std::min<int64_t>(n, (int64_t)t * per), hi = std::min<int64_t>(n, lo + per);
+    if (lo < hi) th.emplace_back(f, lo, hi);
+  }
+  for (auto& x : th) x.join();
+}
+
 int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* flags, const int64_t* offsets,
                             int64_t n_spec, double max_weight, double tolerance, double* diff, double* thr,
                             int64_t* spec, int8_t* kind, int64_t cap) {
   if (n_spec < 0 || (n_spec > 0 && (!su || !obs || !flags || !offsets)) || cap < 0 ||
       (cap > 0 && (!diff || !thr || !spec || !kind)))
     return SST_E_ARG;
-  int64_t k = 0;
-  std::vector<int64_t> side;
-  for (int64_t g = 0; g < n_spec; ++g) {
+  for (int64_t g = 0; g < n_spec; ++g)
+    if (offsets[g + 1] < offsets[g]) return SST_E_ARG;
+  // one spectrum's queries in the reference's order: START pairs, END pairs, singletons
+  auto produce = [&](int64_t g, std::vector<int64_t>& side, auto&& emit) {
     const int64_t lo = offsets[g], hi = offsets[g + 1];
-    if (hi < lo) return SST_E_ARG;
-    for (int sd = 0; sd < 2; ++sd) {  // START pairs, then END pairs (prediction.py:261-329)
+    for (int sd = 0; sd < 2; ++sd) {
       side.clear();
       for (int64_t r = lo; r < hi; ++r)
         if (flags[r] & (1u << sd)) side.push_back(r);
-      window_side(su, side.data(), (int64_t)side.size(), max_weight, [&](int64_t a, int64_t b) {
-        if (k < cap) {
-          diff[k] = su[b] - su[a];
-          thr[k] = tolerance * (obs[a] + obs[b]);
-          spec[k] = g;
-          kind[k] = (int8_t)sd;
-        }
+      window_side(su, side.data(), (int64_t)side.size(), max_weight,
+                  [&](int64_t a, int64_t b) { emit(su[b] - su[a], tolerance * (obs[a] + obs[b]), (int8_t)sd); });
+    }
+    for (int64_t r = lo; r < hi; ++r)
+      if (flags[r] & 4u) emit(su[r], tolerance * obs[r], (int8_t)2);
+  };
+  // pass 1: queries per spectrum; pass 2 (if they fit): each spectrum's at its prefix
+  std::vector<int64_t> base((size_t)n_spec + 1, 0);
+  parallel_ranges(n_spec, 256, [&](int64_t g0, int64_t g1) {
+    std::vector<int64_t> side;
+    for (int64_t g = g0; g < g1; ++g) {
+      int64_t c = 0;
+      produce(g, side, [&](double, double, int8_t) { ++c; });
+      base[(size_t)g + 1] = c;
+    }
+  });
+  for (int64_t g = 0; g < n_spec; ++g) base[(size_t)g + 1] += base[(size_t)g];
+  const int64_t total = base[(size_t)n_spec];
+  if (total > cap) return total;
+  parallel_ranges(n_spec, 256, [&](int64_t g0, int64_t g1) {
+    std::vector<int64_t> side;
+    for (int64_t g = g0; g < g1; ++g) {
+      int64_t k = base[(size_t)g];
+      produce(g, side, [&](double d, double t, int8_t kd) {
+        diff[k] = d;
+        thr[k] = t;
+        spec[k] = g;
+        kind[k] = kd;
         ++k;
       });
     }
-    for (int64_t r = lo; r < hi; ++r)  // then the singletons' own masses
-      if (flags[r] & 4u) {
-        if (k < cap) {
-          diff[k] = su[r];
-          thr[k] = tolerance * obs[r];
-          spec[k] = g;
-          kind[k] = 2;
-        }
-        ++k;
-      }
-  }
-  return k;
+  });
+  return total;
 }
 
 int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_groups, int64_t* order) {
@@ -1669,7 +1698,7 @@ int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_
     for (int64_t i = 0; i < n; ++i) order[pos[(size_t)group[i]]++] = i;  // stable: input order per group
   }
   // each group by key, ties in input order; groups split over a few threads
-  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const unsigned hw = host_threads();
   const int64_t per = (n_groups + hw - 1) / hw;
   auto work = [&](int64_t g0, int64_t g1) {
     for (int64_t g = g0; g < g1; ++g)

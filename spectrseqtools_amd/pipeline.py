@@ -124,7 +124,7 @@ def su_diff_queries(c: Classified, explanation_masses, tolerance=MATCHING_THRESH
     side = np.array([("START" in n) | (("END" in n) << 1) for n in c.names], dtype=np.uint8)
     flags = side[c.brk] | (np.asarray(c.singleton, dtype=np.uint8) << 2)
     d, t, g, k = _su_diff_queries(c.su, c.obs, flags, c.offsets, max_w, tolerance)
-    return Queries(d, t, g, k.astype(np.int64))
+    return Queries(d, t, g, k)
 
 
 def bin_queries(c: Classified, tolerance=MATCHING_THRESHOLD):

@@ -85,13 +85,29 @@ def main():
     max_len = pipeline.max_len_of(su_seq, TOLERANCE, min_int)  # cli.py:158-170
 
     def explain_grouped(q):
-        """One engine call per max_len group; returns statuses, counts, timing."""
+        """One engine call per max_len group; returns statuses, counts, timing.
+        Groups from the spectra's max_len (one radix sort of the queries' small
+        group ids, not one full scan of the queries per group)."""
         st = np.zeros(len(q.diff), np.int8)
         cnt = np.zeros(len(q.diff), np.uint64)
-        lens = max_len[q.spec]
+        lens_u, spec_gid = np.unique(max_len, return_inverse=True)
+        if len(q.spec) and (np.diff(q.spec) >= 0).all():  # spectrum-major: a group is its spectra's ranges
+            qoff = np.searchsorted(q.spec, np.arange(len(max_len) + 1))
+            groups = []
+            for gi in range(len(lens_u)):
+                sp = np.flatnonzero(spec_gid == gi)
+                ln = qoff[sp + 1] - qoff[sp]
+                groups.append(np.repeat(qoff[sp] - (np.cumsum(ln) - ln), ln) + np.arange(int(ln.sum())))
+        else:
+            gid = spec_gid.astype(np.uint16)[q.spec]
+            order = np.argsort(gid, kind="stable")  # radix sort (16-bit keys)
+            cuts = np.concatenate([[0], np.cumsum(np.bincount(gid, minlength=len(lens_u)))])
+            groups = [order[cuts[gi]:cuts[gi + 1]] for gi in range(len(lens_u))]
         calls = 0
-        for L in np.unique(lens):
-            m = np.flatnonzero(lens == L)
+        for gi, L in enumerate(lens_u):
+            m = groups[gi]
+            if len(m) == 0:
+                continue
             dp.seq = SequenceInformation(max_len=int(L), su_mass=0.0, obs_mass=0.0, modification_rate=0.5)
             A = round(dp.seq.modification_rate * dp.seq.max_len)  # common.py:55
             r = dp.device_table.explain(q.diff[m], q.thr[m], dp.tolerance, dp.precision, A, cap=args.cap)
