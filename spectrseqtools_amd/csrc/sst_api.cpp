@@ -748,7 +748,8 @@ void free_result_bufs(sst_result* r) {
 uint64_t* ctl_block(sst_result* r, int parity) { return (uint64_t*)r->ctl.p + parity * kCtlWords; }
 
 OutArgs out_args(sst_result* r) {
-  static_assert(kCtlArenaRetries < kCtlWords && kCtlStats + kNumStats <= kCtlDhits && 2 * 2 >= kNumClasses,
+  static_assert(kCtlArenaRetries < kCtlStats && kCtlStats + kNumStats <= kCtlDhits && kCtlDhits < kCtlWords &&
+                    kCtlWords <= kScanWG && 2 * 2 >= kNumClasses,
                 "control block layout");
   OutArgs o{};
   uint64_t* ctl = ctl_block(r, r->parity);
