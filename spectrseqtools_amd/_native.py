@@ -28,7 +28,7 @@ EXPORTS = (
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
     "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
     "sst_window_pairs", "sst_is_valid_peaks", "sst_is_valid_peaks_device", "sst_result_pair_hits",
-    "sst_table_pair_records", "sst_su_diff_queries", "sst_sort_rows",
+    "sst_table_pair_records", "sst_su_diff_queries", "sst_sort_rows", "sst_step_device",
 )
 
 # kernel ids of sst_profile_read
@@ -129,6 +129,8 @@ def load_library(path=LIB_PATH):
     lib.sst_su_diff_queries.restype = _I64
     lib.sst_sort_rows.argtypes = [_P, _P, _I64, _I64, _P]
     lib.sst_sort_rows.restype = _I
+    lib.sst_step_device.argtypes = [_P, _P, _I64, _P, _I, _P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
+    lib.sst_step_device.restype = _I
     return lib
 
 
@@ -553,6 +555,23 @@ class DeviceTable:
                                                                     int(max_mods_scalar), int(bool(with_memo)),
                                                                     int(cap), ctypes.byref(h)),
                           "sst_explain_batch_device")
+        if reuse is not None:
+            reuse.n = n
+            return reuse
+        return ExplainResult(self.engine, h, n)
+
+    def step_device(self, d_obs, n_peaks, shifts, d_valid_out, d_mass, d_thr, n, tolerance, precision,
+                    max_mods_scalar, d_mods=None, with_memo=True, cap=2 ** 32, reuse=None):
+        """sst_step_device: is_valid over peaks x breakage shifts (into
+        d_valid_out, breakage-major) and an explain batch, queued together (one
+        launch when the scan packs its own result).  Returns the ExplainResult."""
+        sh = np.ascontiguousarray(shifts, dtype=np.float64)
+        h = ctypes.c_void_p(reuse.handle.value if reuse is not None else None)
+        self.engine.check(self.engine._lib.sst_step_device(self.handle, d_obs, int(n_peaks), _ptr(sh), len(sh),
+                                                           d_valid_out, d_mass, d_thr, int(n), float(tolerance),
+                                                           float(precision), d_mods, int(max_mods_scalar),
+                                                           int(bool(with_memo)), int(cap), ctypes.byref(h)),
+                          "sst_step_device")
         if reuse is not None:
             reuse.n = n
             return reuse

@@ -904,8 +904,18 @@ int launch_pack(sst_result* r, const uint64_t* scan_hdr = nullptr) {
 // deferred-class launch (eager_tail; otherwise settle() launches it only if
 // the scan routed a window to it) and the result pack.  Tables without the
 // pair list run k_bitset_scan + k_explain_expand and always the tail.
+// is_valid over peaks x breakage weights issued with a pass (sst_step_device)
+struct PeaksJob {
+  const double* obs;
+  int64_t n;
+  const double* shifts;
+  int n_shifts;
+  int8_t* out;
+};
+
 int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double* d_thr, const int64_t* d_mods,
-                 int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count, bool eager_tail) {
+                 int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count, bool eager_tail,
+                 const PeaksJob* peaks = nullptr) {
   sst_ctx* c = t->ctx;
   r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count};
   const int64_t n = r->n;
@@ -922,6 +932,12 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   r->tail_ran = false;
   r->arrays_ready = false;
   r->bitset_scan = !t->args.pairs_enabled;
+  if (n == 0 && peaks && peaks->n > 0 && peaks->n_shifts > 0) {
+    Prof p(c, SST_K_IS_VALID);
+    HIP_OK(c, launch_is_valid_peaks(t->args.valid, t->args.limit, t->args.full_lo, t->args.full_hi,
+                                    t->args.first_reach, peaks->obs, peaks->n, peaks->shifts, peaks->n_shifts, tol,
+                                    prec, peaks->out, c->stream));
+  }
   if (n == 0) {  // nothing to launch: an empty, settled result
     HIP_OK(c, hipMemsetAsync(ctl_block(r, r->parity ^ 1), 0, kCtlWords * 8, c->stream));
     r->n_hits = r->payload_bytes = 0;
@@ -948,9 +964,20 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
     static const char* dbg = getenv("SST_PACK_DBG");
     o.dbg = dbg ? atoi(dbg) : 0;
   }
+  const bool step = peaks && peaks->n > 0 && peaks->n_shifts == 4 && fused;
+  if (peaks && peaks->n > 0 && peaks->n_shifts > 0 && !step) {  // A7 in its own launch, before the pass
+    Prof p(c, SST_K_IS_VALID);
+    HIP_OK(c, launch_is_valid_peaks(t->args.valid, t->args.limit, t->args.full_lo, t->args.full_hi,
+                                    t->args.first_reach, peaks->obs, peaks->n, peaks->shifts, peaks->n_shifts, tol,
+                                    prec, peaks->out, c->stream));
+  }
   {
     Prof p(c, SST_K_EXPLAIN_MAIN);
-    HIP_OK(c, launch_explain_scan(t->args, q, o, r->n_wg, c->stream));
+    if (step)
+      HIP_OK(c, launch_step(t->args, q, o, r->n_wg, peaks->obs, peaks->n, peaks->shifts, tol, prec, peaks->out,
+                            c->stream));
+    else
+      HIP_OK(c, launch_explain_scan(t->args, q, o, r->n_wg, c->stream));
   }
   if (fused) return SST_OK;
   if (r->bitset_scan) {  // the expand kernel routes the windows the bitset scan queued
@@ -1137,6 +1164,37 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
     return rc;
   }
   int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count, false);
+  if (rc) {
+    if (!reuse) {
+      free_result_bufs(r);
+      delete r;
+    }
+    return rc;
+  }
+  *out = r;
+  return SST_OK;
+}
+
+int sst_step_device(sst_table* t, const double* d_obs, int64_t n_peaks, const double* shifts, int n_shifts,
+                    int8_t* d_valid_out, const double* d_mass, const double* d_thr, int64_t n, double tol, double prec,
+                    const int64_t* d_mods, int64_t mods_scalar, int with_memo, uint64_t cap_count, sst_result** out) {
+  if (!t || !out || n < 0 || n > SST_MAX_EXPLAIN_BATCH || (n > 0 && !d_mass) || n_peaks < 0 ||
+      n_peaks > INT32_MAX || n_shifts < 0 || n_shifts > 64 || (int64_t)n_shifts * n_peaks > INT32_MAX ||
+      (n_peaks > 0 && n_shifts > 0 && (!d_obs || !d_valid_out || !shifts)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  sst_result* r = *out;
+  const bool reuse = r != nullptr;
+  if (reuse) {
+    if (r->ctx != c || n > r->cap_n) return fail(c, SST_E_ARG, "result reuse: other ctx or capacity < n");
+    r->n = n;
+  } else if (int rc = alloc_result(t, n, &r)) {
+    return rc;
+  }
+  const PeaksJob job{d_obs, n_peaks, shifts, n_shifts, d_valid_out};
+  int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count, false, &job);
   if (rc) {
     if (!reuse) {
       free_result_bufs(r);

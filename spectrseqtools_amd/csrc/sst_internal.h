@@ -264,6 +264,10 @@ hipError_t launch_is_valid(const uint64_t* valid, int64_t limit, int64_t full_lo
 hipError_t launch_is_valid_peaks(const uint64_t* valid, int64_t limit, int64_t full_lo, int64_t full_hi,
                                  int64_t first_reach, const double* obs, int64_t n, const double* shifts, int n_w,
                                  double tol, double prec, int8_t* out, hipStream_t st);
+// the pair scan with is_valid over peaks x 4 breakage weights in front of it, one launch (k_step)
+hipError_t launch_step(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks, const double* obs,
+                       int64_t n_peaks, const double* shifts4, double tol, double prec, int8_t* valid_out,
+                       hipStream_t st);
 hipError_t launch_explain_scan(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,
                                hipStream_t st);
 hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,

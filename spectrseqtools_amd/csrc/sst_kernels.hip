@@ -412,8 +412,7 @@ __global__ __launch_bounds__(256) void k_is_valid(ValidArgs v) {
 // query) and its NW windows are quantised together, so their bitset loads
 // are in flight at once.
 template <int NW>
-__global__ __launch_bounds__(256) void k_is_valid_peaks(ValidArgs v, PeakShifts sh) {
-  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void is_valid_peak(const ValidArgs& v, const PeakShifts& sh, const uint32_t p) {
   if (p >= (uint32_t)v.n) return;
   const double obs = __builtin_nontemporal_load(v.mass + p);
   const double t = v.tol * obs;
@@ -431,6 +430,10 @@ __global__ __launch_bounds__(256) void k_is_valid_peaks(ValidArgs v, PeakShifts 
     if (inr && !full && bf >= (double)v.first_reach) hit = any_bits(v.valid, (uint32_t)af, (uint32_t)bf);
     v.out[(size_t)k * v.n + p] = hit ? (int8_t)1 : (act && hif >= (double)v.limit ? (int8_t)-1 : (int8_t)0);
   }
+}
+template <int NW>
+__global__ __launch_bounds__(256) void k_is_valid_peaks(ValidArgs v, PeakShifts sh) {
+  is_valid_peak<NW>(v, sh, blockIdx.x * 256 + threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1505,11 +1508,12 @@ __device__ __forceinline__ uint32_t pair_bytes(const PairLds& p, uint32_t first,
 // workgroup writes the header); otherwise its payload region and 8-B records
 // {query, count | bytes << 16} for k_result_pack.
 template <bool THR, bool MODS>
-__global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
+__device__ __forceinline__ void explain_scan_wg(const TableArgs& t, const QueryArgs& q, const OutArgs& out,
+                                                const uint32_t bid, const uint32_t nbid) {
   extern __shared__ uint32_t lds_pair_img[];
-  if (blockIdx.x == 0) {
+  if (bid == 0) {
     if (threadIdx.x < (unsigned)out.ctl_words) out.ctl_next[threadIdx.x] = 0;
-    for (uint32_t k = threadIdx.x; k < gridDim.x; k += blockDim.x) out.agg_next[k] = 0;
+    for (uint32_t k = threadIdx.x; k < nbid; k += blockDim.x) out.agg_next[k] = 0;
   }
   const int n_img = 2 * (t.n_pairs + 2) + t.n_buckets;
   // 16-B copies (the image is padded to 16 B; 4-B copies: scan +2.5 us)
@@ -1521,8 +1525,8 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   const int lane = threadIdx.x & 63;
   // wave-uniform in SGPRs (the buffer resources below must be scalar)
   const uint32_t w_in = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wave = blockIdx.x * (kScanWG / 64) + w_in;
-  const uint32_t n_waves = gridDim.x * (kScanWG / 64);
+  const uint32_t wave = bid * (kScanWG / 64) + w_in;
+  const uint32_t n_waves = nbid * (kScanWG / 64);
   const uint32_t n = (uint32_t)q.n;  // < 2^32 - 64 (host checks)
   const uint32_t ntiles = (n + 63) >> 6;
   const double limitf = (double)t.limit;
@@ -1615,7 +1619,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
   // partial round of tiles is spread over all CUs (not over the first few
   // workgroups) while tiles 2j, 2j+1 -- one 128-B line of status bytes --
   // stay in one workgroup, i.e. one XCD's L2 (A/B: -0.8 us)
-  const uint32_t vw = (((w_in >> 1) * gridDim.x + blockIdx.x) << 1) | (w_in & 1u);
+  const uint32_t vw = (((w_in >> 1) * nbid + bid) << 1) | (w_in & 1u);
   fetch(vw, mA, tA, mmA);
   // two dropped stores where a tile's stores would be: the loop entry then has
   // the same VMEM count between the two prefetches as every later round, so
@@ -1676,9 +1680,9 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
       wg_h += wg_part[k].x;
       wg_u += wg_part[k].y;
     }
-    out.wg_tally[blockIdx.x] = make_uint2(wg_h, wg_u);
+    out.wg_tally[bid] = make_uint2(wg_h, wg_u);
     if (out.fused)  // publish (8-B agent-scope store: flag and sums in one word)
-      __hip_atomic_store(out.agg + blockIdx.x, (1ull << 63) | ((uint64_t)wg_u << 32) | wg_h, __ATOMIC_RELAXED,
+      __hip_atomic_store(out.agg + bid, (1ull << 63) | ((uint64_t)wg_u << 32) | wg_h, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
   // The first kPreChunks x 64 hit records, their payload sizes (LDS) and
@@ -1707,7 +1711,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     // look-back over workgroups: each publishes once, when its tiles are
     // done); the last workgroup also has every total and writes the header
     if (w_in == 0) {
-      const uint32_t b = blockIdx.x;
+      const uint32_t b = bid;
       uint32_t ph = 0, pu = 0;
       for (uint32_t k0 = 0; k0 < b; k0 += 64) {
         const uint32_t k = k0 + lane;
@@ -1726,7 +1730,7 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
       if (lane == 0) {
         wg_pre[0] = ph;
         wg_pre[1] = pu;
-        if (b == gridDim.x - 1) {  // every workgroup before this one has published: the totals
+        if (b == nbid - 1) {  // every workgroup before this one has published: the totals
           uint64_t* ctl = out.cursor;  // the pass's control block
           const uint64_t ctr01 = ctl_read(ctl, kCtlCounters), ctr23 = ctl_read(ctl, kCtlCounters + 1);
           const uint64_t total = ((uint64_t)pu + wg_u) << 4;
@@ -1810,6 +1814,25 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
     emit(k, r, pb, run + (incl - pb));
     run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   }
+}
+template <bool THR, bool MODS>
+__global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
+  explain_scan_wg<THR, MODS>(t, q, out, blockIdx.x, gridDim.x);
+}
+// One launch for a step of both predicates (sst_step_device): the first
+// a7_blocks workgroups run is_valid over peaks x 4 breakage weights (1 024
+// peaks each), the rest are the pair scan's grid; the scan's workgroups are
+// dispatched as the A7 ones finish (in-order dispatch: its look-back only
+// waits for scan workgroups dispatched before), so the two overlap at the
+// seam and share one launch.
+template <bool THR, bool MODS>
+__global__ __launch_bounds__(kScanWG, 8) void k_step(TableArgs t, QueryArgs q, OutArgs out, ValidArgs v, PeakShifts sh,
+                                                   uint32_t a7_blocks) {
+  if (blockIdx.x < a7_blocks) {
+    is_valid_peak<4>(v, sh, blockIdx.x * kScanWG + threadIdx.x);
+    return;
+  }
+  explain_scan_wg<THR, MODS>(t, q, out, blockIdx.x - a7_blocks, gridDim.x - a7_blocks);
 }
 
 // Tables without the pair list (uploaded tables, literal-sweep rows): every
@@ -3175,6 +3198,27 @@ hipError_t launch_explain_scan(const TableArgs& t, const QueryArgs& q, const Out
     hipLaunchKernelGGL((k_explain_scan<false, true>), dim3(n_blocks), dim3(kScanWG), dyn, st, t, q, o);
   else
     hipLaunchKernelGGL((k_explain_scan<false, false>), dim3(n_blocks), dim3(kScanWG), dyn, st, t, q, o);
+  return hipGetLastError();
+}
+hipError_t launch_step(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks, const double* obs,
+                       int64_t n_peaks, const double* shifts4, double tol, double prec, int8_t* valid_out,
+                       hipStream_t st) {
+  if (!t.pairs_enabled || q.n <= 0) return hipErrorInvalidValue;
+  const size_t dyn = scan_dyn_lds(t);
+  ValidArgs v{t.valid, t.limit, t.full_lo, t.full_hi, t.first_reach, obs, nullptr, n_peaks, tol, prec, 1.0 / prec,
+              valid_out};
+  PeakShifts sh{};
+  for (int k = 0; k < 4; ++k) sh.shift[k] = shifts4[k];
+  const uint32_t a7 = (uint32_t)((n_peaks + kScanWG - 1) / kScanWG);
+  const dim3 grid(a7 + (uint32_t)n_blocks);
+  if (q.thr && q.max_mods)
+    hipLaunchKernelGGL((k_step<true, true>), grid, dim3(kScanWG), dyn, st, t, q, o, v, sh, a7);
+  else if (q.thr)
+    hipLaunchKernelGGL((k_step<true, false>), grid, dim3(kScanWG), dyn, st, t, q, o, v, sh, a7);
+  else if (q.max_mods)
+    hipLaunchKernelGGL((k_step<false, true>), grid, dim3(kScanWG), dyn, st, t, q, o, v, sh, a7);
+  else
+    hipLaunchKernelGGL((k_step<false, false>), grid, dim3(kScanWG), dyn, st, t, q, o, v, sh, a7);
   return hipGetLastError();
 }
 hipError_t launch_explain_expand(const TableArgs& t, const QueryArgs& q, const OutArgs& o, int n_blocks,

@@ -217,3 +217,32 @@ def test_wire_pair_hits_roundtrip(engine, dev, rows):
     cnt_, off_ = decode_hits(st_, hits_)
     assert np.array_equal(st_, res.status)
     assert canonical_digest(st_, cnt_, off_, pay_) == canonical_digest(res.status, res.count, res.offset, res.payload)
+
+
+def test_step_device_equals_separate_calls(engine, dev, rows):
+    """sst_step_device (is_valid over peaks and the explain pass in one
+    launch) gives the same is_valid bytes and the same answers as
+    sst_is_valid_peaks_device + sst_explain_batch_device, over result reuse;
+    and with 3 breakage weights (two launches)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(16)
+    n = 40_000
+    masses, thr = _queries(rng, rows, n, 2)
+    obs = np.sort(rng.uniform(150.0, 9000.0, 25_000))
+    dev_t = torch.device("cuda", engine.device)
+    dm, dt, do = (torch.from_numpy(np.ascontiguousarray(x)).to(dev_t) for x in (masses, thr, obs))
+    for shifts in (np.array([0.0, 375.183, 537.119, 912.303]), np.array([0.0, 375.183, 537.119])):
+        out_a = torch.full((len(shifts) * len(obs),), 9, dtype=torch.int8, device=dev_t)
+        out_b = torch.full_like(out_a, 7)
+        torch.cuda.synchronize()
+        res = None
+        for _ in range(2):
+            res = dev.step_device(do.data_ptr(), len(obs), shifts, out_a.data_ptr(), dm.data_ptr(), dt.data_ptr(), n,
+                                  TOL, PREC, 10, reuse=res)
+            res.fetch_device()
+        dev.is_valid_peaks_device(do.data_ptr(), len(obs), shifts, TOL, PREC, out_b.data_ptr())
+        ref = dev.explain_device(dm.data_ptr(), dt.data_ptr(), n, TOL, PREC, 10)
+        ref.fetch_device()
+        engine.synchronize()
+        assert np.array_equal(out_a.cpu().numpy(), out_b.cpu().numpy())
+        _same(res, ref, n)

@@ -17,7 +17,7 @@ from collections import defaultdict
 def bench_name(k):
     """sst::k_explain_scan<true> -> k_explain_scan (the names bench.py reports)."""
     k = k.replace("sst::", "")
-    return k.split("<")[0] if k.startswith("k_explain_scan") else k
+    return k.split("<")[0] if k.startswith(("k_explain_scan", "k_step")) else k
 
 
 def main():
