@@ -170,9 +170,9 @@ def main():
                     help="1: queue the A7 batch on a second HIP stream, concurrent with the A8 chain "
                          "(sst_ctx_set_stream); 0: both on the engine stream, one after the other")
     ap.add_argument("--fused-step", type=int, default=1,
-                    help="1 (default): A7 and A8 in one launch (sst_step_device: the is_valid workgroups in "
-                         "front of the pair scan's grid; same-box A/B: 72 against 78 us per step); 0: two "
-                         "launches (then the roofline kernel is the scan alone)")
+                    help="1 (default): A7 and A8 in one launch (sst_step_device: the is_valid workgroups "
+                         "behind the pair scan's grid, filling its tail); 0: two launches (then the roofline "
+                         "kernel is the scan alone)")
     ap.add_argument("--no-validate", action="store_true",
                     help="diagnostic builds only: skip the result checks after the timed region")
     ap.add_argument("--no-events", action="store_true",

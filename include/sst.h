@@ -167,8 +167,8 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
  * the explanation stage issue them: sst_is_valid_peaks_device(d_obs, n_peaks,
  * shifts, n_shifts -> d_valid_out) and sst_explain_batch_device(d_mass, ...,
  * out), with the same results.  With 4 breakage weights and a pass whose scan
- * packs its own result, both run in one launch (the is_valid workgroups
- * first, the pair scan's grid behind them); otherwise as two launches.  No
+ * packs its own result, both run in one launch (the pair scan's grid, the
+ * is_valid workgroups behind it); otherwise as two launches.  No
  * reference equivalent (it issues the two per row). */
 int sst_step_device(sst_table* t, const double* d_obs, int64_t n_peaks, const double* shifts, int n_shifts,
                     int8_t* d_valid_out, const double* d_mass, const double* d_thr, int64_t n, double tolerance,

@@ -1819,20 +1819,22 @@ template <bool THR, bool MODS>
 __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryArgs q, OutArgs out) {
   explain_scan_wg<THR, MODS>(t, q, out, blockIdx.x, gridDim.x);
 }
-// One launch for a step of both predicates (sst_step_device): the first
-// a7_blocks workgroups run is_valid over peaks x 4 breakage weights (1 024
-// peaks each), the rest are the pair scan's grid; the scan's workgroups are
-// dispatched as the A7 ones finish (in-order dispatch: its look-back only
-// waits for scan workgroups dispatched before), so the two overlap at the
-// seam and share one launch.
+// One launch for a step of both predicates (sst_step_device): the pair
+// scan's grid, then a7_blocks workgroups of is_valid over peaks x 4 breakage
+// weights (1 024 peaks each).  The scan's workgroups are dispatched first (its
+// look-back only ever waits for scan workgroups dispatched before it); the
+// is_valid ones fill the slots the scan's workgroups free as they finish --
+// the scan's tail -- and the step pays one launch.  (is_valid in front of
+// the scan instead: 8 us slower per step, same-box A/B.)
 template <bool THR, bool MODS>
 __global__ __launch_bounds__(kScanWG, 8) void k_step(TableArgs t, QueryArgs q, OutArgs out, ValidArgs v, PeakShifts sh,
                                                    uint32_t a7_blocks) {
-  if (blockIdx.x < a7_blocks) {
-    is_valid_peak<4>(v, sh, blockIdx.x * kScanWG + threadIdx.x);
+  const uint32_t n_scan = gridDim.x - a7_blocks;
+  if (blockIdx.x >= n_scan) {
+    is_valid_peak<4>(v, sh, (blockIdx.x - n_scan) * kScanWG + threadIdx.x);
     return;
   }
-  explain_scan_wg<THR, MODS>(t, q, out, blockIdx.x - a7_blocks, gridDim.x - a7_blocks);
+  explain_scan_wg<THR, MODS>(t, q, out, blockIdx.x, n_scan);
 }
 
 // Tables without the pair list (uploaded tables, literal-sweep rows): every
