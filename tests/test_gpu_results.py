@@ -246,3 +246,42 @@ def test_step_device_equals_separate_calls(engine, dev, rows):
         engine.synchronize()
         assert np.array_equal(out_a.cpu().numpy(), out_b.cpu().numpy())
         _same(res, ref, n)
+
+
+def test_empty_batches(engine, dev, rows):
+    """Zero-length batches on every entry point: empty results (no launch
+    faults), a result reused from full to empty and back, and the step entry
+    point with no peaks or no explain queries."""
+    torch = pytest.importorskip("torch")
+    e = np.zeros(0)
+    assert len(dev.is_valid(e, e, TOL, PREC)) == 0
+    r0 = dev.explain(e, e, TOL, PREC, 10)
+    assert r0.n == 0 and len(r0.status) == 0
+    dev_t = torch.device("cuda", engine.device)
+    rng = np.random.default_rng(17)
+    masses, thr = _queries(rng, rows, 1000, 2)
+    dm = torch.from_numpy(masses).to(dev_t)
+    dt = torch.from_numpy(thr).to(dev_t)
+    obs = torch.from_numpy(np.sort(rng.uniform(200.0, 5000.0, 300))).to(dev_t)
+    out = torch.full((4 * 300,), 9, dtype=torch.int8, device=dev_t)
+    shifts = np.array([0.0, 375.183, 537.119, 912.303])
+    torch.cuda.synchronize()
+    res = None
+    for n in (1000, 0, 1000, 0):  # a result has the capacity of its first pass
+        res = dev.explain_device(dm.data_ptr(), dt.data_ptr(), n, TOL, PREC, 10, reuse=res)
+        nh, nb = res.settle()
+        res.fetch_device()
+        if n == 0:
+            assert nh == 0 and nb == 0 and len(res.status) == 0
+        else:
+            _same(res, dev.explain(masses, thr, TOL, PREC, 10), n)
+    ref = dev.is_valid_peaks(obs.cpu().numpy(), shifts, TOL, PREC)
+    s0 = dev.step_device(obs.data_ptr(), 300, shifts, out.data_ptr(), dm.data_ptr(), dt.data_ptr(), 0, TOL, PREC, 10)
+    s0.fetch_device()
+    engine.synchronize()
+    assert len(s0.status) == 0 and np.array_equal(out.cpu().numpy(), ref)
+    s1 = dev.step_device(obs.data_ptr(), 0, shifts, out.data_ptr(), dm.data_ptr(), dt.data_ptr(), 1000, TOL, PREC, 10)
+    s1.fetch_device()
+    _same(s1, dev.explain(masses, thr, TOL, PREC, 10), 1000)
+    ptr, nh = s1.hit_list_device()
+    assert nh == int(np.isin(s1.status, (_native.SST_SOME, _native.SST_OVERFLOW)).sum())
