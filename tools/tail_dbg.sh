@@ -1,5 +1,5 @@
 cd /root/repo; export TMPDIR=/tmp
-for v in 0 1 2 4 0; do
+for v in 0 1 4 5; do
   export SST_TAIL_DBG=$v
   rm -rf gpurun_out/td_$v
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/td_$v -o run -- python3 bench.py --workload config1 --steps 20 --no-cpu-baseline --no-validate > gpurun_out/td_$v.json 2> gpurun_out/td_$v.err || exit $?
