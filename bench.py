@@ -11,11 +11,11 @@ spectra (10k spectra, ~1M peaks, full 104-mass /
         reference's sliding window emits (prediction.py:286-329), budget
         round(0.5*max_len)                  -> k_explain_main (+ deferred kernels)
   * N>1: spectra shard by rank (weak scaling: `--spectra` per GPU); each
-        step's complete result of every rank (wire format v3, parallel.wire_pack:
-        2-bit A7 / A8 codes, 4 B per pair-path hit, the deferred hits' records
-        and payload; ~10 MB per rank per config-3 step) is gathered to rank 0 over
-        RCCL on a second stream while the next step computes (--no-gather:
-        results stay in each rank's HBM).
+        step's complete result of every rank (wire format v4, sst_wire_pack:
+        1-bit A7 / A8 codes, ~16 bits per pair-path hit, the deferred hits'
+        records and payload; ~5.4 MB per rank per config-3 step) is packed on
+        the device and gathered to rank 0 over RCCL on other streams while the
+        next step computes (--no-gather: results stay in each rank's HBM).
 value = peaks of all ranks / step time (max over ranks).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--spectra S]
@@ -192,8 +192,8 @@ def main():
     from spectrseqtools_amd import _native
     from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
     from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
-    from spectrseqtools_amd.parallel import (Gatherer, canonical_digest, decode_hits, device_bytes, dist_env, pair_key,
-                                             wire_pack, wire_size, wire_unpack)
+    from spectrseqtools_amd.parallel import (Gatherer, canonical_digest, decode_hits, dist_env, wire_unpack,
+                                             wire_used_bytes)
 
     rank, world, local = dist_env()
     if world != args.gpus:
@@ -237,13 +237,18 @@ def main():
     gath = Gatherer(dist, dev_t) if (dist and not args.no_gather) else None
     side = torch.cuda.Stream(device=dev_t) if args.a7_stream else None
     settled = {"n": 0, "sent": 0}
-    # N>1 delivery: step j's result goes to rank 0 on a second stream while
-    # step j+1 computes.  pass_done[j&1]: step j's kernels (engine stream);
-    # copied[j&1]: its wire copy (comm stream), which the engine stream waits
-    # for before step j+2 reuses the same result buffers
+    # N>1 delivery: step j's result goes to rank 0 while step j+1 computes.
+    # pass_done[j&1]: step j's kernels (engine stream); the pack stream packs
+    # it (sst_wire_pack, one kernel) into wire buffer j&1 once the gather of
+    # step j-2 has read that buffer (gathered[j&1]); copied[j&1]: that pack,
+    # which the engine stream waits for before step j+2 reuses the same
+    # result buffers; the comm stream gathers the packed buffer
     comm = torch.cuda.Stream(device=dev_t) if gath is not None else None
+    packer = torch.cuda.Stream(device=dev_t) if gath is not None else None
     pass_done = [torch.cuda.Event(), torch.cuda.Event()]
     copied = [None, None]
+    gathered = [None, None]
+    wbuf = [None, None]
 
     def settle(r):
         nh, nb = r.settle()
@@ -253,26 +258,31 @@ def main():
         settled["n"] += 1
 
     def send(j):
-        """Step j's complete result of this rank -> rank 0 (wire format v3:
-        parallel.wire_pack -- 2-bit A7 and A8 codes, 4 B per pair-path hit,
-        which rank 0 expands from its own copy of the table's pair list, and
-        records + payload of the deferred paths' hits)."""
+        """Step j's complete result of this rank -> rank 0 in the wire format
+        v4 (sst_wire_pack, include/sst.h: 1-bit is_valid and status codes,
+        per pair-path hit its first pair-list entry in w bits and a 2-bit
+        count, which rank 0 expands from its own copy of the table's pair
+        list; records + payload of the deferred paths' hits; a list of the
+        rare rest)."""
         r = results[j & 1]
         settle(r)  # host: the pass's header (routed windows / retries handled)
-        hits, n_hits = r.hit_list_device()
-        refs, n_pair, pair_bytes, n_wg = r.pair_hits_device()
-        st, _c, _o, pay, nb = r.device_views(arrays=False)
+        packer.wait_event(pass_done[j & 1])
+        if side is not None:
+            packer.wait_stream(side)
+        if gathered[j & 1] is not None:
+            packer.wait_event(gathered[j & 1])
+        engine.set_stream(packer.cuda_stream)
+        r.wire_pack(outs7[j & 1].data_ptr(), n7, wbuf[j & 1].data_ptr(), wbuf[j & 1].numel())
+        engine.set_stream(None)
+        ev = torch.cuda.Event()
+        ev.record(packer)
+        copied[j & 1] = ev
         with torch.cuda.stream(comm):
-            comm.wait_event(pass_done[j & 1])
-            if side is not None:
-                comm.wait_stream(side)
-            wire = wire_pack(outs7[j & 1], device_bytes(st, n8, dev_t), device_bytes(hits, 16 * n_hits, dev_t),
-                             device_bytes(pay, nb, dev_t), device_bytes(refs, 2 * n_pair, dev_t), n_pair, pair_bytes,
-                             n_wg, pkey)
-            ev = torch.cuda.Event()
-            ev.record(comm)
-            copied[j & 1] = ev
-            gath.gather(wire)
+            comm.wait_event(ev)
+            gath.gather(wbuf[j & 1])
+            ev2 = torch.cuda.Event()
+            ev2.record(comm)
+            gathered[j & 1] = ev2
         settled["sent"] += 1
 
     def step(k):
@@ -327,9 +337,18 @@ def main():
     ref_digest = result_digest(ref)
     if gath is not None:
         precs = tdev.pair_records()
-        pkey = pair_key(precs)
-        _r, n_pair0, pair_bytes0, _w = ref.pair_hits_device()
-        gath.agree(wire_size(n7, n8, n_hits0, payload0, n_pair0, pair_bytes0))
+        # the wire size: the fixed part (host-known) + the reference pass's list
+        fixed = ref.wire_pack(outs7[0].data_ptr(), n7)
+        probe = torch.empty(fixed + 8 * (n7 + n8 + n_hits0), dtype=torch.uint8, device=dev_t)
+        torch.cuda.synchronize()
+        ref.wire_pack(outs7[0].data_ptr(), n7, probe.data_ptr(), probe.numel())
+        engine.synchronize()
+        hdr = probe[:128].cpu().numpy()
+        used, wire_list = wire_used_bytes(hdr), int(hdr.view(np.uint64)[9])
+        del probe
+        gath.agree(used)
+        wbuf = [torch.empty(gath.max, dtype=torch.uint8, device=dev_t) for _ in range(2)]
+        torch.cuda.synchronize()
         ref_canon = canonical_digest(ref.status, ref.count, ref.offset, ref.payload)
     for k in range(args.warmup):
         step(k)
@@ -500,10 +519,11 @@ def main():
             "a7_stream": ("side stream, concurrent with the A8 chain" if args.a7_stream else "engine stream"),
             "parallelism": ((f"spectra sharded over {world} GPUs; every step's complete result of every rank "
                              f"gathered to rank 0 ({'RCCL' if args.backend == 'nccl' else 'gloo'}, wire format "
-                             f"parallel.wire_pack), overlapped with the next step"
+                             f"v4, sst_wire_pack), overlapped with the next step"
                              if gath is not None else f"spectra sharded over {world} GPUs, results kept per rank")
                             if world > 1 else "1 GPU"),
             "wire_bytes_per_rank_step": (gath.sizes if gath is not None else None),
+            "wire_list_entries_rank0": (wire_list if gath is not None else None),
         },
         "roofline": {
             "bound": "hbm",

@@ -239,6 +239,35 @@ int sst_result_pair_hits(sst_result* r, void** d_refs, uint64_t* n_pair_hits, ui
  * candidate); *n = 0 for tables without the list.  recs may be NULL (size
  * query). */
 int sst_table_pair_records(sst_table* t, uint32_t* recs, int64_t cap, int64_t* n);
+/* One rank's complete step result in the gather's wire format v4, packed on
+ * the device by one kernel on the ctx stream (settles r first): d_valid the
+ * step's n_valid is_valid codes (int8 -1 / 0 / 1), r its explain result.
+ * The layout (8-B aligned sections; spectrseqtools_amd/parallel.py,
+ * wire_unpack, decodes it):
+ *   header   16 x u64: magic "SSTW4", n_valid, n_explain, n_pair, n_explicit,
+ *            explicit payload bytes, n_scan_wg, pair key (FNV-1a of the pair
+ *            records), w, n_list, list capacity, list offset, 4 x 0
+ *   valid    1 bit per is_valid query: True
+ *   status   2 bits per explain query: 0 NONE, 1 EMPTY, 2 SOME / OVERFLOW /
+ *            ABORTED, 3 listed
+ *   first    per pair hit (sst_result_pair_hits, scan order) its first
+ *            pair-list entry in w bits, w = ceil(log2(pair-list entries))
+ *   codes    per pair hit 3 bits, 10 per u32: its count 1..7, 0 = listed
+ *   explicit 12-B records {u32 query | kind << 30, u32 a, u32 b} of the
+ *            other hits: kind 0 SOME (a = candidates, b = payload offset),
+ *            1 OVERFLOW / 2 ABORTED (a, b = the exact count)
+ *   payload  the explicit hits' payload
+ *   list     n_list 8-B entries {u32 index | type << 30, u32 value}, in no
+ *            particular order: type 0 an is_valid raise, 1 an explain status
+ *            other than NONE / EMPTY / SOME (value: the status byte), 2 a pair hit's
+ *            count outside 1..7 (index: the pair hit, value: the count)
+ * d_out NULL: returns the fixed part's bytes (the list's offset) and packs
+ * nothing; otherwise cap (>= that) bounds the buffer and entries beyond it
+ * are dropped (the header's n_list still counts them: the receiver checks).
+ * d_out must be 8-byte aligned.  Returns the fixed part's bytes or a
+ * negative SST_E_*.  No reference equivalent (the north star's RCCL gather of
+ * candidate compositions). */
+int64_t sst_wire_pack(sst_result* r, const int8_t* d_valid, int64_t n_valid, void* d_out, int64_t cap);
 /* Copy device results to the host views (synchronises the ctx stream). */
 int sst_result_fetch(sst_result* r);
 void sst_result_free(sst_result* r);

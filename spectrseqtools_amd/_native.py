@@ -29,6 +29,7 @@ EXPORTS = (
     "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
     "sst_window_pairs", "sst_is_valid_peaks", "sst_is_valid_peaks_device", "sst_result_pair_hits",
     "sst_table_pair_records", "sst_su_diff_queries", "sst_sort_rows", "sst_step_device",
+    "sst_wire_pack",
 )
 
 # kernel ids of sst_profile_read
@@ -125,6 +126,8 @@ def load_library(path=LIB_PATH):
     lib.sst_result_pair_hits.restype = _I
     lib.sst_table_pair_records.argtypes = [_P, _P, _I64, ctypes.POINTER(_I64)]
     lib.sst_table_pair_records.restype = _I
+    lib.sst_wire_pack.argtypes = [_P, _P, _I64, _P, _I64]
+    lib.sst_wire_pack.restype = _I64
     lib.sst_su_diff_queries.argtypes = [_P, _P, _P, _P, _I64, _D, _D, _P, _P, _P, _P, _I64]
     lib.sst_su_diff_queries.restype = _I64
     lib.sst_sort_rows.argtypes = [_P, _P, _I64, _I64, _P]
@@ -378,6 +381,15 @@ class ExplainResult:
                                                                 ctypes.byref(nb), ctypes.byref(wg)),
                           "sst_result_pair_hits")
         return p.value, int(nh.value), int(nb.value), int(wg.value)
+
+    def wire_pack(self, d_valid, n_valid, d_out=None, cap=0):
+        """sst_wire_pack: this result plus n_valid is_valid codes at d_valid
+        in the gather's wire format v4, packed on the device into d_out (cap
+        bytes).  d_out None: sizing only.  Returns the fixed part's bytes."""
+        n = self.engine._lib.sst_wire_pack(self.handle, d_valid, int(n_valid), d_out, int(cap))
+        if n < 0:
+            self.engine.check(int(n), "sst_wire_pack")
+        return int(n)
 
     def fetch_device(self):
         self.engine.check(self.engine._lib.sst_result_fetch(self.handle), "sst_result_fetch")

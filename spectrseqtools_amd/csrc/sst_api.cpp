@@ -92,6 +92,8 @@ struct sst_table {
   std::vector<int64_t> cap;
   DevBuf packed, index, valid, w, capd, modd, pairs;
   std::vector<uint32_t> pair_recs;  // the pair list's payload records (host copy)
+  uint64_t pair_key = 0;            // their FNV-1a (sst_wire_pack), computed on first use
+  bool pair_key_set = false;
   int scan_blocks = 0;  // resident workgroups of k_explain_scan (depends on the LDS pair list size)
   bool closure = false;  // built here from masses >= C: rows are true closures (layered fast paths valid)
   TableArgs args{};
@@ -1404,6 +1406,85 @@ int sst_table_pair_records(sst_table* t, uint32_t* recs, int64_t cap, int64_t* n
   if (cap < *n) return fail(t->ctx, SST_E_ARG, "pair records: buffer too small");
   memcpy(recs, t->pair_recs.data(), (size_t)*n * 4);
   return SST_OK;
+}
+
+// FNV-1a (63 bits) of the pair records' bytes: parallel.pair_key
+static uint64_t pair_key_of(const std::vector<uint32_t>& recs) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  const uint8_t* p = (const uint8_t*)recs.data();
+  for (size_t i = 0; i < recs.size() * 4; ++i) h = (h ^ p[i]) * 0x100000001B3ull;
+  return h & 0x7FFFFFFFFFFFFFFFull;
+}
+
+static uint64_t align8(uint64_t x) { return (x + 7) & ~7ull; }
+
+int64_t sst_wire_pack(sst_result* r, const int8_t* d_valid, int64_t n_valid, void* d_out, int64_t cap) {
+  if (!r || n_valid < 0 || (n_valid > 0 && !d_valid) || (d_out && cap < 0)) return SST_E_ARG;
+  sst_ctx* c = r->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = settle(r)) return rc;
+  sst_table* t = r->pass.t;
+  const uint64_t n_pair = r->scan_hits, n_exp = r->n_hits - r->scan_hits;
+  const uint64_t xpay = r->payload_bytes - r->scan_bytes;
+  if (r->n_hits < r->scan_hits || r->payload_bytes < r->scan_bytes)
+    return fail(c, SST_E_INTERNAL, "wire pack: pair part larger than the result");
+  if (n_valid >= (1ll << 30) || r->n >= (1ll << 30))
+    return fail(c, SST_E_ARG, "wire pack: list entries index at most 2^30 queries");
+  if (xpay >= (1ull << 32)) return fail(c, SST_E_ARG, "wire pack: explicit payload offsets are 32-bit");
+  const uint64_t E = (n_pair && t) ? t->pair_recs.size() : 0;
+  int w = 1;
+  while (E > 1 && (1ull << w) < E) ++w;  // first entries are < E
+  WireArgs a{};
+  a.valid = d_valid;
+  a.status = (const int8_t*)r->status.p;
+  a.hits = (const uint4*)r->hits.p;
+  a.refs = (const uint16_t*)r->refs.p;
+  a.out = (uint8_t*)d_out;
+  a.n7 = n_valid;
+  a.n8 = r->n;
+  a.n_pair = n_pair;
+  a.n_exp = n_exp;
+  a.pair_bytes = r->scan_bytes;
+  a.w = w;
+  a.nb_v = align8(((uint64_t)n_valid + 7) / 8);
+  a.nb_s = align8(((uint64_t)r->n + 3) / 4);
+  a.nw_f = (n_pair * w + 63) / 64 * 2;
+  a.nw_c = (n_pair + 19) / 20 * 2;
+  a.o_vbits = 8 * kWireHeaderWords;
+  a.o_sbits = a.o_vbits + a.nb_v;
+  a.o_first = a.o_sbits + a.nb_s;
+  a.o_codes = a.o_first + 4 * a.nw_f;
+  a.o_exp = a.o_codes + 4 * a.nw_c;
+  const uint64_t o_pay = a.o_exp + align8(12 * n_exp);
+  a.o_list = o_pay + align8(xpay);
+  if (!d_out) return (int64_t)a.o_list;  // the fixed part's bytes: sizing only
+  if ((uint64_t)cap < a.o_list) return fail(c, SST_E_ARG, "wire pack: buffer smaller than the fixed part");
+  if ((uintptr_t)d_out & 7) return fail(c, SST_E_ARG, "wire pack: buffer not 8-byte aligned");
+  a.list_cap = ((uint64_t)cap - a.o_list) / 8;
+  if (n_pair && !t->pair_key_set) {
+    t->pair_key = pair_key_of(t->pair_recs);
+    t->pair_key_set = true;
+  }
+  const uint64_t hdr[kWireHeaderWords] = {kWireMagic, (uint64_t)n_valid, (uint64_t)r->n, n_pair, n_exp, xpay,
+                                          (uint64_t)r->n_wg, n_pair ? t->pair_key : 0, (uint64_t)w, 0, a.list_cap,
+                                          a.o_list, 0, 0, 0, 0};
+  for (int k = 0; k < kWireHeaderWords; ++k) a.hdr[k] = hdr[k];
+  auto blocks = [](uint64_t n) { return (uint32_t)((n + 255) / 256); };
+  a.be_v = blocks(a.nb_v);
+  a.be_s = a.be_v + blocks(a.nb_s);
+  a.be_f = a.be_s + blocks(a.nw_f);
+  a.be_c = a.be_f + blocks(a.nw_c);
+  a.be_e = std::max<uint32_t>(1, a.be_c + blocks(n_exp));  // >= 1 block: the header
+  uint8_t* out = (uint8_t*)d_out;
+  HIP_OK(c, hipMemsetAsync(out + 8 * kWireListWord, 0, 8, c->stream));  // the list counter
+  if (n_exp & 1) HIP_OK(c, hipMemsetAsync(out + a.o_exp + 12 * n_exp, 0, 4, c->stream));
+  HIP_OK(c, launch_wire_pack(a, c->stream));
+  if (xpay)
+    HIP_OK(c, hipMemcpyAsync(out + o_pay, (const uint8_t*)r->dense.p + r->scan_bytes, xpay, hipMemcpyDeviceToDevice,
+                             c->stream));
+  if (align8(xpay) != xpay) HIP_OK(c, hipMemsetAsync(out + o_pay + xpay, 0, align8(xpay) - xpay, c->stream));
+  return (int64_t)a.o_list;
 }
 
 int sst_result_fetch(sst_result* r) {

@@ -249,6 +249,31 @@ struct ExactWs {
   uint32_t hash_cap;
 };
 
+// The gather's wire format v4 (sst_wire_pack, include/sst.h).  Header words
+// (u64): magic, n_valid, n_explain, n_pair, n_explicit, explicit payload
+// bytes, n_wg, key, w, n_list (the device counter), list capacity, list
+// offset, 4 reserved.  Sections (8-B aligned): valid bits, 2-bit status codes,
+// w-bit first entries, 3-bit count codes (10 per u32), 12-B explicit records, explicit
+// payload, 8-B list entries.
+constexpr uint64_t kWireMagic = 0x3457545353ull;  // "SSTW4"
+constexpr int kWireHeaderWords = 16;
+constexpr int kWireListWord = 9;
+struct WireArgs {
+  const int8_t* valid;
+  const int8_t* status;
+  const uint4* hits;
+  const uint16_t* refs;
+  uint8_t* out;
+  int64_t n7, n8;
+  uint64_t n_pair, n_exp, pair_bytes, list_cap;
+  uint64_t o_vbits, o_sbits, o_first, o_codes, o_exp, o_list;
+  uint64_t nb_v, nb_s, nw_f, nw_c;  // region sizes: bytes, bytes, u32 words, u32 words
+  uint32_t be_v, be_s, be_f, be_c, be_e;  // cumulative block ends per role
+  int w;
+  uint64_t hdr[kWireHeaderWords];
+};
+hipError_t launch_wire_pack(const WireArgs& a, hipStream_t st);
+
 hipError_t launch_bits_seed(uint64_t* R0, int64_t nwords, hipStream_t st);
 hipError_t launch_bits_shift_or(uint64_t* dst, const uint64_t* src, int64_t k, int64_t nwords, int64_t nbits,
                                 hipStream_t st);

@@ -2130,6 +2130,151 @@ __global__ __launch_bounds__(256) void k_hits_to_arrays(const uint4* __restrict_
   }
 }
 
+// ---------------------------------------------------------------------------
+// The gather's wire format v4 (sst_wire_pack): one launch, a role per block
+// range, every output byte written by exactly one thread except the list
+// entries (the rare rest: is_valid raises, statuses other than NONE / EMPTY /
+// SOME, pair hits whose count is not 1..7), whose slots a block takes with one
+// atomic (wire_slots).  HBM-bound byte work: each thread reads
+// 8 code bytes (or 4 status bytes, or 10 hit records) and writes one output
+// byte (or word); no LDS beyond the block's slot arithmetic.
+
+// 8 code bytes from q0 on (bytes past n read as 0)
+__device__ __forceinline__ uint64_t wire_load8(const int8_t* p, int64_t q0, int64_t n) {
+  if (q0 + 8 <= n && ((uintptr_t)(p + q0) & 7) == 0) return *(const uint64_t*)(p + q0);
+  uint64_t v = 0;
+  for (int k = 0; k < 8; ++k)
+    if (q0 + k < n) v |= (uint64_t)(uint8_t)p[q0 + k] << (8 * k);
+  return v;
+}
+
+// First list slot of this thread's n_mine entries: a block-wide prefix sum
+// and one atomic on the header's counter (zeroed by the host before the
+// launch) per block that has any; blocks without entries only pay the
+// barrier.  Entries come in no particular order.  Block-uniform call.
+__device__ __forceinline__ uint64_t wire_slots(const WireArgs& a, uint32_t n_mine) {
+  __shared__ uint32_t s_wave[4];
+  __shared__ unsigned long long s_base;
+  if (!__syncthreads_or(n_mine != 0)) return 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t incl = n_mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_wave[wv] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_base = atomicAdd((unsigned long long*)(a.out + 8 * kWireListWord),
+                       (unsigned long long)(s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3]));
+  __syncthreads();
+  uint64_t base = s_base + incl - n_mine;
+  for (int w = 0; w < wv; ++w) base += s_wave[w];
+  return base;
+}
+
+__device__ __forceinline__ void wire_entry(const WireArgs& a, uint64_t pos, uint32_t type, uint64_t idx,
+                                           uint32_t value) {
+  if (pos < a.list_cap) ((uint2*)(a.out + a.o_list))[pos] = make_uint2((type << 30) | (uint32_t)idx, value);
+}
+
+__global__ __launch_bounds__(256) void k_wire_pack(WireArgs a) {
+  const uint32_t b = blockIdx.x;
+  if (b == 0 && threadIdx.x < kWireHeaderWords && threadIdx.x != kWireListWord)  // the counter stays the host's zero
+    ((uint64_t*)a.out)[threadIdx.x] = a.hdr[threadIdx.x];
+  if (b < a.be_v) {  // valid: byte t = 8 queries' bits (True); raises listed
+    const uint64_t t = (uint64_t)b * 256 + threadIdx.x;
+    const bool act = t < a.nb_v;
+    const uint64_t v = act ? wire_load8(a.valid, (int64_t)t * 8, a.n7) : 0;
+    uint32_t bits = 0, exc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int8_t c = (int8_t)(v >> (8 * k));
+      bits |= (uint32_t)(c == 1) << k;
+      exc |= (uint32_t)(act && (int64_t)t * 8 + k < a.n7 && c == -1) << k;
+    }
+    if (act) a.out[a.o_vbits + t] = (uint8_t)bits;
+    uint64_t pos = wire_slots(a, __builtin_popcount(exc));
+    for (; exc; exc &= exc - 1) wire_entry(a, pos++, 0u, t * 8 + __builtin_ctz(exc), 0u);
+    return;
+  }
+  if (b < a.be_s) {  // status: byte t = 4 queries' 2-bit codes; statuses past SOME listed
+    const uint64_t t = (uint64_t)(b - a.be_v) * 256 + threadIdx.x;
+    const bool act = t < a.nb_s;
+    const int64_t q0 = (int64_t)t * 4;
+    uint32_t v = 0;
+    if (act && q0 + 4 <= a.n8 && ((uintptr_t)(a.status + q0) & 3) == 0) {
+      v = *(const uint32_t*)(a.status + q0);
+    } else if (act) {
+      for (int k = 0; k < 4; ++k)
+        if (q0 + k < a.n8) v |= (uint32_t)(uint8_t)a.status[q0 + k] << (8 * k);
+    }
+    uint32_t codes = 0, exc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int8_t c = (int8_t)(v >> (8 * k));
+      const uint32_t code = c == SST_NONE ? 0u : (c == SST_EMPTY ? 1u : (c == SST_SOME || c == SST_OVERFLOW ||
+                                                                          c == SST_ABORTED) ? 2u : 3u);
+      codes |= code << (2 * k);
+      exc |= (uint32_t)(act && (int64_t)t * 4 + k < a.n8 && c != SST_NONE && c != SST_EMPTY && c != SST_SOME) << k;
+    }
+    if (act) a.out[a.o_sbits + t] = (uint8_t)codes;
+    uint64_t pos = wire_slots(a, __builtin_popcount(exc));
+    for (; exc; exc &= exc - 1) {
+      const int k = __builtin_ctz(exc);
+      wire_entry(a, pos++, 1u, t * 4 + k, (uint32_t)(uint8_t)(v >> (8 * k)));
+    }
+    return;
+  }
+  if (b < a.be_f) {  // u32 word t of the w-bit first entries (field i at bits i*w ..)
+    const uint64_t t = (uint64_t)(b - a.be_s) * 256 + threadIdx.x;
+    if (t >= a.nw_f) return;
+    const uint64_t lo = t * 32, w = (uint64_t)a.w;
+    uint32_t word = 0;
+    for (uint64_t i = lo / w; i * w < lo + 32 && i < a.n_pair; ++i) {
+      const uint64_t f = a.refs[i] & 0x7FFFu;
+      const int64_t sh = (int64_t)(i * w) - (int64_t)lo;
+      word |= (uint32_t)(sh >= 0 ? f << sh : f >> -sh);
+    }
+    ((uint32_t*)(a.out + a.o_first))[t] = word;
+    return;
+  }
+  if (b < a.be_c) {  // u32 word t of the 3-bit count codes (10 per word): 1..7, 0 = listed count
+    const uint64_t t = (uint64_t)(b - a.be_f) * 256 + threadIdx.x;
+    const bool act = t < a.nw_c;
+    uint32_t word = 0, exc = 0;
+    for (int k = 0; k < 10; ++k) {
+      const uint64_t i = t * 10 + k;
+      if (!act || i >= a.n_pair) break;
+      const uint32_t c = a.hits[i].y;
+      if (c >= 1 && c <= 7)
+        word |= c << (3 * k);
+      else
+        exc |= 1u << k;
+    }
+    if (act) ((uint32_t*)(a.out + a.o_codes))[t] = word;
+    uint64_t pos = wire_slots(a, __builtin_popcount(exc));
+    for (; exc; exc &= exc - 1) {
+      const uint64_t i = t * 10 + __builtin_ctz(exc);
+      wire_entry(a, pos++, 2u, i, a.hits[i].y);
+    }
+    return;
+  }
+  if (b < a.be_e) {  // explicit record t {query | kind << 30, a, b}
+    const uint64_t t = (uint64_t)(b - a.be_c) * 256 + threadIdx.x;
+    if (t >= a.n_exp) return;
+    const uint4 r = a.hits[a.n_pair + t];
+    const int8_t s = a.status[r.x];
+    const uint32_t kind = s == SST_OVERFLOW ? 1u : (s == SST_ABORTED ? 2u : 0u);
+    const uint64_t off = (((uint64_t)r.w << 32) | r.z) - a.pair_bytes;
+    uint32_t* o = (uint32_t*)(a.out + a.o_exp) + 3 * t;
+    o[0] = r.x | (kind << 30);
+    o[1] = kind == 0 ? r.y : r.z;
+    o[2] = kind == 0 ? (uint32_t)off : r.w;
+  }
+}
+
 // Deferred fast/no-memo queries with deep stacks: persistent grid, one lane per
 // query, stack in a per-lane slice of the workspace.
 template <int MODE>
@@ -3252,6 +3397,11 @@ hipError_t launch_hits_to_arrays(const uint4* hits, uint64_t n_hits, const int8_
   if (n_hits == 0) return hipSuccess;
   hipLaunchKernelGGL(k_hits_to_arrays, dim3(blocks_for((int64_t)n_hits, 256)), dim3(256), 0, st, hits, n_hits, status,
                      count, offset);
+  return hipGetLastError();
+}
+hipError_t launch_wire_pack(const WireArgs& a, hipStream_t st) {
+  if (a.be_e == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_wire_pack, dim3(a.be_e), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const OutArgs& o, void* ws_deep,

@@ -10,15 +10,19 @@ candidate payload) to the rank that drives the Python pipeline.  RCCL has no
 gatherv: sizes are agreed once (all_gather of lengths), then one padded
 torch.distributed.gather moves the bytes (send/recv over xGMI).
 
-Wire format of one rank's result (wire_pack / wire_unpack, v3), packed on
-the device with a few tensor ops (no host round trip): 2-bit is_valid and
-status codes, 4 B per pair-path hit (its first pair-list entry and count:
-the receiver rebuilds the candidates from its own copy of the table's pair
-list, so those hits send no payload), 12-B records and the payload for the
-few hits of the deferred paths.  About 0.35 B per query + 4 B per hit:
-~10 MB per rank per config-3 step (v2, 12-B records + the dense payload:
-33 MB; the engine's own layout: 51 MB).  wire_unpack + decode_hits +
-candidates read it back with numpy alone.
+Wire format of one rank's result (v4, include/sst.h sst_wire_pack): packed
+on the device by one kernel (no host round trip): 1-bit is_valid codes,
+2-bit status codes (NONE / EMPTY / hit / listed), per pair-path hit its
+first pair-list entry in w = ceil(log2(pair-list entries)) bits and a 2-bit
+count code (3 bits; the receiver rebuilds the candidates from its own copy of the
+table's pair list, so those hits send no payload), 12-B records and the
+payload for the few hits of the deferred paths, and a list of the rare rest
+(is_valid raises, statuses other than NONE / EMPTY / SOME, counts outside
+1..7).  About 0.125 B per is_valid query, 0.25 B per explain query and
+~2 B per pair hit: ~6.7 MB per rank per config-3 step (v3, 2-bit codes and 4 B per pair hit: 10.7 MB;
+v2, 12-B records + the dense payload: 33 MB; the engine's own layout: 51 MB).
+wire_pack_host states the packer in numpy; wire_unpack + decode_hits +
+candidates read a buffer back with numpy alone.
 """
 import os
 
@@ -111,22 +115,30 @@ def device_bytes(ptr, nbytes, device):
     return torch.as_tensor(_Iface(), device=device)
 
 
-WIRE_HEADER = 64
-WIRE_MAGIC = 0x3357545353  # "SSTW3"
+WIRE_HEADER = 128
+WIRE_MAGIC = 0x3457545353  # "SSTW4"
 SST_NONE, SST_EMPTY, SST_SOME, SST_OUT_OF_TABLE, SST_OVERFLOW, SST_ABORTED = 0, 1, 2, -1, -2, -4
 SCAN_WAVES_PER_WG = 16  # k_explain_scan: 1024-lane workgroups
+LIST_RAISE, LIST_STATUS, LIST_COUNT = 0, 1, 2  # wire list entry types
 
 
 def _pack2(codes):
-    """uint8 codes in {0..3} -> 4 per byte (torch, on the codes' device)."""
-    import torch
-
-    n = codes.numel()
-    pad = (-n) % 4
-    if pad:
-        codes = torch.cat([codes, torch.zeros(pad, dtype=torch.uint8, device=codes.device)])
-    c = codes.view(-1, 4)
+    """uint8 codes in {0..3} -> 4 per byte."""
+    c = np.asarray(codes, dtype=np.uint8)
+    c = np.concatenate([c, np.zeros((-len(c)) % 4, np.uint8)]).reshape(-1, 4)
     return c[:, 0] | (c[:, 1] << 2) | (c[:, 2] << 4) | (c[:, 3] << 6)
+
+
+def _pack3(codes):
+    """codes in {0..7} -> 10 per little-endian u32 (bits 3k..3k+2), as bytes."""
+    c = np.asarray(codes, dtype=np.uint32)
+    c = np.concatenate([c, np.zeros((-len(c)) % 10, np.uint32)]).reshape(-1, 10)
+    return (c << (3 * np.arange(10, dtype=np.uint32))).sum(axis=1, dtype=np.uint32).view(np.uint8)
+
+
+def _unpack3(b, n):
+    w = np.asarray(b, dtype=np.uint8)[:4 * ((n + 9) // 10)].view(np.uint32)
+    return ((w[:, None] >> (3 * np.arange(10, dtype=np.uint32))) & 7).ravel()[:n].astype(np.int64)
 
 
 def _unpack2(b, n):
@@ -159,101 +171,134 @@ def scan_order_key(q, n, n_wg):
     return ((b * SCAN_WAVES_PER_WG + w) * rounds + r) * 64 + lane
 
 
-def wire_pack(valid, status, hits, payload, refs=None, n_pair=0, pair_bytes=0, n_wg=0, key=0):
-    """One rank's result in the wire format (v3) as a flat uint8 tensor on
-    the parts' device, built with tensor ops (no host round trip).
-    valid / status: int8 tensors (is_valid results, explain statuses); hits:
-    the engine's dense hit list as a uint8 tensor (16-B records,
-    sst_result_hit_list); payload: the dense payload (uint8); refs, n_pair,
-    pair_bytes, n_wg: the pair-path part (sst_result_pair_hits, refs as a
-    uint8 tensor of 2 B per pair hit); key: pair_key of the table's pair
-    records.
+def _a8(x):
+    return (int(x) + 7) & ~7
 
-      header   8 x i64: magic, n_valid, n_explain, n_pair, n_explicit,
-               payload bytes, n_wg, key
-      valid    2-bit codes (is_valid + 1: 0 raise, 1 False, 2 True), 4 per byte
-      status   2-bit codes: 0 NONE, 1 EMPTY, 2 pair hit, 3 OUT_OF_TABLE or an
-               explicit hit
-      pairs    per pair hit, in the scan's order (scan_order_key): u16 first
-               pair-list entry | 0x8000 for OVERFLOW, u16 count.  The
-               candidates are the entries first .. first + count - 1: no payload
-      explicit 12-B records {u32 query | kind << 30, u32 a, u32 b} of the other
-               hits (deferred paths): kind 0 SOME (a = candidates, b = payload
-               offset), 1 OVERFLOW / 2 ABORTED (a, b = the exact count)
-      payload  the explicit hits' payload ([k][row_0..row_{k-1}] per candidate)
-    """
-    import torch
 
-    dev = status.device
-    st = status.view(torch.int8)
-    r = hits.view(torch.int32).view(-1, 4)
-    nh = r.shape[0]
-    if not 0 <= n_pair <= nh or pair_bytes > payload.numel():
+def first_width(n_entries):
+    """Bits per pair hit's first entry: ceil(log2(pair-list entries)), >= 1."""
+    w = 1
+    while (1 << w) < n_entries:
+        w += 1
+    return w
+
+
+def wire_layout(n_valid, n_explain, n_pair, n_explicit, xpay, w):
+    """Byte offsets of the wire v4 sections (include/sst.h, sst_wire_pack):
+    every section starts 8-byte aligned; 'list' is the fixed part's size."""
+    o = {"valid": WIRE_HEADER}
+    o["status"] = o["valid"] + _a8((n_valid + 7) // 8)
+    o["first"] = o["status"] + _a8((n_explain + 3) // 4)
+    o["codes"] = o["first"] + 8 * ((n_pair * w + 63) // 64)
+    o["explicit"] = o["codes"] + 8 * ((n_pair + 19) // 20)
+    o["payload"] = o["explicit"] + _a8(12 * n_explicit)
+    o["list"] = o["payload"] + _a8(xpay)
+    return o
+
+
+def wire_pack_host(valid, status, hits, payload, refs=None, n_pair=0, pair_bytes=0, n_wg=0, recs=None):
+    """numpy statement of sst_wire_pack (the device packer of the gather's
+    wire format v4) for host-side results: valid / status int8 arrays, hits
+    the dense hit list as u32 [n, 4] {query, count, word lo, word hi}, payload
+    u8, refs u16 per pair hit (first | 0x8000 for OVERFLOW), recs the table's
+    pair records.  Same bytes as the device packer except the list entries'
+    order (here: by type, then index)."""
+    valid = np.asarray(valid, dtype=np.int8)
+    st = np.asarray(status, dtype=np.int8)
+    hits = np.asarray(hits, dtype=np.uint32).reshape(-1, 4)
+    payload = np.asarray(payload, dtype=np.uint8)
+    nh, n7, n8 = len(hits), len(valid), len(st)
+    if not 0 <= n_pair <= nh or pair_bytes > len(payload):
         raise ValueError("wire format: pair part larger than the result")
-    if payload.numel() - pair_bytes >= (1 << 32):
+    if n7 >= 1 << 30 or n8 >= 1 << 30:
+        raise ValueError("wire format: list entries index at most 2^30 queries")
+    n_exp, xpay = nh - n_pair, len(payload) - pair_bytes
+    if xpay >= 1 << 32:
         raise ValueError("wire format: explicit payload offsets are 32-bit")
-    mark = torch.zeros(st.numel(), dtype=torch.bool, device=dev)
+    E = len(recs) if (n_pair and recs is not None) else 0
+    w = first_width(E)
+    o = wire_layout(n7, n8, n_pair, n_exp, xpay, w)
+    # list entries
+    lst = []
+    for q in np.flatnonzero(valid == -1):
+        lst.append((LIST_RAISE, int(q), 0))
+    for q in np.flatnonzero((st != SST_NONE) & (st != SST_EMPTY) & (st != SST_SOME)):
+        lst.append((LIST_STATUS, int(q), int(np.uint8(st[q]))))
+    cnt = hits[:n_pair, 1].astype(np.int64)
+    for i in np.flatnonzero((cnt < 1) | (cnt > 7)):
+        lst.append((LIST_COUNT, int(i), int(cnt[i])))
+    buf = np.zeros(o["list"] + 8 * len(lst), np.uint8)
+    hdr = [WIRE_MAGIC, n7, n8, n_pair, n_exp, xpay, n_wg, pair_key(recs) if n_pair else 0, w, len(lst), len(lst),
+           o["list"], 0, 0, 0, 0]
+    buf[:WIRE_HEADER] = np.array(hdr, dtype=np.uint64).view(np.uint8)
+    vb = np.packbits(valid == 1, bitorder="little")
+    buf[o["valid"]:o["valid"] + len(vb)] = vb
+    hit = (st == SST_SOME) | (st == SST_OVERFLOW) | (st == SST_ABORTED)
+    code = np.where(st == SST_NONE, 0, np.where(st == SST_EMPTY, 1, np.where(hit, 2, 3))).astype(np.uint8)
+    sb = _pack2(code)
+    buf[o["status"]:o["status"] + len(sb)] = sb
     if n_pair:
-        mark[r[:n_pair, 0].long()] = True
-    code8 = torch.where(st == SST_NONE, 0, torch.where(st == SST_EMPTY, 1, torch.where(mark, 2, 3))).to(torch.uint8)
-    code7 = (valid.view(torch.int8) + 1).to(torch.uint8)
-    if n_pair:
-        pairs = torch.stack([refs.view(torch.int16)[:n_pair], r[:n_pair, 1].to(torch.int16)], dim=1)
-    else:
-        pairs = torch.zeros((0, 2), dtype=torch.int16, device=dev)
-    e = r[n_pair:]
-    if e.shape[0]:
-        kind = st[e[:, 0].long()]
-        kind = torch.where(kind == SST_OVERFLOW, 1, torch.where(kind == SST_ABORTED, 2, 0)).to(torch.int32)
+        f = np.asarray(refs, dtype=np.uint16)[:n_pair].astype(np.int64) & 0x7FFF
+        fb = np.packbits(((f[:, None] >> np.arange(w)) & 1).astype(np.uint8).ravel(), bitorder="little")
+        buf[o["first"]:o["first"] + len(fb)] = fb
+        cb = _pack3(np.where((cnt >= 1) & (cnt <= 7), cnt, 0))
+        buf[o["codes"]:o["codes"] + len(cb)] = cb
+    e = hits[n_pair:]
+    if n_exp:
+        s = st[e[:, 0].astype(np.int64)]
+        kind = np.where(s == SST_OVERFLOW, 1, np.where(s == SST_ABORTED, 2, 0)).astype(np.uint32)
         some = kind == 0
-        rec = torch.stack([e[:, 0] | (kind << 30), torch.where(some, e[:, 1], e[:, 2]),
-                           torch.where(some, ((e[:, 2].long() & 0xFFFFFFFF) - int(pair_bytes)).to(torch.int32),
-                                       e[:, 3])], dim=1)
-    else:
-        rec = torch.zeros((0, 3), dtype=torch.int32, device=dev)
-    hdr = torch.tensor([WIRE_MAGIC, valid.numel(), st.numel(), n_pair, nh - n_pair, payload.numel() - pair_bytes,
-                        n_wg, key], dtype=torch.int64, device=dev)
-    return torch.cat([hdr.view(torch.uint8), _pack2(code7), _pack2(code8), pairs.contiguous().view(torch.uint8).view(-1),
-                      rec.contiguous().view(torch.uint8).view(-1), payload.view(torch.uint8)[pair_bytes:]])
-
-
-def wire_size(n_valid, n_explain, n_hits, payload_bytes, n_pair=0, pair_bytes=0):
-    """Bytes of wire_pack's buffer for a result of these sizes."""
-    return (WIRE_HEADER + (n_valid + 3) // 4 + (n_explain + 3) // 4 + 4 * n_pair + 12 * (n_hits - n_pair)
-            + payload_bytes - pair_bytes)
+        off = ((e[:, 2].astype(np.uint64) | (e[:, 3].astype(np.uint64) << np.uint64(32))) - np.uint64(pair_bytes))
+        rec = np.stack([e[:, 0] | (kind << np.uint32(30)), np.where(some, e[:, 1], e[:, 2]),
+                        np.where(some, (off & np.uint64(0xFFFFFFFF)).astype(np.uint32), e[:, 3])], axis=1)
+        buf[o["explicit"]:o["explicit"] + 12 * n_exp] = rec.astype(np.uint32).view(np.uint8).ravel()
+    buf[o["payload"]:o["payload"] + xpay] = payload[pair_bytes:]
+    if lst:
+        ent = np.array([((t << 30) | i, v) for t, i, v in lst], dtype=np.uint32)
+        buf[o["list"]:] = ent.view(np.uint8).ravel()
+    return buf
 
 
 def wire_unpack(buf, recs=None):
-    """numpy form of a wire buffer: (valid i8, status i8, hits u32[n,4] in
-    the engine's record layout {query, count, word lo, word hi}, payload u8).
-    recs: the table's pair records (sst_table_pair_records), needed when the
-    buffer holds pair hits.  The pair hits' candidates are rebuilt from the
-    pair list (dense, in scan order, no pad bytes) ahead of the explicit
-    payload: the same candidates per query as the sender's result, in
-    another payload layout (canonical_digest compares the two)."""
+    """numpy form of a wire v4 buffer (sst_wire_pack / wire_pack_host; a
+    gathered buffer may carry padding after its list): (valid i8, status i8,
+    hits u32[n,4] in the engine's record layout {query, count, word lo, word
+    hi}, payload u8).  recs: the table's pair records
+    (sst_table_pair_records), needed when the buffer holds pair hits.  The
+    pair hits' candidates are rebuilt from the pair list (dense, in scan
+    order, no pad bytes) ahead of the explicit payload: the same candidates
+    per query as the sender's result, in another payload layout
+    (canonical_digest compares the two)."""
     b = np.ascontiguousarray(np.asarray(buf, dtype=np.uint8))
-    magic, n7, n8, npair, nexp, nb, n_wg, key = (int(x) for x in b[:64].view(np.int64))
+    if len(b) < WIRE_HEADER:
+        raise ValueError("not a wire buffer")
+    h = [int(x) for x in b[:WIRE_HEADER].view(np.uint64)]
+    magic, n7, n8, npair, nexp, nb, n_wg, key, w, n_list, list_cap, o_list = h[:12]
     if magic != WIRE_MAGIC:
         raise ValueError("not a wire buffer")
-    o = WIRE_HEADER
-    k7, k8 = (n7 + 3) // 4, (n8 + 3) // 4
-    valid = _unpack2(b[o:o + k7], n7).astype(np.int8) - 1
-    o += k7
-    code = _unpack2(b[o:o + k8], n8)
-    o += k8
-    pairs = b[o:o + 4 * npair].view(np.uint16).reshape(npair, 2)
-    o += 4 * npair
-    rec = b[o:o + 12 * nexp].view(np.uint32).reshape(nexp, 3)
-    o += 12 * nexp
-    xpay = b[o:o + nb]
-    if o + nb != len(b):
-        raise ValueError(f"wire buffer of {len(b)} B, header says {o + nb} B")
-    status = np.select([code == 0, code == 1, code == 2], [SST_NONE, SST_EMPTY, SST_SOME], SST_OUT_OF_TABLE)
-    status = status.astype(np.int8)
-    # pair hits: the queries with code 2, in the scan's order
-    qp = np.flatnonzero(code == 2)
+    o = wire_layout(n7, n8, npair, nexp, nb, w)
+    if o["list"] != o_list:
+        raise ValueError("wire buffer: header and layout disagree")
+    if n_list > list_cap or o_list + 8 * n_list > len(b):
+        raise ValueError(f"wire buffer: {n_list} list entries, room for {min(list_cap, (len(b) - o_list) // 8)}")
+    ent = b[o_list:o_list + 8 * n_list].view(np.uint32).reshape(n_list, 2)
+    typ, idx, val = ent[:, 0] >> 30, (ent[:, 0] & 0x3FFFFFFF).astype(np.int64), ent[:, 1]
+    valid = np.unpackbits(b[o["valid"]:o["status"]], bitorder="little")[:n7].astype(np.int8)
+    valid[idx[typ == LIST_RAISE]] = -1
+    code = _unpack2(b[o["status"]:o["first"]], n8)
+    hit = code == 2
+    status = np.select([code == 1, hit], [SST_EMPTY, SST_SOME], SST_NONE).astype(np.int8)
+    m = typ == LIST_STATUS
+    status[idx[m]] = val[m].astype(np.uint8).view(np.int8)
+    rec = b[o["explicit"]:o["explicit"] + 12 * nexp].view(np.uint32).reshape(nexp, 3)
+    q = (rec[:, 0] & 0x3FFFFFFF).astype(np.int64)
+    kind = rec[:, 0] >> 30
+    # pair hits: the hit bits of queries without an explicit record, in the scan's order
+    pmask = hit.copy()
+    pmask[q] = False
+    qp = np.flatnonzero(pmask)
     if len(qp) != npair:
-        raise ValueError(f"wire buffer: {len(qp)} pair-hit codes, header says {npair}")
+        raise ValueError(f"wire buffer: {len(qp)} pair hits flagged, header says {npair}")
     ppay = np.zeros(0, np.uint8)
     phits = np.zeros((npair, 4), np.uint32)
     if npair:
@@ -261,27 +306,28 @@ def wire_unpack(buf, recs=None):
             raise ValueError("wire buffer: pair hits need the sender's pair records")
         recs = np.asarray(recs, dtype=np.uint32)
         qp = qp[np.argsort(scan_order_key(qp, n8, n_wg), kind="stable")]
-        first = (pairs[:, 0] & 0x7FFF).astype(np.int64)
-        ovf = (pairs[:, 0] >> 15).astype(bool)
-        cnt = pairs[:, 1].astype(np.int64)
+        fb = np.unpackbits(b[o["first"]:o["codes"]], bitorder="little")[:npair * w].reshape(npair, w)
+        first = fb.astype(np.int64) @ (np.int64(1) << np.arange(w, dtype=np.int64))
+        cnt = _unpack3(b[o["codes"]:o["explicit"]], npair)
+        m = typ == LIST_COUNT
+        cnt[idx[m]] = val[m]
+        ovf = status[qp] == SST_OVERFLOW
         status[qp] = np.where(ovf, SST_OVERFLOW, SST_SOME)
         c_some = np.where(ovf, 0, cnt)  # OVERFLOW: the count only
         starts = np.cumsum(c_some) - c_some
-        idx = np.repeat(first - starts, c_some) + np.arange(int(c_some.sum()))
-        r32 = recs[idx]
+        ix = np.repeat(first - starts, c_some) + np.arange(int(c_some.sum()))
+        r32 = recs[ix]
         lens = 1 + (r32 & 0xFF).astype(np.int64)
         ppay = r32.view(np.uint8).reshape(-1, 4)[np.arange(4)[None, :] < lens[:, None]]
         hb = np.zeros(npair, np.int64)  # payload bytes per hit
-        if len(idx):
-            owner = np.repeat(np.arange(npair), c_some)
-            np.add.at(hb, owner, lens)
+        if len(ix):
+            np.add.at(hb, np.repeat(np.arange(npair), c_some), lens)
         off = np.cumsum(hb) - hb
         phits[:, 0] = qp
         phits[:, 1] = cnt
         phits[:, 2] = np.where(ovf, cnt, off & 0xFFFFFFFF)
         phits[:, 3] = np.where(ovf, 0, off >> 32)
-    q = (rec[:, 0] & 0x3FFFFFFF).astype(np.int64)
-    kind = rec[:, 0] >> 30
+    xpay = b[o["payload"]:o["payload"] + nb]
     status[q] = np.select([kind == 1, kind == 2], [SST_OVERFLOW, SST_ABORTED], SST_SOME)
     ehits = np.zeros((nexp, 4), np.uint32)
     ehits[:, 0] = q
@@ -292,6 +338,12 @@ def wire_unpack(buf, recs=None):
     ehits[:, 2] = np.where(some, xoff & np.uint64(0xFFFFFFFF), rec[:, 1])
     ehits[:, 3] = np.where(some, xoff >> np.uint64(32), rec[:, 2])
     return valid, status, np.concatenate([phits, ehits]), np.concatenate([ppay, xpay])
+
+
+def wire_used_bytes(buf):
+    """Bytes a packed wire buffer uses: its fixed part plus its list."""
+    h = np.asarray(buf[:WIRE_HEADER], dtype=np.uint8).view(np.uint64)
+    return int(h[11]) + 8 * int(h[9])
 
 
 def canonical_digest(status, count, offset, payload):

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(HERE, ".."), HERE]
 import _oracle as oracle  # noqa: E402  (test infrastructure: the answers each rank encodes)
 from spectrseqtools_amd.parallel import (Gatherer, candidates, decode_hits, dist_env, pair_key,  # noqa: E402
-                                         scan_order_key, shard_by_weight, shard_range, wire_pack, wire_unpack)
+                                         scan_order_key, shard_by_weight, shard_range, wire_pack_host, wire_unpack)
 
 ROWS = [0, 305042, 306026, 329053, 345048]  # canonical alphabet (a 5 x 377 397 table)
 TOL, PREC, CAP = 1e-5, 1e-3, 1
@@ -31,6 +31,8 @@ def rank_queries(rank, n=600):
     m[:20] = rng.uniform(0.0, 0.2, 20)  # below the first reachable mass: NONE / EMPTY
     t = TOL * rng.uniform(300, 3000, n)
     t[20:120] = rng.uniform(1.0, 3.0, 100)  # wide windows: several candidates (OVERFLOW past CAP)
+    m[120:130], t[120:130] = rng.uniform(648.0, 652.0, 10), 45.0  # all 10 two-row sums: listed counts (> 7)
+    m[130:135] = 1e5  # beyond the table: is_valid raises, explain OUT_OF_TABLE
     return m, t
 
 
@@ -85,6 +87,8 @@ def engine_layout(answers, masses, thr, sums, recs, n_wg):
                 pair.append((i, int(a), int(b - a), over))
             else:
                 other.append((i, sols, over))
+        elif st == -1:
+            status[i] = -1  # SST_OUT_OF_TABLE
         else:
             status[i] = 1 if (st == 1 and n_empty) else 0
     pair.sort(key=lambda x: int(scan_order_key([x[0]], n, n_wg)[0]))
@@ -157,9 +161,11 @@ def main():
     st, hits, pay, refs, n_pair, pair_bytes = engine_layout(ans, masses, thr, sums, recs, n_wg)
     assert 0 < n_pair < len(hits)  # both kinds of hit records travel
     valid = np.array([oracle.is_valid(table, 32, m, t, TOL) for m, t in zip(masses, thr)], np.int8)
-    wire = wire_pack(torch.from_numpy(valid), torch.from_numpy(st), torch.from_numpy(hits.view(np.uint8).ravel()),
-                     torch.from_numpy(pay), torch.from_numpy(refs.view(np.uint8)), n_pair, pair_bytes, n_wg,
-                     pair_key(recs))
+    wire = wire_pack_host(valid, st, hits, pay, refs, n_pair, pair_bytes, n_wg, recs)
+    ent = wire[int(wire[88:96].view(np.uint64)[0]):].view(np.uint32).reshape(-1, 2)
+    kinds = set((ent[:, 0] >> 30).tolist())
+    assert kinds == {0, 1, 2}, kinds  # raises, statuses other than NONE / SOME, pair counts outside 1..7
+    wire = torch.from_numpy(wire)
     g2 = Gatherer(dist, torch.device("cpu"))
     g2.agree(wire.numel())
     got = g2.gather(wire)
@@ -178,6 +184,8 @@ def main():
                 elif s0 == 1 and sols:
                     assert st_r[i] == 2 and sorted(candidates(pay_r, cnt, off, i)) == sols, (r, i)
                     n_some += 1
+                elif s0 == -1:
+                    assert st_r[i] == -1, (r, i)
                 else:
                     assert st_r[i] == (1 if (s0 == 1 and n_empty) else 0), (r, i)
                 n_checked += 1

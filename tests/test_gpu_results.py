@@ -168,39 +168,47 @@ def test_hit_list_matches_result_arrays(engine, dev, rows):
 
 
 def test_wire_pair_hits_roundtrip(engine, dev, rows):
-    """sst_result_pair_hits + parallel.wire_pack / wire_unpack (the N>1
-    gather's wire format v3) on a real device pass: the pair-path hits come
+    """sst_result_pair_hits + sst_wire_pack / parallel.wire_unpack (the N>1
+    gather's wire format v4) on a real device pass: the pair-path hits come
     in the documented scan order (several tile rounds per wave), their refs
-    name the pair-list entries of their candidates (SOME and OVERFLOW), and
-    the decoded wire holds exactly the result's answers (canonical digest:
-    status, counts, every query's candidate bytes)."""
+    name the pair-list entries of their candidates (SOME and OVERFLOW), the
+    device packer writes the bytes of the numpy statement (wire_pack_host;
+    list entries in any order), and the decoded wire holds exactly the
+    result's answers (canonical digest: status, counts, every query's
+    candidate bytes) and the is_valid codes.  A buffer too small for the list
+    is refused by the receiver."""
     torch = pytest.importorskip("torch")
-    from spectrseqtools_amd.parallel import (canonical_digest, decode_hits, device_bytes, pair_key, scan_order_key,
-                                             wire_pack, wire_size, wire_unpack)
+    from spectrseqtools_amd.parallel import (canonical_digest, decode_hits, device_bytes, scan_order_key,
+                                             wire_pack_host, wire_unpack, wire_used_bytes)
 
     rng = np.random.default_rng(15)
     m2, t2 = _queries(rng, rows, 600_000, 2)
     m3, t3 = _queries(rng, rows, 3000, 3)
-    masses, thr = np.concatenate([m2, m3]), np.concatenate([t2, t3])
+    masses, thr = np.concatenate([m2, m3, np.full(7, 1e7)]), np.concatenate([t2, t3, np.full(7, 0.01)])
     perm = rng.permutation(len(masses))
     masses, thr = masses[perm], thr[perm]
     n = len(masses)
     dev_t = torch.device("cuda", engine.device)
     dm = torch.from_numpy(masses).to(dev_t)
     dt = torch.from_numpy(thr).to(dev_t)
+    valid = rng.integers(-1, 2, 100_003).astype(np.int8)
+    dv = torch.from_numpy(valid).to(dev_t)
     torch.cuda.synchronize()
     res = dev.explain_device(dm.data_ptr(), dt.data_ptr(), n, TOL, PREC, 10, cap=3)
     hits_p, n_hits = res.hit_list_device()
     refs_p, n_pair, pair_bytes, n_wg = res.pair_hits_device()
     assert 0 < n_pair < n_hits and n_wg > 1
     assert -(-((n + 63) // 64) // (16 * n_wg)) > 1  # several tile rounds per scan wave
-    st_p, _c, _o, pay_p, nb = res.device_views(arrays=False)
     hits = device_bytes(hits_p, 16 * n_hits, dev_t)
     recs = dev.pair_records()
-    wire = wire_pack(torch.zeros(5, dtype=torch.int8, device=dev_t), device_bytes(st_p, n, dev_t), hits,
-                     device_bytes(pay_p, nb, dev_t), device_bytes(refs_p, 2 * n_pair, dev_t), n_pair, pair_bytes,
-                     n_wg, pair_key(recs))
-    assert wire.numel() == wire_size(5, n, n_hits, nb, n_pair, pair_bytes)
+    fixed = res.wire_pack(dv.data_ptr(), len(valid))  # sizing only
+    cap = fixed + 8 * (len(valid) + n + n_pair)
+    wbuf = torch.zeros(cap, dtype=torch.uint8, device=dev_t)
+    torch.cuda.synchronize()  # the engine stream packs into it
+    assert res.wire_pack(dv.data_ptr(), len(valid), wbuf.data_ptr(), cap) == fixed
+    torch.cuda.synchronize()
+    engine.synchronize()
+    wire = wbuf.cpu().numpy()
     res.fetch_device()
     h = hits.cpu().numpy().view(np.uint32).reshape(-1, 4)
     q = h[:n_pair, 0].astype(np.int64)
@@ -213,10 +221,31 @@ def test_wire_pair_hits_roundtrip(engine, dev, rows):
         first, cnt = int(refs[j] & 0x7FFF), int(h[j, 1])
         want = [tuple((int(r) >> (8 * (k + 1))) & 0xFF for k in range(int(r) & 0xFF)) for r in recs[first:first + cnt]]
         assert res.candidates(int(q[j])) == want, j
-    v_, st_, hits_, pay_ = wire_unpack(wire.cpu().numpy(), recs)
+    # the device packer's bytes = the numpy statement's
+    used = wire_used_bytes(wire)
+    want = wire_pack_host(valid, res.status, h, res.payload, refs, n_pair, pair_bytes, n_wg, recs)
+    assert used == len(want) and used > fixed  # raises, OUT_OF_TABLE / OVERFLOW statuses, counts > 7 listed
+    hw, hh = wire[:128].view(np.uint64).copy(), want[:128].view(np.uint64).copy()
+    hw[10] = hh[10] = 0  # list capacity: the buffer's, not the result's
+    assert np.array_equal(hw, hh)
+    assert np.array_equal(wire[128:fixed], want[128:fixed])
+    srt = lambda b: np.sort(b[fixed:used].view(np.uint64))  # list entries: in any order
+    assert np.array_equal(srt(wire), srt(want))
+    types = set((wire[fixed:used].view(np.uint32)[0::2] >> 30).tolist())
+    assert types == {0, 1, 2}, types
+    v_, st_, hits_, pay_ = wire_unpack(wire, recs)
     cnt_, off_ = decode_hits(st_, hits_)
+    assert np.array_equal(v_, valid)
     assert np.array_equal(st_, res.status)
     assert canonical_digest(st_, cnt_, off_, pay_) == canonical_digest(res.status, res.count, res.offset, res.payload)
+    # no room for the list: the receiver refuses the buffer
+    small = torch.zeros(fixed, dtype=torch.uint8, device=dev_t)
+    torch.cuda.synchronize()
+    res.wire_pack(dv.data_ptr(), len(valid), small.data_ptr(), fixed)
+    torch.cuda.synchronize()
+    engine.synchronize()
+    with pytest.raises(ValueError, match="list entries"):
+        wire_unpack(small.cpu().numpy(), recs)
 
 
 def test_step_device_equals_separate_calls(engine, dev, rows):
