@@ -720,7 +720,7 @@ int sst_is_valid_batch(sst_table* t, const double* mass, const double* thr, int6
 
 namespace {
 
-constexpr int kDeepBlocks = 4096;       // 64-lane blocks per deep role (fast, no-memo) of the deferred kernel:
+constexpr int kDeepBlocks = 4096;       // waves (64 lanes) per deep role (fast, no-memo) of the deferred kernel:
                                         // 4 waves per SIMD, so the latency-bound DFS lanes overlap their loads
 constexpr uint32_t kHashCap0 = 1u << 14;  // exact-path hash entries per lane (first attempt)
 constexpr int kExactLanes0 = 2048;      // exact-path concurrent lanes (first attempt)
