@@ -10,7 +10,10 @@ namespace sst {
 
 constexpr int kMaxRows = 120;      // rows 0..119; index record keeps lo in bits 56..63
 constexpr int kWG = 256;           // workgroup of the lane-per-query kernels (4 waves)
-constexpr int kDefWG = 256;        // k_explain_deferred workgroup (4 waves; the deep role allocates per workgroup)
+#ifndef SST_DEF_WG
+#define SST_DEF_WG 256
+#endif
+constexpr int kDefWG = SST_DEF_WG;        // k_explain_deferred workgroup (4 waves; the deep role allocates per workgroup)
 constexpr int kShallowDepth = 4;   // register-stack depth of the main kernel
 constexpr int kMaxDepth = 96;      // >= max items of any multiset in a table (73 for the full alphabet)
 constexpr int kInfBudget = 1 << 30;  // np.inf budget (decremented at most kMaxDepth times)

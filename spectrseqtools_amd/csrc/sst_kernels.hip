@@ -1184,7 +1184,7 @@ __device__ __forceinline__ uint64_t wave_incl_scan(uint64_t x) {
 // Sum a per-lane counter over the workgroup and add it to stats[k] with one
 // atomic (all threads of the workgroup must call it).
 __device__ __forceinline__ void wg_stat(unsigned long long* stats, int k, uint64_t v) {
-  __shared__ uint64_t red[kWG / 64];
+  __shared__ uint64_t red[1024 / 64];  // up to 1024-lane workgroups
   for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -1345,9 +1345,9 @@ __device__ __forceinline__ TileOut spill_alloc_wg(const OutArgs& out, uint64_t b
   return r;
 }
 __device__ __forceinline__ void emit_result_wg(const OutArgs& out, bool live, uint32_t i, int8_t status,
-                                               uint64_t count, uint64_t off) {
+                                               uint64_t count, uint64_t off, bool lane_owns = true) {
   if (live) out.status[i] = status;
-  const bool hit = live && (status == SST_SOME || status == SST_OVERFLOW || status == SST_ABORTED);
+  const bool hit = live && lane_owns && (status == SST_SOME || status == SST_OVERFLOW || status == SST_ABORTED);
   const uint32_t k = (uint32_t)wg_alloc(out.dhit_count, hit ? 1u : 0u);
   if (hit) {
     const bool some = status == SST_SOME;
@@ -1440,6 +1440,8 @@ __device__ __forceinline__ void pair_store(const PairLds& p, uint32_t first, uin
 // class lists, status pending), run the SHALLOW fast path on the rest (all
 // DFS state and the first 16 payload bytes in VGPRs), allocate payload in the
 // spill area and write the status byte and hit record.
+// WG: workgroup-wide allocation (the caller's trip count is workgroup-uniform)
+template <bool WG = false>
 __device__ __forceinline__ void shallow_item(const TableArgs& t, const QueryArgs& q, const OutArgs& out, const Lds& s,
                                              bool live, uint32_t i, int64_t a, int64_t b, uint32_t flags, int lane,
                                              ShallowStats& st) {
@@ -1469,7 +1471,8 @@ __device__ __forceinline__ void shallow_item(const TableArgs& t, const QueryArgs
     if (deferred) status = (int8_t)kStatusPending;
   }
   route_append(out, q.n, cls, i);
-  const TileOut to = spill_alloc(out, lane, status == SST_SOME ? eo.bytes : 0, status);
+  const uint64_t want = status == SST_SOME ? eo.bytes : 0;
+  const TileOut to = WG ? spill_alloc_wg(out, want, status) : spill_alloc(out, lane, want, status);
   if (to.bytes) {
     if (!sink.over) {
       sink.flush(out.payload + to.off, to.bytes);
@@ -1480,7 +1483,10 @@ __device__ __forceinline__ void shallow_item(const TableArgs& t, const QueryArgs
     }
   }
   // deferred queries: pending here, the deep / exact roles write their result
-  emit_result(out, live, i, to.status, eo.count, to.off, !deferred);
+  if (WG)
+    emit_result_wg(out, live, i, to.status, eo.count, to.off, !deferred);
+  else
+    emit_result(out, live, i, to.status, eo.count, to.off, !deferred);
   st.payload += to.bytes;
 }
 __device__ __forceinline__ void shallow_chunk(const TableArgs& t, const QueryArgs& q, const OutArgs& out, const Lds& s,
@@ -1990,8 +1996,9 @@ __device__ void shallow_list_body(const TableArgs& t, const QueryArgs& q, const 
   const int lane = threadIdx.x & 63;
   const int64_t nthreads = (int64_t)nblk * blockDim.x;
   ShallowStats st{0, 0, 0};
-  for (int64_t j0 = (int64_t)blk * blockDim.x + (threadIdx.x - lane); j0 < (int64_t)n_list; j0 += nthreads) {  // wave-uniform
-    const int64_t j = j0 + lane;
+  // workgroup-uniform trip count: one allocation atomic per workgroup (wg_alloc)
+  for (int64_t jb = (int64_t)blk * blockDim.x; jb < (int64_t)n_list; jb += nthreads) {
+    const int64_t j = jb + threadIdx.x;
     const bool live = j < (int64_t)n_list;
     uint32_t i = 0, flags = 0;
     int64_t a = 1, b = 0;
@@ -2003,7 +2010,7 @@ __device__ void shallow_list_body(const TableArgs& t, const QueryArgs& q, const 
       a = lo < 1 ? 1 : lo;
       b = hi;
     }
-    shallow_item(t, q, out, s, live, i, a, b, flags, lane, st);
+    shallow_item<true>(t, q, out, s, live, i, a, b, flags, lane, st);
   }
   for (int o = 32; o > 0; o >>= 1) {
     st.q += __shfl_down(st.q, o, 64);
