@@ -330,8 +330,15 @@ def main():
                 settle(results[k_last & 1])
 
     # untimed reference pass: sizes for the gather and the expected result
-    tdev.is_valid_peaks_device(obs_d.data_ptr(), P_peaks, shifts, dp.tolerance, dp.precision, outs7[0].data_ptr())
-    ref = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A)
+    # (the same entry point as the timed steps: the dense layout follows the
+    # scan's grid, which the fused step sizes for itself)
+    if args.fused_step:
+        ref = tdev.step_device(obs_d.data_ptr(), P_peaks, shifts, outs7[0].data_ptr(), a8m.data_ptr(), a8t.data_ptr(),
+                               n8, dp.tolerance, dp.precision, A)
+    else:
+        tdev.is_valid_peaks_device(obs_d.data_ptr(), P_peaks, shifts, dp.tolerance, dp.precision,
+                                   outs7[0].data_ptr())
+        ref = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A)
     ref.fetch_device()
     n_hits0, payload0 = ref.settle()
     ref_digest = result_digest(ref)
