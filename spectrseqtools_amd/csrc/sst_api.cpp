@@ -949,8 +949,17 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   r->settled = false;
   if (!c->ws_deep.ensure((size_t)2 * kDeepBlocks * 64 * kMaxDepth * glob_frame_bytes()))
     return fail(c, SST_E_NOMEM, "device allocation failed (deep workspace)");
-  if (c->hash_cap == 0)
-    if (int rc = ensure_exact_ws(c, kHashCap0, kExactLanes0)) return rc;
+  if (c->hash_cap == 0) {
+    // SST_EXACT_HASH_CAP0 (tests): a smaller first memo per lane, so that the
+    // retry ladder (8x the memo over 8x fewer lanes) runs down to its last rung
+    const char* e = getenv("SST_EXACT_HASH_CAP0");
+    uint32_t cap0 = kHashCap0;
+    if (e && atoi(e) >= 16) {
+      cap0 = 16;
+      while (cap0 < (uint32_t)atoi(e) && cap0 < kHashCap0) cap0 <<= 1;
+    }
+    if (int rc = ensure_exact_ws(c, cap0, kExactLanes0)) return rc;
+  }
   QueryArgs q{d_mass, d_thr, d_mods, mods_scalar, n, tol, prec, 1.0 / prec, with_memo, cap_count, kNodeBudget};
   fold_scan_limits(t->args, q);
   OutArgs o = out_args(r);

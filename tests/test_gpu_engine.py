@@ -232,3 +232,19 @@ def test_profile_sampling(full_dev, alphabet_rows):
     assert set(prof) == {_native.K_EXPLAIN_SCAN}
     assert prof[_native.K_EXPLAIN_SCAN][1] == 3  # launches 0, 3 and 6
     assert prof[_native.K_EXPLAIN_SCAN][0] > 0
+
+
+def test_exact_retry_ladder():
+    """The exact path's memo-exhaustion retries, down to the last rung (64
+    lanes: one deferred-kernel workgroup with idle waves), in a child process
+    whose first per-lane memo is 16 entries (SST_EXACT_HASH_CAP0)."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, SST_EXACT_HASH_CAP0="16")
+    here = os.path.dirname(os.path.abspath(__file__))
+    p = subprocess.run([sys.executable, os.path.join(here, "_exact_retry_check.py")], env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    assert "exact retry ladder ok" in p.stdout
