@@ -1876,9 +1876,11 @@ __global__ __launch_bounds__(kScanWG, 8) void k_explain_scan(TableArgs t, QueryA
 // scan's grid, then a7_blocks workgroups of is_valid over peaks x 4 breakage
 // weights (1 024 peaks each).  The scan's workgroups are dispatched first (its
 // look-back only ever waits for scan workgroups dispatched before it); the
-// is_valid ones fill the slots the scan's workgroups free as they finish --
-// the scan's tail -- and the step pays one launch.  (is_valid in front of
-// the scan instead: 8 us slower per step, same-box A/B.)
+// host gives a fused step one scan workgroup per CU (step_scan_wg_per_cu), so
+// the is_valid workgroups run in each CU's other half beside the scan from
+// the start, and the step pays one launch.  (is_valid in front of the scan
+// instead: 8 us slower per step; two scan workgroups per CU, is_valid only in
+// the scan's tail: 2 us slower; same-box A/Bs.)
 template <bool THR, bool MODS>
 __global__ __launch_bounds__(kScanWG, 8) void k_step(TableArgs t, QueryArgs q, OutArgs out, ValidArgs v, PeakShifts sh,
                                                    uint32_t a7_blocks) {
