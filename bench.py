@@ -11,7 +11,7 @@ spectra (10k spectra, ~1M peaks, full 104-mass /
         reference's sliding window emits (prediction.py:286-329), budget
         round(0.5*max_len)                  -> k_explain_main (+ deferred kernels)
   * N>1: spectra shard by rank (weak scaling: `--spectra` per GPU); each
-        step's complete result of every rank (wire format v4, sst_wire_pack:
+        step's complete result of every rank (wire format v5, sst_wire_pack:
         1-bit A7 / A8 codes, ~16 bits per pair-path hit, the deferred hits'
         records and payload; ~5.4 MB per rank per config-3 step) is packed on
         the device and gathered to rank 0 over RCCL on other streams while the
@@ -61,9 +61,15 @@ def result_digest(r):
 
 
 def build_workload(n_spectra, seed, dp):
+    """SURVEY 8(d) config 3's queries for `n_spectra` synthetic spectra: A7 on
+    every peak x breakage weight (classify_fragments' form); A8 on every
+    sliding-window pair of each spectrum's START and END side after the
+    is_valid and sequence-mass filters (the first filter_by_explanation
+    round without singletons), produced by the library's host-native
+    sliding window (sst_su_diff_queries)."""
+    from spectrseqtools_amd._native import su_diff_queries
     from spectrseqtools_amd.masses import build_breakage_dict
-    from spectrseqtools_amd.producers import (MAX_VARIANCE, classify_queries, diff_queries, max_nucleotide_weight,
-                                              sliding_window_pairs)
+    from spectrseqtools_amd.producers import MAX_VARIANCE, classify_queries, max_nucleotide_weight
     from spectrseqtools_amd.synthetic import make_spectra
 
     tol, prec = dp.tolerance, dp.precision
@@ -76,30 +82,24 @@ def build_workload(n_spectra, seed, dp):
     n_brk = len(brk)
     P = len(batch.observed)
     spec = np.tile(batch.spectrum, n_brk)
-    brk_names = np.array(cq.breakage)
-    is_start = np.char.find(brk_names.astype(str), "START") >= 0
-    is_end = np.char.find(brk_names.astype(str), "END") >= 0
+    names = [v[0] for v in brk.values()]
+    code = np.repeat(np.arange(n_brk), P)
+    is_start = np.array(["START" in n for n in names])[code]
+    is_end = np.array(["END" in n for n in names])[code]
     se_w = [k for k, v in brk.items() if "START_END" in v][0]
-    maxw = max_nucleotide_weight()
-    keep = valid == 1
+    # per spectrum by SU mass, ties in breakage-major order (classify_fragments' sort)
     order = np.lexsort((cq.su_mass, spec))
-    order = order[keep[order]]
-    d_all, t_all = [], []
-    bounds = np.searchsorted(spec[order], np.arange(n_spectra + 1))
-    for s in range(n_spectra):
-        idx = order[bounds[s]:bounds[s + 1]]
-        su_seq = batch.seq_mass[s] - se_w * prec
-        su, ob = cq.su_mass[idx], cq.observed[idx]
-        # filter_by_sequence_mass (fragment_classification.py:122-139)
-        full = is_start[idx] & is_end[idx]
-        ok = (su < su_seq + MAX_VARIANCE) & ((su > su_seq - MAX_VARIANCE) | ~full)
-        for side in (is_start, is_end):
-            sel = ok & side[idx]
-            d, t, _ = diff_queries(su[sel], ob[sel], tol, maxw)
-            d_all.append(d)
-            t_all.append(t)
-    diffs = np.concatenate(d_all)
-    dthr = np.concatenate(t_all)
+    order = order[(valid == 1)[order]]
+    su, ob, sp = cq.su_mass[order], cq.observed[order], spec[order]
+    # filter_by_sequence_mass (fragment_classification.py:122-139)
+    su_seq = (batch.seq_mass - se_w * prec)[sp]
+    full = is_start[order] & is_end[order]
+    ok = (su < su_seq + MAX_VARIANCE) & ((su > su_seq - MAX_VARIANCE) | ~full)
+    rows = order[ok]
+    flags = (is_start[rows].astype(np.uint8) | (is_end[rows].astype(np.uint8) << 1))
+    offsets = np.searchsorted(spec[rows], np.arange(n_spectra + 1))
+    diffs, dthr, _, _ = su_diff_queries(cq.su_mass[rows], cq.observed[rows], flags, offsets,
+                                        max_nucleotide_weight(), tol)
     return {
         "peaks": P, "a7_mass": cq.su_mass, "a7_thr": cq.threshold, "a8_mass": diffs, "a8_thr": dthr,
         "spectra": n_spectra, "a7_valid": valid, "obs": np.ascontiguousarray(batch.observed, dtype=np.float64),
@@ -122,12 +122,17 @@ def cpu_baseline(wl_fn, dp, budget_s=10.0, single_budget_s=8.0):
     A = round(dp.seq.modification_rate * dp.seq.max_len)
     all_threads = oracle.LIB.ora_num_threads()
 
+    lookups = []
+
     def leg(threads, budget, n_max):
         def run(wl):
             t0 = time.perf_counter()
             oracle.is_valid_batch(table, 32, wl["a7_mass"], wl["a7_thr"], dp.tolerance, nthreads=threads)
-            oracle.explain_batch(table, 32, alph, wl["a8_mass"], wl["a8_thr"], A, dp.tolerance, nthreads=threads)
-            return time.perf_counter() - t0
+            _, _, lk = oracle.explain_batch(table, 32, alph, wl["a8_mass"], wl["a8_thr"], A, dp.tolerance,
+                                            nthreads=threads)
+            dt = time.perf_counter() - t0
+            lookups.append(float(lk.mean()) if len(lk) else 0.0)
+            return dt
 
         # size the sample from a small probe, then repeat it until ~budget s of
         # CPU work has been timed (the same sample each time: identical results)
@@ -145,6 +150,9 @@ def cpu_baseline(wl_fn, dp, budget_s=10.0, single_budget_s=8.0):
                           f"{threads} OpenMP thread{'s' if threads > 1 else ''}, {total:.1f} s"}
 
     out = leg(all_threads, budget_s, 20000)
+    # table cells the reference DFS reads per A8 query (S of SURVEY 8(d)'s
+    # byte model), counted by the literal restatement on the sample
+    out["survey_lookups_per_a8_query"] = lookups[-1]
     out["single_core"] = leg(1, single_budget_s, 2000)
     return out
 
@@ -156,6 +164,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--spectra", type=int, default=10000, help="spectra per GPU")
     ap.add_argument("--seed", type=int, default=1000)
+    ap.add_argument("--batches", type=int, default=3,
+                    help="distinct config-3 batches cycled over the steps (>= 3: more inputs than the Infinity "
+                         "Cache holds, so every step streams its inputs from HBM)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
                     help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo: rehearsal of the "
@@ -173,6 +184,9 @@ def main():
                     help="1 (default): A7 and A8 in one launch (sst_step_device: the is_valid workgroups "
                          "behind the pair scan's grid, filling its tail); 0: two launches (then the roofline "
                          "kernel is the scan alone)")
+    ap.add_argument("--dump-gathered", default=None,
+                    help="test hook (tests/test_gpu_multirank.py): write the last step's gathered wire buffers "
+                         "(rank 0) and every rank's inputs of that step into this directory")
     ap.add_argument("--no-validate", action="store_true",
                     help="diagnostic builds only: skip the result checks after the timed region")
     ap.add_argument("--no-events", action="store_true",
@@ -218,22 +232,31 @@ def main():
                                  precision=TOLERANCE, seq=seq, engine=engine)
     A = round(seq.modification_rate * seq.max_len)  # calculate_explanations (common.py:55)
     tdev = dp.device_table
-    wl = build_workload(args.spectra, args.seed + rank * 1_000_003, dp)
-    n7, n8 = len(wl["a7_mass"]), len(wl["a8_mass"])
-    obs_d = torch.from_numpy(wl["obs"]).to(dev_t)  # A7 reads the peaks (sst_is_valid_peaks: 4 windows per peak)
-    P_peaks, shifts = len(wl["obs"]), wl["shifts"]
-    a8m = torch.from_numpy(wl["a8_mass"]).to(dev_t)
-    a8t = torch.from_numpy(wl["a8_thr"]).to(dev_t)
+    R = max(1, args.batches)
+    # R distinct batches, cycled step by step: with R >= 3 their inputs (~180
+    # MB each) and one step's outputs exceed the 256 MB Infinity Cache, so no
+    # step's inputs are still on-die from their previous use
+    wls = [build_workload(args.spectra, args.seed + 7919 * b + rank * 1_000_003, dp) for b in range(R)]
+    wl = wls[0]
+    n7s = [len(w["a7_mass"]) for w in wls]
+    n8s = [len(w["a8_mass"]) for w in wls]
+    dev_in = []
+    for w in wls:
+        dev_in.append({"obs": torch.from_numpy(w["obs"]).to(dev_t),
+                       "a8m": torch.from_numpy(w["a8_mass"]).to(dev_t),
+                       "a8t": torch.from_numpy(w["a8_thr"]).to(dev_t), "P": len(w["obs"]), "shifts": w["shifts"],
+                       "n7": len(w["a7_mass"]), "n8": len(w["a8_mass"])})
     # two result sets used in turn: while step k runs on the GPU, the host
     # settles step k-1 (waits for its pass, reads its header, runs any routed
     # deferred windows or retries) -- the pipelined consumer loop of a serving
     # deployment; every step's result is complete and checked inside the
     # timed region
-    outs7 = [torch.empty(n7, dtype=torch.int8, device=dev_t) for _ in range(2)]
+    outs7 = [torch.empty(max(n7s), dtype=torch.int8, device=dev_t) for _ in range(2)]
     torch.cuda.synchronize()
     ext = torch.cuda.ExternalStream(engine.stream, device=dev_t)
 
     results = [None, None]
+    batch_of = [None, None]  # which batch the result set last computed
     gath = Gatherer(dist, dev_t) if (dist and not args.no_gather) else None
     side = torch.cuda.Stream(device=dev_t) if args.a7_stream else None
     settled = {"n": 0, "sent": 0}
@@ -242,37 +265,38 @@ def main():
     # it (sst_wire_pack, one kernel) into wire buffer j&1 once the gather of
     # step j-2 has read that buffer (gathered[j&1]); copied[j&1]: that pack,
     # which the engine stream waits for before step j+2 reuses the same
-    # result buffers; the comm stream gathers the packed buffer
+    # result buffers; the comm stream gathers the packed buffer (sst_wire_pack
+    # itself waits for any work settling queued on the engine stream)
     comm = torch.cuda.Stream(device=dev_t) if gath is not None else None
     packer = torch.cuda.Stream(device=dev_t) if gath is not None else None
     pass_done = [torch.cuda.Event(), torch.cuda.Event()]
     copied = [None, None]
     gathered = [None, None]
     wbuf = [None, None]
+    expect = [None] * R  # per batch: (n_hits, payload bytes) of its reference pass
 
-    def settle(r):
+    def settle(r, b):
         nh, nb = r.settle()
-        if nh != n_hits0 or nb != payload0:
-            raise RuntimeError(f"step result differs from the reference pass: {nh} hits / {nb} B "
-                               f"vs {n_hits0} / {payload0}")
+        if (nh, nb) != expect[b]:
+            raise RuntimeError(f"step result differs from the reference pass: {nh} hits / {nb} B vs {expect[b]}")
         settled["n"] += 1
 
     def send(j):
         """Step j's complete result of this rank -> rank 0 in the wire format
-        v4 (sst_wire_pack, include/sst.h: 1-bit is_valid and status codes,
-        per pair-path hit its first pair-list entry in w bits and a 2-bit
+        v5 (sst_wire_pack, include/sst.h: 1-bit is_valid codes and hit flags,
+        per pair-path hit its first pair-list entry in w bits and a 3-bit
         count, which rank 0 expands from its own copy of the table's pair
         list; records + payload of the deferred paths' hits; a list of the
         rare rest)."""
-        r = results[j & 1]
-        settle(r)  # host: the pass's header (routed windows / retries handled)
+        r, b = results[j & 1], batch_of[j & 1]
+        settle(r, b)  # host: the pass's header (routed windows / retries handled)
         packer.wait_event(pass_done[j & 1])
         if side is not None:
             packer.wait_stream(side)
         if gathered[j & 1] is not None:
             packer.wait_event(gathered[j & 1])
         engine.set_stream(packer.cuda_stream)
-        r.wire_pack(outs7[j & 1].data_ptr(), n7, wbuf[j & 1].data_ptr(), wbuf[j & 1].numel())
+        r.wire_pack(outs7[j & 1].data_ptr(), n7s[b], wbuf[j & 1].data_ptr(), wbuf[j & 1].numel())
         engine.set_stream(None)
         ev = torch.cuda.Event()
         ev.record(packer)
@@ -285,78 +309,86 @@ def main():
             gathered[j & 1] = ev2
         settled["sent"] += 1
 
-    def step(k):
-        cur = k & 1
-        out7 = outs7[cur]
-        if copied[cur] is not None:  # step k-2's wire copy read these buffers
-            ext.wait_event(copied[cur])
-        # A8 first (its persistent scan grid fills the chip), then A7; the two
-        # touch disjoint buffers
+    def launch(b, out7, reuse):
+        d = dev_in[b]
         if args.fused_step:  # A7 and A8 in one launch (sst_step_device)
-            results[cur] = tdev.step_device(obs_d.data_ptr(), P_peaks, shifts, out7.data_ptr(), a8m.data_ptr(),
-                                            a8t.data_ptr(), n8, dp.tolerance, dp.precision, A, reuse=results[cur])
-            if gath is not None:
-                pass_done[cur].record(ext)
-            if k > 0:
-                if gath is not None:
-                    send(k - 1)
-                else:
-                    settle(results[cur ^ 1])
-            return
+            return tdev.step_device(d["obs"].data_ptr(), d["P"], d["shifts"], out7.data_ptr(), d["a8m"].data_ptr(),
+                                    d["a8t"].data_ptr(), d["n8"], dp.tolerance, dp.precision, A, reuse=reuse)
+        res = reuse
         if args.a7_stream != 2:
-            results[cur] = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A,
-                                               reuse=results[cur])
+            res = tdev.explain_device(d["a8m"].data_ptr(), d["a8t"].data_ptr(), d["n8"], dp.tolerance, dp.precision,
+                                      A, reuse=res)
         if side is not None:
             engine.set_stream(side.cuda_stream)
-        tdev.is_valid_peaks_device(obs_d.data_ptr(), P_peaks, shifts, dp.tolerance, dp.precision, out7.data_ptr())
+        tdev.is_valid_peaks_device(d["obs"].data_ptr(), d["P"], d["shifts"], dp.tolerance, dp.precision,
+                                   out7.data_ptr())
         if side is not None:
             engine.set_stream(None)
         if args.a7_stream == 2:
-            results[cur] = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A,
-                                               reuse=results[cur])
+            res = tdev.explain_device(d["a8m"].data_ptr(), d["a8t"].data_ptr(), d["n8"], dp.tolerance, dp.precision,
+                                      A, reuse=res)
+        return res
+
+    def step(k):
+        cur = k & 1
+        if copied[cur] is not None:  # step k-2's wire copy read these buffers
+            ext.wait_event(copied[cur])
+        b = k % R
+        results[cur] = launch(b, outs7[cur], results[cur])
+        batch_of[cur] = b
         if gath is not None:
             pass_done[cur].record(ext)
         if k > 0:  # the previous step's result, while this one runs: settled, and delivered for N>1
             if gath is not None:
                 send(k - 1)
             else:
-                settle(results[cur ^ 1])
+                settle(results[cur ^ 1], batch_of[cur ^ 1])
 
     def drain(k_last):
         if results[k_last & 1] is not None:
             if gath is not None:
                 send(k_last)
             else:
-                settle(results[k_last & 1])
+                settle(results[k_last & 1], batch_of[k_last & 1])
 
-    # untimed reference pass: sizes for the gather and the expected result
-    # (the same entry point as the timed steps: the dense layout follows the
-    # scan's grid, which the fused step sizes for itself)
-    if args.fused_step:
-        ref = tdev.step_device(obs_d.data_ptr(), P_peaks, shifts, outs7[0].data_ptr(), a8m.data_ptr(), a8t.data_ptr(),
-                               n8, dp.tolerance, dp.precision, A)
-    else:
-        tdev.is_valid_peaks_device(obs_d.data_ptr(), P_peaks, shifts, dp.tolerance, dp.precision,
-                                   outs7[0].data_ptr())
-        ref = tdev.explain_device(a8m.data_ptr(), a8t.data_ptr(), n8, dp.tolerance, dp.precision, A)
-    ref.fetch_device()
-    n_hits0, payload0 = ref.settle()
-    ref_digest = result_digest(ref)
+    # untimed reference pass of every batch (the same entry point as the timed
+    # steps: the dense layout follows the scan's grid, which the fused step
+    # sizes for itself): sizes for the gather and each batch's expected result
+    refs = []
+    for b in range(R):
+        rr = launch(b, outs7[0], None)
+        rr.fetch_device()
+        engine.synchronize()
+        a7_ok = np.array_equal(outs7[0][:n7s[b]].cpu().numpy(), wls[b]["a7_valid"])
+        if not a7_ok:
+            raise RuntimeError(f"batch {b}: is_valid bytes differ from the setup pass")
+        expect[b] = rr.settle()
+        refs.append({"digest": result_digest(rr), "stats": rr.stats(), "status": rr.status.copy(),
+                     "canon": canonical_digest(rr.status, rr.count, rr.offset, rr.payload) if gath is not None
+                     else None, "n_hits": expect[b][0],
+                     "pair_hits": rr.pair_hits_device()[1] if args.fused_step else 0,
+                     "used": None, "wire_list": None})
+        if gath is not None:
+            # the wire size: the fixed part (host-known) + the reference pass's list
+            fixed = rr.wire_pack(outs7[0].data_ptr(), n7s[b])
+            probe = torch.empty(fixed + 8 * (n7s[b] + n8s[b] + expect[b][0]), dtype=torch.uint8, device=dev_t)
+            torch.cuda.synchronize()
+            rr.wire_pack(outs7[0].data_ptr(), n7s[b], probe.data_ptr(), probe.numel())
+            engine.synchronize()
+            hdr = probe[:128].cpu().numpy()
+            refs[b]["used"], refs[b]["wire_list"] = wire_used_bytes(hdr), int(hdr.view(np.uint64)[9])
+            del probe
+        if b == int(np.argmax(n8s)):
+            results[0] = rr  # the result sets get the capacity of the largest batch
+        else:
+            rr.close()
+    results[1] = launch(int(np.argmax(n8s)), outs7[1], None)
+    results[1].settle()
     if gath is not None:
         precs = tdev.pair_records()
-        # the wire size: the fixed part (host-known) + the reference pass's list
-        fixed = ref.wire_pack(outs7[0].data_ptr(), n7)
-        probe = torch.empty(fixed + 8 * (n7 + n8 + n_hits0), dtype=torch.uint8, device=dev_t)
-        torch.cuda.synchronize()
-        ref.wire_pack(outs7[0].data_ptr(), n7, probe.data_ptr(), probe.numel())
-        engine.synchronize()
-        hdr = probe[:128].cpu().numpy()
-        used, wire_list = wire_used_bytes(hdr), int(hdr.view(np.uint64)[9])
-        del probe
-        gath.agree(used)
+        gath.agree(max(rf["used"] for rf in refs))
         wbuf = [torch.empty(gath.max, dtype=torch.uint8, device=dev_t) for _ in range(2)]
         torch.cuda.synchronize()
-        ref_canon = canonical_digest(ref.status, ref.count, ref.offset, ref.payload)
     for k in range(args.warmup):
         step(k)
     drain(args.warmup - 1)
@@ -384,35 +416,41 @@ def main():
     elapsed = t1 - t0
     prof = engine.profile_read() if not args.no_events else {}
     engine.profile(False)
+    timed_batches = [k % R for k in range(args.steps)]
+    peaks_mine = sum(dev_in[b]["P"] for b in timed_batches) / args.steps  # peaks per step (mean over the cycle)
+    n7_mine = sum(n7s[b] for b in timed_batches) / args.steps
+    n8_mine = sum(n8s[b] for b in timed_batches) / args.steps
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev_t)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        pk = torch.tensor([wl["peaks"], n7, n8], dtype=torch.int64, device=dev_t)
+        pk = torch.tensor([peaks_mine, n7_mine, n8_mine], dtype=torch.float64, device=dev_t)
         dist.all_reduce(pk)
-        peaks_all, n7_all, n8_all = (int(x) for x in pk.tolist())
+        peaks_all, n7_all, n8_all = (float(x) for x in pk.tolist())
     else:
-        peaks_all, n7_all, n8_all = wl["peaks"], n7, n8
+        peaks_all, n7_all, n8_all = peaks_mine, n7_mine, n8_mine
 
     # every timed step was settled in the loop; the last two steps' results
-    # must equal the reference pass bit for bit (status bytes, hit list,
-    # payload), and A7 the setup pass
+    # must equal their batch's reference pass bit for bit (status bytes, hit
+    # list, payload), and A7 the setup pass
     if settled["n"] != args.steps and not args.no_validate:
         raise RuntimeError(f"{settled['n']} of {args.steps} steps settled")
     if gath is not None and settled["sent"] != args.steps:
         raise RuntimeError(f"{settled['sent']} of {args.steps} steps delivered to rank 0")
-    for r in results:
+    for r, b in zip(results, batch_of):
         if r is not None:
             r.fetch_device()
-            if result_digest(r) != ref_digest and not args.no_validate:
-                raise RuntimeError("a timed step's result differs from the reference pass")
-    res = results[(args.steps - 1) & 1]
-    st = res.status
+            if result_digest(r) != refs[b]["digest"] and not args.no_validate:
+                raise RuntimeError(f"a timed step's result (batch {b}) differs from the reference pass")
+    engine.synchronize()
+    for o, b in zip(outs7, batch_of):
+        assert np.array_equal(o[:n7s[b]].cpu().numpy(), wls[b]["a7_valid"]), \
+            "is_valid results changed between setup and timed runs"
     if gath is not None:
         # rank 0 decodes what it received from every rank in the last step:
         # each rank's result digest must match (and its A7 bytes)
-
-        mine = torch.tensor(np.frombuffer(bytes.fromhex(ref_canon), dtype=np.uint8).copy(), device=dev_t)
+        last_b = (args.steps - 1) % R
+        mine = torch.tensor(np.frombuffer(bytes.fromhex(refs[last_b]["canon"]), dtype=np.uint8).copy(), device=dev_t)
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         if rank == 0 and not args.no_validate:
@@ -421,11 +459,20 @@ def main():
                 cnt_, off_ = decode_hits(st_, hits_)
                 if bytes.fromhex(canonical_digest(st_, cnt_, off_, pay_)) != bytes(want.cpu().numpy()):
                     raise RuntimeError(f"rank {r_}'s gathered result does not decode to its own result")
-    if (st < -2).any() and not args.no_validate:
-        raise RuntimeError(f"internal statuses in results: {np.unique(st[st < -2])}")
-    stats = res.stats()
-    for o in outs7:
-        assert np.array_equal(o.cpu().numpy(), wl["a7_valid"]), "is_valid results changed between setup and timed runs"
+    if args.dump_gathered:
+        os.makedirs(args.dump_gathered, exist_ok=True)
+        last_b = (args.steps - 1) % R
+        w_ = wls[last_b]
+        np.savez(os.path.join(args.dump_gathered, f"inputs_rank{rank}.npz"), a7_mass=w_["a7_mass"],
+                 a7_thr=w_["a7_thr"], a8_mass=w_["a8_mass"], a8_thr=w_["a8_thr"], obs=w_["obs"],
+                 shifts=w_["shifts"], max_mods=np.int64(A))
+        if rank == 0 and gath is not None:
+            np.savez(os.path.join(args.dump_gathered, "gathered.npz"), precs=precs,
+                     **{f"rank{r_}": b_.cpu().numpy() for r_, b_ in enumerate(gath.last)})
+    for rf in refs:
+        st = rf["status"]
+        if (st < -2).any() and not args.no_validate:
+            raise RuntimeError(f"internal statuses in results: {np.unique(st[st < -2])}")
 
     if rank != 0:
         if dist:
@@ -433,45 +480,70 @@ def main():
         return
 
     limit = tdev.n_cols * tdev.compression
-    _, _, w7 = windows(wl["a7_mass"], wl["a7_thr"], dp.precision, limit)
-    _, hi8, w8 = windows(wl["a8_mass"], wl["a8_thr"], dp.precision, limit)
-    # queries the scan answers from the LDS pair list: non-empty windows below
-    # 3 * w_min (budgets never bind there for this config; checked against the
-    # engine's own counter)
     w_min = min(m.mass for m in dp.masses if m.mass > 0)
-    pair = (w8 > 0) & (hi8 < 3 * w_min)
-    n_pair, n_work, nodes = int(stats[6]), int(stats[0]), int(stats[4])
-    if int(pair.sum()) != n_pair and not args.no_validate:
-        raise RuntimeError(f"pair-path partition {int(pair.sum())} != engine counter {n_pair}")
-    some = (st == 2) | (st == -2)
-    # algorithmic HBM bytes per launch (DESIGN.md "Measurement"); the LDS pair
-    # list and the L2-resident bitset are on-chip after first touch but are
-    # counted at 8 B per word touched:
-    #   k_is_valid:       the peak's mass (8, once for its 4 windows) + result (1 per window) + the
-    #                     window's bitset words (8 each)
-    #   k_explain_scan:   mass+thr (16) + status (1) of every query it resolves;
-    #                     pair path: 8-B hit record + payload of each SOME / OVERFLOW;
-    #                     other windows: bitset words (8 each); 16 B worklist item per queued query
-    #   k_explain_expand: worklist item (16) + status/count/offset (17) + 16 B per
-    #                     index record expanded + payload (its bitset words are not counted)
-    #   k_result_pack:    8-B hit record in + 16-B dense record out per hit, the
-    #                     candidate payload read and written once (pad bytes not counted)
-    n_some_pair = int(((st == 2) & pair).sum())
-    cand_bytes = int(stats[7]) - 2 * n_some_pair + int(stats[5])
     # the device path's pair scan packs its own result (fused: no k_result_pack
     # launch): its algorithmic bytes are then the inputs, the status bytes and
     # the dense result (16-B hit record + candidate bytes per query with
-    # candidates); the wave-local records and payload it re-reads are not
+    # candidates, 2-B pair-list ref per pair hit); the wave-local records and
+    # payload it re-reads are not
     fused = _native.K_RESULT_PACK not in prof
-    bytes_k = {
-        "k_is_valid": float(8 * P_peaks + n7 + 8 * w7.sum()),
-        # (stats[7] counts the 2 pad bytes per SOME query of the dword record stores: not algorithmic)
-        "k_explain_scan": float(n8 * 16 + (n8 - n_work) + (16 * n_hits0 + cand_bytes if fused else
-                                                            8 * int((some & pair).sum()) + int(stats[7]) - 2 * n_some_pair)
-                                + 8 * int(w8[~pair].sum()) + 16 * n_work),
-        "k_result_pack": float(24 * n_hits0 + 2 * cand_bytes),
-        "k_explain_expand": float(n_work * (16 + 17) + 16 * nodes + int(stats[5])),
-    }
+
+    def batch_bytes(b):
+        """Algorithmic bytes per launch of each kernel for batch b (DESIGN.md
+        section 4), and the part of them that is L2-resident bitset words."""
+        w_, rf = wls[b], refs[b]
+        stats, st = rf["stats"], rf["status"]
+        _, _, w7 = windows(w_["a7_mass"], w_["a7_thr"], dp.precision, limit)
+        _, hi8, w8 = windows(w_["a8_mass"], w_["a8_thr"], dp.precision, limit)
+        # queries the scan answers from the LDS pair list: non-empty windows
+        # below 3 * w_min (budgets never bind there for this config; checked
+        # against the engine's own counter)
+        pair = (w8 > 0) & (hi8 < 3 * w_min)
+        n_pair, n_work, nodes = int(stats[6]), int(stats[0]), int(stats[4])
+        if int(pair.sum()) != n_pair and not args.no_validate:
+            raise RuntimeError(f"pair-path partition {int(pair.sum())} != engine counter {n_pair}")
+        some = (st == 2) | (st == -2)
+        n7, n8, P = n7s[b], n8s[b], dev_in[b]["P"]
+        # algorithmic HBM bytes per launch; the LDS pair list is on-chip and
+        # the 2.8 MB is_valid bitset L2-resident, both counted at 8 B per
+        # bitset word touched (bitset_l2 below: that part):
+        #   k_is_valid:       the peak's mass (8, once for its 4 windows) + result (1 per window) + the
+        #                     window's bitset words (8 each)
+        #   k_explain_scan:   mass+thr (16) + status (1) of every query it resolves;
+        #                     pair path: dense hit record + payload of each SOME / OVERFLOW;
+        #                     other windows: bitset words (8 each); 16 B worklist item per queued query
+        #   k_explain_expand: worklist item (16) + status/count/offset (17) + 16 B per
+        #                     index record expanded + payload (its bitset words are not counted)
+        #   k_result_pack:    8-B hit record in + 16-B dense record out per hit, the
+        #                     candidate payload read and written once (pad bytes not counted)
+        n_some_pair = int(((st == 2) & pair).sum())
+        cand_bytes = int(stats[7]) - 2 * n_some_pair + int(stats[5])
+        bits7, bits8 = 8 * int(w7.sum()), 8 * int(w8[~pair].sum())
+        bk = {
+            "k_is_valid": float(8 * P + n7 + bits7),
+            # (stats[7] counts the 2 pad bytes per SOME query of the dword record stores: not algorithmic)
+            "k_explain_scan": float(n8 * 16 + (n8 - n_work) +
+                                    (16 * rf["n_hits"] + cand_bytes + 2 * rf["pair_hits"] if fused else
+                                     8 * int((some & pair).sum()) + int(stats[7]) - 2 * n_some_pair)
+                                    + bits8 + 16 * n_work),
+            "k_result_pack": float(24 * rf["n_hits"] + 2 * cand_bytes),
+            "k_explain_expand": float(n_work * (16 + 17) + 16 * nodes + int(stats[5])),
+        }
+        l2 = {"k_is_valid": float(bits7), "k_explain_scan": float(bits8)}
+        if args.fused_step:  # the scan's launch also ran A7 (k_step): its bytes are both predicates'
+            bk["k_explain_scan"] += bk["k_is_valid"]
+            l2["k_explain_scan"] += l2["k_is_valid"]
+        # SURVEY 8(d)'s literal per-query model: 16 B in + 8 B per window word
+        # for every A7 and A8 query, 16 B out and the payload per A8 query, and
+        # 8 B per table cell the reference DFS looks up (S, from the oracle on
+        # the CPU sample: cpu_baseline)
+        lit = float(16 * n7 + 8 * int(w7.sum()) + 32 * n8 + 8 * int(w8.sum()) + cand_bytes)
+        return bk, l2, lit, n8
+
+    per = [batch_bytes(b) for b in range(R)]
+    bytes_k = {k: sum(per[b][0][k] for b in timed_batches) / args.steps for k in per[0][0]}
+    l2_k = {k: sum(per[b][1][k] for b in timed_batches) / args.steps for k in per[0][1]}
+    lit_bytes = sum(per[b][2] for b in timed_batches) / args.steps
     kern = {}
     for kid, (ms, cnt) in prof.items():
         name = _native.KERNEL_NAMES[kid]
@@ -479,27 +551,36 @@ def main():
         if name in bytes_k:
             kern[name]["algorithmic_bytes"] = bytes_k[name]
             kern[name]["achieved_GBps"] = bytes_k[name] / (1e3 * ms / cnt * 1e-6) / 1e9
-    if args.fused_step:  # the scan's launch also ran A7 (k_step): its bytes are both predicates'
-        bytes_k["k_explain_scan"] += bytes_k["k_is_valid"]
-        if "k_explain_scan" in kern:
-            kern["k_explain_scan"]["algorithmic_bytes"] = bytes_k["k_explain_scan"]
-            kern["k_explain_scan"]["achieved_GBps"] = bytes_k["k_explain_scan"] / (kern["k_explain_scan"]["avg_us"] * 1e-6) / 1e9
     dom = max(bytes_k, key=lambda k: kern.get(k, {"avg_us": 0.0})["avg_us"])
     dbytes, dus = bytes_k[dom], kern.get(dom, {"avg_us": float("nan")})["avg_us"]
     achieved = dbytes / (dus * 1e-6) / 1e9
-    traffic = None
+    hbm_only = (dbytes - l2_k.get(dom, 0.0)) / (dus * 1e-6) / 1e9
+    traffic, traffic_src = None, None
+    tkey = ("k_step" if args.fused_step and dom == "k_explain_scan" else dom) + (f"_rot{R}" if R > 1 else "")
     if args.spectra == 10000 and args.seed == 1000:  # the workload the PMC passes in profiles/ measured
         try:
             with open(args.traffic_json) as f:
-                traffic = json.load(f).get("k_step" if args.fused_step and dom == "k_explain_scan" else dom)
+                tj = json.load(f)
+            traffic = tj.get(tkey)
+            traffic_src = tj.get("_source", {}).get(tkey)
         except (OSError, ValueError):
             pass
+    st = refs[timed_batches[-1]]["status"]
+    stats = refs[timed_batches[-1]]["stats"]
+    res = results[(args.steps - 1) & 1]
+    some = (st == 2) | (st == -2)
+    n_hits0 = refs[timed_batches[-1]]["n_hits"]
+    wire_list = refs[timed_batches[-1]]["wire_list"]
     ms_step = 1e3 * elapsed / args.steps
     value = peaks_all / (elapsed / args.steps)
 
     cpu = None
+    lit_frac = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(lambda n: build_workload(n, args.seed, dp), dp)
+        if dom == "k_explain_scan":
+            lit_bytes += 8.0 * cpu["survey_lookups_per_a8_query"] * sum(n8s[b] for b in timed_batches) / args.steps
+            lit_frac = lit_bytes / (dus * 1e-6) / 1e9 / HBM_PEAK_GBPS
 
     line = {
         "metric": METRIC,
@@ -518,6 +599,9 @@ def main():
             "workload": "config3: synthetic spectra (SURVEY 8(d)), full 104-mass/105-row alphabet, <=20-mer, "
                         "A7 (4 breakages/peak) + A8 (sliding-window differences) per step",
             "spectra_per_gpu": args.spectra,
+            "batches": (f"{R} distinct batches of {args.spectra} spectra (seeds {args.seed} + 7919 b), cycled "
+                        f"step by step, {sum(w['obs'].nbytes + w['a8_mass'].nbytes + w['a8_thr'].nbytes for w in wls) / 1e6:.0f} MB "
+                        f"of inputs: no step's inputs are still in the 256 MB Infinity Cache" if R > 1 else "1 batch"),
             "peaks": peaks_all,
             "a7_queries": n7_all,
             "a8_queries": n8_all,
@@ -526,7 +610,7 @@ def main():
             "a7_stream": ("side stream, concurrent with the A8 chain" if args.a7_stream else "engine stream"),
             "parallelism": ((f"spectra sharded over {world} GPUs; every step's complete result of every rank "
                              f"gathered to rank 0 ({'RCCL' if args.backend == 'nccl' else 'gloo'}, wire format "
-                             f"v4, sst_wire_pack), overlapped with the next step"
+                             f"v5, sst_wire_pack), overlapped with the next step"
                              if gath is not None else f"spectra sharded over {world} GPUs, results kept per rank")
                             if world > 1 else "1 GPU"),
             "wire_bytes_per_rank_step": (gath.sizes if gath is not None else None),
@@ -541,12 +625,23 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": dbytes,
+            # the same minus the bitset words (8 B per word touched), which
+            # the 2.8 MB L2-resident bitset serves: bytes that cross HBM
+            "frac_hbm_resident": hbm_only / HBM_PEAK_GBPS,
+            "hbm_resident_bytes_per_launch": dbytes - l2_k.get(dom, 0.0),
+            # SURVEY 8(d)'s literal model (16 B in + 8 B per window word per
+            # query, + 8 B per table cell the reference DFS reads, S from the
+            # oracle on the CPU sample); > 1 is possible: the LDS pair list
+            # answers windows without the table reads the model charges
+            "frac_survey_literal": lit_frac,
+            "survey_literal_bytes_per_launch": lit_bytes if lit_frac is not None else None,
             "avg_launch_us": dus,
             "event_timed_launches": kern.get(dom, {}).get("launches", 0),  # every --event-every-th step
         },
         "kernels": kern,
-        "engine_stats": {"pair": n_pair, "shallow": int(stats[0]), "deep": int(stats[1]), "exact": int(stats[2]),
+        "engine_stats": {"pair": int(stats[6]), "shallow": int(stats[0]), "deep": int(stats[1]), "exact": int(stats[2]),
                          "nomemo": int(stats[3]), "index_loads": int(stats[4]),
                          "candidates": int(res.count[some].sum()), "payload_bytes": int(stats[5] + stats[7]),
                          "hits": n_hits0, "dense_payload_bytes": int(len(res.payload))},

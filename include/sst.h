@@ -203,6 +203,13 @@ int sst_result_settle(sst_result* r, uint64_t* n_hits, uint64_t* payload_bytes);
  *   or SST_ABORTED (the host builds them from the hit list). */
 int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count, const uint64_t** offset,
                     const uint8_t** payload, uint64_t* payload_bytes);
+/* Ordering of a result's device buffers: they are written on the stream that
+ * was the ctx's stream when the pass was queued (the pass stream); settling
+ * queues any further launches (deferred classes, pack, retries) on that same
+ * stream, whatever the ctx's stream is at the time.  sst_wire_pack, the views
+ * and fetch wait (hipStreamWaitEvent) for the work settling queued when they
+ * run on another stream; the pass's own kernels are the caller's to order
+ * (e.g. an event recorded on the pass stream right after the launch). */
 /* Device views (no copy; settle the result first).  d_status and d_payload
  * (the dense payload) are the pass's own output.  d_count / d_offset are
  * per-query u64 arrays built from the hit list only when asked for (pass
@@ -239,17 +246,17 @@ int sst_result_pair_hits(sst_result* r, void** d_refs, uint64_t* n_pair_hits, ui
  * candidate); *n = 0 for tables without the list.  recs may be NULL (size
  * query). */
 int sst_table_pair_records(sst_table* t, uint32_t* recs, int64_t cap, int64_t* n);
-/* One rank's complete step result in the gather's wire format v4, packed on
+/* One rank's complete step result in the gather's wire format v5, packed on
  * the device by one kernel on the ctx stream (settles r first): d_valid the
  * step's n_valid is_valid codes (int8 -1 / 0 / 1), r its explain result.
  * The layout (8-B aligned sections; spectrseqtools_amd/parallel.py,
  * wire_unpack, decodes it):
- *   header   16 x u64: magic "SSTW4", n_valid, n_explain, n_pair, n_explicit,
+ *   header   16 x u64: magic "SSTW5", n_valid, n_explain, n_pair, n_explicit,
  *            explicit payload bytes, n_scan_wg, pair key (FNV-1a of the pair
  *            records), w, n_list, list capacity, list offset, 4 x 0
  *   valid    1 bit per is_valid query: True
- *   status   2 bits per explain query: 0 NONE, 1 EMPTY, 2 SOME / OVERFLOW /
- *            ABORTED, 3 listed
+ *   status   1 bit per explain query: 1 = SOME / OVERFLOW / ABORTED (a hit),
+ *            0 = NONE or listed
  *   first    per pair hit (sst_result_pair_hits, scan order) its first
  *            pair-list entry in w bits, w = ceil(log2(pair-list entries))
  *   codes    per pair hit 3 bits, 10 per u32: its count 1..7, 0 = listed
@@ -259,7 +266,8 @@ int sst_table_pair_records(sst_table* t, uint32_t* recs, int64_t cap, int64_t* n
  *   payload  the explicit hits' payload
  *   list     n_list 8-B entries {u32 index | type << 30, u32 value}, in no
  *            particular order: type 0 an is_valid raise, 1 an explain status
- *            other than NONE / EMPTY / SOME (value: the status byte), 2 a pair hit's
+ *            other than NONE / SOME (value: the status byte; EMPTY, raises,
+ *            OVERFLOW, ABORTED), 2 a pair hit's
  *            count outside 1..7 (index: the pair hit, value: the count)
  * d_out NULL: returns the fixed part's bytes (the list's offset) and packs
  * nothing; otherwise cap (>= that) bounds the buffer and entries beyond it
@@ -294,6 +302,48 @@ int sst_length_bound_batch(sst_table* t, const double* su_mass, const double* ob
                            double precision, int max_len, int64_t max_mods, int direction, int64_t* out,
                            int8_t* status);
 
+/* ---- per-spectrum reduced alphabets ---------------------------------- */
+/* Predictor.filter_by_explanation (prediction.py:170-227) reduces every
+ * spectrum's alphabet to the modifications its explanations name
+ * (adapt_individual_modification_rates_by_alphabet_reduction,
+ * mass_table.py:94-121) and then queries the table rebuilt for that alphabet
+ * (set_up_bit_table over the kept rows, max_mass = max(kept) * 35).  Over many
+ * spectra these entry points answer those rebuilt tables' queries without
+ * building them: spectrum g's alphabet is a row subset of t, the bits of
+ * masks[2g] (rows 0..63) and masks[2g + 1] (rows 64..119); row 0 is implied;
+ * the canonical rows are never dropped by the reference, so every alphabet
+ * holds t's lightest row. */
+
+/* explain_mass_with_table (mass_explanation.py:92-203) on pair-class windows
+ * (hi < 3 * the lightest row mass: every candidate has <= 2 items) of query i
+ * against the table of spectrum spec[i]'s alphabet: the candidates are t's
+ * pair-list entries whose rows lie in the alphabet, in the reference's order.
+ * The caller guarantees the budgets cannot bind (as for any pair-class window
+ * with max_modifications >= 2 and per-row caps >= 2).  Out per query: status
+ * (SST_NONE / SST_EMPTY / SST_SOME; -10 for a window that is not pair-class,
+ * which the caller answers otherwise), the candidate count, the union of the
+ * candidates' rows (rowmask[2i], rowmask[2i + 1]) and the window's pair-list
+ * entry range range[2i] .. range[2i + 1] (its candidates are the entries of
+ * that range whose rows are all in the alphabet; sst_table_pair_records).
+ * t must carry the pair list.  No reference equivalent (batched). */
+int sst_explain_pairs_alpha_device(sst_table* t, const double* d_mass, const double* d_thr, const int32_t* d_spec,
+                                   const uint64_t* d_masks, int64_t n, double tolerance, double precision,
+                                   int8_t* d_status, uint32_t* d_count, uint64_t* d_rowmask, uint32_t* d_range);
+int sst_explain_pairs_alpha(sst_table* t, const double* mass, const double* thr, const int32_t* spec,
+                            const uint64_t* masks, int64_t n_spec, int64_t n, double tolerance, double precision,
+                            int8_t* status, uint32_t* count, uint64_t* rowmask, uint32_t* range);
+/* is_valid_mass (mass_explanation.py:45-89) against the table of each
+ * spectrum's alphabet (its last row: reachability by the alphabet's rows,
+ * the reduced table's extent and last-column mask included): spectrum g's
+ * queries are mass/thr[offsets[g] .. offsets[g+1]), in ascending mass order
+ * (classify_fragments' SU order).  out as sst_is_valid_batch; -10 marks a
+ * query the kernel could not answer (queries out of mass order). */
+int sst_is_valid_alpha_device(sst_table* t, const double* d_mass, const double* d_thr, const int64_t* d_offsets,
+                              int64_t n_spec, const uint64_t* d_masks, double tolerance, double precision,
+                              int8_t* d_out);
+int sst_is_valid_alpha(sst_table* t, const double* mass, const double* thr, const int64_t* offsets, int64_t n_spec,
+                       const uint64_t* masks, double tolerance, double precision, int8_t* out);
+
 /* ---- query producers (host code, no device) --------------------------- */
 /* The sliding window of collect_explanations_per_side
  * (spectrseqtools/prediction.py:286-329) over many sides at once: side j is
@@ -318,6 +368,18 @@ int64_t sst_window_pairs(const double* su, const int64_t* offsets, int64_t n_sid
 int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* flags, const int64_t* offsets,
                             int64_t n_spec, double max_weight, double tolerance, double* diff, double* thr,
                             int64_t* spec, int8_t* kind, int64_t cap);
+/* The explanation dict collect_diff_explanations_for_su builds per spectrum
+ * (prediction.py:261-284): spectrum g's queries [offsets[g], offsets[g+1])
+ * in its order (START pairs, END pairs, singletons) with kind 0 / 1 / 2, their
+ * dict key (the difference, or the singleton's SU mass), explain status and
+ * candidate row union (2 x u64).  Side pairs are stored only with >= 1
+ * explanation, singletons always; a later store of an equal key replaces the
+ * earlier one.  keep[i] = 1 for the queries whose answers the finished dict
+ * holds; union_out[2g..2g+1] = the rows of those answers (the observed
+ * nucleotides of filter_by_explanation, :189-195).  Returns the number of
+ * dict entries over all spectra, or SST_E*.  Host code, up to 16 threads. */
+int64_t sst_dict_union(const int64_t* offsets, int64_t n_spec, const double* key, const int8_t* kind,
+                       const int8_t* status, const uint64_t* rowmask, uint8_t* keep, uint64_t* union_out);
 /* order[0..n): the row permutation that sorts by group (0 <= group < n_groups)
  * then key ascending, ties in row order -- classify_fragments' per-spectrum
  * sort by standard_unit_mass (fragment_classification.py:84), for many

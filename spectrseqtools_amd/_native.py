@@ -29,7 +29,8 @@ EXPORTS = (
     "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
     "sst_window_pairs", "sst_is_valid_peaks", "sst_is_valid_peaks_device", "sst_result_pair_hits",
     "sst_table_pair_records", "sst_su_diff_queries", "sst_sort_rows", "sst_step_device",
-    "sst_wire_pack",
+    "sst_wire_pack", "sst_explain_pairs_alpha", "sst_explain_pairs_alpha_device", "sst_is_valid_alpha",
+    "sst_is_valid_alpha_device", "sst_dict_union",
 )
 
 # kernel ids of sst_profile_read
@@ -134,6 +135,16 @@ def load_library(path=LIB_PATH):
     lib.sst_sort_rows.restype = _I
     lib.sst_step_device.argtypes = [_P, _P, _I64, _P, _I, _P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
     lib.sst_step_device.restype = _I
+    lib.sst_explain_pairs_alpha.argtypes = [_P, _P, _P, _P, _P, _I64, _I64, _D, _D, _P, _P, _P, _P]
+    lib.sst_explain_pairs_alpha.restype = _I
+    lib.sst_explain_pairs_alpha_device.argtypes = [_P, _P, _P, _P, _P, _I64, _D, _D, _P, _P, _P, _P]
+    lib.sst_explain_pairs_alpha_device.restype = _I
+    lib.sst_is_valid_alpha.argtypes = [_P, _P, _P, _P, _I64, _P, _D, _D, _P]
+    lib.sst_is_valid_alpha.restype = _I
+    lib.sst_is_valid_alpha_device.argtypes = [_P, _P, _P, _P, _I64, _P, _D, _D, _P]
+    lib.sst_is_valid_alpha_device.restype = _I
+    lib.sst_dict_union.argtypes = [_P, _I64, _P, _P, _P, _P, _P, _P]
+    lib.sst_dict_union.restype = _I64
     return lib
 
 
@@ -172,6 +183,25 @@ def su_diff_queries(su, obs, flags, offsets, max_weight, tolerance):
         if n <= cap:
             return d[:n], t[:n], g[:n], k[:n]
         cap = int(n)
+
+
+def dict_union(offsets, key, kind, status, rowmask):
+    """sst_dict_union: per spectrum the surviving entries of
+    collect_diff_explanations_for_su's dict (keep[i]) and the union of their
+    candidate rows ([n_spec, 2] u64 masks).  Host code."""
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    key = np.ascontiguousarray(key, dtype=np.float64)
+    kind = np.ascontiguousarray(kind, dtype=np.int8)
+    status = np.ascontiguousarray(status, dtype=np.int8)
+    rowmask = np.ascontiguousarray(rowmask, dtype=np.uint64).reshape(-1, 2)
+    n_spec = len(offsets) - 1
+    keep = np.zeros(len(key), np.uint8)
+    union = np.zeros((max(n_spec, 0), 2), np.uint64)
+    rc = lib().sst_dict_union(_ptr(offsets), n_spec, _ptr(key), _ptr(kind), _ptr(status), _ptr(rowmask), _ptr(keep),
+                              _ptr(union))
+    if rc < 0:
+        raise EngineError(f"sst_dict_union failed ({rc})")
+    return keep.astype(bool), union
 
 
 def sort_rows(group, key, n_groups):
@@ -520,6 +550,39 @@ class DeviceTable:
         self.engine.check(self.engine._lib.sst_is_valid_peaks(self.handle, _ptr(o), len(o), _ptr(sh), len(sh),
                                                               float(tolerance), float(precision), _ptr(out)),
                           "sst_is_valid_peaks")
+        return out
+
+    def explain_pairs_alpha(self, masses, thresholds, spec, masks, tolerance, precision):
+        """sst_explain_pairs_alpha: pair-class windows against per-spectrum
+        reduced alphabets (masks [n_spec, 2] u64 row bits of this table).
+        -> (status i8, count u32, rowmask [n, 2] u64, range [n, 2] u32)."""
+        m = np.ascontiguousarray(masses, dtype=np.float64)
+        t = None if thresholds is None else np.ascontiguousarray(thresholds, dtype=np.float64)
+        sp = np.ascontiguousarray(spec, dtype=np.int32)
+        mk = np.ascontiguousarray(masks, dtype=np.uint64).reshape(-1, 2)
+        n = len(m)
+        st, cnt = np.zeros(n, np.int8), np.zeros(n, np.uint32)
+        rm, rg = np.zeros((n, 2), np.uint64), np.zeros((n, 2), np.uint32)
+        self.engine.check(self.engine._lib.sst_explain_pairs_alpha(self.handle, _ptr(m), _ptr(t), _ptr(sp), _ptr(mk),
+                                                                   len(mk), n, float(tolerance), float(precision),
+                                                                   _ptr(st), _ptr(cnt), _ptr(rm), _ptr(rg)),
+                          "sst_explain_pairs_alpha")
+        return st, cnt, rm, rg
+
+    def is_valid_alpha(self, masses, thresholds, offsets, masks, tolerance, precision):
+        """sst_is_valid_alpha: is_valid_mass against per-spectrum reduced
+        alphabets; spectrum g's queries are [offsets[g], offsets[g+1]) in
+        ascending mass order.  -> int8 (1 / 0 / -1 raise)."""
+        m = np.ascontiguousarray(masses, dtype=np.float64)
+        t = None if thresholds is None else np.ascontiguousarray(thresholds, dtype=np.float64)
+        off = np.ascontiguousarray(offsets, dtype=np.int64)
+        mk = np.ascontiguousarray(masks, dtype=np.uint64).reshape(-1, 2)
+        out = np.zeros(len(m), np.int8)
+        self.engine.check(self.engine._lib.sst_is_valid_alpha(self.handle, _ptr(m), _ptr(t), _ptr(off), len(off) - 1,
+                                                              _ptr(mk), float(tolerance), float(precision), _ptr(out)),
+                          "sst_is_valid_alpha")
+        if (out == -10).any():
+            raise EngineError("sst_is_valid_alpha: queries out of mass order within a spectrum")
         return out
 
     def is_valid_peaks_device(self, d_obs, n_peaks, shifts, tolerance, precision, d_out):

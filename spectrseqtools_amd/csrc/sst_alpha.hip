@@ -1,0 +1,270 @@
+// sst_alpha.hip -- queries on per-spectrum reduced alphabets (gfx950).
+//
+// Predictor.filter_by_explanation (prediction.py:170-227) reduces each
+// spectrum's alphabet to the modifications its explanations name
+// (adapt_individual_modification_rates_by_alphabet_reduction,
+// mass_table.py:94-121) and rebuilds the DP table for it; over a batch of
+// spectra nearly every spectrum ends with its own alphabet, so a table per
+// spectrum is not an option.  Two kernels answer the reduced tables' queries
+// without building them:
+//
+//   k_pairs_alpha   explain_mass_with_table on pair-class windows (every
+//                   candidate has <= 2 items: hi < 3 w_min): the candidates on
+//                   the reduced table are exactly the full table's pair-list
+//                   entries whose rows all lie in the spectrum's alphabet (the
+//                   reduced table is the closure of those rows; budgets that
+//                   cannot bind are the caller's check), in the same order.
+//                   One lane per query; the 40 KB pair list is read through L2.
+//   k_valid_alpha   is_valid_mass on the reduced table: reachability by the
+//                   spectrum's rows (an unbounded knapsack: the reduced table's
+//                   last row), computed as a bitset closure in LDS, one
+//                   workgroup per spectrum.  Every row mass is >= w_min (C, a
+//                   canonical row, is never dropped), so bit m depends only on
+//                   bits m - w_r <= m - w_min: chunks of 2^18 masses (< w_min)
+//                   are filled in order, each word an OR of shifted words of
+//                   the three chunks before it (w_max < 3 * 2^18), in a ring of
+//                   four 32 KB chunks.  The spectrum's windows (in mass order)
+//                   are answered as soon as the chunk holding them is done; a
+//                   run of >= w_max reachable masses ends the closure (every
+//                   later mass is reachable).  The reduced table's extent and
+//                   its last-column mask (mass_table.py:212, :246) bound the
+//                   reachable masses exactly as in set_up_bit_table.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sst_internal.h"
+#include "sst_quant.h"
+
+namespace sst {
+
+namespace {
+
+constexpr int kChunkWords = 4096;              // 64-bit words per chunk
+constexpr int64_t kChunkBits = kChunkWords * 64;  // 262144 masses
+constexpr int kRing = 4;                        // chunks kept in LDS (128 KB)
+constexpr int kValidWG = 1024;
+
+__device__ __forceinline__ bool row_in(uint64_t m0, uint64_t m1, int r) {
+  return r < 64 ? ((m0 >> r) & 1ull) : ((m1 >> (r - 64)) & 1ull);
+}
+
+// 64 closure bits starting at mass x (x may be negative: zeros) from the ring
+__device__ __forceinline__ uint64_t ring_bits(const uint64_t* ring, int64_t x) {
+  if (x < -63) return 0ull;
+  const int64_t wi = x >> 6;  // floor
+  const int s = (int)(x & 63);
+  const uint64_t lo = wi < 0 ? 0ull : ring[((wi >> 12) & (kRing - 1)) * kChunkWords + (wi & (kChunkWords - 1))];
+  if (s == 0) return lo;
+  const int64_t wj = wi + 1;
+  const uint64_t hi = wj < 0 ? 0ull : ring[((wj >> 12) & (kRing - 1)) * kChunkWords + (wj & (kChunkWords - 1))];
+  return (lo >> s) | (hi << (64 - s));
+}
+
+// any closure bit in [a, b] (both inside the ring's chunks)
+__device__ __forceinline__ bool ring_any(const uint64_t* ring, int64_t a, int64_t b) {
+  for (int64_t x = a; x <= b; x += 64) {
+    uint64_t v = ring_bits(ring, x);
+    const int64_t left = b - x + 1;
+    if (left < 64) v &= (1ull << left) - 1ull;
+    if (v) return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
+  __shared__ uint64_t ring[kRing * kChunkWords];
+  __shared__ int s_w[kMaxRows];
+  __shared__ int s_n;
+  __shared__ int64_t s_done;   // queries [q0, s_done) answered
+  __shared__ int s_full;       // a run of >= w_max reachable masses seen
+  __shared__ int s_chunk_full[kRing];
+  const int64_t g = blockIdx.x;
+  const int64_t q0 = a.offsets[g], q1 = a.offsets[g + 1];
+  if (q0 >= q1) return;
+  const uint64_t m0 = a.masks[2 * g], m1 = a.masks[2 * g + 1];
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int r = 1; r < a.n_rows; ++r)
+      if (row_in(m0, m1, r)) s_w[n++] = a.w[r];
+    s_n = n;
+    s_done = q0;
+    s_full = 0;
+  }
+  __syncthreads();
+  const int n_w = s_n;
+  if (n_w == 0) {  // sentinel only: nothing >= 1 is reachable
+    for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) a.out[i] = 0;
+    return;
+  }
+  int wmax = 0, wmin = INT32_MAX;
+  for (int k = 0; k < n_w; ++k) {
+    wmax = s_w[k] > wmax ? s_w[k] : wmax;
+    wmin = s_w[k] < wmin ? s_w[k] : wmin;
+  }
+  // the reduced table (set_up_bit_table with max_mass = max(kept) * 35):
+  // masses < limit exist, the last-column mask leaves masses <= vtop reachable
+  const int64_t max_mass = (int64_t)wmax * 35;
+  const int64_t n_cols = (max_mass + 1 + 31) / 32;
+  const int64_t limit = n_cols * 32;
+  const int64_t vtop = ((max_mass + 1) % 32 == 0) ? (n_cols - 1) * 32 - 1 : max_mass;
+  // the highest window value any query of this spectrum looks at
+  int64_t top = 0;
+  for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) {
+    int64_t lo, hi;
+    quantise(a.mass[i], a.thr ? a.thr[i] : 0.0, a.thr == nullptr, a.tol, a.prec, a.rprec, lo, hi);
+    top = hi > top ? hi : top;
+  }
+  __shared__ int64_t s_top;
+  if (threadIdx.x == 0) s_top = 0;
+  __syncthreads();
+  atomicMax((unsigned long long*)&s_top, (unsigned long long)(top < 0 ? 0 : top));
+  __syncthreads();
+  top = s_top < limit - 1 ? s_top : limit - 1;
+  const int64_t n_chunks = top / kChunkBits + 1;
+  const bool guard_ok = wmin >= kChunkBits && wmax < 3 * kChunkBits;  // the ring's dependency window
+  for (int64_t j = 0; j < n_chunks && guard_ok; ++j) {
+    uint64_t* cur = ring + (j & (kRing - 1)) * kChunkWords;
+    const int64_t base = j * kChunkBits;
+    bool all_ones = true;
+    for (int k = threadIdx.x; k < kChunkWords; k += blockDim.x) {
+      uint64_t v = 0;
+      if (!s_full) {
+        if (j == 0 && k == 0) v = 1ull;  // mass 0: the empty multiset (table[0, 0] seed)
+        for (int r = 0; r < n_w; ++r) v |= ring_bits(ring, base + 64 * (int64_t)k - s_w[r]);
+      } else {
+        v = ~0ull;
+      }
+      cur[k] = v;
+      all_ones &= (v == ~0ull);
+    }
+    const bool chunk_full = __syncthreads_and(all_ones);
+    if (threadIdx.x == 0) {
+      s_chunk_full[j & (kRing - 1)] = chunk_full;
+      // the last three chunks all set: a run of 3 * 2^18 > w_max masses, so
+      // every later mass is reachable
+      if (j >= 2 && chunk_full && s_chunk_full[(j - 1) & (kRing - 1)] && s_chunk_full[(j - 2) & (kRing - 1)])
+        s_full = 1;
+    }
+    __syncthreads();
+    // answer the queries whose windows lie below the end of this chunk (the
+    // rows come sorted by mass, windows are narrow: a query whose hi is in a
+    // later chunk stops the sweep and is answered there)
+    const int64_t end = base + kChunkBits;
+    const bool last = j == n_chunks - 1;
+    for (int64_t i0 = s_done; i0 < q1; i0 += blockDim.x) {
+      const int64_t i = i0 + threadIdx.x;
+      bool ready = false;
+      int8_t res = 0;
+      if (i < q1) {
+        int64_t lo, hi;
+        quantise(a.mass[i], a.thr ? a.thr[i] : 0.0, a.thr == nullptr, a.tol, a.prec, a.rprec, lo, hi);
+        ready = last || hi < end;
+        if (ready) {
+          // is_valid_mass (mass_explanation.py:63-88): skip v <= 0, raise at
+          // the first v >= limit, True at the first reachable v
+          const int64_t x0 = lo < 1 ? 1 : lo;
+          const int64_t x1 = hi < vtop ? hi : vtop;
+          bool any = false;
+          if (x0 <= x1 && x0 < base - 3 * kChunkBits) {
+            res = (int8_t)kStatusPending;  // below the ring (rows not in mass order): reported, not guessed
+          } else {
+            if (x0 <= x1) any = ring_any(ring, x0, x1);
+            res = any ? (int8_t)1 : (hi >= limit && hi >= lo && hi >= 1) ? (int8_t)-1 : (int8_t)0;
+          }
+          a.out[i] = res;
+        }
+      }
+      // the sweep advances over the leading run of answered queries
+      const uint64_t not_ready = __ballot(i < q1 && !ready);
+      __shared__ int s_stop[kValidWG / 64];
+      if ((threadIdx.x & 63) == 0) s_stop[threadIdx.x >> 6] = not_ready ? __builtin_ctzll(not_ready) : 64;
+      __syncthreads();
+      int stop = -1;
+      for (int wv = 0; wv < (int)(blockDim.x >> 6); ++wv)
+        if (s_stop[wv] < 64) {
+          stop = wv * 64 + s_stop[wv];
+          break;
+        }
+      __syncthreads();
+      if (stop >= 0) {
+        if (threadIdx.x == 0) s_done = i0 + stop;
+        __syncthreads();
+        break;
+      }
+      if (threadIdx.x == 0) s_done = i0 + (int64_t)blockDim.x < q1 ? i0 + blockDim.x : q1;
+      __syncthreads();
+    }
+    __syncthreads();
+    if (s_done >= q1) break;
+  }
+  if (!guard_ok)  // alphabets the ring cannot hold (not produced by the reduction): reported, not guessed
+    for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) a.out[i] = (int8_t)kStatusPending;
+}
+
+// Pair-class windows on a per-spectrum alphabet (see the file comment).  Out:
+// status, the number of candidates, the union of their rows and the window's
+// pair-list range [first, end) (the candidates are the entries of that range
+// whose rows are all in the alphabet).  Windows that are not pair-class
+// (hi >= pair_hi) get kStatusPending: the caller answers them otherwise.
+__global__ __launch_bounds__(256) void k_pairs_alpha(TableArgs t, PairAlphaArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  int64_t lo, hi;
+  quantise(a.mass[i], a.thr ? a.thr[i] : 0.0, a.thr == nullptr, a.tol, a.prec, a.rprec, lo, hi);
+  const int32_t g = a.spec[i];
+  const uint64_t m0 = a.masks[2 * (int64_t)g], m1 = a.masks[2 * (int64_t)g + 1];
+  int8_t status = SST_NONE;
+  uint32_t cnt = 0, first = 0, end = 0;
+  uint64_t u0 = 0, u1 = 0;
+  if (hi >= t.pair_hi) {
+    status = (int8_t)kStatusPending;
+  } else if (lo <= hi && hi >= 0) {
+    const bool zero = lo <= 0;  // v == 0: the empty solution [[]]
+    const int64_t x0 = lo < 1 ? 1 : lo;
+    if (x0 <= hi) {
+      const uint32_t* sums = t.pair_data;
+      const uint32_t* recs = sums + (t.n_pairs + 2);
+      const uint32_t* bk = recs + (t.n_pairs + 2);
+      const uint32_t av = (uint32_t)x0, hv = (uint32_t)hi;
+      const uint32_t rel = av > t.pair_base ? av - t.pair_base : 0u;
+      uint32_t k = bk[rel >> t.pair_shift] & 0xFFFFu;
+      const uint32_t a2 = av << 1, h2 = (hv << 1) | 1u;
+      while (sums[k] < a2) ++k;
+      first = k;
+      for (; sums[k] <= h2; ++k) {
+        const uint32_t rec = recs[k];
+        const int top = (int)((rec >> ((rec & 0xFFu) == 1u ? 8 : 16)) & 0xFFu);
+        const int low = (int)((rec >> 8) & 0xFFu);
+        if (row_in(m0, m1, top) && row_in(m0, m1, low)) {
+          ++cnt;
+          if (top < 64) u0 |= 1ull << top; else u1 |= 1ull << (top - 64);
+          if (low < 64) u0 |= 1ull << low; else u1 |= 1ull << (low - 64);
+        }
+      }
+      end = k;
+    }
+    status = cnt ? (int8_t)SST_SOME : zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;
+  }
+  a.status[i] = status;
+  a.count[i] = cnt;
+  a.rowmask[2 * i] = u0;
+  a.rowmask[2 * i + 1] = u1;
+  a.range[2 * i] = first;
+  a.range[2 * i + 1] = end;
+}
+
+hipError_t launch_valid_alpha(const AlphaArgs& a, int64_t n_spec, hipStream_t st) {
+  if (n_spec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_valid_alpha, dim3((uint32_t)n_spec), dim3(kValidWG), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pairs_alpha(const TableArgs& t, const PairAlphaArgs& a, hipStream_t st) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pairs_alpha, dim3((uint32_t)((a.n + 255) / 256)), dim3(256), 0, st, t, a);
+  return hipGetLastError();
+}
+
+}  // namespace sst

@@ -9,6 +9,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -145,6 +146,13 @@ struct sst_result {
   // scan_bytes of the dense payload (0 / 0 after an unfused pass)
   bool scan_hdr_pending = false;
   uint64_t scan_hits = 0, scan_bytes = 0;
+  // the stream the pass was queued on; settle() queues its own launches
+  // there and, when it launched any, records settle_ev after them: later
+  // users of the result on another stream (sst_wire_pack on a pack stream,
+  // fetch) wait for it
+  hipStream_t pass_stream = nullptr;
+  hipEvent_t settle_ev = nullptr;
+  bool settle_ev_pending = false;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
   std::vector<uint8_t> h_payload;
@@ -745,6 +753,8 @@ void free_result_bufs(sst_result* r) {
     b->release();
   if (r->hdr_host) (void)hipHostFree(r->hdr_host);
   r->hdr_host = nullptr;
+  if (r->settle_ev) (void)hipEventDestroy(r->settle_ev);
+  r->settle_ev = nullptr;
 }
 
 uint64_t* ctl_block(sst_result* r, int parity) { return (uint64_t*)r->ctl.p + parity * kCtlWords; }
@@ -852,10 +862,16 @@ int launch_tail(sst_table* t, sst_result* r) {
               kNodeBudget};
   fold_scan_limits(t->args, q);
   OutArgs o = out_args(r);
+#ifdef SST_DIAG  // diagnostic builds only (make DIAG=1): roles switched off, results invalid
   {
-    static const char* dbg = getenv("SST_TAIL_DBG");  // DIAGNOSTIC
+    static const char* dbg = getenv("SST_TAIL_DBG");
     o.dbg = dbg ? atoi(dbg) : 0;
   }
+#endif
+  // the deep roles' DFS stacks (~1.5 GB): allocated at the first pass that
+  // routes windows to them, not with every ctx
+  if (!c->ws_deep.ensure((size_t)2 * kDeepBlocks * 64 * kMaxDepth * glob_frame_bytes()))
+    return fail(c, SST_E_NOMEM, "device allocation failed (deep workspace)");
   ExactWs ws{(char*)c->ws_hash.p, (char*)c->ws_frames.p, (char*)c->ws_stacks.p, (uint64_t*)c->ws_epochs.p,
              c->hash_cap};
   Prof p(c, SST_K_EXPLAIN_DEEP);  // deep, no-memo and exact roles: one launch
@@ -869,6 +885,7 @@ int launch_tail(sst_table* t, sst_result* r) {
 // k_result_pack: dense hit list + dense payload + header of the current pass
 int launch_pack(sst_result* r, const uint64_t* scan_hdr = nullptr) {
   sst_ctx* c = r->ctx;
+  r->pass_stream = c->stream;  // the header the host waits for comes from this stream
   PackArgs pa{};
   if (scan_hdr) {  // after a fused scan: its part of the result is in place
     pa.scan_packed = 1;
@@ -891,10 +908,12 @@ int launch_pack(sst_result* r, const uint64_t* scan_hdr = nullptr) {
   pa.hdr_host = r->hdr_host_dev;
   pa.pass_id = ++r->pack_seq;
   pa.n_wg = r->n_wg;
+#ifdef SST_DIAG  // diagnostic builds only (make DIAG=1): copies skipped, results invalid
   {
     static const char* dbg = getenv("SST_PACK_DBG");
     pa.dbg = dbg ? atoi(dbg) : 0;
   }
+#endif
   {
     Prof p(c, SST_K_RESULT_PACK);
     HIP_OK(c, launch_result_pack(pa, c->stream));
@@ -920,6 +939,8 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
                  const PeaksJob* peaks = nullptr) {
   sst_ctx* c = t->ctx;
   r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count};
+  r->pass_stream = c->stream;
+  r->settle_ev_pending = false;
   const int64_t n = r->n;
   r->arena_bytes = (uint64_t)r->n_scan_waves * r->region_bytes + r->spill_bytes;
   if (!r->ctl.ensure(2 * kCtlWords * 8) || !r->lists.ensure((size_t)kNumClasses * std::max<int64_t>(n, 1) * 4) ||
@@ -941,14 +962,18 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
                                     prec, peaks->out, c->stream));
   }
   if (n == 0) {  // nothing to launch: an empty, settled result
+    // no scan ran to zero what the next pass reads: its control block and
+    // its half of the look-back aggregates
     HIP_OK(c, hipMemsetAsync(ctl_block(r, r->parity ^ 1), 0, kCtlWords * 8, c->stream));
+    HIP_OK(c, hipMemsetAsync((uint64_t*)r->agg.p + (size_t)(r->parity ^ 1) * r->n_wg, 0, (size_t)r->n_wg * 8,
+                             c->stream));
+    r->fused_pass = r->scan_hdr_pending = false;
+    r->scan_hits = r->scan_bytes = 0;
     r->n_hits = r->payload_bytes = 0;
     r->settled = true;
     return SST_OK;
   }
   r->settled = false;
-  if (!c->ws_deep.ensure((size_t)2 * kDeepBlocks * 64 * kMaxDepth * glob_frame_bytes()))
-    return fail(c, SST_E_NOMEM, "device allocation failed (deep workspace)");
   if (c->hash_cap == 0) {
     // SST_EXACT_HASH_CAP0 (tests): a smaller first memo per lane, so that the
     // retry ladder (8x the memo over 8x fewer lanes) runs down to its last rung
@@ -972,8 +997,10 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   if (fused) {
     o.fused = 1;
     o.pass_id = ++r->pack_seq;
+#ifdef SST_DIAG  // diagnostic builds only (make DIAG=1)
     static const char* dbg = getenv("SST_PACK_DBG");
     o.dbg = dbg ? atoi(dbg) : 0;
+#endif
   }
   const bool step = peaks && peaks->n > 0 && peaks->n_shifts == 4 && fused;
   if (peaks && peaks->n > 0 && peaks->n_shifts > 0 && !step) {  // A7 in its own launch, before the pass
@@ -1021,6 +1048,7 @@ int alloc_result(sst_table* t, int64_t n, sst_result** out, bool step = false) {
   if (c->expand_blocks == 0) c->expand_blocks = c->n_cu * explain_expand_blocks_per_cu();
   sst_result* r = new sst_result();
   r->ctx = c;
+  r->pass_stream = c->stream;
   r->n = n;
   r->cap_n = n;
   size_t nn = (size_t)std::max<int64_t>(n, 1);
@@ -1080,7 +1108,7 @@ int wait_header(sst_result* r, uint64_t* h) {
     sched_yield();
     if ((spin & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
       // a long pass (or a lost write): wait for the stream itself, then insist
-      HIP_OK(c, hipStreamSynchronize(c->stream));
+      HIP_OK(c, hipStreamSynchronize(r->pass_stream));
       if (__atomic_load_n(&hv[kHdrPass], __ATOMIC_ACQUIRE) != r->pack_seq)
         return fail(c, SST_E_INTERNAL, "explain: the result header was not written");
       break;
@@ -1099,6 +1127,14 @@ int wait_header(sst_result* r, uint64_t* h) {
 int settle(sst_result* r) {
   if (r->settled) return SST_OK;
   sst_ctx* c = r->ctx;
+  // launches below go to the pass's stream, whatever the ctx's current one is
+  struct StreamScope {
+    sst_ctx* c;
+    hipStream_t saved;
+    ~StreamScope() { c->stream = saved; }
+  } scope{c, c->stream};
+  c->stream = r->pass_stream;
+  bool launched = false;
   for (int attempt = 0;; ++attempt) {
     uint64_t h[kHdrWords];
     if (int rc = wait_header(r, h)) return rc;
@@ -1110,6 +1146,7 @@ int settle(sst_result* r) {
     if (h[kHdrRouted] && !r->tail_ran) {
       if (int rc = launch_tail(r->pass.t, r)) return rc;
       if (int rc = launch_pack(r, r->fused_pass ? h : nullptr)) return rc;
+      launched = true;
       --attempt;
       continue;
     }
@@ -1126,8 +1163,26 @@ int settle(sst_result* r) {
     const auto& p = r->pass;
     if (int rc = explain_pass(p.t, r, p.mass, p.thr, p.mods, p.mods_scalar, p.tol, p.prec, p.with_memo, p.cap, true))
       return rc;
+    launched = true;
+  }
+  if (launched) {
+    if (!r->settle_ev && hipEventCreateWithFlags(&r->settle_ev, hipEventDisableTiming) != hipSuccess) {
+      r->settle_ev = nullptr;
+      return fail(c, SST_E_HIP, "hipEventCreateWithFlags failed");
+    }
+    HIP_OK(c, hipEventRecord(r->settle_ev, r->pass_stream));
+    r->settle_ev_pending = true;
   }
   r->settled = true;
+  return SST_OK;
+}
+
+// Order the ctx's current stream after the work settle() queued on the
+// pass's stream (a no-op when they are the same stream or settle launched
+// nothing): the pass's kernels themselves are the caller's to order.
+int order_after_settle(sst_result* r) {
+  sst_ctx* c = r->ctx;
+  if (r->settle_ev_pending && c->stream != r->pass_stream) HIP_OK(c, hipStreamWaitEvent(c->stream, r->settle_ev, 0));
   return SST_OK;
 }
 
@@ -1137,6 +1192,7 @@ int fetch(sst_result* r) {
   sst_ctx* c = r->ctx;
   const int64_t n = r->n;
   if (int rc = settle(r)) return rc;
+  if (int rc = order_after_settle(r)) return rc;
   r->h_status.resize(n);
   r->h_count.assign(n, 0);
   r->h_offset.assign(n, 0);
@@ -1384,6 +1440,7 @@ int sst_result_device(sst_result* r, int8_t** d_status, uint64_t** d_count, uint
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
   if (int rc = settle(r)) return rc;
+  if (int rc = order_after_settle(r)) return rc;
   if ((d_count || d_offset) && !r->arrays_ready) {  // per-query arrays: built from the hit list on request
     const size_t nn = (size_t)std::max<int64_t>(r->n, 1);
     if (!r->count.ensure(nn * 8) || !r->offset.ensure(nn * 8))
@@ -1449,6 +1506,7 @@ int64_t sst_wire_pack(sst_result* r, const int8_t* d_valid, int64_t n_valid, voi
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
   if (int rc = settle(r)) return rc;
+  if (int rc = order_after_settle(r)) return rc;
   sst_table* t = r->pass.t;
   const uint64_t n_pair = r->scan_hits, n_exp = r->n_hits - r->scan_hits;
   const uint64_t xpay = r->payload_bytes - r->scan_bytes;
@@ -1473,7 +1531,7 @@ int64_t sst_wire_pack(sst_result* r, const int8_t* d_valid, int64_t n_valid, voi
   a.pair_bytes = r->scan_bytes;
   a.w = w;
   a.nb_v = align8(((uint64_t)n_valid + 7) / 8);
-  a.nb_s = align8(((uint64_t)r->n + 3) / 4);
+  a.nb_s = align8(((uint64_t)r->n + 7) / 8);
   a.nw_f = (n_pair * w + 63) / 64 * 2;
   a.nw_c = (n_pair + 19) / 20 * 2;
   a.o_vbits = 8 * kWireHeaderWords;
@@ -1615,6 +1673,114 @@ int sst_is_singleton_batch(sst_ctx* c, const int64_t* masses, int n_masses, cons
                                              (int8_t*)c->out_valid.p))
     return rc;
   HIP_OK(c, hipMemcpyAsync(out, c->out_valid.p, nn, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  return SST_OK;
+}
+
+// ---- per-spectrum reduced alphabets (sst_alpha.hip) --------------------
+static int check_masks(sst_table* t) {
+  if (t->n_rows > 120) return fail(t->ctx, SST_E_ARG, "alphabet masks cover 120 rows");
+  return SST_OK;
+}
+
+int sst_explain_pairs_alpha_device(sst_table* t, const double* d_mass, const double* d_thr, const int32_t* d_spec,
+                                   const uint64_t* d_masks, int64_t n, double tol, double prec, int8_t* d_status,
+                                   uint32_t* d_count, uint64_t* d_rowmask, uint32_t* d_range) {
+  if (!t || n < 0 || n > SST_MAX_EXPLAIN_BATCH ||
+      (n > 0 && (!d_mass || !d_spec || !d_masks || !d_status || !d_count || !d_rowmask || !d_range)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = check_masks(t)) return rc;
+  if (!t->args.pairs_enabled) return fail(c, SST_E_ARG, "pairs on reduced alphabets: the table has no pair list");
+  PairAlphaArgs a{d_mass, d_thr, d_spec, d_masks, n, tol, prec, 1.0 / prec, d_status, d_count, d_rowmask, d_range};
+  HIP_OK(c, launch_pairs_alpha(t->args, a, c->stream));
+  return SST_OK;
+}
+
+// host buffers in, host buffers out (synchronous); scratch on the device
+struct Scratch {
+  std::vector<DevBuf> b;
+  void* get(size_t bytes) {
+    b.emplace_back();
+    return b.back().ensure(bytes ? bytes : 1) ? b.back().p : nullptr;
+  }
+  ~Scratch() {
+    for (auto& x : b) x.release();
+  }
+};
+
+int sst_explain_pairs_alpha(sst_table* t, const double* mass, const double* thr, const int32_t* spec,
+                            const uint64_t* masks, int64_t n_spec, int64_t n, double tol, double prec, int8_t* status,
+                            uint32_t* count, uint64_t* rowmask, uint32_t* range) {
+  if (!t || n < 0 || n_spec < 0 || (n > 0 && (!mass || !spec || !masks || !status || !count || !rowmask || !range)))
+    return SST_E_ARG;
+  if (n == 0) return SST_OK;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  for (int64_t i = 0; i < n; ++i)
+    if (spec[i] < 0 || spec[i] >= n_spec) return fail(c, SST_E_ARG, "pairs on reduced alphabets: spectrum id out of range");
+  Scratch sc;
+  void *dm = sc.get(n * 8), *dt = thr ? sc.get(n * 8) : nullptr, *ds = sc.get(n * 4), *dk = sc.get(n_spec * 16);
+  void *o1 = sc.get(n), *o2 = sc.get(n * 4), *o3 = sc.get(n * 16), *o4 = sc.get(n * 8);
+  if (!dm || (thr && !dt) || !ds || !dk || !o1 || !o2 || !o3 || !o4)
+    return fail(c, SST_E_NOMEM, "device allocation failed (pairs on reduced alphabets)");
+  HIP_OK(c, hipMemcpyAsync(dm, mass, n * 8, hipMemcpyHostToDevice, c->stream));
+  if (thr) HIP_OK(c, hipMemcpyAsync(dt, thr, n * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, hipMemcpyAsync(ds, spec, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, hipMemcpyAsync(dk, masks, n_spec * 16, hipMemcpyHostToDevice, c->stream));
+  if (int rc = sst_explain_pairs_alpha_device(t, (const double*)dm, (const double*)dt, (const int32_t*)ds,
+                                              (const uint64_t*)dk, n, tol, prec, (int8_t*)o1, (uint32_t*)o2,
+                                              (uint64_t*)o3, (uint32_t*)o4))
+    return rc;
+  HIP_OK(c, hipMemcpyAsync(status, o1, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipMemcpyAsync(count, o2, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipMemcpyAsync(rowmask, o3, n * 16, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipMemcpyAsync(range, o4, n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  return SST_OK;
+}
+
+int sst_is_valid_alpha_device(sst_table* t, const double* d_mass, const double* d_thr, const int64_t* d_offsets,
+                              int64_t n_spec, const uint64_t* d_masks, double tol, double prec, int8_t* d_out) {
+  if (!t || n_spec < 0 || n_spec > INT32_MAX || (n_spec > 0 && (!d_mass || !d_offsets || !d_masks || !d_out)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = check_masks(t)) return rc;
+  AlphaArgs a{d_mass, d_thr, d_offsets, d_masks, t->args.w, t->n_rows, tol, prec, 1.0 / prec, d_out};
+  HIP_OK(c, launch_valid_alpha(a, n_spec, c->stream));
+  return SST_OK;
+}
+
+int sst_is_valid_alpha(sst_table* t, const double* mass, const double* thr, const int64_t* offsets, int64_t n_spec,
+                       const uint64_t* masks, double tol, double prec, int8_t* out) {
+  if (!t || n_spec < 0 || (n_spec > 0 && (!offsets || !masks))) return SST_E_ARG;
+  if (n_spec == 0) return SST_OK;
+  const int64_t n = offsets[n_spec];
+  if (offsets[0] != 0 || n < 0 || (n > 0 && (!mass || !out))) return SST_E_ARG;
+  for (int64_t g = 0; g < n_spec; ++g)
+    if (offsets[g + 1] < offsets[g]) return SST_E_ARG;
+  if (n == 0) return SST_OK;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  Scratch sc;
+  void *dm = sc.get(n * 8), *dt = thr ? sc.get(n * 8) : nullptr, *doff = sc.get((n_spec + 1) * 8),
+       *dk = sc.get(n_spec * 16), *dout = sc.get(n);
+  if (!dm || (thr && !dt) || !doff || !dk || !dout)
+    return fail(c, SST_E_NOMEM, "device allocation failed (is_valid on reduced alphabets)");
+  HIP_OK(c, hipMemcpyAsync(dm, mass, n * 8, hipMemcpyHostToDevice, c->stream));
+  if (thr) HIP_OK(c, hipMemcpyAsync(dt, thr, n * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, hipMemcpyAsync(doff, offsets, (n_spec + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIP_OK(c, hipMemcpyAsync(dk, masks, n_spec * 16, hipMemcpyHostToDevice, c->stream));
+  if (int rc = sst_is_valid_alpha_device(t, (const double*)dm, (const double*)dt, (const int64_t*)doff, n_spec,
+                                         (const uint64_t*)dk, tol, prec, (int8_t*)dout))
+    return rc;
+  HIP_OK(c, hipMemcpyAsync(out, dout, n, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   return SST_OK;
 }
@@ -1848,6 +2014,46 @@ int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* 
     }
   });
   return total;
+}
+
+int64_t sst_dict_union(const int64_t* offsets, int64_t n_spec, const double* key, const int8_t* kind,
+                       const int8_t* status, const uint64_t* rowmask, uint8_t* keep, uint64_t* union_out) {
+  if (!offsets || n_spec < 0) return SST_E_ARG;
+  if (n_spec == 0) return 0;
+  const int64_t n = offsets[n_spec];
+  if (n > 0 && (!key || !kind || !status || !rowmask || !keep || !union_out)) return SST_E_ARG;
+  std::atomic<int64_t> kept{0};
+  parallel_ranges(n_spec, 64, [&](int64_t g0, int64_t g1) {
+    std::vector<std::pair<double, int64_t>> v;
+    int64_t mine = 0;
+    for (int64_t gs = g0; gs < g1; ++gs) {
+      const int64_t a = offsets[gs], b = offsets[gs + 1];
+      union_out[2 * gs] = union_out[2 * gs + 1] = 0;
+      v.clear();
+      for (int64_t i = a; i < b; ++i) {
+        keep[i] = 0;
+        // side pairs are stored only with >= 1 explanation (prediction.py:322-323);
+        // singletons always (:277-282)
+        const bool writes = kind[i] == 2 || status[i] == SST_SOME;
+        if (writes) v.push_back({key[i] == 0.0 ? 0.0 : key[i], i});  // -0.0 == 0.0 as dict keys
+      }
+      // the last writer of every key survives (dict assignment order: START
+      // pairs, END pairs, singletons = the queries' order)
+      std::stable_sort(v.begin(), v.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+      for (size_t k = 0; k < v.size(); ++k) {
+        if (k + 1 < v.size() && v[k + 1].first == v[k].first) continue;
+        const int64_t i = v[k].second;
+        keep[i] = 1;
+        ++mine;
+        if (status[i] == SST_SOME) {
+          union_out[2 * gs] |= rowmask[2 * i];
+          union_out[2 * gs + 1] |= rowmask[2 * i + 1];
+        }
+      }
+    }
+    kept += mine;
+  });
+  return kept.load();
 }
 
 int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_groups, int64_t* order) {

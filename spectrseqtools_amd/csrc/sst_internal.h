@@ -253,13 +253,13 @@ struct ExactWs {
   uint32_t hash_cap;
 };
 
-// The gather's wire format v4 (sst_wire_pack, include/sst.h).  Header words
+// The gather's wire format v5 (sst_wire_pack, include/sst.h).  Header words
 // (u64): magic, n_valid, n_explain, n_pair, n_explicit, explicit payload
 // bytes, n_wg, key, w, n_list (the device counter), list capacity, list
-// offset, 4 reserved.  Sections (8-B aligned): valid bits, 2-bit status codes,
+// offset, 4 reserved.  Sections (8-B aligned): valid bits, hit bits,
 // w-bit first entries, 3-bit count codes (10 per u32), 12-B explicit records, explicit
 // payload, 8-B list entries.
-constexpr uint64_t kWireMagic = 0x3457545353ull;  // "SSTW4"
+constexpr uint64_t kWireMagic = 0x3557545353ull;  // "SSTW5"
 constexpr int kWireHeaderWords = 16;
 constexpr int kWireListWord = 9;
 struct WireArgs {
@@ -277,6 +277,34 @@ struct WireArgs {
   uint64_t hdr[kWireHeaderWords];
 };
 hipError_t launch_wire_pack(const WireArgs& a, hipStream_t st);
+
+// queries on per-spectrum reduced alphabets (sst_alpha.hip): spectrum g's
+// alphabet is the row set masks[2g] (rows 0..63) | masks[2g+1] (rows 64..119)
+// of the full table
+struct AlphaArgs {  // k_valid_alpha: is_valid_mass on the reduced tables
+  const double* mass;
+  const double* thr;       // may be null: tolerance * mass
+  const int64_t* offsets;  // [n_spec + 1] query ranges (each in mass order)
+  const uint64_t* masks;
+  const int* w;            // full table row masses
+  int n_rows;
+  double tol, prec, rprec;
+  int8_t* out;
+};
+struct PairAlphaArgs {  // k_pairs_alpha: explain on pair-class windows
+  const double* mass;
+  const double* thr;
+  const int32_t* spec;
+  const uint64_t* masks;
+  int64_t n;
+  double tol, prec, rprec;
+  int8_t* status;
+  uint32_t* count;
+  uint64_t* rowmask;  // [2n]
+  uint32_t* range;    // [2n] pair-list entries [first, end)
+};
+hipError_t launch_valid_alpha(const AlphaArgs& a, int64_t n_spec, hipStream_t st);
+hipError_t launch_pairs_alpha(const TableArgs& t, const PairAlphaArgs& a, hipStream_t st);
 
 hipError_t launch_bits_seed(uint64_t* R0, int64_t nwords, hipStream_t st);
 hipError_t launch_bits_shift_or(uint64_t* dst, const uint64_t* src, int64_t k, int64_t nwords, int64_t nbits,

@@ -37,6 +37,7 @@
 #include <algorithm>
 
 #include "sst_internal.h"
+#include "sst_quant.h"
 
 namespace sst {
 
@@ -79,45 +80,6 @@ __device__ __forceinline__ int rec_lo(ulonglong2 rec) { return (int)(rec.y >> 56
 __device__ __forceinline__ M128 rec_L(ulonglong2 rec) { return {rec.x, rec.y & ((1ull << 56) - 1ull)}; }
 
 __device__ __forceinline__ ulonglong2 ld_index(const ulonglong2* idx, int64_t m) { return idx[m]; }
-
-// Reference quantisation, mass_explanation.py:107,110-114: target =
-// rint(mass / prec) (Python round(x, 0): ties-to-even) and thr = ceil(t / prec)
-// on the IEEE f64 quotient (no fast-math).  The quotient is taken as
-// mass * (1/prec), within 2.5 ulp of the exact one; the correctly rounded
-// division runs only when that product lies within 2^-50 (relative) of a
-// point where rint / ceil change value, so the integers are exactly the
-// reference's.
-__device__ __forceinline__ double rint_quot(double num, double den, double rden) {
-  const double q = num * rden;
-  const double f = q - __builtin_floor(q);
-  if (!(__builtin_fabs(q) < 0x1p40) || __builtin_fabs(f - 0.5) <= __builtin_fabs(q) * 0x1p-50)
-    return __builtin_rint(num / den);
-  return __builtin_rint(q);
-}
-__device__ __forceinline__ double ceil_quot(double num, double den, double rden) {
-  if (num == 0.0) return 0.0;
-  const double q = num * rden;
-  if (!(__builtin_fabs(q) < 0x1p40) || __builtin_fabs(q - __builtin_rint(q)) <= __builtin_fabs(q) * 0x1p-50)
-    return __builtin_ceil(num / den);
-  return __builtin_ceil(q);
-}
-// window [lo, hi] as exact f64 integers (|values| < 2^53)
-__device__ __forceinline__ void quantise_f(double mass, double thr_abs, bool thr_none, double tol, double prec,
-                                           double rprec, double& lo, double& hi) {
-  const double t = thr_none ? tol * mass : thr_abs;
-  const double target = rint_quot(mass, prec, rprec);
-  const double th = ceil_quot(t, prec, rprec);
-  lo = target - th;
-  hi = target + th;
-}
-__device__ __forceinline__ void quantise(double mass, double thr_abs, bool thr_none, double tol, double prec,
-                                         double rprec, int64_t& lo, int64_t& hi) {
-  const double t = thr_none ? tol * mass : thr_abs;
-  const int64_t target = (int64_t)rint_quot(mass, prec, rprec);
-  const int64_t th = (int64_t)ceil_quot(t, prec, rprec);
-  lo = target - th;
-  hi = target + th;
-}
 
 // Window of one query as exact f64 integers: target = rint(mass / prec) and
 // thr = ceil(thr_abs / prec) (mass_explanation.py:107,110-114).  Both
@@ -2187,12 +2149,12 @@ __global__ __launch_bounds__(256) void k_hits_to_arrays(const uint4* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// The gather's wire format v4 (sst_wire_pack): one launch, a role per block
+// The gather's wire format v5 (sst_wire_pack): one launch, a role per block
 // range, every output byte written by exactly one thread except the list
-// entries (the rare rest: is_valid raises, statuses other than NONE / EMPTY /
+// entries (the rare rest: is_valid raises, statuses other than NONE /
 // SOME, pair hits whose count is not 1..7), whose slots a block takes with one
 // atomic (wire_slots).  HBM-bound byte work: each thread reads
-// 8 code bytes (or 4 status bytes, or 10 hit records) and writes one output
+// 8 code or status bytes (or 10 hit records) and writes one output
 // byte (or word); no LDS beyond the block's slot arithmetic.
 
 // 8 code bytes from q0 on (bytes past n read as 0)
@@ -2255,31 +2217,23 @@ __global__ __launch_bounds__(256) void k_wire_pack(WireArgs a) {
     for (; exc; exc &= exc - 1) wire_entry(a, pos++, 0u, t * 8 + __builtin_ctz(exc), 0u);
     return;
   }
-  if (b < a.be_s) {  // status: byte t = 4 queries' 2-bit codes; statuses past SOME listed
+  if (b < a.be_s) {  // status: byte t = 8 queries' hit bits (SOME / OVERFLOW / ABORTED); statuses other
+                     // than NONE / SOME listed (EMPTY is rare: a window reaching mass 0)
     const uint64_t t = (uint64_t)(b - a.be_v) * 256 + threadIdx.x;
     const bool act = t < a.nb_s;
-    const int64_t q0 = (int64_t)t * 4;
-    uint32_t v = 0;
-    if (act && q0 + 4 <= a.n8 && ((uintptr_t)(a.status + q0) & 3) == 0) {
-      v = *(const uint32_t*)(a.status + q0);
-    } else if (act) {
-      for (int k = 0; k < 4; ++k)
-        if (q0 + k < a.n8) v |= (uint32_t)(uint8_t)a.status[q0 + k] << (8 * k);
-    }
-    uint32_t codes = 0, exc = 0;
+    const uint64_t v = act ? wire_load8(a.status, (int64_t)t * 8, a.n8) : 0;
+    uint32_t bits = 0, exc = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 8; ++k) {
       const int8_t c = (int8_t)(v >> (8 * k));
-      const uint32_t code = c == SST_NONE ? 0u : (c == SST_EMPTY ? 1u : (c == SST_SOME || c == SST_OVERFLOW ||
-                                                                          c == SST_ABORTED) ? 2u : 3u);
-      codes |= code << (2 * k);
-      exc |= (uint32_t)(act && (int64_t)t * 4 + k < a.n8 && c != SST_NONE && c != SST_EMPTY && c != SST_SOME) << k;
+      bits |= (uint32_t)(c == SST_SOME || c == SST_OVERFLOW || c == SST_ABORTED) << k;
+      exc |= (uint32_t)(act && (int64_t)t * 8 + k < a.n8 && c != SST_NONE && c != SST_SOME) << k;
     }
-    if (act) a.out[a.o_sbits + t] = (uint8_t)codes;
+    if (act) a.out[a.o_sbits + t] = (uint8_t)bits;
     uint64_t pos = wire_slots(a, __builtin_popcount(exc));
     for (; exc; exc &= exc - 1) {
       const int k = __builtin_ctz(exc);
-      wire_entry(a, pos++, 1u, t * 4 + k, (uint32_t)(uint8_t)(v >> (8 * k)));
+      wire_entry(a, pos++, 1u, t * 8 + k, (uint32_t)(uint8_t)(v >> (8 * k)));
     }
     return;
   }
@@ -3368,8 +3322,8 @@ hipError_t launch_is_valid_peaks(const uint64_t* valid, int64_t limit, int64_t f
   if (n <= 0 || n_w <= 0) return hipSuccess;
   const int grid = (int)blocks_for(n, 256);
   ValidArgs v{valid, limit, full_lo, full_hi, first_reach, obs, nullptr, n, tol, prec, 1.0 / prec, out};
-  PeakShifts sh{};
-  for (int k = 0; k < n_w; ++k) sh.shift[k] = shifts[k];
+  PeakShifts sh{};  // 4 slots: the default branch below builds its own per group of 4
+  for (int k = 0; k < n_w && k < 4; ++k) sh.shift[k] = shifts[k];
   switch (n_w) {  // the reference's breakage dicts: 4 weights (FULL_BREAKAGE_DICT: up to 16)
     case 1: hipLaunchKernelGGL(k_is_valid_peaks<1>, dim3(grid), dim3(256), 0, st, v, sh); break;
     case 2: hipLaunchKernelGGL(k_is_valid_peaks<2>, dim3(grid), dim3(256), 0, st, v, sh); break;

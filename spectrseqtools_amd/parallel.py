@@ -10,17 +10,19 @@ candidate payload) to the rank that drives the Python pipeline.  RCCL has no
 gatherv: sizes are agreed once (all_gather of lengths), then one padded
 torch.distributed.gather moves the bytes (send/recv over xGMI).
 
-Wire format of one rank's result (v4, include/sst.h sst_wire_pack): packed
+Wire format of one rank's result (v5, include/sst.h sst_wire_pack): packed
 on the device by one kernel (no host round trip): 1-bit is_valid codes,
-2-bit status codes (NONE / EMPTY / hit / listed), per pair-path hit its
-first pair-list entry in w = ceil(log2(pair-list entries)) bits and a 2-bit
-count code (3 bits; the receiver rebuilds the candidates from its own copy of the
+1-bit hit flags per explain query (SOME / OVERFLOW / ABORTED; EMPTY and the
+other rare statuses in the list), per pair-path hit its
+first pair-list entry in w = ceil(log2(pair-list entries)) bits and a 3-bit
+count code ( the receiver rebuilds the candidates from its own copy of the
 table's pair list, so those hits send no payload), 12-B records and the
 payload for the few hits of the deferred paths, and a list of the rare rest
-(is_valid raises, statuses other than NONE / EMPTY / SOME, counts outside
-1..7).  About 0.125 B per is_valid query, 0.25 B per explain query and
-~2 B per pair hit: ~6.7 MB per rank per config-3 step (v3, 2-bit codes and 4 B per pair hit: 10.7 MB;
-v2, 12-B records + the dense payload: 33 MB; the engine's own layout: 51 MB).
+(is_valid raises, statuses other than NONE / SOME, counts outside 1..7).
+About 0.125 B per is_valid query, 0.125 B per explain query and ~2 B per
+pair hit: ~5.4 MB per rank per config-3 step (v4, 2-bit status codes: 6.7
+MB; v3, 2-bit codes and 4 B per pair hit: 10.7 MB; v2, 12-B records + the
+dense payload: 33 MB; the engine's own layout: 51 MB).
 wire_pack_host states the packer in numpy; wire_unpack + decode_hits +
 candidates read a buffer back with numpy alone.
 """
@@ -116,17 +118,10 @@ def device_bytes(ptr, nbytes, device):
 
 
 WIRE_HEADER = 128
-WIRE_MAGIC = 0x3457545353  # "SSTW4"
+WIRE_MAGIC = 0x3557545353  # "SSTW5"
 SST_NONE, SST_EMPTY, SST_SOME, SST_OUT_OF_TABLE, SST_OVERFLOW, SST_ABORTED = 0, 1, 2, -1, -2, -4
 SCAN_WAVES_PER_WG = 16  # k_explain_scan: 1024-lane workgroups
 LIST_RAISE, LIST_STATUS, LIST_COUNT = 0, 1, 2  # wire list entry types
-
-
-def _pack2(codes):
-    """uint8 codes in {0..3} -> 4 per byte."""
-    c = np.asarray(codes, dtype=np.uint8)
-    c = np.concatenate([c, np.zeros((-len(c)) % 4, np.uint8)]).reshape(-1, 4)
-    return c[:, 0] | (c[:, 1] << 2) | (c[:, 2] << 4) | (c[:, 3] << 6)
 
 
 def _pack3(codes):
@@ -139,12 +134,6 @@ def _pack3(codes):
 def _unpack3(b, n):
     w = np.asarray(b, dtype=np.uint8)[:4 * ((n + 9) // 10)].view(np.uint32)
     return ((w[:, None] >> (3 * np.arange(10, dtype=np.uint32))) & 7).ravel()[:n].astype(np.int64)
-
-
-def _unpack2(b, n):
-    b = np.asarray(b, dtype=np.uint8)
-    c = np.stack([b & 3, (b >> 2) & 3, (b >> 4) & 3, b >> 6], axis=1).ravel()
-    return c[:n]
 
 
 def pair_key(recs):
@@ -184,11 +173,11 @@ def first_width(n_entries):
 
 
 def wire_layout(n_valid, n_explain, n_pair, n_explicit, xpay, w):
-    """Byte offsets of the wire v4 sections (include/sst.h, sst_wire_pack):
+    """Byte offsets of the wire v5 sections (include/sst.h, sst_wire_pack):
     every section starts 8-byte aligned; 'list' is the fixed part's size."""
     o = {"valid": WIRE_HEADER}
     o["status"] = o["valid"] + _a8((n_valid + 7) // 8)
-    o["first"] = o["status"] + _a8((n_explain + 3) // 4)
+    o["first"] = o["status"] + _a8((n_explain + 7) // 8)
     o["codes"] = o["first"] + 8 * ((n_pair * w + 63) // 64)
     o["explicit"] = o["codes"] + 8 * ((n_pair + 19) // 20)
     o["payload"] = o["explicit"] + _a8(12 * n_explicit)
@@ -198,7 +187,7 @@ def wire_layout(n_valid, n_explain, n_pair, n_explicit, xpay, w):
 
 def wire_pack_host(valid, status, hits, payload, refs=None, n_pair=0, pair_bytes=0, n_wg=0, recs=None):
     """numpy statement of sst_wire_pack (the device packer of the gather's
-    wire format v4) for host-side results: valid / status int8 arrays, hits
+    wire format v5) for host-side results: valid / status int8 arrays, hits
     the dense hit list as u32 [n, 4] {query, count, word lo, word hi}, payload
     u8, refs u16 per pair hit (first | 0x8000 for OVERFLOW), recs the table's
     pair records.  Same bytes as the device packer except the list entries'
@@ -222,7 +211,7 @@ def wire_pack_host(valid, status, hits, payload, refs=None, n_pair=0, pair_bytes
     lst = []
     for q in np.flatnonzero(valid == -1):
         lst.append((LIST_RAISE, int(q), 0))
-    for q in np.flatnonzero((st != SST_NONE) & (st != SST_EMPTY) & (st != SST_SOME)):
+    for q in np.flatnonzero((st != SST_NONE) & (st != SST_SOME)):
         lst.append((LIST_STATUS, int(q), int(np.uint8(st[q]))))
     cnt = hits[:n_pair, 1].astype(np.int64)
     for i in np.flatnonzero((cnt < 1) | (cnt > 7)):
@@ -234,8 +223,7 @@ def wire_pack_host(valid, status, hits, payload, refs=None, n_pair=0, pair_bytes
     vb = np.packbits(valid == 1, bitorder="little")
     buf[o["valid"]:o["valid"] + len(vb)] = vb
     hit = (st == SST_SOME) | (st == SST_OVERFLOW) | (st == SST_ABORTED)
-    code = np.where(st == SST_NONE, 0, np.where(st == SST_EMPTY, 1, np.where(hit, 2, 3))).astype(np.uint8)
-    sb = _pack2(code)
+    sb = np.packbits(hit, bitorder="little")
     buf[o["status"]:o["status"] + len(sb)] = sb
     if n_pair:
         f = np.asarray(refs, dtype=np.uint16)[:n_pair].astype(np.int64) & 0x7FFF
@@ -260,7 +248,7 @@ def wire_pack_host(valid, status, hits, payload, refs=None, n_pair=0, pair_bytes
 
 
 def wire_unpack(buf, recs=None):
-    """numpy form of a wire v4 buffer (sst_wire_pack / wire_pack_host; a
+    """numpy form of a wire v5 buffer (sst_wire_pack / wire_pack_host; a
     gathered buffer may carry padding after its list): (valid i8, status i8,
     hits u32[n,4] in the engine's record layout {query, count, word lo, word
     hi}, payload u8).  recs: the table's pair records
@@ -285,9 +273,8 @@ def wire_unpack(buf, recs=None):
     typ, idx, val = ent[:, 0] >> 30, (ent[:, 0] & 0x3FFFFFFF).astype(np.int64), ent[:, 1]
     valid = np.unpackbits(b[o["valid"]:o["status"]], bitorder="little")[:n7].astype(np.int8)
     valid[idx[typ == LIST_RAISE]] = -1
-    code = _unpack2(b[o["status"]:o["first"]], n8)
-    hit = code == 2
-    status = np.select([code == 1, hit], [SST_EMPTY, SST_SOME], SST_NONE).astype(np.int8)
+    hit = np.unpackbits(b[o["status"]:o["first"]], bitorder="little")[:n8].astype(bool)
+    status = np.where(hit, SST_SOME, SST_NONE).astype(np.int8)
     m = typ == LIST_STATUS
     status[idx[m]] = val[m].astype(np.uint8).view(np.int8)
     rec = b[o["explicit"]:o["explicit"] + 12 * nexp].view(np.uint32).reshape(nexp, 3)

@@ -19,12 +19,22 @@ in flat arrays (spectrum id per row) instead of per-spectrum frames:
                  bin of a side explains whole fragment masses (deep windows:
                  the engine's deferred DFS kernels).
 
+  4. fixpoint   (prediction.py:170-227, filter_by_explanation): every round
+                 of every spectrum at once -- the pair-class explains of all
+                 spectra against their own reduced alphabets (one
+                 sst_explain_pairs_alpha call: the reduced tables are never
+                 built), the explanation dicts' surviving entries and observed
+                 rows (sst_dict_union, host-native), the alphabet reduction as
+                 row-mask arithmetic, and is_valid of every remaining fragment
+                 against its spectrum's reduced table (one sst_is_valid_alpha
+                 call); spectra whose alphabet stopped shrinking drop out.
+
 Every stage's rows equal what the per-spectrum mirrors produce
-(tests/test_pipeline.py).  Budgets follow each spectrum's max_len (the cli
-derives it from the sequence mass, cli.py:158-177): spectra are grouped by
-max_len and each group is one engine call with that group's row caps.
-Alphabet reduction (a per-spectrum table rebuild) and the MILP are not
-batched stages.
+(tests/test_pipeline.py); the fixpoint's rounds equal the reference's own
+(tests/golden/callers.json.gz).  Budgets follow each spectrum's max_len (the
+cli derives it from the sequence mass, cli.py:158-177): spectra are grouped
+by max_len and each group is one engine call with that group's row caps.
+The MILP is not a batched stage.
 """
 from dataclasses import dataclass
 
@@ -184,3 +194,124 @@ def bin_queries(c: Classified, tolerance=MATCHING_THRESHOLD):
     cat = (lambda x: np.concatenate(x)) if d_all else (lambda x: np.zeros(0))
     return Queries(cat(d_all), cat(t_all), cat(s_all).astype(np.int64), cat(k_all).astype(np.int64),
                    cat(sd_all).astype(np.int8))
+
+
+def row_masks(rows_bool):
+    """[S, N] bool row membership -> [S, 2] u64 masks (rows 0..63, 64..119)."""
+    b = np.asarray(rows_bool, dtype=bool)
+    S, N = b.shape
+    out = np.zeros((S, 2), np.uint64)
+    for r in range(N):
+        if b[:, r].any():
+            out[b[:, r], r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    return out
+
+
+def mask_rows(masks, n_rows):
+    """[S, 2] u64 masks -> [S, n_rows] bool."""
+    m = np.asarray(masks, dtype=np.uint64).reshape(-1, 2)
+    r = np.arange(n_rows)
+    return ((m[:, r >> 6] >> (r & 63).astype(np.uint64)) & np.uint64(1)).astype(bool)
+
+
+@dataclass
+class Fixpoint:
+    """filter_by_explanation over many spectra: final alphabets (row masks of
+    the full table), the surviving rows of the Classified frame, the rounds
+    each spectrum ran, and the last round's queries / answers (the
+    explanation dict the skeleton stage reads: keep marks its entries)."""
+    alpha: np.ndarray        # [S, 2] u64
+    alive: np.ndarray        # [rows] bool
+    rounds: np.ndarray       # [S]
+    history: list            # per round: (active spectra [S] bool, alpha [S, 2], alive [rows]) when recorded
+    last: dict               # spectrum-major arrays of the final round: diff, thr, spec, kind, status, count,
+    #                          rowmask, range, keep
+
+
+def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolerance=MATCHING_THRESHOLD,
+                    record=False):
+    """Predictor.filter_by_explanation (prediction.py:170-202) for every
+    spectrum of `c` at once.  dp_table: the full alphabet's table (its rows
+    are the mask bits); max_len[s]: spectrum s's SequenceInformation.max_len
+    (its budgets).  Per round and spectrum, as the reference: explain every
+    sliding-window pair of both sides and every singleton (the dict
+    collect_diff_explanations_for_su builds), reduce the alphabet to the
+    canonical rows plus the modifications the dict's explanations name
+    (adapt_individual_modification_rates_by_alphabet_reduction,
+    mass_table.py:94-100), keep the fragments is_valid_mass accepts on the
+    reduced table (:204-227); repeat while the alphabet shrank.  Every window
+    of these rounds is pair-class (a difference below the heaviest nucleotide,
+    or a singleton's mass); budgets cannot bind once max_modifications and the
+    modification rows' caps are >= 2, which is checked (smaller budgets raise
+    NotImplementedError: the per-spectrum mirror handles them)."""
+    dev = dp_table.device_table
+    masses = dp_table.masses
+    N = len(masses)
+    S = len(c.offsets) - 1
+    max_len = np.broadcast_to(np.asarray(max_len, dtype=np.int64), (S,))
+    is_mod = np.array([m.is_modification for m in masses])
+    rate = np.array([m.modification_rate for m in masses], dtype=np.float64)
+    rows_all = np.zeros((1, N), bool)
+    rows_all[0, 1:] = True
+    alpha = np.repeat(row_masks(rows_all), S, axis=0)
+    canon = row_masks((~is_mod & (np.arange(N) > 0))[None, :])[0]
+    # budgets: max_modifications = round(0.5 max_len) (common.py:55) and the
+    # modification rows' caps round(max_len * rate) (mass_explanation.py:158-172)
+    A = np.array([round(dp_table.seq.modification_rate * int(L)) for L in max_len], dtype=np.int64)
+    cap_min = np.array([min([round(int(L) * r) for r in rate[is_mod]] or [2]) for L in max_len], dtype=np.int64)
+    if (A < 2).any() or (cap_min < 2).any():
+        raise NotImplementedError("filter_fixpoint: budgets that can bind on pair windows (max_len too small)")
+    max_w = max(explanation_masses.get_column("monoisotopic_mass").to_list()) + PHOSPHATE_LINK_MASS
+    side = np.array([("START" in n) | (("END" in n) << 1) for n in c.names], dtype=np.uint8)
+    flags = side[c.brk] | (np.asarray(c.singleton, dtype=np.uint8) << 2)
+    alive = np.ones(len(c.su), bool)
+    active = np.ones(S, bool)
+    rounds = np.zeros(S, np.int64)
+    history = []
+    parts = []  # (spectra active in the round, the round's queries and answers)
+    pop = lambda m: np.array([bin(int(a)).count("1") + bin(int(b)).count("1") for a, b in m], dtype=np.int64)
+    while active.any():
+        rows = np.flatnonzero(alive & active[c.spec])
+        off = np.searchsorted(c.spec[rows], np.arange(S + 1))
+        d, t, g, k = _su_diff_queries(c.su[rows], c.obs[rows], flags[rows], off, max_w, tolerance)
+        st, cnt, rm, rg = dev.explain_pairs_alpha(d, t, g, alpha, tolerance, dp_table.precision)
+        if (st == -10).any():
+            raise NotImplementedError("filter_fixpoint: a window outside the pair class")
+        q_off = np.searchsorted(g, np.arange(S + 1))
+        from ._native import dict_union
+
+        keep, union = dict_union(q_off, d, k, st, rm)
+        new_alpha = alpha.copy()
+        new_alpha[active] = canon[None, :] | (alpha[active] & union[active])
+        changed = pop(new_alpha) != pop(alpha)
+        parts.append((active.copy(), {"diff": d, "thr": t, "spec": g, "kind": k, "status": st, "count": cnt, "rowmask": rm,
+                      "range": rg, "keep": keep}))
+        alpha = new_alpha
+        rounds[active] += 1
+        # _reduce_alphabet's is_valid_mass filter on the reduced tables (:211-227)
+        v = dev.is_valid_alpha(c.su[rows], tolerance * c.obs[rows], off, alpha, tolerance, dp_table.precision)
+        if (v < 0).any():
+            raise NotImplementedError("is_valid_mass raised on a reduced table (window past its extent)")
+        alive[rows[v != 1]] = False
+        if record:
+            history.append((active.copy(), alpha.copy(), alive.copy()))
+        active &= changed
+    return Fixpoint(alpha, alive, rounds, history, _final_round(parts, S))
+
+
+def _final_round(parts, S):
+    """Each spectrum's queries and answers of its last round, spectrum-major."""
+    if not parts:
+        return {}
+    final_part = np.full(S, -1, np.int64)
+    for j, (act, _) in enumerate(parts):
+        final_part[act] = j
+    out = {}
+    keys = parts[0][1].keys()
+    sel = []
+    for j, (_, rd) in enumerate(parts):
+        sel.append(final_part[rd["spec"]] == j)
+    for kk in keys:
+        out[kk] = np.concatenate([rd[kk][m] for (_, rd), m in zip(parts, sel)])
+    order = np.argsort(out["spec"], kind="stable")
+    return {kk: v[order] for kk, v in out.items()}

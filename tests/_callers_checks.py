@@ -170,3 +170,66 @@ def check_classify_batch(recs, dps_by_ctx):
         for f, c, b in zip(frames, cuts, batch):
             assert classify_fragments(f, dp, bd, intensity_cutoff=c).to_dict() == b.to_dict()
     return np.int64(0)
+
+
+def classified_of(rec):
+    """pipeline.Classified of one reference classify_fragments frame (its rows
+    in the frame's order: SU order, the `index` Predictor.predict gives)."""
+    from spectrseqtools_amd import pipeline
+
+    cols = rec["classify"]["columns"]
+    rows = rec["classify"]["rows"]
+    col = {c: [r[i] for r in rows] for i, c in enumerate(cols)}
+    names = sorted(set(col["breakage"]))
+    n = len(rows)
+    return pipeline.Classified(np.zeros(n, np.int64), np.asarray(col["standard_unit_mass"], dtype=np.float64),
+                               np.asarray(col["observed_mass"], dtype=np.float64),
+                               np.asarray(col["fragment_index"], dtype=np.int64),
+                               np.asarray([names.index(b) for b in col["breakage"]], dtype=np.int64),
+                               np.asarray(col["is_singleton"], dtype=bool), names, np.array([0, n], np.int64), 0, 0)
+
+
+def check_fixpoint(rec, dp):
+    """pipeline.filter_fixpoint (every round of every spectrum batched) on the
+    reference's classify frame == the reference's own filter_by_explanation:
+    the alphabet and the kept fragment indices after every round, the number
+    of rounds, and the final explanation dict (keys and candidate rows)."""
+    from spectrseqtools_amd import pipeline
+
+    c = classified_of(rec)
+    fx = pipeline.filter_fixpoint(c, dp, [dp.seq.max_len], EXPLANATION_MASSES, record=True)
+    want = rec["filter"]["rounds"]
+    assert int(fx.rounds[0]) == len(want) == len(fx.history)
+    for k, (act, alpha, alive) in enumerate(fx.history):
+        rows = pipeline.mask_rows(alpha, len(dp.masses))[0]
+        got_masses = [0] + [dp.masses[r].mass for r in range(1, len(dp.masses)) if rows[r]]
+        assert got_masses == want[k]["masses"], k
+        assert np.flatnonzero(alive).tolist() == want[k]["kept_index"], k
+    # the final dict: surviving entries, their keys and candidate rows (full-table rows)
+    last = fx.last
+    recs = dp.device_table.pair_records()
+    alpha_rows = pipeline.mask_rows(fx.alpha, len(dp.masses))[0]
+    got = {}
+    for i in np.flatnonzero(last["keep"]):
+        st = int(last["status"][i])
+        if st == 2:
+            lo, hi = (int(x) for x in last["range"][i])
+            cands = []
+            for e in recs[lo:hi]:
+                k = int(e) & 0xFF
+                rr = tuple((int(e) >> (8 * (j + 1))) & 0xFF for j in range(k))
+                if all(alpha_rows[r] for r in rr):
+                    cands.append(rr)
+            assert len(cands) == int(last["count"][i])
+            got[repr(float(last["diff"][i]))] = sorted(cands)
+        else:
+            got[repr(float(last["diff"][i]))] = None if st == 0 else []
+    # fixture rows index the final reduced table; map them to full-table rows
+    full_of = [r for r in range(len(dp.masses)) if r == 0 or alpha_rows[r]]
+    want_d = {}
+    for k, v in rec["filter"]["explanations"].items():
+        want_d[k] = None if v is None else sorted(tuple(full_of[x] for x in t) for t in v)
+    assert sorted(got) == sorted(want_d)
+    for k in want_d:
+        assert got[k] == want_d[k], k
+    return fx

@@ -4,37 +4,57 @@
 
 TEST INFRASTRUCTURE.  Uses make_golden.py's set-up (the pandas-backed polars
 stand-in in tests/golden/standin/, the reference's own DynamicProgrammingTable,
-is_valid_mass and explain_mass_with_table).
+is_valid_mass and explain_mass_with_table) plus import-only stand-ins for the
+modules prediction.py / skeleton_building.py import but never use on these
+paths: loguru (logger.warning only), pulp (linear_program.py; every name
+raises), ms_deisotope and clr_loader (common.py's RAW reader), and typing.Self
+(Python 3.10; annotations only).  Every function below runs UNMODIFIED; the
+generator only observes (instance-level wrappers that record what the
+reference's own methods return).
 
   callers.json.gz, per reference test spectrum (tests/testcases/test_0[1-8]):
-    classify   the output frame of the reference's own
-               fragment_classification.classify_fragments (:17-101): columns and
-               rows, run unmodified through the stand-in
+    classify   the output frame of fragment_classification.classify_fragments
+               (:17-101)
     filter     Predictor.filter_by_explanation (prediction.py:170-202) on that
-               frame as Predictor.predict prepares it (:68-80): the alphabet
-               after every reduction round, the fragment `index` values kept and
-               the last round's explanation dict (diff -> sorted row-index
-               tuples, or None).  prediction.py cannot be imported (typing.Self,
-               loguru, pulp), so collect_diff_explanations_for_su /
-               collect_explanations_per_side / _reduce_alphabet are restated
-               here line for line; every explain / is_valid answer and every
-               alphabet reduction (table rebuild) is the reference's own code.
+               frame as Predictor.predict prepares it (:68-80): the alphabet and
+               the fragment `index` values kept after every _reduce_alphabet
+               round (:204-227), and the returned explanation dict (diff ->
+               sorted row-index tuples, or None)
+    skeleton   SkeletonBuilder._predict_skeleton (skeleton_building.py:114-196)
+               per side (START, END) with those explanations on the reduced
+               table: the skeleton (sorted names per position), the kept
+               fragments' index / min_end / max_end, the explain queries it
+               issued; then select_sequence_length_with_jaccard (:315-370) on
+               the two skeletons: its alphabet reduction, both
+               compute_sequence_length_bound results and the chosen length, and
+               combine_skeleton_sequences (:494-516) at that length
 
-Usage:  python tests/golden/make_callers_golden.py
+Set order: explanation lists follow Python set iteration of name tuples
+(hash-seed dependent in the reference); the generator runs with
+PYTHONHASHSEED=0 and records whether a second seed changes any skeleton
+(`seed_independent`).
+
+Usage:  PYTHONHASHSEED=0 XDG_CACHE_HOME=/tmp/sst_refcache python tests/golden/make_callers_golden.py
 """
-import csv
 import os
+import subprocess
 import sys
 import time
+import typing
+
+if not hasattr(typing, "Self"):  # Python 3.10: prediction.py:3 imports it for annotations only
+    typing.Self = typing.Any
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
-import make_golden as G  # noqa: E402  (sets sys.path: stand-in first, then the reference)
+import make_golden as G  # noqa: E402  (sets sys.path: stand-ins first, then the reference)
 import polars as pl  # noqa: E402  (the stand-in)
 import yaml  # noqa: E402
 
 import spectrseqtools.fragment_classification as FC  # noqa: E402
+import spectrseqtools.prediction as PR  # noqa: E402
+import spectrseqtools.skeleton_building as SB  # noqa: E402
 
 M, MT, ME, EM, REF = G.M, G.MT, G.ME, G.EM, G.REF
 
@@ -49,70 +69,79 @@ def frame_dump(df):
     return {"columns": df.columns, "rows": [[_jsonable(x) for x in r] for r in df.rows()]}
 
 
-def wrap_rows(dp, names_set):
-    return None if names_set is None else [list(t) for t in G.rows_of(dp, names_set)]
+def expl_rows(dp, expl):
+    """A calculate_explanations list (Explanation objects) or None -> sorted
+    row-index tuples of dp's alphabet."""
+    return None if expl is None else [list(t) for t in G.rows_of(dp, [tuple(e) for e in expl])]
 
 
-def calculate_explanations(diff, threshold, dp):
-    """common.py:47-65 (the module imports ms_deisotope / mono at load)."""
-    r = ME.explain_mass_with_table(diff, dp_table=dp,
-                                   max_modifications=round(dp.seq.modification_rate * dp.seq.max_len),
-                                   threshold=threshold).explanations
-    return r  # the name set; list(Explanation) wrapping is order-only
+def skeleton_dump(sk):
+    return [sorted(p) for p in sk]
 
 
-def per_side(rows, dp):
-    """prediction.py:286-329 restated (rows: (su, obs) sorted by su)."""
-    maxw = max(EM.get_column("monoisotopic_mass").to_list()) + M.PHOSPHATE_LINK_MASS
-    su = [r[0] for r in rows]
-    obs = [r[1] for r in rows]
-    start, end = 0, 1
-    out = {}
-    while end < len(rows):
-        if (end - start) <= 0:
-            end += 1
-            continue
-        diff = su[end] - su[start]
-        if diff > maxw:
-            start += 1
-            end = start + 1
-            continue
-        thr = dp.tolerance * (obs[start] + obs[end])
-        expl = calculate_explanations(diff, thr, dp)
-        if expl is not None and len(expl) >= 1:
-            out[diff] = expl
-        if end == len(rows) - 1:
-            start += 1
-        else:
-            end += 1
-    return out
-
-
-def collect(frags, dp):
-    """prediction.py:261-284 restated; frags: dicts in frame order."""
-    e = {**per_side([(f["standard_unit_mass"], f["observed_mass"]) for f in frags if "START" in f["breakage"]], dp),
-         **per_side([(f["standard_unit_mass"], f["observed_mass"]) for f in frags if "END" in f["breakage"]], dp)}
-    for f in frags:
-        if f["is_singleton"]:
-            e[f["standard_unit_mass"]] = calculate_explanations(f["standard_unit_mass"],
-                                                                dp.tolerance * f["observed_mass"], dp)
-    return e
-
-
-def filter_by_explanation(frags, dp):
-    """prediction.py:170-227 restated (the reduction and is_valid are the reference's)."""
+def filter_by_explanation(frame, dp):
+    """Predictor.filter_by_explanation, unmodified, with its _reduce_alphabet
+    observed per round."""
+    pred = PR.Predictor(dp, EM)
     rounds = []
-    old = -1
-    expl = {}
-    while old != len(dp.masses):
-        old = len(dp.masses)
-        expl = collect(frags, dp)
-        observed = {nuc for ex in expl.values() if ex is not None for t in ex for nuc in t}
-        dp.adapt_individual_modification_rates_by_alphabet_reduction(observed)
-        frags = [f for f in frags if ME.is_valid_mass(f["standard_unit_mass"], dp,
-                                                       threshold=dp.tolerance * f["observed_mass"])]
-        rounds.append({"masses": [int(m.mass) for m in dp.masses], "kept_index": [f["index"] for f in frags]})
-    return rounds, {repr(k): wrap_rows(dp, v) for k, v in expl.items()}
+    orig = pred._reduce_alphabet
+
+    def observed(nucleotide_list, fragments):
+        out = orig(nucleotide_list, fragments)
+        rounds.append({"masses": [int(m.mass) for m in dp.masses],
+                       "kept_index": [int(x) for x in out.get_column("index").to_list()]})
+        return out
+
+    pred._reduce_alphabet = observed
+    frags, expl = pred.filter_by_explanation(frame)
+    return frags, expl, rounds
+
+
+def skeleton(frags, expl, dp):
+    """SkeletonBuilder._predict_skeleton per side and the Jaccard length
+    selection, unmodified, with explain / length-bound calls observed."""
+    sb = SB.SkeletonBuilder(explanations=expl, dp_table=dp)
+    queries = []
+    orig_calc = SB.calculate_explanations
+
+    def calc(diff, threshold, dp_table):
+        r = orig_calc(diff, threshold, dp_table)
+        queries.append([diff, threshold, expl_rows(dp_table, r)])
+        return r
+
+    bounds = []
+    orig_lb = SB.compute_sequence_length_bound
+
+    def lb(dp_table, dir):
+        v = orig_lb(dp_table=dp_table, dir=dir)
+        bounds.append([dir, int(v)])
+        return v
+
+    SB.calculate_explanations, SB.compute_sequence_length_bound = calc, lb
+    try:
+        out = {}
+        for side in ("START", "END"):
+            queries.clear()
+            n_warn = len(SB.logger.records)
+            sk, fr = sb._predict_skeleton(fragments=frags.filter(pl.col("breakage").str.contains(side)),
+                                          skeleton_seq=[set() for _ in range(dp.seq.max_len)])
+            out[side] = {"skeleton": skeleton_dump(sk), "sk_sets": sk,
+                         "kept_index": [int(x) for x in fr.get_column("index").to_list()],
+                         "min_end": [int(x) for x in fr.get_column("min_end").to_list()],
+                         "max_end": [int(x) for x in fr.get_column("max_end").to_list()],
+                         "queries": list(queries), "warnings": len(SB.logger.records) - n_warn}
+        start_sk, end_sk = out["START"].pop("sk_sets"), out["END"].pop("sk_sets")[::-1]
+        try:
+            seq_len = sb.select_sequence_length_with_jaccard(start_skeleton=start_sk, end_skeleton=end_sk)
+            combined = skeleton_dump(SB.combine_skeleton_sequences(seq_len, start_sk, end_sk))
+            err = None
+        except Exception as e:  # the reference raises when no length fits the sequence mass
+            seq_len, combined, err = None, None, f"{type(e).__name__}: {e}"
+        out["jaccard"] = {"masses": [int(m.mass) for m in dp.masses], "bounds": list(bounds), "seq_len": seq_len,
+                          "combined": combined, "error": err}
+        return out
+    finally:
+        SB.calculate_explanations, SB.compute_sequence_length_bound = orig_calc, orig_lb
 
 
 def main():
@@ -128,22 +157,38 @@ def main():
         cutoff = meta.get("intensity_cutoff", M.DEFAULT_INTENSITY_CUTOFF)
         cid = f"callers_{tc}"
         dp = G.make_ctx(cid, max_len, M.MATCHING_THRESHOLD, su=su_seq)
-        G.CTX[cid]["obs_mass"] = meta["sequence_mass"]
+        G.CTX[cid]["obs_mass"] = dp.seq.obs_mass = meta["sequence_mass"]  # cli.py:149-176
         classified = FC.classify_fragments(frame, dp, bd, intensity_cutoff=cutoff)
         rec = {"ctx": G.CTX[cid], "intensity_cutoff": cutoff, "tags": [meta.get("label_mass_5T", 555.1294),
                                                                          meta.get("label_mass_3T", 455.1491)],
                "input": frame_dump(frame), "classify": frame_dump(classified)}
         # Predictor.predict's framing (prediction.py:68-80)
-        cols = classified.columns
-        rows = [dict(zip(cols, r)) for r in classified.rows()]
-        rows = [dict(r, orig_index=i) for i, r in enumerate(rows)]
-        rows = sorted(rows, key=lambda r: r["standard_unit_mass"])
-        rows = [dict(r, index=i) for i, r in enumerate(rows)]
-        rec["filter"] = dict(zip(("rounds", "explanations"), filter_by_explanation(rows, dp)))
+        prepared = (classified.with_row_index(name="orig_index").sort("standard_unit_mass")
+                    .with_row_index(name="index"))
+        prepared = prepared.with_columns(pl.lit(0, dtype=pl.Int64).alias("min_end"),
+                                         pl.lit(-1, dtype=pl.Int64).alias("max_end"))
+        frags, expl, rounds = filter_by_explanation(prepared, dp)
+        rec["filter"] = {"rounds": rounds, "explanations": {repr(k): expl_rows(dp, v) for k, v in expl.items()}}
+        rec["skeleton"] = skeleton(frags, expl, dp)
         out[tc] = rec
         print(f"  {tc}: {len(frame)} fragments -> {len(classified)} classified, "
-              f"{len(rec['filter']['rounds'])} reduction rounds, {time.time() - t0:.0f}s", flush=True)
+              f"{len(rec['filter']['rounds'])} reduction rounds, skeleton length "
+              f"{rec['skeleton']['jaccard']['seq_len']}, {time.time() - t0:.0f}s", flush=True)
         del dp
+    if "--probe-seed" in sys.argv:  # child run under another hash seed: skeletons only
+        import json
+        print("SKELETONS=" + json.dumps({tc: r["skeleton"] for tc, r in out.items()}))
+        return
+    # the same skeletons under another PYTHONHASHSEED?
+    import json
+    env = dict(os.environ, PYTHONHASHSEED="12345")
+    probe = subprocess.run([sys.executable, os.path.abspath(__file__), "--probe-seed"], env=env, check=True,
+                           capture_output=True, text=True).stdout
+    other = json.loads(probe.split("SKELETONS=", 1)[1])
+    for tc in out:
+        out[tc]["skeleton"]["seed_independent"] = other[tc] == json.loads(json.dumps(out[tc]["skeleton"]))
+        print(f"  {tc}: skeleton seed-independent: {out[tc]['skeleton']['seed_independent']}")
+    out["_meta"] = {"pythonhashseed": os.environ.get("PYTHONHASHSEED")}
     G.dump("callers.json.gz", out, gz=True)
 
 

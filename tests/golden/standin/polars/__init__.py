@@ -2,7 +2,9 @@
 hot-path modules (masses.py, mass_table.py, mass_explanation.py) touch at import
 time and in `DynamicProgrammingTable`, plus the frame plumbing of
 fragment_classification.classify_fragments (lit, struct.map_elements, concat,
-with_row_index, rename, drop, comparisons, str.contains).
+with_row_index, rename, drop, comparisons, str.contains), and of the reference's
+Predictor.filter_by_explanation and SkeletonBuilder._predict_skeleton
+(DataFrame.item, row/column assignment).
 
 TEST INFRASTRUCTURE ONLY.  polars is not installed in this image and there is no
 network.  This module is put on sys.path solely by tests/golden/make_golden.py
@@ -118,7 +120,9 @@ def concat(frames):
 
 
 class Series(list):
-    def __init__(self, x):
+    def __init__(self, x, values=None):
+        if isinstance(x, str):  # Series(name, values)
+            self.name, x = x, values
         if isinstance(x, DataFrame):
             x = x._d.iloc[:, 0].tolist()
         super().__init__(x)
@@ -217,6 +221,22 @@ class DataFrame:
 
     def __len__(self):
         return len(self._d)
+
+    def replace_column(self, index, series):
+        d = self._d.copy()
+        d[d.columns[index]] = list(series)
+        return DataFrame(d)
+
+    def __repr__(self):
+        return repr(self._d)
+
+    def item(self, row, column):
+        v = self._d.iloc[row][column]
+        return v.item() if hasattr(v, "item") else v
+
+    def __setitem__(self, key, value):
+        row, column = key
+        self._d.at[self._d.index[row], column] = value
 
 
 def read_csv(path, separator=","):

@@ -111,3 +111,12 @@ def test_classify_batch_equals_single(fake, callers):
         rec = callers[tc]
         groups.setdefault(tc, (C.make_dp(rec["ctx"]), [rec]))
     C.check_classify_batch(None, groups)
+
+
+@pytest.mark.parametrize("tc", SPECTRA)
+def test_fixpoint_vs_reference(fake, callers, tc):
+    """The batched fixpoint (pipeline.filter_fixpoint) reproduces the
+    reference's own filter_by_explanation round by round."""
+    rec = callers[tc]
+    dp = C.make_dp(rec["ctx"])
+    C.check_fixpoint(rec, dp)

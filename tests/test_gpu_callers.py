@@ -56,6 +56,17 @@ def test_per_side_and_calculate_explanations(engine, population, tc):
         assert C.rows_of_expl(dp, one) == (None if r[4] is None else sorted(tuple(x) for x in r[4]))
 
 
+@pytest.mark.parametrize("tc", SPECTRA)
+def test_fixpoint_vs_reference(engine, callers, tc):
+    """pipeline.filter_fixpoint on the HIP engine (k_pairs_alpha and
+    k_valid_alpha against every round's reduced alphabet) == the reference's
+    own filter_by_explanation: alphabets and kept fragments after every
+    round, the final explanation dict."""
+    rec = callers[tc]
+    dp = C.make_dp(rec["ctx"], engine=engine)
+    C.check_fixpoint(rec, dp)
+
+
 def test_classify_batch(engine, callers):
     groups = {tc: (C.make_dp(callers[tc]["ctx"], engine=engine), [callers[tc]]) for tc in ("test_01", "test_05")}
     C.check_classify_batch(None, groups)

@@ -31,39 +31,33 @@ def fullsize():
     return dp, wl
 
 
-def test_fullsize_is_valid_vs_oracle(fullsize):
-    dp, wl = fullsize
-    ms = [m.mass for m in dp.masses]
-    host = oracle.build_table(ms, max(ms) * 35, 32)
-    got = dp.device_table.is_valid(wl["a7_mass"], wl["a7_thr"], dp.tolerance, dp.precision)
-    want = oracle.is_valid_batch(host, 32, wl["a7_mass"], wl["a7_thr"], dp.tolerance, nthreads=16)
-    assert len(got) > 4_000_000
-    assert np.array_equal(got, want)
-
-
-def test_fullsize_explain_vs_oracle_and_properties(fullsize):
+@pytest.fixture(scope="module")
+def oracle_a8(fullsize):
+    """The C oracle's statuses / counts for all A8 queries (OpenMP), mapped
+    to the engine's status codes; computed once for the module."""
     from spectrseqtools_amd import _native
 
     dp, wl = fullsize
-    ms = np.array([m.mass for m in dp.masses], dtype=np.int64)
-    A = round(dp.seq.modification_rate * dp.seq.max_len)
-    masses, thr = wl["a8_mass"], wl["a8_thr"]
-    res = dp.device_table.explain(masses, thr, dp.tolerance, dp.precision, A)
-    assert res.n > 10_000_000
-    # statuses and counts: the C oracle (literal restatement), all queries
-    host = oracle.build_table(list(ms), int(ms.max()) * 35, 32)
-    alph = oracle.Alphabet(list(ms), [m.is_modification for m in dp.masses],
+    ms = [m.mass for m in dp.masses]
+    host = oracle.build_table(ms, max(ms) * 35, 32)
+    alph = oracle.Alphabet(ms, [m.is_modification for m in dp.masses],
                            [round(dp.seq.max_len * m.modification_rate) for m in dp.masses])
-    ost, ocnt, _ = oracle.explain_batch(host, 32, alph, masses, thr, A, dp.tolerance, nthreads=16)
+    A = round(dp.seq.modification_rate * dp.seq.max_len)
+    ost, ocnt, _ = oracle.explain_batch(host, 32, alph, wl["a8_mass"], wl["a8_thr"], A, dp.tolerance, nthreads=16)
     want = np.where(ost < 0, _native.SST_OUT_OF_TABLE,
                     np.where(ost == 0, _native.SST_NONE, np.where(ocnt > 0, _native.SST_SOME, _native.SST_EMPTY)))
-    assert np.array_equal(res.status.astype(np.int64), want)
+    return host, alph, want, ocnt
+
+
+def _check_candidates(res, masses, thr, ms, prec):
+    """Every candidate of every SOME query: rows ascending, sum inside the
+    quantised window, distinct within its query, and in the reference's order
+    (ascending sum, then top row)."""
+    from spectrseqtools_amd import _native
+
     some = res.status == _native.SST_SOME
-    assert np.array_equal(res.count[some].astype(np.int64), ocnt[some])
-    # every candidate: rows ascending, sum inside the quantised window, distinct
-    # within its query, and in the reference's order (ascending sum, then row)
-    target = np.rint(masses / dp.precision)
-    th = np.ceil(thr / dp.precision)
+    target = np.rint(masses / prec)
+    th = np.ceil(thr / prec)
     lo, hi = (target - th)[some], (target + th)[some]
     pos = res.offset[some].astype(np.int64)
     cnt = res.count[some].astype(np.int64)
@@ -87,7 +81,34 @@ def test_fullsize_explain_vs_oracle_and_properties(fullsize):
         pos[act] = p + 1 + k
 
 
-def test_fullsize_device_path_reused_vs_oracle(fullsize):
+def test_fullsize_is_valid_vs_oracle(fullsize):
+    dp, wl = fullsize
+    ms = [m.mass for m in dp.masses]
+    host = oracle.build_table(ms, max(ms) * 35, 32)
+    got = dp.device_table.is_valid(wl["a7_mass"], wl["a7_thr"], dp.tolerance, dp.precision)
+    want = oracle.is_valid_batch(host, 32, wl["a7_mass"], wl["a7_thr"], dp.tolerance, nthreads=16)
+    assert len(got) > 4_000_000
+    assert np.array_equal(got, want)
+
+
+def test_fullsize_explain_vs_oracle_and_properties(fullsize, oracle_a8):
+    from spectrseqtools_amd import _native
+
+    dp, wl = fullsize
+    host, alph, want, ocnt = oracle_a8
+    ms = np.array([m.mass for m in dp.masses], dtype=np.int64)
+    A = round(dp.seq.modification_rate * dp.seq.max_len)
+    masses, thr = wl["a8_mass"], wl["a8_thr"]
+    res = dp.device_table.explain(masses, thr, dp.tolerance, dp.precision, A)
+    assert res.n > 10_000_000
+    # statuses and counts: the C oracle (literal restatement), all queries
+    assert np.array_equal(res.status.astype(np.int64), want)
+    some = res.status == _native.SST_SOME
+    assert np.array_equal(res.count[some].astype(np.int64), ocnt[some])
+    _check_candidates(res, masses, thr, ms, dp.precision)
+
+
+def test_fullsize_device_path_reused_vs_oracle(fullsize, oracle_a8):
     """The path bench.py times, at its full size: explain_device on HBM inputs
     into one result object reused over two passes (the pass packs its own
     dense result; the host settles it by polling the header), then fetched.
@@ -120,12 +141,7 @@ def test_fullsize_device_path_reused_vs_oracle(fullsize):
         assert len(res.payload) == n_bytes
         digests.append((res.status.tobytes(), recs.tobytes(), res.payload.tobytes()))
     assert digests[0] == digests[1]
-    host = oracle.build_table(list(ms), int(ms.max()) * 35, 32)
-    alph = oracle.Alphabet(list(ms), [m.is_modification for m in dp.masses],
-                           [round(dp.seq.max_len * m.modification_rate) for m in dp.masses])
-    ost, ocnt, _ = oracle.explain_batch(host, 32, alph, masses, thr, A, dp.tolerance, nthreads=16)
-    want = np.where(ost < 0, _native.SST_OUT_OF_TABLE,
-                    np.where(ost == 0, _native.SST_NONE, np.where(ocnt > 0, _native.SST_SOME, _native.SST_EMPTY)))
+    host, alph, want, ocnt = oracle_a8
     assert np.array_equal(res.status.astype(np.int64), want)
     some = res.status == _native.SST_SOME
     assert np.array_equal(res.count[some].astype(np.int64), ocnt[some])
@@ -149,3 +165,80 @@ def test_fullsize_device_path_reused_vs_oracle(fullsize):
     total = ms[r0] + np.where(k >= 2, ms[r1], 0)
     assert ((k >= 1) & (k <= 2)).all()
     assert ((total >= target[qs] - th[qs]) & (total <= target[qs] + th[qs])).all()
+
+
+def test_fullsize_step_device_vs_oracle(fullsize, oracle_a8):
+    """The exact launch bench.py times: sst_step_device --
+    k_step, one scan workgroup per CU, ~41 tile rounds per scan wave, the
+    is_valid workgroups beside it -- on the full config-3 workload, twice into
+    one reused result.  Against the oracle: the A7 byte of every (peak x
+    breakage) pair, every A8 status and count, the exact candidate lists of a
+    sample, the candidates' properties for all queries, the dense hit list and
+    the wire-v5 decode of the pass (scan order, pair refs)."""
+    torch = pytest.importorskip("torch")
+    from spectrseqtools_amd import _native
+    from spectrseqtools_amd.parallel import canonical_digest, decode_hits, device_bytes, scan_order_key, wire_unpack
+
+    dp, wl = fullsize
+    host, alph, want, ocnt = oracle_a8
+    ms = np.array([m.mass for m in dp.masses], dtype=np.int64)
+    A = round(dp.seq.modification_rate * dp.seq.max_len)
+    masses, thr = wl["a8_mass"], wl["a8_thr"]
+    n, P = len(masses), len(wl["obs"])
+    dev = torch.device("cuda", 0)
+    dm, dt, do = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (masses, thr, wl["obs"]))
+    out7 = torch.full((4 * P,), 9, dtype=torch.int8, device=dev)
+    torch.cuda.synchronize()
+    tdev = dp.device_table
+    res, digests = None, []
+    for _ in range(2):
+        out7.fill_(9)
+        torch.cuda.synchronize()
+        res = tdev.step_device(do.data_ptr(), P, wl["shifts"], out7.data_ptr(), dm.data_ptr(), dt.data_ptr(), n,
+                               dp.tolerance, dp.precision, A, reuse=res)
+        n_hits, n_bytes = res.settle()
+        ptr, nh = res.hit_list_device()
+        assert nh == n_hits
+        recs = device_bytes(ptr, 16 * nh, dev).cpu().numpy().view(np.uint32).reshape(-1, 4)
+        res.fetch_device()
+        digests.append((res.status.tobytes(), recs.tobytes(), res.payload.tobytes()))
+    assert digests[0] == digests[1]
+    # the timed grid: one scan workgroup per CU, many tile rounds per wave
+    refs_p, n_pair, pair_bytes, n_wg = res.pair_hits_device()
+    assert n_wg >= 64 and -(-((n + 63) // 64) // (16 * n_wg)) >= 8, n_wg
+    # A7: every (breakage, peak) byte against the oracle
+    engine_sync = _native.get_engine(0)
+    engine_sync.synchronize()
+    a7 = out7.cpu().numpy()
+    assert len(a7) == len(wl["a7_mass"]) > 4_000_000
+    assert np.array_equal(a7, oracle.is_valid_batch(host, 32, wl["a7_mass"], wl["a7_thr"], dp.tolerance, nthreads=16))
+    # A8: all statuses and counts
+    assert np.array_equal(res.status.astype(np.int64), want)
+    some = res.status == _native.SST_SOME
+    assert np.array_equal(res.count[some].astype(np.int64), ocnt[some])
+    _check_candidates(res, masses, thr, ms, dp.precision)
+    # exact candidate lists (reference order) of a sample of the hits
+    rng = np.random.default_rng(31)
+    for i in rng.choice(np.flatnonzero(some), 3000, replace=False):
+        st, sols, _, _ = oracle.explain_table(host, 32, alph, masses[i], thr[i], dp.tolerance, A)
+        assert res.candidates(int(i)) == sols, i
+    # the dense hit list: pair-path hits first, in the scan's order
+    q = recs[:, 0].astype(np.int64)
+    assert len(q) == int(np.isin(res.status, (_native.SST_SOME, _native.SST_OVERFLOW)).sum())
+    assert len(np.unique(q)) == len(q)
+    assert np.array_equal(recs[:, 1].astype(np.int64), res.count[q].astype(np.int64))
+    off = recs[:, 2].astype(np.int64) | (recs[:, 3].astype(np.int64) << 32)
+    assert np.array_equal(off[some[q]], res.offset[q][some[q]].astype(np.int64))
+    assert 0 < n_pair <= len(q)
+    assert (np.diff(scan_order_key(q[:n_pair], n, n_wg)) > 0).all()
+    # wire v5 of this pass decodes to the same result
+    precs = tdev.pair_records()
+    fixed = res.wire_pack(out7.data_ptr(), 4 * P)
+    wbuf = torch.zeros(fixed + 8 * (4 * P + n + n_pair), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    res.wire_pack(out7.data_ptr(), 4 * P, wbuf.data_ptr(), wbuf.numel())
+    engine_sync.synchronize()
+    v_, st_, hits_, pay_ = wire_unpack(wbuf.cpu().numpy(), precs)
+    cnt_, off_ = decode_hits(st_, hits_)
+    assert np.array_equal(v_, a7) and np.array_equal(st_, res.status)
+    assert canonical_digest(st_, cnt_, off_, pay_) == canonical_digest(res.status, res.count, res.offset, res.payload)

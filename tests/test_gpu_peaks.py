@@ -42,3 +42,23 @@ def test_is_valid_peaks_vs_expanded_and_oracle(rows):
             assert int(got[i]) == oracle.is_valid(host, 32, su[i], thr[i], TOL), i
         assert (got == -1).any() and (got == 1).any() and (got == 0).any()
     dev.close()
+
+
+def test_is_valid_peaks_many_shifts(rows):
+    """More than 4 breakage weights (the reference's FULL_BREAKAGE_DICT gives
+    up to 16): launched four weights at a time, equal to the expanded
+    per-query batch and the oracle."""
+    eng = _native.get_engine(0)
+    dev = _native.DeviceTable.build(rows, max(rows) * 35, 32, engine=eng)
+    host = oracle.build_table(rows, max(rows) * 35, 32)
+    rng = np.random.default_rng(22)
+    obs = rng.uniform(300, 9000, 5000)
+    for n_w in (5, 7, 16, 64):
+        shifts = np.sort(rng.uniform(0.0, 1500.0, n_w))
+        got = dev.is_valid_peaks(obs, shifts, TOL, PREC)
+        su = np.concatenate([obs - s for s in shifts])
+        thr = TOL * np.tile(obs, n_w)
+        assert np.array_equal(got, dev.is_valid(su, thr, TOL, PREC)), n_w
+        for i in rng.integers(0, len(su), 500):
+            assert int(got[i]) == oracle.is_valid(host, 32, su[i], thr[i], TOL), (n_w, i)
+    dev.close()

@@ -169,7 +169,7 @@ def test_hit_list_matches_result_arrays(engine, dev, rows):
 
 def test_wire_pair_hits_roundtrip(engine, dev, rows):
     """sst_result_pair_hits + sst_wire_pack / parallel.wire_unpack (the N>1
-    gather's wire format v4) on a real device pass: the pair-path hits come
+    gather's wire format v5) on a real device pass: the pair-path hits come
     in the documented scan order (several tile rounds per wave), their refs
     name the pair-list entries of their candidates (SOME and OVERFLOW), the
     device packer writes the bytes of the numpy statement (wire_pack_host;
@@ -314,3 +314,47 @@ def test_empty_batches(engine, dev, rows):
     _same(s1, dev.explain(masses, thr, TOL, PREC, 10), 1000)
     ptr, nh = s1.hit_list_device()
     assert nh == int(np.isin(s1.status, (_native.SST_SOME, _native.SST_OVERFLOW)).sum())
+
+
+def test_reuse_across_empty_pass_with_lookback(engine, dev, rows):
+    """A result reused big -> empty -> a different big batch, with enough
+    queries for several scan workgroups (the fused scan's decoupled look-back
+    runs): after the empty pass the next pass's dense result, pair-path part
+    and wire pack equal a fresh result's (an empty pass must zero the
+    look-back aggregates and the scan header the next pass reads)."""
+    torch = pytest.importorskip("torch")
+    from spectrseqtools_amd.parallel import canonical_digest, decode_hits, wire_unpack
+
+    rng = np.random.default_rng(18)
+    n = 150_000
+    batches = [_queries(rng, rows, n, 2), _queries(rng, rows, n, 2, thr_hi=9000)]
+    dev_t = torch.device("cuda", engine.device)
+    dd = [tuple(torch.from_numpy(np.ascontiguousarray(x)).to(dev_t) for x in b) for b in batches]
+    valid = np.zeros(16, np.int8)
+    dv = torch.from_numpy(valid).to(dev_t)
+    torch.cuda.synchronize()
+    recs = dev.pair_records()
+    res = None
+    for b, nn in ((0, n), (0, 0), (1, n), (1, 0), (0, n), (1, n)):
+        dm, dt = dd[b]
+        res = dev.explain_device(dm.data_ptr(), dt.data_ptr(), nn, TOL, PREC, 10, reuse=res)
+        res.fetch_device()
+        if nn == 0:
+            assert res.settle() == (0, 0)
+            continue
+        fresh = dev.explain_device(dm.data_ptr(), dt.data_ptr(), nn, TOL, PREC, 10)
+        fresh.fetch_device()
+        _, n_pair, pair_bytes, n_wg = res.pair_hits_device()
+        assert n_wg > 1 and (n_pair, pair_bytes) == fresh.pair_hits_device()[1:3]
+        assert res.settle() == fresh.settle()
+        assert canonical_digest(res.status, res.count, res.offset, res.payload) == \
+            canonical_digest(fresh.status, fresh.count, fresh.offset, fresh.payload)
+        fixed = res.wire_pack(dv.data_ptr(), len(valid))
+        wbuf = torch.zeros(fixed + 8 * (len(valid) + nn + n_pair), dtype=torch.uint8, device=dev_t)
+        torch.cuda.synchronize()
+        res.wire_pack(dv.data_ptr(), len(valid), wbuf.data_ptr(), wbuf.numel())
+        engine.synchronize()
+        v_, st_, hits_, pay_ = wire_unpack(wbuf.cpu().numpy(), recs)
+        cnt_, off_ = decode_hits(st_, hits_)
+        assert canonical_digest(st_, cnt_, off_, pay_) == \
+            canonical_digest(fresh.status, fresh.count, fresh.offset, fresh.payload)
