@@ -61,27 +61,41 @@ def result_digest(r):
 
 
 def build_workload(n_spectra, seed, dp):
-    """SURVEY 8(d) config 3's queries for `n_spectra` synthetic spectra: A7 on
-    every peak x breakage weight (classify_fragments' form); A8 on every
-    sliding-window pair of each spectrum's START and END side after the
-    is_valid and sequence-mass filters (the first filter_by_explanation
-    round without singletons), produced by the library's host-native
-    sliding window (sst_su_diff_queries)."""
+    """SURVEY 8(d) config 3's queries for `n_spectra` synthetic spectra (see
+    workload_from)."""
+    from spectrseqtools_amd.synthetic import make_spectra
+
+    batch = make_spectra(n_spectra, seed=seed)
+    # a peak list comes sorted by mass (the rows step merges the breakages'
+    # sorted streams); fragment_index = the position in this list
+    obs = batch.observed[np.lexsort((batch.observed, batch.spectrum))]
+    return workload_from(obs, batch.offsets, batch.seq_mass, dp)
+
+
+def workload_from(obs, offsets, seq_mass, dp, intensity=None, intensity_cutoff=0.5e6, mass_cutoff=50000.0):
+    """A7 on every peak x breakage weight (classify_fragments' form); A8 on
+    every sliding-window pair of each spectrum's START and END side after the
+    is_valid, intensity / mass and sequence-mass filters (the first
+    filter_by_explanation round without singletons), produced on the host by
+    the library's host-native sliding window (sst_su_diff_queries).  The
+    peaks of a spectrum must be sorted by mass."""
     from spectrseqtools_amd._native import su_diff_queries
     from spectrseqtools_amd.masses import build_breakage_dict
     from spectrseqtools_amd.producers import MAX_VARIANCE, classify_queries, max_nucleotide_weight
-    from spectrseqtools_amd.synthetic import make_spectra
 
     tol, prec = dp.tolerance, dp.precision
-    batch = make_spectra(n_spectra, seed=seed)
+    obs = np.ascontiguousarray(obs, dtype=np.float64)
+    offsets = np.asarray(offsets, dtype=np.int64)
+    n_spectra = len(offsets) - 1
+    spectrum = np.repeat(np.arange(n_spectra), np.diff(offsets))
     brk = build_breakage_dict(555.1294, 455.1491)
-    cq = classify_queries(batch.observed, brk, prec, tol)
+    cq = classify_queries(obs, brk, prec, tol)
     valid = dp.device_table.is_valid(cq.su_mass, cq.threshold, tol, prec)  # setup pass: selects the window inputs
     if (valid < 0).any():
         raise RuntimeError("synthetic peak outside the DP table")
     n_brk = len(brk)
-    P = len(batch.observed)
-    spec = np.tile(batch.spectrum, n_brk)
+    P = len(obs)
+    spec = np.tile(spectrum, n_brk)
     names = [v[0] for v in brk.values()]
     code = np.repeat(np.arange(n_brk), P)
     is_start = np.array(["START" in n for n in names])[code]
@@ -89,21 +103,30 @@ def build_workload(n_spectra, seed, dp):
     se_w = [k for k, v in brk.items() if "START_END" in v][0]
     # per spectrum by SU mass, ties in breakage-major order (classify_fragments' sort)
     order = np.lexsort((cq.su_mass, spec))
-    order = order[(valid == 1)[order]]
-    su, ob, sp = cq.su_mass[order], cq.observed[order], spec[order]
+    inten = np.ones(P, bool) if intensity is None else np.asarray(intensity) > intensity_cutoff
+    keep = (valid == 1) & np.tile(inten & (obs < mass_cutoff), n_brk)
+    order = order[keep[order]]
+    su, sp = cq.su_mass[order], spec[order]
     # filter_by_sequence_mass (fragment_classification.py:122-139)
-    su_seq = (batch.seq_mass - se_w * prec)[sp]
+    su_seq = (np.asarray(seq_mass) - se_w * prec)[sp]
     full = is_start[order] & is_end[order]
     ok = (su < su_seq + MAX_VARIANCE) & ((su > su_seq - MAX_VARIANCE) | ~full)
     rows = order[ok]
     flags = (is_start[rows].astype(np.uint8) | (is_end[rows].astype(np.uint8) << 1))
-    offsets = np.searchsorted(spec[rows], np.arange(n_spectra + 1))
-    diffs, dthr, _, _ = su_diff_queries(cq.su_mass[rows], cq.observed[rows], flags, offsets,
+    offs = np.searchsorted(spec[rows], np.arange(n_spectra + 1))
+    diffs, dthr, _, _ = su_diff_queries(cq.su_mass[rows], cq.observed[rows], flags, offs,
                                         max_nucleotide_weight(), tol)
     return {
         "peaks": P, "a7_mass": cq.su_mass, "a7_thr": cq.threshold, "a8_mass": diffs, "a8_thr": dthr,
-        "spectra": n_spectra, "a7_valid": valid, "obs": np.ascontiguousarray(batch.observed, dtype=np.float64),
+        "spectra": n_spectra, "a7_valid": valid, "obs": obs,
         "shifts": np.array([w * prec for w in brk], dtype=np.float64),  # classify_fragments' su = obs - w * prec
+        # the rows step's inputs: peak ranges per spectrum, SU sequence masses,
+        # each breakage's sides (bit 0 START, bit 1 END)
+        "peak_off": np.ascontiguousarray(offsets, dtype=np.int64),
+        "su_seq": np.ascontiguousarray(np.asarray(seq_mass) - se_w * prec, dtype=np.float64),
+        "sides": np.array([("START" in v[0]) | (("END" in v[0]) << 1) for v in brk.values()], dtype=np.uint8),
+        "max_weight": max_nucleotide_weight(),
+        "side_rows": int((flags & 1).astype(bool).sum() + (flags & 2).astype(bool).sum()),
     }
 
 
@@ -187,6 +210,11 @@ def main():
     ap.add_argument("--dump-gathered", default=None,
                     help="test hook (tests/test_gpu_multirank.py): write the last step's gathered wire buffers "
                          "(rank 0) and every rank's inputs of that step into this directory")
+    ap.add_argument("--a8-source", default="rows", choices=("rows", "queries"),
+                    help="rows (default): each step starts from the peaks -- A7, the classification filters, the "
+                         "per-side SU order and the sliding window's pairs on the device (sst_step_rows_device); "
+                         "queries: the A8 (mass, threshold) pairs are produced on the host before timing "
+                         "(sst_step_device, round 2's line)")
     ap.add_argument("--no-validate", action="store_true",
                     help="diagnostic builds only: skip the result checks after the timed region")
     ap.add_argument("--no-events", action="store_true",
@@ -240,12 +268,19 @@ def main():
     wl = wls[0]
     n7s = [len(w["a7_mass"]) for w in wls]
     n8s = [len(w["a8_mass"]) for w in wls]
+    rows_mode = args.a8_source == "rows"
+    if rows_mode:
+        args.fused_step = 1
     dev_in = []
     for w in wls:
-        dev_in.append({"obs": torch.from_numpy(w["obs"]).to(dev_t),
-                       "a8m": torch.from_numpy(w["a8_mass"]).to(dev_t),
-                       "a8t": torch.from_numpy(w["a8_thr"]).to(dev_t), "P": len(w["obs"]), "shifts": w["shifts"],
-                       "n7": len(w["a7_mass"]), "n8": len(w["a8_mass"])})
+        d = {"obs": torch.from_numpy(w["obs"]).to(dev_t), "P": len(w["obs"]), "shifts": w["shifts"],
+             "n7": len(w["a7_mass"]), "n8": len(w["a8_mass"])}
+        if rows_mode:
+            d.update(poff=torch.from_numpy(w["peak_off"]).to(dev_t), su_seq=torch.from_numpy(w["su_seq"]).to(dev_t))
+        else:
+            d.update(a8m=torch.from_numpy(w["a8_mass"]).to(dev_t), a8t=torch.from_numpy(w["a8_thr"]).to(dev_t))
+        dev_in.append(d)
+    cap8 = int(max(n8s) * 1.05) + 1024  # the rows step's query capacity
     # two result sets used in turn: while step k runs on the GPU, the host
     # settles step k-1 (waits for its pass, reads its header, runs any routed
     # deferred windows or retries) -- the pipelined consumer loop of a serving
@@ -311,6 +346,11 @@ def main():
 
     def launch(b, out7, reuse):
         d = dev_in[b]
+        if rows_mode:  # everything from the peaks on the device (sst_step_rows_device)
+            w = wls[b]
+            return tdev.step_rows_device(d["obs"].data_ptr(), d["poff"].data_ptr(), len(w["peak_off"]) - 1, d["P"],
+                                         d["su_seq"].data_ptr(), d["shifts"], w["sides"], out7.data_ptr(),
+                                         w["max_weight"], dp.tolerance, dp.precision, A, cap8, reuse=reuse)
         if args.fused_step:  # A7 and A8 in one launch (sst_step_device)
             return tdev.step_device(d["obs"].data_ptr(), d["P"], d["shifts"], out7.data_ptr(), d["a8m"].data_ptr(),
                                     d["a8t"].data_ptr(), d["n8"], dp.tolerance, dp.precision, A, reuse=reuse)
@@ -363,6 +403,22 @@ def main():
         if not a7_ok:
             raise RuntimeError(f"batch {b}: is_valid bytes differ from the setup pass")
         expect[b] = rr.settle()
+        if rows_mode:
+            # the device producers must issue exactly the host producers' queries:
+            # the same answers as the explain pass over the host-built (mass,
+            # threshold) pairs (which tests/test_gpu_fullsize.py checks against the oracle)
+            if rr.n != n8s[b]:
+                raise RuntimeError(f"batch {b}: the rows step issued {rr.n} queries, the host producers {n8s[b]}")
+            dm_ = torch.from_numpy(wls[b]["a8_mass"]).to(dev_t)
+            dt_ = torch.from_numpy(wls[b]["a8_thr"]).to(dev_t)
+            torch.cuda.synchronize()
+            hq = tdev.explain_device(dm_.data_ptr(), dt_.data_ptr(), n8s[b], dp.tolerance, dp.precision, A)
+            hq.fetch_device()
+            if canonical_digest(hq.status, hq.count, hq.offset, hq.payload) != \
+                    canonical_digest(rr.status, rr.count, rr.offset, rr.payload):
+                raise RuntimeError(f"batch {b}: the rows step's answers differ from the host-produced queries'")
+            hq.close()
+            del dm_, dt_
         refs.append({"digest": result_digest(rr), "stats": rr.stats(), "status": rr.status.copy(),
                      "canon": canonical_digest(rr.status, rr.count, rr.offset, rr.payload) if gath is not None
                      else None, "n_hits": expect[b][0],
@@ -530,7 +586,16 @@ def main():
             "k_explain_expand": float(n_work * (16 + 17) + 16 * nodes + int(stats[5])),
         }
         l2 = {"k_is_valid": float(bits7), "k_explain_scan": float(bits8)}
-        if args.fused_step:  # the scan's launch also ran A7 (k_step): its bytes are both predicates'
+        if rows_mode:
+            # the step from the peaks: each peak (8) read once, its A7 codes and
+            # bitset words, every side row written to scratch and read back
+            # (16 + 16), then per query its status byte and per hit the dense
+            # record (16), the pair-list ref (2) and the candidate bytes; the
+            # queries themselves never touch HBM
+            bk["k_explain_scan"] = float(8 * P + n7 + bits7 + 32 * w_["side_rows"] + n8 +
+                                         18 * rf["n_hits"] + cand_bytes)
+            l2["k_explain_scan"] = float(bits7)
+        elif args.fused_step:  # the scan's launch also ran A7 (k_step): its bytes are both predicates'
             bk["k_explain_scan"] += bk["k_is_valid"]
             l2["k_explain_scan"] += l2["k_is_valid"]
         # SURVEY 8(d)'s literal per-query model: 16 B in + 8 B per window word
@@ -556,7 +621,8 @@ def main():
     achieved = dbytes / (dus * 1e-6) / 1e9
     hbm_only = (dbytes - l2_k.get(dom, 0.0)) / (dus * 1e-6) / 1e9
     traffic, traffic_src = None, None
-    tkey = ("k_step" if args.fused_step and dom == "k_explain_scan" else dom) + (f"_rot{R}" if R > 1 else "")
+    tkey = ("k_rows" if rows_mode else "k_step" if args.fused_step and dom == "k_explain_scan" else dom) + \
+        (f"_rot{R}" if R > 1 else "")
     if args.spectra == 10000 and args.seed == 1000:  # the workload the PMC passes in profiles/ measured
         try:
             with open(args.traffic_json) as f:
@@ -598,6 +664,9 @@ def main():
         "config": {
             "workload": "config3: synthetic spectra (SURVEY 8(d)), full 104-mass/105-row alphabet, <=20-mer, "
                         "A7 (4 breakages/peak) + A8 (sliding-window differences) per step",
+            "a8_source": ("rows: A7, classification filters, per-side SU order and sliding-window pairs formed on "
+                          "the device from the peaks inside each step (sst_step_rows_device)" if rows_mode else
+                          "queries: A8 (mass, threshold) pairs produced on the host before timing"),
             "spectra_per_gpu": args.spectra,
             "batches": (f"{R} distinct batches of {args.spectra} spectra (seeds {args.seed} + 7919 b), cycled "
                         f"step by step, {sum(w['obs'].nbytes + w['a8_mass'].nbytes + w['a8_thr'].nbytes for w in wls) / 1e6:.0f} MB "
@@ -618,7 +687,8 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("k_step (k_is_valid_peaks + k_explain_scan in one launch)" if args.fused_step and
+            "kernel": ("k_rows_count + k_rows_scan + k_rows_emit (the step from the peaks)" if rows_mode else
+                       "k_step (k_is_valid_peaks + k_explain_scan in one launch)" if args.fused_step and
                        dom == "k_explain_scan" else dom),
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
@@ -645,7 +715,8 @@ def main():
                          "nomemo": int(stats[3]), "index_loads": int(stats[4]),
                          "candidates": int(res.count[some].sum()), "payload_bytes": int(stats[5] + stats[7]),
                          "hits": n_hits0, "dense_payload_bytes": int(len(res.payload))},
-        "step": ("k_is_valid + k_explain_scan (packing its own dense result)" if fused else
+        "step": ("k_rows_count + k_rows_scan + k_rows_emit (from the peaks)" if rows_mode else
+                 "k_is_valid + k_explain_scan (packing its own dense result)" if fused else
                  "k_is_valid + k_explain_scan + k_result_pack") +
                 " per step: status bytes, dense hit list and dense payload of every query (the complete "
                 "result); the host settles step k-1 while step k runs",

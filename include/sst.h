@@ -187,6 +187,33 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
                                 double tolerance, double precision, const int64_t* max_mods, int64_t max_mods_scalar,
                                 uint64_t cap_per_query, sst_result** out);
 
+/* The step from the peaks: classify_fragments' is_valid and filters
+ * (fragment_classification.py:17-101: A7 of every peak x breakage weight into
+ * d_valid_out as sst_is_valid_peaks_device, the intensity / mass cuts and
+ * filter_by_sequence_mass against d_su_seq[spectrum]) and the first
+ * filter_by_explanation round's sliding-window explains of both sides
+ * (prediction.py:261-329; no singletons), every producer on the device:
+ * per spectrum the kept rows of each side in SU order (a merge of the
+ * breakages' sorted streams), the window pairs in closed form and each pair's
+ * difference and threshold formed in the kernels.  Spectrum g's peaks are
+ * d_obs[d_peak_off[g] .. d_peak_off[g+1]) in ascending mass order (at most
+ * 1024); sides[k]: bit 0 = breakage k's rows are on the START side, bit 1 = on
+ * the END side (both: the sequence-mass lower cut applies); d_intensity may
+ * be NULL (every peak passes).  The result holds the explain answers in query
+ * order (spectrum-major; START pairs then END pairs; the order
+ * collect_diff_explanations_for_su issues them) and the number of queries
+ * (sst_result_queries; at most max_queries); its hits all come from the pair
+ * list (sst_result_pair_hits, n_scan_wg = 0: query order).  Every window must
+ * be pair-class with budgets that cannot bind (checked: SST_E_ARG otherwise).
+ * No reference equivalent (the reference issues these one row at a time). */
+int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_peak_off, int64_t n_spec,
+                         int64_t n_peaks, const double* d_intensity, double intensity_cutoff, double mass_cutoff,
+                         const double* d_su_seq, const double* shifts, const uint8_t* sides, int n_shifts,
+                         double max_weight, double tolerance, double precision, int64_t max_mods_scalar,
+                         uint64_t cap_per_query, int64_t max_queries, int8_t* d_valid_out, sst_result** out);
+/* Number of explain queries of a result (settles it first). */
+int sst_result_queries(sst_result* r, int64_t* n);
+
 /* Wait for a result's pass and complete it (see sst_explain_batch_device);
  * reports the dense hit list's length and the dense payload's size.  Other
  * work queued on the ctx stream after the pass keeps running.  No reference
@@ -368,6 +395,46 @@ int64_t sst_window_pairs(const double* su, const int64_t* offsets, int64_t n_sid
 int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* flags, const int64_t* offsets,
                             int64_t n_spec, double max_weight, double tolerance, double* diff, double* thr,
                             int64_t* spec, int8_t* kind, int64_t cap);
+/* ---- config 5 on the device ---------------------------------------------
+ * classify_fragments and the filter_by_explanation fixpoint over many spectra
+ * with every array in HBM.  Rows of spectrum g live in slots
+ * 4 * d_peak_off[g] + i, i < d_rows[g] (d_rows_* arrays of 4 * n_peaks):
+ * su, observed mass, meta = breakage | sides << 2 | is_singleton << 4 | peak
+ * position << 8, alive.  Peaks in ascending mass order, <= 512 per spectrum;
+ * shifts / sides as sst_step_rows_device.  d_err collects | 1 a spectrum over
+ * 512 peaks, 2 over 2048 rows, 4 a window outside the pair class, 8 a window
+ * past a table's end (the reference raises), 16 a dict too large for the LDS
+ * hash, 32 rows out of mass order; the caller checks it. */
+/* classify_fragments (fragment_classification.py:17-101): A7 into d_valid_out
+ * (may be NULL), the filters, is_singleton against t's masses, SU order. */
+int sst_classify_rows_device(sst_table* t, const double* d_obs, const int64_t* d_peak_off, int64_t n_spec,
+                             int64_t n_peaks, const double* d_intensity, double intensity_cutoff, double mass_cutoff,
+                             const double* d_su_seq, const double* shifts, const uint8_t* sides, int n_shifts,
+                             double max_weight, double tolerance, double precision, int8_t* d_valid_out,
+                             double* d_rows_su, double* d_rows_ob, uint32_t* d_rows_meta, uint8_t* d_alive,
+                             uint32_t* d_rows, uint32_t* d_err);
+/* One filter_by_explanation round (prediction.py:170-202) of the spectra with
+ * d_active[g]: their alive rows' window pairs and singletons explained
+ * against d_alpha[2g..2g+1] (row masks of t; the caller keeps budgets from
+ * binding, see sst_explain_pairs_alpha), the explanation dict's surviving
+ * entries, d_alpha_next = the canonical rows | (alphabet & observed rows),
+ * d_active_next[g] = the alphabet shrank (d_n_active counts those);
+ * d_rounds[g] += 1, d_queries[g] += the round's explain queries.  Settled
+ * spectra carry their alphabet over. */
+int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                         const double* d_rows_ob, const uint32_t* d_rows_meta, uint8_t* d_alive,
+                         const uint32_t* d_rows, const uint64_t* d_alpha, uint64_t* d_alpha_next,
+                         const uint8_t* d_active, uint8_t* d_active_next, uint32_t* d_rounds, uint32_t* d_queries,
+                         uint32_t* d_n_active, double max_weight, double tolerance, double precision,
+                         uint32_t* d_err);
+/* _reduce_alphabet's filter (prediction.py:211-227): is_valid_mass of the
+ * alive rows of the d_active spectra against their reduced tables (d_alpha),
+ * AND-ed into d_alive. */
+int sst_valid_rows_alpha_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                                const double* d_rows_ob, const uint32_t* d_rows, const uint64_t* d_alpha,
+                                const uint8_t* d_active, uint8_t* d_alive, double tolerance, double precision,
+                                uint32_t* d_err);
+
 /* The explanation dict collect_diff_explanations_for_su builds per spectrum
  * (prediction.py:261-284): spectrum g's queries [offsets[g], offsets[g+1])
  * in its order (START pairs, END pairs, singletons) with kind 0 / 1 / 2, their

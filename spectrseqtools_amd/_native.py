@@ -30,7 +30,8 @@ EXPORTS = (
     "sst_window_pairs", "sst_is_valid_peaks", "sst_is_valid_peaks_device", "sst_result_pair_hits",
     "sst_table_pair_records", "sst_su_diff_queries", "sst_sort_rows", "sst_step_device",
     "sst_wire_pack", "sst_explain_pairs_alpha", "sst_explain_pairs_alpha_device", "sst_is_valid_alpha",
-    "sst_is_valid_alpha_device", "sst_dict_union",
+    "sst_is_valid_alpha_device", "sst_dict_union", "sst_step_rows_device", "sst_result_queries",
+    "sst_classify_rows_device", "sst_fix_round_device", "sst_valid_rows_alpha_device",
 )
 
 # kernel ids of sst_profile_read
@@ -145,6 +146,18 @@ def load_library(path=LIB_PATH):
     lib.sst_is_valid_alpha_device.restype = _I
     lib.sst_dict_union.argtypes = [_P, _I64, _P, _P, _P, _P, _P, _P]
     lib.sst_dict_union.restype = _I64
+    lib.sst_step_rows_device.argtypes = [_P, _P, _P, _I64, _I64, _P, _D, _D, _P, _P, _P, _I, _D, _D, _D, _I64, _U64,
+                                         _I64, _P, _PP]
+    lib.sst_step_rows_device.restype = _I
+    lib.sst_result_queries.argtypes = [_P, ctypes.POINTER(_I64)]
+    lib.sst_result_queries.restype = _I
+    lib.sst_classify_rows_device.argtypes = [_P, _P, _P, _I64, _I64, _P, _D, _D, _P, _P, _P, _I, _D, _D, _D, _P, _P,
+                                             _P, _P, _P, _P, _P]
+    lib.sst_classify_rows_device.restype = _I
+    lib.sst_fix_round_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _D, _D, _D, _P]
+    lib.sst_fix_round_device.restype = _I
+    lib.sst_valid_rows_alpha_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _P]
+    lib.sst_valid_rows_alpha_device.restype = _I
     return lib
 
 
@@ -353,7 +366,7 @@ class ExplainResult:
         nb = _U64()
         self.engine.check(L.sst_result_host(self.handle, ctypes.byref(st), ctypes.byref(cnt), ctypes.byref(off),
                                             ctypes.byref(pay), ctypes.byref(nb)), "sst_result_host")
-        n = self.n
+        n = self.n = self.queries()
 
         def view(p, dtype, k):
             if k == 0 or not p.value:
@@ -366,6 +379,13 @@ class ExplainResult:
         self.offset = view(off, np.uint64, n)
         self.payload = view(pay, np.uint8, int(nb.value))
         return self
+
+    def queries(self):
+        """Number of explain queries (sst_result_queries; the rows step learns
+        it from its pass)."""
+        n = _I64()
+        self.engine.check(self.engine._lib.sst_result_queries(self.handle, ctypes.byref(n)), "sst_result_queries")
+        return int(n.value)
 
     def settle(self):
         """Wait for the pass and complete it (sst_result_settle):
@@ -634,6 +654,24 @@ class DeviceTable:
             reuse.n = n
             return reuse
         return ExplainResult(self.engine, h, n)
+
+    def step_rows_device(self, d_obs, d_peak_off, n_spec, n_peaks, d_su_seq, shifts, sides, d_valid_out, max_weight,
+                         tolerance, precision, max_mods_scalar, max_queries, d_intensity=None, intensity_cutoff=0.5e6,
+                         mass_cutoff=50000.0, cap=2 ** 32, reuse=None):
+        """sst_step_rows_device: classify_fragments' is_valid + filters and
+        the first filter_by_explanation round's window explains from the
+        peaks, all on the device (queued, no host sync)."""
+        sh = np.ascontiguousarray(shifts, dtype=np.float64)
+        sd = np.ascontiguousarray(sides, dtype=np.uint8)
+        h = ctypes.c_void_p(reuse.handle.value if reuse is not None else None)
+        self.engine.check(self.engine._lib.sst_step_rows_device(
+            self.handle, d_obs, d_peak_off, int(n_spec), int(n_peaks), d_intensity, float(intensity_cutoff),
+            float(mass_cutoff), d_su_seq, _ptr(sh), _ptr(sd), len(sh), float(max_weight), float(tolerance),
+            float(precision), int(max_mods_scalar), int(cap), int(max_queries), d_valid_out, ctypes.byref(h)),
+            "sst_step_rows_device")
+        if reuse is not None:
+            return reuse
+        return ExplainResult(self.engine, h, int(max_queries))
 
     def step_device(self, d_obs, n_peaks, shifts, d_valid_out, d_mass, d_thr, n, tolerance, precision,
                     max_mods_scalar, d_mods=None, with_memo=True, cap=2 ** 32, reuse=None):

@@ -73,6 +73,19 @@ __device__ __forceinline__ bool ring_any(const uint64_t* ring, int64_t a, int64_
 
 }  // namespace
 
+__device__ __forceinline__ void alpha_window(const AlphaArgs& a, int64_t i, int64_t& lo, int64_t& hi) {
+  const double t = a.thr_obs ? a.tol * a.thr_obs[i] : a.thr ? a.thr[i] : 0.0;
+  quantise(a.mass[i], t, a.thr == nullptr && a.thr_obs == nullptr, a.tol, a.prec, a.rprec, lo, hi);
+}
+__device__ __forceinline__ void alpha_put(const AlphaArgs& a, int64_t i, int8_t res) {
+  if (!a.alive) {
+    a.out[i] = res;
+  } else if (a.alive[i]) {
+    if (res != 1) a.alive[i] = 0;
+    if (res == -1 || res == (int8_t)kStatusPending) atomicOr(a.err, res == -1 ? 8u : 32u);
+  }
+}
+
 __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   __shared__ uint64_t ring[kRing * kChunkWords];
   __shared__ int s_w[kMaxRows];
@@ -81,7 +94,9 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   __shared__ int s_full;       // a run of >= w_max reachable masses seen
   __shared__ int s_chunk_full[kRing];
   const int64_t g = blockIdx.x;
-  const int64_t q0 = a.offsets[g], q1 = a.offsets[g + 1];
+  if (a.active && !a.active[g]) return;
+  const int64_t q0 = a.counts ? 4 * a.offsets[g] : a.offsets[g];
+  const int64_t q1 = a.counts ? q0 + a.counts[g] : a.offsets[g + 1];
   if (q0 >= q1) return;
   const uint64_t m0 = a.masks[2 * g], m1 = a.masks[2 * g + 1];
   if (threadIdx.x == 0) {
@@ -95,7 +110,7 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   __syncthreads();
   const int n_w = s_n;
   if (n_w == 0) {  // sentinel only: nothing >= 1 is reachable
-    for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) a.out[i] = 0;
+    for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) alpha_put(a, i, 0);
     return;
   }
   int wmax = 0, wmin = INT32_MAX;
@@ -113,7 +128,7 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   int64_t top = 0;
   for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) {
     int64_t lo, hi;
-    quantise(a.mass[i], a.thr ? a.thr[i] : 0.0, a.thr == nullptr, a.tol, a.prec, a.rprec, lo, hi);
+    alpha_window(a, i, lo, hi);
     top = hi > top ? hi : top;
   }
   __shared__ int64_t s_top;
@@ -159,7 +174,7 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
       int8_t res = 0;
       if (i < q1) {
         int64_t lo, hi;
-        quantise(a.mass[i], a.thr ? a.thr[i] : 0.0, a.thr == nullptr, a.tol, a.prec, a.rprec, lo, hi);
+        alpha_window(a, i, lo, hi);
         ready = last || hi < end;
         if (ready) {
           // is_valid_mass (mass_explanation.py:63-88): skip v <= 0, raise at
@@ -173,7 +188,7 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
             if (x0 <= x1) any = ring_any(ring, x0, x1);
             res = any ? (int8_t)1 : (hi >= limit && hi >= lo && hi >= 1) ? (int8_t)-1 : (int8_t)0;
           }
-          a.out[i] = res;
+          alpha_put(a, i, res);
         }
       }
       // the sweep advances over the leading run of answered queries
@@ -200,7 +215,7 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
     if (s_done >= q1) break;
   }
   if (!guard_ok)  // alphabets the ring cannot hold (not produced by the reduction): reported, not guessed
-    for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) a.out[i] = (int8_t)kStatusPending;
+    for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) alpha_put(a, i, (int8_t)kStatusPending);
 }
 
 // Pair-class windows on a per-spectrum alphabet (see the file comment).  Out:

@@ -153,6 +153,10 @@ struct sst_result {
   hipStream_t pass_stream = nullptr;
   hipEvent_t settle_ev = nullptr;
   bool settle_ev_pending = false;
+  // the step from the peaks (sst_step_rows_device): its pass writes the dense
+  // result in query order and produces its own queries (n from the header)
+  bool rows_pass = false;
+  DevBuf rows_su, rows_ob, rows_side, rows_tot, rows_offs, rows_ctl;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
   std::vector<uint8_t> h_payload;
@@ -749,7 +753,8 @@ constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses pe
 
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->hits, &r->dense, &r->payload, &r->ctl, &r->lists, &r->wave_stats, &r->work,
-                    &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->refs, &r->stage, &r->count, &r->offset})
+                    &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->refs, &r->stage, &r->count,
+                    &r->offset, &r->rows_su, &r->rows_ob, &r->rows_side, &r->rows_tot, &r->rows_offs, &r->rows_ctl})
     b->release();
   if (r->hdr_host) (void)hipHostFree(r->hdr_host);
   r->hdr_host = nullptr;
@@ -941,6 +946,7 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count};
   r->pass_stream = c->stream;
   r->settle_ev_pending = false;
+  r->rows_pass = false;
   const int64_t n = r->n;
   r->arena_bytes = (uint64_t)r->n_scan_waves * r->region_bytes + r->spill_bytes;
   if (!r->ctl.ensure(2 * kCtlWords * 8) || !r->lists.ensure((size_t)kNumClasses * std::max<int64_t>(n, 1) * 4) ||
@@ -1138,6 +1144,13 @@ int settle(sst_result* r) {
   for (int attempt = 0;; ++attempt) {
     uint64_t h[kHdrWords];
     if (int rc = wait_header(r, h)) return rc;
+    if (r->rows_pass) {  // the step from the peaks: its queries, all answered from the pair list
+      if (h[kHdrRowsErr])
+        return fail(c, SST_E_ARG, "rows step: " + std::string(h[kHdrRowsErr] & 1 ? "a spectrum has more than 1024 peaks"
+                                                            : h[kHdrRowsErr] & 2 ? "a side has more than 2048 rows"
+                                                            : "more queries / payload than the result holds"));
+      r->n = (int64_t)h[kHdrQueries];
+    }
     if (r->scan_hdr_pending) {  // the fused scan's own header
       r->scan_hits = h[kHdrHits];
       r->scan_bytes = h[kHdrPayload];
@@ -1190,15 +1203,17 @@ int order_after_settle(sst_result* r) {
 // and the dense payload.
 int fetch(sst_result* r) {
   sst_ctx* c = r->ctx;
-  const int64_t n = r->n;
   if (int rc = settle(r)) return rc;
+  const int64_t n = r->n;  // after settling: a rows-step pass learns its query count from the header
   if (int rc = order_after_settle(r)) return rc;
   r->h_status.resize(n);
   r->h_count.assign(n, 0);
   r->h_offset.assign(n, 0);
   std::vector<uint4> hv(r->n_hits);
   std::vector<unsigned long long> ws((size_t)r->n_scan_waves * kNumStats);
-  if (n) {
+  if (n && r->rows_pass) {
+    HIP_OK(c, hipMemcpyAsync(r->h_status.data(), r->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  } else if (n) {
     HIP_OK(c, hipMemcpyAsync(r->h_status.data(), r->status.p, n, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipMemcpyAsync(r->h_stats, ctl_block(r, r->parity) + kCtlStats, kNumStats * 8, hipMemcpyDeviceToHost,
                              c->stream));
@@ -1211,7 +1226,11 @@ int fetch(sst_result* r) {
   if (r->payload_bytes)
     HIP_OK(c, hipMemcpyAsync(r->h_payload.data(), r->dense.p, r->payload_bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
-  if (n && !r->bitset_scan)  // k_bitset_scan's waves write zero counters
+  if (r->rows_pass) {  // no scan waves: every query was a pair-list window
+    for (auto& x : r->h_stats) x = 0;
+    r->h_stats[kStatPair] = (uint64_t)n;
+    r->h_stats[kStatPairPayload] = r->payload_bytes;
+  } else if (n && !r->bitset_scan)  // k_bitset_scan's waves write zero counters
     for (int64_t w = 0; w < r->n_scan_waves; ++w)
       for (int k = 0; k < kNumStats; ++k) r->h_stats[k] += ws[(size_t)w * kNumStats + k];
   for (const uint4& h : hv) {
@@ -1284,6 +1303,110 @@ int sst_step_device(sst_table* t, const double* d_obs, int64_t n_peaks, const do
       delete r;
     }
     return rc;
+  }
+  *out = r;
+  return SST_OK;
+}
+
+int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_peak_off, int64_t n_spec,
+                         int64_t n_peaks, const double* d_intensity, double intensity_cutoff, double mass_cutoff,
+                         const double* d_su_seq, const double* shifts, const uint8_t* sides, int n_shifts,
+                         double max_weight, double tol, double prec, int64_t max_mods_scalar, uint64_t cap_per_query,
+                         int64_t max_queries, int8_t* d_valid_out, sst_result** out) {
+  if (!t || !out || n_spec < 1 || n_peaks < 0 || n_peaks > INT32_MAX || n_shifts < 1 || n_shifts > 4 || !shifts ||
+      !sides || !d_obs || !d_peak_off || !d_su_seq || !d_valid_out || max_queries < 1 ||
+      max_queries > SST_MAX_EXPLAIN_BATCH || (int64_t)n_shifts * n_peaks > INT32_MAX)
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (!t->args.pairs_enabled) return fail(c, SST_E_ARG, "rows step: the table has no pair list");
+  // every window must be pair-class with budgets that cannot bind: a
+  // difference <= max_weight, a threshold <= tol * 2 * mass_cutoff
+  const double hi_max = (max_weight + tol * 2.0 * mass_cutoff) / prec + 2.0;
+  if (!(hi_max < (double)t->args.pair_hi))
+    return fail(c, SST_E_ARG, "rows step: windows may leave the pair class (max_weight / mass_cutoff too large)");
+  if (t->args.any_mod) {
+    if (max_mods_scalar >= 0 && max_mods_scalar < 2)
+      return fail(c, SST_E_ARG, "rows step: max_modifications < 2 can bind on pair windows");
+    for (int r = 1; r < t->n_rows; ++r)
+      if (t->is_mod[r] && t->cap[r] < 2) return fail(c, SST_E_ARG, "rows step: a modification cap < 2 can bind");
+  }
+  sst_result* r = *out;
+  const bool reuse = r != nullptr;
+  if (reuse) {
+    if (r->ctx != c || max_queries > r->cap_n) return fail(c, SST_E_ARG, "result reuse: other ctx or capacity");
+  } else if (int rc = alloc_result(t, max_queries, &r)) {
+    return rc;
+  }
+  auto bail = [&](int rc) {
+    if (!reuse) {
+      free_result_bufs(r);
+      delete r;
+    }
+    return rc;
+  };
+  const size_t P = (size_t)n_peaks, S = (size_t)n_spec;
+  const bool fresh = !r->rows_ctl.p;
+  if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, (uint64_t)16 * r->cap_n + (1u << 20))) ||
+      !r->rows_su.ensure(std::max<size_t>(1, 4 * P) * 8) || !r->rows_ob.ensure(std::max<size_t>(1, 4 * P) * 8) ||
+      !r->rows_side.ensure(2 * S * 4) || !r->rows_tot.ensure(3 * S * 4) || !r->rows_offs.ensure(3 * S * 8) ||
+      !r->rows_ctl.ensure(64))
+    return bail(fail(c, SST_E_NOMEM, "device allocation failed (rows step)"));
+  if (fresh) HIP_OK(c, hipMemsetAsync(r->rows_ctl.p, 0, 64, c->stream));
+  r->pass = {t, nullptr, nullptr, nullptr, max_mods_scalar, tol, prec, 1, cap_per_query};
+  r->pass_stream = c->stream;
+  r->settle_ev_pending = false;
+  r->rows_pass = true;
+  ++r->pass_id;
+  r->tail_ran = true;  // nothing to route
+  r->arrays_ready = false;
+  r->bitset_scan = false;
+  r->fused_pass = true;
+  r->scan_hdr_pending = true;
+  r->scan_hits = r->scan_bytes = 0;
+  r->settled = false;
+  RowsArgs a{};
+  a.obs = d_obs;
+  a.peak_off = d_peak_off;
+  a.n_spec = n_spec;
+  a.n_peaks = n_peaks;
+  a.intensity = d_intensity;
+  a.intensity_cutoff = intensity_cutoff;
+  a.mass_cutoff = mass_cutoff;
+  a.max_variance = 1.0;  // fragment_classification.py:8
+  a.su_seq = d_su_seq;
+  for (int k = 0; k < n_shifts; ++k) {
+    a.shift[k] = shifts[k];
+    a.sides[k] = sides[k];
+  }
+  a.n_shifts = n_shifts;
+  a.max_weight = max_weight;
+  a.tol = tol;
+  a.prec = prec;
+  a.rprec = 1.0 / prec;
+  a.cap = (uint32_t)std::min<uint64_t>(cap_per_query, UINT32_MAX);
+  a.valid_out = d_valid_out;
+  a.rows_su = (double*)r->rows_su.p;
+  a.rows_ob = (double*)r->rows_ob.p;
+  a.side_rows = (uint32_t*)r->rows_side.p;
+  a.totals = (uint32_t*)r->rows_tot.p;
+  a.offs = (uint64_t*)r->rows_offs.p;
+  a.ctl = (uint64_t*)r->rows_ctl.p;
+  a.err = (uint32_t*)((char*)r->rows_ctl.p + 32);
+  a.done = (uint32_t*)((char*)r->rows_ctl.p + 40);
+  a.cap_queries = (uint64_t)r->cap_n;
+  a.cap_bytes = r->dense.bytes;
+  a.status = (int8_t*)r->status.p;
+  a.hits = (uint4*)r->hits.p;
+  a.refs = (uint16_t*)r->refs.p;
+  a.dense = (uint8_t*)r->dense.p;
+  a.hdr = (uint64_t*)r->hdr.p;
+  a.hdr_host = r->hdr_host_dev;
+  a.pass_id = ++r->pack_seq;
+  {
+    Prof p(c, SST_K_EXPLAIN_MAIN);
+    HIP_OK(c, launch_rows_step(t->args, a, c->n_cu, scan_dyn_lds(t->args), c->stream));
   }
   *out = r;
   return SST_OK;
@@ -1422,6 +1545,15 @@ int sst_result_settle(sst_result* r, uint64_t* n_hits, uint64_t* payload_bytes) 
   return SST_OK;
 }
 
+int sst_result_queries(sst_result* r, int64_t* n) {
+  if (!r || !n) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(r->ctx->mu);
+  if (int rc = set_device(r->ctx)) return rc;
+  if (int rc = settle(r)) return rc;
+  *n = r->n;
+  return SST_OK;
+}
+
 int sst_result_host(sst_result* r, const int8_t** status, const uint64_t** count, const uint64_t** offset,
                     const uint8_t** payload, uint64_t* payload_bytes) {
   if (!r) return SST_E_ARG;
@@ -1477,7 +1609,7 @@ int sst_result_pair_hits(sst_result* r, void** d_refs, uint64_t* n_pair_hits, ui
   if (d_refs) *d_refs = r->refs.p;
   if (n_pair_hits) *n_pair_hits = r->scan_hits;
   if (pair_bytes) *pair_bytes = r->scan_bytes;
-  if (n_scan_wg) *n_scan_wg = r->n_wg;
+  if (n_scan_wg) *n_scan_wg = r->rows_pass ? 0 : r->n_wg;  // 0: the hits come in query order
   return SST_OK;
 }
 
@@ -1550,7 +1682,7 @@ int64_t sst_wire_pack(sst_result* r, const int8_t* d_valid, int64_t n_valid, voi
     t->pair_key_set = true;
   }
   const uint64_t hdr[kWireHeaderWords] = {kWireMagic, (uint64_t)n_valid, (uint64_t)r->n, n_pair, n_exp, xpay,
-                                          (uint64_t)r->n_wg, n_pair ? t->pair_key : 0, (uint64_t)w, 0, a.list_cap,
+                                          (uint64_t)(r->rows_pass ? 0 : r->n_wg), n_pair ? t->pair_key : 0, (uint64_t)w, 0, a.list_cap,
                                           a.o_list, 0, 0, 0, 0};
   for (int k = 0; k < kWireHeaderWords; ++k) a.hdr[k] = hdr[k];
   auto blocks = [](uint64_t n) { return (uint32_t)((n + 255) / 256); };
@@ -1751,7 +1883,149 @@ int sst_is_valid_alpha_device(sst_table* t, const double* d_mass, const double* 
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
   if (int rc = check_masks(t)) return rc;
-  AlphaArgs a{d_mass, d_thr, d_offsets, d_masks, t->args.w, t->n_rows, tol, prec, 1.0 / prec, d_out};
+  AlphaArgs a{};
+  a.mass = d_mass;
+  a.thr = d_thr;
+  a.offsets = d_offsets;
+  a.masks = d_masks;
+  a.w = t->args.w;
+  a.n_rows = t->n_rows;
+  a.tol = tol;
+  a.prec = prec;
+  a.rprec = 1.0 / prec;
+  a.out = d_out;
+  HIP_OK(c, launch_valid_alpha(a, n_spec, c->stream));
+  return SST_OK;
+}
+
+// ---- config 5 on the device (sst_pipe.hip) ---------------------------
+static int pipe_args(sst_table* t, const double* d_obs, const int64_t* d_peak_off, int64_t n_spec, int64_t n_peaks,
+                     const double* d_intensity, double intensity_cutoff, double mass_cutoff, const double* d_su_seq,
+                     const double* shifts, const uint8_t* sides, int n_shifts, double max_weight, double tol,
+                     double prec, PipeArgs& a) {
+  if (!t || n_spec < 0 || n_spec > INT32_MAX || n_peaks < 0 || n_shifts < 1 || n_shifts > 4 || !shifts || !sides ||
+      (n_spec > 0 && (!d_obs || !d_peak_off || !d_su_seq)))
+    return SST_E_ARG;
+  if (!t->args.pairs_enabled) return fail(t->ctx, SST_E_ARG, "pipeline: the table has no pair list");
+  const double hi_max = (max_weight + tol * 2.0 * mass_cutoff) / prec + 2.0;
+  if (!(hi_max < (double)t->args.pair_hi))
+    return fail(t->ctx, SST_E_ARG, "pipeline: windows may leave the pair class (max_weight / mass_cutoff too large)");
+  a = PipeArgs{};
+  a.obs = d_obs;
+  a.peak_off = d_peak_off;
+  a.n_spec = n_spec;
+  a.n_peaks = n_peaks;
+  a.intensity = d_intensity;
+  a.intensity_cutoff = intensity_cutoff;
+  a.mass_cutoff = mass_cutoff;
+  a.max_variance = 1.0;  // fragment_classification.py:8
+  a.su_seq = d_su_seq;
+  for (int k = 0; k < n_shifts; ++k) {
+    a.shift[k] = shifts[k];
+    a.sides[k] = sides[k];
+  }
+  a.n_shifts = n_shifts;
+  a.max_weight = max_weight;
+  a.tol = tol;
+  a.prec = prec;
+  a.rprec = 1.0 / prec;
+  for (int r = 1; r < t->n_rows; ++r)
+    if (!t->is_mod[r]) a.canon[r >> 6] |= 1ull << (r & 63);
+  return SST_OK;
+}
+
+int sst_classify_rows_device(sst_table* t, const double* d_obs, const int64_t* d_peak_off, int64_t n_spec,
+                             int64_t n_peaks, const double* d_intensity, double intensity_cutoff, double mass_cutoff,
+                             const double* d_su_seq, const double* shifts, const uint8_t* sides, int n_shifts,
+                             double max_weight, double tol, double prec, int8_t* d_valid_out, double* d_rows_su,
+                             double* d_rows_ob, uint32_t* d_rows_meta, uint8_t* d_alive, uint32_t* d_rows,
+                             uint32_t* d_err) {
+  PipeArgs a;
+  if (int rc = pipe_args(t, d_obs, d_peak_off, n_spec, n_peaks, d_intensity, intensity_cutoff, mass_cutoff, d_su_seq,
+                         shifts, sides, n_shifts, max_weight, tol, prec, a))
+    return rc;
+  if (n_spec > 0 && (!d_rows_su || !d_rows_ob || !d_rows_meta || !d_alive || !d_rows || !d_err)) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (!c->singleton_masses.ensure((size_t)t->n_rows * 8)) return fail(c, SST_E_NOMEM, "device allocation failed");
+  HIP_OK(c, hipMemcpyAsync(c->singleton_masses.p, t->masses.data(), (size_t)t->n_rows * 8, hipMemcpyHostToDevice,
+                           c->stream));
+  a.masses = (const int64_t*)c->singleton_masses.p;
+  a.n_masses = t->n_rows;
+  a.valid_out = d_valid_out;
+  a.r_su = d_rows_su;
+  a.r_ob = d_rows_ob;
+  a.r_meta = d_rows_meta;
+  a.alive = d_alive;
+  a.cnt = d_rows;
+  a.err = d_err;
+  Prof p(c, SST_K_IS_VALID);
+  HIP_OK(c, launch_classify_rows(t->args, a, c->n_cu, c->stream));
+  return SST_OK;
+}
+
+int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                         const double* d_rows_ob, const uint32_t* d_rows_meta, uint8_t* d_alive,
+                         const uint32_t* d_rows, const uint64_t* d_alpha, uint64_t* d_alpha_next,
+                         const uint8_t* d_active, uint8_t* d_active_next, uint32_t* d_rounds, uint32_t* d_queries,
+                         uint32_t* d_n_active, double max_weight, double tol, double prec, uint32_t* d_err) {
+  const double zero_shift = 0.0;
+  const uint8_t zero_side = 0;
+  PipeArgs a;
+  if (int rc = pipe_args(t, d_rows_su, d_peak_off, n_spec, 0, nullptr, 0.0, 0.0, d_rows_su, &zero_shift,
+                         &zero_side, 1, max_weight, tol, prec, a))
+    return rc;
+  if (n_spec > 0 && (!d_rows_ob || !d_rows_meta || !d_alive || !d_rows || !d_alpha || !d_alpha_next || !d_active ||
+                     !d_active_next || !d_rounds || !d_queries || !d_n_active || !d_err))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = check_masks(t)) return rc;
+  a.r_su = const_cast<double*>(d_rows_su);
+  a.r_ob = const_cast<double*>(d_rows_ob);
+  a.r_meta = const_cast<uint32_t*>(d_rows_meta);
+  a.alive = d_alive;
+  a.cnt = const_cast<uint32_t*>(d_rows);
+  a.alpha = d_alpha;
+  a.alpha_next = d_alpha_next;
+  a.active = d_active;
+  a.active_next = d_active_next;
+  a.rounds = d_rounds;
+  a.queries = d_queries;
+  a.n_active = d_n_active;
+  a.err = d_err;
+  Prof p(c, SST_K_EXPLAIN_MAIN);
+  HIP_OK(c, launch_fix_round(t->args, a, c->n_cu, c->stream));
+  return SST_OK;
+}
+
+int sst_valid_rows_alpha_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                                const double* d_rows_ob, const uint32_t* d_rows, const uint64_t* d_alpha,
+                                const uint8_t* d_active, uint8_t* d_alive, double tol, double prec, uint32_t* d_err) {
+  if (!t || n_spec < 0 || n_spec > INT32_MAX ||
+      (n_spec > 0 && (!d_peak_off || !d_rows_su || !d_rows_ob || !d_rows || !d_alpha || !d_alive || !d_err)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = check_masks(t)) return rc;
+  AlphaArgs a{};
+  a.mass = d_rows_su;
+  a.thr_obs = d_rows_ob;  // the rows' thresholds: tolerance * observed mass (prediction.py:219)
+  a.offsets = d_peak_off;
+  a.counts = d_rows;
+  a.masks = d_alpha;
+  a.active = d_active;
+  a.alive = d_alive;
+  a.err = d_err;
+  a.w = t->args.w;
+  a.n_rows = t->n_rows;
+  a.tol = tol;
+  a.prec = prec;
+  a.rprec = 1.0 / prec;
+  Prof p(c, SST_K_IS_VALID);
   HIP_OK(c, launch_valid_alpha(a, n_spec, c->stream));
   return SST_OK;
 }

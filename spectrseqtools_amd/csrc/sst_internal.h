@@ -186,7 +186,9 @@ enum {
   kHdrCursor = 5,       // raw spill cursor (sizes a retry's spill area)
   kHdrPass = 6,         // pass id the header belongs to
   kHdrRegionNeed = 7,   // largest region a scan wave would have needed (sizes a retry's regions)
-  kHdrWords = 8
+  kHdrQueries = 8,      // explain queries of the pass (the rows step produces its own)
+  kHdrRowsErr = 9,      // rows step: 1 a spectrum over kRowsMaxPeaks, 2 a side over kRowsMaxSide, 4 no room
+  kHdrWords = 10
 };
 
 struct PackArgs {
@@ -284,7 +286,12 @@ hipError_t launch_wire_pack(const WireArgs& a, hipStream_t st);
 struct AlphaArgs {  // k_valid_alpha: is_valid_mass on the reduced tables
   const double* mass;
   const double* thr;       // may be null: tolerance * mass
-  const int64_t* offsets;  // [n_spec + 1] query ranges (each in mass order)
+  const double* thr_obs;   // may be null: else thr = tolerance * thr_obs[i] (the rows' observed masses)
+  const int64_t* offsets;  // [n_spec + 1] query ranges (each in mass order); with `base`: peak offsets
+  const uint32_t* counts;  // may be null; else spectrum g's queries are [4 offsets[g], + counts[g]) (row slots)
+  const uint8_t* active;   // may be null; else only spectra with active[g] are answered
+  uint8_t* alive;          // may be null; else alive[i] &= (answer == 1) instead of writing out
+  uint32_t* err;           // with alive: | 8 when a row's window leaves its reduced table
   const uint64_t* masks;
   const int* w;            // full table row masses
   int n_rows;
@@ -304,6 +311,77 @@ struct PairAlphaArgs {  // k_pairs_alpha: explain on pair-class windows
   uint32_t* range;    // [2n] pair-list entries [first, end)
 };
 hipError_t launch_valid_alpha(const AlphaArgs& a, int64_t n_spec, hipStream_t st);
+
+// the step from the peaks (sst_rows.hip)
+constexpr int kRowsMaxPeaks = 1024;   // peaks per spectrum a workgroup holds
+constexpr int kRowsMaxSide = 2048;    // rows per side (two breakages per side at most ... x 2 headroom)
+struct RowsArgs {
+  const double* obs;          // [n_peaks] sorted within each spectrum
+  const int64_t* peak_off;    // [n_spec + 1]
+  int64_t n_spec, n_peaks;
+  const double* intensity;    // may be null: every peak passes
+  double intensity_cutoff, mass_cutoff, max_variance;
+  const double* su_seq;       // [n_spec] SequenceInformation.su_mass per spectrum
+  double shift[4];
+  uint8_t sides[4];           // per breakage: bit0 START side, bit1 END side
+  int n_shifts;
+  double max_weight, tol, prec, rprec;
+  uint32_t cap;               // candidate cap (OVERFLOW beyond)
+  int8_t* valid_out;          // [n_shifts * n_peaks]
+  double* rows_su;            // scratch [4 * n_peaks]
+  double* rows_ob;
+  uint32_t* side_rows;        // [2 n_spec]
+  uint32_t* totals;           // [3 n_spec] queries, hits, payload bytes
+  uint64_t* offs;             // [3 n_spec]
+  uint64_t* ctl;              // [4] totals
+  uint32_t* err;
+  uint32_t* done;
+  uint64_t cap_queries, cap_bytes;
+  int8_t* status;
+  uint4* hits;
+  uint16_t* refs;
+  uint8_t* dense;
+  uint64_t* hdr;
+  uint64_t* hdr_host;
+  uint64_t pass_id;
+};
+hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, size_t dyn, hipStream_t st);
+
+// config 5 on the device (sst_pipe.hip)
+constexpr int kPipeMaxPeaks = 512;   // peaks per spectrum the classify workgroup holds
+constexpr int kPipeMaxRows = 2048;   // rows per spectrum (4 breakages)
+struct PipeArgs {
+  const double* obs;          // [n_peaks], sorted within each spectrum
+  const int64_t* peak_off;    // [n_spec + 1]; rows of spectrum g live at slots 4 * peak_off[g] + i
+  int64_t n_spec, n_peaks;
+  const double* intensity;
+  double intensity_cutoff, mass_cutoff, max_variance;
+  const double* su_seq;
+  double shift[4];
+  uint8_t sides[4];
+  int n_shifts;
+  double max_weight, tol, prec, rprec;
+  const int64_t* masses;      // the table's integer masses (is_singleton)
+  int n_masses;
+  int8_t* valid_out;          // may be null: A7 codes [n_shifts * n_peaks]
+  double* r_su;
+  double* r_ob;
+  uint32_t* r_meta;           // breakage | sides << 2 | singleton << 4 | peak << 8
+  uint8_t* alive;
+  uint32_t* cnt;              // [n_spec] rows
+  const uint64_t* alpha;      // [2 n_spec] this round's alphabets
+  uint64_t* alpha_next;
+  const uint8_t* active;      // [n_spec] spectra running this round
+  uint8_t* active_next;
+  uint32_t* rounds;           // [n_spec]
+  uint32_t* queries;          // [n_spec] explain queries issued over the rounds
+  uint32_t* n_active;         // spectra whose alphabet shrank this round
+  uint64_t canon[2];          // the canonical rows (never dropped)
+  uint32_t* err;
+};
+hipError_t launch_classify_rows(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st);
+hipError_t launch_fix_round(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st);
+size_t rows_lds_bytes();
 hipError_t launch_pairs_alpha(const TableArgs& t, const PairAlphaArgs& a, hipStream_t st);
 
 hipError_t launch_bits_seed(uint64_t* R0, int64_t nwords, hipStream_t st);

@@ -81,65 +81,6 @@ __device__ __forceinline__ M128 rec_L(ulonglong2 rec) { return {rec.x, rec.y & (
 
 __device__ __forceinline__ ulonglong2 ld_index(const ulonglong2* idx, int64_t m) { return idx[m]; }
 
-// Window of one query as exact f64 integers: target = rint(mass / prec) and
-// thr = ceil(thr_abs / prec) (mass_explanation.py:107,110-114).  Both
-// quotients are taken as x * (1/prec), within 2.5 ulp of the exact one; the
-// correctly rounded division runs only when a product lies within 2^-50
-// (relative) of a point where rint / ceil change value, or is huge, so the
-// integers are exactly the reference's.  Straight-line except for that rare
-// fallback (the lean form of rint_quot / ceil_quot).
-__device__ __forceinline__ void quantise_lean(double m, double t, double prec, double rprec, double& lof,
-                                              double& hif) {
-  const double qm = m * rprec, qt = t * rprec;
-  double rm = __builtin_rint(qm), ct = __builtin_ceil(qt);
-  const double dm = qm - rm, dt = qt - __builtin_rint(qt);  // exact
-  const bool slow = !(__builtin_fabs(qm) < 0x1p40) | !(__builtin_fabs(qt) < 0x1p40) |
-                    (0.5 - __builtin_fabs(dm) <= __builtin_fabs(qm) * 0x1p-50) |
-                    (__builtin_fabs(dt) <= __builtin_fabs(qt) * 0x1p-50);
-  if (__builtin_expect(slow, 0)) {
-    rm = __builtin_rint(m / prec);
-    ct = __builtin_ceil(t / prec);
-  }
-  lof = rm - ct;
-  hif = rm + ct;
-}
-
-// any bit of valid in [a, b] (a <= b, both < limit)
-__device__ __forceinline__ bool any_bits(const uint64_t* valid, int64_t a, int64_t b) {
-  int64_t wa = a >> 6, wb = b >> 6;
-  for (int64_t wi = wa; wi <= wb; ++wi) {
-    uint64_t x = valid[wi];
-    if (wi == wa) x &= ~0ull << (a & 63);
-    if (wi == wb) x &= ~0ull >> (63 - (b & 63));
-    if (x) return true;
-  }
-  return false;
-}
-__device__ __forceinline__ int count_bits(const uint64_t* valid, int64_t a, int64_t b) {
-  int64_t wa = a >> 6, wb = b >> 6;
-  int c = 0;
-  for (int64_t wi = wa; wi <= wb; ++wi) {
-    uint64_t x = valid[wi];
-    if (wi == wa) x &= ~0ull << (a & 63);
-    if (wi == wb) x &= ~0ull >> (63 - (b & 63));
-    c += __builtin_popcountll(x);
-  }
-  return c;
-}
-
-// is_valid_mass semantics (mass_explanation.py:63-88): ascending scan, skip
-// v <= 0, raise at the first v >= limit, True at the first reachable v.
-__device__ __forceinline__ int8_t valid_window(const uint64_t* valid, int64_t limit, int64_t lo, int64_t hi,
-                                               int64_t full_lo = 1, int64_t full_hi = 1, int64_t first_reach = 0) {
-  if (hi < lo) return 0;
-  int64_t a = lo < 1 ? 1 : lo;
-  if (a > hi) return 0;
-  int64_t b = hi < limit - 1 ? hi : limit - 1;
-  if (a <= b && b >= full_lo && a < full_hi) return 1;  // meets the all-reachable run: no bitset load
-  if (a <= b && b >= first_reach && any_bits(valid, a, b)) return 1;  // below first_reach: nothing reachable
-  return hi >= limit ? (int8_t)-1 : (int8_t)0;
-}
-
 // ---------------------------------------------------------------------------
 // table build: bitsets R_r over masses [0, M), R_r = R_{r-1} closed under +w_r
 // ---------------------------------------------------------------------------

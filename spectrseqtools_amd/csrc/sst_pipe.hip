@@ -1,0 +1,412 @@
+// sst_pipe.hip -- the prediction pipeline's explanation stages over many
+// spectra, device-resident, gfx950.
+//
+//   k_classify_rows  classify_fragments (fragment_classification.py:17-101)
+//                    per spectrum: is_valid of every peak x breakage weight,
+//                    the intensity / mass / sequence-mass filters, is_singleton
+//                    (:104-119) and the SU order of the kept rows (a merge of
+//                    the breakages' sorted streams, ties breakage-major as the
+//                    reference's stable sort).  Rows go to fixed slots
+//                    (spectrum g: 4 * peak_off[g] + i), no compaction pass.
+//   k_fix_round      one filter_by_explanation round (prediction.py:170-227)
+//                    of every spectrum still reducing: the alive rows, the
+//                    sliding-window pairs of both sides (closed form, as the
+//                    rows step) and the singletons; every query against the
+//                    spectrum's alphabet (the full table's pair list with the
+//                    row mask: the reduced table's answers); the explanation
+//                    dict's last-writer semantics (a side pair is stored only
+//                    with >= 1 explanation, a singleton always, a later equal
+//                    key replaces an earlier one) in an LDS hash; the union of
+//                    the surviving answers' rows -> the reduced alphabet
+//                    (canonical rows kept); the spectrum stays active while
+//                    the alphabet shrinks.  is_valid on the reduced tables
+//                    follows in k_valid_alpha (sst_alpha.hip, AND-ed into the
+//                    rows' alive flags).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sst_internal.h"
+#include "sst_quant.h"
+
+namespace sst {
+
+namespace {
+
+constexpr int kPipeWG = 1024;
+constexpr int kHashSlots = 4096;
+constexpr uint64_t kEmptyKey = ~0ull;
+
+__device__ __forceinline__ bool in_mask(uint64_t m0, uint64_t m1, int r) {
+  return r < 64 ? ((m0 >> r) & 1ull) : ((m1 >> (r - 64)) & 1ull);
+}
+
+// pair-list window [a, hi] (a >= 1, hi < pair_hi) against a row mask: the
+// number of entries whose rows are all in the mask and the union of their rows
+__device__ __forceinline__ uint32_t masked_walk(const TableArgs& t, uint32_t a, uint32_t hi, uint64_t m0, uint64_t m1,
+                                                uint64_t& u0, uint64_t& u1) {
+  const uint32_t* sums = t.pair_data;
+  const uint32_t* recs = sums + (t.n_pairs + 2);
+  const uint32_t* bk = recs + (t.n_pairs + 2);
+  const uint32_t rel = a > t.pair_base ? a - t.pair_base : 0u;
+  uint32_t k = bk[rel >> t.pair_shift] & 0xFFFFu;
+  const uint32_t a2 = a << 1, h2 = (hi << 1) | 1u;
+  while (sums[k] < a2) ++k;
+  uint32_t cnt = 0;
+  for (; sums[k] <= h2; ++k) {
+    const uint32_t rec = recs[k];
+    const int top = (int)((rec >> ((rec & 0xFFu) == 1u ? 8 : 16)) & 0xFFu);
+    const int low = (int)((rec >> 8) & 0xFFu);
+    if (in_mask(m0, m1, top) && in_mask(m0, m1, low)) {
+      ++cnt;
+      if (top < 64) u0 |= 1ull << top; else u1 |= 1ull << (top - 64);
+      if (low < 64) u0 |= 1ull << low; else u1 |= 1ull << (low - 64);
+    }
+  }
+  return cnt;
+}
+
+// explain status of a pair-class window against the mask (NONE / EMPTY / SOME)
+__device__ __forceinline__ int8_t masked_answer(const TableArgs& t, double mass, double thr, double prec,
+                                                double rprec, uint64_t m0, uint64_t m1, uint64_t& u0, uint64_t& u1,
+                                                bool& pair_class) {
+  double lof, hif;
+  quantise_lean(mass, thr, prec, rprec, lof, hif);
+  u0 = u1 = 0;
+  pair_class = hif < (double)t.pair_hi;
+  if (!pair_class || hif < 0.0) return SST_NONE;
+  const double af = lof < 1.0 ? 1.0 : lof;
+  uint32_t cnt = 0;
+  if (af <= hif) cnt = masked_walk(t, (uint32_t)af, (uint32_t)hif, m0, m1, u0, u1);
+  return cnt ? (int8_t)SST_SOME : lof <= 0.0 ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;
+}
+
+struct ClsLds {
+  double obs[kPipeMaxPeaks];
+  uint16_t kidx[4][kPipeMaxPeaks];
+  uint8_t keep[kPipeMaxPeaks];
+  uint32_t kcnt[4];
+  int64_t masses[kMaxRows];
+  uint32_t w[16];
+};
+
+}  // namespace
+
+__global__ __launch_bounds__(kPipeWG) void k_classify_rows(TableArgs t, PipeArgs a) {
+  __shared__ ClsLds L;
+  for (int r = threadIdx.x; r < a.n_masses; r += blockDim.x) L.masses[r] = a.masses[r];
+  __syncthreads();
+  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
+    const int64_t p0 = a.peak_off[g];
+    const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
+    if (P > (uint32_t)kPipeMaxPeaks) {
+      if (threadIdx.x == 0) {
+        atomicOr(a.err, 1u);
+        a.cnt[g] = 0;
+      }
+      continue;
+    }
+    const double su_seq = a.su_seq[g];
+    for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) {
+      const double o = a.obs[p0 + p];
+      L.obs[p] = o;
+      uint8_t kp = 0;
+      for (int k = 0; k < a.n_shifts; ++k) {
+        const double su = o - a.shift[k];
+        double lof, hif;
+        quantise_lean(su, a.tol * o, a.prec, a.rprec, lof, hif);
+        const int8_t code =
+            valid_window(t.valid, t.limit, (int64_t)lof, (int64_t)hif, t.full_lo, t.full_hi, t.first_reach);
+        if (a.valid_out) a.valid_out[(int64_t)k * a.n_peaks + p0 + p] = code;
+        if (code < 0) atomicOr(a.err, 8u);  // is_valid_mass raises: the reference's classify would too
+        const bool inten = a.intensity ? a.intensity[p0 + p] > a.intensity_cutoff : true;
+        const bool full = (a.sides[k] & 3) == 3;
+        const bool keep = code == 1 && inten && o < a.mass_cutoff && su < su_seq + a.max_variance &&
+                          (su > su_seq - a.max_variance || !full);
+        kp |= (uint8_t)keep << k;
+      }
+      L.keep[p] = kp;
+    }
+    __syncthreads();
+    for (int k = 0; k < a.n_shifts; ++k) {
+      uint32_t carry = 0;
+      for (uint32_t q0 = 0; q0 < P; q0 += blockDim.x) {
+        const uint32_t p = q0 + threadIdx.x;
+        const uint32_t f = p < P ? (L.keep[p] >> k) & 1u : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl(f, L.w, tot);
+        if (f) L.kidx[k][carry + ex] = (uint16_t)p;
+        carry += tot;
+      }
+      if (threadIdx.x == 0) L.kcnt[k] = carry;
+    }
+    __syncthreads();
+    // every kept row's place in the spectrum's SU order (all breakages)
+    uint32_t n = 0;
+    for (int k = 0; k < a.n_shifts; ++k) n += L.kcnt[k];
+    const int64_t base = 4 * p0;
+    for (int k = 0; k < a.n_shifts; ++k) {
+      const double sk = a.shift[k];
+      for (uint32_t j = threadIdx.x; j < L.kcnt[k]; j += blockDim.x) {
+        const uint32_t p = L.kidx[k][j];
+        const double su = L.obs[p] - sk;
+        uint32_t pos = j;
+        for (int k2 = 0; k2 < a.n_shifts; ++k2) {
+          if (k2 == k) continue;
+          const double s2 = a.shift[k2];
+          uint32_t lo = 0, hi = L.kcnt[k2];
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const double v = L.obs[L.kidx[k2][mid]] - s2;
+            if (v < su || (v == su && k2 < k)) lo = mid + 1;
+            else hi = mid;
+          }
+          pos += lo;
+        }
+        // is_singleton (:104-119): a table row mass (the sentinel 0 included) in the window
+        int64_t lo, hi;
+        quantise(su, a.tol * L.obs[p], false, a.tol, a.prec, a.rprec, lo, hi);
+        int l = 0, r = a.n_masses;
+        while (l < r) {
+          const int mid = (l + r) >> 1;
+          if (L.masses[mid] < lo) l = mid + 1;
+          else r = mid;
+        }
+        const bool single = lo <= hi && l < a.n_masses && L.masses[l] <= hi;
+        a.r_su[base + pos] = su;
+        a.r_ob[base + pos] = L.obs[p];
+        a.r_meta[base + pos] = (uint32_t)k | ((uint32_t)a.sides[k] << 2) | ((uint32_t)single << 4) | (p << 8);
+        a.alive[base + pos] = 1;
+      }
+    }
+    if (threadIdx.x == 0) a.cnt[g] = n;
+    __syncthreads();
+  }
+}
+
+namespace {
+
+struct FixLds {
+  double su[kPipeMaxRows];
+  double ob[kPipeMaxRows];
+  uint16_t side[2][kPipeMaxRows];   // alive rows of each side (indices into su / ob), SU order
+  uint16_t single[kPipeMaxRows];    // alive singleton rows
+  uint32_t qoff[2][kPipeMaxRows + 1];
+  uint64_t hkey[kHashSlots];
+  uint32_t hidx[kHashSlots];
+  uint32_t n_side[2], n_single, n_alive;
+  int sstar[2];
+  uint32_t w[16];
+  unsigned long long u0, u1;
+  uint32_t writers;
+};
+
+__device__ __forceinline__ double side_su(const FixLds& L, int sd, uint32_t r) { return L.su[L.side[sd][r]]; }
+
+// s* and the per-row pair counts' prefix of side sd (the rows step's closed form)
+__device__ uint32_t fix_side_pairs(FixLds& L, int sd, double mw) {
+  const uint32_t n = L.n_side[sd];
+  if (threadIdx.x == 0) L.sstar[sd] = n ? (int)n - 1 : 0;
+  __syncthreads();
+  for (uint32_t r = threadIdx.x; r + 1 < n; r += blockDim.x)
+    if (!(side_su(L, sd, n - 1) - side_su(L, sd, r) > mw)) atomicMin(&L.sstar[sd], (int)r);
+  __syncthreads();
+  const uint32_t ss = (uint32_t)L.sstar[sd];
+  uint32_t carry = 0;
+  for (uint32_t r0 = 0; r0 < n; r0 += blockDim.x) {
+    const uint32_t r = r0 + threadIdx.x;
+    uint32_t c = 0;
+    if (r + 1 < n) {
+      if (r < ss) {
+        uint32_t lo = r + 1, hi = n - 1;
+        const double sr = side_su(L, sd, r);
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (side_su(L, sd, mid) - sr > mw) hi = mid;
+          else lo = mid + 1;
+        }
+        c = lo - r - 1;
+      } else if (r == ss) {
+        c = n - 1 - r;
+      } else {
+        c = 1;
+      }
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl(c, L.w, tot);
+    if (r < n) L.qoff[sd][r] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) L.qoff[sd][n] = carry;
+  __syncthreads();
+  return carry;
+}
+
+// query o of the round (START pairs, END pairs, singletons): its key, mass and threshold
+__device__ __forceinline__ void fix_query(const FixLds& L, uint32_t o, uint32_t q0, uint32_t q1, double tol,
+                                          double& mass, double& thr, bool& single) {
+  single = o >= q0 + q1;
+  if (single) {
+    const uint32_t r = L.single[o - q0 - q1];
+    mass = L.su[r];
+    thr = tol * L.ob[r];  // prediction.py:280
+    return;
+  }
+  const int sd = o >= q0;
+  const uint32_t q = sd ? o - q0 : o;
+  const uint32_t n = L.n_side[sd];
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (L.qoff[sd][mid] <= q) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t s = lo;
+  const uint32_t e = s <= (uint32_t)L.sstar[sd] ? s + 1 + (q - L.qoff[sd][s]) : n - 1;
+  const uint32_t rs = L.side[sd][s], re = L.side[sd][e];
+  mass = L.su[re] - L.su[rs];
+  thr = tol * (L.ob[rs] + L.ob[re]);  // calculate_error_threshold, l1 (common.py:37-44)
+}
+
+__device__ __forceinline__ uint64_t key_bits(double k) {
+  if (k == 0.0) k = 0.0;  // -0.0 and 0.0 are one dict key
+  return (uint64_t)__double_as_longlong(k);
+}
+__device__ __forceinline__ uint32_t key_hash(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  return (uint32_t)x & (kHashSlots - 1);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kPipeWG) void k_fix_round(TableArgs t, PipeArgs a) {
+  __shared__ FixLds L;
+  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
+    if (!a.active[g]) {  // settled earlier: its alphabet carries over
+      if (threadIdx.x == 0) {
+        a.alpha_next[2 * g] = a.alpha[2 * g];
+        a.alpha_next[2 * g + 1] = a.alpha[2 * g + 1];
+        a.active_next[g] = 0;
+      }
+      continue;
+    }
+    const int64_t base = 4 * a.peak_off[g];
+    const uint32_t nr = a.cnt[g];
+    if (nr > (uint32_t)kPipeMaxRows) {
+      if (threadIdx.x == 0) {
+        atomicOr(a.err, 2u);
+        a.alpha_next[2 * g] = a.alpha[2 * g];
+        a.alpha_next[2 * g + 1] = a.alpha[2 * g + 1];
+        a.active_next[g] = 0;
+      }
+      continue;
+    }
+    // the alive rows (SU order) and each side's / the singletons' lists
+    uint32_t carry[4] = {0, 0, 0, 0};
+    for (uint32_t r0 = 0; r0 < nr; r0 += blockDim.x) {
+      const uint32_t r = r0 + threadIdx.x;
+      const bool al = r < nr && a.alive[base + r];
+      const uint32_t meta = al ? a.r_meta[base + r] : 0u;
+      uint32_t tot;
+      const uint32_t ex = block_excl(al ? 1u : 0u, L.w, tot);
+      const uint32_t i = carry[0] + ex;
+      if (al) {
+        L.su[i] = a.r_su[base + r];
+        L.ob[i] = a.r_ob[base + r];
+      }
+      carry[0] += tot;
+      for (int c = 0; c < 3; ++c) {
+        const bool f = al && ((meta >> (2 + c)) & 1u);  // START, END, singleton
+        const uint32_t x = block_excl(f ? 1u : 0u, L.w, tot);
+        if (f) (c < 2 ? L.side[c] : L.single)[carry[c + 1] + x] = (uint16_t)i;
+        carry[c + 1] += tot;
+      }
+    }
+    if (threadIdx.x == 0) {
+      L.n_alive = carry[0];
+      L.n_side[0] = carry[1];
+      L.n_side[1] = carry[2];
+      L.n_single = carry[3];
+      L.u0 = L.u1 = 0;
+      L.writers = 0;
+    }
+    for (int k = threadIdx.x; k < kHashSlots; k += blockDim.x) {
+      L.hkey[k] = kEmptyKey;
+      L.hidx[k] = 0;
+    }
+    __syncthreads();
+    const uint32_t q0 = fix_side_pairs(L, 0, a.max_weight);
+    const uint32_t q1 = fix_side_pairs(L, 1, a.max_weight);
+    const uint32_t Q = q0 + q1 + L.n_single;
+    const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+    // pass A: every query's answer; writers insert their key, the last (largest order) wins
+    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+      double mass, thr;
+      bool single, pc;
+      fix_query(L, o, q0, q1, a.tol, mass, thr, single);
+      uint64_t u0, u1;
+      const int8_t st = masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
+      if (!pc) atomicOr(a.err, 4u);  // not pair-class: never for these windows (the host checks)
+      if (!(single || st == SST_SOME)) continue;
+      const uint64_t key = key_bits(mass);
+      uint32_t h = key_hash(key);
+      for (int probe = 0; probe < kHashSlots; ++probe, h = (h + 1) & (kHashSlots - 1)) {
+        const unsigned long long prev = atomicCAS((unsigned long long*)&L.hkey[h], kEmptyKey, key);
+        if (prev == kEmptyKey || prev == key) {
+          atomicMax(&L.hidx[h], o + 1);
+          if (prev == kEmptyKey) atomicAdd(&L.writers, 1u);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (L.writers > kHashSlots * 3 / 4) {  // too full to trust the probe bound: reported
+      if (threadIdx.x == 0) atomicOr(a.err, 16u);
+    }
+    // pass B: the dict's surviving entries -> the observed rows
+    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+      double mass, thr;
+      bool single, pc;
+      fix_query(L, o, q0, q1, a.tol, mass, thr, single);
+      uint64_t u0, u1;
+      const int8_t st = masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
+      if (st != SST_SOME) continue;  // None / set() entries name no nucleotide
+      const uint64_t key = key_bits(mass);
+      uint32_t h = key_hash(key);
+      for (int probe = 0; probe < kHashSlots && L.hkey[h] != key; ++probe) h = (h + 1) & (kHashSlots - 1);
+      if (L.hkey[h] == key && L.hidx[h] == o + 1) {
+        if (u0) atomicOr(&L.u0, (unsigned long long)u0);
+        if (u1) atomicOr(&L.u1, (unsigned long long)u1);
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      // adapt_individual_modification_rates_by_alphabet_reduction: canonical
+      // rows stay, a modification stays iff an explanation names it
+      const uint64_t n0 = a.canon[0] | (m0 & L.u0), n1 = a.canon[1] | (m1 & L.u1);
+      a.alpha_next[2 * g] = n0;
+      a.alpha_next[2 * g + 1] = n1;
+      const bool changed = __builtin_popcountll(n0) + __builtin_popcountll(n1) !=
+                           __builtin_popcountll(m0) + __builtin_popcountll(m1);
+      a.active_next[g] = changed;
+      a.rounds[g] += 1;
+      a.queries[g] += Q;
+      if (changed) atomicAdd(a.n_active, 1u);
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_classify_rows(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st) {
+  if (a.n_spec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_classify_rows, dim3(n_wg), dim3(kPipeWG), 0, st, t, a);
+  return hipGetLastError();
+}
+hipError_t launch_fix_round(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st) {
+  if (a.n_spec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fix_round, dim3(n_wg), dim3(kPipeWG), 0, st, t, a);
+  return hipGetLastError();
+}
+
+}  // namespace sst

@@ -110,6 +110,14 @@ def classify(obs, offsets, su_seq, dp_table, breakage_dict, intensity=None, inte
     return Classified(spec[rows], su[rows], ob[rows], frag[rows], brk[rows], sing, names, off, len(su), len(keep))
 
 
+def subset(c: Classified, keep):
+    """The rows of c where keep is set (e.g. a fixpoint's surviving rows)."""
+    idx = np.flatnonzero(np.asarray(keep, dtype=bool))
+    off = np.searchsorted(c.spec[idx], np.arange(len(c.offsets)))
+    return Classified(c.spec[idx], c.su[idx], c.obs[idx], c.frag[idx], c.brk[idx], c.singleton[idx], c.names, off,
+                      c.n_valid_queries, c.n_singleton_queries)
+
+
 def _sides(c: Classified, side):
     """Rows of one side per spectrum (SU order kept): row ids and offsets."""
     m = np.array([side in n for n in c.names], dtype=bool)[c.brk]
@@ -226,6 +234,7 @@ class Fixpoint:
     history: list            # per round: (active spectra [S] bool, alpha [S, 2], alive [rows]) when recorded
     last: dict               # spectrum-major arrays of the final round: diff, thr, spec, kind, status, count,
     #                          rowmask, range, keep
+    queries: list = None     # per round: (explain queries, is_valid queries)
 
 
 def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolerance=MATCHING_THRESHOLD,
@@ -269,6 +278,7 @@ def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolera
     rounds = np.zeros(S, np.int64)
     history = []
     parts = []  # (spectra active in the round, the round's queries and answers)
+    n_queries = []
     pop = lambda m: np.array([bin(int(a)).count("1") + bin(int(b)).count("1") for a, b in m], dtype=np.int64)
     while active.any():
         rows = np.flatnonzero(alive & active[c.spec])
@@ -293,10 +303,11 @@ def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolera
         if (v < 0).any():
             raise NotImplementedError("is_valid_mass raised on a reduced table (window past its extent)")
         alive[rows[v != 1]] = False
+        n_queries.append((len(d), len(rows)))
         if record:
             history.append((active.copy(), alpha.copy(), alive.copy()))
         active &= changed
-    return Fixpoint(alpha, alive, rounds, history, _final_round(parts, S))
+    return Fixpoint(alpha, alive, rounds, history, _final_round(parts, S), n_queries)
 
 
 def _final_round(parts, S):

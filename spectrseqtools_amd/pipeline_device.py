@@ -1,0 +1,160 @@
+"""Config 5 with every stage's arrays in HBM: classify_fragments
+and the filter_by_explanation fixpoint over many spectra, driven from the
+host one launch per stage / round (sst_classify_rows_device,
+sst_fix_round_device, sst_valid_rows_alpha_device; kernels in
+csrc/sst_pipe.hip and csrc/sst_alpha.hip).  The host only loops the rounds
+(one 4-byte read per round: how many spectra are still reducing).
+
+Rows of spectrum g sit in slots 4 * peak_off[g] + i (i < rows[g]), in the
+SU order of its classify_fragments frame, so a row's slot offset is the
+`index` Predictor.predict gives it (prediction.py:68-72).  PyTorch provides
+the device memory only; every computation is the library's.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native
+from .masses import MATCHING_THRESHOLD, PHOSPHATE_LINK_MASS
+from .pipeline import mask_rows, row_masks
+
+ERR_BITS = {1: "a spectrum has more than 512 peaks", 2: "a spectrum has more than 2048 rows",
+            4: "a window outside the pair class", 8: "is_valid_mass raised (a window past a table's end)",
+            16: "an explanation dict too large for the LDS hash", 32: "rows out of mass order"}
+
+
+def _check_err(err):
+    e = int(err.item())
+    if e:
+        raise _native.EngineError("device pipeline: " + "; ".join(v for k, v in ERR_BITS.items() if e & k))
+
+
+@dataclass
+class DeviceRows:
+    """classify_fragments' frames of a batch, on the device."""
+    peak_off: object   # torch int64 [S + 1]
+    su: object         # torch f64 [4 P] row slots
+    obs: object
+    meta: object       # torch int32: breakage | sides << 2 | singleton << 4 | peak << 8
+    alive: object      # torch uint8
+    rows: object       # torch int32 [S]
+    valid: object      # torch int8 [4 P] A7 codes (breakage-major) or None
+    names: list        # breakage label per code
+
+
+def classify_device(dp_table, obs, offsets, su_seq, breakage_dict, intensity=None, intensity_cutoff=0.5e6,
+                    mass_cutoff=50000, keep_valid=False, device=None):
+    """Stage 1 on the device.  obs: every spectrum's peaks in ascending mass
+    order (spectrum g: obs[offsets[g]:offsets[g+1]]), su_seq[g] its
+    SequenceInformation.su_mass."""
+    import torch
+
+    dev = device or torch.device("cuda", dp_table.device_table.engine.device)
+    obs_t = torch.as_tensor(np.ascontiguousarray(obs, dtype=np.float64), device=dev)
+    off_t = torch.as_tensor(np.ascontiguousarray(offsets, dtype=np.int64), device=dev)
+    su_t = torch.as_tensor(np.ascontiguousarray(su_seq, dtype=np.float64), device=dev)
+    int_t = None if intensity is None else torch.as_tensor(np.ascontiguousarray(intensity, dtype=np.float64),
+                                                           device=dev)
+    P, S = len(obs), len(offsets) - 1
+    weights = list(breakage_dict.keys())
+    names = [breakage_dict[w][0] for w in weights]
+    shifts = np.array([w * dp_table.precision for w in weights], dtype=np.float64)
+    sides = np.array([("START" in n) | (("END" in n) << 1) for n in names], dtype=np.uint8)
+    max_w = _max_weight()
+    su = torch.empty(max(1, 4 * P), dtype=torch.float64, device=dev)
+    ob = torch.empty_like(su)
+    meta = torch.empty(max(1, 4 * P), dtype=torch.int32, device=dev)
+    alive = torch.zeros(max(1, 4 * P), dtype=torch.uint8, device=dev)
+    rows = torch.zeros(max(1, S), dtype=torch.int32, device=dev)
+    valid = torch.empty(max(1, len(weights) * P), dtype=torch.int8, device=dev) if keep_valid else None
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    eng = dp_table.device_table.engine
+    torch.cuda.synchronize(dev)
+    eng.check(eng._lib.sst_classify_rows_device(
+        dp_table.device_table.handle, obs_t.data_ptr(), off_t.data_ptr(), S, P,
+        None if int_t is None else int_t.data_ptr(), float(intensity_cutoff), float(mass_cutoff), su_t.data_ptr(),
+        _native._ptr(shifts), _native._ptr(sides), len(shifts), float(max_w), float(dp_table.tolerance),
+        float(dp_table.precision), None if valid is None else valid.data_ptr(), su.data_ptr(), ob.data_ptr(),
+        meta.data_ptr(), alive.data_ptr(), rows.data_ptr(), err.data_ptr()), "sst_classify_rows_device")
+    eng.synchronize()
+    _check_err(err)
+    return DeviceRows(off_t, su, ob, meta, alive, rows, valid, names)
+
+
+def _max_weight(explanation_masses=None):
+    from .masses import EXPLANATION_MASSES
+
+    em = explanation_masses if explanation_masses is not None else EXPLANATION_MASSES
+    return max(em.get_column("monoisotopic_mass").to_list()) + PHOSPHATE_LINK_MASS
+
+
+@dataclass
+class DeviceFixpoint:
+    alpha: np.ndarray     # [S, 2] u64 final alphabets (row masks of the full table)
+    rounds: np.ndarray    # [S]
+    queries: np.ndarray   # [S] explain queries over all rounds
+    history: list         # per round (recorded): (active [S] bool, alpha [S, 2], alive slots)
+    n_rounds: int
+
+
+def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=MATCHING_THRESHOLD, record=False):
+    """Stage 2 on the device: Predictor.filter_by_explanation (prediction.py:
+    170-202) for every spectrum, one sst_fix_round_device + one
+    sst_valid_rows_alpha_device launch per round, until no alphabet shrinks.
+    max_len[s] bounds the budgets (checked as in pipeline.filter_fixpoint)."""
+    import torch
+
+    masses = dp_table.masses
+    N = len(masses)
+    S = len(rows.rows)
+    dev = rows.su.device
+    is_mod = np.array([m.is_modification for m in masses])
+    rate = np.array([m.modification_rate for m in masses], dtype=np.float64)
+    max_len = np.broadcast_to(np.asarray(max_len, dtype=np.int64), (S,))
+    A = np.array([round(dp_table.seq.modification_rate * int(L)) for L in max_len], dtype=np.int64)
+    cap_min = np.array([min([round(int(L) * r) for r in rate[is_mod]] or [2]) for L in max_len], dtype=np.int64)
+    if (A < 2).any() or (cap_min < 2).any():
+        raise NotImplementedError("fixpoint_device: budgets that can bind on pair windows (max_len too small)")
+    full = np.zeros((1, N), bool)
+    full[0, 1:] = True
+    alpha = torch.as_tensor(np.repeat(row_masks(full), S, axis=0).view(np.int64), device=dev).contiguous()
+    alpha_next = torch.empty_like(alpha)
+    active = torch.ones(S, dtype=torch.uint8, device=dev)
+    active_next = torch.empty_like(active)
+    rounds = torch.zeros(S, dtype=torch.int32, device=dev)
+    queries = torch.zeros(S, dtype=torch.int32, device=dev)
+    n_active = torch.zeros(1, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    eng = dp_table.device_table.engine
+    L = eng._lib
+    h = dp_table.device_table.handle
+    history = []
+    n_rounds = 0
+    max_w = _max_weight()
+    torch.cuda.synchronize(dev)
+    while True:
+        n_active.zero_()
+        torch.cuda.synchronize(dev)
+        eng.check(L.sst_fix_round_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(), rows.obs.data_ptr(),
+                                         rows.meta.data_ptr(), rows.alive.data_ptr(), rows.rows.data_ptr(),
+                                         alpha.data_ptr(), alpha_next.data_ptr(), active.data_ptr(),
+                                         active_next.data_ptr(), rounds.data_ptr(), queries.data_ptr(),
+                                         n_active.data_ptr(), float(max_w), float(tolerance),
+                                         float(dp_table.precision), err.data_ptr()), "sst_fix_round_device")
+        eng.check(L.sst_valid_rows_alpha_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(),
+                                                rows.obs.data_ptr(), rows.rows.data_ptr(), alpha_next.data_ptr(),
+                                                active.data_ptr(), rows.alive.data_ptr(), float(tolerance),
+                                                float(dp_table.precision), err.data_ptr()),
+                  "sst_valid_rows_alpha_device")
+        eng.synchronize()
+        n_rounds += 1
+        if record:
+            history.append((active.cpu().numpy().astype(bool), alpha_next.cpu().numpy().view(np.uint64).copy(),
+                            rows.alive.cpu().numpy().astype(bool)))
+        _check_err(err)
+        alpha, alpha_next = alpha_next, alpha
+        active, active_next = active_next, active
+        if int(n_active.item()) == 0:
+            break
+    return DeviceFixpoint(alpha.cpu().numpy().view(np.uint64).copy(), rounds.cpu().numpy(),
+                          queries.cpu().numpy(), history, n_rounds)

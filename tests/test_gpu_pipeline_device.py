@@ -1,0 +1,97 @@
+"""GPU tests of the device-resident config-5 stages (pipeline_device:
+sst_classify_rows_device, sst_fix_round_device, sst_valid_rows_alpha_device):
+  * on the reference's 8 test spectra: the classified rows equal the
+    reference's own classify_fragments frame row for row, and every
+    filter_by_explanation round's alphabet and kept fragments equal the
+    reference's (tests/golden/callers.json.gz);
+  * on synthetic spectra: rows, final alphabets, surviving rows and round
+    counts equal the host-driven columnar stages (pipeline.classify /
+    filter_fixpoint, pinned to the per-spectrum mirrors in the CPU suite)."""
+import numpy as np
+import pytest
+
+import _callers_checks as C
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+SPECTRA = ["test_01", "test_02", "test_03", "test_04", "test_05", "test_06", "test_07", "test_08"]
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from spectrseqtools_amd import _native
+
+    return _native.get_engine(0)
+
+
+@pytest.fixture(scope="module")
+def callers():
+    return load_golden("callers.json.gz")
+
+
+@pytest.mark.parametrize("tc", SPECTRA)
+def test_device_classify_and_fixpoint_vs_reference(engine, callers, tc):
+    from spectrseqtools_amd import pipeline_device as PD
+    from spectrseqtools_amd.masses import build_breakage_dict
+    from spectrseqtools_amd.pipeline import mask_rows
+
+    rec = callers[tc]
+    dp = C.make_dp(rec["ctx"], engine=engine)
+    cols = rec["input"]["columns"]
+    inp = {c: [r[i] for r in rec["input"]["rows"]] for i, c in enumerate(cols)}
+    obs = np.asarray(inp["observed_mass" if "observed_mass" in inp else "neutral_mass"], dtype=np.float64)
+    inten = np.asarray(inp["intensity"], dtype=np.float64) if "intensity" in inp else None
+    perm = np.argsort(obs, kind="stable")  # the device stage takes a mass-sorted peak list
+    bd = build_breakage_dict(*rec["tags"])
+    rows = PD.classify_device(dp, obs[perm], [0, len(obs)], [dp.seq.su_mass], bd,
+                              intensity=None if inten is None else inten[perm],
+                              intensity_cutoff=rec["intensity_cutoff"])
+    n = int(rows.rows.cpu()[0])
+    want = rec["classify"]
+    wc = {c: [r[i] for r in want["rows"]] for i, c in enumerate(want["columns"])}
+    assert n == len(want["rows"])
+    meta = rows.meta.cpu().numpy()[:n].astype(np.int64)
+    assert rows.su.cpu().numpy()[:n].tolist() == wc["standard_unit_mass"]
+    assert rows.obs.cpu().numpy()[:n].tolist() == wc["observed_mass"]
+    assert [rows.names[m & 3] for m in meta] == wc["breakage"]
+    assert [bool((m >> 4) & 1) for m in meta] == wc["is_singleton"]
+    assert perm[meta >> 8].tolist() == wc["fragment_index"]
+    fx = PD.fixpoint_device(dp, rows, [dp.seq.max_len], record=True)
+    rounds = rec["filter"]["rounds"]
+    assert fx.n_rounds == len(rounds) == int(fx.rounds[0])
+    for k, (act, alpha, alive) in enumerate(fx.history):
+        rr = mask_rows(alpha, len(dp.masses))[0]
+        assert [0] + [dp.masses[r].mass for r in range(1, len(dp.masses)) if rr[r]] == rounds[k]["masses"], k
+        assert np.flatnonzero(alive[:n]).tolist() == rounds[k]["kept_index"], k
+
+
+def test_device_stages_equal_host_driven(engine):
+    from spectrseqtools_amd import pipeline, pipeline_device as PD
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict
+    from spectrseqtools_amd.synthetic import make_spectra
+
+    b = make_spectra(600, seed=31)
+    obs = b.observed[np.lexsort((b.observed, b.spectrum))]
+    bd = build_breakage_dict(555.1294, 455.1491)
+    w_full = [k for k, v in bd.items() if "START_END" in v][0]
+    su_seq = b.seq_mass - w_full * TOLERANCE
+    seq = SequenceInformation(max_len=20, su_mass=float(su_seq[0]), obs_mass=float(b.seq_mass[0]),
+                              modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=engine)
+    max_len = pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:]))
+    c = pipeline.classify(obs, b.offsets, su_seq, dp, bd)
+    rows = PD.classify_device(dp, obs, b.offsets, su_seq, bd)
+    cnt = rows.rows.cpu().numpy()
+    assert np.array_equal(cnt, np.diff(c.offsets))
+    slot = (4 * b.offsets[:-1])[c.spec] + (np.arange(len(c.spec)) - c.offsets[c.spec])
+    assert np.array_equal(rows.su.cpu().numpy()[slot], c.su)
+    meta = rows.meta.cpu().numpy()[slot].astype(np.int64)
+    assert np.array_equal(meta & 3, c.brk) and np.array_equal(((meta >> 4) & 1).astype(bool), c.singleton)
+    fx_h = pipeline.filter_fixpoint(c, dp, max_len, EXPLANATION_MASSES)
+    fx_d = PD.fixpoint_device(dp, rows, max_len)
+    assert np.array_equal(fx_d.alpha, fx_h.alpha)
+    assert np.array_equal(fx_d.rounds, fx_h.rounds)
+    assert np.array_equal(rows.alive.cpu().numpy()[slot].astype(bool), fx_h.alive)
+    assert int(fx_d.queries.sum()) == sum(q[0] for q in fx_h.queries)

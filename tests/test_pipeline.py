@@ -84,3 +84,30 @@ def test_bin_queries_equal_per_spectrum(setup):
             assert got == want, (s, side)
             n_total += len(want)
     assert n_total > 0
+
+
+def test_fixpoint_equals_per_spectrum_mirror(setup):
+    """pipeline.filter_fixpoint over synthetic spectra == Predictor.
+    filter_by_explanation run spectrum by spectrum (each with its own table
+    and alphabet reductions): final alphabets, surviving fragments, and the
+    final explanation dict's keys."""
+    from _callers_checks import prepared
+
+    batch, dp, c, frames = setup
+    S = 6
+    sub = pipeline.subset(c, c.spec < S)
+    sub.offsets = sub.offsets[:S + 1]
+    fx = pipeline.filter_fixpoint(sub, dp, [dp.seq.max_len] * S, EXPLANATION_MASSES)
+    alpha_rows = pipeline.mask_rows(fx.alpha, len(dp.masses))
+    for s in range(S):
+        dps = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                      precision=TOLERANCE, seq=SequenceInformation(
+                                          max_len=dp.seq.max_len, su_mass=dp.seq.su_mass, obs_mass=dp.seq.obs_mass,
+                                          modification_rate=0.5))
+        frags, expl = Predictor(dps, EXPLANATION_MASSES).filter_by_explanation(prepared(frames[s]))
+        assert [m.mass for m in dps.masses] == [0] + [dp.masses[r].mass for r in range(1, len(dp.masses))
+                                                      if alpha_rows[s, r]], s
+        r = slice(sub.offsets[s], sub.offsets[s + 1])
+        assert np.flatnonzero(fx.alive[r]).tolist() == frags.get_column("index").to_list(), s
+        m = (fx.last["spec"] == s) & fx.last["keep"]
+        assert sorted(map(repr, fx.last["diff"][m].tolist())) == sorted(map(repr, expl)), s

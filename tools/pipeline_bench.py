@@ -4,18 +4,24 @@ stages over many synthetic spectra, batched on the GPU engine
 (spectrseqtools_amd/pipeline.py):
 
   stage 1  classify_fragments      is_valid (peaks x 4 breakages) + is_singleton
-  stage 2  first filter_by_explanation round: sliding-window SU differences of
-           both sides + singleton masses -> explain
-  stage 3  skeleton bins: each side's bins, first bin's whole masses and every
-           later bin against its predecessor -> explain (deep windows: the
-           deferred DFS kernels)
+  stage 2  filter_by_explanation, every round of every spectrum batched
+           (pipeline.filter_fixpoint): sliding-window SU differences of both
+           sides + singleton masses explained against each spectrum's own
+           reduced alphabet (k_pairs_alpha), the dict's observed rows
+           (sst_dict_union), alphabet reduction as row masks, is_valid of the
+           remaining fragments on the reduced tables (k_valid_alpha); until
+           every spectrum's alphabet is stable
+  stage 3  skeleton bins on the surviving fragments and reduced alphabets:
+           each side's bins, first bin's whole masses and every later bin
+           against its predecessor -> explain (pair-class windows:
+           k_pairs_alpha; the rest are counted)
 
 One process per GPU (torch.distributed.run for N > 1, spectra sharded by
 rank, no collective in the data path); every stage is timed over all of this
 rank's spectra with barriers around it, max over ranks.  The full alphabet's
-table serves every spectrum (the reference's per-spectrum alphabet reduction
-is a table rebuild, timed separately: `reduction_rebuild_ms`); each explain
-call covers the spectra of one max_len (their row caps and budget).  Results
+table serves every spectrum; the per-spectrum reduced alphabets are row
+masks over it (no table is rebuilt; a reference-style rebuild is timed
+separately: `reduction_rebuild_ms`).  Results
 come back to the host (status, counts, payload: PCIe included).  The
 reference Python cannot run on the GPU box; `reference_estimate_s` prices the
 same query counts at its measured single-core rates (is_valid
@@ -39,7 +45,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spectra", type=int, default=100000, help="spectra per GPU")
     ap.add_argument("--seed", type=int, default=7)
-    ap.add_argument("--cap", type=int, default=1 << 16, help="candidate cap per query (OVERFLOW beyond)")
     args = ap.parse_args()
 
     import torch
@@ -84,38 +89,6 @@ def main():
     min_int = min(m.mass for m in dp.masses[1:])
     max_len = pipeline.max_len_of(su_seq, TOLERANCE, min_int)  # cli.py:158-170
 
-    def explain_grouped(q):
-        """One engine call per max_len group; returns statuses, counts, timing.
-        Groups from the spectra's max_len (one radix sort of the queries' small
-        group ids, not one full scan of the queries per group)."""
-        st = np.zeros(len(q.diff), np.int8)
-        cnt = np.zeros(len(q.diff), np.uint64)
-        lens_u, spec_gid = np.unique(max_len, return_inverse=True)
-        if len(q.spec) and (np.diff(q.spec) >= 0).all():  # spectrum-major: a group is its spectra's ranges
-            qoff = np.searchsorted(q.spec, np.arange(len(max_len) + 1))
-            groups = []
-            for gi in range(len(lens_u)):
-                sp = np.flatnonzero(spec_gid == gi)
-                ln = qoff[sp + 1] - qoff[sp]
-                groups.append(np.repeat(qoff[sp] - (np.cumsum(ln) - ln), ln) + np.arange(int(ln.sum())))
-        else:
-            gid = spec_gid.astype(np.uint16)[q.spec]
-            order = np.argsort(gid, kind="stable")  # radix sort (16-bit keys)
-            cuts = np.concatenate([[0], np.cumsum(np.bincount(gid, minlength=len(lens_u)))])
-            groups = [order[cuts[gi]:cuts[gi + 1]] for gi in range(len(lens_u))]
-        calls = 0
-        for gi, L in enumerate(lens_u):
-            m = groups[gi]
-            if len(m) == 0:
-                continue
-            dp.seq = SequenceInformation(max_len=int(L), su_mass=0.0, obs_mass=0.0, modification_rate=0.5)
-            A = round(dp.seq.modification_rate * dp.seq.max_len)  # common.py:55
-            r = dp.device_table.explain(q.diff[m], q.thr[m], dp.tolerance, dp.precision, A, cap=args.cap)
-            st[m] = r.status
-            cnt[m] = r.count
-            calls += 1
-        return st, cnt, calls
-
     stages = {}
     engine.profile(True)
     barrier()
@@ -128,23 +101,29 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    q2 = pipeline.su_diff_queries(c, EXPLANATION_MASSES)
-    st2, cnt2, calls2 = explain_grouped(q2)
+    fx = pipeline.filter_fixpoint(c, dp, max_len, EXPLANATION_MASSES)
     barrier()
-    stages["su_diffs"] = {"s": tmax(time.perf_counter() - t0), "queries": len(q2.diff), "engine_calls": calls2,
-                          "with_candidates": int(((st2 == 2) | (st2 == -2)).sum()),
-                          "candidates": int(cnt2[st2 == 2].sum())}
-    stages["su_diffs"]["kernels"] = {_native.KERNEL_NAMES.get(k, str(k)): v for k, v in engine.profile_read().items()}
+    alpha_u = np.unique(fx.alpha, axis=0)
+    stages["fixpoint"] = {"s": tmax(time.perf_counter() - t0), "rounds_max": int(fx.rounds.max()),
+                          "rounds_histogram": {int(k): int(v) for k, v in zip(*np.unique(fx.rounds, return_counts=True))},
+                          "final_round_queries": int(len(fx.last.get("diff", []))),
+                          "explain_queries_per_round": [int(x[0]) for x in fx.queries],
+                          "is_valid_queries_per_round": [int(x[1]) for x in fx.queries],
+                          "rows_kept": int(fx.alive.sum()), "rows_in": int(len(fx.alive)),
+                          "distinct_alphabets": int(len(alpha_u)),
+                          "mean_alphabet_rows": float(pipeline.mask_rows(fx.alpha, len(dp.masses)).sum(1).mean() + 1)}
+    stages["fixpoint"]["kernels"] = {_native.KERNEL_NAMES.get(k, str(k)): v for k, v in engine.profile_read().items()}
 
     barrier()
     t0 = time.perf_counter()
-    q3 = pipeline.bin_queries(c)
-    st3, cnt3, calls3 = explain_grouped(q3)
+    c3 = pipeline.subset(c, fx.alive)
+    q3 = pipeline.bin_queries(c3)
+    st3, cnt3, _, _ = dp.device_table.explain_pairs_alpha(q3.diff, q3.thr, q3.spec, fx.alpha, dp.tolerance,
+                                                          dp.precision)
     barrier()
-    stages["bins"] = {"s": tmax(time.perf_counter() - t0), "queries": len(q3.diff), "engine_calls": calls3,
-                      "with_candidates": int(((st3 == 2) | (st3 == -2)).sum()),
-                      "overflow": int((st3 == -2).sum()), "candidates": int(cnt3[st3 == 2].sum())}
-    stages["bins"]["kernels"] = {_native.KERNEL_NAMES.get(k, str(k)): v for k, v in engine.profile_read().items()}
+    stages["bins"] = {"s": tmax(time.perf_counter() - t0), "queries": len(q3.diff),
+                      "pair_class": int((st3 != -10).sum()), "not_pair_class": int((st3 == -10).sum()),
+                      "with_candidates": int((st3 == 2).sum()), "candidates": int(cnt3[st3 == 2].sum())}
     engine.profile(False)
 
     # per-spectrum alphabet reduction = a table rebuild (canonical + 3 mods)
@@ -166,12 +145,13 @@ def main():
         peaks_all, spectra_all = (int(x) for x in t.tolist())
     else:
         peaks_all, spectra_all = peaks, args.spectra
-    ref_est = (stages["classify"]["is_valid_queries"] / 70e3 +
-               (stages["su_diffs"]["queries"] + stages["bins"]["queries"]) / 4.0e3)
+    ref_est = ((stages["classify"]["is_valid_queries"] + sum(x[1] for x in fx.queries)) / 70e3 +
+               (sum(x[0] for x in fx.queries) + stages["bins"]["queries"]) / 4.0e3)
     if rank == 0:
         print(json.dumps({
-            "workload": "config5: explanation stages of the prediction pipeline (classify_fragments, first "
-                        "filter_by_explanation round, skeleton bin queries) over synthetic spectra, full alphabet",
+            "workload": "config5: explanation stages of the prediction pipeline (classify_fragments, the "
+                        "filter_by_explanation fixpoint with per-spectrum alphabets, skeleton bin queries on the "
+                        "reduced alphabets) over synthetic spectra",
             "n_gpus": world, "spectra": spectra_all, "peaks": peaks_all,
             "stages": stages, "total_s": total_s,
             "spectra_per_s": spectra_all / total_s, "peaks_per_s": peaks_all / total_s,
