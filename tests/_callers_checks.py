@@ -233,3 +233,36 @@ def check_fixpoint(rec, dp):
     for k in want_d:
         assert got[k] == want_d[k], k
     return fx
+
+
+def check_skeleton_vs_reference(rec, dp, frags, expl):
+    """SkeletonBuilder._predict_skeleton (skeleton_building.py:114-196) per
+    side and select_sequence_length_with_jaccard (:315-370) with its two
+    length bounds == the reference's own results (callers.json.gz)."""
+    from spectrseqtools_amd.skeleton_building import SkeletonBuilder, combine_skeleton_sequences
+
+    want = rec["skeleton"]
+    sb = SkeletonBuilder(explanations=expl, dp_table=dp)
+    sks = {}
+    for side in ("START", "END"):
+        sub = frags.filter_mask([side in b for b in frags.get_column("breakage").to_list()])
+        sk, fr = sb._predict_skeleton(Frame(sub.to_dict()), [set() for _ in range(dp.seq.max_len)])
+        w = want[side]
+        assert [sorted(p) for p in sk] == w["skeleton"], side
+        assert fr.get_column("index").to_list() == w["kept_index"], side
+        assert fr.get_column("min_end").to_list() == w["min_end"], side
+        assert fr.get_column("max_end").to_list() == w["max_end"], side
+        sks[side] = sk
+    start_sk, end_sk = sks["START"], sks["END"][::-1]
+    j = want["jaccard"]
+    try:
+        seq_len = sb.select_sequence_length_with_jaccard(start_skeleton=start_sk, end_skeleton=end_sk)
+        err = None
+    except Exception as e:  # noqa: BLE001 -- the reference raises a bare Exception here too
+        seq_len, err = None, f"{type(e).__name__}: {e}"
+    assert [m.mass for m in dp.masses] == j["masses"]
+    assert err == j["error"]
+    if seq_len is not None:
+        assert seq_len == j["seq_len"]
+        assert [sorted(p) for p in combine_skeleton_sequences(seq_len, start_sk, end_sk)] == j["combined"]
+    return seq_len

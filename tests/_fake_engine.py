@@ -124,6 +124,19 @@ class FakeDeviceTable:
             out[a:b] = oracle.is_valid_batch(tab, 32, masses[a:b], thresholds[a:b], tolerance, precision=precision)
         return out
 
+    def length_bound(self, su_masses, obs_masses, tolerance, precision, max_len, max_mods, direction,
+                     exact_only=False):
+        out = np.zeros(len(su_masses), np.int64)
+        st = np.zeros(len(su_masses), np.int8)
+        for i, (su, ob) in enumerate(zip(su_masses, obs_masses)):
+            v = oracle.length_bound(self.table, 32, self.alph, su, ob, tolerance, int(max_len), int(max_mods),
+                                    direction, precision=precision)
+            if v is None:
+                st[i] = _native.SST_OUT_OF_TABLE
+            else:
+                out[i] = v
+        return out, st
+
     def explain(self, masses, thresholds, tolerance, precision, max_mods, with_memo=True, cap=2 ** 32):
         self.calls += 1
         masses = np.asarray(masses, dtype=np.float64)

@@ -120,3 +120,20 @@ def test_fixpoint_vs_reference(fake, callers, tc):
     rec = callers[tc]
     dp = C.make_dp(rec["ctx"])
     C.check_fixpoint(rec, dp)
+
+
+@pytest.mark.parametrize("tc", SPECTRA)
+def test_skeleton_vs_reference(tc):
+    """The skeleton walk and the Jaccard length selection against the
+    reference's own results, under the reference run's hash seed (child
+    process: oracle-backed tables)."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PYTHONHASHSEED="0")
+    p = subprocess.run([sys.executable, os.path.join(here, "_skeleton_check.py"), tc, "cpu"], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert f"skeleton ok {tc}" in p.stdout

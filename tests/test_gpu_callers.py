@@ -67,6 +67,23 @@ def test_fixpoint_vs_reference(engine, callers, tc):
     C.check_fixpoint(rec, dp)
 
 
+@pytest.mark.parametrize("tc", SPECTRA)
+def test_skeleton_vs_reference(tc):
+    """The batched skeleton walk and the Jaccard length selection (its two
+    length bounds on the GPU) against the reference's own results, under the
+    reference run's hash seed (child process on GPU 0)."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PYTHONHASHSEED="0")
+    p = subprocess.run([sys.executable, os.path.join(here, "_skeleton_check.py"), tc, "gpu"], env=env,
+                       capture_output=True, text=True, timeout=250)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert f"skeleton ok {tc}" in p.stdout
+
+
 def test_classify_batch(engine, callers):
     groups = {tc: (C.make_dp(callers[tc]["ctx"], engine=engine), [callers[tc]]) for tc in ("test_01", "test_05")}
     C.check_classify_batch(None, groups)
