@@ -50,14 +50,13 @@ def windows(masses, thr, prec, limit):
 
 
 def result_digest(r):
-    """SHA-256 over a fetched result: status bytes, per-query counts and
-    offsets (from the hit list) and the dense payload."""
-    import hashlib
+    """SHA-256 of a fetched result's answers: status bytes, per-query counts
+    and every query's candidate bytes (parallel.canonical_digest: a result
+    object reused across batches keeps stale pad bytes between payload
+    records, which are layout, not answers)."""
+    from spectrseqtools_amd.parallel import canonical_digest
 
-    h = hashlib.sha256()
-    for a in (r.status, r.count, r.offset, r.payload):
-        h.update(np.ascontiguousarray(a).tobytes())
-    return h.hexdigest()
+    return canonical_digest(r.status, r.count, r.offset, r.payload)
 
 
 def build_workload(n_spectra, seed, dp):

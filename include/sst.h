@@ -400,9 +400,9 @@ int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* 
  * with every array in HBM.  Rows of spectrum g live in slots
  * 4 * d_peak_off[g] + i, i < d_rows[g] (d_rows_* arrays of 4 * n_peaks):
  * su, observed mass, meta = breakage | sides << 2 | is_singleton << 4 | peak
- * position << 8, alive.  Peaks in ascending mass order, <= 512 per spectrum;
+ * position << 8, alive.  Peaks in ascending mass order, <= 1024 per spectrum;
  * shifts / sides as sst_step_rows_device.  d_err collects | 1 a spectrum over
- * 512 peaks, 2 over 2048 rows, 4 a window outside the pair class, 8 a window
+ * 1024 peaks, 2 over 2048 rows, 4 a window outside the pair class, 8 a window
  * past a table's end (the reference raises), 16 a dict too large for the LDS
  * hash, 32 rows out of mass order; the caller checks it. */
 /* classify_fragments (fragment_classification.py:17-101): A7 into d_valid_out

@@ -348,7 +348,7 @@ struct RowsArgs {
 hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, size_t dyn, hipStream_t st);
 
 // config 5 on the device (sst_pipe.hip)
-constexpr int kPipeMaxPeaks = 512;   // peaks per spectrum the classify workgroup holds
+constexpr int kPipeMaxPeaks = 1024;  // peaks per spectrum the classify workgroup holds
 constexpr int kPipeMaxRows = 2048;   // rows per spectrum (4 breakages)
 struct PipeArgs {
   const double* obs;          // [n_peaks], sorted within each spectrum

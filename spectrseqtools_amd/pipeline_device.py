@@ -18,7 +18,7 @@ from . import _native
 from .masses import MATCHING_THRESHOLD, PHOSPHATE_LINK_MASS
 from .pipeline import mask_rows, row_masks
 
-ERR_BITS = {1: "a spectrum has more than 512 peaks", 2: "a spectrum has more than 2048 rows",
+ERR_BITS = {1: "a spectrum has more than 1024 peaks", 2: "a spectrum has more than 2048 rows",
             4: "a window outside the pair class", 8: "is_valid_mass raised (a window past a table's end)",
             16: "an explanation dict too large for the LDS hash", 32: "rows out of mass order"}
 
