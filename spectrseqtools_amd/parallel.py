@@ -149,8 +149,10 @@ def scan_order_key(q, n, n_wg):
     """Sort key of queries q (int64) in the pair scan's hit order for a batch
     of n queries on n_wg workgroups: workgroup, its wave, the wave's tile
     round, lane (include/sst.h, sst_result_pair_hits; sst_kernels.hip
-    k_explain_scan's tile order)."""
+    k_explain_scan's tile order); n_wg = 0: query order (the rows step)."""
     q = np.asarray(q, dtype=np.int64)
+    if n_wg == 0:  # a rows-step result (sst_step_rows_device): its hits come in query order
+        return q
     n_waves = SCAN_WAVES_PER_WG * n_wg
     rounds = max(1, -(-((n + 63) // 64) // n_waves))
     tile, lane = q >> 6, q & 63

@@ -34,3 +34,13 @@ def test_world_size_2_gloo():
     for rank, (p, out) in enumerate(zip(procs, outs)):
         assert p.returncode == 0, f"rank {rank} failed:\n{out}"
         assert f"ok rank {rank}" in out
+
+
+def test_scan_order_key_query_order():
+    """n_wg = 0 (a rows-step result): the pair hits come in query order."""
+    import numpy as np
+
+    from spectrseqtools_amd.parallel import scan_order_key
+
+    q = np.array([5, 1, 9, 3])
+    assert scan_order_key(q, 100, 0).tolist() == q.tolist()
