@@ -315,6 +315,7 @@ hipError_t launch_valid_alpha(const AlphaArgs& a, int64_t n_spec, hipStream_t st
 // the step from the peaks (sst_rows.hip)
 constexpr int kRowsMaxPeaks = 1024;   // peaks per spectrum a workgroup holds
 constexpr int kRowsMaxSide = 2048;    // rows per side (two breakages per side at most ... x 2 headroom)
+constexpr int kRowsWaveMaxPeaks = 160;  // spectra up to this many peaks: one wave each (k_rows_*_w)
 struct RowsArgs {
   const double* obs;          // [n_peaks] sorted within each spectrum
   const int64_t* peak_off;    // [n_spec + 1]
@@ -336,6 +337,8 @@ struct RowsArgs {
   uint64_t* ctl;              // [4] totals
   uint32_t* err;
   uint32_t* done;
+  uint32_t* tickets;          // [3] next spectrum of k_rows_count_w / k_rows_emit_w, big-spectrum count
+  uint32_t* big;              // [n_spec] spectra over kRowsWaveMaxPeaks peaks (the block kernels')
   uint64_t cap_queries, cap_bytes;
   int8_t* status;
   uint4* hits;

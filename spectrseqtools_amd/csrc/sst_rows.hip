@@ -40,6 +40,16 @@
 
 namespace sst {
 
+#ifdef SST_ROWS_PROF  // phase clocks of the wave kernels (diagnostic builds; printed by the last workgroup)
+__device__ unsigned long long g_rows_prof[8];
+#define RPROF_T(v) const uint64_t v = wall_clock64()
+#define RPROF_ADD(i, d) \
+  if ((threadIdx.x & 63) == 0) atomicAdd(&g_rows_prof[i], (unsigned long long)(d))
+#else
+#define RPROF_T(v)
+#define RPROF_ADD(i, d)
+#endif
+
 namespace {
 
 constexpr int kRowsWG = 1024;
@@ -254,9 +264,12 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_count(TableArgs t, RowsArgs a)
   extern __shared__ uint32_t dyn[];
   __shared__ SpecLds L;
   __shared__ uint32_t s_acc[3];
+  const uint32_t n_big = a.tickets[2];  // spectra k_rows_count_w left to the block kernels
+  if (n_big == 0) return;
   PairImg img;
   stage_img(t, dyn, img);
-  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
+  for (uint32_t i = blockIdx.x; i < n_big; i += gridDim.x) {
+    const int64_t g = a.big[i];
     if (!load_spectrum(L, t, a, g, true)) {
       if (threadIdx.x == 0) {
         atomicOr(a.err, 1u);
@@ -306,20 +319,66 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_count(TableArgs t, RowsArgs a)
   }
 }
 
-// exclusive offsets of every spectrum's queries, hits and payload bytes (one
-// workgroup) and the totals
+// exclusive offsets of every spectrum's queries, hits and payload bytes and
+// the totals (one workgroup; chunks of kScanChunk spectra staged through LDS
+// so that loads and stores are coalesced, each thread scanning a contiguous
+// run of kScanPer)
+constexpr int kScanPer = 4;
+constexpr int kScanChunk = kScanPer * kRowsWG;
+
+__device__ __forceinline__ uint64_t block_excl64(uint64_t v, uint64_t* s_w, uint64_t& total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint64_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_w[wv] = incl;
+  __syncthreads();
+  uint64_t base = 0, tot = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+    const uint64_t x = s_w[w];
+    if (w < wv) base += x;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return base + incl - v;
+}
+
 __global__ __launch_bounds__(kRowsWG) void k_rows_scan(RowsArgs a) {
-  __shared__ uint32_t s_w[16];
+  extern __shared__ uint64_t s_buf[];  // [3 * kScanChunk]: the chunk's offsets (its totals staged as u32 first)
+  uint32_t* s_tot = (uint32_t*)s_buf;
+  __shared__ uint64_t s_w[16];
   uint64_t carry[3] = {0, 0, 0};
-  for (int64_t g0 = 0; g0 < a.n_spec; g0 += blockDim.x) {
-    const int64_t g = g0 + threadIdx.x;
-    for (int c = 0; c < 3; ++c) {
-      const uint32_t v = g < a.n_spec ? a.totals[3 * g + c] : 0u;
-      uint32_t tot;
-      const uint32_t ex = block_excl(v, s_w, tot);
-      if (g < a.n_spec) a.offs[3 * g + c] = carry[c] + ex;
-      carry[c] += tot;
-    }
+  for (int64_t c0 = 0; c0 < a.n_spec; c0 += kScanChunk) {
+    const int m = (int)(a.n_spec - c0 < kScanChunk ? a.n_spec - c0 : kScanChunk);
+    for (int i = threadIdx.x; i < 3 * m; i += blockDim.x) s_tot[i] = a.totals[3 * c0 + i];
+    __syncthreads();
+    const int j0 = threadIdx.x * kScanPer;
+    uint32_t v[3 * kScanPer];
+    uint64_t run[3] = {0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < kScanPer; ++j)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        v[3 * j + c] = j0 + j < m ? s_tot[3 * (j0 + j) + c] : 0u;
+        run[c] += v[3 * j + c];
+      }
+    uint64_t base[3], tot[3];
+    for (int c = 0; c < 3; ++c) base[c] = carry[c] + block_excl64(run[c], s_w, tot[c]);  // (syncs: s_tot is free)
+#pragma unroll
+    for (int j = 0; j < kScanPer; ++j)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        if (j0 + j < m) s_buf[3 * (j0 + j) + c] = base[c];
+        base[c] += v[3 * j + c];
+      }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 3 * m; i += blockDim.x) a.offs[3 * c0 + i] = s_buf[i];
+    __syncthreads();
+    for (int c = 0; c < 3; ++c) carry[c] += tot[c];
   }
   if (threadIdx.x == 0) {
     a.ctl[0] = carry[0];
@@ -332,10 +391,12 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_scan(RowsArgs a) {
 __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) {
   extern __shared__ uint32_t dyn[];
   __shared__ SpecLds L;
+  const uint32_t n_big = a.tickets[2];
   PairImg img;
-  stage_img(t, dyn, img);
+  if (n_big) stage_img(t, dyn, img);
   const bool room = !(*(volatile uint32_t*)a.err & 4u);
-  for (int64_t g = blockIdx.x; g < a.n_spec && room; g += gridDim.x) {
+  for (uint32_t i = blockIdx.x; i < n_big && room; i += gridDim.x) {
+    const int64_t g = a.big[i];
     if (a.peak_off[g + 1] - a.peak_off[g] > kRowsMaxPeaks) continue;
     uint64_t qb = a.offs[3 * g], hb = a.offs[3 * g + 1], bb = a.offs[3 * g + 2];
     for (int sd = 0; sd < 2; ++sd) {
@@ -393,6 +454,7 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
   if (s_last && threadIdx.x == 0) {
     __threadfence();
     *a.done = 0;  // the next pass's counters
+    a.tickets[0] = a.tickets[1] = a.tickets[2] = 0;
     const uint32_t err = *(volatile uint32_t*)a.err;
     *a.err = 0;
     uint64_t h[kHdrWords] = {0};
@@ -401,9 +463,401 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
     h[kHdrPass] = a.pass_id;
     h[kHdrQueries] = a.ctl[0];
     h[kHdrRowsErr] = err;
+#ifdef SST_ROWS_PROF
+    printf("rows prof (10 ns ticks, summed over spectra): ticket %llu load %llu merge %llu answer %llu tail %llu n %llu | emit ticket %llu body %llu\n",
+           g_rows_prof[0], g_rows_prof[1], g_rows_prof[2], g_rows_prof[3], g_rows_prof[4], g_rows_prof[5],
+           g_rows_prof[6], g_rows_prof[7]);
+    for (int k = 0; k < 8; ++k) g_rows_prof[k] = 0;
+#endif
     for (int k = 0; k < kHdrWords; ++k) a.hdr[k] = h[k];
     for (int k = 0; k < kHdrWords; ++k)
       __hip_atomic_store(a.hdr_host + k, h[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One wave per spectrum (spectra of <= kRowsWaveMaxPeaks peaks, i.e. every
+// spectrum of a 10..20-mer): a spectrum's phases are short dependent chains
+// (bitset loads, LDS binary searches, pair-list walks), so many spectra must
+// be in flight per CU -- four waves per workgroup, several workgroups per CU,
+// each wave its own spectrum, wave-level prefix sums (no barriers).  The
+// pair list is read through L2 (40 KB, resident); the block kernels above
+// take the larger spectra.
+namespace {
+
+constexpr int kWP = kRowsWaveMaxPeaks;
+constexpr int kWS = 2 * kRowsWaveMaxPeaks;  // rows per side: two breakages per side
+constexpr int kWavesPerWG = 4;
+
+struct WaveLds {
+  double obs[kWP];
+  double su[kWS];
+  double ob[kWS];
+  uint16_t qoff[kWS + 1];  // a side has < 2^16 pairs (kWS (kWS - 1) / 2)
+  uint16_t kidx[4][kWP];
+  uint8_t keep[kWP];
+  uint32_t kcnt[4];
+  uint32_t sstar;
+};
+
+// LDS written by some lanes of the wave, read by others: order the accesses
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t& total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  total = __shfl(incl, 63, 64);
+  return incl - v;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t y = __shfl_xor(v, d, 64);
+    v = y < v ? y : v;
+  }
+  return v;
+}
+
+// A7, filters and the kept rows of every breakage (peak order) of spectrum g
+__device__ void wave_load(WaveLds& L, const TableArgs& t, const RowsArgs& a, int64_t p0, uint32_t P, double su_seq,
+                          bool write_a7) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t p = lane; p < P; p += 64) {
+    const double o = a.obs[p0 + p];
+    L.obs[p] = o;
+    uint8_t kp = 0;
+    for (int k = 0; k < a.n_shifts; ++k) {
+      const double su = o - a.shift[k];
+      double lof, hif;
+      quantise_lean(su, a.tol * o, a.prec, a.rprec, lof, hif);
+      const int8_t code =
+          valid_window(t.valid, t.limit, (int64_t)lof, (int64_t)hif, t.full_lo, t.full_hi, t.first_reach);
+      if (write_a7) a.valid_out[(int64_t)k * a.n_peaks + p0 + p] = code;
+      const bool inten = a.intensity ? a.intensity[p0 + p] > a.intensity_cutoff : true;
+      const bool full = (a.sides[k] & 3) == 3;
+      const bool keep = code == 1 && inten && o < a.mass_cutoff && su < su_seq + a.max_variance &&
+                        (su > su_seq - a.max_variance || !full);
+      kp |= (uint8_t)keep << k;
+    }
+    L.keep[p] = kp;
+  }
+  for (int k = 0; k < a.n_shifts; ++k) {
+    uint32_t carry = 0;
+    for (uint32_t q0 = 0; q0 < P; q0 += 64) {
+      const uint32_t p = q0 + lane;
+      const bool f = p < P && ((L.keep[p] >> k) & 1u);
+      const uint64_t bal = __ballot(f);
+      if (f) L.kidx[k][carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = (uint16_t)p;
+      carry += (uint32_t)__builtin_popcountll(bal);
+    }
+    if (lane == 0) L.kcnt[k] = carry;
+  }
+}
+
+// side sd's rows into L.su / L.ob (SU order) and its window pairs' prefix;
+// returns the row count (or ~0 when it does not fit) and the pair count
+__device__ uint32_t wave_side(WaveLds& L, const RowsArgs& a, int sd, uint32_t& Q) {
+  const int lane = threadIdx.x & 63;
+  uint32_t n = 0;
+  for (int k = 0; k < a.n_shifts; ++k)
+    if ((a.sides[k] >> sd) & 1) n += L.kcnt[k];
+  Q = 0;
+  if (n > (uint32_t)kWS) return 0xFFFFFFFFu;
+  for (int k = 0; k < a.n_shifts; ++k) {
+    if (!((a.sides[k] >> sd) & 1)) continue;
+    const double sk = a.shift[k];
+    for (uint32_t j = lane; j < L.kcnt[k]; j += 64) {
+      const uint32_t p = L.kidx[k][j];
+      const double su = L.obs[p] - sk;
+      uint32_t pos = j;
+      for (int k2 = 0; k2 < a.n_shifts; ++k2) {
+        if (k2 == k || !((a.sides[k2] >> sd) & 1)) continue;
+        const double s2 = a.shift[k2];
+        uint32_t lo = 0, hi = L.kcnt[k2];
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          const double v = L.obs[L.kidx[k2][mid]] - s2;
+          if (v < su || (v == su && k2 < k)) lo = mid + 1;
+          else hi = mid;
+        }
+        pos += lo;
+      }
+      L.su[pos] = su;
+      L.ob[pos] = L.obs[p];
+    }
+  }
+  wsync();
+  // s*: the first start whose difference to the last row is within max_weight
+  uint32_t ss = n ? n - 1 : 0;
+  for (uint32_t r = lane; r + 1 < n; r += 64)
+    if (!(L.su[n - 1] - L.su[r] > a.max_weight)) ss = r < ss ? r : ss;
+  ss = wave_min(ss);
+  uint32_t carry = 0;
+  for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+    const uint32_t r = r0 + lane;
+    uint32_t c = 0;
+    if (r + 1 < n) {
+      if (r < ss) {
+        uint32_t lo = r + 1, hi = n - 1;
+        const double sr = L.su[r];
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (L.su[mid] - sr > a.max_weight) hi = mid;
+          else lo = mid + 1;
+        }
+        c = lo - r - 1;
+      } else if (r == ss) {
+        c = n - 1 - r;
+      } else {
+        c = 1;
+      }
+    }
+    uint32_t tot;
+    const uint32_t ex = wave_excl(c, tot);
+    if (r < n) L.qoff[r] = carry + ex;
+    carry += tot;
+  }
+  if (lane == 0) {
+    L.qoff[n] = carry;
+    L.sstar = ss;
+  }
+  wsync();
+  Q = carry;
+  return n;
+}
+
+__device__ __forceinline__ void wave_pair(const WaveLds& L, uint32_t n, uint32_t q, uint32_t& s, uint32_t& e) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (L.qoff[mid] <= q) lo = mid;
+    else hi = mid;
+  }
+  s = lo;
+  e = s <= L.sstar ? s + 1 + (q - L.qoff[s]) : n - 1;
+}
+
+__device__ __forceinline__ QAns wave_answer(const WaveLds& L, const PairImg& img, const RowsArgs& a, uint32_t s,
+                                            uint32_t e) {
+  const double diff = L.su[e] - L.su[s];
+  const double thr = a.tol * (L.ob[s] + L.ob[e]);
+  double lof, hif;
+  quantise_lean(diff, thr, a.prec, a.rprec, lof, hif);
+  QAns r{SST_NONE, 0, 0, 0};
+  if (lof <= hif && hif >= 0.0) {
+    const double af = lof < 1.0 ? 1.0 : lof;
+    if (af <= hif) r.cnt = img_walk(img, (uint32_t)af, (uint32_t)hif, r.first, r.bytes);
+    if (r.cnt > a.cap) r.status = SST_OVERFLOW;
+    else if (r.cnt) r.status = SST_SOME;
+    else if (lof <= 0.0) r.status = SST_EMPTY;
+  }
+  return r;
+}
+
+// the next spectrum for this wave (dynamic: spectra differ in cost)
+__device__ __forceinline__ int64_t next_spectrum(uint32_t* ticket) {
+  uint32_t g = 0;
+  if ((threadIdx.x & 63) == 0) g = atomicAdd(ticket, 1u);
+  return (int64_t)__shfl(g, 0, 64);
+}
+
+__device__ __forceinline__ PairImg global_img(const TableArgs& t) {
+  const int n_s = t.n_pairs + 2;
+  return PairImg{t.pair_data, t.pair_data + n_s, t.pair_data + 2 * n_s, t.pair_base, t.pair_shift};
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, RowsArgs a) {
+  __shared__ WaveLds Ls[kWavesPerWG];
+  WaveLds& L = Ls[threadIdx.x >> 6];
+  const int lane = threadIdx.x & 63;
+#ifndef SST_ROWS_IMG_LDS  // the pair list through L2: 16 waves per CU (staged in LDS: 8, measured slower)
+  const PairImg img = global_img(t);
+#else
+  extern __shared__ uint32_t dyn[];
+  PairImg img;
+  stage_img(t, dyn, img);
+#endif
+  for (;;) {
+    RPROF_T(c0);
+    const int64_t g = next_spectrum(&a.tickets[0]);
+    if (g >= a.n_spec) break;
+    const int64_t p0 = a.peak_off[g];
+    const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
+    if (P > (uint32_t)kWP) {  // the block kernels'
+      if (lane == 0) a.big[atomicAdd(&a.tickets[2], 1u)] = (uint32_t)g;
+      continue;
+    }
+    RPROF_T(c1);
+    RPROF_ADD(0, c1 - c0);
+    wave_load(L, t, a, p0, P, a.su_seq[g], true);
+    wsync();
+    RPROF_T(c2);
+    RPROF_ADD(1, c2 - c1);
+    uint32_t nq = 0, nh = 0, nb = 0, n0 = 0, n1 = 0;
+    bool ok = true;
+    for (int sd = 0; sd < 2; ++sd) {
+      uint32_t Q;
+      RPROF_T(c3);
+      const uint32_t n = wave_side(L, a, sd, Q);
+      RPROF_T(c4);
+      RPROF_ADD(2, c4 - c3);
+      if (n == 0xFFFFFFFFu) {
+        ok = false;
+        break;
+      }
+      if (sd) n1 = n;
+      else n0 = n;
+      double* rs = a.rows_su + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
+      double* ro = a.rows_ob + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
+      for (uint32_t r = lane; r < n; r += 64) {
+        rs[r] = L.su[r];
+        ro[r] = L.ob[r];
+      }
+      for (uint32_t q = lane; q < Q; q += 64) {
+        uint32_t s, e;
+        wave_pair(L, n, q, s, e);
+        const QAns r = wave_answer(L, img, a, s, e);
+        nh += (r.status == SST_SOME || r.status == SST_OVERFLOW);
+        nb += r.status == SST_SOME ? r.bytes + 2u : 0u;
+      }
+      nq += Q;
+      wsync();
+      RPROF_T(c5);
+      RPROF_ADD(3, c5 - c4);
+    }
+    RPROF_T(c6);
+    uint32_t th, tb;
+    wave_excl(nh, th);
+    wave_excl(nb, tb);
+    if (lane == 0) {
+      if (!ok) atomicOr(a.err, 2u);
+      a.totals[3 * g] = ok ? nq : 0u;
+      a.totals[3 * g + 1] = ok ? th : 0u;
+      a.totals[3 * g + 2] = ok ? tb : 0u;
+      a.side_rows[2 * g] = ok ? n0 : 0u;
+      a.side_rows[2 * g + 1] = ok ? n1 : 0u;
+    }
+    wsync();
+    RPROF_T(c7);
+    RPROF_ADD(4, c7 - c6);
+    RPROF_ADD(5, 1);
+  }
+}
+
+__global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, RowsArgs a) {
+  __shared__ WaveLds Ls[kWavesPerWG];
+  WaveLds& L = Ls[threadIdx.x >> 6];
+  const int lane = threadIdx.x & 63;
+#ifndef SST_ROWS_IMG_LDS  // the pair list through L2: 16 waves per CU (staged in LDS: 8, measured slower)
+  const PairImg img = global_img(t);
+#else
+  extern __shared__ uint32_t dyn[];
+  PairImg img;
+  stage_img(t, dyn, img);
+#endif
+  const bool room = !(*(volatile uint32_t*)a.err & 4u);
+  for (;;) {
+    RPROF_T(e0);
+    const int64_t g = room ? next_spectrum(&a.tickets[1]) : a.n_spec;
+    if (g >= a.n_spec) break;
+    RPROF_T(e1);
+    RPROF_ADD(6, e1 - e0);
+    const int64_t p0 = a.peak_off[g];
+    const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
+    if (P > (uint32_t)kWP) continue;
+    uint64_t qb = a.offs[3 * g], hb = a.offs[3 * g + 1], bb = a.offs[3 * g + 2];
+    for (int sd = 0; sd < 2; ++sd) {
+      const uint32_t n = a.side_rows[2 * g + sd];
+      const double* rs = a.rows_su + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
+      const double* ro = a.rows_ob + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
+      for (uint32_t r = lane; r < n; r += 64) {
+        L.su[r] = rs[r];
+        L.ob[r] = ro[r];
+      }
+      wsync();
+      // s* and the pair prefix (as in the count pass, from the stored rows)
+      uint32_t ss = n ? n - 1 : 0;
+      for (uint32_t r = lane; r + 1 < n; r += 64)
+        if (!(L.su[n - 1] - L.su[r] > a.max_weight)) ss = r < ss ? r : ss;
+      ss = wave_min(ss);
+      uint32_t carry = 0;
+      for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+        const uint32_t r = r0 + lane;
+        uint32_t c = 0;
+        if (r + 1 < n) {
+          if (r < ss) {
+            uint32_t lo = r + 1, hi = n - 1;
+            const double sr = L.su[r];
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi) >> 1;
+              if (L.su[mid] - sr > a.max_weight) hi = mid;
+              else lo = mid + 1;
+            }
+            c = lo - r - 1;
+          } else if (r == ss) {
+            c = n - 1 - r;
+          } else {
+            c = 1;
+          }
+        }
+        uint32_t tot;
+        const uint32_t ex = wave_excl(c, tot);
+        if (r < n) L.qoff[r] = carry + ex;
+        carry += tot;
+      }
+      if (lane == 0) {
+        L.qoff[n] = carry;
+        L.sstar = ss;
+      }
+      wsync();
+      const uint32_t Q = carry;
+      for (uint32_t q0 = 0; q0 < Q; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        QAns r{SST_NONE, 0, 0, 0};
+        if (q < Q) {
+          uint32_t s, e;
+          wave_pair(L, n, q, s, e);
+          r = wave_answer(L, img, a, s, e);
+          a.status[qb + q] = r.status;
+        }
+        const bool hit = r.status == SST_SOME || r.status == SST_OVERFLOW;
+        uint32_t th, tb;
+        const uint32_t xh = wave_excl(hit ? 1u : 0u, th);
+        const uint32_t xb = wave_excl(r.status == SST_SOME ? r.bytes + 2u : 0u, tb);
+        if (hit) {
+          const uint64_t off = bb + xb;
+          const uint64_t word = r.status == SST_SOME ? off : (uint64_t)r.cnt;
+          a.hits[hb + xh] = make_uint4((uint32_t)(qb + q), r.cnt, (uint32_t)word, (uint32_t)(word >> 32));
+          a.refs[hb + xh] = (uint16_t)(r.first | (r.status == SST_OVERFLOW ? 0x8000u : 0u));
+          if (r.status == SST_SOME) {
+            uint8_t* dst = a.dense + off;
+            for (uint32_t k = r.first; k < r.first + r.cnt; ++k) {
+              const uint32_t rec = img.recs[k];
+              *(u32_unal*)dst = rec;
+              dst += (rec & 0xFFu) + 1u;
+            }
+          }
+        }
+        hb += th;
+        bb += tb;
+      }
+      qb += Q;
+      wsync();
+    }
+    RPROF_T(e2);
+    RPROF_ADD(7, e2 - e1);
   }
 }
 
@@ -411,9 +865,28 @@ size_t rows_lds_bytes() { return sizeof(SpecLds); }
 
 hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, size_t dyn, hipStream_t st) {
   if (a.n_spec <= 0 || !t.pairs_enabled) return hipErrorInvalidValue;
+#ifndef SST_ROWS_IMG_LDS
+  const size_t wdyn = 0;
+#else
+  const size_t wdyn = dyn;
+#endif
+  // 4-wave workgroups, as many as are resident (each wave takes spectra from a ticket)
+  static int occ = 0;
+  static size_t occ_dyn = ~(size_t)0;
+  if (occ_dyn != wdyn) {
+    int c1 = 0, c2 = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, k_rows_count_w, 64 * kWavesPerWG, wdyn) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&c2, k_rows_emit_w, 64 * kWavesPerWG, wdyn) != hipSuccess)
+      return hipErrorLaunchFailure;
+    occ = c1 < c2 ? c1 : c2;
+    occ_dyn = wdyn;
+  }
+  const int wave_wg = n_wg * (occ > 0 ? occ : 1);
+  hipLaunchKernelGGL(k_rows_count_w, dim3(wave_wg), dim3(64 * kWavesPerWG), wdyn, st, t, a);
   hipLaunchKernelGGL(k_rows_count, dim3(n_wg), dim3(kRowsWG), dyn, st, t, a);
-  hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kRowsWG), 0, st, a);
-  hipLaunchKernelGGL(k_rows_emit, dim3(n_wg), dim3(kRowsWG), dyn, st, t, a);
+  hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kRowsWG), 3 * kScanChunk * sizeof(uint64_t), st, a);
+  hipLaunchKernelGGL(k_rows_emit_w, dim3(wave_wg), dim3(64 * kWavesPerWG), wdyn, st, t, a);
+  hipLaunchKernelGGL(k_rows_emit, dim3(n_wg), dim3(kRowsWG), dyn, st, t, a);  // last: writes the header
   return hipGetLastError();
 }
 
