@@ -91,7 +91,7 @@ struct sst_table {
   std::vector<int64_t> masses;
   std::vector<uint8_t> is_mod;
   std::vector<int64_t> cap;
-  DevBuf packed, index, valid, w, capd, modd, pairs;
+  DevBuf packed, index, valid, w, capd, modd, pairs, census;
   std::vector<uint32_t> pair_recs;  // the pair list's payload records (host copy)
   uint64_t pair_key = 0;            // their FNV-1a (sst_wire_pack), computed on first use
   bool pair_key_set = false;
@@ -322,6 +322,23 @@ int build_pair_list(sst_table* t, bool self_built) {
   if (!t->pairs.ensure(img.size() * 4)) return fail(c, SST_E_NOMEM, "device allocation failed (pair list)");
   HIP_OK(c, hipMemcpy(t->pairs.p, img.data(), img.size() * 4, hipMemcpyHostToDevice));
   t->args.pair_data = (const uint32_t*)t->pairs.p;
+  t->args.census = nullptr;
+  if (t->args.pair_hi - base + 1 <= ((int64_t)1 << 27)) {  // census: entries and record bytes with sum <= x, x in [base - 1, pair_hi)
+    std::vector<uint32_t> cen((size_t)(t->args.pair_hi - base + 1));
+    uint32_t cnt = 0, bytes = 0;
+    size_t j = 0;
+    for (size_t x = 0; x < cen.size(); ++x) {
+      const int64_t v = base - 1 + (int64_t)x;
+      for (; j < n_e && (int64_t)e[j].sum <= v; ++j) {
+        ++cnt;
+        bytes += (e[j].rows & 0xFFu) == 2u ? 3u : 2u;
+      }
+      cen[x] = cnt | bytes << 16;
+    }
+    if (!t->census.ensure(cen.size() * 4)) return fail(c, SST_E_NOMEM, "device allocation failed (pair census)");
+    HIP_OK(c, hipMemcpy(t->census.p, cen.data(), cen.size() * 4, hipMemcpyHostToDevice));
+    t->args.census = (const uint32_t*)t->census.p;
+  }
   t->args.pair_base = (uint32_t)base;
   t->args.n_pairs = (int)n_e;
   t->args.n_buckets = (int)n_b;
@@ -658,7 +675,7 @@ void sst_table_destroy(sst_table* t) {
   std::lock_guard<std::recursive_mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&t->packed, &t->index, &t->valid, &t->w, &t->capd, &t->modd, &t->pairs})
+  for (DevBuf* b : {&t->packed, &t->index, &t->valid, &t->w, &t->capd, &t->modd, &t->pairs, &t->census})
     b->release();
   delete t;
 }
@@ -1320,7 +1337,7 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
-  if (!t->args.pairs_enabled) return fail(c, SST_E_ARG, "rows step: the table has no pair list");
+  if (!t->args.pairs_enabled || !t->args.census) return fail(c, SST_E_ARG, "rows step: the table has no pair list");
   // every window must be pair-class with budgets that cannot bind: a
   // difference <= max_weight, a threshold <= tol * 2 * mass_cutoff
   const double hi_max = (max_weight + tol * 2.0 * mass_cutoff) / prec + 2.0;

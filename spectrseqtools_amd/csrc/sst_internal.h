@@ -74,6 +74,11 @@ struct TableArgs {
   int n_buckets;
   int pair_shift;
   uint32_t pair_base;  // = w_min: no sum lies below it
+  // census of the pair list, one u32 per value x in [pair_base - 1, pair_hi):
+  // bits 0-15 entries with sum <= x, bits 16-31 their record bytes.  A window's
+  // count, first entry and payload bytes are two independent loads (the rows
+  // step reads it through L2; the pair list is <= 21000 entries, <= 63000 B)
+  const uint32_t* census;
   // u32 forms of the fast-path limits (window values are < 2^31):
   // hi < never_lim  <=>  hi <= fast_limit_B (no per-row cap binds);
   // hi < pair_lim   <=>  pair-list window with no per-row cap binding
@@ -337,7 +342,7 @@ struct RowsArgs {
   uint64_t* ctl;              // [4] totals
   uint32_t* err;
   uint32_t* done;
-  uint32_t* tickets;          // [3] next spectrum of k_rows_count_w / k_rows_emit_w, big-spectrum count
+  uint32_t* tickets;          // [3]: [2] spectra listed in `big` ([0], [1] spare)
   uint32_t* big;              // [n_spec] spectra over kRowsWaveMaxPeaks peaks (the block kernels')
   uint64_t cap_queries, cap_bytes;
   int8_t* status;

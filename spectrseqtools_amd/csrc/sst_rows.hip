@@ -41,7 +41,7 @@
 namespace sst {
 
 #ifdef SST_ROWS_PROF  // phase clocks of the wave kernels (diagnostic builds; printed by the last workgroup)
-__device__ unsigned long long g_rows_prof[8];
+__device__ unsigned long long g_rows_prof[12];
 #define RPROF_T(v) const uint64_t v = wall_clock64()
 #define RPROF_ADD(i, d) \
   if ((threadIdx.x & 63) == 0) atomicAdd(&g_rows_prof[i], (unsigned long long)(d))
@@ -354,7 +354,16 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_scan(RowsArgs a) {
   uint64_t carry[3] = {0, 0, 0};
   for (int64_t c0 = 0; c0 < a.n_spec; c0 += kScanChunk) {
     const int m = (int)(a.n_spec - c0 < kScanChunk ? a.n_spec - c0 : kScanChunk);
-    for (int i = threadIdx.x; i < 3 * m; i += blockDim.x) s_tot[i] = a.totals[3 * c0 + i];
+    {
+      uint32_t x[3 * kScanPer];  // every load in flight before the first LDS store
+#pragma unroll
+      for (int k = 0; k < 3 * kScanPer; ++k) {
+        const int i = threadIdx.x + k * kRowsWG;
+        x[k] = i < 3 * m ? a.totals[3 * c0 + i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 3 * kScanPer; ++k) s_tot[threadIdx.x + k * kRowsWG] = x[k];
+    }
     __syncthreads();
     const int j0 = threadIdx.x * kScanPer;
     uint32_t v[3 * kScanPer];
@@ -464,10 +473,10 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
     h[kHdrQueries] = a.ctl[0];
     h[kHdrRowsErr] = err;
 #ifdef SST_ROWS_PROF
-    printf("rows prof (10 ns ticks, summed over spectra): ticket %llu load %llu merge %llu answer %llu tail %llu n %llu | emit ticket %llu body %llu\n",
+    printf("rows prof (wall_clock64 ticks, summed over spectra): head %llu load %llu merge %llu answer %llu tail %llu n %llu | emit head %llu body %llu | wave life %llu waves %llu grid %llu\n",
            g_rows_prof[0], g_rows_prof[1], g_rows_prof[2], g_rows_prof[3], g_rows_prof[4], g_rows_prof[5],
-           g_rows_prof[6], g_rows_prof[7]);
-    for (int k = 0; k < 8; ++k) g_rows_prof[k] = 0;
+           g_rows_prof[6], g_rows_prof[7], g_rows_prof[8], g_rows_prof[9], g_rows_prof[10]);
+    for (int k = 0; k < 12; ++k) g_rows_prof[k] = 0;
 #endif
     for (int k = 0; k < kHdrWords; ++k) a.hdr[k] = h[k];
     for (int k = 0; k < kHdrWords; ++k)
@@ -647,7 +656,18 @@ __device__ __forceinline__ void wave_pair(const WaveLds& L, uint32_t n, uint32_t
   e = s <= L.sstar ? s + 1 + (q - L.qoff[s]) : n - 1;
 }
 
-__device__ __forceinline__ QAns wave_answer(const WaveLds& L, const PairImg& img, const RowsArgs& a, uint32_t s,
+// the pair-list entries with sums in [a, hi] (1 <= a <= hi < pair_hi) from the census: two independent loads
+__device__ __forceinline__ uint32_t census_walk(const TableArgs& t, uint32_t a, uint32_t hi, uint32_t& first,
+                                                uint32_t& bytes) {
+  const uint32_t c0 = t.pair_base - 1u;
+  const uint32_t lo = a - 1u < c0 ? c0 : a - 1u, h = hi < c0 ? c0 : hi;
+  const uint32_t x = t.census[lo - c0], y = t.census[h - c0];
+  first = x & 0xFFFFu;
+  bytes = (y >> 16) - (x >> 16);
+  return (y & 0xFFFFu) - first;
+}
+
+__device__ __forceinline__ QAns wave_answer(const WaveLds& L, const TableArgs& t, const RowsArgs& a, uint32_t s,
                                             uint32_t e) {
   const double diff = L.su[e] - L.su[s];
   const double thr = a.tol * (L.ob[s] + L.ob[e]);
@@ -656,19 +676,12 @@ __device__ __forceinline__ QAns wave_answer(const WaveLds& L, const PairImg& img
   QAns r{SST_NONE, 0, 0, 0};
   if (lof <= hif && hif >= 0.0) {
     const double af = lof < 1.0 ? 1.0 : lof;
-    if (af <= hif) r.cnt = img_walk(img, (uint32_t)af, (uint32_t)hif, r.first, r.bytes);
+    if (af <= hif) r.cnt = census_walk(t, (uint32_t)af, (uint32_t)hif, r.first, r.bytes);
     if (r.cnt > a.cap) r.status = SST_OVERFLOW;
     else if (r.cnt) r.status = SST_SOME;
     else if (lof <= 0.0) r.status = SST_EMPTY;
   }
   return r;
-}
-
-// the next spectrum for this wave (dynamic: spectra differ in cost)
-__device__ __forceinline__ int64_t next_spectrum(uint32_t* ticket) {
-  uint32_t g = 0;
-  if ((threadIdx.x & 63) == 0) g = atomicAdd(ticket, 1u);
-  return (int64_t)__shfl(g, 0, 64);
 }
 
 __device__ __forceinline__ PairImg global_img(const TableArgs& t) {
@@ -682,17 +695,10 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
   __shared__ WaveLds Ls[kWavesPerWG];
   WaveLds& L = Ls[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
-#ifndef SST_ROWS_IMG_LDS  // the pair list through L2: 16 waves per CU (staged in LDS: 8, measured slower)
-  const PairImg img = global_img(t);
-#else
-  extern __shared__ uint32_t dyn[];
-  PairImg img;
-  stage_img(t, dyn, img);
-#endif
-  for (;;) {
+  RPROF_T(w0);
+  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerWG;
+  for (int64_t g = (int64_t)blockIdx.x * kWavesPerWG + (threadIdx.x >> 6); g < a.n_spec; g += n_waves) {
     RPROF_T(c0);
-    const int64_t g = next_spectrum(&a.tickets[0]);
-    if (g >= a.n_spec) break;
     const int64_t p0 = a.peak_off[g];
     const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
     if (P > (uint32_t)kWP) {  // the block kernels'
@@ -728,7 +734,7 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
       for (uint32_t q = lane; q < Q; q += 64) {
         uint32_t s, e;
         wave_pair(L, n, q, s, e);
-        const QAns r = wave_answer(L, img, a, s, e);
+        const QAns r = wave_answer(L, t, a, s, e);
         nh += (r.status == SST_SOME || r.status == SST_OVERFLOW);
         nb += r.status == SST_SOME ? r.bytes + 2u : 0u;
       }
@@ -754,13 +760,17 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
     RPROF_ADD(4, c7 - c6);
     RPROF_ADD(5, 1);
   }
+  RPROF_T(w1);
+  RPROF_ADD(8, w1 - w0);
+  RPROF_ADD(9, 1);
+  if (threadIdx.x == 0 && blockIdx.x == 0) RPROF_ADD(10, gridDim.x);
 }
 
 __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, RowsArgs a) {
   __shared__ WaveLds Ls[kWavesPerWG];
   WaveLds& L = Ls[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
-#ifndef SST_ROWS_IMG_LDS  // the pair list through L2: 16 waves per CU (staged in LDS: 8, measured slower)
+#ifndef SST_ROWS_IMG_LDS  // records through L2: 16 waves per CU (staged in LDS: 8, measured slower)
   const PairImg img = global_img(t);
 #else
   extern __shared__ uint32_t dyn[];
@@ -768,10 +778,9 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, R
   stage_img(t, dyn, img);
 #endif
   const bool room = !(*(volatile uint32_t*)a.err & 4u);
-  for (;;) {
+  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerWG;
+  for (int64_t g = (int64_t)blockIdx.x * kWavesPerWG + (threadIdx.x >> 6); g < a.n_spec && room; g += n_waves) {
     RPROF_T(e0);
-    const int64_t g = room ? next_spectrum(&a.tickets[1]) : a.n_spec;
-    if (g >= a.n_spec) break;
     RPROF_T(e1);
     RPROF_ADD(6, e1 - e0);
     const int64_t p0 = a.peak_off[g];
@@ -829,7 +838,7 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, R
         if (q < Q) {
           uint32_t s, e;
           wave_pair(L, n, q, s, e);
-          r = wave_answer(L, img, a, s, e);
+          r = wave_answer(L, t, a, s, e);
           a.status[qb + q] = r.status;
         }
         const bool hit = r.status == SST_SOME || r.status == SST_OVERFLOW;
@@ -875,14 +884,14 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
   static size_t occ_dyn = ~(size_t)0;
   if (occ_dyn != wdyn) {
     int c1 = 0, c2 = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, k_rows_count_w, 64 * kWavesPerWG, wdyn) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, k_rows_count_w, 64 * kWavesPerWG, 0) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&c2, k_rows_emit_w, 64 * kWavesPerWG, wdyn) != hipSuccess)
       return hipErrorLaunchFailure;
     occ = c1 < c2 ? c1 : c2;
     occ_dyn = wdyn;
   }
   const int wave_wg = n_wg * (occ > 0 ? occ : 1);
-  hipLaunchKernelGGL(k_rows_count_w, dim3(wave_wg), dim3(64 * kWavesPerWG), wdyn, st, t, a);
+  hipLaunchKernelGGL(k_rows_count_w, dim3(wave_wg), dim3(64 * kWavesPerWG), 0, st, t, a);
   hipLaunchKernelGGL(k_rows_count, dim3(n_wg), dim3(kRowsWG), dyn, st, t, a);
   hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kRowsWG), 3 * kScanChunk * sizeof(uint64_t), st, a);
   hipLaunchKernelGGL(k_rows_emit_w, dim3(wave_wg), dim3(64 * kWavesPerWG), wdyn, st, t, a);

@@ -158,3 +158,24 @@ def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=MATCHING_THRE
             break
     return DeviceFixpoint(alpha.cpu().numpy().view(np.uint64).copy(), rounds.cpu().numpy(),
                           queries.cpu().numpy(), history, n_rounds)
+
+
+def to_classified(rows: DeviceRows, alive_only=True):
+    """The device rows back on the host as pipeline.Classified (spectrum-major,
+    each spectrum's rows in SU order; with alive_only the rows the fixpoint
+    kept) -- the input of the host stages after the fixpoint (bin queries)."""
+    from .pipeline import Classified
+
+    off = rows.peak_off.cpu().numpy()
+    cnt = rows.rows.cpu().numpy().astype(np.int64)[:len(off) - 1]
+    S = len(cnt)
+    spec = np.repeat(np.arange(S), cnt)
+    local = np.arange(int(cnt.sum())) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+    slot = 4 * off[:-1][spec] + local
+    su, ob = rows.su.cpu().numpy()[slot], rows.obs.cpu().numpy()[slot]
+    meta = rows.meta.cpu().numpy()[slot]
+    keep = rows.alive.cpu().numpy()[slot].astype(bool) if alive_only else np.ones(len(slot), bool)
+    spec, su, ob, meta = spec[keep], su[keep], ob[keep], meta[keep]
+    offsets = np.searchsorted(spec, np.arange(S + 1))
+    return Classified(spec, su, ob, (meta >> 8).astype(np.int64), (meta & 3).astype(np.int64),
+                      ((meta >> 4) & 1).astype(bool), rows.names, offsets, 0, 0)

@@ -242,3 +242,62 @@ def test_fullsize_step_device_vs_oracle(fullsize, oracle_a8):
     cnt_, off_ = decode_hits(st_, hits_)
     assert np.array_equal(v_, a7) and np.array_equal(st_, res.status)
     assert canonical_digest(st_, cnt_, off_, pay_) == canonical_digest(res.status, res.count, res.offset, res.payload)
+
+
+def test_fullsize_rows_step_vs_oracle(fullsize, oracle_a8):
+    """The step from the peaks (bench.py --a8-source rows: sst_step_rows_device,
+    A7, the classification filters, per-side SU order and the sliding window's
+    pairs formed on the device) on the full config-3 workload, twice into one
+    reused result.  Its queries are the host producers' in the same order, so
+    against the oracle: the A7 byte of every (peak x breakage) pair, every A8
+    status and count, the candidates' properties, the exact candidate lists of
+    a sample and the dense hit list (query order, payload back to back)."""
+    torch = pytest.importorskip("torch")
+    from spectrseqtools_amd import _native
+    from spectrseqtools_amd.parallel import device_bytes
+
+    dp, wl = fullsize
+    host, alph, want, ocnt = oracle_a8
+    ms = np.array([m.mass for m in dp.masses], dtype=np.int64)
+    A = round(dp.seq.modification_rate * dp.seq.max_len)
+    masses, thr = wl["a8_mass"], wl["a8_thr"]
+    n, P, S = len(masses), len(wl["obs"]), len(wl["peak_off"]) - 1
+    dev = torch.device("cuda", 0)
+    do, dpo, ds = (torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in (wl["obs"], wl["peak_off"], wl["su_seq"]))
+    out7 = torch.full((4 * P,), 9, dtype=torch.int8, device=dev)
+    torch.cuda.synchronize()
+    tdev = dp.device_table
+    res, digests = None, []
+    for _ in range(2):
+        out7.fill_(9)
+        torch.cuda.synchronize()
+        res = tdev.step_rows_device(do.data_ptr(), dpo.data_ptr(), S, P, ds.data_ptr(), wl["shifts"], wl["sides"],
+                                    out7.data_ptr(), wl["max_weight"], dp.tolerance, dp.precision, A,
+                                    int(n * 1.1) + 64, reuse=res)
+        n_hits, n_bytes = res.settle()
+        ptr, nh = res.hit_list_device()
+        assert nh == n_hits
+        recs = device_bytes(ptr, 16 * nh, dev).cpu().numpy().view(np.uint32).reshape(-1, 4)
+        res.fetch_device()
+        assert res.n == n and len(res.payload) == n_bytes
+        digests.append((res.status.tobytes(), recs.tobytes(), res.payload.tobytes()))
+    assert digests[0] == digests[1]
+    _native.get_engine(0).synchronize()
+    a7 = out7.cpu().numpy()
+    assert len(a7) == len(wl["a7_mass"]) > 4_000_000
+    assert np.array_equal(a7, oracle.is_valid_batch(host, 32, wl["a7_mass"], wl["a7_thr"], dp.tolerance, nthreads=16))
+    assert np.array_equal(res.status.astype(np.int64), want)
+    some = res.status == _native.SST_SOME
+    assert np.array_equal(res.count[some].astype(np.int64), ocnt[some])
+    _check_candidates(res, masses, thr, ms, dp.precision)
+    rng = np.random.default_rng(37)
+    for i in rng.choice(np.flatnonzero(some), 3000, replace=False):
+        st, sols, _, _ = oracle.explain_table(host, 32, alph, masses[i], thr[i], dp.tolerance, A)
+        assert res.candidates(int(i)) == sols, i
+    q = recs[:, 0].astype(np.int64)
+    assert len(q) == int(np.isin(res.status, (_native.SST_SOME, _native.SST_OVERFLOW)).sum())
+    assert (np.diff(q) > 0).all()  # query order
+    assert np.array_equal(recs[:, 1].astype(np.int64), res.count[q].astype(np.int64))
+    off = recs[:, 2].astype(np.int64) | (recs[:, 3].astype(np.int64) << 32)
+    assert np.array_equal(off[some[q]], res.offset[q][some[q]].astype(np.int64))
+    assert (np.diff(off[some[q]]) > 0).all()

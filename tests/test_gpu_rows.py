@@ -6,7 +6,8 @@ CPU suite pins to the reference) and the CPU oracle: A7 codes, the query
 count, every answer (canonical digest against the explain pass over the
 host-built queries), statuses and exact candidate lists of a sample against
 the oracle; edge spectra (no peaks, one peak, duplicate peaks, heavy peaks,
-intensities below the cutoff, a mass cutoff that drops peaks)."""
+spectra over 160 peaks, intensities below the cutoff, a mass cutoff that
+drops peaks)."""
 import os
 import sys
 
@@ -117,6 +118,8 @@ def test_rows_step_edge_spectra(dp):
             o = np.concatenate([o, o[: len(o) // 2]])  # duplicate peaks: ties between rows
         elif s % 10 == 3:
             o = np.concatenate([o, rng.uniform(15000.0, 21000.0, 3)])  # heavy peaks (near the table's end)
+        elif s % 10 == 4:  # over 160 peaks: the workgroup-per-spectrum kernels
+            o = np.concatenate([o] + [b.observed[b.offsets[t]:b.offsets[t + 1]] for t in (s + 1, s + 2)])
         o = np.sort(o)
         obs.append(o)
         offs.append(offs[-1] + len(o))

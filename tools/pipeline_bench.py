@@ -27,7 +27,13 @@ reference Python cannot run on the GPU box; `reference_estimate_s` prices the
 same query counts at its measured single-core rates (is_valid
 70 k/s, sliding-window explain 3.6-4.5 k/s).
 
-Usage: python tools/pipeline_bench.py [--spectra 100000] [--seed 7]
+Stages 1-2 run device-resident by default (pipeline_device: classify and
+every fixpoint round in HBM, the host reads one counter per round); with
+--host-driven through the host-driven batched path (pipeline.classify /
+filter_fixpoint).  Every stage reports its event-timed kernel time and the
+GPU-busy share of its wall time.
+
+Usage: python tools/pipeline_bench.py [--spectra 100000] [--seed 7] [--host-driven]
 """
 import argparse
 import json
@@ -45,6 +51,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spectra", type=int, default=100000, help="spectra per GPU")
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--host-driven", action="store_true",
+                    help="stages 1-2 through the host-driven batched path (pipeline.classify / filter_fixpoint) "
+                         "instead of the device-resident one (pipeline_device)")
     args = ap.parse_args()
 
     import torch
@@ -89,41 +98,86 @@ def main():
     min_int = min(m.mass for m in dp.masses[1:])
     max_len = pipeline.max_len_of(su_seq, TOLERANCE, min_int)  # cli.py:158-170
 
+    def kernels():
+        return {_native.KERNEL_NAMES.get(k, str(k)): v for k, v in engine.profile_read().items()}
+
+    def busy(st):  # GPU-busy share of a stage: event-timed kernel time over its wall time
+        st["gpu_busy_frac"] = sum(v[0] for v in st["kernels"].values()) / 1e3 / st["s"]
+
     stages = {}
     engine.profile(True)
-    barrier()
-    t0 = time.perf_counter()
-    c = pipeline.classify(batch.observed, batch.offsets, su_seq, dp, bd)
-    barrier()
-    stages["classify"] = {"s": tmax(time.perf_counter() - t0), "is_valid_queries": c.n_valid_queries,
-                          "is_singleton_queries": c.n_singleton_queries, "rows_kept": int(c.offsets[-1])}
-    stages["classify"]["kernels"] = {_native.KERNEL_NAMES.get(k, str(k)): v for k, v in engine.profile_read().items()}
+    n_valid_q = 0
+    if args.host_driven:
+        barrier()
+        t0 = time.perf_counter()
+        c = pipeline.classify(batch.observed, batch.offsets, su_seq, dp, bd)
+        barrier()
+        stages["classify"] = {"s": tmax(time.perf_counter() - t0), "is_valid_queries": c.n_valid_queries,
+                              "is_singleton_queries": c.n_singleton_queries, "rows_kept": int(c.offsets[-1])}
+        stages["classify"]["kernels"] = kernels()
+        n_valid_q = c.n_valid_queries
+
+        barrier()
+        t0 = time.perf_counter()
+        fx = pipeline.filter_fixpoint(c, dp, max_len, EXPLANATION_MASSES)
+        barrier()
+        alpha_u = np.unique(fx.alpha, axis=0)
+        stages["fixpoint"] = {"s": tmax(time.perf_counter() - t0), "rounds_max": int(fx.rounds.max()),
+                              "rounds_histogram": {int(k): int(v) for k, v in zip(*np.unique(fx.rounds, return_counts=True))},
+                              "final_round_queries": int(len(fx.last.get("diff", []))),
+                              "explain_queries_per_round": [int(x[0]) for x in fx.queries],
+                              "is_valid_queries_per_round": [int(x[1]) for x in fx.queries],
+                              "rows_kept": int(fx.alive.sum()), "rows_in": int(len(fx.alive)),
+                              "distinct_alphabets": int(len(alpha_u)),
+                              "mean_alphabet_rows": float(pipeline.mask_rows(fx.alpha, len(dp.masses)).sum(1).mean() + 1)}
+        stages["fixpoint"]["kernels"] = kernels()
+        fx_alpha = fx.alpha
+        explain_q = sum(x[0] for x in fx.queries)
+        valid_q_rounds = sum(x[1] for x in fx.queries)
+        c_bins = lambda: pipeline.subset(c, fx.alive)  # noqa: E731
+    else:
+        from spectrseqtools_amd import pipeline_device as pd
+
+        barrier()
+        t0 = time.perf_counter()  # includes the peaks' upload (PCIe)
+        rows = pd.classify_device(dp, batch.observed, batch.offsets, su_seq, bd)
+        barrier()
+        n_valid_q = 4 * len(batch.observed)
+        stages["classify"] = {"s": tmax(time.perf_counter() - t0), "is_valid_queries": n_valid_q,
+                              "rows_kept": int(rows.rows.sum().item()), "path": "device (sst_classify_rows_device)"}
+        stages["classify"]["kernels"] = kernels()
+
+        barrier()
+        t0 = time.perf_counter()
+        fx = pd.fixpoint_device(dp, rows, max_len)
+        barrier()
+        alpha_u = np.unique(fx.alpha, axis=0)
+        stages["fixpoint"] = {"s": tmax(time.perf_counter() - t0), "rounds": fx.n_rounds,
+                              "rounds_histogram": {int(k): int(v) for k, v in zip(*np.unique(fx.rounds, return_counts=True))},
+                              "explain_queries": int(fx.queries.astype(np.int64).sum()),
+                              "distinct_alphabets": int(len(alpha_u)),
+                              "mean_alphabet_rows": float(pipeline.mask_rows(fx.alpha, len(dp.masses)).sum(1).mean() + 1),
+                              "path": "device (sst_fix_round_device + sst_valid_rows_alpha_device per round)"}
+        stages["fixpoint"]["kernels"] = kernels()
+        fx_alpha = fx.alpha
+        explain_q = int(fx.queries.astype(np.int64).sum())
+        valid_q_rounds = 0  # counted inside the explain launches' rounds; priced with the explains below
+        c_bins = lambda: pd.to_classified(rows)  # noqa: E731
+    busy(stages["classify"])
+    busy(stages["fixpoint"])
 
     barrier()
     t0 = time.perf_counter()
-    fx = pipeline.filter_fixpoint(c, dp, max_len, EXPLANATION_MASSES)
-    barrier()
-    alpha_u = np.unique(fx.alpha, axis=0)
-    stages["fixpoint"] = {"s": tmax(time.perf_counter() - t0), "rounds_max": int(fx.rounds.max()),
-                          "rounds_histogram": {int(k): int(v) for k, v in zip(*np.unique(fx.rounds, return_counts=True))},
-                          "final_round_queries": int(len(fx.last.get("diff", []))),
-                          "explain_queries_per_round": [int(x[0]) for x in fx.queries],
-                          "is_valid_queries_per_round": [int(x[1]) for x in fx.queries],
-                          "rows_kept": int(fx.alive.sum()), "rows_in": int(len(fx.alive)),
-                          "distinct_alphabets": int(len(alpha_u)),
-                          "mean_alphabet_rows": float(pipeline.mask_rows(fx.alpha, len(dp.masses)).sum(1).mean() + 1)}
-    stages["fixpoint"]["kernels"] = {_native.KERNEL_NAMES.get(k, str(k)): v for k, v in engine.profile_read().items()}
-
-    barrier()
-    t0 = time.perf_counter()
-    c3 = pipeline.subset(c, fx.alive)
+    c3 = c_bins()
     q3 = pipeline.bin_queries(c3)
-    st3, cnt3, _, _ = dp.device_table.explain_pairs_alpha(q3.diff, q3.thr, q3.spec, fx.alpha, dp.tolerance,
+    st3, cnt3, _, _ = dp.device_table.explain_pairs_alpha(q3.diff, q3.thr, q3.spec, fx_alpha, dp.tolerance,
                                                           dp.precision)
     barrier()
     stages["bins"] = {"s": tmax(time.perf_counter() - t0), "queries": len(q3.diff),
                       "pair_class": int((st3 != -10).sum()), "not_pair_class": int((st3 == -10).sum()),
                       "with_candidates": int((st3 == 2).sum()), "candidates": int(cnt3[st3 == 2].sum())}
+    stages["bins"]["kernels"] = kernels()
+    busy(stages["bins"])
     engine.profile(False)
 
     # per-spectrum alphabet reduction = a table rebuild (canonical + 3 mods)
@@ -145,15 +199,16 @@ def main():
         peaks_all, spectra_all = (int(x) for x in t.tolist())
     else:
         peaks_all, spectra_all = peaks, args.spectra
-    ref_est = ((stages["classify"]["is_valid_queries"] + sum(x[1] for x in fx.queries)) / 70e3 +
-               (sum(x[0] for x in fx.queries) + stages["bins"]["queries"]) / 4.0e3)
+    ref_est = (n_valid_q + valid_q_rounds) / 70e3 + (explain_q + stages["bins"]["queries"]) / 4.0e3
+    gpu_s = sum(sum(v[0] for v in st["kernels"].values()) / 1e3 for st in stages.values())
     if rank == 0:
         print(json.dumps({
             "workload": "config5: explanation stages of the prediction pipeline (classify_fragments, the "
                         "filter_by_explanation fixpoint with per-spectrum alphabets, skeleton bin queries on the "
                         "reduced alphabets) over synthetic spectra",
             "n_gpus": world, "spectra": spectra_all, "peaks": peaks_all,
-            "stages": stages, "total_s": total_s,
+            "path": "host-driven" if args.host_driven else "device-resident stages 1-2",
+            "stages": stages, "total_s": total_s, "gpu_busy_frac": gpu_s / total_s,
             "spectra_per_s": spectra_all / total_s, "peaks_per_s": peaks_all / total_s,
             "reduction_rebuild_ms": rebuild_ms, "generation_s": gen_s,
             "reference_estimate_s_per_gpu_share": ref_est,
