@@ -400,7 +400,8 @@ int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* 
  * with every array in HBM.  Rows of spectrum g live in slots
  * 4 * d_peak_off[g] + i, i < d_rows[g] (d_rows_* arrays of 4 * n_peaks):
  * su, observed mass, meta = breakage | sides << 2 | is_singleton << 4 | peak
- * position << 8, alive.  Peaks in ascending mass order, <= 1024 per spectrum;
+ * position << 8, alive.  Peaks in any order (ranked by mass on the device, equal
+ * masses in their given order), <= 1024 per spectrum;
  * shifts / sides as sst_step_rows_device.  d_err collects | 1 a spectrum over
  * 1024 peaks, 2 over 2048 rows, 4 a window outside the pair class, 8 a window
  * past a table's end (the reference raises), 16 a dict too large for the LDS
@@ -427,6 +428,27 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
                          const uint8_t* d_active, uint8_t* d_active_next, uint32_t* d_rounds, uint32_t* d_queries,
                          uint32_t* d_n_active, double max_weight, double tolerance, double precision,
                          uint32_t* d_err);
+/* SkeletonBuilder._predict_skeleton's speculative bin queries
+ * (skeleton_building.py:114-160; replaces the per-bin explain calls of
+ * :131-160 for every spectrum at once) over the rows a fixpoint kept
+ * (d_alive), on each spectrum's alphabet d_alpha: per side, bins are runs of
+ * rows whose SU step is <= tol * (obs_prev + obs); the side's first bin
+ * explains its rows' SU masses against 0 (threshold tol * obs), every later
+ * bin each (predecessor row, row) difference (tol * (obs_p + obs_r)); a
+ * side's last bin only with >= 2 rows.  Two calls: count (d_n_q[S] queries
+ * per spectrum, d_q_off[S + 1] their exclusive offsets, the total last), then
+ * emit into d_status / d_count [total], spectrum-major (START side, then END;
+ * bins in order; a bin's pairs predecessor-row-major).  Statuses SST_NONE /
+ * EMPTY / SOME, or -10 for a window outside the pair class (hi >= 3 w_min:
+ * the caller's general path).  d_err bit 2: a spectrum over 2048 rows. */
+int sst_bins_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                          const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                          const uint32_t* d_rows, double tol, uint32_t* d_n_q, uint64_t* d_q_off, uint32_t* d_err);
+int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                         const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                         const uint32_t* d_rows, const uint64_t* d_alpha, double tol, double prec,
+                         const uint64_t* d_q_off, int8_t* d_status, uint32_t* d_count, uint32_t* d_err);
+
 /* _reduce_alphabet's filter (prediction.py:211-227): is_valid_mass of the
  * alive rows of the d_active spectra against their reduced tables (d_alpha),
  * AND-ed into d_alive. */

@@ -32,6 +32,7 @@ EXPORTS = (
     "sst_wire_pack", "sst_explain_pairs_alpha", "sst_explain_pairs_alpha_device", "sst_is_valid_alpha",
     "sst_is_valid_alpha_device", "sst_dict_union", "sst_step_rows_device", "sst_result_queries",
     "sst_classify_rows_device", "sst_fix_round_device", "sst_valid_rows_alpha_device",
+    "sst_bins_count_device", "sst_bins_emit_device",
 )
 
 # kernel ids of sst_profile_read
@@ -158,6 +159,10 @@ def load_library(path=LIB_PATH):
     lib.sst_fix_round_device.restype = _I
     lib.sst_valid_rows_alpha_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _P]
     lib.sst_valid_rows_alpha_device.restype = _I
+    lib.sst_bins_count_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _D, _P, _P, _P]
+    lib.sst_bins_count_device.restype = _I
+    lib.sst_bins_emit_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _P, _P, _P, _P]
+    lib.sst_bins_emit_device.restype = _I
     return lib
 
 

@@ -2020,6 +2020,67 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
   return SST_OK;
 }
 
+static int bins_args(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                     const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                     const uint32_t* d_rows, double tol, double prec, uint64_t* d_q_off, uint32_t* d_err, PipeArgs& a) {
+  if (!t || n_spec < 0 || n_spec > INT32_MAX || !d_q_off ||
+      (n_spec > 0 && (!d_peak_off || !d_rows_su || !d_rows_ob || !d_rows_meta || !d_alive || !d_rows || !d_err)))
+    return SST_E_ARG;
+  if (!t->args.pairs_enabled) return fail(t->ctx, SST_E_ARG, "skeleton bins: the table has no pair list");
+  a = PipeArgs{};
+  a.peak_off = d_peak_off;
+  a.n_spec = n_spec;
+  a.r_su = const_cast<double*>(d_rows_su);
+  a.r_ob = const_cast<double*>(d_rows_ob);
+  a.r_meta = const_cast<uint32_t*>(d_rows_meta);
+  a.alive = const_cast<uint8_t*>(d_alive);
+  a.cnt = const_cast<uint32_t*>(d_rows);
+  a.tol = tol;
+  a.prec = prec;
+  a.rprec = 1.0 / prec;
+  a.q_off = d_q_off;
+  a.err = d_err;
+  return SST_OK;
+}
+
+int sst_bins_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                          const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                          const uint32_t* d_rows, double tol, uint32_t* d_n_q, uint64_t* d_q_off, uint32_t* d_err) {
+  PipeArgs a;
+  if (int rc = bins_args(t, d_peak_off, n_spec, d_rows_su, d_rows_ob, d_rows_meta, d_alive, d_rows, tol, 1.0,
+                         d_q_off, d_err, a))
+    return rc;
+  if (n_spec > 0 && !d_n_q) return SST_E_ARG;
+  a.n_q = d_n_q;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  Prof p(c, SST_K_IS_VALID);
+  HIP_OK(c, launch_bins_count(a, c->n_cu, c->stream));
+  return SST_OK;
+}
+
+int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                         const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                         const uint32_t* d_rows, const uint64_t* d_alpha, double tol, double prec,
+                         const uint64_t* d_q_off, int8_t* d_status, uint32_t* d_count, uint32_t* d_err) {
+  PipeArgs a;
+  if (int rc = bins_args(t, d_peak_off, n_spec, d_rows_su, d_rows_ob, d_rows_meta, d_alive, d_rows, tol, prec,
+                         const_cast<uint64_t*>(d_q_off), d_err, a))
+    return rc;
+  if (n_spec > 0 && (!d_alpha || !d_status || !d_count)) return SST_E_ARG;
+  a.alpha = d_alpha;
+  a.q_status = d_status;
+  a.q_count = d_count;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = check_masks(t)) return rc;
+  Prof p(c, SST_K_EXPLAIN_MAIN);
+  HIP_OK(c, launch_bins_emit(t->args, a, c->n_cu, c->stream));
+  return SST_OK;
+}
+
 int sst_valid_rows_alpha_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                                 const double* d_rows_ob, const uint32_t* d_rows, const uint64_t* d_alpha,
                                 const uint8_t* d_active, uint8_t* d_alive, double tol, double prec, uint32_t* d_err) {

@@ -359,7 +359,7 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
 constexpr int kPipeMaxPeaks = 1024;  // peaks per spectrum the classify workgroup holds
 constexpr int kPipeMaxRows = 2048;   // rows per spectrum (4 breakages)
 struct PipeArgs {
-  const double* obs;          // [n_peaks], sorted within each spectrum
+  const double* obs;          // [n_peaks], any order within each spectrum
   const int64_t* peak_off;    // [n_spec + 1]; rows of spectrum g live at slots 4 * peak_off[g] + i
   int64_t n_spec, n_peaks;
   const double* intensity;
@@ -385,8 +385,14 @@ struct PipeArgs {
   uint32_t* queries;          // [n_spec] explain queries issued over the rounds
   uint32_t* n_active;         // spectra whose alphabet shrank this round
   uint64_t canon[2];          // the canonical rows (never dropped)
+  uint32_t* n_q;              // [n_spec] skeleton bin queries (k_bins count pass)
+  uint64_t* q_off;            // [n_spec + 1] their exclusive offsets (total last)
+  int8_t* q_status;           // [total] per bin query: SST_NONE / EMPTY / SOME, kStatusPending off the pair class
+  uint32_t* q_count;          // [total] candidates on the spectrum's alphabet
   uint32_t* err;
 };
+hipError_t launch_bins_count(const PipeArgs& a, int n_wg, hipStream_t st);
+hipError_t launch_bins_emit(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st);
 hipError_t launch_classify_rows(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st);
 hipError_t launch_fix_round(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st);
 size_t rows_lds_bytes();

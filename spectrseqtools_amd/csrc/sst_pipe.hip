@@ -6,7 +6,9 @@
 //                    the intensity / mass / sequence-mass filters, is_singleton
 //                    (:104-119) and the SU order of the kept rows (a merge of
 //                    the breakages' sorted streams, ties breakage-major as the
-//                    reference's stable sort).  Rows go to fixed slots
+//                    reference's stable sort; a spectrum whose peaks are not in
+//                    mass order is ranked in LDS first, equal masses in their
+//                    given order).  Rows go to fixed slots
 //                    (spectrum g: 4 * peak_off[g] + i), no compaction pass.
 //   k_fix_round      one filter_by_explanation round (prediction.py:170-227)
 //                    of every spectrum still reducing: the alive rows, the
@@ -22,6 +24,17 @@
 //                    the alphabet shrinks.  is_valid on the reduced tables
 //                    follows in k_valid_alpha (sst_alpha.hip, AND-ed into the
 //                    rows' alive flags).
+//   k_bins_count /   SkeletonBuilder._predict_skeleton's speculative bin
+//   k_bins_emit      queries (skeleton_building.py:114-160) over the rows the
+//                    fixpoint kept: per side, bins are runs of rows whose SU
+//                    step is within the pair threshold; the side's first bin
+//                    explains its whole masses (against 0), every later bin
+//                    each (predecessor row, row) difference; a side's last bin
+//                    only when it has two rows or more (:150-153).  Count pass,
+//                    exclusive scan (k_scan_u32), then every query answered on
+//                    its spectrum's alphabet into a dense spectrum-major list
+//                    (per spectrum: START side, then END; per side its bins in
+//                    order, a bin's pairs predecessor-row-major).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -80,8 +93,16 @@ __device__ __forceinline__ int8_t masked_answer(const TableArgs& t, double mass,
   return cnt ? (int8_t)SST_SOME : lof <= 0.0 ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;
 }
 
+// every peak's mass <= the next one's (whole list, any P)
+__device__ __forceinline__ bool peaks_sorted(const double* obs, uint32_t P) {
+  bool ok = true;
+  for (uint32_t p = threadIdx.x; p + 1 < P; p += blockDim.x) ok &= obs[p] <= obs[p + 1];
+  return __syncthreads_and(ok);
+}
+
 struct ClsLds {
   double obs[kPipeMaxPeaks];
+  uint16_t ord[kPipeMaxPeaks];      // peaks in (mass, position) order
   uint16_t kidx[4][kPipeMaxPeaks];
   uint8_t keep[kPipeMaxPeaks];
   uint32_t kcnt[4];
@@ -127,11 +148,28 @@ __global__ __launch_bounds__(kPipeWG) void k_classify_rows(TableArgs t, PipeArgs
       L.keep[p] = kp;
     }
     __syncthreads();
+    // the peaks in ascending mass order, equal masses in their given order (a
+    // peak list need not be sorted; a breakage's rows are then in SU order)
+    const bool sorted = peaks_sorted(L.obs, P);
+    for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) {
+      uint32_t rank = p;
+      if (!sorted) {
+        const double o = L.obs[p];
+        rank = 0;
+        for (uint32_t q = 0; q < P; ++q) {
+          const double v = L.obs[q];
+          rank += (v < o) | ((v == o) & (q < p));
+        }
+      }
+      L.ord[rank] = (uint16_t)p;
+    }
+    __syncthreads();
     for (int k = 0; k < a.n_shifts; ++k) {
       uint32_t carry = 0;
       for (uint32_t q0 = 0; q0 < P; q0 += blockDim.x) {
-        const uint32_t p = q0 + threadIdx.x;
-        const uint32_t f = p < P ? (L.keep[p] >> k) & 1u : 0u;
+        const uint32_t i = q0 + threadIdx.x;
+        const uint32_t p = i < P ? L.ord[i] : 0u;
+        const uint32_t f = i < P ? (L.keep[p] >> k) & 1u : 0u;
         uint32_t tot;
         const uint32_t ex = block_excl(f, L.w, tot);
         if (f) L.kidx[k][carry + ex] = (uint16_t)p;
@@ -396,6 +434,228 @@ __global__ __launch_bounds__(kPipeWG) void k_fix_round(TableArgs t, PipeArgs a) 
     }
     __syncthreads();
   }
+}
+
+namespace {
+
+struct BinLds {
+  double su[kPipeMaxRows];
+  double ob[kPipeMaxRows];
+  uint16_t side[2][kPipeMaxRows];        // alive rows of each side, SU order
+  uint16_t bstart[2][kPipeMaxRows + 1];  // per side: first row of each bin, then the row count
+  uint32_t qoff[2][kPipeMaxRows + 1];    // per side: exclusive prefix of each bin's queries
+  uint32_t n_side[2], nb[2];
+  uint32_t w[16];
+};
+
+// the alive rows of spectrum g and each side's list (false: too many rows)
+__device__ bool bins_load(BinLds& L, const PipeArgs& a, int64_t g) {
+  const int64_t base = 4 * a.peak_off[g];
+  const uint32_t nr = a.cnt[g];
+  if (nr > (uint32_t)kPipeMaxRows) return false;
+  uint32_t carry[3] = {0, 0, 0};
+  for (uint32_t r0 = 0; r0 < nr; r0 += blockDim.x) {
+    const uint32_t r = r0 + threadIdx.x;
+    const bool al = r < nr && a.alive[base + r];
+    const uint32_t meta = al ? a.r_meta[base + r] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl(al ? 1u : 0u, L.w, tot);
+    const uint32_t i = carry[0] + ex;
+    if (al) {
+      L.su[i] = a.r_su[base + r];
+      L.ob[i] = a.r_ob[base + r];
+    }
+    carry[0] += tot;
+    for (int c = 0; c < 2; ++c) {
+      const bool f = al && ((meta >> (2 + c)) & 1u);  // START, END
+      const uint32_t x = block_excl(f ? 1u : 0u, L.w, tot);
+      if (f) L.side[c][carry[c + 1] + x] = (uint16_t)i;
+      carry[c + 1] += tot;
+    }
+  }
+  if (threadIdx.x == 0) {
+    L.n_side[0] = carry[1];
+    L.n_side[1] = carry[2];
+  }
+  __syncthreads();
+  return true;
+}
+
+// side sd's bins and each bin's query count prefix; returns the side's queries
+__device__ uint32_t bins_side(BinLds& L, int sd, double tol) {
+  const uint32_t n = L.n_side[sd];
+  const uint16_t* rs = L.side[sd];
+  uint32_t carry = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {
+    const uint32_t i = i0 + threadIdx.x;
+    // row i joins row i - 1's bin when their SU step is within the pair threshold (:130-136)
+    const bool starts = i < n && (i == 0 || !(L.su[rs[i]] - L.su[rs[i - 1]] <= tol * (L.ob[rs[i - 1]] + L.ob[rs[i]])));
+    uint32_t tot;
+    const uint32_t ex = block_excl(starts ? 1u : 0u, L.w, tot);
+    if (starts) L.bstart[sd][carry + ex] = (uint16_t)i;
+    carry += tot;
+  }
+  const uint32_t nb = carry;
+  if (threadIdx.x == 0) {
+    L.bstart[sd][nb] = (uint16_t)n;
+    L.nb[sd] = nb;
+  }
+  __syncthreads();
+  carry = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += blockDim.x) {
+    const uint32_t b = b0 + threadIdx.x;
+    uint32_t c = 0;
+    if (b < nb) {
+      const uint32_t size = (uint32_t)L.bstart[sd][b + 1] - L.bstart[sd][b];
+      const bool closed = b + 1 < nb || size > 1;  // a later row closes it, or the side's last row joined it
+      if (closed) c = b == 0 ? size : ((uint32_t)L.bstart[sd][b] - L.bstart[sd][b - 1]) * size;
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl(c, L.w, tot);
+    if (b < nb) L.qoff[sd][b] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) L.qoff[sd][nb] = carry;
+  __syncthreads();
+  return carry;
+}
+
+// query q of side sd: the first bin's whole mass against 0, a later bin's
+// (predecessor row, row) difference; threshold as calculate_error_threshold
+__device__ __forceinline__ void bins_query(const BinLds& L, int sd, uint32_t q, double tol, double& mass,
+                                           double& thr) {
+  uint32_t lo = 0, hi = L.nb[sd];  // last bin with qoff <= q (empty bins share their successor's offset)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (L.qoff[sd][mid] <= q) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t b = lo, local = q - L.qoff[sd][b];
+  const uint16_t* rs = L.side[sd];
+  if (b == 0) {
+    const uint32_t m = rs[L.bstart[sd][0] + local];
+    mass = L.su[m];
+    thr = tol * (0.0 + L.ob[m]);
+    return;
+  }
+  const uint32_t csz = (uint32_t)L.bstart[sd][b + 1] - L.bstart[sd][b];
+  const uint32_t p = rs[L.bstart[sd][b - 1] + local / csz], r = rs[L.bstart[sd][b] + local % csz];
+  mass = L.su[r] - L.su[p];
+  thr = tol * (L.ob[p] + L.ob[r]);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kPipeWG) void k_bins_count(PipeArgs a) {
+  __shared__ BinLds L;
+  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
+    if (!bins_load(L, a, g)) {
+      if (threadIdx.x == 0) {
+        atomicOr(a.err, 2u);
+        a.n_q[g] = 0;
+      }
+      continue;
+    }
+    const uint32_t q0 = bins_side(L, 0, a.tol);
+    const uint32_t q1 = bins_side(L, 1, a.tol);
+    if (threadIdx.x == 0) a.n_q[g] = q0 + q1;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kPipeWG) void k_bins_emit(TableArgs t, PipeArgs a) {
+  __shared__ BinLds L;
+  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
+    if (!bins_load(L, a, g)) continue;
+    const uint32_t q0 = bins_side(L, 0, a.tol);
+    const uint32_t q1 = bins_side(L, 1, a.tol);
+    const uint64_t base = a.q_off[g];
+    const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+    for (uint32_t o = threadIdx.x; o < q0 + q1; o += blockDim.x) {
+      const int sd = o >= q0;
+      double mass, thr;
+      bins_query(L, sd, sd ? o - q0 : o, a.tol, mass, thr);
+      double lof, hif;
+      quantise_lean(mass, thr, a.prec, a.rprec, lof, hif);
+      int8_t st = SST_NONE;
+      uint32_t cnt = 0;
+      if (!(hif < (double)t.pair_hi)) {
+        st = (int8_t)kStatusPending;  // not a pair-class window: the caller's other path
+      } else if (hif >= 0.0) {
+        const double af = lof < 1.0 ? 1.0 : lof;
+        uint64_t u0 = 0, u1 = 0;
+        if (af <= hif) cnt = masked_walk(t, (uint32_t)af, (uint32_t)hif, m0, m1, u0, u1);
+        st = cnt ? (int8_t)SST_SOME : lof <= 0.0 ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;
+      }
+      a.q_status[base + o] = st;
+      a.q_count[base + o] = cnt;
+    }
+    __syncthreads();
+  }
+}
+
+// exclusive prefix of n u32 counts into n + 1 u64 offsets (one workgroup,
+// chunks staged through LDS so that loads and stores are coalesced)
+__global__ __launch_bounds__(kPipeWG) void k_scan_u32(const uint32_t* in, uint64_t* out, int64_t n) {
+  constexpr int kPer = 8, kChunk = kPer * kPipeWG;
+  __shared__ uint64_t s_buf[kChunk];
+  __shared__ uint64_t s_w[16];
+  uint64_t carry = 0;
+  for (int64_t c0 = 0; c0 < n; c0 += kChunk) {
+    const int m = (int)(n - c0 < kChunk ? n - c0 : kChunk);
+    uint32_t x[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int i = threadIdx.x + k * kPipeWG;
+      x[k] = i < m ? in[c0 + i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) s_buf[threadIdx.x + k * kPipeWG] = x[k];
+    __syncthreads();
+    uint64_t v[kPer], run = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      v[j] = s_buf[threadIdx.x * kPer + j];
+      run += v[j];
+    }
+    // block-wide exclusive scan of the runs (wave shuffles, then the waves' sums)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint64_t incl = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    uint64_t base = carry, tot = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+      if (w < wv) base += s_w[w];
+      tot += s_w[w];
+    }
+    base += incl - run;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+      s_buf[threadIdx.x * kPer + j] = base;
+      base += v[j];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += blockDim.x) out[c0 + i] = s_buf[i];
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[n] = carry;
+}
+
+hipError_t launch_bins_count(const PipeArgs& a, int n_wg, hipStream_t st) {
+  if (a.n_spec > 0) hipLaunchKernelGGL(k_bins_count, dim3(n_wg), dim3(kPipeWG), 0, st, a);
+  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(kPipeWG), 0, st, (const uint32_t*)a.n_q, a.q_off, a.n_spec);
+  return hipGetLastError();
+}
+hipError_t launch_bins_emit(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st) {
+  if (a.n_spec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bins_emit, dim3(n_wg), dim3(kPipeWG), 0, st, t, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_classify_rows(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st) {

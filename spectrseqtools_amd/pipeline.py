@@ -266,8 +266,9 @@ def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolera
     canon = row_masks((~is_mod & (np.arange(N) > 0))[None, :])[0]
     # budgets: max_modifications = round(0.5 max_len) (common.py:55) and the
     # modification rows' caps round(max_len * rate) (mass_explanation.py:158-172)
-    A = np.array([round(dp_table.seq.modification_rate * int(L)) for L in max_len], dtype=np.int64)
-    cap_min = np.array([min([round(int(L) * r) for r in rate[is_mod]] or [2]) for L in max_len], dtype=np.int64)
+    A = np.round(dp_table.seq.modification_rate * max_len.astype(np.float64)).astype(np.int64)  # ties to even
+    cap_min = (np.round(np.outer(max_len.astype(np.float64), rate[is_mod])).min(axis=1).astype(np.int64)
+               if is_mod.any() else np.full(S, 2, dtype=np.int64))
     if (A < 2).any() or (cap_min < 2).any():
         raise NotImplementedError("filter_fixpoint: budgets that can bind on pair windows (max_len too small)")
     max_w = max(explanation_masses.get_column("monoisotopic_mass").to_list()) + PHOSPHATE_LINK_MASS
@@ -279,7 +280,7 @@ def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolera
     history = []
     parts = []  # (spectra active in the round, the round's queries and answers)
     n_queries = []
-    pop = lambda m: np.array([bin(int(a)).count("1") + bin(int(b)).count("1") for a, b in m], dtype=np.int64)
+    pop = lambda m: np.bitwise_count(np.asarray(m, dtype=np.uint64)).sum(axis=1)  # noqa: E731
     while active.any():
         rows = np.flatnonzero(alive & active[c.spec])
         off = np.searchsorted(c.spec[rows], np.arange(S + 1))

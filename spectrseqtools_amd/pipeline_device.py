@@ -1,9 +1,11 @@
-"""Config 5 with every stage's arrays in HBM: classify_fragments
-and the filter_by_explanation fixpoint over many spectra, driven from the
-host one launch per stage / round (sst_classify_rows_device,
-sst_fix_round_device, sst_valid_rows_alpha_device; kernels in
-csrc/sst_pipe.hip and csrc/sst_alpha.hip).  The host only loops the rounds
-(one 4-byte read per round: how many spectra are still reducing).
+"""Config 5 with every stage's arrays in HBM: classify_fragments,
+the filter_by_explanation fixpoint and the skeleton's speculative bin
+queries over many spectra, driven from the host one launch per stage / round
+(sst_classify_rows_device, sst_fix_round_device, sst_valid_rows_alpha_device,
+sst_bins_count_device / sst_bins_emit_device; kernels in csrc/sst_pipe.hip
+and csrc/sst_alpha.hip).  The host only loops the rounds (one 4-byte read per
+round: how many spectra are still reducing) and sizes the bin answers (one
+8-byte read).
 
 Rows of spectrum g sit in slots 4 * peak_off[g] + i (i < rows[g]), in the
 SU order of its classify_fragments frame, so a row's slot offset is the
@@ -44,9 +46,11 @@ class DeviceRows:
 
 def classify_device(dp_table, obs, offsets, su_seq, breakage_dict, intensity=None, intensity_cutoff=0.5e6,
                     mass_cutoff=50000, keep_valid=False, device=None):
-    """Stage 1 on the device.  obs: every spectrum's peaks in ascending mass
-    order (spectrum g: obs[offsets[g]:offsets[g+1]]), su_seq[g] its
-    SequenceInformation.su_mass."""
+    """Stage 1 on the device.  obs: every spectrum's peaks (spectrum g:
+    obs[offsets[g]:offsets[g+1]]), su_seq[g] its SequenceInformation.su_mass.
+    Peaks may come in any order: the kernel ranks each spectrum's peaks by
+    mass in LDS (equal masses keep their order, so the rows' SU order and its
+    ties are the reference's); the rows' peak positions are the caller's."""
     import torch
 
     dev = device or torch.device("cuda", dp_table.device_table.engine.device)
@@ -111,8 +115,10 @@ def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=MATCHING_THRE
     is_mod = np.array([m.is_modification for m in masses])
     rate = np.array([m.modification_rate for m in masses], dtype=np.float64)
     max_len = np.broadcast_to(np.asarray(max_len, dtype=np.int64), (S,))
-    A = np.array([round(dp_table.seq.modification_rate * int(L)) for L in max_len], dtype=np.int64)
-    cap_min = np.array([min([round(int(L) * r) for r in rate[is_mod]] or [2]) for L in max_len], dtype=np.int64)
+    # round() on the same f64 products, ties to even like Python's round (vectorised over spectra)
+    A = np.round(dp_table.seq.modification_rate * max_len.astype(np.float64)).astype(np.int64)
+    cap_min = (np.round(np.outer(max_len.astype(np.float64), rate[is_mod])).min(axis=1).astype(np.int64)
+               if is_mod.any() else np.full(S, 2, dtype=np.int64))
     if (A < 2).any() or (cap_min < 2).any():
         raise NotImplementedError("fixpoint_device: budgets that can bind on pair windows (max_len too small)")
     full = np.zeros((1, N), bool)
@@ -179,3 +185,46 @@ def to_classified(rows: DeviceRows, alive_only=True):
     offsets = np.searchsorted(spec, np.arange(S + 1))
     return Classified(spec, su, ob, (meta >> 8).astype(np.int64), (meta & 3).astype(np.int64),
                       ((meta >> 4) & 1).astype(bool), rows.names, offsets, 0, 0)
+
+
+@dataclass
+class DeviceBins:
+    """The skeleton's speculative bin queries of every spectrum, answered on
+    its alphabet (spectrum-major: START side, then END; bins in order)."""
+    q_off: np.ndarray     # [S + 1] query offsets per spectrum
+    status: object        # torch int8 [Q]: SST_NONE / EMPTY / SOME, -10 off the pair class
+    count: object         # torch int32 [Q] candidates
+
+
+def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=MATCHING_THRESHOLD):
+    """Stage 3 on the device (SkeletonBuilder._predict_skeleton's bins,
+    skeleton_building.py:114-160) over the rows the fixpoint kept
+    (rows.alive) and the final alphabets `alpha` ([S, 2] u64 row masks)."""
+    import torch
+
+    S = len(rows.rows)
+    dev = rows.su.device
+    a = torch.as_tensor(np.ascontiguousarray(alpha, dtype=np.uint64).view(np.int64), device=dev)
+    n_q = torch.zeros(max(1, S), dtype=torch.int32, device=dev)
+    q_off = torch.zeros(S + 1, dtype=torch.int64, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    eng = dp_table.device_table.engine
+    L = eng._lib
+    h = dp_table.device_table.handle
+    torch.cuda.synchronize(dev)
+    eng.check(L.sst_bins_count_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(), rows.obs.data_ptr(),
+                                      rows.meta.data_ptr(), rows.alive.data_ptr(), rows.rows.data_ptr(),
+                                      float(tolerance), n_q.data_ptr(), q_off.data_ptr(), err.data_ptr()),
+              "sst_bins_count_device")
+    eng.synchronize()
+    _check_err(err)
+    total = int(q_off[S].item())
+    status = torch.empty(max(1, total), dtype=torch.int8, device=dev)
+    count = torch.empty(max(1, total), dtype=torch.int32, device=dev)
+    eng.check(L.sst_bins_emit_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(), rows.obs.data_ptr(),
+                                     rows.meta.data_ptr(), rows.alive.data_ptr(), rows.rows.data_ptr(), a.data_ptr(),
+                                     float(tolerance), float(dp_table.precision), q_off.data_ptr(),
+                                     status.data_ptr(), count.data_ptr(), err.data_ptr()), "sst_bins_emit_device")
+    eng.synchronize()
+    _check_err(err)
+    return DeviceBins(q_off.cpu().numpy(), status[:total], count[:total])

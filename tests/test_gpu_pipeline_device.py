@@ -4,9 +4,12 @@ sst_classify_rows_device, sst_fix_round_device, sst_valid_rows_alpha_device):
     reference's own classify_fragments frame row for row, and every
     filter_by_explanation round's alphabet and kept fragments equal the
     reference's (tests/golden/callers.json.gz);
-  * on synthetic spectra: rows, final alphabets, surviving rows and round
-    counts equal the host-driven columnar stages (pipeline.classify /
-    filter_fixpoint, pinned to the per-spectrum mirrors in the CPU suite)."""
+  * on synthetic spectra (peaks sorted and as generated): rows, final
+    alphabets, surviving rows and round counts equal the host-driven columnar
+    stages (pipeline.classify / filter_fixpoint, pinned to the per-spectrum
+    mirrors in the CPU suite), and the device skeleton-bin answers equal the
+    host-built bin queries (pipeline.bin_queries) answered on the same
+    alphabets."""
 import numpy as np
 import pytest
 
@@ -41,10 +44,8 @@ def test_device_classify_and_fixpoint_vs_reference(engine, callers, tc):
     inp = {c: [r[i] for r in rec["input"]["rows"]] for i, c in enumerate(cols)}
     obs = np.asarray(inp["observed_mass" if "observed_mass" in inp else "neutral_mass"], dtype=np.float64)
     inten = np.asarray(inp["intensity"], dtype=np.float64) if "intensity" in inp else None
-    perm = np.argsort(obs, kind="stable")  # the device stage takes a mass-sorted peak list
-    bd = build_breakage_dict(*rec["tags"])
-    rows = PD.classify_device(dp, obs[perm], [0, len(obs)], [dp.seq.su_mass], bd,
-                              intensity=None if inten is None else inten[perm],
+    bd = build_breakage_dict(*rec["tags"])  # the reference's own input, in its peak order
+    rows = PD.classify_device(dp, obs, [0, len(obs)], [dp.seq.su_mass], bd, intensity=inten,
                               intensity_cutoff=rec["intensity_cutoff"])
     n = int(rows.rows.cpu()[0])
     want = rec["classify"]
@@ -55,7 +56,7 @@ def test_device_classify_and_fixpoint_vs_reference(engine, callers, tc):
     assert rows.obs.cpu().numpy()[:n].tolist() == wc["observed_mass"]
     assert [rows.names[m & 3] for m in meta] == wc["breakage"]
     assert [bool((m >> 4) & 1) for m in meta] == wc["is_singleton"]
-    assert perm[meta >> 8].tolist() == wc["fragment_index"]
+    assert (meta >> 8).tolist() == wc["fragment_index"]
     fx = PD.fixpoint_device(dp, rows, [dp.seq.max_len], record=True)
     rounds = rec["filter"]["rounds"]
     assert fx.n_rounds == len(rounds) == int(fx.rounds[0])
@@ -65,14 +66,17 @@ def test_device_classify_and_fixpoint_vs_reference(engine, callers, tc):
         assert np.flatnonzero(alive[:n]).tolist() == rounds[k]["kept_index"], k
 
 
-def test_device_stages_equal_host_driven(engine):
+@pytest.mark.parametrize("peak_order", ["sorted", "as_generated"])
+def test_device_stages_equal_host_driven(engine, peak_order):
     from spectrseqtools_amd import pipeline, pipeline_device as PD
     from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
     from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict
     from spectrseqtools_amd.synthetic import make_spectra
 
     b = make_spectra(600, seed=31)
-    obs = b.observed[np.lexsort((b.observed, b.spectrum))]
+    # as generated, each spectrum's noise peaks follow its fragment peaks (not
+    # in mass order): the device ranks them, the host sorts the rows
+    obs = b.observed[np.lexsort((b.observed, b.spectrum))] if peak_order == "sorted" else b.observed
     bd = build_breakage_dict(555.1294, 455.1491)
     w_full = [k for k, v in bd.items() if "START_END" in v][0]
     su_seq = b.seq_mass - w_full * TOLERANCE
@@ -89,9 +93,25 @@ def test_device_stages_equal_host_driven(engine):
     assert np.array_equal(rows.su.cpu().numpy()[slot], c.su)
     meta = rows.meta.cpu().numpy()[slot].astype(np.int64)
     assert np.array_equal(meta & 3, c.brk) and np.array_equal(((meta >> 4) & 1).astype(bool), c.singleton)
+    assert np.array_equal(meta >> 8, c.frag)  # the caller's peak positions
+    assert np.array_equal(PD.to_classified(rows, alive_only=False).frag, c.frag)
     fx_h = pipeline.filter_fixpoint(c, dp, max_len, EXPLANATION_MASSES)
     fx_d = PD.fixpoint_device(dp, rows, max_len)
     assert np.array_equal(fx_d.alpha, fx_h.alpha)
     assert np.array_equal(fx_d.rounds, fx_h.rounds)
     assert np.array_equal(rows.alive.cpu().numpy()[slot].astype(bool), fx_h.alive)
     assert int(fx_d.queries.sum()) == sum(q[0] for q in fx_h.queries)
+    # stage 3: the skeleton's bin queries on the device against the host-built
+    # queries (pipeline.bin_queries, pinned to the per-spectrum walk in the CPU
+    # suite) answered by explain_pairs_alpha; host order -> spectrum-major
+    c3 = pipeline.subset(c, fx_h.alive)
+    q3 = pipeline.bin_queries(c3)
+    st3, cnt3, _, _ = dp.device_table.explain_pairs_alpha(q3.diff, q3.thr, q3.spec, fx_h.alpha, dp.tolerance,
+                                                          dp.precision)
+    order = np.lexsort((q3.side, q3.spec))  # stable: a side's queries keep their order
+    db = PD.bins_device(dp, rows, fx_d.alpha)
+    S = len(b.offsets) - 1
+    assert np.array_equal(np.diff(db.q_off), np.bincount(q3.spec, minlength=S))
+    assert np.array_equal(db.status.cpu().numpy(), st3[order])
+    assert np.array_equal(db.count.cpu().numpy().astype(np.int64), cnt3[order].astype(np.int64))
+    assert (st3 == 2).sum() > 0

@@ -27,10 +27,11 @@ reference Python cannot run on the GPU box; `reference_estimate_s` prices the
 same query counts at its measured single-core rates (is_valid
 70 k/s, sliding-window explain 3.6-4.5 k/s).
 
-Stages 1-2 run device-resident by default (pipeline_device: classify and
-every fixpoint round in HBM, the host reads one counter per round); with
---host-driven through the host-driven batched path (pipeline.classify /
-filter_fixpoint).  Every stage reports its event-timed kernel time and the
+All three stages run device-resident by default (pipeline_device: classify,
+every fixpoint round and the bin queries in HBM; the host reads one counter
+per round and the bins' total); with --host-driven through the host-driven
+batched path (pipeline.classify / filter_fixpoint / bin_queries +
+k_pairs_alpha).  Every stage reports its event-timed kernel time and the
 GPU-busy share of its wall time.
 
 Usage: python tools/pipeline_bench.py [--spectra 100000] [--seed 7] [--host-driven]
@@ -134,7 +135,7 @@ def main():
         fx_alpha = fx.alpha
         explain_q = sum(x[0] for x in fx.queries)
         valid_q_rounds = sum(x[1] for x in fx.queries)
-        c_bins = lambda: pipeline.subset(c, fx.alive)  # noqa: E731
+        rows = None
     else:
         from spectrseqtools_amd import pipeline_device as pd
 
@@ -162,20 +163,31 @@ def main():
         fx_alpha = fx.alpha
         explain_q = int(fx.queries.astype(np.int64).sum())
         valid_q_rounds = 0  # counted inside the explain launches' rounds; priced with the explains below
-        c_bins = lambda: pd.to_classified(rows)  # noqa: E731
+
     busy(stages["classify"])
     busy(stages["fixpoint"])
 
     barrier()
     t0 = time.perf_counter()
-    c3 = c_bins()
-    q3 = pipeline.bin_queries(c3)
-    st3, cnt3, _, _ = dp.device_table.explain_pairs_alpha(q3.diff, q3.thr, q3.spec, fx_alpha, dp.tolerance,
-                                                          dp.precision)
+    if rows is None:  # host-built bin queries, answered by k_pairs_alpha
+        c3 = pipeline.subset(c, fx.alive)
+        q3 = pipeline.bin_queries(c3)
+        st3, cnt3, _, _ = dp.device_table.explain_pairs_alpha(q3.diff, q3.thr, q3.spec, fx_alpha, dp.tolerance,
+                                                              dp.precision)
+        n_bins_q = len(q3.diff)
+        n_some, n_pend, n_cand = int((st3 == 2).sum()), int((st3 == -10).sum()), int(cnt3[st3 == 2].sum())
+    else:  # device-resident: bins formed and answered in HBM, only the tallies read back
+        from spectrseqtools_amd import pipeline_device as pd
+
+        db = pd.bins_device(dp, rows, fx_alpha)
+        some = db.status == 2
+        n_bins_q = int(db.q_off[-1])
+        n_some, n_pend = int(some.sum().item()), int((db.status == -10).sum().item())
+        n_cand = int(db.count[some].sum().item())
     barrier()
-    stages["bins"] = {"s": tmax(time.perf_counter() - t0), "queries": len(q3.diff),
-                      "pair_class": int((st3 != -10).sum()), "not_pair_class": int((st3 == -10).sum()),
-                      "with_candidates": int((st3 == 2).sum()), "candidates": int(cnt3[st3 == 2].sum())}
+    stages["bins"] = {"s": tmax(time.perf_counter() - t0), "queries": n_bins_q,
+                      "pair_class": n_bins_q - n_pend, "not_pair_class": n_pend,
+                      "with_candidates": n_some, "candidates": n_cand}
     stages["bins"]["kernels"] = kernels()
     busy(stages["bins"])
     engine.profile(False)
@@ -207,7 +219,7 @@ def main():
                         "filter_by_explanation fixpoint with per-spectrum alphabets, skeleton bin queries on the "
                         "reduced alphabets) over synthetic spectra",
             "n_gpus": world, "spectra": spectra_all, "peaks": peaks_all,
-            "path": "host-driven" if args.host_driven else "device-resident stages 1-2",
+            "path": "host-driven" if args.host_driven else "device-resident",
             "stages": stages, "total_s": total_s, "gpu_busy_frac": gpu_s / total_s,
             "spectra_per_s": spectra_all / total_s, "peaks_per_s": peaks_all / total_s,
             "reduction_rebuild_ms": rebuild_ms, "generation_s": gen_s,
