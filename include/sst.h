@@ -451,7 +451,9 @@ int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
 
 /* _reduce_alphabet's filter (prediction.py:211-227): is_valid_mass of the
  * alive rows of the d_active spectra against their reduced tables (d_alpha),
- * AND-ed into d_alive. */
+ * AND-ed into d_alive.  A spectrum whose alphabet did not change needs no
+ * re-filter (its rows already passed that table), so a fixpoint passes the
+ * round's changed flags (sst_fix_round_device's d_active_next). */
 int sst_valid_rows_alpha_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                                 const double* d_rows_ob, const uint32_t* d_rows, const uint64_t* d_alpha,
                                 const uint8_t* d_active, uint8_t* d_alive, double tolerance, double precision,

@@ -39,29 +39,32 @@ namespace sst {
 
 namespace {
 
-constexpr int kChunkWords = 4096;              // 64-bit words per chunk
-constexpr int64_t kChunkBits = kChunkWords * 64;  // 262144 masses
-constexpr int kRing = 4;                        // chunks kept in LDS (128 KB)
+constexpr int kChunkWords = 8192;                 // 32-bit words per chunk
+constexpr int64_t kChunkBits = kChunkWords * 32;  // 262144 masses
+constexpr int kRing = 4;                          // chunks kept in LDS (128 KB)
+constexpr int kRingMask = kRing * kChunkWords - 1;
 constexpr int kValidWG = 1024;
 
 __device__ __forceinline__ bool row_in(uint64_t m0, uint64_t m1, int r) {
   return r < 64 ? ((m0 >> r) & 1ull) : ((m1 >> (r - 64)) & 1ull);
 }
 
+__device__ __forceinline__ uint64_t ring_word(const uint32_t* ring, int64_t wi) {
+  return wi < 0 ? 0ull : (uint64_t)ring[wi & kRingMask];
+}
+
 // 64 closure bits starting at mass x (x may be negative: zeros) from the ring
-__device__ __forceinline__ uint64_t ring_bits(const uint64_t* ring, int64_t x) {
+__device__ __forceinline__ uint64_t ring_bits(const uint32_t* ring, int64_t x) {
   if (x < -63) return 0ull;
-  const int64_t wi = x >> 6;  // floor
-  const int s = (int)(x & 63);
-  const uint64_t lo = wi < 0 ? 0ull : ring[((wi >> 12) & (kRing - 1)) * kChunkWords + (wi & (kChunkWords - 1))];
+  const int64_t wi = x >> 5;  // floor
+  const int s = (int)(x & 31);
+  const uint64_t lo = ring_word(ring, wi) | ring_word(ring, wi + 1) << 32;
   if (s == 0) return lo;
-  const int64_t wj = wi + 1;
-  const uint64_t hi = wj < 0 ? 0ull : ring[((wj >> 12) & (kRing - 1)) * kChunkWords + (wj & (kChunkWords - 1))];
-  return (lo >> s) | (hi << (64 - s));
+  return (lo >> s) | (ring_word(ring, wi + 2) << (64 - s));
 }
 
 // any closure bit in [a, b] (both inside the ring's chunks)
-__device__ __forceinline__ bool ring_any(const uint64_t* ring, int64_t a, int64_t b) {
+__device__ __forceinline__ bool ring_any(const uint32_t* ring, int64_t a, int64_t b) {
   for (int64_t x = a; x <= b; x += 64) {
     uint64_t v = ring_bits(ring, x);
     const int64_t left = b - x + 1;
@@ -87,7 +90,7 @@ __device__ __forceinline__ void alpha_put(const AlphaArgs& a, int64_t i, int8_t 
 }
 
 __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
-  __shared__ uint64_t ring[kRing * kChunkWords];
+  __shared__ uint32_t ring[kRing * kChunkWords + 64];  // + slot 0's first 64 words again (reads past the end)
   __shared__ int s_w[kMaxRows];
   __shared__ int s_n;
   __shared__ int64_t s_done;   // queries [q0, s_done) answered
@@ -113,6 +116,11 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
     for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) alpha_put(a, i, 0);
     return;
   }
+  // chunks below mass 0 read as empty: zero the ring (slots are reused across spectra)
+  for (int i = threadIdx.x; i < kRing * kChunkWords + 64; i += blockDim.x) ring[i] = 0u;
+  // the row masses, lane r of every wave holding rows r and r + 64
+  const int w_lo = (int)(threadIdx.x & 63) < n_w ? s_w[threadIdx.x & 63] : 0;
+  const int w_hi = (int)(threadIdx.x & 63) + 64 < n_w ? s_w[(threadIdx.x & 63) + 64] : 0;
   int wmax = 0, wmin = INT32_MAX;
   for (int k = 0; k < n_w; ++k) {
     wmax = s_w[k] > wmax ? s_w[k] : wmax;
@@ -140,19 +148,44 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   const int64_t n_chunks = top / kChunkBits + 1;
   const bool guard_ok = wmin >= kChunkBits && wmax < 3 * kChunkBits;  // the ring's dependency window
   for (int64_t j = 0; j < n_chunks && guard_ok; ++j) {
-    uint64_t* cur = ring + (j & (kRing - 1)) * kChunkWords;
+    uint32_t* cur = ring + (j & (kRing - 1)) * kChunkWords;
     const int64_t base = j * kChunkBits;
     bool all_ones = true;
-    for (int k = threadIdx.x; k < kChunkWords; k += blockDim.x) {
-      uint64_t v = 0;
+    // Each wave writes 63 consecutive words per pass: a row's shifted word
+    // for output word o needs ring words wi and wi + 1, and wi + 1 is the next
+    // lane's wi (a DPP lane shift), so the 64 lanes read 64 words and the
+    // last lane only supplies its neighbour.  The shift is wave-uniform.
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, n_wv = blockDim.x >> 6;
+    for (int o0 = 63 * wv; o0 < kChunkWords; o0 += 63 * n_wv) {
+      const int o = o0 + lane;
+      uint32_t v = 0;
       if (!s_full) {
-        if (j == 0 && k == 0) v = 1ull;  // mass 0: the empty multiset (table[0, 0] seed)
-        for (int r = 0; r < n_w; ++r) v |= ring_bits(ring, base + 64 * (int64_t)k - s_w[r]);
+        if (j == 0 && o == 0) v = 1u;  // mass 0: the empty multiset (table[0, 0] seed)
+        // the wave's first output mass (masses < limit < 2^31), wave-uniform: the
+        // shifts and ring offsets below are scalar arithmetic
+        const int m0 = (int)base + 32 * __builtin_amdgcn_readfirstlane(o0);
+        // two rows per step: their LDS reads are in flight together
+        for (int r = 0; r < n_w; r += 2) {
+          // the rows' masses from the lanes that hold the list (no LDS round trip)
+          const int x0 = m0 - __builtin_amdgcn_readlane(r < 64 ? w_lo : w_hi, r & 63);
+          const int r1 = r + 1 < n_w ? r + 1 : r;
+          const int x1 = m0 - __builtin_amdgcn_readlane(r1 < 64 ? w_lo : w_hi, r1 & 63);
+          // ring words from the wave's first shifted word (negative masses: the
+          // zeroed slots of chunks not yet filled; past the end: the copy of slot 0)
+          const uint32_t lo0 = ring[((x0 >> 5) & kRingMask) + lane], lo1 = ring[((x1 >> 5) & kRingMask) + lane];
+          const uint32_t nx0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo0, 0x130, 0xF, 0xF, false);  // wave_shl:1
+          const uint32_t nx1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo1, 0x130, 0xF, 0xF, false);
+          v |= __builtin_amdgcn_alignbit(nx0, lo0, (uint32_t)x0 & 31u);  // ({nx, lo} >> shift) low word
+          v |= __builtin_amdgcn_alignbit(nx1, lo1, (uint32_t)x1 & 31u);  // (r1 == r at an odd tail: same bits)
+        }
       } else {
-        v = ~0ull;
+        v = ~0u;
       }
-      cur[k] = v;
-      all_ones &= (v == ~0ull);
+      if (lane < 63 && o < kChunkWords) {
+        cur[o] = v;
+        if ((j & (kRing - 1)) == 0 && o < 64) ring[kRing * kChunkWords + o] = v;
+        all_ones &= (v == ~0u);
+      }
     }
     const bool chunk_full = __syncthreads_and(all_ones);
     if (threadIdx.x == 0) {

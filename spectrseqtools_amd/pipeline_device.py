@@ -147,9 +147,11 @@ def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=MATCHING_THRE
                                          active_next.data_ptr(), rounds.data_ptr(), queries.data_ptr(),
                                          n_active.data_ptr(), float(max_w), float(tolerance),
                                          float(dp_table.precision), err.data_ptr()), "sst_fix_round_device")
+        # re-filter only the spectra whose alphabet shrank: an unchanged alphabet is
+        # the table the rows already passed (round 1: classify's full table)
         eng.check(L.sst_valid_rows_alpha_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(),
                                                 rows.obs.data_ptr(), rows.rows.data_ptr(), alpha_next.data_ptr(),
-                                                active.data_ptr(), rows.alive.data_ptr(), float(tolerance),
+                                                active_next.data_ptr(), rows.alive.data_ptr(), float(tolerance),
                                                 float(dp_table.precision), err.data_ptr()),
                   "sst_valid_rows_alpha_device")
         eng.synchronize()
