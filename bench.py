@@ -209,11 +209,11 @@ def main():
     ap.add_argument("--dump-gathered", default=None,
                     help="test hook (tests/test_gpu_multirank.py): write the last step's gathered wire buffers "
                          "(rank 0) and every rank's inputs of that step into this directory")
-    ap.add_argument("--a8-source", default="rows", choices=("rows", "queries"),
-                    help="rows (default): each step starts from the peaks -- A7, the classification filters, the "
-                         "per-side SU order and the sliding window's pairs on the device (sst_step_rows_device); "
-                         "queries: the A8 (mass, threshold) pairs are produced on the host before timing "
-                         "(sst_step_device, round 2's line)")
+    ap.add_argument("--a8-source", default="queries", choices=("rows", "queries"),
+                    help="queries (default, the headline line): the A8 (mass, threshold) pairs are produced on "
+                         "the host before timing (sst_step_device); rows: each step starts from the peaks -- A7, "
+                         "the classification filters, the per-side SU order and the sliding window's pairs on "
+                         "the device (sst_step_rows_device, the second config-3 line)")
     ap.add_argument("--no-validate", action="store_true",
                     help="diagnostic builds only: skip the result checks after the timed region")
     ap.add_argument("--no-events", action="store_true",

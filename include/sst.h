@@ -419,7 +419,7 @@ int sst_classify_rows_device(sst_table* t, const double* d_obs, const int64_t* d
  * against d_alpha[2g..2g+1] (row masks of t; the caller keeps budgets from
  * binding, see sst_explain_pairs_alpha), the explanation dict's surviving
  * entries, d_alpha_next = the canonical rows | (alphabet & observed rows),
- * d_active_next[g] = the alphabet shrank (d_n_active counts those);
+ * d_active_next[g] = the alphabet shrank (*d_n_active, zeroed by the call, counts those);
  * d_rounds[g] += 1, d_queries[g] += the round's explain queries.  Settled
  * spectra carry their alphabet over. */
 int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,

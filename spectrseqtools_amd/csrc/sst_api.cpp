@@ -2015,6 +2015,7 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
   a.queries = d_queries;
   a.n_active = d_n_active;
   a.err = d_err;
+  if (n_spec > 0) HIP_OK(c, hipMemsetAsync(d_n_active, 0, sizeof(uint32_t), c->stream));  // this round's count
   Prof p(c, SST_K_EXPLAIN_MAIN);
   HIP_OK(c, launch_fix_round(t->args, a, c->n_cu, c->stream));
   return SST_OK;

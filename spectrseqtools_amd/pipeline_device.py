@@ -129,8 +129,8 @@ def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=MATCHING_THRE
     active_next = torch.empty_like(active)
     rounds = torch.zeros(S, dtype=torch.int32, device=dev)
     queries = torch.zeros(S, dtype=torch.int32, device=dev)
-    n_active = torch.zeros(1, dtype=torch.int32, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    ctl = torch.zeros(2, dtype=torch.int32, device=dev)  # [0] spectra whose alphabet shrank, [1] error bits
+    n_active, err = ctl[0:1], ctl[1:2]
     eng = dp_table.device_table.engine
     L = eng._lib
     h = dp_table.device_table.handle
@@ -138,9 +138,7 @@ def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=MATCHING_THRE
     n_rounds = 0
     max_w = _max_weight()
     torch.cuda.synchronize(dev)
-    while True:
-        n_active.zero_()
-        torch.cuda.synchronize(dev)
+    while True:  # per round: two launches, one synchronize, one 8-byte read
         eng.check(L.sst_fix_round_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(), rows.obs.data_ptr(),
                                          rows.meta.data_ptr(), rows.alive.data_ptr(), rows.rows.data_ptr(),
                                          alpha.data_ptr(), alpha_next.data_ptr(), active.data_ptr(),
@@ -159,10 +157,12 @@ def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=MATCHING_THRE
         if record:
             history.append((active.cpu().numpy().astype(bool), alpha_next.cpu().numpy().view(np.uint64).copy(),
                             rows.alive.cpu().numpy().astype(bool)))
-        _check_err(err)
+        n_act, e = (int(x) for x in ctl.cpu().tolist())
+        if e:
+            _check_err(err)
         alpha, alpha_next = alpha_next, alpha
         active, active_next = active_next, active
-        if int(n_active.item()) == 0:
+        if n_act == 0:
             break
     return DeviceFixpoint(alpha.cpu().numpy().view(np.uint64).copy(), rounds.cpu().numpy(),
                           queries.cpu().numpy(), history, n_rounds)
