@@ -342,11 +342,15 @@ def test_reuse_across_empty_pass_with_lookback(engine, dev, rows):
         if nn == 0:
             assert res.settle() == (0, 0)
             continue
+        # the reference: a result that never saw an empty pass.  Whether a pass
+        # keeps its pair-path part depends on the arena it finds (a pass that
+        # outgrows it re-runs unfused, reporting no pair-path part), so the
+        # comparison is of the decoded results, not of that split
         fresh = dev.explain_device(dm.data_ptr(), dt.data_ptr(), nn, TOL, PREC, 10)
         fresh.fetch_device()
         _, n_pair, pair_bytes, n_wg = res.pair_hits_device()
-        assert n_wg > 1 and (n_pair, pair_bytes) == fresh.pair_hits_device()[1:3]
-        assert res.settle() == fresh.settle()
+        assert n_wg > 1
+        assert res.settle()[0] == fresh.settle()[0]  # hits (the payload's pad bytes follow the layout)
         assert canonical_digest(res.status, res.count, res.offset, res.payload) == \
             canonical_digest(fresh.status, fresh.count, fresh.offset, fresh.payload)
         fixed = res.wire_pack(dv.data_ptr(), len(valid))
