@@ -156,7 +156,7 @@ struct sst_result {
   // the step from the peaks (sst_step_rows_device): its pass writes the dense
   // result in query order and produces its own queries (n from the header)
   bool rows_pass = false;
-  DevBuf rows_su, rows_ob, rows_side, rows_tot, rows_offs, rows_ctl, rows_big;
+  DevBuf rows_su, rows_ob, rows_side, rows_tot, rows_chunk, rows_ctl, rows_big;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
   std::vector<uint8_t> h_payload;
@@ -771,7 +771,7 @@ constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses pe
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->hits, &r->dense, &r->payload, &r->ctl, &r->lists, &r->wave_stats, &r->work,
                     &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->refs, &r->stage, &r->count,
-                    &r->offset, &r->rows_su, &r->rows_ob, &r->rows_side, &r->rows_tot, &r->rows_offs, &r->rows_ctl, &r->rows_big})
+                    &r->offset, &r->rows_su, &r->rows_ob, &r->rows_side, &r->rows_tot, &r->rows_chunk, &r->rows_ctl, &r->rows_big})
     b->release();
   if (r->hdr_host) (void)hipHostFree(r->hdr_host);
   r->hdr_host = nullptr;
@@ -1364,10 +1364,11 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
     return rc;
   };
   const size_t P = (size_t)n_peaks, S = (size_t)n_spec;
+  const size_t NC = (size_t)c->n_cu * 64;  // chunk capacity: >= the wave kernels' waves (launch_rows_step checks)
   const bool fresh = !r->rows_ctl.p;
   if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, (uint64_t)16 * r->cap_n + (1u << 20))) ||
       !r->rows_su.ensure(std::max<size_t>(1, 4 * P) * 8) || !r->rows_ob.ensure(std::max<size_t>(1, 4 * P) * 8) ||
-      !r->rows_side.ensure(2 * S * 4) || !r->rows_tot.ensure(3 * S * 4) || !r->rows_offs.ensure(3 * S * 8) ||
+      !r->rows_side.ensure(2 * S * 4) || !r->rows_tot.ensure(3 * S * 4) || !r->rows_chunk.ensure(2 * 3 * NC * 8) ||
       !r->rows_big.ensure(S * 4) || !r->rows_ctl.ensure(64))
     return bail(fail(c, SST_E_NOMEM, "device allocation failed (rows step)"));
   if (fresh) HIP_OK(c, hipMemsetAsync(r->rows_ctl.p, 0, 64, c->stream));
@@ -1408,7 +1409,9 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   a.rows_ob = (double*)r->rows_ob.p;
   a.side_rows = (uint32_t*)r->rows_side.p;
   a.totals = (uint32_t*)r->rows_tot.p;
-  a.offs = (uint64_t*)r->rows_offs.p;
+  a.chunk_tot = (unsigned long long*)r->rows_chunk.p;
+  a.chunk_off = (uint64_t*)r->rows_chunk.p + 3 * NC;
+  a.chunk_cap = (int64_t)NC;
   a.ctl = (uint64_t*)r->rows_ctl.p;
   a.err = (uint32_t*)((char*)r->rows_ctl.p + 32);
   a.done = (uint32_t*)((char*)r->rows_ctl.p + 40);

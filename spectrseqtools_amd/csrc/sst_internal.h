@@ -338,7 +338,10 @@ struct RowsArgs {
   double* rows_ob;
   uint32_t* side_rows;        // [2 n_spec]
   uint32_t* totals;           // [3 n_spec] queries, hits, payload bytes
-  uint64_t* offs;             // [3 n_spec]
+  unsigned long long* chunk_tot;  // [3 n_chunks] totals of each wave's contiguous chunk of spectra
+  uint64_t* chunk_off;        // [3 n_chunks] their exclusive offsets (k_rows_scan)
+  int64_t chunk, n_chunks;    // spectra per chunk, chunks (= waves of the wave kernels' grid; set at launch)
+  int64_t chunk_cap;          // chunk arrays' capacity (chunks)
   uint64_t* ctl;              // [4] totals
   uint32_t* err;
   uint32_t* done;

@@ -25,13 +25,16 @@
 //     (calculate_error_threshold, l1) -> a pair-class window answered from
 //     the LDS pair list (every difference is <= max_weight < 3 w_min).
 //
-// Three launches: k_rows_count (A7, rows to scratch, per-spectrum totals of
-// queries / hits / payload bytes), k_rows_scan (spectrum offsets), k_rows_emit
-// (statuses, dense hit list with pair-list refs, dense payload; the last
-// workgroup writes the header).  Both spectrum kernels are persistent (one
-// 1024-lane workgroup per CU, the 40 KB pair image staged once) and walk the
-// spectra grid-stride.  The result is sst_result's dense layout in query order
-// (spectrum-major; START pairs, then END pairs).
+// Launches: k_rows_count_w (one wave per contiguous chunk of spectra, each
+// spectrum of <= 160 peaks in turn; larger spectra are listed for
+// k_rows_count, one workgroup each): A7, rows to scratch, per-spectrum totals
+// of queries / hits / payload bytes and each chunk's sums; k_rows_scan: the
+// chunks' exclusive offsets (one workgroup over one value per wave);
+// k_rows_emit_w / k_rows_emit: each spectrum's offsets (its chunk's plus the
+// chunk's earlier spectra's totals), statuses, dense hit list with pair-list
+// refs, dense payload; the last workgroup writes the header.  The result is
+// sst_result's dense layout in query order (spectrum-major; START pairs, then
+// END pairs).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -314,15 +317,21 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_count(TableArgs t, RowsArgs a)
       a.totals[3 * g + 2] = s_acc[2];
       a.side_rows[2 * g] = nside[0];
       a.side_rows[2 * g + 1] = nside[1];
+      // into its chunk's totals (the wave kernel wrote the chunk's other spectra's)
+      unsigned long long* ct = a.chunk_tot + 3 * (g / a.chunk);
+      if (nq) atomicAdd(ct, (unsigned long long)nq);
+      if (s_acc[1]) atomicAdd(ct + 1, (unsigned long long)s_acc[1]);
+      if (s_acc[2]) atomicAdd(ct + 2, (unsigned long long)s_acc[2]);
     }
     __syncthreads();
   }
 }
 
-// exclusive offsets of every spectrum's queries, hits and payload bytes and
-// the totals (one workgroup; chunks of kScanChunk spectra staged through LDS
-// so that loads and stores are coalesced, each thread scanning a contiguous
-// run of kScanPer)
+// exclusive offsets of the wave kernels' chunks (each wave's contiguous run of
+// spectra; the workgroup kernels add the big spectra's totals to their chunk)
+// and the pass totals: one workgroup, each thread a contiguous run of kScanPer
+// chunks.  A spectrum's own offset is its chunk's plus the totals of the
+// chunk's earlier spectra (the emitting wave walks them in order).
 constexpr int kScanPer = 4;
 constexpr int kScanChunk = kScanPer * kRowsWG;
 
@@ -348,45 +357,23 @@ __device__ __forceinline__ uint64_t block_excl64(uint64_t v, uint64_t* s_w, uint
 }
 
 __global__ __launch_bounds__(kRowsWG) void k_rows_scan(RowsArgs a) {
-  extern __shared__ uint64_t s_buf[];  // [3 * kScanChunk]: the chunk's offsets (its totals staged as u32 first)
-  uint32_t* s_tot = (uint32_t*)s_buf;
   __shared__ uint64_t s_w[16];
+  const int64_t nb = a.n_chunks;
   uint64_t carry[3] = {0, 0, 0};
-  for (int64_t c0 = 0; c0 < a.n_spec; c0 += kScanChunk) {
-    const int m = (int)(a.n_spec - c0 < kScanChunk ? a.n_spec - c0 : kScanChunk);
-    {
-      uint32_t x[3 * kScanPer];  // every load in flight before the first LDS store
+  for (int64_t c0 = 0; c0 < nb; c0 += kScanChunk) {
+    const int64_t j0 = c0 + (int64_t)threadIdx.x * kScanPer;
+    uint64_t v[3 * kScanPer], run[3] = {0, 0, 0};
 #pragma unroll
-      for (int k = 0; k < 3 * kScanPer; ++k) {
-        const int i = threadIdx.x + k * kRowsWG;
-        x[k] = i < 3 * m ? a.totals[3 * c0 + i] : 0u;
-      }
+    for (int k = 0; k < 3 * kScanPer; ++k) v[k] = j0 + k / 3 < nb ? a.chunk_tot[3 * j0 + k] : 0ull;
 #pragma unroll
-      for (int k = 0; k < 3 * kScanPer; ++k) s_tot[threadIdx.x + k * kRowsWG] = x[k];
-    }
-    __syncthreads();
-    const int j0 = threadIdx.x * kScanPer;
-    uint32_t v[3 * kScanPer];
-    uint64_t run[3] = {0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < kScanPer; ++j)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        v[3 * j + c] = j0 + j < m ? s_tot[3 * (j0 + j) + c] : 0u;
-        run[c] += v[3 * j + c];
-      }
+    for (int k = 0; k < 3 * kScanPer; ++k) run[k % 3] += v[k];
     uint64_t base[3], tot[3];
-    for (int c = 0; c < 3; ++c) base[c] = carry[c] + block_excl64(run[c], s_w, tot[c]);  // (syncs: s_tot is free)
+    for (int c = 0; c < 3; ++c) base[c] = carry[c] + block_excl64(run[c], s_w, tot[c]);
 #pragma unroll
-    for (int j = 0; j < kScanPer; ++j)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        if (j0 + j < m) s_buf[3 * (j0 + j) + c] = base[c];
-        base[c] += v[3 * j + c];
-      }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 3 * m; i += blockDim.x) a.offs[3 * c0 + i] = s_buf[i];
-    __syncthreads();
+    for (int k = 0; k < 3 * kScanPer; ++k) {
+      if (j0 + k / 3 < nb) a.chunk_off[3 * j0 + k] = base[k % 3];
+      base[k % 3] += v[k];
+    }
     for (int c = 0; c < 3; ++c) carry[c] += tot[c];
   }
   if (threadIdx.x == 0) {
@@ -407,7 +394,17 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
   for (uint32_t i = blockIdx.x; i < n_big && room; i += gridDim.x) {
     const int64_t g = a.big[i];
     if (a.peak_off[g + 1] - a.peak_off[g] > kRowsMaxPeaks) continue;
-    uint64_t qb = a.offs[3 * g], hb = a.offs[3 * g + 1], bb = a.offs[3 * g + 2];
+    // its offsets: its chunk's plus the chunk's earlier spectra's totals
+    __shared__ unsigned long long s_off[3];
+    const int64_t ch = g / a.chunk;
+    if (threadIdx.x < 3) s_off[threadIdx.x] = a.chunk_off[3 * ch + threadIdx.x];
+    __syncthreads();
+    for (int64_t h = ch * a.chunk + threadIdx.x; h < g; h += blockDim.x)
+      for (int c = 0; c < 3; ++c)
+        if (a.totals[3 * h + c]) atomicAdd(&s_off[c], (unsigned long long)a.totals[3 * h + c]);
+    __syncthreads();
+    uint64_t qb = s_off[0], hb = s_off[1], bb = s_off[2];
+    __syncthreads();
     for (int sd = 0; sd < 2; ++sd) {
       const uint32_t n = a.side_rows[2 * g + sd];
       const double* rs = a.rows_su + 4 * a.peak_off[g] + (sd ? 2 * (a.peak_off[g + 1] - a.peak_off[g]) : 0);
@@ -696,8 +693,11 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
   WaveLds& L = Ls[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
   RPROF_T(w0);
-  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerWG;
-  for (int64_t g = (int64_t)blockIdx.x * kWavesPerWG + (threadIdx.x >> 6); g < a.n_spec; g += n_waves) {
+  // this wave's chunk: spectra [w * chunk, (w + 1) * chunk)
+  const int64_t w = (int64_t)blockIdx.x * kWavesPerWG + (threadIdx.x >> 6);
+  const int64_t g_end = (w + 1) * a.chunk < a.n_spec ? (w + 1) * a.chunk : a.n_spec;
+  uint64_t cq = 0, chh = 0, cb = 0;  // the chunk's totals (its big spectra: the workgroup kernel adds theirs)
+  for (int64_t g = w * a.chunk; g < g_end; ++g) {
     RPROF_T(c0);
     const int64_t p0 = a.peak_off[g];
     const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
@@ -755,10 +755,20 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
       a.side_rows[2 * g] = ok ? n0 : 0u;
       a.side_rows[2 * g + 1] = ok ? n1 : 0u;
     }
+    if (ok) {
+      cq += nq;
+      chh += th;
+      cb += tb;
+    }
     wsync();
     RPROF_T(c7);
     RPROF_ADD(4, c7 - c6);
     RPROF_ADD(5, 1);
+  }
+  if (lane == 0 && w < a.n_chunks) {
+    a.chunk_tot[3 * w] = cq;
+    a.chunk_tot[3 * w + 1] = chh;
+    a.chunk_tot[3 * w + 2] = cb;
   }
   RPROF_T(w1);
   RPROF_ADD(8, w1 - w0);
@@ -778,15 +788,26 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, R
   stage_img(t, dyn, img);
 #endif
   const bool room = !(*(volatile uint32_t*)a.err & 4u);
-  const int64_t n_waves = (int64_t)gridDim.x * kWavesPerWG;
-  for (int64_t g = (int64_t)blockIdx.x * kWavesPerWG + (threadIdx.x >> 6); g < a.n_spec && room; g += n_waves) {
+  const int64_t w = (int64_t)blockIdx.x * kWavesPerWG + (threadIdx.x >> 6);
+  const int64_t g_end = (w + 1) * a.chunk < a.n_spec ? (w + 1) * a.chunk : a.n_spec;
+  uint64_t off[3] = {0, 0, 0};
+  if (room && w < a.n_chunks) {
+    off[0] = a.chunk_off[3 * w];
+    off[1] = a.chunk_off[3 * w + 1];
+    off[2] = a.chunk_off[3 * w + 2];
+  }
+  for (int64_t g = w * a.chunk; g < g_end && room; ++g) {
     RPROF_T(e0);
     RPROF_T(e1);
     RPROF_ADD(6, e1 - e0);
     const int64_t p0 = a.peak_off[g];
     const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
-    if (P > (uint32_t)kWP) continue;
-    uint64_t qb = a.offs[3 * g], hb = a.offs[3 * g + 1], bb = a.offs[3 * g + 2];
+    uint64_t qb = off[0], hb = off[1], bb = off[2];
+    // the next spectrum's offsets (this one's totals: the count kernels')
+    off[0] += a.totals[3 * g];
+    off[1] += a.totals[3 * g + 1];
+    off[2] += a.totals[3 * g + 2];
+    if (P > (uint32_t)kWP) continue;  // the workgroup kernel's
     for (int sd = 0; sd < 2; ++sd) {
       const uint32_t n = a.side_rows[2 * g + sd];
       const double* rs = a.rows_su + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
@@ -879,7 +900,7 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
 #else
   const size_t wdyn = dyn;
 #endif
-  // 4-wave workgroups, as many as are resident (each wave takes spectra from a ticket)
+  // 4-wave workgroups, as many as are resident (each wave a contiguous chunk of spectra)
   static int occ = 0;
   static size_t occ_dyn = ~(size_t)0;
   if (occ_dyn != wdyn) {
@@ -891,11 +912,16 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
     occ_dyn = wdyn;
   }
   const int wave_wg = n_wg * (occ > 0 ? occ : 1);
-  hipLaunchKernelGGL(k_rows_count_w, dim3(wave_wg), dim3(64 * kWavesPerWG), 0, st, t, a);
-  hipLaunchKernelGGL(k_rows_count, dim3(n_wg), dim3(kRowsWG), dyn, st, t, a);
-  hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kRowsWG), 3 * kScanChunk * sizeof(uint64_t), st, a);
-  hipLaunchKernelGGL(k_rows_emit_w, dim3(wave_wg), dim3(64 * kWavesPerWG), wdyn, st, t, a);
-  hipLaunchKernelGGL(k_rows_emit, dim3(n_wg), dim3(kRowsWG), dyn, st, t, a);  // last: writes the header
+  // contiguous chunks of spectra, one per wave of the wave kernels' grid
+  RowsArgs b = a;
+  b.n_chunks = (int64_t)wave_wg * kWavesPerWG;
+  b.chunk = (a.n_spec + b.n_chunks - 1) / b.n_chunks;
+  if (b.n_chunks > a.chunk_cap) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rows_count_w, dim3(wave_wg), dim3(64 * kWavesPerWG), 0, st, t, b);
+  hipLaunchKernelGGL(k_rows_count, dim3(n_wg), dim3(kRowsWG), dyn, st, t, b);
+  hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kRowsWG), 0, st, b);
+  hipLaunchKernelGGL(k_rows_emit_w, dim3(wave_wg), dim3(64 * kWavesPerWG), wdyn, st, t, b);
+  hipLaunchKernelGGL(k_rows_emit, dim3(n_wg), dim3(kRowsWG), dyn, st, t, b);  // last: writes the header
   return hipGetLastError();
 }
 
