@@ -76,8 +76,9 @@ def workload_from(obs, offsets, seq_mass, dp, intensity=None, intensity_cutoff=0
     every sliding-window pair of each spectrum's START and END side after the
     is_valid, intensity / mass and sequence-mass filters (the first
     filter_by_explanation round without singletons), produced on the host by
-    the library's host-native sliding window (sst_su_diff_queries).  The
-    peaks of a spectrum must be sorted by mass."""
+    the library's host-native sliding window (sst_su_diff_queries).  Rows are
+    ordered per spectrum by SU mass, ties in breakage-major then peak order
+    (the reference's stable sort), whatever the peaks' order."""
     from spectrseqtools_amd._native import su_diff_queries
     from spectrseqtools_amd.masses import build_breakage_dict
     from spectrseqtools_amd.producers import MAX_VARIANCE, classify_queries, max_nucleotide_weight

@@ -196,8 +196,9 @@ int sst_explain_recursion_batch(sst_table* t, const double* mass, const double* 
  * per spectrum the kept rows of each side in SU order (a merge of the
  * breakages' sorted streams), the window pairs in closed form and each pair's
  * difference and threshold formed in the kernels.  Spectrum g's peaks are
- * d_obs[d_peak_off[g] .. d_peak_off[g+1]) in ascending mass order (at most
- * 1024); sides[k]: bit 0 = breakage k's rows are on the START side, bit 1 = on
+ * d_obs[d_peak_off[g] .. d_peak_off[g+1]) in any order (at most 1024; a list
+ * not in mass order is ranked on the device, equal masses in their given
+ * order); sides[k]: bit 0 = breakage k's rows are on the START side, bit 1 = on
  * the END side (both: the sequence-mass lower cut applies); d_intensity may
  * be NULL (every peak passes).  The result holds the explain answers in query
  * order (spectrum-major; START pairs then END pairs; the order

@@ -88,6 +88,7 @@ struct SpecLds {
   uint32_t qoff[kRowsMaxSide + 1];  // exclusive prefix of pairs per start row
   uint16_t kidx[4][kRowsMaxPeaks];  // peak of the j-th kept row of breakage k
   uint8_t keep[kRowsMaxPeaks];      // bit k: the row (k, p) is kept
+  uint16_t ord[kRowsMaxPeaks];      // peaks in (mass, position) order when they do not come sorted
   uint32_t kcnt[4];
   uint32_t w[16];
   int sstar;
@@ -210,12 +211,29 @@ __device__ bool load_spectrum(SpecLds& L, const TableArgs& t, const RowsArgs& a,
     L.keep[p] = kp;
   }
   __syncthreads();
-  // per breakage: kept rows in peak order (= SU order)
+  // peaks in mass order (ranked here when the list is not sorted; equal
+  // masses in their given order): each breakage's kept rows in SU order
+  bool ok = true;
+  for (uint32_t p = threadIdx.x; p + 1 < P; p += blockDim.x) ok &= L.obs[p] <= L.obs[p + 1];
+  const bool sorted = __syncthreads_and(ok);
+  if (!sorted) {
+    for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) {
+      const double o = L.obs[p];
+      uint32_t rank = 0;
+      for (uint32_t q = 0; q < P; ++q) {
+        const double v = L.obs[q];
+        rank += (v < o) | ((v == o) & (q < p));
+      }
+      L.ord[rank] = (uint16_t)p;
+    }
+    __syncthreads();
+  }
   for (int k = 0; k < a.n_shifts; ++k) {
     uint32_t carry = 0;
     for (uint32_t p0_ = 0; p0_ < P; p0_ += blockDim.x) {
-      const uint32_t p = p0_ + threadIdx.x;
-      const uint32_t f = p < P ? (L.keep[p] >> k) & 1u : 0u;
+      const uint32_t i = p0_ + threadIdx.x;
+      const uint32_t p = i < P ? (sorted ? i : L.ord[i]) : 0u;
+      const uint32_t f = i < P ? (L.keep[p] >> k) & 1u : 0u;
       uint32_t tot;
       const uint32_t ex = block_excl(f, L.w, tot);
       if (f) L.kidx[k][carry + ex] = (uint16_t)p;
@@ -502,6 +520,7 @@ struct WaveLds {
   uint16_t qoff[kWS + 1];  // a side has < 2^16 pairs (kWS (kWS - 1) / 2)
   uint16_t kidx[4][kWP];
   uint8_t keep[kWP];
+  uint8_t ord[kWP];  // peaks in (mass, position) order when they do not come sorted
   uint32_t kcnt[4];
   uint32_t sstar;
 };
@@ -556,11 +575,30 @@ __device__ void wave_load(WaveLds& L, const TableArgs& t, const RowsArgs& a, int
     }
     L.keep[p] = kp;
   }
+  wsync();
+  // a peak list need not be sorted: rank the peaks by mass (equal masses in
+  // their given order) so that each breakage's rows come in SU order
+  bool sorted = true;
+  for (uint32_t p = lane; p + 1 < P; p += 64) sorted &= L.obs[p] <= L.obs[p + 1];
+  sorted = __ballot(!sorted) == 0;
+  if (!sorted) {
+    for (uint32_t p = lane; p < P; p += 64) {
+      const double o = L.obs[p];
+      uint32_t rank = 0;
+      for (uint32_t q = 0; q < P; ++q) {
+        const double v = L.obs[q];
+        rank += (v < o) | ((v == o) & (q < p));
+      }
+      L.ord[rank] = (uint8_t)p;
+    }
+    wsync();
+  }
   for (int k = 0; k < a.n_shifts; ++k) {
     uint32_t carry = 0;
     for (uint32_t q0 = 0; q0 < P; q0 += 64) {
-      const uint32_t p = q0 + lane;
-      const bool f = p < P && ((L.keep[p] >> k) & 1u);
+      const uint32_t i = q0 + lane;
+      const uint32_t p = i < P ? (sorted ? i : L.ord[i]) : 0u;
+      const bool f = i < P && ((L.keep[p] >> k) & 1u);
       const uint64_t bal = __ballot(f);
       if (f) L.kidx[k][carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = (uint16_t)p;

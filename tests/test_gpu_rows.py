@@ -6,8 +6,8 @@ CPU suite pins to the reference) and the CPU oracle: A7 codes, the query
 count, every answer (canonical digest against the explain pass over the
 host-built queries), statuses and exact candidate lists of a sample against
 the oracle; edge spectra (no peaks, one peak, duplicate peaks, heavy peaks,
-spectra over 160 peaks, intensities below the cutoff, a mass cutoff that
-drops peaks)."""
+spectra over 160 peaks, peaks not in mass order, intensities below the
+cutoff, a mass cutoff that drops peaks)."""
 import os
 import sys
 
@@ -121,6 +121,8 @@ def test_rows_step_edge_spectra(dp):
         elif s % 10 == 4:  # over 160 peaks: the workgroup-per-spectrum kernels
             o = np.concatenate([o] + [b.observed[b.offsets[t]:b.offsets[t + 1]] for t in (s + 1, s + 2)])
         o = np.sort(o)
+        if s % 10 == 5:
+            o = np.concatenate([o, o[:3]])[rng.permutation(len(o) + 3)]  # unsorted, with ties: ranked on the device
         obs.append(o)
         offs.append(offs[-1] + len(o))
         seqm.append(b.seq_mass[s])
