@@ -102,17 +102,30 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   const int64_t q1 = a.counts ? q0 + a.counts[g] : a.offsets[g + 1];
   if (q0 >= q1) return;
   const uint64_t m0 = a.masks[2 * g], m1 = a.masks[2 * g + 1];
+  // with every canonical row kept the closure starts from theirs (shared, in
+  // L2) and only the other rows are added per spectrum
+  __shared__ int s_wmax_all, s_use_c;
   if (threadIdx.x == 0) {
-    int n = 0;
+    int n = 0, wmax_all = 0;
     for (int r = 1; r < a.n_rows; ++r)
-      if (row_in(m0, m1, r)) s_w[n++] = a.w[r];
+      if (row_in(m0, m1, r)) wmax_all = a.w[r] > wmax_all ? a.w[r] : wmax_all;
+    // the reduced table ends below ceil((35 w_max + 1) / 32) * 32: the shared
+    // closure must cover it
+    const int64_t lim = ((int64_t)wmax_all * 35 + 32) / 32 * 32;
+    const int uc = a.canon_closure && (m0 & a.canon0) == a.canon0 && (m1 & a.canon1) == a.canon1 &&
+                   lim <= 32 * a.canon_words;
+    for (int r = 1; r < a.n_rows; ++r)
+      if (row_in(m0, m1, r) && !(uc && row_in(a.canon0, a.canon1, r))) s_w[n++] = a.w[r];
     s_n = n;
+    s_wmax_all = wmax_all;
+    s_use_c = uc;
     s_done = q0;
     s_full = 0;
   }
   __syncthreads();
+  const bool use_c = s_use_c;
   const int n_w = s_n;
-  if (n_w == 0) {  // sentinel only: nothing >= 1 is reachable
+  if (n_w == 0 && !use_c) {  // sentinel only: nothing >= 1 is reachable
     for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) alpha_put(a, i, 0);
     return;
   }
@@ -121,14 +134,15 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   // the row masses, lane r of every wave holding rows r and r + 64
   const int w_lo = (int)(threadIdx.x & 63) < n_w ? s_w[threadIdx.x & 63] : 0;
   const int w_hi = (int)(threadIdx.x & 63) + 64 < n_w ? s_w[(threadIdx.x & 63) + 64] : 0;
-  int wmax = 0, wmin = INT32_MAX;
+  int wmax = 0, wmin = INT32_MAX;  // of the rows added per spectrum (the ring's dependency window)
   for (int k = 0; k < n_w; ++k) {
     wmax = s_w[k] > wmax ? s_w[k] : wmax;
     wmin = s_w[k] < wmin ? s_w[k] : wmin;
   }
+  if (n_w == 0) wmin = wmax = kChunkBits;  // the canonical closure alone
   // the reduced table (set_up_bit_table with max_mass = max(kept) * 35):
   // masses < limit exist, the last-column mask leaves masses <= vtop reachable
-  const int64_t max_mass = (int64_t)wmax * 35;
+  const int64_t max_mass = (int64_t)s_wmax_all * 35;
   const int64_t n_cols = (max_mass + 1 + 31) / 32;
   const int64_t limit = n_cols * 32;
   const int64_t vtop = ((max_mass + 1) % 32 == 0) ? (n_cols - 1) * 32 - 1 : max_mass;
@@ -160,7 +174,12 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
       const int o = o0 + lane;
       uint32_t v = 0;
       if (!s_full) {
-        if (j == 0 && o == 0) v = 1u;  // mass 0: the empty multiset (table[0, 0] seed)
+        if (use_c) {  // includes mass 0; masses past the full table (>= every reduced table's end): none
+          const int64_t cw = j * kChunkWords + o;
+          v = o < kChunkWords && cw < a.canon_words ? a.canon_closure[cw] : 0u;
+        } else if (j == 0 && o == 0) {
+          v = 1u;  // mass 0: the empty multiset (table[0, 0] seed)
+        }
         // the wave's first output mass (masses < limit < 2^31), wave-uniform: the
         // shifts and ring offsets below are scalar arithmetic
         const int m0 = (int)base + 32 * __builtin_amdgcn_readfirstlane(o0);

@@ -91,7 +91,8 @@ struct sst_table {
   std::vector<int64_t> masses;
   std::vector<uint8_t> is_mod;
   std::vector<int64_t> cap;
-  DevBuf packed, index, valid, w, capd, modd, pairs, census;
+  DevBuf packed, index, valid, w, capd, modd, pairs, census, canon_c;
+  int64_t canon_c_words = 0;  // the canonical rows' closure (k_valid_alpha), built at first use
   std::vector<uint32_t> pair_recs;  // the pair list's payload records (host copy)
   uint64_t pair_key = 0;            // their FNV-1a (sst_wire_pack), computed on first use
   bool pair_key_set = false;
@@ -675,7 +676,7 @@ void sst_table_destroy(sst_table* t) {
   std::lock_guard<std::recursive_mutex> g(c->mu);
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&t->packed, &t->index, &t->valid, &t->w, &t->capd, &t->modd, &t->pairs, &t->census})
+  for (DevBuf* b : {&t->packed, &t->index, &t->valid, &t->w, &t->capd, &t->modd, &t->pairs, &t->census, &t->canon_c})
     b->release();
   delete t;
 }
@@ -1837,6 +1838,47 @@ static int check_masks(sst_table* t) {
   return SST_OK;
 }
 
+// k_valid_alpha's shared start: the closure of the canonical rows over the
+// table's masses [0, M), as u32 words (bit m: m is a sum of canonical rows).
+// Host-built once per table (every row mass is >= 64, so word i depends only
+// on earlier words).
+static int canon_closure(sst_table* t, AlphaArgs& a) {
+  sst_ctx* c = t->ctx;
+  a.canon0 = a.canon1 = 0;
+  std::vector<int64_t> cw;
+  for (int r = 1; r < t->n_rows; ++r)
+    if (!t->is_mod[r]) {
+      (r < 64 ? a.canon0 : a.canon1) |= 1ull << (r & 63);
+      cw.push_back(t->masses[r]);
+    }
+  a.canon_closure = nullptr;
+  a.canon_words = 0;
+  for (int64_t w : cw)
+    if (w < 64) return SST_OK;  // not word-separable: every spectrum runs its whole closure
+  if (!t->canon_c_words) {
+    const int64_t nw = (t->M + 31) / 32;
+    std::vector<uint32_t> bits((size_t)nw, 0u);
+    auto get = [&](int64_t m) -> uint32_t {  // 32 bits from mass m on (m may be negative: zeros)
+      if (m <= -32) return 0u;
+      const int64_t wi = m >= 0 ? m / 32 : -1 - (-m - 1) / 32;
+      const int s = (int)(m - wi * 32);
+      const uint64_t lo = wi >= 0 ? bits[(size_t)wi] : 0u, hi = wi + 1 >= 0 && wi + 1 < nw ? bits[(size_t)wi + 1] : 0u;
+      return (uint32_t)(((hi << 32) | lo) >> s);
+    };
+    for (int64_t i = 0; i < nw; ++i) {
+      uint32_t v = i == 0 ? 1u : 0u;
+      for (int64_t w : cw) v |= get(32 * i - w);
+      bits[(size_t)i] = v;
+    }
+    if (!t->canon_c.ensure((size_t)nw * 4)) return fail(c, SST_E_NOMEM, "device allocation failed (canonical closure)");
+    HIP_OK(c, hipMemcpy(t->canon_c.p, bits.data(), (size_t)nw * 4, hipMemcpyHostToDevice));
+    t->canon_c_words = nw;
+  }
+  a.canon_closure = (const uint32_t*)t->canon_c.p;
+  a.canon_words = t->canon_c_words;
+  return SST_OK;
+}
+
 int sst_explain_pairs_alpha_device(sst_table* t, const double* d_mass, const double* d_thr, const int32_t* d_spec,
                                    const uint64_t* d_masks, int64_t n, double tol, double prec, int8_t* d_status,
                                    uint32_t* d_count, uint64_t* d_rowmask, uint32_t* d_range) {
@@ -1916,6 +1958,7 @@ int sst_is_valid_alpha_device(sst_table* t, const double* d_mass, const double* 
   a.prec = prec;
   a.rprec = 1.0 / prec;
   a.out = d_out;
+  if (int rc = canon_closure(t, a)) return rc;
   HIP_OK(c, launch_valid_alpha(a, n_spec, c->stream));
   return SST_OK;
 }
@@ -2109,6 +2152,7 @@ int sst_valid_rows_alpha_device(sst_table* t, const int64_t* d_peak_off, int64_t
   a.tol = tol;
   a.prec = prec;
   a.rprec = 1.0 / prec;
+  if (int rc = canon_closure(t, a)) return rc;
   Prof p(c, SST_K_IS_VALID);
   HIP_OK(c, launch_valid_alpha(a, n_spec, c->stream));
   return SST_OK;

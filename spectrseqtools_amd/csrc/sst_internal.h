@@ -302,6 +302,13 @@ struct AlphaArgs {  // k_valid_alpha: is_valid_mass on the reduced tables
   int n_rows;
   double tol, prec, rprec;
   int8_t* out;
+  // the closure of the table's canonical rows (every alphabet the reduction
+  // produces keeps them): bit m of u32 word m / 32 set iff m is a sum of
+  // canonical rows, for m < 32 canon_words; a spectrum whose mask holds every
+  // canonical row starts its closure from it and adds only its other rows
+  const uint32_t* canon_closure;  // may be null
+  int64_t canon_words;
+  uint64_t canon0, canon1;  // the canonical rows' mask
 };
 struct PairAlphaArgs {  // k_pairs_alpha: explain on pair-class windows
   const double* mass;
