@@ -520,70 +520,6 @@ struct GlobStack {
   __device__ __forceinline__ int top(int d) const { return at(d).top; }
 };
 
-// The deep roles' stacks: a lane's first kLdsDepth frames in LDS (structure of
-// arrays, lane-minor: conflict-free), deeper ones in its interleaved global
-// slice.  Every DFS step reads and writes the current frame, so the shallow
-// levels -- all of them for windows of <= kLdsDepth items -- cost an LDS round
-// trip instead of an L2 one.
-constexpr int kLdsDepth = 8;
-struct DeepLds {
-  uint64_t a[kLdsDepth][kDefWG], b[kLdsDepth][kDefWG];
-  uint32_t m[kLdsDepth][kDefWG];
-  int A[kLdsDepth][kDefWG], B[kLdsDepth][kDefWG];
-  uint8_t r[kLdsDepth][kDefWG], top[kLdsDepth][kDefWG];
-};
-struct HybStack {
-  DeepLds* L;
-  int t;              // this lane's column (threadIdx.x)
-  GlobFrame* f;       // this lane's global frame 0 (levels >= kLdsDepth used)
-  uint32_t stride;    // lanes of the role
-  static constexpr int depth = kMaxDepth;
-  __device__ __forceinline__ GlobFrame& at(int d) const { return f[(size_t)d * stride]; }
-  __device__ __forceinline__ uint32_t m(int d) const { return d < kLdsDepth ? L->m[d][t] : at(d).m; }
-  __device__ __forceinline__ M128 mask(int d) const {
-    return d < kLdsDepth ? M128{L->a[d][t], L->b[d][t]} : M128{at(d).a, at(d).b};
-  }
-  __device__ __forceinline__ uint8_t row(int d) const { return d < kLdsDepth ? L->r[d][t] : at(d).r; }
-  __device__ __forceinline__ void set(int d, uint32_t m, M128 k) {
-    if (d < kLdsDepth) {
-      L->m[d][t] = m;
-      L->a[d][t] = k.a;
-      L->b[d][t] = k.b;
-    } else {
-      at(d).m = m;
-      at(d).a = k.a;
-      at(d).b = k.b;
-    }
-  }
-  __device__ __forceinline__ void set_mask(int d, M128 k) {
-    if (d < kLdsDepth) {
-      L->a[d][t] = k.a;
-      L->b[d][t] = k.b;
-    } else {
-      at(d).a = k.a;
-      at(d).b = k.b;
-    }
-  }
-  __device__ __forceinline__ void set_row(int d, int r) {
-    if (d < kLdsDepth) L->r[d][t] = (uint8_t)r;
-    else at(d).r = (uint8_t)r;
-  }
-  __device__ __forceinline__ void set_budget(int d, int A, int B, int top) {
-    if (d < kLdsDepth) {
-      L->A[d][t] = A;
-      L->B[d][t] = B;
-      L->top[d][t] = (uint8_t)top;
-    } else {
-      at(d).A = A;
-      at(d).B = B;
-      at(d).top = (uint8_t)top;
-    }
-  }
-  __device__ __forceinline__ int A(int d) const { return d < kLdsDepth ? L->A[d][t] : at(d).A; }
-  __device__ __forceinline__ int B(int d) const { return d < kLdsDepth ? L->B[d][t] : at(d).B; }
-  __device__ __forceinline__ int top(int d) const { return d < kLdsDepth ? (int)L->top[d][t] : (int)at(d).top; }
-};
-
 // ---------------------------------------------------------------------------
 // exact path: per-lane open-addressing hash, one 32-B entry per visited mass
 // ---------------------------------------------------------------------------
@@ -2294,13 +2230,13 @@ __global__ __launch_bounds__(256) void k_wire_pack(WireArgs a) {
 // query, stack in a per-lane slice of the workspace.
 template <int MODE>
 __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs& out, int cls, GlobFrame* ws, Lds& s,
-                          DeepLds& dl, int blk, int nblk) {
+                          int blk, int nblk) {
   const uint32_t n_list = out.counters[cls];
   if (n_list == 0) return;  // block-uniform: nothing queued for this role
   stage_rows(s, t);
   const int64_t gid = (int64_t)blk * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)nblk * blockDim.x;
-  HybStack st{&dl, (int)threadIdx.x, ws + gid, (uint32_t)nthreads};
+  GlobStack st{ws + gid, (uint32_t)nthreads};
   uint64_t st_n = 0, st_nodes = 0;
   // workgroup-uniform trip count: the payload allocation and the hit records
   // take one atomic per workgroup (wg_alloc), not one per wave or query
@@ -2445,7 +2381,6 @@ __global__ __launch_bounds__(kDefWG) void k_explain_deferred(TableArgs t, QueryA
                                                              ExactWs ws, int shallow_blocks, int deep_blocks,
                                                              int exact_lanes) {
   __shared__ Lds s;
-  __shared__ DeepLds dl;
   int b = blockIdx.x;
   if (b < shallow_blocks) {
     if (!(out.dbg & 1)) shallow_list_body(t, q, out, s, b, shallow_blocks);  // DIAGNOSTIC 1: no SHALLOW role
@@ -2454,9 +2389,9 @@ __global__ __launch_bounds__(kDefWG) void k_explain_deferred(TableArgs t, QueryA
   b -= shallow_blocks;
   if (out.dbg & 2) return;  // DIAGNOSTIC 2: no deep / exact roles
   if (b < deep_blocks)
-    deep_body<MODE_FAST>(t, q, out, kClassDeep, ws_deep, s, dl, b, deep_blocks);
+    deep_body<MODE_FAST>(t, q, out, kClassDeep, ws_deep, s, b, deep_blocks);
   else if (b < 2 * deep_blocks)  // second half of the deep workspace
-    deep_body<MODE_NOMEMO>(t, q, out, kClassNomemo, ws_deep + (size_t)deep_blocks * kDefWG * kMaxDepth, s, dl,
+    deep_body<MODE_NOMEMO>(t, q, out, kClassNomemo, ws_deep + (size_t)deep_blocks * kDefWG * kMaxDepth, s,
                            b - deep_blocks, deep_blocks);
   else
     exact_body(t, q, out, ws, s, b - 2 * deep_blocks, exact_lanes);
