@@ -163,6 +163,26 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
                              double tolerance, double precision, const int64_t* d_max_mods, int64_t max_mods_scalar,
                              int with_memo, uint64_t cap_per_query, sst_result** out);
 
+/* sst_explain_batch_device against per-query reduced alphabets without
+ * rebuilding a table: query i is answered as explain_mass_with_table on the
+ * table DynamicProgrammingTable._reduce_nucleotide_list (mass_table.py:
+ * 94-121) would rebuild for the rows of alphabet d_spec[i] (d_spec null: all
+ * queries alphabet 0), given as a row mask over this table's rows:
+ * d_alpha[2 g] rows 0..63, d_alpha[2 g + 1] rows 64..127 (row 0, the
+ * sentinel, is implied).  The kept rows keep their caps (sst_table_set_budgets
+ * of this table).  Every window with values goes to the deferred DFS roles,
+ * which walk the alphabet's rows only (the pair scan answers none); a window
+ * reaching the reduced table's extent max(kept) * 35 is SST_OUT_OF_TABLE as in
+ * the reference, one inside that table's last packed word SST_ABORTED (the
+ * reference's last-column mask is not modelled).  Replaces a table rebuild +
+ * explain_mass_with_table per alphabet (prediction.py:207 -> :216-227,
+ * skeleton_building.py:212 -> :436).  Results, reuse and settling as for
+ * sst_explain_batch_device; d_spec / d_alpha must stay valid until settled. */
+int sst_explain_alpha_batch_device(sst_table* t, const double* d_mass, const double* d_thr, const int32_t* d_spec,
+                                   const uint64_t* d_alpha, int64_t n, double tolerance, double precision,
+                                   const int64_t* d_max_mods, int64_t max_mods_scalar, int with_memo,
+                                   uint64_t cap_per_query, sst_result** out);
+
 /* One step of both predicates on device buffers, as classify_fragments and
  * the explanation stage issue them: sst_is_valid_peaks_device(d_obs, n_peaks,
  * shifts, n_shifts -> d_valid_out) and sst_explain_batch_device(d_mass, ...,
@@ -441,14 +461,20 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
  * emit into d_status / d_count [total], spectrum-major (START side, then END;
  * bins in order; a bin's pairs predecessor-row-major).  Statuses SST_NONE /
  * EMPTY / SOME, or -10 for a window outside the pair class (hi >= 3 w_min:
- * the caller's general path).  d_err bit 2: a spectrum over 2048 rows. */
+ * the caller's general path).  With d_n_def non-null (zeroed by the caller),
+ * those windows are also listed, in any order, for
+ * sst_explain_alpha_batch_device: d_def_mass / d_def_thr / d_def_spec /
+ * d_def_q[*d_n_def] = window mass, threshold, spectrum and index into
+ * d_status (capacity: the total).  d_err bit 2: a spectrum over 2048 rows. */
 int sst_bins_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                           const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
                           const uint32_t* d_rows, double tol, uint32_t* d_n_q, uint64_t* d_q_off, uint32_t* d_err);
 int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                          const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
                          const uint32_t* d_rows, const uint64_t* d_alpha, double tol, double prec,
-                         const uint64_t* d_q_off, int8_t* d_status, uint32_t* d_count, uint32_t* d_err);
+                         const uint64_t* d_q_off, int8_t* d_status, uint32_t* d_count, double* d_def_mass,
+                         double* d_def_thr, int32_t* d_def_spec, uint64_t* d_def_q, uint32_t* d_n_def,
+                         uint32_t* d_err);
 
 /* _reduce_alphabet's filter (prediction.py:211-227): is_valid_mass of the
  * alive rows of the d_active spectra against their reduced tables (d_alpha),

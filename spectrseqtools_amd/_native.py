@@ -23,7 +23,7 @@ EXPORTS = (
     "sst_device_count", "sst_ctx_create", "sst_ctx_destroy", "sst_last_error", "sst_ctx_stream",
     "sst_ctx_synchronize", "sst_table_build", "sst_table_upload", "sst_table_set_budgets", "sst_table_shape",
     "sst_table_download", "sst_table_destroy", "sst_is_valid_batch", "sst_is_valid_batch_device",
-    "sst_explain_batch", "sst_explain_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
+    "sst_explain_batch", "sst_explain_batch_device", "sst_explain_alpha_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
     "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
@@ -103,6 +103,7 @@ def load_library(path=LIB_PATH):
     lib.sst_is_valid_batch_device.argtypes = [_P, _P, _P, _I64, _D, _D, _P]
     lib.sst_explain_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
     lib.sst_explain_batch_device.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
+    lib.sst_explain_alpha_batch_device.argtypes = [_P, _P, _P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
     lib.sst_result_host.argtypes = [_P, _PP, _PP, _PP, _PP, ctypes.POINTER(_U64)]
     lib.sst_result_device.argtypes = [_P, _PP, _PP, _PP, _PP, ctypes.POINTER(_U64)]
     lib.sst_result_hit_list.argtypes = [_P, _PP, ctypes.POINTER(_U64)]
@@ -161,7 +162,8 @@ def load_library(path=LIB_PATH):
     lib.sst_valid_rows_alpha_device.restype = _I
     lib.sst_bins_count_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _D, _P, _P, _P]
     lib.sst_bins_count_device.restype = _I
-    lib.sst_bins_emit_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _P, _P, _P, _P]
+    lib.sst_bins_emit_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _P, _P, _P, _P, _P, _P, _P,
+                                         _P, _P]
     lib.sst_bins_emit_device.restype = _I
     return lib
 
@@ -659,6 +661,41 @@ class DeviceTable:
             reuse.n = n
             return reuse
         return ExplainResult(self.engine, h, n)
+
+    def explain_alpha_device(self, d_mass, d_thr, d_spec, d_alpha, n, tolerance, precision, max_mods_scalar,
+                             d_mods=None, with_memo=True, cap=2 ** 32, reuse=None):
+        """sst_explain_alpha_batch_device: explain_device with query i answered
+        on the reduced alphabet d_alpha[d_spec[i]] (u64 row-mask pairs over this
+        table's rows), as the rebuilt reduced table would answer it."""
+        h = ctypes.c_void_p(reuse.handle.value if reuse is not None else None)
+        self.engine.check(self.engine._lib.sst_explain_alpha_batch_device(
+            self.handle, d_mass, d_thr, d_spec, d_alpha, int(n), float(tolerance), float(precision), d_mods,
+            int(max_mods_scalar), int(bool(with_memo)), int(cap), ctypes.byref(h)), "sst_explain_alpha_batch_device")
+        if reuse is not None:
+            reuse.n = n
+            return reuse
+        return ExplainResult(self.engine, h, n)
+
+    def explain_alpha(self, masses, thresholds, spec, alpha, tolerance, precision, max_mods, with_memo=True,
+                      cap=2 ** 32):
+        """Host-buffer form of explain_alpha_device (tests, small batches):
+        uploads the inputs, settles and fetches the result."""
+        import torch
+
+        dev = torch.device("cuda", self.engine.device)
+        n = len(masses)
+        dm = torch.as_tensor(np.ascontiguousarray(masses, dtype=np.float64), device=dev)
+        dt = torch.as_tensor(np.ascontiguousarray(thresholds, dtype=np.float64), device=dev)
+        ds = torch.as_tensor(np.ascontiguousarray(spec, dtype=np.int32), device=dev)
+        da = torch.as_tensor(np.ascontiguousarray(alpha, dtype=np.uint64).view(np.int64), device=dev)
+        mods = np.broadcast_to(np.asarray(max_mods, dtype=np.int64), (n,))
+        dmods = torch.as_tensor(np.ascontiguousarray(mods), device=dev)
+        torch.cuda.synchronize(dev)
+        res = self.explain_alpha_device(dm.data_ptr(), dt.data_ptr(), ds.data_ptr(), da.data_ptr(), n, tolerance,
+                                        precision, 0, d_mods=dmods.data_ptr(), with_memo=with_memo, cap=cap)
+        res.fetch_device()
+        del dm, dt, ds, da, dmods
+        return res
 
     def step_rows_device(self, d_obs, d_peak_off, n_spec, n_peaks, d_su_seq, shifts, sides, d_valid_out, max_weight,
                          tolerance, precision, max_mods_scalar, max_queries, d_intensity=None, intensity_cutoff=0.5e6,

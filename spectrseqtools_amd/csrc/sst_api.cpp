@@ -139,6 +139,8 @@ struct sst_result {
     double tol, prec;
     int with_memo;
     uint64_t cap;
+    const uint64_t* alpha;  // per-query alphabets (sst_explain_alpha_batch_device) or null
+    const int32_t* spec;
   } pass{};
   uint64_t arena_bytes = 0;
   uint64_t n_hits = 0, payload_bytes = 0;
@@ -884,6 +886,9 @@ int launch_tail(sst_table* t, sst_result* r) {
   QueryArgs q{ps.mass, ps.thr, ps.mods, ps.mods_scalar, r->n, ps.tol, ps.prec, 1.0 / ps.prec, ps.with_memo, ps.cap,
               kNodeBudget};
   fold_scan_limits(t->args, q);
+  q.alpha = ps.alpha;
+  q.spec = ps.spec;
+  q.comp = (int)t->C;
   OutArgs o = out_args(r);
 #ifdef SST_DIAG  // diagnostic builds only (make DIAG=1): roles switched off, results invalid
   {
@@ -959,9 +964,9 @@ struct PeaksJob {
 
 int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double* d_thr, const int64_t* d_mods,
                  int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count, bool eager_tail,
-                 const PeaksJob* peaks = nullptr) {
+                 const PeaksJob* peaks = nullptr, const uint64_t* d_alpha = nullptr, const int32_t* d_spec = nullptr) {
   sst_ctx* c = t->ctx;
-  r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count};
+  r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count, d_alpha, d_spec};
   r->pass_stream = c->stream;
   r->settle_ev_pending = false;
   r->rows_pass = false;
@@ -1009,8 +1014,16 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
     }
     if (int rc = ensure_exact_ws(c, cap0, kExactLanes0)) return rc;
   }
+  // per-query alphabets: the scan answers no window itself (its pair list and
+  // SHALLOW role know the full alphabet only) and routes every window with
+  // values to the deferred roles, which walk the alphabet's rows only
+  TableArgs ta = t->args;
+  if (d_alpha) ta.pair_lim = 0, ta.shallow_hi = 0;
   QueryArgs q{d_mass, d_thr, d_mods, mods_scalar, n, tol, prec, 1.0 / prec, with_memo, cap_count, kNodeBudget};
-  fold_scan_limits(t->args, q);
+  fold_scan_limits(ta, q);
+  q.alpha = d_alpha;
+  q.spec = d_spec;
+  q.comp = (int)t->C;
   OutArgs o = out_args(r);
   // the pair scan packs its own result (and writes the header) when no
   // deferred-class launch follows it in this pass
@@ -1039,12 +1052,12 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
       HIP_OK(c, launch_step(t->args, q, o, r->n_wg, peaks->obs, peaks->n, peaks->shifts, tol, prec, peaks->out,
                             c->stream));
     else
-      HIP_OK(c, launch_explain_scan(t->args, q, o, r->n_wg, c->stream));
+      HIP_OK(c, launch_explain_scan(ta, q, o, r->n_wg, c->stream));
   }
   if (fused) return SST_OK;
   if (r->bitset_scan) {  // the expand kernel routes the windows the bitset scan queued
     Prof p(c, SST_K_EXPLAIN_EXPAND);
-    HIP_OK(c, launch_explain_expand(t->args, q, o, r->n_expand_waves / (kWG / 64), c->stream));
+    HIP_OK(c, launch_explain_expand(ta, q, o, r->n_expand_waves / (kWG / 64), c->stream));
     eager_tail = true;
   }
   if (eager_tail)
@@ -1192,7 +1205,8 @@ int settle(sst_result* r) {
     HIP_OK(c, hipStreamSynchronize(c->stream));  // the pack may still run: buffers are about to be replaced
     if (int rc = grow_for_retry(r, regions, spill, exact, h[kHdrCursor], h[kHdrRegionNeed])) return rc;
     const auto& p = r->pass;
-    if (int rc = explain_pass(p.t, r, p.mass, p.thr, p.mods, p.mods_scalar, p.tol, p.prec, p.with_memo, p.cap, true))
+    if (int rc = explain_pass(p.t, r, p.mass, p.thr, p.mods, p.mods_scalar, p.tol, p.prec, p.with_memo, p.cap, true,
+                              nullptr, p.alpha, p.spec))
       return rc;
     launched = true;
   }
@@ -1295,6 +1309,35 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
   return SST_OK;
 }
 
+int sst_explain_alpha_batch_device(sst_table* t, const double* d_mass, const double* d_thr, const int32_t* d_spec,
+                                   const uint64_t* d_alpha, int64_t n, double tol, double prec,
+                                   const int64_t* d_mods, int64_t mods_scalar, int with_memo, uint64_t cap_count,
+                                   sst_result** out) {
+  if (!t || !out || n < 0 || n > SST_MAX_EXPLAIN_BATCH || (n > 0 && (!d_mass || !d_alpha))) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  sst_result* r = *out;
+  const bool reuse = r != nullptr;
+  if (reuse) {
+    if (r->ctx != c || n > r->cap_n) return fail(c, SST_E_ARG, "result reuse: other ctx or capacity < n");
+    r->n = n;
+  } else if (int rc = alloc_result(t, n, &r)) {
+    return rc;
+  }
+  int rc = explain_pass(t, r, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count, false, nullptr,
+                        d_alpha, d_spec);
+  if (rc) {
+    if (!reuse) {
+      free_result_bufs(r);
+      delete r;
+    }
+    return rc;
+  }
+  *out = r;
+  return SST_OK;
+}
+
 int sst_step_device(sst_table* t, const double* d_obs, int64_t n_peaks, const double* shifts, int n_shifts,
                     int8_t* d_valid_out, const double* d_mass, const double* d_thr, int64_t n, double tol, double prec,
                     const int64_t* d_mods, int64_t mods_scalar, int with_memo, uint64_t cap_count, sst_result** out) {
@@ -1373,7 +1416,7 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
       !r->rows_big.ensure(S * 4) || !r->rows_ctl.ensure(64))
     return bail(fail(c, SST_E_NOMEM, "device allocation failed (rows step)"));
   if (fresh) HIP_OK(c, hipMemsetAsync(r->rows_ctl.p, 0, 64, c->stream));
-  r->pass = {t, nullptr, nullptr, nullptr, max_mods_scalar, tol, prec, 1, cap_per_query};
+  r->pass = {t, nullptr, nullptr, nullptr, max_mods_scalar, tol, prec, 1, cap_per_query, nullptr, nullptr};
   r->pass_stream = c->stream;
   r->settle_ev_pending = false;
   r->rows_pass = true;
@@ -2110,7 +2153,9 @@ int sst_bins_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spe
 int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                          const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
                          const uint32_t* d_rows, const uint64_t* d_alpha, double tol, double prec,
-                         const uint64_t* d_q_off, int8_t* d_status, uint32_t* d_count, uint32_t* d_err) {
+                         const uint64_t* d_q_off, int8_t* d_status, uint32_t* d_count, double* d_def_mass,
+                         double* d_def_thr, int32_t* d_def_spec, uint64_t* d_def_q, uint32_t* d_n_def,
+                         uint32_t* d_err) {
   PipeArgs a;
   if (int rc = bins_args(t, d_peak_off, n_spec, d_rows_su, d_rows_ob, d_rows_meta, d_alive, d_rows, tol, prec,
                          const_cast<uint64_t*>(d_q_off), d_err, a))
@@ -2119,6 +2164,12 @@ int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
   a.alpha = d_alpha;
   a.q_status = d_status;
   a.q_count = d_count;
+  if (d_n_def && (!d_def_mass || !d_def_thr || !d_def_spec || !d_def_q)) return SST_E_ARG;
+  a.def_mass = d_def_mass;
+  a.def_thr = d_def_thr;
+  a.def_spec = d_def_spec;
+  a.def_q = d_def_q;
+  a.n_def = d_n_def;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;

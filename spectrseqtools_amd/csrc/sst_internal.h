@@ -105,6 +105,11 @@ struct QueryArgs {
   // budget, hi < pair_hi_lim <=> pair-class window whose budgets cannot bind,
   // hi < never_hi_lim <=> fast-path theorem; cap32 = min(cap_count, 2^32-1)
   uint32_t pair_hi_lim = 0, never_hi_lim = 0, cap32 = 0;
+  // per-query alphabets (sst_explain_alpha_batch_device): alpha[2 g], [2 g + 1]
+  // = row mask of alphabet g over the table's rows, spec[i] = query i's alphabet
+  const uint64_t* alpha = nullptr;
+  const int32_t* spec = nullptr;
+  int comp = 32;  // the table's compression (masses per packed word)
 };
 
 // Arena layout of one explain pass:
@@ -399,6 +404,13 @@ struct PipeArgs {
   uint64_t* q_off;            // [n_spec + 1] their exclusive offsets (total last)
   int8_t* q_status;           // [total] per bin query: SST_NONE / EMPTY / SOME, kStatusPending off the pair class
   uint32_t* q_count;          // [total] candidates on the spectrum's alphabet
+  // off-pair-class bin queries listed for the masked explain (may be null):
+  // window mass, threshold, spectrum and bin-query index; n_def their count
+  double* def_mass;
+  double* def_thr;
+  int32_t* def_spec;
+  uint64_t* def_q;
+  uint32_t* n_def;
   uint32_t* err;
 };
 hipError_t launch_bins_count(const PipeArgs& a, int n_wg, hipStream_t st);

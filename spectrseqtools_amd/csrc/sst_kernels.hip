@@ -587,41 +587,73 @@ struct EnumOut {
   int fail;  // 1 depth, 2 node budget
 };
 
+// The candidate's rows as the sinks read them: depths below 8 from a packed
+// register, deeper ones from the lane's stack.
+template <typename Stack>
+struct PathView {
+  const Stack& st;
+  uint64_t p0;  // row of depth d < 8 at bits 8d .. 8d+7
+  __device__ __forceinline__ uint8_t row(int d) const { return d < 8 ? (uint8_t)(p0 >> (8 * d)) : st.row(d); }
+};
+
+// The current frame (mass, rows left, budgets) lives in registers; the stack
+// holds only ancestors that still have rows left, and a 128-bit register
+// bitmap marks their depths.  A finished frame therefore returns straight to
+// the deepest such ancestor with one stack read (a single-candidate window:
+// none at all), instead of reading back every level on the way up; each
+// descent costs one dependent load (the child's index record).
 template <int MODE, typename Stack, typename Sink>
 __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, uint32_t v, int A0,
-                               Sink& sink, uint64_t node_budget, EnumOut& o) {
+                               Sink& sink, uint64_t node_budget, EnumOut& o, M128 am) {
   const int top_row = t.n_rows - 1;
-  M128 k0;
+  M128 k;
   if (MODE == MODE_EXACT) {
     const HEntry* e = h->find(v);
     if (!e) return;
-    k0 = mand(M128{e->en0, e->en1}, rows_upto(top_row));
+    k = mand(M128{e->en0, e->en1}, rows_upto(top_row));
   } else {
     ulonglong2 rec = ld_index(t.index, v);
     o.nodes++;
-    k0 = mand(rec_L(rec), rows_upto(top_row));
+    k = mand(mand(rec_L(rec), rows_upto(top_row)), am);
   }
-  st.set(0, v, k0);
-  if (MODE == MODE_NOMEMO) st.set_budget(0, A0, s.cap[top_row], top_row);
+  uint32_t m = v;
+  int A = A0, B = s.cap[top_row], top = top_row;  // budgets: MODE_NOMEMO only
   int d = 0;
+  uint64_t pend0 = 0, pend1 = 0;  // depths (0..63, 64..127) of saved frames with rows left
+  PathView<Stack> path{st, 0};
   while (true) {
-    M128 k = st.mask(d);
     if (mzero(k)) {
-      if (d == 0) break;
-      --d;
+      if ((pend0 | pend1) == 0) break;
+      if (pend1) {  // deepest pending ancestor
+        d = 127 - __builtin_clzll(pend1);
+        pend1 &= ~(1ull << (d - 64));
+      } else {
+        d = 63 - __builtin_clzll(pend0);
+        pend0 &= ~(1ull << d);
+      }
+      m = st.m(d);
+      k = st.mask(d);
+      if (MODE == MODE_NOMEMO) {
+        A = st.A(d);
+        B = st.B(d);
+        top = st.top(d);
+      }
       continue;
     }
-    int rr = mlow(k);
-    st.set_mask(d, mclear(k, rr));
+    const int rr = mlow(k);
+    k = mclear(k, rr);
     int Bv = 0;
     if (MODE == MODE_NOMEMO) {
-      Bv = (rr == st.top(d)) ? st.B(d) : s.cap[rr];
-      if (s.mod[rr] && !(st.A(d) > 0 && Bv > 0)) continue;
+      Bv = (rr == top) ? B : s.cap[rr];
+      if (s.mod[rr] && !(A > 0 && Bv > 0)) continue;
     }
-    int64_t child = (int64_t)st.m(d) - s.w[rr];
-    st.set_row(d, rr);
+    const int64_t child = (int64_t)m - s.w[rr];
+    if (d < 8)
+      path.p0 = (path.p0 & ~(0xFFull << (8 * d))) | ((uint64_t)rr << (8 * d));
+    else
+      st.set_row(d, rr);
     if (child == 0) {
-      sink.put(st, d, o.bytes);
+      sink.put(path, d, o.bytes);
       o.bytes += (uint64_t)(d + 2);
       o.count++;
       continue;
@@ -643,17 +675,28 @@ __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s,
       ulonglong2 rec = ld_index(t.index, child);
       o.nodes++;
       if (rec_lo(rec) > rr) continue;
-      kc = mand(rec_L(rec), rows_upto(rr));
+      kc = mand(mand(rec_L(rec), rows_upto(rr)), am);
     }
     if (d + 1 >= Stack::depth) {
       o.fail = 1;
       return;
     }
+    if (!mzero(k)) {  // save this frame only if it has rows left
+      st.set(d, m, k);
+      if (MODE == MODE_NOMEMO) st.set_budget(d, A, B, top);
+      if (d < 64)
+        pend0 |= 1ull << d;
+      else
+        pend1 |= 1ull << (d - 64);
+    }
     ++d;
-    st.set(d, (uint32_t)child, kc);
+    m = (uint32_t)child;
+    k = kc;
     if (MODE == MODE_NOMEMO) {
-      int md = s.mod[rr];
-      st.set_budget(d, st.A(d - 1) - md, Bv - md, rr);
+      const int md = s.mod[rr];
+      A -= md;
+      B = Bv - md;
+      top = rr;
     }
   }
 }
@@ -661,7 +704,8 @@ __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s,
 // payload bytes/counts of a whole window [a, b] of roots
 template <int MODE, typename Stack, typename Sink>
 __device__ __forceinline__ void enumerate_window(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, int64_t a, int64_t b,
-                                 int A0, Sink& sink, uint64_t node_budget, EnumOut& o) {
+                                 int A0, Sink& sink, uint64_t node_budget, EnumOut& o,
+                                 M128 am = M128{~0ull, ~0ull}) {
   if (a > b) return;
   int64_t wa = a >> 6, wb = b >> 6;
   for (int64_t wi = wa; wi <= wb; ++wi) {
@@ -672,7 +716,7 @@ __device__ __forceinline__ void enumerate_window(const TableArgs& t, const Lds& 
       int bit = __builtin_ctzll(x);
       x &= x - 1;
       uint32_t v = (uint32_t)((wi << 6) + bit);
-      enumerate_root<MODE>(t, s, st, h, v, A0, sink, node_budget, o);
+      enumerate_root<MODE>(t, s, st, h, v, A0, sink, node_budget, o, am);
       if (o.fail) return;
     }
   }
@@ -772,7 +816,7 @@ struct P1Frame {
 // Memo entry meta: hv (bits 0-7), ne (8-15), lo (16-23).
 template <bool WAVE>
 __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& h, uint32_t m, int r, int A, int B,
-                                        bool& nonempty, uint64_t& nodes, M128& en_out, HEntry*& ent) {
+                                        bool& nonempty, uint64_t& nodes, M128& en_out, HEntry*& ent, M128 am) {
   // the index record and the memo's first probe slot (key, meta and the
   // enabled mask: the whole 32-B entry) are independent: issue them together
   // (both were prefetched by the parent frame)
@@ -829,6 +873,7 @@ __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& 
       }
     }
   }
+  en = mand(en, am);  // a reduced alphabet: left branches on its rows only
   e->en0 = en_old0 | en.a;
   e->en1 = en_old1 | en.b;
   e->meta = (meta & 0xFF00u) | ((uint32_t)lo << 16) | (uint32_t)r;
@@ -877,14 +922,14 @@ __device__ __forceinline__ void p1_set_ne(HEntry* e, int rr) {  // lowest non-em
 // and pop, not per row).
 template <bool WAVE>
 __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
-                           uint64_t node_budget, uint64_t& nodes) {
+                           uint64_t node_budget, uint64_t& nodes, M128 am) {
   const int top = t.n_rows - 1;
   for (int64_t v = a; v <= b; ++v) {
     if (!((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;
     bool ne_dummy;
     M128 rest;
     HEntry* e;
-    int pr = p1_visit<WAVE>(t, s, h, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes, rest, e);
+    int pr = p1_visit<WAVE>(t, s, h, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes, rest, e, am);
     if (pr < 0) return -1;
     if (pr == 0) continue;
     uint32_t m = (uint32_t)v;
@@ -918,7 +963,8 @@ __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* f
         if (d + 1 >= kMaxDepth) return -2;
         M128 cen;
         HEntry* cent;
-        const int pushed = p1_visit<WAVE>(t, s, h, (uint32_t)child, rr, A - md, Bv - md, nonempty, nodes, cen, cent);
+        const int pushed =
+            p1_visit<WAVE>(t, s, h, (uint32_t)child, rr, A - md, Bv - md, nonempty, nodes, cen, cent, am);
         if (pushed < 0) return -1;
         if (pushed) {  // descend: save this frame (its pending row is rr)
           fr[d++] = P1Frame{rest.a, rest.b, e, m, A, B, (uint8_t)rtop, (uint8_t)(rr + 1), 0, 0};
@@ -990,14 +1036,14 @@ __device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, co
 // leaves one memory round trip per visited node: its index record and memo
 // entry, loaded together (p1_visit).
 __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
-                                uint64_t node_budget, uint64_t& nodes) {
+                                uint64_t node_budget, uint64_t& nodes, M128 am) {
   const int top = t.n_rows - 1;
   for (int64_t v = a; v <= b; ++v) {
     if (!((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;
     bool ne_dummy;
     M128 rest;
     HEntry* e;
-    int pr = p1_visit<true>(t, s, h, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes, rest, e);
+    int pr = p1_visit<true>(t, s, h, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes, rest, e, am);
     if (pr < 0) return -1;
     if (pr == 0) continue;
     uint32_t m = (uint32_t)v, meta = h.last_meta;
@@ -1035,7 +1081,8 @@ __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Fra
         if (d + 1 >= kMaxDepth) return -2;
         M128 cen;
         HEntry* cent;
-        const int pushed = p1_visit<true>(t, s, h, (uint32_t)child, rr, A - md, Bv - md, nonempty, nodes, cen, cent);
+        const int pushed =
+            p1_visit<true>(t, s, h, (uint32_t)child, rr, A - md, Bv - md, nonempty, nodes, cen, cent, am);
         if (pushed < 0) return -1;
         if (pushed) {  // descend: save this frame (its pending row is rr)
           fr[d++] = P1Frame{rest.a, rest.b, e, m, A, B, (uint8_t)rtop, (uint8_t)(rr + 1), (uint8_t)ne, 0, meta};
@@ -1062,10 +1109,10 @@ __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Fra
 // and the lanes split only the prefetch loads (p1_visit).
 template <bool WAVE>
 __device__ int phase1(const TableArgs& t, const Lds& s, Hash& h, P1Frame* fr, int64_t a, int64_t b, int A0,
-                      uint64_t node_budget, uint64_t& nodes) {
+                      uint64_t node_budget, uint64_t& nodes, M128 am = M128{~0ull, ~0ull}) {
   h.sink = 0;
-  const int rc = WAVE ? phase1_body_wave(t, s, h, fr, a, b, A0, node_budget, nodes)
-                      : phase1_body<WAVE>(t, s, h, fr, a, b, A0, node_budget, nodes);
+  const int rc = WAVE ? phase1_body_wave(t, s, h, fr, a, b, A0, node_budget, nodes, am)
+                      : phase1_body<WAVE>(t, s, h, fr, a, b, A0, node_budget, nodes, am);
   // (never true) keeps every lane's prefetch loads alive; a ballot keeps rc uniform
   return __ballot(h.sink == 0x5bd1e9955bd1e995ull) ? rc - 100 : rc;
 }
@@ -2226,6 +2273,30 @@ __global__ __launch_bounds__(256) void k_wire_pack(WireArgs a) {
   }
 }
 
+// The row mask of query i's alphabet (sst_explain_alpha_batch_device: its
+// spectrum's reduced alphabet over this table's rows; all rows otherwise).
+__device__ __forceinline__ M128 query_alpha(const QueryArgs& q, int64_t i) {
+  if (!q.alpha) return M128{~0ull, ~0ull};
+  const int64_t g = q.spec ? (int64_t)q.spec[i] : 0;
+  return M128{q.alpha[2 * g], q.alpha[2 * g + 1]};
+}
+// A reduced table is rebuilt up to max(kept masses) * 35 (mass_table.py:
+// 114-117, MAX_SEQ_LENGTH) with ceil((max_mass + 1) / C) words per row.  A
+// window reaching its extent raises (status OUT_OF_TABLE, :134-138); one in
+// its last word, whose bits the reference's last-column mask may clear
+// (mass_table.py:246), is not modelled by the full table's rows: ABORTED.
+__device__ __forceinline__ int8_t alpha_extent_status(const TableArgs& t, const QueryArgs& q, const Lds& s, M128 am,
+                                                      int64_t hi) {
+  if (!q.alpha) return SST_NONE;
+  am = mand(am, rows_upto(t.n_rows - 1));
+  const int top = am.b ? 127 - __builtin_clzll(am.b) : 63 - __builtin_clzll(am.a | 1ull);
+  const int64_t max_mass = (int64_t)s.w[top] * 35;
+  const int64_t lim = (max_mass + q.comp) / q.comp * q.comp;  // ceil((max_mass + 1) / C) * C
+  if (hi >= lim) return SST_OUT_OF_TABLE;
+  if (hi >= lim - q.comp) return SST_ABORTED;
+  return SST_NONE;
+}
+
 // Deferred fast/no-memo queries with deep stacks: persistent grid, one lane per
 // query, stack in a per-lane slice of the workspace.
 template <int MODE>
@@ -2249,18 +2320,25 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
     int8_t status = SST_NONE;
     uint64_t bytes = 0;
     RegSinkDeep rs;  // the candidates' first 32 bytes, written by the counting DFS
+    M128 am{~0ull, ~0ull};
     if (live) {
       i = out.lists[(int64_t)cls * q.n + j];
+      am = query_alpha(q, i);
       int64_t lo, hi;
       quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
       A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
       const bool has_zero = lo <= 0 && hi >= 0;
       a = lo < 1 ? 1 : lo;
       b = hi;
-      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, rs, q.node_budget, eo);
+      const int8_t ext = alpha_extent_status(t, q, s, am, b);
+      if (ext != SST_NONE) a = 1, b = 0;  // nothing to enumerate
+      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, rs, q.node_budget, eo, am);
       status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
       bytes = eo.bytes;
-      if (eo.fail) {
+      if (ext != SST_NONE) {
+        status = ext;
+        bytes = 0;
+      } else if (eo.fail) {
         status = SST_ABORTED;
         bytes = 0;
       } else if (eo.count > q.cap_count) {
@@ -2281,7 +2359,7 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
     } else if (to.bytes) {  // more than 32 bytes: enumerate again straight into the arena
       MemSink ms{out.payload + to.off, ~0ull};
       EnumOut e2{0, 0, 0, 0};
-      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2);
+      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2, am);
     }
     emit_result_wg(out, live, (uint32_t)i, to.status, eo.count, to.off);
     if (live) {
@@ -2319,8 +2397,10 @@ __device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs
     int8_t status = SST_NONE;
     EnumOut eo{0, 0, 0, 0};
     uint64_t bytes = 0, nodes = 0;
+    M128 am{~0ull, ~0ull};
     if (live) {
       i = out.lists[(int64_t)kClassExact * q.n + j];
+      am = query_alpha(q, i);
       int64_t lo, hi;
       quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
       A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
@@ -2329,8 +2409,12 @@ __device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs
       b = hi;
       h.epoch = ++ws.epochs[gid];
       h.used = 0;
-      const int rc = phase1<false>(t, s, h, fr, a, b, A0, q.node_budget, nodes);
-      if (rc == -1) {
+      const int8_t ext = alpha_extent_status(t, q, s, am, b);
+      if (ext != SST_NONE) a = 1, b = 0;
+      const int rc = ext != SST_NONE ? -4 : phase1<false>(t, s, h, fr, a, b, A0, q.node_budget, nodes, am);
+      if (rc == -4) {
+        status = ext;
+      } else if (rc == -1) {
         status = (int8_t)kStatusExactRetry;
         atomicAdd(out.exact_retries, 1ull);  // lets the host see it without a status scan (settle)
       } else if (rc < 0) {

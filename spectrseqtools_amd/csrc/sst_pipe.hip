@@ -579,8 +579,9 @@ __global__ __launch_bounds__(kPipeWG) void k_bins_emit(TableArgs t, PipeArgs a) 
       quantise_lean(mass, thr, a.prec, a.rprec, lof, hif);
       int8_t st = SST_NONE;
       uint32_t cnt = 0;
-      if (!(hif < (double)t.pair_hi)) {
-        st = (int8_t)kStatusPending;  // not a pair-class window: the caller's other path
+      const bool pend = !(hif < (double)t.pair_hi);
+      if (pend) {
+        st = (int8_t)kStatusPending;  // not a pair-class window: listed for the masked explain
       } else if (hif >= 0.0) {
         const double af = lof < 1.0 ? 1.0 : lof;
         uint64_t u0 = 0, u1 = 0;
@@ -589,6 +590,19 @@ __global__ __launch_bounds__(kPipeWG) void k_bins_emit(TableArgs t, PipeArgs a) 
       }
       a.q_status[base + o] = st;
       a.q_count[base + o] = cnt;
+      if (a.n_def) {  // one returning atomic per wave instruction
+        const uint64_t bal = __ballot(pend);
+        if (pend) {
+          const int lane = threadIdx.x & 63, leader = __builtin_ctzll(bal);
+          uint32_t pos = 0;
+          if (lane == leader) pos = atomicAdd(a.n_def, (uint32_t)__builtin_popcountll(bal));
+          pos = __shfl(pos, leader, 64) + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+          a.def_mass[pos] = mass;
+          a.def_thr[pos] = thr;
+          a.def_spec[pos] = (int32_t)g;
+          a.def_q[pos] = base + o;
+        }
+      }
     }
     __syncthreads();
   }

@@ -194,14 +194,21 @@ class DeviceBins:
     """The skeleton's speculative bin queries of every spectrum, answered on
     its alphabet (spectrum-major: START side, then END; bins in order)."""
     q_off: np.ndarray     # [S + 1] query offsets per spectrum
-    status: object        # torch int8 [Q]: SST_NONE / EMPTY / SOME, -10 off the pair class
+    status: object        # torch int8 [Q]: SST_NONE / EMPTY / SOME (-10 off the pair class when not answered)
     count: object         # torch int32 [Q] candidates
+    deferred: dict = None  # the off-pair-class queries' masked explain: n, per max_len group results, tallies
 
 
-def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=MATCHING_THRESHOLD):
+def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=MATCHING_THRESHOLD, max_len=None):
     """Stage 3 on the device (SkeletonBuilder._predict_skeleton's bins,
     skeleton_building.py:114-160) over the rows the fixpoint kept
-    (rows.alive) and the final alphabets `alpha` ([S, 2] u64 row masks)."""
+    (rows.alive) and the final alphabets `alpha` ([S, 2] u64 row masks).
+    Pair-class windows are answered by k_bins_emit; with max_len (per
+    spectrum) the others -- the sides' first bins' whole masses and wide bin
+    differences -- are listed by it and answered by the masked explain
+    (sst_explain_alpha_batch_device, the DFS roles on each spectrum's
+    alphabet), one pass per max_len group (its budgets: round(0.5 max_len),
+    caps round(max_len * rate), common.py:55, mass_explanation.py:158-172)."""
     import torch
 
     S = len(rows.rows)
@@ -223,10 +230,67 @@ def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=MATCHING_THRESHOLD)
     total = int(q_off[S].item())
     status = torch.empty(max(1, total), dtype=torch.int8, device=dev)
     count = torch.empty(max(1, total), dtype=torch.int32, device=dev)
+    defer = max_len is not None
+    if defer:
+        d_mass = torch.empty(max(1, total), dtype=torch.float64, device=dev)
+        d_thr = torch.empty_like(d_mass)
+        d_spec = torch.empty(max(1, total), dtype=torch.int32, device=dev)
+        d_q = torch.empty(max(1, total), dtype=torch.int64, device=dev)
+        n_def = torch.zeros(1, dtype=torch.int32, device=dev)
+    ptr = (lambda x: x.data_ptr()) if defer else (lambda x: None)
     eng.check(L.sst_bins_emit_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(), rows.obs.data_ptr(),
                                      rows.meta.data_ptr(), rows.alive.data_ptr(), rows.rows.data_ptr(), a.data_ptr(),
                                      float(tolerance), float(dp_table.precision), q_off.data_ptr(),
-                                     status.data_ptr(), count.data_ptr(), err.data_ptr()), "sst_bins_emit_device")
+                                     status.data_ptr(), count.data_ptr(), ptr(d_mass) if defer else None,
+                                     ptr(d_thr) if defer else None, ptr(d_spec) if defer else None,
+                                     ptr(d_q) if defer else None, ptr(n_def) if defer else None, err.data_ptr()),
+              "sst_bins_emit_device")
     eng.synchronize()
     _check_err(err)
-    return DeviceBins(q_off.cpu().numpy(), status[:total], count[:total])
+    out = DeviceBins(q_off.cpu().numpy(), status[:total], count[:total])
+    if defer:
+        out.deferred = answer_deferred(dp_table, a, d_mass, d_thr, d_spec, d_q, int(n_def.item()), max_len,
+                                       status, count)
+    return out
+
+
+def answer_deferred(dp_table, alpha, d_mass, d_thr, d_spec, d_q, n, max_len, status, count):
+    """The listed off-pair-class windows through the masked explain, one pass
+    per max_len group (the rows' caps follow max_len); statuses and counts
+    scattered into the bin-query arrays.  Returns the per-group results."""
+    import torch
+
+    dt = dp_table.device_table
+    eng = dt.engine
+    info = {"queries": n, "groups": [], "results": []}
+    if n == 0:
+        return info
+    spec = d_spec[:n].cpu().numpy()
+    ml = np.asarray(max_len, dtype=np.int64)[spec]
+    order = np.argsort(ml, kind="stable")
+    o = torch.as_tensor(order, device=d_mass.device)
+    mass, thr = d_mass[:n][o].contiguous(), d_thr[:n][o].contiguous()
+    sp, qi = d_spec[:n][o].contiguous(), d_q[:n][o].contiguous()
+    ml_s = ml[order]
+    info["spec"], info["mass"], info["thr"] = sp.cpu().numpy(), mass.cpu().numpy(), thr.cpu().numpy()
+    bounds = np.flatnonzero(np.diff(ml_s)) + 1
+    starts = np.concatenate([[0], bounds])
+    ends = np.concatenate([bounds, [n]])
+    masses = dp_table.masses
+    is_mod = [m.is_modification for m in masses]
+    A_rate = dp_table.seq.modification_rate
+    for s0, s1 in zip(starts.tolist(), ends.tolist()):
+        L = int(ml_s[s0])
+        dt.set_budgets(is_mod, [round(L * m.modification_rate) for m in masses])
+        k = int(s1 - s0)
+        res = dt.explain_alpha_device(mass.data_ptr() + 8 * s0, thr.data_ptr() + 8 * s0, sp.data_ptr() + 4 * s0,
+                                      alpha.data_ptr(), k, dp_table.tolerance, dp_table.precision,
+                                      round(A_rate * L))
+        res.fetch_device()
+        idx = qi[s0:s1]
+        status[idx] = torch.as_tensor(res.status, device=status.device)
+        count[idx] = torch.as_tensor(res.count.astype(np.int32), device=count.device)
+        info["groups"].append((L, k))
+        info["results"].append((int(s0), res))
+    info["order"] = order
+    return info

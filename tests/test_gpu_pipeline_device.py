@@ -115,3 +115,73 @@ def test_device_stages_equal_host_driven(engine, peak_order):
     assert np.array_equal(db.status.cpu().numpy(), st3[order])
     assert np.array_equal(db.count.cpu().numpy().astype(np.int64), cnt3[order].astype(np.int64))
     assert (st3 == 2).sum() > 0
+
+
+def test_device_bins_deferred_vs_rebuilt_tables(engine):
+    """Stage 3's off-pair-class bin queries (the sides' first bins' whole
+    masses, wide bin differences) answered by the masked explain on each
+    spectrum's final alphabet with its own budgets (max_len groups), against
+    the oracle on that alphabet's rebuilt table; the pair-class answers are
+    those of the plain emit."""
+    import _oracle as oracle
+    from spectrseqtools_amd import _native, pipeline, pipeline_device as PD
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict
+    from spectrseqtools_amd.synthetic import make_spectra
+
+    b = make_spectra(400, seed=37)
+    bd = build_breakage_dict(555.1294, 455.1491)
+    w_full = [k for k, v in bd.items() if "START_END" in v][0]
+    su_seq = b.seq_mass - w_full * TOLERANCE
+    seq = SequenceInformation(max_len=20, su_mass=float(su_seq[0]), obs_mass=float(b.seq_mass[0]),
+                              modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=engine)
+    max_len = pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:]))
+    # every other spectrum loses its peaks below 1.6 kDa (missing short
+    # fragments): its sides' first bins are whole masses of 3+ nucleotides,
+    # off the pair class (the exact replay with binding budgets)
+    spec = np.repeat(np.arange(len(b.offsets) - 1), np.diff(b.offsets))
+    keep = (spec % 2 == 1) | (b.observed > 1600.0)
+    obs = b.observed[keep]
+    offsets = np.concatenate([[0], np.cumsum(np.bincount(spec[keep], minlength=len(b.offsets) - 1))])
+    rows = PD.classify_device(dp, obs, offsets, su_seq, bd)
+    fx = PD.fixpoint_device(dp, rows, max_len)
+    plain = PD.bins_device(dp, rows, fx.alpha)
+    full = PD.bins_device(dp, rows, fx.alpha, max_len=max_len)
+    st0, st1 = plain.status.cpu().numpy(), full.status.cpu().numpy()
+    pend = st0 == -10
+    assert pend.sum() == full.deferred["queries"] > 100
+    assert np.array_equal(st0[~pend], st1[~pend])
+    assert not (st1 == -10).any()
+    d = full.deferred
+    ms_all = [m.mass for m in dp.masses]
+    is_mod = [m.is_modification for m in dp.masses]
+    rate = [m.modification_rate for m in dp.masses]
+    masks = pipeline.mask_rows(fx.alpha, len(ms_all))
+    tabs = {}
+    n_checked = n_some = 0
+    spec_l, mass_l, thr_l = d["spec"], d["mass"], d["thr"]  # list order of the results
+    for s0, res in d["results"]:
+        for j in range(0, res.n, 5):
+            k = s0 + j
+            g = int(spec_l[k])
+            keep = [0] + [r for r in range(1, len(ms_all)) if masks[g, r]]
+            if g not in tabs:
+                ms = [ms_all[r] for r in keep]
+                tabs[g] = (oracle.build_table(ms, max(ms) * 35, 32),
+                           oracle.Alphabet(ms, [is_mod[r] for r in keep],
+                                           [round(int(max_len[g]) * rate[r]) for r in keep]))
+            tab, alph = tabs[g]
+            A = round(dp.seq.modification_rate * int(max_len[g]))
+            st, sols, n_e, _ = oracle.explain_table(tab, 32, alph, mass_l[k], thr_l[k], dp.tolerance, A)
+            want = [tuple(keep[x] for x in t) for t in sols]
+            want_st = (_native.SST_OUT_OF_TABLE if st < 0 else _native.SST_SOME if want else
+                       _native.SST_EMPTY if n_e else _native.SST_NONE)
+            assert int(res.status[j]) == want_st, (k, g, mass_l[k])
+            if want_st == _native.SST_SOME:
+                assert res.candidates(j) == want, (k, g)
+                n_some += 1
+            n_checked += 1
+    assert n_checked > 50 and n_some > 10
+

@@ -14,7 +14,10 @@ stages over many synthetic spectra, batched on the GPU engine
   stage 3  skeleton bins on the surviving fragments and reduced alphabets:
            each side's bins, first bin's whole masses and every later bin
            against its predecessor -> explain (pair-class windows:
-           k_pairs_alpha; the rest are counted)
+           k_bins_emit's masked pair list; the rest -- whole masses, wide
+           differences -- through the masked explain's DFS roles on each
+           spectrum's alphabet, one pass per max_len group; the host-driven
+           path counts them)
 
 One process per GPU (torch.distributed.run for N > 1, spectra sharded by
 rank, no collective in the data path); every stage is timed over all of this
@@ -119,7 +122,7 @@ def main():
 
         rw = pd.classify_device(dp, o0, s0, su_seq[:S0], bd)
         fw = pd.fixpoint_device(dp, rw, m0)
-        bw = pd.bins_device(dp, rw, fw.alpha)
+        bw = pd.bins_device(dp, rw, fw.alpha, max_len=m0)
         sw = bw.status == 2
         int(sw.sum().item()), int((bw.status == -10).sum().item()), int(bw.count[sw].sum().item())
     engine.synchronize()
@@ -198,15 +201,20 @@ def main():
     else:  # device-resident: bins formed and answered in HBM, only the tallies read back
         from spectrseqtools_amd import pipeline_device as pd
 
-        db = pd.bins_device(dp, rows, fx_alpha)
+        db = pd.bins_device(dp, rows, fx_alpha, max_len=max_len)
         some = db.status == 2
         n_bins_q = int(db.q_off[-1])
+        n_def = db.deferred["queries"]
         n_some, n_pend = int(some.sum().item()), int((db.status == -10).sum().item())
         n_cand = int(db.count[some].sum().item())
     barrier()
     stages["bins"] = {"s": tmax(time.perf_counter() - t0), "queries": n_bins_q,
-                      "pair_class": n_bins_q - n_pend, "not_pair_class": n_pend,
+                      "pair_class": n_bins_q - (n_pend if rows is None else n_def),
+                      "not_pair_class": n_pend if rows is None else n_def,
+                      "not_pair_class_unanswered": n_pend,
                       "with_candidates": n_some, "candidates": n_cand}
+    if rows is not None:
+        stages["bins"]["masked_explain_groups"] = [list(x) for x in db.deferred["groups"]]
     stages["bins"]["kernels"] = kernels()
     busy(stages["bins"])
     engine.profile(False)
