@@ -441,6 +441,17 @@ int sst_device_count(void) {
   return n;
 }
 
+#ifdef SST_DIAG_TIME  // timing builds only (tools/c1_time.py)
+}  // extern "C"
+namespace sst {
+hipError_t diag_time_read(void* dst, size_t bytes);
+hipError_t diag_time_clear();
+}  // namespace sst
+extern "C" {
+int sst_diag_time_read(void* dst, size_t bytes) { return sst::diag_time_read(dst, bytes) == hipSuccess ? 0 : -1; }
+int sst_diag_time_clear() { return sst::diag_time_clear() == hipSuccess ? 0 : -1; }
+#endif
+
 int sst_ctx_create(int device, sst_ctx** out) {
   if (!out) return SST_E_ARG;
   *out = nullptr;

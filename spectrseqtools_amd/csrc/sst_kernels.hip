@@ -446,6 +446,43 @@ struct RegSinkDeep {
     }
   }
 };
+// The first two candidates of a deep-path lane as their packed paths (rows
+// of depths 0..7, PathView::p0) and depths, kept in VGPRs during the
+// counting DFS: a leaf costs two register moves instead of assembling its
+// payload record byte by byte inside the divergent DFS loop (config 1: one
+// candidate of <= 8 items per query; the record bytes were 10 of its 51 us).
+// A third candidate or a deeper one sets `over` (the lane enumerates again
+// straight into the arena).
+struct RegSinkPaths {
+  uint64_t p0 = 0, p1 = 0;
+  int d0 = 0, d1 = 0, n = 0;
+  bool over = false;
+  template <typename Path>
+  __device__ __forceinline__ void put(const Path& path, int d, uint64_t) {
+    if (n >= 2 || d >= 8) {
+      over = true;
+      return;
+    }
+    if (n == 0) {
+      p0 = path.p0;
+      d0 = d;
+    } else {
+      p1 = path.p0;
+      d1 = d;
+    }
+    ++n;
+  }
+  // record [d + 1][rows ascending] = [d + 1][row(d) .. row(0)]
+  __device__ __forceinline__ static void record(uint8_t* dst, uint64_t p, int d) {
+    dst[0] = (uint8_t)(d + 1);
+    for (int k = 0; k <= d; ++k) dst[1 + k] = (uint8_t)(p >> (8 * (d - k)));
+  }
+  __device__ __forceinline__ void flush(uint8_t* dst, uint64_t) const {
+    if (n > 0) record(dst, p0, d0);
+    if (n > 1) record(dst + d0 + 2, p1, d1);
+  }
+};
+
 // Sinks of the shallow path receive the (<= 3) rows ascending as scalars.
 struct CountSink3 {
   __device__ __forceinline__ void put(uint64_t, int, int, int, int) {}
@@ -585,6 +622,7 @@ struct EnumOut {
   uint64_t bytes;
   uint64_t nodes;
   int fail;  // 1 depth, 2 node budget
+  uint32_t iters = 0;  // loop iterations (timing builds)
 };
 
 // The candidate's rows as the sinks read them: depths below 8 from a packed
@@ -622,6 +660,9 @@ __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s,
   uint64_t pend0 = 0, pend1 = 0;  // depths (0..63, 64..127) of saved frames with rows left
   PathView<Stack> path{st, 0};
   while (true) {
+#ifdef SST_DIAG_TIME
+    o.iters++;
+#endif
     if (mzero(k)) {
       if ((pend0 | pend1) == 0) break;
       if (pend1) {  // deepest pending ancestor
@@ -2273,6 +2314,20 @@ __global__ __launch_bounds__(256) void k_wire_pack(WireArgs a) {
   }
 }
 
+#ifdef SST_DIAG_TIME  // timing builds only (tools/c1_time.py): per-wave phase clocks of the deep role
+__device__ uint64_t g_diag_time[1 << 20];
+#define DIAG_T(k)                                                                                        \
+  do {                                                                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memrealtime();                                                \
+    if ((threadIdx.x & 63) == 0 && MODE == MODE_FAST)                                                    \
+      g_diag_time[8 * ((int64_t)blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) + (k)] = t_;               \
+  } while (0)
+#else
+#define DIAG_T(k) \
+  do {            \
+  } while (0)
+#endif
+
 // The row mask of query i's alphabet (sst_explain_alpha_batch_device: its
 // spectrum's reduced alphabet over this table's rows; all rows otherwise).
 __device__ __forceinline__ M128 query_alpha(const QueryArgs& q, int64_t i) {
@@ -2302,12 +2357,14 @@ __device__ __forceinline__ int8_t alpha_extent_status(const TableArgs& t, const 
 template <int MODE>
 __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs& out, int cls, GlobFrame* ws, Lds& s,
                           int blk, int nblk) {
+  DIAG_T(0);
   const uint32_t n_list = out.counters[cls];
   if (n_list == 0) return;  // block-uniform: nothing queued for this role
   stage_rows(s, t);
   const int64_t gid = (int64_t)blk * blockDim.x + threadIdx.x;
   const int64_t nthreads = (int64_t)nblk * blockDim.x;
   GlobStack st{ws + gid, (uint32_t)nthreads};
+  DIAG_T(1);
   uint64_t st_n = 0, st_nodes = 0;
   // workgroup-uniform trip count: the payload allocation and the hit records
   // take one atomic per workgroup (wg_alloc), not one per wave or query
@@ -2319,7 +2376,7 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
     EnumOut eo{0, 0, 0, 0};
     int8_t status = SST_NONE;
     uint64_t bytes = 0;
-    RegSinkDeep rs;  // the candidates' first 32 bytes, written by the counting DFS
+    RegSinkPaths rs;  // the first two candidates' paths, kept by the counting DFS
     M128 am{~0ull, ~0ull};
     if (live) {
       i = out.lists[(int64_t)cls * q.n + j];
@@ -2332,6 +2389,7 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
       b = hi;
       const int8_t ext = alpha_extent_status(t, q, s, am, b);
       if (ext != SST_NONE) a = 1, b = 0;  // nothing to enumerate
+      DIAG_T(2);
       enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, rs, q.node_budget, eo, am);
       status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
       bytes = eo.bytes;
@@ -2353,7 +2411,9 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
       }
       continue;
     }
+    DIAG_T(3);
     const TileOut to = spill_alloc_wg(out, bytes, status);
+    DIAG_T(4);
     if (to.bytes && !rs.over) {
       rs.flush(out.payload + to.off, to.bytes);
     } else if (to.bytes) {  // more than 32 bytes: enumerate again straight into the arena
@@ -2362,12 +2422,22 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
       enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2, am);
     }
     emit_result_wg(out, live, (uint32_t)i, to.status, eo.count, to.off);
+    DIAG_T(5);
+#ifdef SST_DIAG_TIME
+    {
+      uint32_t it = eo.iters;
+      for (int o_ = 32; o_ > 0; o_ >>= 1) it = max(it, (uint32_t)__shfl_xor((int)it, o_, 64));
+      if ((threadIdx.x & 63) == 0 && MODE == MODE_FAST)
+        g_diag_time[8 * ((int64_t)blk * (blockDim.x >> 6) + (threadIdx.x >> 6)) + 7] = it;
+    }
+#endif
     if (live) {
       st_n++;
       st_nodes += eo.nodes;
     }
   }
   wg_stat(out.stats, MODE == MODE_FAST ? kStatDeep : kStatNomemo, st_n);
+  DIAG_T(6);
   wg_stat(out.stats, kStatNodes, st_nodes);
 }
 
@@ -3446,6 +3516,18 @@ hipError_t launch_wire_pack(const WireArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_wire_pack, dim3(a.be_e), dim3(256), 0, st, a);
   return hipGetLastError();
 }
+#ifdef SST_DIAG_TIME
+hipError_t diag_time_read(void* dst, size_t bytes) { return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_diag_time), bytes); }
+hipError_t diag_time_clear() {
+  static uint64_t zeros[1 << 16];
+  for (size_t o = 0; o < sizeof(g_diag_time); o += sizeof(zeros)) {
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_diag_time), zeros, sizeof(zeros), o);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+#endif
+
 hipError_t launch_explain_deferred(const TableArgs& t, const QueryArgs& q, const OutArgs& o, void* ws_deep,
                                    int shallow_blocks, int deep_blocks, const ExactWs& ws, int exact_blocks,
                                    hipStream_t st) {
