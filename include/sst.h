@@ -345,6 +345,23 @@ int sst_result_stats(const sst_result* r, uint64_t* stats_out /* [8] */);
  * min([]) raises ValueError), SST_ABORTED (DFS node budget exhausted: no
  * bound).  Synchronous, host buffers. */
 #define SST_LB_EMPTY_WINDOW (-5)
+/* sst_length_bound_batch on per-query reduced alphabets (the table
+ * adapt_individual_modification_rates_by_alphabet_reduction would rebuild,
+ * mass_table.py:94-121, as select_sequence_length_with_jaccard / _with_lp
+ * call it after reducing to the skeleton's nucleotides, skeleton_building.py:
+ * 212-224, 324-336): query i on alphabet spec[i] (spec NULL: alphabet 0) of
+ * n_alpha row masks alpha[2 g], alpha[2 g + 1] over the table's rows; the
+ * exact replay with the mask, no table rebuilt.  A window reaching the reduced
+ * table's extent is SST_OUT_OF_TABLE, one in its last packed word
+ * SST_ABORTED (as sst_explain_alpha_batch_device).  direction must be 0
+ * ("lower"; SST_E_ARG otherwise): the reference's upper bound counts a
+ * visited child that returned the default as -1 + 1 = 0, and the masked walk
+ * visits children the rebuilt table would not (reachable only with dropped
+ * rows), so "upper" needs the rebuilt table.  Host buffers. */
+int sst_length_bound_alpha_batch(sst_table* t, const double* su_mass, const double* obs_mass, const int32_t* spec,
+                                 const uint64_t* alpha, int64_t n_alpha, int64_t n, double tolerance,
+                                 double precision, int max_len, int64_t max_mods, int direction, int64_t* out,
+                                 int8_t* status);
 #define SST_LB_EXACT_ONLY 2 /* direction flag: skip the layered fast path (tests) */
 int sst_length_bound_batch(sst_table* t, const double* su_mass, const double* obs_mass, int64_t n, double tolerance,
                            double precision, int max_len, int64_t max_mods, int direction, int64_t* out,

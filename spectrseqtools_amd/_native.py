@@ -32,7 +32,7 @@ EXPORTS = (
     "sst_wire_pack", "sst_explain_pairs_alpha", "sst_explain_pairs_alpha_device", "sst_is_valid_alpha",
     "sst_is_valid_alpha_device", "sst_dict_union", "sst_step_rows_device", "sst_result_queries",
     "sst_classify_rows_device", "sst_fix_round_device", "sst_valid_rows_alpha_device",
-    "sst_bins_count_device", "sst_bins_emit_device",
+    "sst_bins_count_device", "sst_bins_emit_device", "sst_length_bound_alpha_batch",
 )
 
 # kernel ids of sst_profile_read
@@ -119,6 +119,7 @@ def load_library(path=LIB_PATH):
     lib.sst_profile_sample.argtypes = [_P, ctypes.c_uint32]
     lib.sst_profile_read.argtypes = [_P, _P, _P]
     lib.sst_length_bound_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _I, _I64, _I, _P, _P]
+    lib.sst_length_bound_alpha_batch.argtypes = [_P, _P, _P, _P, _P, _I64, _I64, _D, _D, _I, _I64, _I, _P, _P]
     lib.sst_explain_recursion_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _U64, _PP]
     lib.sst_is_singleton_batch.argtypes = [_P, _P, _I, _P, _P, _I64, _D, _D, _P]
     lib.sst_is_singleton_batch_device.argtypes = [_P, _P, _I, _P, _P, _I64, _D, _D, _P]
@@ -566,6 +567,24 @@ class DeviceTable:
                                                                   float(tolerance), float(precision), int(max_len),
                                                                   int(max_mods), d, _ptr(out), _ptr(st)),
                           "sst_length_bound_batch")
+        return out, st
+
+    def length_bound_alpha(self, su_masses, obs_masses, spec, alpha, tolerance, precision, max_len, max_mods,
+                           direction):
+        """length_bound with query i on the reduced alphabet alpha[spec[i]]
+        ([n_alpha, 2] u64 row masks; sst_length_bound_alpha_batch)."""
+        su = np.ascontiguousarray(su_masses, dtype=np.float64)
+        ob = np.ascontiguousarray(obs_masses, dtype=np.float64)
+        sp = np.ascontiguousarray(spec, dtype=np.int32)
+        al = np.ascontiguousarray(alpha, dtype=np.uint64).reshape(-1, 2)
+        if su.shape != ob.shape or sp.shape != su.shape:
+            raise ValueError("su_masses, obs_masses and spec differ in length")
+        out = np.zeros(len(su), np.int64)
+        st = np.zeros(len(su), np.int8)
+        d = {"lower": 0, "upper": 1}[direction] if isinstance(direction, str) else int(direction)
+        self.engine.check(self.engine._lib.sst_length_bound_alpha_batch(
+            self.handle, _ptr(su), _ptr(ob), _ptr(sp), _ptr(al), len(al), len(su), float(tolerance),
+            float(precision), int(max_len), int(max_mods), d, _ptr(out), _ptr(st)), "sst_length_bound_alpha_batch")
         return out, st
 
     def is_valid_peaks(self, observed, shifts, tolerance, precision):

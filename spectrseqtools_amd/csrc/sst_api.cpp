@@ -2249,8 +2249,11 @@ int sst_is_valid_alpha(sst_table* t, const double* mass, const double* thr, cons
   return SST_OK;
 }
 
-int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, int64_t n, double tol, double prec,
-                           int max_len, int64_t max_mods, int direction, int64_t* out, int8_t* status) {
+}  // extern "C"
+namespace {
+static int length_bound_batch(sst_table* t, const double* su, const double* obs, int64_t n, double tol, double prec,
+                              int max_len, int64_t max_mods, int direction, int64_t* out, int8_t* status,
+                              const int32_t* spec, const uint64_t* alpha, int64_t n_alpha) {
   const bool exact_only = (direction & SST_LB_EXACT_ONLY) != 0;
   direction &= ~SST_LB_EXACT_ONLY;
   if (!t || n < 0 || n > INT32_MAX || (n > 0 && (!su || !obs || !out || !status)) || (direction != 0 && direction != 1) ||
@@ -2261,10 +2264,18 @@ int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, in
   if (int rc = set_device(c)) return rc;
   if (n == 0) return SST_OK;
   const size_t nn = (size_t)n;
-  DevBuf d_su, d_obs, d_out, d_st, d_list, d_cnt, layers;
+  DevBuf d_su, d_obs, d_out, d_st, d_list, d_cnt, layers, d_spec, d_alpha;
   if (!d_su.ensure(nn * 8) || !d_obs.ensure(nn * 8) || !d_out.ensure(nn * 8) || !d_st.ensure(nn) ||
       !d_list.ensure(nn * 4) || !d_cnt.ensure(4))
     return fail(c, SST_E_NOMEM, "device allocation failed (length bound)");
+  if (alpha) {
+    for (int64_t i = 0; spec && i < n; ++i)
+      if (spec[i] < 0 || spec[i] >= n_alpha) return fail(c, SST_E_ARG, "length bound: alphabet index out of range");
+    if (!d_alpha.ensure((size_t)n_alpha * 16) || (spec && !d_spec.ensure(nn * 4)))
+      return fail(c, SST_E_NOMEM, "device allocation failed (length bound alphabets)");
+    HIP_OK(c, hipMemcpyAsync(d_alpha.p, alpha, (size_t)n_alpha * 16, hipMemcpyHostToDevice, c->stream));
+    if (spec) HIP_OK(c, hipMemcpyAsync(d_spec.p, spec, nn * 4, hipMemcpyHostToDevice, c->stream));
+  }
   HIP_OK(c, hipMemcpyAsync(d_su.p, su, nn * 8, hipMemcpyHostToDevice, c->stream));
   HIP_OK(c, hipMemcpyAsync(d_obs.p, obs, nn * 8, hipMemcpyHostToDevice, c->stream));
   HIP_OK(c, hipMemsetAsync(d_cnt.p, 0, 4, c->stream));
@@ -2283,10 +2294,13 @@ int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, in
   q.exact_list = (uint32_t*)d_list.p;
   q.exact_count = (uint32_t*)d_cnt.p;
   q.node_budget = kLBNodeBudget;
+  q.alpha = alpha ? (const uint64_t*)d_alpha.p : nullptr;
+  q.spec = alpha && spec ? (const int32_t*)d_spec.p : nullptr;
+  q.comp = (int)t->C;
   // fast path: layered reachability up to the largest window (a host-side
   // over-estimate; the kernel re-checks hi < layer_limit exactly), kept below
   // the reference's masked last column
-  if (t->closure && t->args.w_min > 0 && !exact_only) {
+  if (t->closure && t->args.w_min > 0 && !exact_only && !alpha) {
     double hmax = 0;
     for (int64_t i = 0; i < n; ++i) hmax = std::max(hmax, (su[i] + tol * std::fabs(obs[i])) / prec + 4.0);
     const int64_t safe = (t->n_cols - 1) * t->C;
@@ -2347,6 +2361,28 @@ int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, in
     if (status[i] == kStatusPending || status[i] == kStatusExactRetry)
       return fail(c, SST_E_INTERNAL, "length bound: query left unresolved (internal error)");
   return SST_OK;
+}
+
+}  // namespace
+extern "C" {
+
+int sst_length_bound_batch(sst_table* t, const double* su, const double* obs, int64_t n, double tol, double prec,
+                           int max_len, int64_t max_mods, int direction, int64_t* out, int8_t* status) {
+  return length_bound_batch(t, su, obs, n, tol, prec, max_len, max_mods, direction, out, status, nullptr, nullptr,
+                            0);
+}
+
+int sst_length_bound_alpha_batch(sst_table* t, const double* su, const double* obs, const int32_t* spec,
+                                 const uint64_t* alpha, int64_t n_alpha, int64_t n, double tol, double prec,
+                                 int max_len, int64_t max_mods, int direction, int64_t* out, int8_t* status) {
+  // "lower" only: a left child that is reachable in the full table but not with
+  // the kept rows returns the default (-1) there, and the reference's upper
+  // bound counts such a visited child as -1 + 1 = 0 where the rebuilt table
+  // would not visit it at all; the lower bound's default (max_len
+  // + 1) can never win a min, so its masked replay is exact
+  if (!alpha || n_alpha <= 0 || (direction & ~SST_LB_EXACT_ONLY) != 0) return SST_E_ARG;
+  return length_bound_batch(t, su, obs, n, tol, prec, max_len, max_mods, direction, out, status, spec, alpha,
+                            n_alpha);
 }
 
 }  // extern "C"

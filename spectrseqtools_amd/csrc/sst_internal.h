@@ -255,6 +255,11 @@ struct LBArgs {
   int n_layers;
   int64_t layer_limit;     // layers cover masses [0, layer_limit)
   uint64_t node_budget;
+  // per-query alphabets (sst_length_bound_alpha_batch): row masks alpha[2 g],
+  // [2 g + 1] over the table's rows, spec[i] = query i's; null: all rows
+  const uint64_t* alpha = nullptr;
+  const int32_t* spec = nullptr;
+  int comp = 32;
 };
 
 struct ExactWs {

@@ -700,6 +700,34 @@ __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s,
       continue;
     }
     if (child < 0) continue;
+    if (MODE == MODE_FAST && t.census && child < t.pair_hi && d + 3 <= Stack::depth) {
+      // at most 2 items remain (child < 3 w_min): the pair list's entries of sum
+      // == child are the subtree's leaves, sorted by (sum, top row) -- the
+      // DFS's order here (first row ascending, the second then fixed) -- read
+      // through L2 from the census instead of 2 random index-record fetches
+      const uint32_t c0 = t.pair_base - 1u, cc = (uint32_t)child;
+      const uint32_t lo_x = cc - 1u < c0 ? c0 : cc - 1u, hi_x = cc < c0 ? c0 : cc;
+      const uint32_t e0 = t.census[lo_x - c0] & 0xFFFFu, e1 = t.census[hi_x - c0] & 0xFFFFu;
+      const uint32_t* recs = t.pair_data + (t.n_pairs + 2);
+      for (uint32_t e = e0; e < e1; ++e) {
+        const uint32_t rec = recs[e];
+        const int n = (int)(rec & 0xFFu);
+        const int top = (int)((rec >> (n == 1 ? 8 : 16)) & 0xFFu), low = (int)((rec >> 8) & 0xFFu);
+        if (top > rr) break;
+        if (!mtest(am, top) || !mtest(am, low)) continue;  // a row outside the query's alphabet
+        for (int j = 0; j < n; ++j) {
+          const int dj = d + 1 + j, rj = j == 0 ? top : low;
+          if (dj < 8)
+            path.p0 = (path.p0 & ~(0xFFull << (8 * dj))) | ((uint64_t)rj << (8 * dj));
+          else
+            st.set_row(dj, rj);
+        }
+        sink.put(path, d + n, o.bytes);
+        o.bytes += (uint64_t)(d + n + 2);
+        o.count++;
+      }
+      continue;
+    }
     if (o.nodes >= node_budget) {
       o.fail = 2;
       return;
@@ -2775,8 +2803,18 @@ __global__ __launch_bounds__(256) void k_length_fast(TableArgs t, LBArgs q) {
     q.status[i] = SST_OUT_OF_TABLE;  // NotImplementedError (mass_table.py:383-387)
     return;
   }
+  if (q.alpha) {  // a reduced alphabet: its table's extent (as explain, §3), then the exact replay
+    const int64_t g = q.spec ? (int64_t)q.spec[i] : 0;
+    M128 am = mand(M128{q.alpha[2 * g], q.alpha[2 * g + 1]}, rows_upto(t.n_rows - 1));
+    const int top = am.b ? 127 - __builtin_clzll(am.b) : 63 - __builtin_clzll(am.a | 1ull);
+    const int64_t lim = ((int64_t)t.w[top] * 35 + q.comp) / q.comp * q.comp;
+    if (hi >= lim - q.comp) {
+      q.status[i] = hi >= lim ? (int8_t)SST_OUT_OF_TABLE : (int8_t)SST_ABORTED;
+      return;
+    }
+  }
   const int64_t a = lo < 0 ? 0 : lo;
-  const bool fast = q.layers && hi < q.layer_limit && budgets_never_bind(t, hi, q.A0);
+  const bool fast = !q.alpha && q.layers && hi < q.layer_limit && budgets_never_bind(t, hi, q.A0);
   if (!fast) {
     const uint32_t slot = atomicAdd(q.exact_count, 1u);
     q.exact_list[slot] = (uint32_t)i;
@@ -2832,7 +2870,12 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
     h.used = 0;
     uint64_t nodes = 0;
     const int64_t a = lo < 1 ? 1 : lo;
-    int rc = phase1<WAVE>(t, s, h, fr, a, hi, q.A0, q.node_budget, nodes);
+    M128 am{~0ull, ~0ull};
+    if (q.alpha) {
+      const int64_t g = q.spec ? (int64_t)q.spec[i] : 0;
+      am = M128{q.alpha[2 * g], q.alpha[2 * g + 1]};
+    }
+    int rc = phase1<WAVE>(t, s, h, fr, a, hi, q.A0, q.node_budget, nodes, am);
     if (rc == -1) {
       q.status[i] = (int8_t)kStatusExactRetry;
       continue;

@@ -134,3 +134,41 @@ def test_explain_alpha_full_mask_equals_plain_explain(setup):
     assert np.array_equal(res.status, ref.status)
     for i in range(len(mass)):
         assert res.candidates(i) == ref.candidates(i), i
+
+
+def test_length_bound_alpha_vs_rebuilt_tables(setup, direction="lower"):
+    """compute_sequence_length_bound(dir="lower") after the skeleton's
+    alphabet reduction (skeleton_building.py:212-224): sequence masses of
+    5..14-mers over each alphabet's rows, A = round(0.5 max_len) with binding
+    caps, on the masked full table against the oracle on the rebuilt table;
+    "upper" is refused (the reference's upper bound sees the visits the mask
+    adds)."""
+    rows, dev, is_mod, caps = setup
+    rng = np.random.default_rng(75)
+    alphas = _alphabets(rows, rng, 6)
+    masks = row_masks(np.array([[r in a for r in range(len(rows))] for a in alphas]))
+    su, spec = [], []
+    for g, a in enumerate(alphas):
+        w = np.array([rows[r] for r in a])
+        k = rng.integers(5, 15, 12)
+        su.append(np.array([w[rng.integers(0, len(w), kk)].sum() for kk in k]) * PREC + rng.normal(0, 0.002, 12))
+        spec.append(np.full(12, g, np.int32))
+    su, spec = np.concatenate(su), np.concatenate(spec)
+    obs = su + 912.303  # a START_END fragment's observed mass
+    max_len, A = 20, 10
+    out, st = dev.length_bound_alpha(su, obs, spec, masks, TOL, PREC, max_len, A, direction)
+    n_ok = 0
+    for i in range(len(su)):
+        full = [0] + alphas[spec[i]]
+        ms = [rows[r] for r in full]
+        tab = oracle.build_table(ms, max(ms) * 35, 32)
+        alph = oracle.Alphabet(ms, [is_mod[r] for r in full], [caps[r] for r in full])
+        want = oracle.length_bound(tab, 32, alph, su[i], obs[i], TOL, max_len, A, direction)
+        if want is None:
+            assert int(st[i]) != 0, i
+            continue
+        assert int(st[i]) == 0 and int(out[i]) == want, (i, int(st[i]), int(out[i]), want)
+        n_ok += 1
+    assert n_ok >= 60
+    with pytest.raises(_native.EngineError):  # "upper" needs the rebuilt table (include/sst.h)
+        dev.length_bound_alpha(su, obs, spec, masks, TOL, PREC, max_len, A, "upper")
