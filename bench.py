@@ -839,6 +839,14 @@ def main_config1(args, engine, dist, rank, world, dev_t):
         raise RuntimeError(f"pair-path partition {int(pair.sum())} != engine counter {int(stats[6])}")
     n_hit_def = int((some & ~pair).sum())
     bytes_def = float(n_def * 17 + 16 * nodes + int(stats[5]) + 16 * n_hit_def)
+    traffic, traffic_src = None, None  # PMC-derived HBM bytes per launch (tools/pmc_c1.sh -> profiles/traffic.json)
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        traffic = tj.get("k_explain_deferred_c1")
+        traffic_src = tj.get("_source", {}).get("k_explain_deferred_c1")
+    except (OSError, ValueError):
+        pass
     kern = {}
     for kid, (ms_, cnt) in prof.items():
         kern[_native.KERNEL_NAMES[kid]] = {"avg_us": 1e3 * ms_ / cnt, "launches": cnt}
@@ -866,8 +874,12 @@ def main_config1(args, engine, dist, rank, world, dev_t):
         "config": {"workload": "config1: whole masses of random canonical 1..8-mers (+ the reference test's 7 x 3), "
                                "canonical 5-row table, budget round(0.5 len) per query", "queries_per_gpu": n},
         "roofline": {"bound": "hbm", "kernel": "k_explain_deferred", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "algorithmic_bytes_per_launch": bytes_def, "avg_launch_us": dus},
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "traffic_source": traffic_src, "algorithmic_bytes_per_launch": bytes_def, "avg_launch_us": dus,
+                     "random_line_fetches_per_launch": nodes,
+                     "random_line_rate_note": "the DFS fetches one index record per node: "
+                                              f"{nodes / (dus * 1e-6) / 1e9:.1f} G fetches/s against the ~50 G/s "
+                                              "a dependent random chase reaches (profiles/r3_chase_probe.txt)"},
         "kernels": kern,
         "engine_stats": {"pair": int(stats[6]), "deep": int(stats[1]), "exact": int(stats[2]),
                          "nomemo": int(stats[3]), "index_loads": nodes, "candidates": int(res.count[some].sum()),
