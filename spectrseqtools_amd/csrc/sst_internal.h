@@ -338,6 +338,9 @@ hipError_t launch_valid_alpha(const AlphaArgs& a, int64_t n_spec, hipStream_t st
 constexpr int kRowsMaxPeaks = 1024;   // peaks per spectrum a workgroup holds
 constexpr int kRowsMaxSide = 2048;    // rows per side (two breakages per side at most ... x 2 headroom)
 constexpr int kRowsWaveMaxPeaks = 160;  // spectra up to this many peaks: one wave each (k_rows_*_w)
+// answer slots per peak and side of the rows step's count pass (config 3:
+// 10 queries per peak over both sides)
+constexpr int kRowsAnsPerPeak = 12;
 struct RowsArgs {
   const double* obs;          // [n_peaks] sorted within each spectrum
   const int64_t* peak_off;    // [n_spec + 1]
@@ -354,6 +357,13 @@ struct RowsArgs {
   double* rows_su;            // scratch [4 * n_peaks]
   double* rows_ob;
   uint32_t* side_rows;        // [2 n_spec]
+  // the wave kernels' answers, written once by the count pass: one u64 per
+  // query (status | count << 8 | first entry << 24 | record bytes << 40),
+  // side sd of spectrum g at kRowsAnsPerPeak * (2 peak_off[g] + sd * P_g)
+  // when its queries fit there (kRowsAnsPerPeak * P_g slots; else the emit
+  // pass answers that side again from its scratch rows)
+  uint64_t* ans;              // [2 kRowsAnsPerPeak n_peaks]
+  uint32_t* ans_q;            // [2 n_spec] the side's queries, ~0: did not fit
   uint32_t* totals;           // [3 n_spec] queries, hits, payload bytes
   unsigned long long* chunk_tot;  // [3 n_chunks] totals of each wave's contiguous chunk of spectra
   uint64_t* chunk_off;        // [3 n_chunks] their exclusive offsets (k_rows_scan)

@@ -27,12 +27,15 @@
 //
 // Launches: k_rows_count_w (one wave per contiguous chunk of spectra, each
 // spectrum of <= 160 peaks in turn; larger spectra are listed for
-// k_rows_count, one workgroup each): A7, rows to scratch, per-spectrum totals
-// of queries / hits / payload bytes and each chunk's sums; k_rows_scan: the
-// chunks' exclusive offsets (one workgroup over one value per wave);
-// k_rows_emit_w / k_rows_emit: each spectrum's offsets (its chunk's plus the
-// chunk's earlier spectra's totals), statuses, dense hit list with pair-list
-// refs, dense payload; the last workgroup writes the header.  The result is
+// k_rows_count, one workgroup each): A7, every window pair answered once
+// (8 B per query to scratch, the pass's one answer per pair), per-spectrum
+// totals of queries / hits / payload bytes and each chunk's sums;
+// k_rows_scan: the chunks' exclusive offsets (one workgroup over one value per
+// wave); k_rows_emit_w: each spectrum's offsets (its chunk's plus the chunk's
+// earlier spectra's totals), then its answers streamed back into statuses,
+// the dense hit list with pair-list refs and the dense payload;
+// k_rows_count / k_rows_emit do the same for the big spectra (rows to
+// scratch, answered in both passes); the last workgroup writes the header.  The result is
 // sst_result's dense layout in query order (spectrum-major; START pairs, then
 // END pairs).
 #include <hip/hip_runtime.h>
@@ -763,11 +766,20 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
       }
       if (sd) n1 = n;
       else n0 = n;
-      double* rs = a.rows_su + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
-      double* ro = a.rows_ob + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
-      for (uint32_t r = lane; r < n; r += 64) {
-        rs[r] = L.su[r];
-        ro[r] = L.ob[r];
+      // every pair is answered here, once: the emit pass reads the answers
+      // back in query order instead of re-forming and re-answering the pairs
+      // (the side's fixed slots; a side with more queries keeps its rows in
+      // scratch and is answered again by the emit pass)
+      const uint64_t base = (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P);
+      const bool fits = Q <= (uint32_t)kRowsAnsPerPeak * P;
+      if (lane == 0) a.ans_q[2 * g + sd] = fits ? Q : 0xFFFFFFFFu;
+      if (!fits) {
+        double* rs = a.rows_su + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
+        double* ro = a.rows_ob + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
+        for (uint32_t r = lane; r < n; r += 64) {
+          rs[r] = L.su[r];
+          ro[r] = L.ob[r];
+        }
       }
       for (uint32_t q = lane; q < Q; q += 64) {
         uint32_t s, e;
@@ -775,6 +787,9 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
         const QAns r = wave_answer(L, t, a, s, e);
         nh += (r.status == SST_SOME || r.status == SST_OVERFLOW);
         nb += r.status == SST_SOME ? r.bytes + 2u : 0u;
+        if (fits)
+          a.ans[base + q] = (uint64_t)(uint8_t)r.status | (uint64_t)(r.cnt & 0xFFFFu) << 8 |
+                            (uint64_t)(r.first & 0xFFFFu) << 24 | (uint64_t)r.bytes << 40;
       }
       nq += Q;
       wsync();
@@ -847,57 +862,69 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, R
     off[2] += a.totals[3 * g + 2];
     if (P > (uint32_t)kWP) continue;  // the workgroup kernel's
     for (int sd = 0; sd < 2; ++sd) {
+      uint32_t Q = a.ans_q[2 * g + sd];
+      const bool stored = Q != 0xFFFFFFFFu;  // the count pass's answers, in query order
+      const uint64_t base = (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P);
       const uint32_t n = a.side_rows[2 * g + sd];
-      const double* rs = a.rows_su + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
-      const double* ro = a.rows_ob + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
-      for (uint32_t r = lane; r < n; r += 64) {
-        L.su[r] = rs[r];
-        L.ob[r] = ro[r];
-      }
-      wsync();
-      // s* and the pair prefix (as in the count pass, from the stored rows)
-      uint32_t ss = n ? n - 1 : 0;
-      for (uint32_t r = lane; r + 1 < n; r += 64)
-        if (!(L.su[n - 1] - L.su[r] > a.max_weight)) ss = r < ss ? r : ss;
-      ss = wave_min(ss);
-      uint32_t carry = 0;
-      for (uint32_t r0 = 0; r0 < n; r0 += 64) {
-        const uint32_t r = r0 + lane;
-        uint32_t c = 0;
-        if (r + 1 < n) {
-          if (r < ss) {
-            uint32_t lo = r + 1, hi = n - 1;
-            const double sr = L.su[r];
-            while (lo < hi) {
-              const uint32_t mid = (lo + hi) >> 1;
-              if (L.su[mid] - sr > a.max_weight) hi = mid;
-              else lo = mid + 1;
-            }
-            c = lo - r - 1;
-          } else if (r == ss) {
-            c = n - 1 - r;
-          } else {
-            c = 1;
-          }
+      if (!stored) {  // too many queries for the side's slots: the rows back from scratch, answered again
+        const double* rs = a.rows_su + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
+        const double* ro = a.rows_ob + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
+        for (uint32_t r = lane; r < n; r += 64) {
+          L.su[r] = rs[r];
+          L.ob[r] = ro[r];
         }
-        uint32_t tot;
-        const uint32_t ex = wave_excl(c, tot);
-        if (r < n) L.qoff[r] = carry + ex;
-        carry += tot;
+        wsync();
+        uint32_t ss = n ? n - 1 : 0;
+        for (uint32_t r = lane; r + 1 < n; r += 64)
+          if (!(L.su[n - 1] - L.su[r] > a.max_weight)) ss = r < ss ? r : ss;
+        ss = wave_min(ss);
+        uint32_t carry = 0;
+        for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+          const uint32_t r = r0 + lane;
+          uint32_t c = 0;
+          if (r + 1 < n) {
+            if (r < ss) {
+              uint32_t lo = r + 1, hi = n - 1;
+              const double sr = L.su[r];
+              while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (L.su[mid] - sr > a.max_weight) hi = mid;
+                else lo = mid + 1;
+              }
+              c = lo - r - 1;
+            } else if (r == ss) {
+              c = n - 1 - r;
+            } else {
+              c = 1;
+            }
+          }
+          uint32_t tot;
+          const uint32_t ex = wave_excl(c, tot);
+          if (r < n) L.qoff[r] = carry + ex;
+          carry += tot;
+        }
+        if (lane == 0) {
+          L.qoff[n] = carry;
+          L.sstar = ss;
+        }
+        wsync();
+        Q = carry;
       }
-      if (lane == 0) {
-        L.qoff[n] = carry;
-        L.sstar = ss;
-      }
-      wsync();
-      const uint32_t Q = carry;
       for (uint32_t q0 = 0; q0 < Q; q0 += 64) {
         const uint32_t q = q0 + lane;
         QAns r{SST_NONE, 0, 0, 0};
         if (q < Q) {
-          uint32_t s, e;
-          wave_pair(L, n, q, s, e);
-          r = wave_answer(L, t, a, s, e);
+          if (stored) {
+            const uint64_t v = __builtin_nontemporal_load(&a.ans[base + q]);
+            r.status = (int8_t)(uint8_t)v;
+            r.cnt = (uint32_t)(v >> 8) & 0xFFFFu;
+            r.first = (uint32_t)(v >> 24) & 0xFFFFu;
+            r.bytes = (uint32_t)(v >> 40);
+          } else {
+            uint32_t s, e;
+            wave_pair(L, n, q, s, e);
+            r = wave_answer(L, t, a, s, e);
+          }
           a.status[qb + q] = r.status;
         }
         const bool hit = r.status == SST_SOME || r.status == SST_OVERFLOW;
