@@ -177,7 +177,9 @@ int sst_explain_batch_device(sst_table* t, const double* d_mass, const double* d
  * reference's last-column mask is not modelled).  Replaces a table rebuild +
  * explain_mass_with_table per alphabet (prediction.py:207 -> :216-227,
  * skeleton_building.py:212 -> :436).  Results, reuse and settling as for
- * sst_explain_batch_device; d_spec / d_alpha must stay valid until settled. */
+ * sst_explain_batch_device; every d_spec[i] must index d_alpha (device
+ * buffers are not range-checked), and d_spec / d_alpha must stay valid until
+ * the pass is settled. */
 int sst_explain_alpha_batch_device(sst_table* t, const double* d_mass, const double* d_thr, const int32_t* d_spec,
                                    const uint64_t* d_alpha, int64_t n, double tolerance, double precision,
                                    const int64_t* d_max_mods, int64_t max_mods_scalar, int with_memo,
