@@ -76,6 +76,19 @@ __device__ __forceinline__ M128 mclear(M128 x, int r) {
 }
 __device__ __forceinline__ bool mtest(M128 x, int r) { return r < 64 ? (x.a >> r) & 1ull : (x.b >> (r - 64)) & 1ull; }
 
+// tables of <= 64 rows (NW): every mask lives in .a; zeroing .b lets the
+// compiler drop the second word from the DFS loop's mask arithmetic
+template <bool NW>
+__device__ __forceinline__ M128 nrm(M128 x) {
+  if (NW) x.b = 0;
+  return x;
+}
+template <bool NW>
+__device__ __forceinline__ M128 rows_upto_nw(int r) {
+  if (NW) return M128{r >= 63 ? ~0ull : ((2ull << r) - 1ull), 0};
+  return rows_upto(r);
+}
+
 __device__ __forceinline__ int rec_lo(ulonglong2 rec) { return (int)(rec.y >> 56); }
 __device__ __forceinline__ M128 rec_L(ulonglong2 rec) { return {rec.x, rec.y & ((1ull << 56) - 1ull)}; }
 
@@ -640,7 +653,7 @@ struct PathView {
 // the deepest such ancestor with one stack read (a single-candidate window:
 // none at all), instead of reading back every level on the way up; each
 // descent costs one dependent load (the child's index record).
-template <int MODE, typename Stack, typename Sink>
+template <int MODE, bool NW = false, typename Stack, typename Sink>
 __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, uint32_t v, int A0,
                                Sink& sink, uint64_t node_budget, EnumOut& o, M128 am) {
   const int top_row = t.n_rows - 1;
@@ -652,7 +665,7 @@ __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s,
   } else {
     ulonglong2 rec = ld_index(t.index, v);
     o.nodes++;
-    k = mand(mand(rec_L(rec), rows_upto(top_row)), am);
+    k = nrm<NW>(mand(mand(rec_L(rec), rows_upto_nw<NW>(top_row)), am));
   }
   uint32_t m = v;
   int A = A0, B = s.cap[top_row], top = top_row;  // budgets: MODE_NOMEMO only
@@ -673,7 +686,7 @@ __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s,
         pend0 &= ~(1ull << d);
       }
       m = st.m(d);
-      k = st.mask(d);
+      k = nrm<NW>(st.mask(d));
       if (MODE == MODE_NOMEMO) {
         A = st.A(d);
         B = st.B(d);
@@ -744,7 +757,7 @@ __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s,
       ulonglong2 rec = ld_index(t.index, child);
       o.nodes++;
       if (rec_lo(rec) > rr) continue;
-      kc = mand(mand(rec_L(rec), rows_upto(rr)), am);
+      kc = nrm<NW>(mand(mand(rec_L(rec), rows_upto_nw<NW>(rr)), am));
     }
     if (d + 1 >= Stack::depth) {
       o.fail = 1;
@@ -771,7 +784,7 @@ __device__ __forceinline__ void enumerate_root(const TableArgs& t, const Lds& s,
 }
 
 // payload bytes/counts of a whole window [a, b] of roots
-template <int MODE, typename Stack, typename Sink>
+template <int MODE, bool NW = false, typename Stack, typename Sink>
 __device__ __forceinline__ void enumerate_window(const TableArgs& t, const Lds& s, Stack& st, const Hash* h, int64_t a, int64_t b,
                                  int A0, Sink& sink, uint64_t node_budget, EnumOut& o,
                                  M128 am = M128{~0ull, ~0ull}) {
@@ -785,7 +798,7 @@ __device__ __forceinline__ void enumerate_window(const TableArgs& t, const Lds& 
       int bit = __builtin_ctzll(x);
       x &= x - 1;
       uint32_t v = (uint32_t)((wi << 6) + bit);
-      enumerate_root<MODE>(t, s, st, h, v, A0, sink, node_budget, o, am);
+      enumerate_root<MODE, NW>(t, s, st, h, v, A0, sink, node_budget, o, am);
       if (o.fail) return;
     }
   }
@@ -2382,7 +2395,7 @@ __device__ __forceinline__ int8_t alpha_extent_status(const TableArgs& t, const 
 
 // Deferred fast/no-memo queries with deep stacks: persistent grid, one lane per
 // query, stack in a per-lane slice of the workspace.
-template <int MODE>
+template <int MODE, bool NW = false>
 __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs& out, int cls, GlobFrame* ws, Lds& s,
                           int blk, int nblk) {
   DIAG_T(0);
@@ -2418,7 +2431,7 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
       const int8_t ext = alpha_extent_status(t, q, s, am, b);
       if (ext != SST_NONE) a = 1, b = 0;  // nothing to enumerate
       DIAG_T(2);
-      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, rs, q.node_budget, eo, am);
+      enumerate_window<MODE, NW>(t, s, st, nullptr, a, b, A0, rs, q.node_budget, eo, am);
       status = eo.count ? SST_SOME : (has_zero ? SST_EMPTY : SST_NONE);
       bytes = eo.bytes;
       if (ext != SST_NONE) {
@@ -2447,7 +2460,7 @@ __device__ void deep_body(const TableArgs& t, const QueryArgs& q, const OutArgs&
     } else if (to.bytes) {  // more than 32 bytes: enumerate again straight into the arena
       MemSink ms{out.payload + to.off, ~0ull};
       EnumOut e2{0, 0, 0, 0};
-      enumerate_window<MODE>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2, am);
+      enumerate_window<MODE, NW>(t, s, st, nullptr, a, b, A0, ms, ~0ull, e2, am);
     }
     emit_result_wg(out, live, (uint32_t)i, to.status, eo.count, to.off);
     DIAG_T(5);
@@ -2570,8 +2583,12 @@ __global__ __launch_bounds__(kDefWG) void k_explain_deferred(TableArgs t, QueryA
   }
   b -= shallow_blocks;
   if (out.dbg & 2) return;  // DIAGNOSTIC 2: no deep / exact roles
-  if (b < deep_blocks)
-    deep_body<MODE_FAST>(t, q, out, kClassDeep, ws_deep, s, b, deep_blocks);
+  if (b < deep_blocks) {
+    if (t.n_rows <= 64)  // the canonical and most reduced tables: one mask word
+      deep_body<MODE_FAST, true>(t, q, out, kClassDeep, ws_deep, s, b, deep_blocks);
+    else
+      deep_body<MODE_FAST>(t, q, out, kClassDeep, ws_deep, s, b, deep_blocks);
+  }
   else if (b < 2 * deep_blocks)  // second half of the deep workspace
     deep_body<MODE_NOMEMO>(t, q, out, kClassNomemo, ws_deep + (size_t)deep_blocks * kDefWG * kMaxDepth, s,
                            b - deep_blocks, deep_blocks);
