@@ -533,7 +533,19 @@ int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_
 #define SST_K_EXPLAIN_EXACT 4  /* reserved (merged into SST_K_EXPLAIN_DEFERRED) */
 #define SST_K_EXPLAIN_EXPAND 5
 #define SST_K_RESULT_PACK 6 /* k_result_pack: dense hit list + payload of a pass */
-#define SST_K_COUNT 8
+/* config 5 (the device-resident pipeline stages) */
+#define SST_K_CLASSIFY_ROWS 7 /* k_classify_rows (sst_classify_rows_device) */
+#define SST_K_FIX_ROUND 8     /* k_fix_round (sst_fix_round_device) */
+#define SST_K_VALID_ALPHA 9   /* k_valid_alpha (sst_valid_rows_alpha_device, sst_is_valid_alpha*) */
+#define SST_K_BINS_COUNT 10   /* k_bins_count + k_scan_u32 (sst_bins_count_device) */
+#define SST_K_BINS_EMIT 11    /* k_bins_emit (sst_bins_emit_device) */
+#define SST_K_DICT 12         /* k_dict_count / k_dict_build (sst_dict_final_device) */
+#define SST_K_SKEL_WALK 13    /* k_skel_walk (sst_skeleton_walk_device) */
+#define SST_K_REACH_ROWS 14   /* k_reach_rows (sst_reach_rows_device) */
+#define SST_K_LENGTH_BOUND 15 /* k_length_fast / k_length_exact (length-bound batches) */
+#define SST_K_JACCARD 16      /* k_jaccard (sst_jaccard_device) */
+#define SST_K_PAIRS_ALPHA 17  /* k_pairs_alpha (sst_explain_pairs_alpha*) */
+#define SST_K_COUNT 24
 /* When enabled, every kernel launch of this ctx is bracketed by hipEvents
  * recorded on the ctx stream; sst_profile_read synchronises and returns the
  * summed milliseconds and launch counts per kernel id since the last read

@@ -38,9 +38,16 @@ EXPORTS = (
 # kernel ids of sst_profile_read
 K_IS_VALID, K_EXPLAIN_SCAN, K_EXPLAIN_DEEP, K_EXPLAIN_NOMEMO, K_EXPLAIN_EXACT, K_EXPLAIN_EXPAND = 0, 1, 2, 3, 4, 5
 K_RESULT_PACK = 6
+(K_CLASSIFY_ROWS, K_FIX_ROUND, K_VALID_ALPHA, K_BINS_COUNT, K_BINS_EMIT, K_DICT, K_SKEL_WALK, K_REACH_ROWS,
+ K_LENGTH_BOUND, K_JACCARD, K_PAIRS_ALPHA) = range(7, 18)
+K_COUNT = 24  # SST_K_COUNT
 KERNEL_NAMES = {K_IS_VALID: "k_is_valid", K_EXPLAIN_SCAN: "k_explain_scan", K_EXPLAIN_DEEP: "k_explain_deferred",
                 K_EXPLAIN_EXPAND: "k_explain_expand",
-                K_RESULT_PACK: "k_result_pack"}  # ids 3, 4: reserved (merged into the deferred launch)
+                K_RESULT_PACK: "k_result_pack",  # ids 3, 4: reserved (merged into the deferred launch)
+                K_CLASSIFY_ROWS: "k_classify_rows", K_FIX_ROUND: "k_fix_round", K_VALID_ALPHA: "k_valid_alpha",
+                K_BINS_COUNT: "k_bins_count", K_BINS_EMIT: "k_bins_emit", K_DICT: "k_dict_build",
+                K_SKEL_WALK: "k_skel_walk", K_REACH_ROWS: "k_reach_rows", K_LENGTH_BOUND: "k_length_bound",
+                K_JACCARD: "k_jaccard", K_PAIRS_ALPHA: "k_pairs_alpha"}
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -320,10 +327,10 @@ class Engine:
 
     def profile_read(self):
         """{kernel id: (total ms, launches)} since the last read."""
-        ms = np.zeros(8, np.float64)
-        n = np.zeros(8, np.int64)
+        ms = np.zeros(K_COUNT, np.float64)
+        n = np.zeros(K_COUNT, np.int64)
         self.check(self._lib.sst_profile_read(self.handle, _ptr(ms), _ptr(n)), "sst_profile_read")
-        return {k: (float(ms[k]), int(n[k])) for k in range(8) if n[k]}
+        return {k: (float(ms[k]), int(n[k])) for k in range(K_COUNT) if n[k]}
 
     def close(self):
         if self.handle:

@@ -1675,6 +1675,7 @@ int sst_result_hit_list(sst_result* r, void** d_hits, uint64_t* n_hits) {
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
   if (int rc = settle(r)) return rc;
+  if (int rc = order_after_settle(r)) return rc;  // settling's extra launches wrote these buffers
   *d_hits = r->hits.p;
   *n_hits = r->n_hits;
   return SST_OK;
@@ -1686,6 +1687,7 @@ int sst_result_pair_hits(sst_result* r, void** d_refs, uint64_t* n_pair_hits, ui
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
   if (int rc = settle(r)) return rc;
+  if (int rc = order_after_settle(r)) return rc;
   if (d_refs) *d_refs = r->refs.p;
   if (n_pair_hits) *n_pair_hits = r->scan_hits;
   if (pair_bytes) *pair_bytes = r->scan_bytes;
@@ -1948,6 +1950,7 @@ int sst_explain_pairs_alpha_device(sst_table* t, const double* d_mass, const dou
   if (int rc = check_masks(t)) return rc;
   if (!t->args.pairs_enabled) return fail(c, SST_E_ARG, "pairs on reduced alphabets: the table has no pair list");
   PairAlphaArgs a{d_mass, d_thr, d_spec, d_masks, n, tol, prec, 1.0 / prec, d_status, d_count, d_rowmask, d_range};
+  Prof p(c, SST_K_PAIRS_ALPHA);
   HIP_OK(c, launch_pairs_alpha(t->args, a, c->stream));
   return SST_OK;
 }
@@ -2016,6 +2019,7 @@ int sst_is_valid_alpha_device(sst_table* t, const double* d_mass, const double* 
   a.rprec = 1.0 / prec;
   a.out = d_out;
   if (int rc = canon_closure(t, a)) return rc;
+  Prof p(c, SST_K_VALID_ALPHA);
   HIP_OK(c, launch_valid_alpha(a, n_spec, c->stream));
   return SST_OK;
 }
@@ -2082,7 +2086,7 @@ int sst_classify_rows_device(sst_table* t, const double* d_obs, const int64_t* d
   a.alive = d_alive;
   a.cnt = d_rows;
   a.err = d_err;
-  Prof p(c, SST_K_IS_VALID);
+  Prof p(c, SST_K_CLASSIFY_ROWS);
   HIP_OK(c, launch_classify_rows(t->args, a, c->n_cu, c->stream));
   return SST_OK;
 }
@@ -2119,7 +2123,7 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
   a.n_active = d_n_active;
   a.err = d_err;
   if (n_spec > 0) HIP_OK(c, hipMemsetAsync(d_n_active, 0, sizeof(uint32_t), c->stream));  // this round's count
-  Prof p(c, SST_K_EXPLAIN_MAIN);
+  Prof p(c, SST_K_FIX_ROUND);
   HIP_OK(c, launch_fix_round(t->args, a, c->n_cu, c->stream));
   return SST_OK;
 }
@@ -2159,7 +2163,7 @@ int sst_bins_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spe
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
-  Prof p(c, SST_K_IS_VALID);
+  Prof p(c, SST_K_BINS_COUNT);
   HIP_OK(c, launch_bins_count(a, c->n_cu, c->stream));
   return SST_OK;
 }
@@ -2188,7 +2192,7 @@ int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
   if (int rc = check_masks(t)) return rc;
-  Prof p(c, SST_K_EXPLAIN_MAIN);
+  Prof p(c, SST_K_BINS_EMIT);
   HIP_OK(c, launch_bins_emit(t->args, a, c->n_cu, c->stream));
   return SST_OK;
 }
@@ -2218,7 +2222,7 @@ int sst_valid_rows_alpha_device(sst_table* t, const int64_t* d_peak_off, int64_t
   a.prec = prec;
   a.rprec = 1.0 / prec;
   if (int rc = canon_closure(t, a)) return rc;
-  Prof p(c, SST_K_IS_VALID);
+  Prof p(c, SST_K_VALID_ALPHA);
   HIP_OK(c, launch_valid_alpha(a, n_spec, c->stream));
   return SST_OK;
 }
@@ -2328,7 +2332,10 @@ static int length_bound_batch(sst_table* t, const double* su, const double* obs,
   // fast kernel (queues the rest), then the exact kernel; retried with a
   // larger per-lane memo while any query reports hash exhaustion
   uint32_t n_exact = 0;
-  HIP_OK(c, launch_length_bound(t->args, q, nullptr, nullptr, nullptr, 0, 0, true, c->stream));
+  {
+    Prof p(c, SST_K_LENGTH_BOUND);
+    HIP_OK(c, launch_length_bound(t->args, q, nullptr, nullptr, nullptr, 0, 0, true, c->stream));
+  }
   HIP_OK(c, hipMemcpyAsync(&n_exact, d_cnt.p, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   std::vector<int8_t> st(nn);
@@ -2344,6 +2351,7 @@ static int length_bound_batch(sst_table* t, const double* su, const double* obs,
           !frames.ensure((size_t)units * lb_frame_bytes()))
         return fail(c, SST_E_NOMEM, "device allocation failed (length-bound memo)");
       HIP_OK(c, hipMemsetAsync(hash.p, 0, hash.bytes, c->stream));
+      Prof p(c, SST_K_LENGTH_BOUND);
       HIP_OK(c, launch_length_bound(t->args, q, (char*)hash.p, (int8_t*)vals.p, (char*)frames.p, cap, units, false,
                                     c->stream));
       HIP_OK(c, hipMemcpyAsync(st.data(), d_st.p, nn, hipMemcpyDeviceToHost, c->stream));

@@ -1924,6 +1924,16 @@ __global__ __launch_bounds__(kScanWG, 8) void k_step(TableArgs t, QueryArgs q, O
   explain_scan_wg<THR, MODS>(t, q, out, blockIdx.x, n_scan);
 }
 
+// the extent ceil((max(kept) * 35 + 1) / C) * C of query i's reduced table
+// (per-query alphabets; the top kept row below the table's row count)
+__device__ __forceinline__ int64_t reduced_limit(const TableArgs& t, const QueryArgs& q, int64_t i) {
+  const int64_t g = q.spec ? (int64_t)q.spec[i] : 0;
+  const M128 am = mand(M128{q.alpha[2 * g], q.alpha[2 * g + 1]}, rows_upto(t.n_rows - 1));
+  const int top = am.b ? 127 - __builtin_clzll(am.b) : 63 - __builtin_clzll(am.a | 1ull);
+  const int64_t max_mass = (int64_t)t.w[top] * 35;
+  return (max_mass + q.comp) / q.comp * q.comp;
+}
+
 // Tables without the pair list (uploaded tables, literal-sweep rows): every
 // non-empty window is checked against the valid bitset here, then queued for
 // the expand kernel (<= 3 items) or the deferred class lists.
@@ -1949,7 +1959,12 @@ __global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryAr
       if (q.max_mods) mm = q.max_mods[i];
     }
     const bool nonempty = live && lof <= hif;
-    const bool oot = nonempty && !(hif < (double)t.limit);  // mass_explanation.py:134-138 (NameError)
+    // the table's extent; with a per-query alphabet, its reduced table's
+    // (max(kept) * 35, mass_table.py:114-117): every window value at or past
+    // it raises, reachable or not (mass_explanation.py:134-138, NameError)
+    double limf = (double)t.limit;
+    if (q.alpha && live) limf = fmin(limf, (double)reduced_limit(t, q, i));
+    const bool oot = nonempty && !(hif < limf);
     const bool zero = nonempty && !oot && lof <= 0.0 && hif >= 0.0;  // v == 0 -> [[]] (:130-131)
     const double af = lof < 1.0 ? 1.0 : lof;
     const bool active = nonempty && !oot && af <= hif;

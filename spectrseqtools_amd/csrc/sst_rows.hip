@@ -39,6 +39,7 @@
 // sst_result's dense layout in query order (spectrum-major; START pairs, then
 // END pairs).
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <stdint.h>
 
 #include "sst_internal.h"
@@ -966,15 +967,27 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
   const size_t wdyn = dyn;
 #endif
   // 4-wave workgroups, as many as are resident (each wave a contiguous chunk of spectra)
-  static int occ = 0;
-  static size_t occ_dyn = ~(size_t)0;
-  if (occ_dyn != wdyn) {
+  // (the occupancy of the two wave kernels: with no dynamic LDS a per-process
+  // constant, computed once -- contexts on other threads see the finished
+  // value, never a torn one; the pair-image variant asks every time)
+  auto occupancy = [](size_t d, int* out) {
     int c1 = 0, c2 = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c1, k_rows_count_w, 64 * kWavesPerWG, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&c2, k_rows_emit_w, 64 * kWavesPerWG, wdyn) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&c2, k_rows_emit_w, 64 * kWavesPerWG, d) != hipSuccess)
       return hipErrorLaunchFailure;
-    occ = c1 < c2 ? c1 : c2;
-    occ_dyn = wdyn;
+    *out = c1 < c2 ? c1 : c2;
+    return hipSuccess;
+  };
+  static std::once_flag occ_once;
+  static int occ0 = 0;
+  static hipError_t occ0_err = hipSuccess;
+  int occ = 0;
+  if (wdyn == 0) {
+    std::call_once(occ_once, [&] { occ0_err = occupancy(0, &occ0); });
+    if (occ0_err != hipSuccess) return occ0_err;
+    occ = occ0;
+  } else if (hipError_t e = occupancy(wdyn, &occ); e != hipSuccess) {
+    return e;
   }
   const int wave_wg = n_wg * (occ > 0 ? occ : 1);
   // contiguous chunks of spectra, one per wave of the wave kernels' grid

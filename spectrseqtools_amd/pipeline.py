@@ -237,7 +237,7 @@ class Fixpoint:
     queries: list = None     # per round: (explain queries, is_valid queries)
 
 
-def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolerance=MATCHING_THRESHOLD,
+def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolerance=None,
                     record=False):
     """Predictor.filter_by_explanation (prediction.py:170-202) for every
     spectrum of `c` at once.  dp_table: the full alphabet's table (its rows
@@ -253,6 +253,7 @@ def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolera
     or a singleton's mass); budgets cannot bind once max_modifications and the
     modification rows' caps are >= 2, which is checked (smaller budgets raise
     NotImplementedError: the per-spectrum mirror handles them)."""
+    tolerance = dp_table.tolerance if tolerance is None else tolerance  # prediction.py:219, :280, :315
     dev = dp_table.device_table
     masses = dp_table.masses
     N = len(masses)

@@ -17,7 +17,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _native
-from .masses import MATCHING_THRESHOLD, PHOSPHATE_LINK_MASS
+from .masses import PHOSPHATE_LINK_MASS
 from .pipeline import mask_rows, row_masks
 
 ERR_BITS = {1: "a spectrum has more than 1024 peaks", 2: "a spectrum has more than 2048 rows",
@@ -101,11 +101,12 @@ class DeviceFixpoint:
     n_rounds: int
 
 
-def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=MATCHING_THRESHOLD, record=False):
+def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=None, record=False):
     """Stage 2 on the device: Predictor.filter_by_explanation (prediction.py:
     170-202) for every spectrum, one sst_fix_round_device + one
     sst_valid_rows_alpha_device launch per round, until no alphabet shrinks.
     max_len[s] bounds the budgets (checked as in pipeline.filter_fixpoint)."""
+    tolerance = dp_table.tolerance if tolerance is None else tolerance  # prediction.py:219, :280, :315
     import torch
 
     masses = dp_table.masses
@@ -199,7 +200,7 @@ class DeviceBins:
     deferred: dict = None  # the off-pair-class queries' masked explain: n, per max_len group results, tallies
 
 
-def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=MATCHING_THRESHOLD, max_len=None):
+def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=None, max_len=None):
     """Stage 3 on the device (SkeletonBuilder._predict_skeleton's bins,
     skeleton_building.py:114-160) over the rows the fixpoint kept
     (rows.alive) and the final alphabets `alpha` ([S, 2] u64 row masks).
@@ -209,6 +210,7 @@ def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=MATCHING_THRESHOLD,
     (sst_explain_alpha_batch_device, the DFS roles on each spectrum's
     alphabet), one pass per max_len group (its budgets: round(0.5 max_len),
     caps round(max_len * rate), common.py:55, mass_explanation.py:158-172)."""
+    tolerance = dp_table.tolerance if tolerance is None else tolerance  # prediction.py:219, :280, :315
     import torch
 
     S = len(rows.rows)

@@ -172,3 +172,39 @@ def test_length_bound_alpha_vs_rebuilt_tables(setup, direction="lower"):
     assert n_ok >= 60
     with pytest.raises(_native.EngineError):  # "upper" needs the rebuilt table (include/sst.h)
         dev.length_bound_alpha(su, obs, spec, masks, TOL, PREC, max_len, A, "upper")
+
+
+def test_explain_alpha_rootless_window_past_reduced_extent():
+    """A window at or past the REDUCED table's extent raises in the reference
+    (mass_explanation.py:133-138) whether or not any of its values is
+    reachable; on a table without the pair list (an uploaded table: the
+    bitset scan answers rootless windows itself) such a window must still be
+    SST_OUT_OF_TABLE, as the oracle on the rebuilt table says."""
+    eng = _native.get_engine(0)
+    ms = [0, 1000, 1500, 2200]
+    words = oracle.build_table(ms, max(ms) * 35, 32)
+    dev = _native.DeviceTable.upload(ms, words, 32, engine=eng)
+    dev.set_budgets([False, False, False, False], [0, 20, 20, 20])
+    kept = [0, 1, 2]  # max(kept) * 35 = 52500 < the full table's 77000
+    red = [ms[r] for r in kept]
+    red_tab = oracle.build_table(red, max(red) * 35, 32)
+    alph = oracle.Alphabet(red, [False] * 3, [0, 20, 20])
+    masks = row_masks(np.array([[r in kept for r in range(len(ms))]]))
+    # rootless (no sum of 1000/1500/2200 ends in ...01..03) in the reduced table's last word,
+    # past its extent, and a reachable control below it
+    mass = np.array([60.002, 52.530, 70.0015, 45.000, 52.499])
+    thr = np.array([0.001, 0.0005, 0.0005, 0.001, 0.0004])
+    res = dev.explain_alpha(mass, thr, np.zeros(len(mass), np.int32), masks, TOL, PREC, -1)
+    n_oot = 0
+    for i in range(len(mass)):
+        st, sols, n_e, _ = oracle.explain_table(red_tab, 32, alph, mass[i], thr[i], TOL, -1)
+        if st < 0:
+            assert int(res.status[i]) == _native.SST_OUT_OF_TABLE, (i, int(res.status[i]))
+            n_oot += 1
+        else:
+            want = [tuple(kept[x] for x in t) for t in sols]
+            want_st = _native.SST_SOME if want else (_native.SST_EMPTY if n_e else _native.SST_NONE)
+            assert int(res.status[i]) in (want_st, _native.SST_ABORTED), (i, int(res.status[i]), want_st)
+            if int(res.status[i]) == want_st == _native.SST_SOME:
+                assert res.candidates(i) == want
+    assert n_oot >= 2
