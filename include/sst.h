@@ -523,6 +523,18 @@ int64_t sst_dict_union(const int64_t* offsets, int64_t n_spec, const double* key
  * spectra (numpy.lexsort((rows, key, group))). */
 int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_groups, int64_t* order);
 
+/* ---- CPython set order (the skeleton walk's emulation, sst_pyset.h) ---- */
+/* hash(tuple) of a tuple whose items hash to item_hashes[0..n) (CPython
+ * 3.8+ tuplehash, 64-bit): the hash of an explanation's name tuple
+ * (mass_explanation.py:302-318) from the names' str hashes. */
+int64_t sst_py_tuple_hash(const int64_t* item_hashes, int64_t n);
+/* The iteration order of a set built by adding elements keys[0..n) (distinct
+ * keys = distinct elements, hashes[i] = hash(element i)) in that order to an
+ * empty set (CPython 3.7-3.12 setobject.c): order[0..m) receives the keys in
+ * iteration order; returns m (the distinct elements) or SST_E*.  Host code:
+ * it exists so that tests can pin the walk's emulation to the interpreter. */
+int64_t sst_pyset_order(const int32_t* keys, const int64_t* hashes, int64_t n, int32_t* order);
+
 /* ---- measurement ------------------------------------------------------ */
 /* Kernel ids for sst_profile_read. */
 #define SST_K_IS_VALID 0

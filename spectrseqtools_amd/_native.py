@@ -33,6 +33,7 @@ EXPORTS = (
     "sst_is_valid_alpha_device", "sst_dict_union", "sst_step_rows_device", "sst_result_queries",
     "sst_classify_rows_device", "sst_fix_round_device", "sst_valid_rows_alpha_device",
     "sst_bins_count_device", "sst_bins_emit_device", "sst_length_bound_alpha_batch",
+    "sst_py_tuple_hash", "sst_pyset_order",
 )
 
 # kernel ids of sst_profile_read
@@ -142,6 +143,10 @@ def load_library(path=LIB_PATH):
     lib.sst_wire_pack.restype = _I64
     lib.sst_su_diff_queries.argtypes = [_P, _P, _P, _P, _I64, _D, _D, _P, _P, _P, _P, _I64]
     lib.sst_su_diff_queries.restype = _I64
+    lib.sst_py_tuple_hash.argtypes = [_P, _I64]
+    lib.sst_py_tuple_hash.restype = _I64
+    lib.sst_pyset_order.argtypes = [_P, _P, _I64, _P]
+    lib.sst_pyset_order.restype = _I64
     lib.sst_sort_rows.argtypes = [_P, _P, _I64, _I64, _P]
     lib.sst_sort_rows.restype = _I
     lib.sst_step_device.argtypes = [_P, _P, _I64, _P, _I, _P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
@@ -230,6 +235,24 @@ def dict_union(offsets, key, kind, status, rowmask):
     if rc < 0:
         raise EngineError(f"sst_dict_union failed ({rc})")
     return keep.astype(bool), union
+
+
+def py_tuple_hash(item_hashes):
+    """sst_py_tuple_hash: hash(tuple) from its items' hashes (host code)."""
+    h = np.ascontiguousarray(item_hashes, dtype=np.int64)
+    return int(lib().sst_py_tuple_hash(_ptr(h), len(h)))
+
+
+def pyset_order(keys, hashes):
+    """sst_pyset_order: the iteration order of a set built by adding the
+    elements `keys` (hashes `hashes`) in order (host code)."""
+    k = np.ascontiguousarray(keys, dtype=np.int32)
+    h = np.ascontiguousarray(hashes, dtype=np.int64)
+    out = np.empty(len(k), np.int32)
+    m = lib().sst_pyset_order(_ptr(k), _ptr(h), len(k), _ptr(out))
+    if m < 0:
+        raise EngineError(f"sst_pyset_order failed ({m})")
+    return out[:m].tolist()
 
 
 def sort_rows(group, key, n_groups):

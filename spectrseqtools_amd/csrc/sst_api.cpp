@@ -22,6 +22,7 @@
 
 #include "sst.h"
 #include "sst_internal.h"
+#include "sst_pyset.h"
 
 using namespace sst;
 
@@ -2598,4 +2599,29 @@ int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_
     for (auto& x : th) x.join();
   }
   return SST_OK;
+}
+
+// ---- CPython set order (sst_pyset.h), for the skeleton walk's tests -------
+extern "C" int64_t sst_py_tuple_hash(const int64_t* item_hashes, int64_t n) {
+  uint64_t acc = sst::pyset::tuple_hash_init();
+  for (int64_t i = 0; i < n; ++i) acc = (uint64_t)sst::pyset::tuple_hash_step(acc, item_hashes[i]);
+  return sst::pyset::tuple_hash_final(acc, n);
+}
+
+extern "C" int64_t sst_pyset_order(const int32_t* keys, const int64_t* hashes, int64_t n, int32_t* order) {
+  if (n < 0 || n > (1 << 24) || (n > 0 && (!keys || !hashes || !order))) return SST_E_ARG;
+  const uint32_t cap = sst::pyset::table_size_for((uint32_t)n);
+  std::vector<int32_t> k0(cap), k1(cap);
+  std::vector<int64_t> h0(cap), h1(cap);
+  sst::pyset::Table t{{k0.data(), k1.data()}, {h0.data(), h1.data()}, cap, 0, 0, 0, false};
+  sst::pyset::clear(t);
+  for (int64_t i = 0; i < n; ++i) {
+    if (keys[i] < 0) return SST_E_ARG;
+    sst::pyset::add(t, keys[i], hashes[i]);
+  }
+  if (t.overflow) return SST_E_ARG;
+  int64_t m = 0;
+  for (uint32_t s = 0; s <= t.mask; ++s)
+    if (t.key[t.cur][s] >= 0) order[m++] = t.key[t.cur][s];
+  return m;
 }

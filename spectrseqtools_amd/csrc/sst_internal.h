@@ -416,6 +416,7 @@ struct PipeArgs {
   uint32_t* n_active;         // spectra whose alphabet shrank this round
   uint64_t canon[2];          // the canonical rows (never dropped)
   uint32_t* n_q;              // [n_spec] skeleton bin queries (k_bins count pass)
+  uint32_t* n_q0;             // may be null: [n_spec] of those, the START side's
   uint64_t* q_off;            // [n_spec + 1] their exclusive offsets (total last)
   int8_t* q_status;           // [total] per bin query: SST_NONE / EMPTY / SOME, kStatusPending off the pair class
   uint32_t* q_count;          // [total] candidates on the spectrum's alphabet
@@ -428,6 +429,23 @@ struct PipeArgs {
   uint32_t* n_def;
   uint32_t* err;
 };
+// filter_by_explanation's final explanation dict per spectrum (sst_pipe.hip,
+// k_dict): the dict the last round built (prediction.py:261-329: a side pair
+// is stored only with >= 1 explanation, a singleton always, a later equal key
+// replaces an earlier one) over the final alive rows and alphabet.  The
+// skeleton walk looks its bin differences up in it (skeleton_building.py:
+// 429-430) -- a hit answers with the dict's value, i.e. the same window at
+// the last writer's threshold.
+struct DictArgs {
+  uint32_t* n_q;         // count pass: [n_spec] the final round's queries (>= its entries)
+  const uint64_t* off;   // build pass: [n_spec + 1] region offsets (exclusive scan of n_q)
+  uint64_t* key;         // [total] keys ascending (double bits, -0.0 folded into 0.0)
+  double* thr;           // [total] the last writer's threshold
+  uint32_t* n_ent;       // [n_spec] entries
+};
+hipError_t launch_dict(const TableArgs& t, const PipeArgs& a, const DictArgs& d, bool count_only, int n_wg,
+                       hipStream_t st);
+hipError_t launch_scan_u32(const uint32_t* in, uint64_t* out, int64_t n, hipStream_t st);
 hipError_t launch_bins_count(const PipeArgs& a, int n_wg, hipStream_t st);
 hipError_t launch_bins_emit(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st);
 hipError_t launch_classify_rows(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st);

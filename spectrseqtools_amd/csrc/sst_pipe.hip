@@ -436,6 +436,110 @@ __global__ __launch_bounds__(kPipeWG) void k_fix_round(TableArgs t, PipeArgs a) 
   }
 }
 
+// filter_by_explanation's final dict (DictArgs): the last round's queries
+// over the final alive rows, answered on the final alphabet; count pass: the
+// query count per spectrum; build pass: the last writer per key (LDS hash, as
+// k_fix_round), then the entries sorted by key into the spectrum's region.
+__global__ __launch_bounds__(kPipeWG) void k_dict(TableArgs t, PipeArgs a, DictArgs d, int count_only) {
+  __shared__ FixLds L;
+  __shared__ uint32_t ent[kHashSlots];
+  __shared__ uint32_t n_ent;
+  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
+    const int64_t base = 4 * a.peak_off[g];
+    const uint32_t nr = a.cnt[g];
+    if (nr > (uint32_t)kPipeMaxRows) {
+      if (threadIdx.x == 0) {
+        atomicOr(a.err, 2u);
+        if (count_only) d.n_q[g] = 0;
+        else d.n_ent[g] = 0;
+      }
+      continue;
+    }
+    uint32_t carry[4] = {0, 0, 0, 0};
+    for (uint32_t r0 = 0; r0 < nr; r0 += blockDim.x) {
+      const uint32_t r = r0 + threadIdx.x;
+      const bool al = r < nr && a.alive[base + r];
+      const uint32_t meta = al ? a.r_meta[base + r] : 0u;
+      uint32_t tot;
+      const uint32_t ex = block_excl(al ? 1u : 0u, L.w, tot);
+      const uint32_t i = carry[0] + ex;
+      if (al) {
+        L.su[i] = a.r_su[base + r];
+        L.ob[i] = a.r_ob[base + r];
+      }
+      carry[0] += tot;
+      for (int c = 0; c < 3; ++c) {
+        const bool f = al && ((meta >> (2 + c)) & 1u);  // START, END, singleton
+        const uint32_t x = block_excl(f ? 1u : 0u, L.w, tot);
+        if (f) (c < 2 ? L.side[c] : L.single)[carry[c + 1] + x] = (uint16_t)i;
+        carry[c + 1] += tot;
+      }
+    }
+    if (threadIdx.x == 0) {
+      L.n_alive = carry[0];
+      L.n_side[0] = carry[1];
+      L.n_side[1] = carry[2];
+      L.n_single = carry[3];
+      L.writers = 0;
+      n_ent = 0;
+    }
+    if (!count_only)
+      for (int k = threadIdx.x; k < kHashSlots; k += blockDim.x) {
+        L.hkey[k] = kEmptyKey;
+        L.hidx[k] = 0;
+      }
+    __syncthreads();
+    const uint32_t q0 = fix_side_pairs(L, 0, a.max_weight);
+    const uint32_t q1 = fix_side_pairs(L, 1, a.max_weight);
+    const uint32_t Q = q0 + q1 + L.n_single;
+    if (count_only) {
+      if (threadIdx.x == 0) d.n_q[g] = Q;
+      __syncthreads();
+      continue;
+    }
+    const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+      double mass, thr;
+      bool single, pc;
+      fix_query(L, o, q0, q1, a.tol, mass, thr, single);
+      uint64_t u0, u1;
+      const int8_t st = masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
+      if (!pc) atomicOr(a.err, 4u);
+      if (!(single || st == SST_SOME)) continue;
+      const uint64_t key = key_bits(mass);
+      uint32_t h = key_hash(key);
+      for (int probe = 0; probe < kHashSlots; ++probe, h = (h + 1) & (kHashSlots - 1)) {
+        const unsigned long long prev = atomicCAS((unsigned long long*)&L.hkey[h], kEmptyKey, key);
+        if (prev == kEmptyKey || prev == key) {
+          atomicMax(&L.hidx[h], o + 1);
+          if (prev == kEmptyKey) atomicAdd(&L.writers, 1u);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (L.writers > kHashSlots * 3 / 4 && threadIdx.x == 0) atomicOr(a.err, 16u);
+    // the occupied slots, then each entry's rank by key (entries are few)
+    for (int k = threadIdx.x; k < kHashSlots; k += blockDim.x)
+      if (L.hkey[k] != kEmptyKey) ent[atomicAdd(&n_ent, 1u)] = (uint32_t)k;
+    __syncthreads();
+    const uint32_t E = n_ent;
+    const uint64_t out0 = d.off[g];
+    for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) {
+      const uint64_t key = L.hkey[ent[e]];
+      uint32_t rank = 0;
+      for (uint32_t f = 0; f < E; ++f) rank += L.hkey[ent[f]] < key;  // keys are distinct
+      double mass, thr;
+      bool single;
+      fix_query(L, L.hidx[ent[e]] - 1, q0, q1, a.tol, mass, thr, single);
+      d.key[out0 + rank] = key;
+      d.thr[out0 + rank] = thr;
+    }
+    if (threadIdx.x == 0) d.n_ent[g] = E;
+    __syncthreads();
+  }
+}
+
 namespace {
 
 struct BinLds {
@@ -553,12 +657,16 @@ __global__ __launch_bounds__(kPipeWG) void k_bins_count(PipeArgs a) {
       if (threadIdx.x == 0) {
         atomicOr(a.err, 2u);
         a.n_q[g] = 0;
+        if (a.n_q0) a.n_q0[g] = 0;
       }
       continue;
     }
     const uint32_t q0 = bins_side(L, 0, a.tol);
     const uint32_t q1 = bins_side(L, 1, a.tol);
-    if (threadIdx.x == 0) a.n_q[g] = q0 + q1;
+    if (threadIdx.x == 0) {
+      a.n_q[g] = q0 + q1;
+      if (a.n_q0) a.n_q0[g] = q0;
+    }
     __syncthreads();
   }
 }
@@ -659,6 +767,17 @@ __global__ __launch_bounds__(kPipeWG) void k_scan_u32(const uint32_t* in, uint64
     __syncthreads();
   }
   if (threadIdx.x == 0) out[n] = carry;
+}
+
+hipError_t launch_dict(const TableArgs& t, const PipeArgs& a, const DictArgs& d, bool count_only, int n_wg,
+                       hipStream_t st) {
+  if (a.n_spec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dict, dim3(n_wg), dim3(kPipeWG), 0, st, t, a, d, count_only ? 1 : 0);
+  return hipGetLastError();
+}
+hipError_t launch_scan_u32(const uint32_t* in, uint64_t* out, int64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(kPipeWG), 0, st, in, out, n);
+  return hipGetLastError();
 }
 
 hipError_t launch_bins_count(const PipeArgs& a, int n_wg, hipStream_t st) {
