@@ -487,7 +487,8 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
  * d_status (capacity: the total).  d_err bit 2: a spectrum over 2048 rows. */
 int sst_bins_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                           const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
-                          const uint32_t* d_rows, double tol, uint32_t* d_n_q, uint64_t* d_q_off, uint32_t* d_err);
+                          const uint32_t* d_rows, double tol, uint32_t* d_n_q, uint64_t* d_q_off, uint32_t* d_err,
+                          uint32_t* d_n_q0 /* may be NULL: the START side's count per spectrum */);
 int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                          const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
                          const uint32_t* d_rows, const uint64_t* d_alpha, double tol, double prec,
@@ -522,6 +523,166 @@ int64_t sst_dict_union(const int64_t* offsets, int64_t n_spec, const double* key
  * sort by standard_unit_mass (fragment_classification.py:84), for many
  * spectra (numpy.lexsort((rows, key, group))). */
 int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_groups, int64_t* order);
+
+/* ---- config 5: SkeletonBuilder._predict_skeleton's walk --------------- */
+/* One lane per (spectrum, side) walks the side's rows the fixpoint kept
+ * (skeleton_building.py:114-196): bins, each closed bin explained against the
+ * last bin with explanations (explain_bin_differences :372-421, the first
+ * against 0) after filter_by_explanation's final dict (:423-440),
+ * update_skeleton_for_given_explanations (:442-482) with CPython's set order
+ * (sst_pyset_order; name hashes from the caller's interpreter), min_end /
+ * max_end per bin.  Pair-class windows are answered in the lane; the others
+ * come from the masked explain: stage 3's speculative queries (s_*), and
+ * re-queries (a bin explained against an older bin) listed by the lane when
+ * their answers are missing -- the side is then SST_WALK_SUSPENDED, and the
+ * caller answers req_* (sst_explain_alpha_batch_device), adds them as round
+ * n_rounds (rq_*: per side its block start << 32 | count in the round's
+ * lists) and walks the suspended sides again (they replay from the start).
+ * SST_WALK_BIG: a bin outgrew the lane's scratch capacities (walk that side
+ * again with larger ones).  All pointers are device pointers. */
+#define SST_WALK_MAX_ROUNDS 16
+#define SST_WALK_DONE 0
+#define SST_WALK_SUSPENDED 1
+#define SST_WALK_BIG 2
+#define SST_WALK_RAISE 3   /* an answer raised in the reference (window past the reduced table) */
+#define SST_WALK_LIMIT 4   /* an engine limit: rows, positions, request list, OVERFLOW / ABORTED answer */
+#define SST_WALK_ROUNDS 5  /* more than SST_WALK_MAX_ROUNDS re-query rounds */
+#define SST_WALK_MISSING 6 /* a DFS answer was not supplied */
+typedef struct sst_walk_args {
+  const int64_t* peak_off;   /* [n_spec + 1]: rows of spectrum g at slots 4 peak_off[g] + i (SU order) */
+  const uint32_t* cnt;       /* [n_spec] rows */
+  const double* r_su;
+  const double* r_ob;
+  const uint32_t* r_meta;    /* breakage | sides << 2 | singleton << 4 | peak << 8 */
+  const uint8_t* alive;      /* the rows the fixpoint kept */
+  const uint64_t* alpha;     /* [2 n_spec] the fixpoint's alphabets (row masks) */
+  const int32_t* max_len;    /* [n_spec] SequenceInformation.max_len */
+  const uint8_t* pair_ok;    /* [n_spec] budgets cannot bind on pair-class windows */
+  int64_t n_spec;
+  int64_t slots;             /* 4 * peaks */
+  double tol, prec, rprec;
+  const uint64_t* d_off;     /* the final dict (sst_dict_build_device) */
+  const uint32_t* d_n;
+  const uint64_t* d_key;
+  const double* d_thr;
+  const uint64_t* q_off;     /* stage 3 (sst_bins_count_device): per spectrum its queries' offset */
+  const uint32_t* q0;        /* and its START side's count */
+  const uint64_t* s_ptr;     /* per stage-3 query off the pair class: first payload record (sst_result_refs_device) */
+  const uint32_t* s_n;
+  const int8_t* s_st;
+  int n_rounds;
+  const uint64_t* rq_block[SST_WALK_MAX_ROUNDS];
+  const uint64_t* rq_ptr[SST_WALK_MAX_ROUNDS];
+  const uint32_t* rq_n[SST_WALK_MAX_ROUNDS];
+  const int8_t* rq_st[SST_WALK_MAX_ROUNDS];
+  uint64_t* req_block;       /* [2 n_spec] this round's blocks (zeroed by the caller) */
+  double* req_mass;
+  double* req_thr;
+  int32_t* req_spec;
+  uint32_t* req_count;
+  uint64_t req_cap;
+  const int64_t* name_hash;  /* [n_rows] hash() of each row's nucleoside name */
+  const uint32_t* sides;     /* side ids 2 g + (0 START, 1 END) to walk */
+  uint32_t n_sides;
+  uint8_t* scratch;          /* n_sides * scratch_stride bytes (sst_walk_scratch_bytes) */
+  uint64_t scratch_stride;
+  uint32_t pos_cap, len_cap, expl_cap, cand_cap, tset_cap;
+  uint16_t* side_rows;       /* [2 slots] */
+  const uint64_t* skel_off;  /* [n_spec] exclusive prefix of 2 max_len */
+  uint64_t* skel;            /* spectrum g, side sd, position i: masks at 2 (skel_off[g] + sd max_len[g] + i) */
+  int32_t* min_end;          /* [2 slots] per side */
+  int32_t* max_end;
+  uint8_t* kept;             /* [2 slots] per side: not rejected by the walk */
+  uint8_t* side_status;      /* [2 n_spec] SST_WALK_* */
+  uint32_t* n_suspended;
+  uint32_t* n_big;
+} sst_walk_args;
+/* Scratch bytes per walked side for the given capacities (pos_cap, tset_cap:
+ * powers of two >= the set tables the positions / a query's candidates need,
+ * sst_pyset_table_size). */
+uint64_t sst_walk_scratch_bytes(uint32_t pos_cap, uint32_t len_cap, uint32_t expl_cap, uint32_t cand_cap,
+                                uint32_t tset_cap);
+/* CPython's table size after n distinct additions to an empty set. */
+uint32_t sst_pyset_table_size(uint32_t n);
+int sst_skel_walk_device(sst_table* t, const sst_walk_args* a);
+/* Candidate references of a result's queries (settles it first): for query
+ * i, d_st[d_dst[i]] = its status, d_n[...] = its candidates (SOME) or exact
+ * count (OVERFLOW / ABORTED), d_ptr[...] = the device address of its first
+ * payload record (SOME; else 0).  Valid while the result lives unchanged. */
+int sst_result_refs_device(sst_result* r, const int64_t* d_dst, uint64_t* d_ptr, uint32_t* d_n, int8_t* d_st);
+/* filter_by_explanation's final explanation dict per spectrum
+ * (prediction.py:261-329 over the final rows and alphabet).  Count pass:
+ * d_n_q[g] = the last round's queries, d_off = their exclusive offsets
+ * (n_spec + 1 entries, total last); build pass: keys ascending (double bits)
+ * and the last writer's threshold into [d_off[g], + d_n_ent[g]). */
+int sst_dict_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                          const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                          const uint32_t* d_rows, double max_weight, double tol, uint32_t* d_n_q, uint64_t* d_off,
+                          uint32_t* d_err);
+int sst_dict_build_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                          const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                          const uint32_t* d_rows, const uint64_t* d_alpha, double max_weight, double tol, double prec,
+                          const uint64_t* d_off, uint64_t* d_key, double* d_thr, uint32_t* d_n_ent, uint32_t* d_err);
+
+/* select_sequence_length_with_jaccard (skeleton_building.py:315-370) and
+ * combine_skeleton_sequences (:494-516) per spectrum, one lane each: the
+ * START skeleton and the reversed END skeleton (sst_walk_args.skel layout),
+ * the two length bounds on the skeleton alphabet (sst_length_bounds_reach_
+ * device) and that alphabet's row masses; validate_sequence_length_by_mass
+ * (:291-313) in the reference's float order (sequential f64 sums, CPython
+ * 3.10's sum()).  Outputs: seq_len[g], the combined skeleton (masks at
+ * 2 (comb_off[g] + i), i < seq_len[g]; comb_off[g] + max_len[g] positions
+ * reserved) and status[g]: SST_JAC_OK, SST_JAC_NO_LENGTH (the reference's
+ * "No sequence length fitting ..." Exception), SST_JAC_INDEX (an IndexError
+ * in combine_skeleton_sequences: seq_len > max_len), SST_JAC_BOUNDS (a
+ * length bound raised: status_lb[g] != 0). */
+#define SST_JAC_OK 0
+#define SST_JAC_NO_LENGTH 1
+#define SST_JAC_INDEX 2
+#define SST_JAC_BOUNDS 3
+typedef struct sst_jaccard_args {
+  int64_t n_spec;
+  const int32_t* max_len;     /* [n_spec] */
+  const uint64_t* skel_off;   /* [n_spec] as sst_walk_args.skel_off */
+  const uint64_t* skel;
+  const int64_t* lower;       /* [n_spec] the length bounds */
+  const int64_t* upper;
+  const int8_t* status_lb;
+  const double* su_mass;      /* [n_spec] SequenceInformation.su_mass */
+  const double* row_mass;     /* [n_rows] integer mass * precision (nucleoside_masses) */
+  const uint64_t* comb_off;   /* [n_spec] exclusive prefix of max_len */
+  uint64_t* comb;             /* combined skeleton masks */
+  int32_t* seq_len;
+  int8_t* status;
+  double max_variance;        /* fragment_classification.MAX_VARIANCE */
+} sst_jaccard_args;
+int sst_jaccard_device(sst_table* t, const sst_jaccard_args* a);
+/* The skeleton's alphabet per spectrum (skeleton_building.py:319-326):
+ * d_out[2g..2g+1] = d_alpha[2g..] & (the table's canonical rows | every row
+ * either side's skeleton names at any of its max_len positions). */
+int sst_skeleton_alpha_device(sst_table* t, int64_t n_spec, const int32_t* d_max_len, const uint64_t* d_skel_off,
+                              const uint64_t* d_skel, const uint64_t* d_alpha, uint64_t* d_out);
+
+/* compute_sequence_length_bound (mass_table.py:343-487) after the skeleton's
+ * alphabet reduction (skeleton_building.py:315-336), both directions, for
+ * queries on per-spectrum reduced alphabets, exact without a table rebuild:
+ * sst_reach_rows_device writes, per spectrum g, the reachability bitset of
+ * each kept row k (row 0 excluded, ascending): bit m of u32 word
+ * d_bits[d_off[g] + k * d_words[g] + m / 32] <=> m is a sum of kept rows up
+ * to that one (the rebuilt table's pair(r_k, m) != 0), for m < 32 d_words[g]
+ * (>= the highest window value + 1).  sst_length_bounds_reach_device then
+ * replays the reference's memoised DFS once per query (spectrum d_spec[i])
+ * on those pairs and derives both bounds from it: d_lower[i] / d_upper[i],
+ * d_status[i] 0 ok, SST_OUT_OF_TABLE (the reference raises), SST_ABORTED (a
+ * window in the reduced table's masked last word, or a guard), -5 an empty
+ * window.  Budgets: max_len, max_mods and the table's caps
+ * (sst_table_set_budgets) as in sst_length_bound_batch.  Device pointers. */
+int sst_reach_rows_device(sst_table* t, const uint64_t* d_alpha, const int64_t* d_words, const uint64_t* d_off,
+                          int64_t n_spec, uint32_t* d_bits);
+int sst_length_bounds_reach_device(sst_table* t, const double* d_su, const double* d_obs, const int32_t* d_spec,
+                                   const uint64_t* d_alpha, const uint32_t* d_reach_bits, const uint64_t* d_reach_off,
+                                   const int64_t* d_reach_words, int64_t n, double tol, double prec, int max_len,
+                                   int64_t max_mods, int64_t* d_lower, int64_t* d_upper, int8_t* d_status);
 
 /* ---- CPython set order (the skeleton walk's emulation, sst_pyset.h) ---- */
 /* hash(tuple) of a tuple whose items hash to item_hashes[0..n) (CPython

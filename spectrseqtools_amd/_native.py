@@ -33,7 +33,9 @@ EXPORTS = (
     "sst_is_valid_alpha_device", "sst_dict_union", "sst_step_rows_device", "sst_result_queries",
     "sst_classify_rows_device", "sst_fix_round_device", "sst_valid_rows_alpha_device",
     "sst_bins_count_device", "sst_bins_emit_device", "sst_length_bound_alpha_batch",
-    "sst_py_tuple_hash", "sst_pyset_order",
+    "sst_py_tuple_hash", "sst_pyset_order", "sst_pyset_table_size", "sst_walk_scratch_bytes",
+    "sst_skel_walk_device", "sst_result_refs_device", "sst_dict_count_device", "sst_dict_build_device",
+    "sst_reach_rows_device", "sst_length_bounds_reach_device", "sst_jaccard_device", "sst_skeleton_alpha_device",
 )
 
 # kernel ids of sst_profile_read
@@ -60,6 +62,45 @@ _PP = ctypes.POINTER(ctypes.c_void_p)
 
 class EngineError(RuntimeError):
     pass
+
+
+WALK_MAX_ROUNDS = 16  # SST_WALK_MAX_ROUNDS
+(WALK_DONE, WALK_SUSPENDED, WALK_BIG, WALK_RAISE, WALK_LIMIT, WALK_ROUNDS, WALK_MISSING) = range(7)
+
+
+JAC_OK, JAC_NO_LENGTH, JAC_INDEX, JAC_BOUNDS = range(4)
+
+
+class JaccardArgs(ctypes.Structure):
+    """sst_jaccard_args (include/sst.h)."""
+    _fields_ = [("n_spec", ctypes.c_int64), ("max_len", ctypes.c_void_p), ("skel_off", ctypes.c_void_p),
+                ("skel", ctypes.c_void_p), ("lower", ctypes.c_void_p), ("upper", ctypes.c_void_p),
+                ("status_lb", ctypes.c_void_p), ("su_mass", ctypes.c_void_p), ("row_mass", ctypes.c_void_p),
+                ("comb_off", ctypes.c_void_p), ("comb", ctypes.c_void_p), ("seq_len", ctypes.c_void_p),
+                ("status", ctypes.c_void_p), ("max_variance", ctypes.c_double)]
+
+
+class WalkArgs(ctypes.Structure):
+    """sst_walk_args (include/sst.h): device pointers of the skeleton walk."""
+    _R = WALK_MAX_ROUNDS
+    _fields_ = [("peak_off", ctypes.c_void_p), ("cnt", ctypes.c_void_p), ("r_su", ctypes.c_void_p),
+                ("r_ob", ctypes.c_void_p), ("r_meta", ctypes.c_void_p), ("alive", ctypes.c_void_p),
+                ("alpha", ctypes.c_void_p), ("max_len", ctypes.c_void_p), ("pair_ok", ctypes.c_void_p),
+                ("n_spec", ctypes.c_int64), ("slots", ctypes.c_int64), ("tol", ctypes.c_double),
+                ("prec", ctypes.c_double), ("rprec", ctypes.c_double), ("d_off", ctypes.c_void_p),
+                ("d_n", ctypes.c_void_p), ("d_key", ctypes.c_void_p), ("d_thr", ctypes.c_void_p),
+                ("q_off", ctypes.c_void_p), ("q0", ctypes.c_void_p), ("s_ptr", ctypes.c_void_p),
+                ("s_n", ctypes.c_void_p), ("s_st", ctypes.c_void_p), ("n_rounds", ctypes.c_int),
+                ("rq_block", ctypes.c_void_p * _R), ("rq_ptr", ctypes.c_void_p * _R),
+                ("rq_n", ctypes.c_void_p * _R), ("rq_st", ctypes.c_void_p * _R), ("req_block", ctypes.c_void_p),
+                ("req_mass", ctypes.c_void_p), ("req_thr", ctypes.c_void_p), ("req_spec", ctypes.c_void_p),
+                ("req_count", ctypes.c_void_p), ("req_cap", ctypes.c_uint64), ("name_hash", ctypes.c_void_p),
+                ("sides", ctypes.c_void_p), ("n_sides", ctypes.c_uint32), ("scratch", ctypes.c_void_p),
+                ("scratch_stride", ctypes.c_uint64), ("pos_cap", ctypes.c_uint32), ("len_cap", ctypes.c_uint32),
+                ("expl_cap", ctypes.c_uint32), ("cand_cap", ctypes.c_uint32), ("tset_cap", ctypes.c_uint32),
+                ("side_rows", ctypes.c_void_p), ("skel_off", ctypes.c_void_p), ("skel", ctypes.c_void_p),
+                ("min_end", ctypes.c_void_p), ("max_end", ctypes.c_void_p), ("kept", ctypes.c_void_p),
+                ("side_status", ctypes.c_void_p), ("n_suspended", ctypes.c_void_p), ("n_big", ctypes.c_void_p)]
 
 
 def _share_hip_runtime_with_torch():
@@ -173,11 +214,31 @@ def load_library(path=LIB_PATH):
     lib.sst_fix_round_device.restype = _I
     lib.sst_valid_rows_alpha_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _P]
     lib.sst_valid_rows_alpha_device.restype = _I
-    lib.sst_bins_count_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _D, _P, _P, _P]
+    lib.sst_bins_count_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _D, _P, _P, _P, _P]
     lib.sst_bins_count_device.restype = _I
     lib.sst_bins_emit_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _P, _P, _P, _P, _P, _P, _P,
                                          _P, _P]
     lib.sst_bins_emit_device.restype = _I
+    lib.sst_pyset_table_size.argtypes = [ctypes.c_uint32]
+    lib.sst_pyset_table_size.restype = ctypes.c_uint32
+    lib.sst_walk_scratch_bytes.argtypes = [ctypes.c_uint32] * 5
+    lib.sst_walk_scratch_bytes.restype = ctypes.c_uint64
+    lib.sst_skel_walk_device.argtypes = [_P, ctypes.POINTER(WalkArgs)]
+    lib.sst_skel_walk_device.restype = _I
+    lib.sst_result_refs_device.argtypes = [_P, _P, _P, _P, _P]
+    lib.sst_result_refs_device.restype = _I
+    lib.sst_dict_count_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _D, _D, _P, _P, _P]
+    lib.sst_dict_count_device.restype = _I
+    lib.sst_dict_build_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _D, _P, _P, _P, _P, _P]
+    lib.sst_dict_build_device.restype = _I
+    lib.sst_reach_rows_device.argtypes = [_P, _P, _P, _P, _I64, _P]
+    lib.sst_reach_rows_device.restype = _I
+    lib.sst_length_bounds_reach_device.argtypes = [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _D, _D, _I, _I64, _P, _P, _P]
+    lib.sst_length_bounds_reach_device.restype = _I
+    lib.sst_jaccard_device.argtypes = [_P, ctypes.POINTER(JaccardArgs)]
+    lib.sst_jaccard_device.restype = _I
+    lib.sst_skeleton_alpha_device.argtypes = [_P, _I64, _P, _P, _P, _P, _P]
+    lib.sst_skeleton_alpha_device.restype = _I
     return lib
 
 
@@ -253,6 +314,15 @@ def pyset_order(keys, hashes):
     if m < 0:
         raise EngineError(f"sst_pyset_order failed ({m})")
     return out[:m].tolist()
+
+
+def pyset_table_size(n):
+    """CPython's set table size after n distinct additions (sst_pyset_table_size)."""
+    return int(lib().sst_pyset_table_size(int(n)))
+
+
+def walk_scratch_bytes(pos_cap, len_cap, expl_cap, cand_cap, tset_cap):
+    return int(lib().sst_walk_scratch_bytes(pos_cap, len_cap, expl_cap, cand_cap, tset_cap))
 
 
 def sort_rows(group, key, n_groups):

@@ -2154,13 +2154,15 @@ static int bins_args(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, co
 
 int sst_bins_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                           const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
-                          const uint32_t* d_rows, double tol, uint32_t* d_n_q, uint64_t* d_q_off, uint32_t* d_err) {
+                          const uint32_t* d_rows, double tol, uint32_t* d_n_q, uint64_t* d_q_off, uint32_t* d_err,
+                          uint32_t* d_n_q0) {
   PipeArgs a;
   if (int rc = bins_args(t, d_peak_off, n_spec, d_rows_su, d_rows_ob, d_rows_meta, d_alive, d_rows, tol, 1.0,
                          d_q_off, d_err, a))
     return rc;
   if (n_spec > 0 && !d_n_q) return SST_E_ARG;
   a.n_q = d_n_q;
+  a.n_q0 = d_n_q0;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
@@ -2624,4 +2626,248 @@ extern "C" int64_t sst_pyset_order(const int32_t* keys, const int64_t* hashes, i
   for (uint32_t s = 0; s <= t.mask; ++s)
     if (t.key[t.cur][s] >= 0) order[m++] = t.key[t.cur][s];
   return m;
+}
+
+// ---- config 5: final dict, skeleton walk, candidate references -----------
+extern "C" int sst_dict_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                                     const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                                     const uint32_t* d_rows, double max_weight, double tol, uint32_t* d_n_q,
+                                     uint64_t* d_off, uint32_t* d_err) {
+  if (!t || n_spec < 0 || n_spec > INT32_MAX || !d_off ||
+      (n_spec > 0 && (!d_peak_off || !d_rows_su || !d_rows_ob || !d_rows_meta || !d_alive || !d_rows || !d_n_q ||
+                      !d_err)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  sst::PipeArgs a{};
+  a.peak_off = d_peak_off;
+  a.n_spec = n_spec;
+  a.r_su = const_cast<double*>(d_rows_su);
+  a.r_ob = const_cast<double*>(d_rows_ob);
+  a.r_meta = const_cast<uint32_t*>(d_rows_meta);
+  a.alive = const_cast<uint8_t*>(d_alive);
+  a.cnt = const_cast<uint32_t*>(d_rows);
+  a.max_weight = max_weight;
+  a.tol = tol;
+  a.err = d_err;
+  sst::DictArgs d{};
+  d.n_q = d_n_q;
+  Prof p(c, SST_K_DICT);
+  HIP_OK(c, sst::launch_dict(t->args, a, d, true, c->n_cu, c->stream));
+  HIP_OK(c, sst::launch_scan_u32(d_n_q, d_off, n_spec, c->stream));
+  return SST_OK;
+}
+
+extern "C" int sst_dict_build_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                                     const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                                     const uint32_t* d_rows, const uint64_t* d_alpha, double max_weight, double tol,
+                                     double prec, const uint64_t* d_off, uint64_t* d_key, double* d_thr,
+                                     uint32_t* d_n_ent, uint32_t* d_err) {
+  if (!t || n_spec < 0 || n_spec > INT32_MAX ||
+      (n_spec > 0 && (!d_peak_off || !d_rows_su || !d_rows_ob || !d_rows_meta || !d_alive || !d_rows || !d_alpha ||
+                      !d_off || !d_n_ent || !d_err)))
+    return SST_E_ARG;
+  if (!t->args.pairs_enabled) return fail(t->ctx, SST_E_ARG, "final dict: the table has no pair list");
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = check_masks(t)) return rc;
+  sst::PipeArgs a{};
+  a.peak_off = d_peak_off;
+  a.n_spec = n_spec;
+  a.r_su = const_cast<double*>(d_rows_su);
+  a.r_ob = const_cast<double*>(d_rows_ob);
+  a.r_meta = const_cast<uint32_t*>(d_rows_meta);
+  a.alive = const_cast<uint8_t*>(d_alive);
+  a.cnt = const_cast<uint32_t*>(d_rows);
+  a.alpha = d_alpha;
+  a.max_weight = max_weight;
+  a.tol = tol;
+  a.prec = prec;
+  a.rprec = 1.0 / prec;
+  a.err = d_err;
+  sst::DictArgs d{};
+  d.off = d_off;
+  d.key = d_key;
+  d.thr = d_thr;
+  d.n_ent = d_n_ent;
+  Prof p(c, SST_K_DICT);
+  HIP_OK(c, sst::launch_dict(t->args, a, d, false, c->n_cu, c->stream));
+  return SST_OK;
+}
+
+extern "C" uint32_t sst_pyset_table_size(uint32_t n) { return sst::pyset::table_size_for(n); }
+
+extern "C" uint64_t sst_walk_scratch_bytes(uint32_t pos_cap, uint32_t len_cap, uint32_t expl_cap, uint32_t cand_cap,
+                                           uint32_t tset_cap) {
+  return sst::walk_scratch_bytes(pos_cap, len_cap, expl_cap, cand_cap, tset_cap);
+}
+
+extern "C" int sst_skel_walk_device(sst_table* t, const sst_walk_args* a) {
+  if (!t || !a) return SST_E_ARG;
+  if (a->n_sides == 0) return SST_OK;
+  if (!a->peak_off || !a->cnt || !a->r_su || !a->r_ob || !a->r_meta || !a->alive || !a->alpha || !a->max_len ||
+      !a->pair_ok || !a->d_off || !a->d_n || !a->q_off || !a->q0 || !a->s_ptr || !a->s_n || !a->s_st ||
+      !a->req_block || !a->req_mass || !a->req_thr || !a->req_spec || !a->req_count || !a->name_hash || !a->sides ||
+      !a->scratch || !a->side_rows || !a->skel_off || !a->skel || !a->min_end || !a->max_end || !a->kept ||
+      !a->side_status || !a->n_suspended || !a->n_big || a->n_rounds < 0 || a->n_rounds > SST_WALK_MAX_ROUNDS)
+    return SST_E_ARG;
+  for (int r = 0; r < a->n_rounds; ++r)
+    if (!a->rq_block[r] || !a->rq_ptr[r] || !a->rq_n[r] || !a->rq_st[r]) return SST_E_ARG;
+  if (a->pos_cap < sst::pyset::kMinSize || a->tset_cap < sst::pyset::kMinSize || (a->pos_cap & (a->pos_cap - 1)) ||
+      (a->tset_cap & (a->tset_cap - 1)) || a->len_cap < 2 || a->len_cap > 128 ||
+      a->scratch_stride < sst::walk_scratch_bytes(a->pos_cap, a->len_cap, a->expl_cap, a->cand_cap, a->tset_cap))
+    return fail(t->ctx, SST_E_ARG, "skeleton walk: scratch capacities");
+  if (!t->args.pairs_enabled) return fail(t->ctx, SST_E_ARG, "skeleton walk: the table has no pair list");
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = check_masks(t)) return rc;
+  Prof p(c, SST_K_SKEL_WALK);
+  HIP_OK(c, sst::launch_skel_walk(t->args, *a, c->stream));
+  return SST_OK;
+}
+
+extern "C" int sst_result_refs_device(sst_result* r, const int64_t* d_dst, uint64_t* d_ptr, uint32_t* d_n,
+                                      int8_t* d_st) {
+  if (!r) return SST_E_ARG;
+  sst_ctx* c = r->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (int rc = settle(r)) return rc;
+  if (int rc = order_after_settle(r)) return rc;
+  if (r->n > 0 && (!d_dst || !d_ptr || !d_n || !d_st)) return SST_E_ARG;
+  HIP_OK(c, sst::launch_result_refs((const int8_t*)r->status.p, r->n, (const uint4*)r->hits.p, r->n_hits,
+                                    (const uint8_t*)r->dense.p, d_dst, d_ptr, d_n, d_st, c->stream));
+  return SST_OK;
+}
+
+// ---- config 5: both length bounds on the skeleton alphabets ---------------
+extern "C" int sst_reach_rows_device(sst_table* t, const uint64_t* d_alpha, const int64_t* d_words,
+                                     const uint64_t* d_off, int64_t n_spec, uint32_t* d_bits) {
+  if (!t || n_spec < 0 || (n_spec > 0 && (!d_alpha || !d_words || !d_off || !d_bits))) return SST_E_ARG;
+  if (t->args.w_min < 1024) return fail(t->ctx, SST_E_ARG, "reach rows: row masses below 1024 (the LDS ring)");
+  for (int r = 1; r < t->n_rows; ++r)
+    if (t->masses[r] >= (1 << 19)) return fail(t->ctx, SST_E_ARG, "reach rows: a row mass of 2^19 or more");
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  sst::ReachArgs a{d_alpha, d_words, d_off, d_bits, t->args.w, t->n_rows, n_spec};
+  Prof p(c, SST_K_REACH_ROWS);
+  HIP_OK(c, sst::launch_reach_rows(a, c->n_cu, c->stream));
+  return SST_OK;
+}
+
+extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, const double* d_obs,
+                                              const int32_t* d_spec, const uint64_t* d_alpha,
+                                              const uint32_t* d_reach_bits, const uint64_t* d_reach_off,
+                                              const int64_t* d_reach_words, int64_t n, double tol, double prec,
+                                              int max_len, int64_t max_mods, int64_t* d_lower, int64_t* d_upper,
+                                              int8_t* d_status) {
+  if (!t || n < 0 || n > INT32_MAX || max_len < 0 || max_len > 120 ||
+      (n > 0 && (!d_su || !d_obs || !d_spec || !d_alpha || !d_reach_bits || !d_reach_off || !d_reach_words ||
+                 !d_lower || !d_upper || !d_status)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (n == 0) return SST_OK;
+  const size_t nn = (size_t)n;
+  DevBuf d_list, d_cnt;
+  if (!d_list.ensure(nn * 4) || !d_cnt.ensure(4)) return fail(c, SST_E_NOMEM, "device allocation failed (length bound)");
+  HIP_OK(c, hipMemsetAsync(d_cnt.p, 0, 4, c->stream));
+  LBArgs q{};
+  q.su = d_su;
+  q.obs = d_obs;
+  q.n = n;
+  q.tol = tol;
+  q.prec = prec;
+  q.rprec = 1.0 / prec;
+  q.A0 = (int)std::max<int64_t>(0, std::min<int64_t>(max_mods, kInfBudget));
+  q.dir = 0;
+  q.max_len = max_len;
+  q.out = d_lower;
+  q.status = d_status;
+  q.exact_list = (uint32_t*)d_list.p;
+  q.exact_count = (uint32_t*)d_cnt.p;
+  q.node_budget = kLBNodeBudget;
+  q.alpha = d_alpha;
+  q.spec = d_spec;
+  q.comp = (int)t->C;
+  q.reach_bits = d_reach_bits;
+  q.reach_off = d_reach_off;
+  q.reach_words = d_reach_words;
+  q.both = 1;
+  q.out_hi = d_upper;
+  uint32_t n_exact = 0;
+  {
+    Prof p(c, SST_K_LENGTH_BOUND);  // windows, extents; every live query is listed for the replay
+    HIP_OK(c, launch_length_bound(t->args, q, nullptr, nullptr, nullptr, 0, 0, true, c->stream));
+  }
+  HIP_OK(c, hipMemcpyAsync(&n_exact, d_cnt.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  std::vector<int8_t> st(nn);
+  int units = (int)std::min<uint32_t>(1024, std::max<uint32_t>(1, n_exact));
+  uint32_t cap = memo_cap0(units, kLBHashCap0);
+  while (n_exact) {
+    DevBuf hash, vals, frames;
+    if (!hash.ensure((size_t)units * cap * hash_entry_bytes()) || !vals.ensure((size_t)units * cap * kMaxRows) ||
+        !frames.ensure((size_t)units * lb_frame_bytes()))
+      return fail(c, SST_E_NOMEM, "device allocation failed (length-bound memo)");
+    HIP_OK(c, hipMemsetAsync(hash.p, 0, hash.bytes, c->stream));
+    {
+      Prof p(c, SST_K_LENGTH_BOUND);
+      HIP_OK(c, launch_length_bound(t->args, q, (char*)hash.p, (int8_t*)vals.p, (char*)frames.p, cap, units, false,
+                                    c->stream));
+    }
+    HIP_OK(c, hipMemcpyAsync(st.data(), d_status, nn, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    // the queries whose memo ran out: again, alone, with 8x the memo
+    std::vector<uint32_t> retry;
+    for (size_t i = 0; i < nn; ++i)
+      if (st[i] == kStatusExactRetry) retry.push_back((uint32_t)i);
+    if (retry.empty()) break;
+    if ((size_t)std::max(1, units / 8) * cap * 8 * (hash_entry_bytes() + kMaxRows) > kMaxMemoBytes)
+      return fail(c, SST_E_NOMEM, "length bound: memo would exceed the workspace limit");
+    cap *= 8;
+    units = std::max(1, std::min<int>(units / 8, (int)retry.size()));
+    n_exact = (uint32_t)retry.size();
+    HIP_OK(c, hipMemcpyAsync(d_list.p, retry.data(), retry.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipMemcpyAsync(d_cnt.p, &n_exact, 4, hipMemcpyHostToDevice, c->stream));
+  }
+  for (size_t i = 0; i < nn; ++i)
+    if (st[i] == kStatusPending || st[i] == kStatusExactRetry)
+      return fail(c, SST_E_INTERNAL, "length bound: query left unresolved (internal error)");
+  return SST_OK;
+}
+
+extern "C" int sst_jaccard_device(sst_table* t, const sst_jaccard_args* a) {
+  if (!t || !a || a->n_spec < 0) return SST_E_ARG;
+  if (a->n_spec == 0) return SST_OK;
+  if (!a->max_len || !a->skel_off || !a->skel || !a->lower || !a->upper || !a->status_lb || !a->su_mass ||
+      !a->row_mass || !a->comb_off || !a->comb || !a->seq_len || !a->status)
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  Prof p(c, SST_K_JACCARD);
+  HIP_OK(c, sst::launch_jaccard(*a, c->stream));
+  return SST_OK;
+}
+
+extern "C" int sst_skeleton_alpha_device(sst_table* t, int64_t n_spec, const int32_t* d_max_len,
+                                         const uint64_t* d_skel_off, const uint64_t* d_skel, const uint64_t* d_alpha,
+                                         uint64_t* d_out) {
+  if (!t || n_spec < 0 || (n_spec > 0 && (!d_max_len || !d_skel_off || !d_skel || !d_alpha || !d_out))) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  uint64_t canon[2] = {0, 0};
+  for (int r = 1; r < t->n_rows; ++r)
+    if (!t->is_mod[r]) canon[r >> 6] |= 1ull << (r & 63);
+  Prof p(c, SST_K_JACCARD);
+  HIP_OK(c, sst::launch_skel_alpha(n_spec, d_max_len, d_skel_off, d_skel, d_alpha, canon[0], canon[1], d_out,
+                                   c->stream));
+  return SST_OK;
 }

@@ -260,7 +260,30 @@ struct LBArgs {
   const uint64_t* alpha = nullptr;
   const int32_t* spec = nullptr;
   int comp = 32;
+  // with the alphabets' per-row reachability (ReachArgs layout, spectrum
+  // spec[i]): the replay reads the reduced table's pairs from it instead of
+  // the full table's index -- exact for both directions; both = 1: one replay
+  // gives the lower bound in out[] and the upper in out_hi[]
+  const uint32_t* reach_bits = nullptr;
+  const uint64_t* reach_off = nullptr;
+  const int64_t* reach_words = nullptr;
+  int both = 0;
+  int64_t* out_hi = nullptr;
 };
+
+// per-row reachability of reduced alphabets (sst_reach.hip): spectrum g's
+// kept rows r_0 < r_1 < ... (alpha, row 0 excluded), row k's bitset of
+// masses [0, 32 words[g]) at bits + off[g] + k * words[g] (u32 words)
+struct ReachArgs {
+  const uint64_t* alpha;   // [2 n_spec]
+  const int64_t* words;    // [n_spec]
+  const uint64_t* off;     // [n_spec]
+  uint32_t* bits;
+  const int* w;            // the table's row masses
+  int n_rows;
+  int64_t n_spec;
+};
+hipError_t launch_reach_rows(const ReachArgs& a, int n_wg, hipStream_t st);
 
 struct ExactWs {
   char* hash;
@@ -446,6 +469,21 @@ struct DictArgs {
 hipError_t launch_dict(const TableArgs& t, const PipeArgs& a, const DictArgs& d, bool count_only, int n_wg,
                        hipStream_t st);
 hipError_t launch_scan_u32(const uint32_t* in, uint64_t* out, int64_t n, hipStream_t st);
+// the skeleton walk (sst_skel.hip, k_skel_walk): the public sst_walk_args
+constexpr int kWalkMaxRounds = SST_WALK_MAX_ROUNDS;
+enum { kWalkDone = SST_WALK_DONE, kWalkSuspended = SST_WALK_SUSPENDED, kWalkBig = SST_WALK_BIG,
+       kWalkRaise = SST_WALK_RAISE, kWalkLimit = SST_WALK_LIMIT, kWalkRounds = SST_WALK_ROUNDS,
+       kWalkMissing = SST_WALK_MISSING };
+using WalkArgs = sst_walk_args;
+hipError_t launch_skel_walk(const TableArgs& t, const WalkArgs& a, hipStream_t st);
+hipError_t launch_jaccard(const sst_jaccard_args& a, hipStream_t st);
+hipError_t launch_skel_alpha(int64_t n_spec, const int32_t* max_len, const uint64_t* skel_off, const uint64_t* skel,
+                             const uint64_t* alpha, uint64_t canon0, uint64_t canon1, uint64_t* out, hipStream_t st);
+hipError_t launch_result_refs(const int8_t* status, int64_t n, const uint4* hits, uint64_t n_hits,
+                              const uint8_t* payload, const int64_t* dst, uint64_t* ptr, uint32_t* cnt, int8_t* st,
+                              hipStream_t stream);
+uint64_t walk_scratch_bytes(uint32_t pos_cap, uint32_t len_cap, uint32_t expl_cap, uint32_t cand_cap,
+                            uint32_t tset_cap);
 hipError_t launch_bins_count(const PipeArgs& a, int n_wg, hipStream_t st);
 hipError_t launch_bins_emit(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st);
 hipError_t launch_classify_rows(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st);

@@ -579,6 +579,23 @@ struct HEntry {
   uint32_t pad;
   uint64_t en0, en1;
 };
+// The reduced table's pairs from per-row reachability bitsets (sst_reach.hip,
+// one query per wave): kept row k (k-th kept full-table row, ascending) has
+// R_k = the masses its rows and the kept rows below reach.  Lane L holds kept
+// rows L and L + 64 (full-table row, mass) and the ranks among the kept rows
+// of full-table rows L and L + 64 (-1: dropped).
+struct ReachView {
+  const uint32_t* bits;  // R_k at bits + k * W
+  int64_t W;             // words per row: masses [0, 32 W)
+  int K;
+  int row0, row1, w0, w1;
+  int rank0, rank1;
+};
+__device__ __forceinline__ bool reach_bit(const ReachView& rv, int k, int64_t x) {
+  if (x < 0 || (x >> 5) >= rv.W) return false;
+  return (rv.bits[(int64_t)k * rv.W + (x >> 5)] >> (x & 31)) & 1u;
+}
+
 struct Hash {
   HEntry* e;
   uint32_t mask;  // capacity - 1
@@ -587,6 +604,8 @@ struct Hash {
   uint32_t limit;
   uint64_t sink = 0;  // folds prefetch loads (see p1_visit)
   uint32_t last_meta = 0;  // meta written by the last first visit (p1_visit)
+  bool reach = false;      // wave mode only: node records from rv, not the full table's index
+  ReachView rv{};
   __device__ __forceinline__ uint32_t slot(uint32_t m) const { return (m * 0x9E3779B1u) & mask; }
   // returns entry pointer or nullptr if absent
   __device__ __forceinline__ HEntry* find(uint32_t m) const {
@@ -891,6 +910,34 @@ struct P1Frame {
   uint32_t meta;                  // the entry's meta as this frame wrote it (wave mode)
 };
 
+// the index record of mass m on the reduced table (wave-uniform m): left
+// bits of the kept rows r with m - w_r in R_r, lo = the lowest kept row
+// whose R holds m (255: unreachable), in the full-table index's packing
+__device__ __forceinline__ ulonglong2 reach_rec(const ReachView& rv, uint32_t m) {
+  const int lane = threadIdx.x & 63;
+  bool in0 = false, in1 = false, b0 = false, b1 = false;
+  if (lane < rv.K) {
+    in0 = reach_bit(rv, lane, m);
+    b0 = reach_bit(rv, lane, (int64_t)m - rv.w0);
+  }
+  if (lane + 64 < rv.K) {
+    in1 = reach_bit(rv, lane + 64, m);
+    b1 = reach_bit(rv, lane + 64, (int64_t)m - rv.w1);
+  }
+  const uint64_t M0 = __ballot(in0), M1 = __ballot(in1), L0 = __ballot(b0), L1 = __ballot(b1);
+  int lo = 255;
+  if (M0 | M1) {
+    const int kk = M0 ? __builtin_ctzll(M0) : 64 + __builtin_ctzll(M1);
+    const int ra = __shfl(rv.row0, kk & 63, 64), rb = __shfl(rv.row1, kk & 63, 64);
+    lo = kk < 64 ? ra : rb;
+  }
+  auto lbit = [&](int rank) {
+    return rank >= 0 && (rank < 64 ? ((L0 >> rank) & 1ull) : ((L1 >> (rank - 64)) & 1ull));
+  };
+  const uint64_t La = __ballot(lbit(rv.rank0)), Lb = __ballot(lbit(rv.rank1));
+  return make_ulonglong2(La, (Lb & ((1ull << 56) - 1ull)) | ((uint64_t)lo << 56));
+}
+
 // visit (m, r, A, B): returns 1 if (m, r) is a first visit (its newly
 // visited rows' enabled-left mask in *en, its memo entry in *ent: the caller
 // makes it the current frame), 0 otherwise (memo hit or pair == 0; *nonempty
@@ -903,7 +950,9 @@ __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& 
   // enabled mask: the whole 32-B entry) are independent: issue them together
   // (both were prefetched by the parent frame)
   const uint32_t sl = h.slot(m);
-  const ulonglong2 rec = ld_index(t.index, m);
+  ulonglong2 rec;
+  if (WAVE && h.reach) rec = reach_rec(h.rv, m);
+  else rec = ld_index(t.index, m);
   const ulonglong2 kv = *(const ulonglong2*)&h.e[sl];
   const ulonglong2 ev = *(const ulonglong2*)&h.e[sl].en0;
   nodes++;
@@ -963,7 +1012,9 @@ __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& 
   // the frame will visit (m - w_rr, rr) for every enabled row: issue their
   // index-record and first-probe loads now, independently, so the visits
   // that follow hit the cache instead of paying dependent HBM round trips
-  if (WAVE) {
+  if (WAVE && h.reach) {
+    // reduced-table records are assembled from the rows' bitsets: no prefetch
+  } else if (WAVE) {
     // one query per wave: lane L takes rows L and L + 64 -- and, speculating
     // one level deeper, the children (c0 - w_s, s <= rr0) of the first enabled
     // row rr0, the frame the DFS enters next, whose own records are then
@@ -1087,9 +1138,13 @@ __device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, co
     desc[half] = false;
     if (r < t.n_rows && mtest(rows, r)) {
       const int64_t c = (int64_t)m - s.w[r];
+      bool reach_c;
+      if (c <= 0) reach_c = false;
+      else if (h.reach) reach_c = reach_bit(h.rv, half ? h.rv.rank1 : h.rv.rank0, c);  // c in R_r (r kept)
+      else reach_c = r >= rec_lo(ld_index(t.index, c));
       if (c == 0) {
         nrow = nrow < r ? nrow : r;
-      } else if (c > 0 && r >= rec_lo(ld_index(t.index, c))) {
+      } else if (reach_c) {
         const HEntry* ce = h.find((uint32_t)c);
         const uint32_t meta = ce ? ce->meta : 0xFFFFu;
         const int hv = (meta & 0xFF) == 0xFF ? -1 : (int)(meta & 0xFF);
@@ -1121,7 +1176,7 @@ __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Fra
                                 uint64_t node_budget, uint64_t& nodes, M128 am) {
   const int top = t.n_rows - 1;
   for (int64_t v = a; v <= b; ++v) {
-    if (!((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;
+    if (h.reach ? !reach_bit(h.rv, h.rv.K - 1, v) : !((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;
     bool ne_dummy;
     M128 rest;
     HEntry* e;
@@ -2727,7 +2782,7 @@ __device__ __forceinline__ int lb_scan(int dir, int x) {  // inclusive prefix co
   return x;
 }
 __device__ __forceinline__ M128 lb_uncomputed(const TableArgs& t, const Lds& s, const Hash& h, const HEntry* e,
-                                              uint32_t m, bool& bad) {
+                                              uint32_t m, bool& bad, uint32_t pass) {
   const int lane = threadIdx.x & 63;
   const M128 en{e->en0, e->en1};
   bool u[2], miss = false;
@@ -2738,20 +2793,22 @@ __device__ __forceinline__ M128 lb_uncomputed(const TableArgs& t, const Lds& s, 
     if (r < t.n_rows && mtest(en, r) && m != (uint32_t)s.w[r]) {
       const HEntry* ce = h.find(m - (uint32_t)s.w[r]);  // visited by phase 1 (the edge was taken)
       miss |= ce == nullptr;
-      u[half] = ce && ce->pad == 0;
+      u[half] = ce && ce->pad != pass;
     }
   }
   bad = __ballot(miss) != 0;
   return M128{(uint64_t)__ballot(u[0]), (uint64_t)__ballot(u[1])};
 }
+// pass: the value of `pad` that marks a node computed by this pass (one
+// phase 1 can feed two passes, the lower and the upper bound)
 __device__ int lb_values_wave(const TableArgs& t, const Lds& s, const Hash& h, int8_t* vals, LBWFrame* fr,
-                              HEntry* root_e, uint32_t root, int dir, int dflt) {
+                              HEntry* root_e, uint32_t root, int dir, int dflt, uint32_t pass = 1) {
   const int lane = threadIdx.x & 63;
   const int neutral = dir ? -128 : 127;  // identity of max / min over int8 values
   HEntry* e = root_e;
   uint32_t m = root;
   bool bad = false;
-  M128 u = lb_uncomputed(t, s, h, e, m, bad);
+  M128 u = lb_uncomputed(t, s, h, e, m, bad, pass);
   if (bad) return -3;
   int d = 0;
   for (;;) {
@@ -2761,12 +2818,12 @@ __device__ int lb_values_wave(const TableArgs& t, const Lds& s, const Hash& h, i
       const uint32_t c = m - (uint32_t)s.w[r];
       HEntry* ce = h.find(c);
       if (!ce) return -3;
-      if (ce->pad != 0) continue;  // computed meanwhile, inside an earlier sibling's subtree
+      if (ce->pad == pass) continue;  // computed meanwhile, inside an earlier sibling's subtree
       if (d + 1 >= kMaxDepth) return -2;
       fr[d++] = LBWFrame{u.a, u.b, e, m, 0};
       e = ce;
       m = c;
-      u = lb_uncomputed(t, s, h, e, m, bad);
+      u = lb_uncomputed(t, s, h, e, m, bad, pass);
       if (bad) return -3;
       continue;
     }
@@ -2797,7 +2854,7 @@ __device__ int lb_values_wave(const TableArgs& t, const Lds& s, const Hash& h, i
       const int r = lane + 64 * half;
       if (r < kMaxRows && r >= lo && r <= hv) row[r] = (int8_t)lb_combine(dir, dflt, half ? p1 : p0);
     }
-    e->pad = 1;  // values computed
+    e->pad = pass;  // values computed
     if (d == 0) return 0;
     const LBWFrame f = fr[--d];
     u = M128{f.u0, f.u1};
@@ -2817,11 +2874,12 @@ __device__ __forceinline__ bool lb_window(const LBArgs& q, int64_t i, int64_t& l
   return lo <= hi;
 }
 
-__device__ __forceinline__ int64_t lb_finish(const LBArgs& q, int best) {
+__device__ __forceinline__ int64_t lb_finish(const LBArgs& q, int best, int dir) {
   // mass_table.py:476-484: the default bound becomes 1 (lower) / max_len (upper)
-  if (q.dir == 0) return best >= q.max_len + 1 ? 1 : best;
+  if (dir == 0) return best >= q.max_len + 1 ? 1 : best;
   return best == -1 ? q.max_len : best;
 }
+__device__ __forceinline__ int64_t lb_finish(const LBArgs& q, int best) { return lb_finish(q, best, q.dir); }
 
 __global__ __launch_bounds__(256) void k_length_fast(TableArgs t, LBArgs q) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2906,6 +2964,30 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
     if (q.alpha) {
       const int64_t g = q.spec ? (int64_t)q.spec[i] : 0;
       am = M128{q.alpha[2 * g], q.alpha[2 * g + 1]};
+      if (WAVE && q.reach_bits) {  // the reduced table's pairs from its rows' reachability
+        const int lane = threadIdx.x & 63;
+        const M128 kept = mand(mand(am, rows_upto(t.n_rows - 1)), rows_from(1));
+        const int n_lo = __builtin_popcountll(kept.a);
+        const int r1 = lane + 64;
+        const bool k0 = (kept.a >> lane) & 1ull, k1 = (kept.b >> lane) & 1ull;
+        const int rank0 = k0 ? __builtin_popcountll(kept.a & ((1ull << lane) - 1ull)) : -1;
+        const int rank1 = k1 ? n_lo + __builtin_popcountll(kept.b & ((1ull << lane) - 1ull)) : -1;
+        __shared__ int s_krow[kMaxRows];
+        if (k0) s_krow[rank0] = lane;
+        if (k1) s_krow[rank1] = r1;
+        __syncthreads();
+        h.reach = true;
+        h.rv.bits = q.reach_bits + q.reach_off[g];
+        h.rv.W = q.reach_words[g];
+        h.rv.K = n_lo + __builtin_popcountll(kept.b);
+        h.rv.row0 = lane < h.rv.K ? s_krow[lane] : 0;
+        h.rv.row1 = lane + 64 < h.rv.K ? s_krow[lane + 64] : 0;
+        h.rv.w0 = s.w[h.rv.row0];
+        h.rv.w1 = s.w[h.rv.row1];
+        h.rv.rank0 = rank0;
+        h.rv.rank1 = rank1;
+        __syncthreads();
+      }
     }
     int rc = phase1<WAVE>(t, s, h, fr, a, hi, q.A0, q.node_budget, nodes, am);
     if (rc == -1) {
@@ -2916,26 +2998,37 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
       q.status[i] = SST_ABORTED;
       continue;
     }
-    const int dflt = q.dir ? -1 : q.max_len + 1;
-    int best = dflt;
-    if (lo <= 0 && hi >= 0) best = lb_combine(q.dir, best, 0);  // total_mass == 0 -> 0
-    for (int64_t v = a; v <= hi && rc == 0; ++v) {
-      if (!((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;  // pair(top, v) == 0: default
-      HEntry* e = h.find((uint32_t)v);
-      if (!e) {
-        rc = -3;
-        break;
+    // the value DP over phase 1's DAG: one direction, or (both) the lower
+    // bound then the upper from the same first visits (pass 1, 2)
+    const int n_dir = WAVE && q.both ? 2 : 1;
+    int64_t res[2] = {0, 0};
+    for (int di = 0; di < n_dir && rc == 0; ++di) {
+      const int dir = q.both ? di : q.dir;
+      const uint32_t pass = (uint32_t)di + 1;
+      const int dflt = dir ? -1 : q.max_len + 1;
+      int best = dflt;
+      if (lo <= 0 && hi >= 0) best = lb_combine(dir, best, 0);  // total_mass == 0 -> 0
+      for (int64_t v = a; v <= hi && rc == 0; ++v) {
+        // pair(top, v) == 0: default
+        if (h.reach ? !reach_bit(h.rv, h.rv.K - 1, v) : !((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;
+        HEntry* e = h.find((uint32_t)v);
+        if (!e) {
+          rc = -3;
+          break;
+        }
+        if (e->pad != pass)
+          rc = WAVE ? lb_values_wave(t, s, h, lv, (LBWFrame*)lf, e, (uint32_t)v, dir, dflt, pass)
+                    : lb_values(t, s, h, lv, lf, e, (uint32_t)v, dir, dflt);
+        if (rc == 0) best = lb_combine(dir, best, lv[(size_t)(e - h.e) * kMaxRows + top]);
       }
-      if (e->pad == 0)
-        rc = WAVE ? lb_values_wave(t, s, h, lv, (LBWFrame*)lf, e, (uint32_t)v, q.dir, dflt)
-                  : lb_values(t, s, h, lv, lf, e, (uint32_t)v, q.dir, dflt);
-      if (rc == 0) best = lb_combine(q.dir, best, lv[(size_t)(e - h.e) * kMaxRows + top]);
+      res[di] = lb_finish(q, best, dir);
     }
     if (rc < 0) {
       q.status[i] = SST_ABORTED;
       continue;
     }
-    q.out[i] = lb_finish(q, best);
+    q.out[i] = res[0];
+    if (q.both) q.out_hi[i] = res[1];
     q.status[i] = 0;
   }
 }

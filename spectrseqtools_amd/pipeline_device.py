@@ -12,6 +12,7 @@ SU order of its classify_fragments frame, so a row's slot offset is the
 `index` Predictor.predict gives it (prediction.py:68-72).  PyTorch provides
 the device memory only; every computation is the library's.
 """
+import ctypes
 from dataclasses import dataclass
 
 import numpy as np
@@ -198,6 +199,9 @@ class DeviceBins:
     status: object        # torch int8 [Q]: SST_NONE / EMPTY / SOME (-10 off the pair class when not answered)
     count: object         # torch int32 [Q] candidates
     deferred: dict = None  # the off-pair-class queries' masked explain: n, per max_len group results, tallies
+    q_off_dev: object = None  # torch int64 [S + 1] (the walk's view of the speculative queries)
+    q0_dev: object = None     # torch int32 [S] the START side's count
+    alpha_dev: object = None  # torch int64 [S, 2] the alphabets they were answered on
 
 
 def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=None, max_len=None):
@@ -217,6 +221,7 @@ def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=None, max_len=None)
     dev = rows.su.device
     a = torch.as_tensor(np.ascontiguousarray(alpha, dtype=np.uint64).view(np.int64), device=dev)
     n_q = torch.zeros(max(1, S), dtype=torch.int32, device=dev)
+    n_q0 = torch.zeros(max(1, S), dtype=torch.int32, device=dev)
     q_off = torch.zeros(S + 1, dtype=torch.int64, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     eng = dp_table.device_table.engine
@@ -225,7 +230,8 @@ def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=None, max_len=None)
     torch.cuda.synchronize(dev)
     eng.check(L.sst_bins_count_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(), rows.obs.data_ptr(),
                                       rows.meta.data_ptr(), rows.alive.data_ptr(), rows.rows.data_ptr(),
-                                      float(tolerance), n_q.data_ptr(), q_off.data_ptr(), err.data_ptr()),
+                                      float(tolerance), n_q.data_ptr(), q_off.data_ptr(), err.data_ptr(),
+                                      n_q0.data_ptr()),
               "sst_bins_count_device")
     eng.synchronize()
     _check_err(err)
@@ -249,7 +255,8 @@ def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=None, max_len=None)
               "sst_bins_emit_device")
     eng.synchronize()
     _check_err(err)
-    out = DeviceBins(q_off.cpu().numpy(), status[:total], count[:total])
+    out = DeviceBins(q_off.cpu().numpy(), status[:total], count[:total], q_off_dev=q_off, q0_dev=n_q0,
+                     alpha_dev=a)
     if defer:
         out.deferred = answer_deferred(dp_table, a, d_mass, d_thr, d_spec, d_q, int(n_def.item()), max_len,
                                        status, count)
@@ -295,4 +302,413 @@ def answer_deferred(dp_table, alpha, d_mass, d_thr, d_spec, d_q, n, max_len, sta
         info["groups"].append((L, k))
         info["results"].append((int(s0), res))
     info["order"] = order
+    info["dst"] = qi  # sorted position -> bin-query index
     return info
+
+
+# ---------------------------------------------------------------------------
+# Stage 4: SkeletonBuilder._predict_skeleton's walk on the device
+# (skeleton_building.py:114-196, 372-482; kernels in csrc/sst_skel.hip)
+# ---------------------------------------------------------------------------
+def budgets_pair_ok(dp_table, max_len):
+    """Per spectrum: budgets cannot bind on a pair-class window (<= 2 items):
+    max_modifications = round(0.5 max_len) (common.py:55) and every
+    modification row's cap round(max_len * rate) (mass_explanation.py:158-172)
+    are >= 2 -- the fast-path theorem for the lane's pair-list answers."""
+    masses = dp_table.masses
+    is_mod = np.array([m.is_modification for m in masses])
+    rate = np.array([m.modification_rate for m in masses], dtype=np.float64)
+    ml = np.asarray(max_len, dtype=np.int64).astype(np.float64)
+    A = np.round(dp_table.seq.modification_rate * ml).astype(np.int64)
+    cap_min = (np.round(np.outer(ml, rate[is_mod])).min(axis=1).astype(np.int64) if is_mod.any()
+               else np.full(len(ml), 2, dtype=np.int64))
+    return (A >= 2) & (cap_min >= 2)
+
+
+def name_hashes(dp_table):
+    """hash() of each table row's nucleoside name in this interpreter (the
+    set order the reference's explanation lists follow, common.py:60-65)."""
+    from .mass_explanation import MASS_NAMES
+
+    out = np.zeros(len(dp_table.masses), np.int64)
+    for r, m in enumerate(dp_table.masses):
+        if r == 0:
+            continue
+        names = MASS_NAMES[m.mass]
+        if len(names) != 1:  # mass_explanation.py:302-318 would expand the product of equal-mass names
+            raise NotImplementedError("skeleton walk: an integer mass with several nucleoside names")
+        out[r] = hash(names[0])
+    return out
+
+
+@dataclass
+class DeviceDict:
+    off: object    # torch int64 [S + 1]
+    n: object      # torch int32 [S]
+    key: object    # torch int64 (double bits, ascending per spectrum)
+    thr: object    # torch f64
+
+
+def final_dict_device(dp_table, rows: DeviceRows, alpha_dev, tolerance=None):
+    """filter_by_explanation's final explanation dict of every spectrum
+    (prediction.py:261-329 over the fixpoint's rows and alphabets), as
+    sorted (key, last writer's threshold) lists on the device."""
+    import torch
+
+    tolerance = dp_table.tolerance if tolerance is None else tolerance
+    S = len(rows.rows)
+    dev = rows.su.device
+    eng = dp_table.device_table.engine
+    L = eng._lib
+    h = dp_table.device_table.handle
+    n_q = torch.zeros(max(1, S), dtype=torch.int32, device=dev)
+    off = torch.zeros(S + 1, dtype=torch.int64, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    max_w = _max_weight()
+    args = (h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(), rows.obs.data_ptr(), rows.meta.data_ptr(),
+            rows.alive.data_ptr(), rows.rows.data_ptr())
+    torch.cuda.synchronize(dev)
+    eng.check(L.sst_dict_count_device(*args, float(max_w), float(tolerance), n_q.data_ptr(), off.data_ptr(),
+                                      err.data_ptr()), "sst_dict_count_device")
+    eng.synchronize()
+    total = int(off[S].item())
+    key = torch.empty(max(1, total), dtype=torch.int64, device=dev)
+    thr = torch.empty(max(1, total), dtype=torch.float64, device=dev)
+    n_ent = torch.zeros(max(1, S), dtype=torch.int32, device=dev)
+    eng.check(L.sst_dict_build_device(*args, alpha_dev.data_ptr(), float(max_w), float(tolerance),
+                                      float(dp_table.precision), off.data_ptr(), key.data_ptr(), thr.data_ptr(),
+                                      n_ent.data_ptr(), err.data_ptr()), "sst_dict_build_device")
+    eng.synchronize()
+    _check_err(err)
+    return DeviceDict(off, n_ent, key, thr)
+
+
+def _masked_explain_refs(dp_table, alpha_dev, mass, thr, spec, n, max_len, dst, ptr, cnt, st):
+    """Windows answered by the masked explain on their spectra's alphabets,
+    one pass per max_len group (budgets follow max_len); each window's
+    candidate reference lands at dst[i] of (ptr, cnt, st).  Returns the
+    results (their payload backs the references)."""
+    import torch
+
+    dt = dp_table.device_table
+    eng = dt.engine
+    if n == 0:
+        return []
+    sp_h = spec[:n].cpu().numpy()
+    ml = np.asarray(max_len, dtype=np.int64)[sp_h]
+    order = np.argsort(ml, kind="stable")
+    o = torch.as_tensor(order, device=mass.device)
+    ms, th, sp = mass[:n][o].contiguous(), thr[:n][o].contiguous(), spec[:n][o].contiguous()
+    ds = dst[:n][o].contiguous()
+    ml_s = ml[order]
+    bounds = np.flatnonzero(np.diff(ml_s)) + 1
+    masses = dp_table.masses
+    is_mod = [m.is_modification for m in masses]
+    out = []
+    for s0, s1 in zip(np.concatenate([[0], bounds]).tolist(), np.concatenate([bounds, [n]]).tolist()):
+        Lm = int(ml_s[s0])
+        dt.set_budgets(is_mod, [round(Lm * m.modification_rate) for m in masses])
+        res = dt.explain_alpha_device(ms.data_ptr() + 8 * s0, th.data_ptr() + 8 * s0, sp.data_ptr() + 4 * s0,
+                                      alpha_dev.data_ptr(), s1 - s0, dp_table.tolerance, dp_table.precision,
+                                      round(dp_table.seq.modification_rate * Lm))
+        eng.check(eng._lib.sst_result_refs_device(res.handle, ds.data_ptr() + 8 * s0, ptr.data_ptr(),
+                                                  cnt.data_ptr(), st.data_ptr()), "sst_result_refs_device")
+        out.append(res)
+    return out
+
+
+@dataclass
+class DeviceSkeleton:
+    """_predict_skeleton of both sides of every spectrum (device arrays)."""
+    max_len: np.ndarray   # [S]
+    skel_off: np.ndarray  # [S + 1] exclusive prefix of 2 max_len (positions)
+    skel: object          # torch int64 [2 total, 2]: spectrum g, side sd, position i at skel_off[g] + sd max_len + i
+    min_end: object       # torch int32 [2, slots] (row slots; side 0 START, 1 END)
+    max_end: object
+    kept: object          # torch uint8 [2, slots]: rows the walk did not reject (alive rows of the side)
+    status: np.ndarray    # [2 S] SST_WALK_* per side
+    launches: int         # walk launches (re-query rounds + 1, and big-capacity reruns)
+    requeries: int        # re-query windows the masked explain answered
+    dict_entries: int
+    results: list         # the masked explain results the references point into
+
+
+def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, tolerance=None, caps=(64, 32),
+                    big_caps=(8192, 8192)):
+    """Stage 4 on the device: SkeletonBuilder._predict_skeleton for the START
+    and END rows of every spectrum (the rows the fixpoint kept, its final
+    alphabets `alpha` [S, 2] u64), with filter_by_explanation's final dict.
+    `bins`: stage 3's bins_device(..., max_len=max_len) result (computed here
+    when None).  caps = (explanations per bin, candidates per query) of the
+    lanes' scratch; sides that outgrow them are walked again with big_caps."""
+    import torch
+
+    tolerance = dp_table.tolerance if tolerance is None else tolerance
+    S = len(rows.rows)
+    dev = rows.su.device
+    eng = dp_table.device_table.engine
+    L = eng._lib
+    h = dp_table.device_table.handle
+    max_len = np.ascontiguousarray(np.broadcast_to(np.asarray(max_len, dtype=np.int64), (S,)))
+    if bins is None:
+        bins = bins_device(dp_table, rows, alpha, tolerance=tolerance, max_len=max_len)
+    alpha_dev = bins.alpha_dev
+    dct = final_dict_device(dp_table, rows, alpha_dev, tolerance)
+    Q = int(bins.q_off[-1])
+    s_ptr = torch.zeros(max(1, Q), dtype=torch.int64, device=dev)
+    s_n = torch.zeros(max(1, Q), dtype=torch.int32, device=dev)
+    s_st = torch.full((max(1, Q),), -10, dtype=torch.int8, device=dev)
+    results = []
+    if bins.deferred is not None and bins.deferred["queries"]:
+        d = bins.deferred
+        dst = d["dst"]
+        for s0, res in d["results"]:
+            eng.check(L.sst_result_refs_device(res.handle, dst.data_ptr() + 8 * s0, s_ptr.data_ptr(), s_n.data_ptr(),
+                                               s_st.data_ptr()), "sst_result_refs_device")
+            results.append(res)
+    elif bins.deferred is None:
+        raise ValueError("skeleton_device: stage 3 must answer its off-pair-class queries (bins_device(max_len=...))")
+    ml_t = torch.as_tensor(max_len.astype(np.int32), device=dev)
+    pair_ok = torch.as_tensor(budgets_pair_ok(dp_table, max_len).astype(np.uint8), device=dev)
+    skel_off = np.concatenate([[0], np.cumsum(2 * max_len)]).astype(np.int64)
+    skel = torch.zeros((max(1, int(skel_off[-1])), 2), dtype=torch.int64, device=dev)
+    skel_off_t = torch.as_tensor(skel_off, device=dev)
+    slots = int(rows.su.numel())
+    min_end = torch.zeros((2, slots), dtype=torch.int32, device=dev)
+    max_end = torch.full((2, slots), -1, dtype=torch.int32, device=dev)
+    kept = torch.zeros((2, slots), dtype=torch.uint8, device=dev)
+    side_rows = torch.zeros(2 * slots, dtype=torch.int16, device=dev)
+    status = torch.zeros(max(1, 2 * S), dtype=torch.uint8, device=dev)
+    ctl = torch.zeros(3, dtype=torch.int32, device=dev)  # suspended, big, request count
+    nh = torch.as_tensor(name_hashes(dp_table), device=dev)
+    ml_max = int(max_len.max()) if S else 1
+    len_cap = ml_max + 2
+    if len_cap > 128:
+        raise NotImplementedError("skeleton walk: max_len above 126")
+    pos_cap = _native.pyset_table_size(ml_max + 1)
+    req_cap = max(1 << 16, Q)
+    req_mass = torch.empty(req_cap, dtype=torch.float64, device=dev)
+    req_thr = torch.empty_like(req_mass)
+    req_spec = torch.empty(req_cap, dtype=torch.int32, device=dev)
+    a = _native.WalkArgs()
+    a.peak_off, a.cnt, a.r_su, a.r_ob = (rows.peak_off.data_ptr(), rows.rows.data_ptr(), rows.su.data_ptr(),
+                                         rows.obs.data_ptr())
+    a.r_meta, a.alive, a.alpha, a.max_len = rows.meta.data_ptr(), rows.alive.data_ptr(), alpha_dev.data_ptr(), \
+        ml_t.data_ptr()
+    a.pair_ok, a.n_spec, a.slots = pair_ok.data_ptr(), S, slots
+    a.tol, a.prec, a.rprec = float(tolerance), float(dp_table.precision), 1.0 / float(dp_table.precision)
+    a.d_off, a.d_n, a.d_key, a.d_thr = dct.off.data_ptr(), dct.n.data_ptr(), dct.key.data_ptr(), dct.thr.data_ptr()
+    a.q_off, a.q0 = bins.q_off_dev.data_ptr(), bins.q0_dev.data_ptr()
+    a.s_ptr, a.s_n, a.s_st = s_ptr.data_ptr(), s_n.data_ptr(), s_st.data_ptr()
+    a.req_mass, a.req_thr, a.req_spec = req_mass.data_ptr(), req_thr.data_ptr(), req_spec.data_ptr()
+    a.req_count, a.req_cap = ctl.data_ptr() + 8, req_cap
+    a.name_hash = nh.data_ptr()
+    a.side_rows, a.skel_off, a.skel = side_rows.data_ptr(), skel_off_t.data_ptr(), skel.data_ptr()
+    a.min_end, a.max_end, a.kept = min_end.data_ptr(), max_end.data_ptr(), kept.data_ptr()
+    a.side_status, a.n_suspended, a.n_big = status.data_ptr(), ctl.data_ptr(), ctl.data_ptr() + 4
+    a.pos_cap, a.len_cap = pos_cap, len_cap
+    rounds = []  # per re-query round: (block, ptr, n, st) tensors
+    keep_alive = []
+    mode = {}  # side -> big
+    run = np.arange(2 * S, dtype=np.int32)
+    big = np.zeros(0, np.int32)
+    launches = 0
+    n_req_total = 0
+    torch.cuda.synchronize(dev)
+    while len(run) or len(big):
+        req_block = torch.zeros(max(1, 2 * S), dtype=torch.int64, device=dev)
+        a.req_block = req_block.data_ptr()
+        a.n_rounds = len(rounds)
+        for r, (blk, p_, n_, s_) in enumerate(rounds):
+            a.rq_block[r], a.rq_ptr[r], a.rq_n[r], a.rq_st[r] = (blk.data_ptr(), p_.data_ptr(), n_.data_ptr(),
+                                                                  s_.data_ptr())
+        ctl.zero_()
+        for sides, (e_cap, c_cap) in ((run, caps), (big, big_caps)):
+            if not len(sides):
+                continue
+            t_cap = _native.pyset_table_size(c_cap)
+            stride = _native.walk_scratch_bytes(pos_cap, len_cap, e_cap, c_cap, t_cap)
+            scratch = torch.empty(len(sides) * stride, dtype=torch.uint8, device=dev)
+            sides_t = torch.as_tensor(sides, device=dev)
+            a.sides, a.n_sides = sides_t.data_ptr(), len(sides)
+            a.scratch, a.scratch_stride = scratch.data_ptr(), stride
+            a.expl_cap, a.cand_cap, a.tset_cap = e_cap, c_cap, t_cap
+            eng.check(L.sst_skel_walk_device(h, ctypes.byref(a)), "sst_skel_walk_device")
+            keep_alive.append((scratch, sides_t))
+            launches += 1
+        eng.synchronize()
+        keep_alive.clear()
+        n_susp, n_big, n_req = (int(x) for x in ctl.cpu().tolist())
+        st_h = status.cpu().numpy()
+        was_big = np.zeros(2 * S, bool)
+        was_big[big] = True
+        new_big = np.flatnonzero((st_h == _native.WALK_BIG) & ~was_big).astype(np.int32)
+        st_h[big[st_h[big] == _native.WALK_BIG]] = _native.WALK_LIMIT  # outgrew the big capacities too
+        if len(big):
+            status[torch.as_tensor(big.astype(np.int64), device=dev)] = torch.as_tensor(st_h[big], device=dev)
+        susp = np.flatnonzero(st_h == _native.WALK_SUSPENDED).astype(np.int32)
+        run = susp[~was_big[susp]]
+        big = np.concatenate([susp[was_big[susp]], new_big]).astype(np.int32)
+        if n_req:
+            if len(rounds) >= _native.WALK_MAX_ROUNDS:
+                break
+            if n_req > req_cap:
+                raise _native.EngineError("skeleton walk: re-query list overflow")
+            p_ = torch.zeros(n_req, dtype=torch.int64, device=dev)
+            n_ = torch.zeros(n_req, dtype=torch.int32, device=dev)
+            s_ = torch.full((n_req,), -10, dtype=torch.int8, device=dev)
+            dst = torch.arange(n_req, dtype=torch.int64, device=dev)
+            res = _masked_explain_refs(dp_table, alpha_dev, req_mass, req_thr, req_spec, n_req, max_len, dst, p_, n_,
+                                       s_)
+            results.extend(res)
+            rounds.append((req_block, p_, n_, s_))
+            n_req_total += n_req
+    return DeviceSkeleton(max_len, skel_off, skel, min_end, max_end, kept, status.cpu().numpy()[:2 * S], launches,
+                          n_req_total, int(dct.n.sum().item()), results)
+
+
+def skeleton_frames(dp_table, rows: DeviceRows, sk: DeviceSkeleton, g):
+    """Spectrum g's walk as the reference's values: per side (START, END) the
+    skeleton (sorted names per position), the kept rows' `index` (their place
+    among the spectrum's rows: Predictor.predict's SU-order index), min_end
+    and max_end -- the fields tests/golden/callers.json.gz records."""
+    from .mass_explanation import MASS_NAMES
+
+    ml = int(sk.max_len[g])
+    off = int(rows.peak_off[g].item()) * 4
+    n = int(rows.rows[g].item())
+    alive = rows.alive[off:off + n].cpu().numpy().astype(bool)
+    meta = rows.meta[off:off + n].cpu().numpy().astype(np.int64)
+    out = {}
+    skel = sk.skel[int(sk.skel_off[g]):int(sk.skel_off[g]) + 2 * ml].cpu().numpy().view(np.uint64)
+    names = [None] + [MASS_NAMES[m.mass][0] for m in dp_table.masses[1:]]
+    for sd, side in enumerate(("START", "END")):
+        pos = []
+        for i in range(ml):
+            m0, m1 = int(skel[sd * ml + i, 0]), int(skel[sd * ml + i, 1])
+            rows_i = [r for r in range(len(names)) if (m0 >> r) & 1 or (r >= 64 and (m1 >> (r - 64)) & 1)]
+            pos.append(sorted(names[r] for r in rows_i))
+        on = alive & (((meta >> (2 + sd)) & 1) == 1)
+        kp = sk.kept[sd, off:off + n].cpu().numpy().astype(bool) & on
+        idx = np.flatnonzero(kp)
+        out[side] = {"skeleton": pos, "kept_index": idx.tolist(),
+                     "min_end": sk.min_end[sd, off + idx].cpu().numpy().tolist() if len(idx) else [],
+                     "max_end": sk.max_end[sd, off + idx].cpu().numpy().tolist() if len(idx) else []}
+    return out
+
+
+# ---------------------------------------------------------------------------
+# Stage 5: select_sequence_length_with_jaccard on the device (its two length
+# bounds on each spectrum's skeleton alphabet) and combine_skeleton_sequences
+# (skeleton_building.py:315-370, 494-516; mass_table.py:343-487)
+# ---------------------------------------------------------------------------
+@dataclass
+class DeviceLength:
+    alpha: np.ndarray     # [S, 2] u64 the skeleton's alphabets
+    lower: np.ndarray     # [S] compute_sequence_length_bound(dir="lower")
+    upper: np.ndarray     # [S] (dir="upper")
+    lb_status: np.ndarray  # [S] 0 ok, else the bound raised (SST_OUT_OF_TABLE / ABORTED / -5)
+    seq_len: np.ndarray   # [S] the chosen length
+    status: np.ndarray    # [S] SST_JAC_*
+    comb_off: np.ndarray  # [S + 1]
+    comb: object          # torch int64 [total, 2] the combined skeleton (masks)
+    reach_batches: int
+
+
+def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=8 << 30):
+    """Stage 5: each spectrum's skeleton alphabet (the canonical rows and the
+    modifications its START / END skeletons name), both length bounds on it
+    (sst_reach_rows_device + sst_length_bounds_reach_device: the reduced
+    table's pairs from its rows' reachability, one replay per spectrum, in
+    batches whose bitsets fit `reach_budget_bytes`, one pass per max_len
+    group), then the Jaccard selection and the combined skeleton (k_jaccard)."""
+    import torch
+
+    dt = dp_table.device_table
+    eng = dt.engine
+    L = eng._lib
+    h = dt.handle
+    S = len(sk.max_len)
+    dev = sk.skel.device
+    ml = sk.max_len.astype(np.int64)
+    ml_t = torch.as_tensor(ml.astype(np.int32), device=dev)
+    skel_off_t = torch.as_tensor(sk.skel_off, device=dev)
+    a_sk = torch.empty((max(1, S), 2), dtype=torch.int64, device=dev)
+    eng.check(L.sst_skeleton_alpha_device(h, S, ml_t.data_ptr(), skel_off_t.data_ptr(), sk.skel.data_ptr(),
+                                          alpha_dev.data_ptr(), a_sk.data_ptr()), "sst_skeleton_alpha_device")
+    alpha_sk = a_sk.cpu().numpy().view(np.uint64)[:S].copy()
+    su = np.asarray(su_seq, dtype=np.float64)
+    ob = np.asarray(obs_seq, dtype=np.float64)
+    prec, tol = dp_table.precision, dp_table.tolerance
+    hi = np.rint(su / prec) + np.ceil(tol * ob / prec)  # the window's top (mass_table.py:354-359)
+    words = (np.maximum(hi, 0).astype(np.int64) >> 5) + 2
+    from .pipeline import mask_rows
+
+    n_rows = len(dp_table.masses)
+    K = mask_rows(alpha_sk, n_rows)[:, 1:].sum(axis=1).astype(np.int64)
+    need = 4 * K * words
+    lower = np.zeros(S, np.int64)
+    upper = np.zeros(S, np.int64)
+    lb_st = np.zeros(S, np.int8)
+    masses = dp_table.masses
+    is_mod = [m.is_modification for m in masses]
+    n_batches = 0
+    g0 = 0
+    while g0 < S:
+        g1, tot = g0, 0
+        while g1 < S and (g1 == g0 or tot + need[g1] <= reach_budget_bytes):
+            tot += int(need[g1])
+            g1 += 1
+        n = g1 - g0
+        off = np.concatenate([[0], np.cumsum(need[g0:g1] // 4)[:-1]]).astype(np.int64)
+        bits = torch.empty(max(1, int(tot // 4)), dtype=torch.int32, device=dev)
+        al_t = torch.as_tensor(alpha_sk[g0:g1].view(np.int64), device=dev).contiguous()
+        w_t = torch.as_tensor(words[g0:g1], device=dev)
+        o_t = torch.as_tensor(off, device=dev)
+        eng.check(L.sst_reach_rows_device(h, al_t.data_ptr(), w_t.data_ptr(), o_t.data_ptr(), n, bits.data_ptr()),
+                  "sst_reach_rows_device")
+        order = np.argsort(ml[g0:g1], kind="stable")
+        ml_s = ml[g0:g1][order]
+        su_t = torch.as_tensor(su[g0:g1][order], device=dev)
+        ob_t = torch.as_tensor(ob[g0:g1][order], device=dev)
+        sp_t = torch.as_tensor(order.astype(np.int32), device=dev)
+        lo_t = torch.zeros(n, dtype=torch.int64, device=dev)
+        up_t = torch.zeros(n, dtype=torch.int64, device=dev)
+        st_t = torch.zeros(n, dtype=torch.int8, device=dev)
+        bnd = np.flatnonzero(np.diff(ml_s)) + 1
+        for s0, s1 in zip(np.concatenate([[0], bnd]).tolist(), np.concatenate([bnd, [n]]).tolist()):
+            Lm = int(ml_s[s0])
+            dt.set_budgets(is_mod, [round(Lm * m.modification_rate) for m in masses])
+            A = round(dp_table.seq.modification_rate * Lm)
+            eng.check(L.sst_length_bounds_reach_device(
+                h, su_t.data_ptr() + 8 * s0, ob_t.data_ptr() + 8 * s0, sp_t.data_ptr() + 4 * s0, al_t.data_ptr(),
+                bits.data_ptr(), o_t.data_ptr(), w_t.data_ptr(), s1 - s0, float(tol), float(prec), Lm, A,
+                lo_t.data_ptr() + 8 * s0, up_t.data_ptr() + 8 * s0, st_t.data_ptr() + s0),
+                "sst_length_bounds_reach_device")
+        idx = g0 + order
+        lower[idx] = lo_t.cpu().numpy()
+        upper[idx] = up_t.cpu().numpy()
+        lb_st[idx] = st_t.cpu().numpy()
+        del bits
+        n_batches += 1
+        g0 = g1
+    # Jaccard + combine
+    comb_off = np.concatenate([[0], np.cumsum(ml)]).astype(np.int64)
+    comb = torch.zeros((max(1, int(comb_off[-1])), 2), dtype=torch.int64, device=dev)
+    lo_d = torch.as_tensor(lower, device=dev)
+    up_d = torch.as_tensor(upper, device=dev)
+    st_d = torch.as_tensor(lb_st, device=dev)
+    su_d = torch.as_tensor(su, device=dev)
+    rm = torch.as_tensor(np.array([m.mass * prec for m in masses], dtype=np.float64), device=dev)
+    co_d = torch.as_tensor(comb_off, device=dev)
+    seq_len = torch.zeros(max(1, S), dtype=torch.int32, device=dev)
+    jst = torch.zeros(max(1, S), dtype=torch.int8, device=dev)
+    from .fragment_classification import MAX_VARIANCE
+
+    ja = _native.JaccardArgs(S, ml_t.data_ptr(), skel_off_t.data_ptr(), sk.skel.data_ptr(), lo_d.data_ptr(),
+                             up_d.data_ptr(), st_d.data_ptr(), su_d.data_ptr(), rm.data_ptr(), co_d.data_ptr(),
+                             comb.data_ptr(), seq_len.data_ptr(), jst.data_ptr(), float(MAX_VARIANCE))
+    eng.check(L.sst_jaccard_device(h, ctypes.byref(ja)), "sst_jaccard_device")
+    eng.synchronize()
+    return DeviceLength(alpha_sk, lower, upper, lb_st, seq_len.cpu().numpy()[:S], jst.cpu().numpy()[:S], comb_off,
+                        comb, n_batches)

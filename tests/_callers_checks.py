@@ -266,3 +266,64 @@ def check_skeleton_vs_reference(rec, dp, frags, expl):
         assert seq_len == j["seq_len"]
         assert [sorted(p) for p in combine_skeleton_sequences(seq_len, start_sk, end_sk)] == j["combined"]
     return seq_len
+
+
+def device_pipeline_skeleton(rec, dp):
+    """The device-resident stages on one reference spectrum, in its own peak
+    order: classify_device -> fixpoint_device -> bins_device (with the masked
+    explain) -> skeleton_device.  Returns (rows, fixpoint, skeleton)."""
+    import numpy as np
+
+    from spectrseqtools_amd import pipeline_device as PD
+
+    cols = rec["input"]["columns"]
+    inp = {c: [r[i] for r in rec["input"]["rows"]] for i, c in enumerate(cols)}
+    obs = np.asarray(inp["observed_mass" if "observed_mass" in inp else "neutral_mass"], dtype=np.float64)
+    inten = np.asarray(inp["intensity"], dtype=np.float64) if "intensity" in inp else None
+    bd = build_breakage_dict(*rec["tags"])
+    rows = PD.classify_device(dp, obs, [0, len(obs)], [dp.seq.su_mass], bd, intensity=inten,
+                              intensity_cutoff=rec["intensity_cutoff"])
+    fx = PD.fixpoint_device(dp, rows, [dp.seq.max_len])
+    bins = PD.bins_device(dp, rows, fx.alpha, max_len=[dp.seq.max_len])
+    sk = PD.skeleton_device(dp, rows, fx.alpha, [dp.seq.max_len], bins=bins)
+    return rows, fx, sk
+
+
+def check_skeleton_device_vs_reference(rec, dp):
+    """skeleton_device (k_skel_walk) == the reference's _predict_skeleton per
+    side (callers.json.gz "skeleton"): skeleton, kept fragments, min_end,
+    max_end.  Run under the reference run's hash seed."""
+    from spectrseqtools_amd import _native
+    from spectrseqtools_amd import pipeline_device as PD
+
+    rows, fx, sk = device_pipeline_skeleton(rec, dp)
+    assert (sk.status == _native.WALK_DONE).all(), sk.status
+    got = PD.skeleton_frames(dp, rows, sk, 0)
+    for side in ("START", "END"):
+        w = rec["skeleton"][side]
+        assert got[side]["skeleton"] == w["skeleton"], (side, got[side]["skeleton"], w["skeleton"])
+        assert got[side]["kept_index"] == w["kept_index"], side
+        assert got[side]["min_end"] == w["min_end"], side
+        assert got[side]["max_end"] == w["max_end"], side
+    # stage 5: the skeleton alphabet, both length bounds on it, the Jaccard
+    # length and the combined skeleton (select_sequence_length_with_jaccard)
+    bins_alpha = PD.bins_device(dp, rows, fx.alpha).alpha_dev
+    ln = PD.length_device(dp, sk, bins_alpha, [dp.seq.su_mass], [dp.seq.obs_mass])
+    j = rec["skeleton"]["jaccard"]
+    from spectrseqtools_amd.pipeline import mask_rows
+
+    kept = mask_rows(ln.alpha, len(dp.masses))[0]
+    assert [0] + [dp.masses[r].mass for r in range(1, len(dp.masses)) if kept[r]] == j["masses"]
+    assert [["lower", int(ln.lower[0])], ["upper", int(ln.upper[0])]] == j["bounds"], (ln.lower, ln.upper, j["bounds"])
+    if j["error"] is None:
+        assert int(ln.status[0]) == _native.JAC_OK, int(ln.status[0])
+        assert int(ln.seq_len[0]) == j["seq_len"]
+        from spectrseqtools_amd.mass_explanation import MASS_NAMES
+
+        names = [None] + [MASS_NAMES[m.mass][0] for m in dp.masses[1:]]
+        comb = ln.comb[:int(ln.seq_len[0])].cpu().numpy().view(np.uint64)
+        got_c = [sorted(names[r] for r in range(1, len(names)) if (int(c[r >> 6]) >> (r & 63)) & 1) for c in comb]
+        assert got_c == j["combined"]
+    else:
+        assert int(ln.status[0]) == _native.JAC_NO_LENGTH, (int(ln.status[0]), j["error"])
+    return sk

@@ -5,7 +5,7 @@ jaccard on the filter's output equal the reference's own results
 (callers.json.gz "skeleton").  Explanation lists follow Python set order in
 the reference and in the mirror alike, so the hash seed must match.
 
-usage: python tests/_skeleton_check.py TEST_ID [cpu|gpu]
+usage: python tests/_skeleton_check.py TEST_ID [cpu|gpu|device]
 TEST INFRASTRUCTURE."""
 import os
 import sys
@@ -23,7 +23,11 @@ def main():
     from conftest import load_golden
 
     engine = None
-    if mode == "cpu":
+    if mode == "device":
+        from spectrseqtools_amd import _native
+
+        engine = _native.get_engine(0)
+    elif mode == "cpu":
         import _fake_engine
 
         _fake_engine.install(pytest.MonkeyPatch())
@@ -33,6 +37,10 @@ def main():
         engine = _native.get_engine(0)
     rec = load_golden("callers.json.gz")[tc]
     dp = C.make_dp(rec["ctx"], engine=engine)
+    if mode == "device":  # the device-resident pipeline (k_skel_walk)
+        sk = C.check_skeleton_device_vs_reference(rec, dp)
+        print(f"skeleton ok {tc} device launches={sk.launches} requeries={sk.requeries}")
+        return
     C.check_classify(rec, dp)
     frags, expl = C.check_filter(rec, dp)
     C.check_skeleton_vs_reference(rec, dp, frags, expl)

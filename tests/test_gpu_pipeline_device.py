@@ -185,3 +185,23 @@ def test_device_bins_deferred_vs_rebuilt_tables(engine):
             n_checked += 1
     assert n_checked > 50 and n_some > 10
 
+
+
+@pytest.mark.parametrize("tc", SPECTRA)
+def test_device_skeleton_walk_vs_reference(tc):
+    """Stage 4 on the device (k_skel_walk after classify / fixpoint / bins on
+    the device): each side's skeleton, kept fragments, min_end and max_end ==
+    the reference's own SkeletonBuilder._predict_skeleton (callers.json.gz),
+    under the reference run's hash seed (child process on GPU 0: the lanes
+    order explanations as CPython's sets do, from this interpreter's name
+    hashes; test_04 / test_08 depend on that order)."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PYTHONHASHSEED="0")
+    p = subprocess.run([sys.executable, os.path.join(here, "_skeleton_check.py"), tc, "device"], env=env,
+                       capture_output=True, text=True, timeout=250)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert f"skeleton ok {tc} device" in p.stdout
