@@ -234,8 +234,8 @@ def main():
     from spectrseqtools_amd import _native
     from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
     from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
-    from spectrseqtools_amd.parallel import (Gatherer, canonical_digest, decode_hits, dist_env, wire_unpack,
-                                             wire_used_bytes)
+    from spectrseqtools_amd.parallel import (WIRE_HEADER, Gatherer, canonical_digest, decode_hits, dist_env,
+                                             wire_unpack, wire_used_bytes)
 
     rank, world, local = dist_env()
     if world != args.gpus:
@@ -309,6 +309,8 @@ def main():
     gathered = [None, None]
     wbuf = [None, None]
     expect = [None] * R  # per batch: (n_hits, payload bytes) of its reference pass
+    wire_sizes = []  # per delivered step: every rank's agreed wire bytes
+    hdr_host = None
 
     def settle(r, b):
         nh, nb = r.settle()
@@ -336,6 +338,14 @@ def main():
         ev = torch.cuda.Event()
         ev.record(packer)
         copied[j & 1] = ev
+        # this step's wire size (the packed header: fixed part + its list),
+        # agreed with one all_gather of an int64 per rank inside the timed loop
+        # (RCCL has no gatherv: the gather then moves the largest rank's size)
+        with torch.cuda.stream(packer):
+            hdr_host.copy_(wbuf[j & 1][:WIRE_HEADER], non_blocking=True)
+        ev.synchronize()
+        sizes = gath.agree(wire_used_bytes(hdr_host.numpy()), capacity=wbuf[j & 1].numel())
+        wire_sizes.append(sizes)
         with torch.cuda.stream(comm):
             comm.wait_event(ev)
             gath.gather(wbuf[j & 1])
@@ -423,17 +433,13 @@ def main():
                      "canon": canonical_digest(rr.status, rr.count, rr.offset, rr.payload) if gath is not None
                      else None, "n_hits": expect[b][0],
                      "pair_hits": rr.pair_hits_device()[1] if args.fused_step else 0,
-                     "used": None, "wire_list": None})
+                     "cap": None})
         if gath is not None:
-            # the wire size: the fixed part (host-known) + the reference pass's list
+            # the wire buffer's capacity: the fixed part (host-known from the
+            # result's sizes) + a list slot for every query and hit (the bound
+            # sst_wire_pack accepts); each timed step agrees its used size
             fixed = rr.wire_pack(outs7[0].data_ptr(), n7s[b])
-            probe = torch.empty(fixed + 8 * (n7s[b] + n8s[b] + expect[b][0]), dtype=torch.uint8, device=dev_t)
-            torch.cuda.synchronize()
-            rr.wire_pack(outs7[0].data_ptr(), n7s[b], probe.data_ptr(), probe.numel())
-            engine.synchronize()
-            hdr = probe[:128].cpu().numpy()
-            refs[b]["used"], refs[b]["wire_list"] = wire_used_bytes(hdr), int(hdr.view(np.uint64)[9])
-            del probe
+            refs[b]["cap"] = fixed + 8 * (n7s[b] + n8s[b] + expect[b][0])
         if b == int(np.argmax(n8s)):
             results[0] = rr  # the result sets get the capacity of the largest batch
         else:
@@ -442,8 +448,9 @@ def main():
     results[1].settle()
     if gath is not None:
         precs = tdev.pair_records()
-        gath.agree(max(rf["used"] for rf in refs))
-        wbuf = [torch.empty(gath.max, dtype=torch.uint8, device=dev_t) for _ in range(2)]
+        cap_w = max(rf["cap"] for rf in refs)
+        wbuf = [torch.empty(cap_w, dtype=torch.uint8, device=dev_t) for _ in range(2)]
+        hdr_host = torch.empty(WIRE_HEADER, dtype=torch.uint8).pin_memory()
         torch.cuda.synchronize()
     for k in range(args.warmup):
         step(k)
@@ -461,6 +468,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     settled["n"] = settled["sent"] = 0
+    wire_sizes.clear()  # the timed steps' agreed sizes
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(k)
@@ -636,7 +644,7 @@ def main():
     res = results[(args.steps - 1) & 1]
     some = (st == 2) | (st == -2)
     n_hits0 = refs[timed_batches[-1]]["n_hits"]
-    wire_list = refs[timed_batches[-1]]["wire_list"]
+    ws_arr = np.asarray(wire_sizes, dtype=np.int64) if wire_sizes else None  # [delivered steps, ranks]
     ms_step = 1e3 * elapsed / args.steps
     value = peaks_all / (elapsed / args.steps)
 
@@ -682,8 +690,10 @@ def main():
                              f"v5, sst_wire_pack), overlapped with the next step"
                              if gath is not None else f"spectra sharded over {world} GPUs, results kept per rank")
                             if world > 1 else "1 GPU"),
-            "wire_bytes_per_rank_step": (gath.sizes if gath is not None else None),
-            "wire_list_entries_rank0": (wire_list if gath is not None else None),
+            "wire_bytes_per_rank_step": ({"mean": ws_arr.mean(axis=0).tolist(), "max": ws_arr.max(axis=0).tolist(),
+                                          "steps": int(len(ws_arr)),
+                                          "agreed": "per timed step: all_gather of each rank's packed size"}
+                                         if ws_arr is not None else None),
         },
         "roofline": {
             "bound": "hbm",

@@ -2749,7 +2749,7 @@ extern "C" int sst_reach_rows_device(sst_table* t, const uint64_t* d_alpha, cons
   if (!t || n_spec < 0 || (n_spec > 0 && (!d_alpha || !d_words || !d_off || !d_bits))) return SST_E_ARG;
   if (t->args.w_min < 1024) return fail(t->ctx, SST_E_ARG, "reach rows: row masses below 1024 (the LDS ring)");
   for (int r = 1; r < t->n_rows; ++r)
-    if (t->masses[r] >= (1 << 19)) return fail(t->ctx, SST_E_ARG, "reach rows: a row mass of 2^19 or more");
+    if (t->masses[r] >= (1 << 20)) return fail(t->ctx, SST_E_ARG, "reach rows: a row mass of 2^20 or more");
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;

@@ -73,7 +73,11 @@ class Gatherer:
         self.sizes = None
         self.recv = None
 
-    def agree(self, nbytes):
+    def agree(self, nbytes, capacity=None):
+        """All-gather every rank's byte count (one int64 each); rank 0 keeps
+        receive buffers of `capacity` bytes (default: the agreed maximum) and
+        reuses them while later agreements fit (a per-step agreement costs the
+        one small all_gather, no allocation)."""
         import torch
 
         t = torch.tensor([int(nbytes)], dtype=torch.int64, device=self.device)
@@ -82,8 +86,10 @@ class Gatherer:
         self.sizes = [int(x.item()) for x in out]
         self.max = max(self.sizes) if self.sizes else 0
         if self.dist.get_rank() == 0:
-            self.recv = [torch.empty(self.max, dtype=torch.uint8, device=self.device)
-                         for _ in range(self.dist.get_world_size())]
+            cap = max(self.max, int(capacity or 0))
+            if self.recv is None or self.recv[0].numel() < self.max:
+                self.recv = [torch.empty(cap, dtype=torch.uint8, device=self.device)
+                             for _ in range(self.dist.get_world_size())]
         return self.sizes
 
     def gather(self, buf):
@@ -95,8 +101,10 @@ class Gatherer:
         if buf.numel() < self.max:
             pad = torch.zeros(self.max - buf.numel(), dtype=torch.uint8, device=buf.device)
             buf = torch.cat([buf, pad])
+        elif buf.numel() > self.max:  # a buffer with room past its used bytes: send the agreed size only
+            buf = buf[:self.max]
         if rank == 0:
-            self.dist.gather(buf, gather_list=self.recv, dst=0)
+            self.dist.gather(buf, gather_list=[r[:self.max] for r in self.recv], dst=0)
             self.last = [r[:n] for r, n in zip(self.recv, self.sizes)]
             return self.last
         self.dist.gather(buf, dst=0)

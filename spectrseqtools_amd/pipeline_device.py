@@ -26,6 +26,43 @@ ERR_BITS = {1: "a spectrum has more than 1024 peaks", 2: "a spectrum has more th
             16: "an explanation dict too large for the LDS hash", 32: "rows out of mass order"}
 
 
+def _one_stream(fn):
+    """Run a stage with the engine and PyTorch on one stream.  The stages mix
+    engine launches (the ctx's stream) with PyTorch uploads, fills and reads
+    (the caller's current stream); on two streams a kernel could read an
+    input before its upload lands, or a read see a buffer before the kernel
+    that fills it has run.  The stage runs on a private stream that first
+    waits for the caller's, with the engine queued on it
+    (sst_ctx_set_stream); the caller's stream waits for it at the end."""
+    import functools
+
+    @functools.wraps(fn)
+    def run(dp_table, *args, **kw):
+        import torch
+
+        eng = dp_table.device_table.engine
+        dev = torch.device("cuda", eng.device)
+        st = _STREAMS.get(eng.device)
+        if st is None:
+            st = _STREAMS[eng.device] = torch.cuda.Stream(device=dev)
+        caller = torch.cuda.current_stream(dev)
+        prev = getattr(eng, "_stage_stream", None)  # an enclosing stage's (stages nest)
+        st.wait_stream(caller)
+        try:
+            with torch.cuda.stream(st):
+                eng.set_stream(st.cuda_stream)
+                eng._stage_stream = st.cuda_stream
+                return fn(dp_table, *args, **kw)
+        finally:
+            eng.set_stream(prev)
+            eng._stage_stream = prev
+            caller.wait_stream(st)
+    return run
+
+
+_STREAMS = {}
+
+
 def _check_err(err):
     e = int(err.item())
     if e:
@@ -45,6 +82,7 @@ class DeviceRows:
     names: list        # breakage label per code
 
 
+@_one_stream
 def classify_device(dp_table, obs, offsets, su_seq, breakage_dict, intensity=None, intensity_cutoff=0.5e6,
                     mass_cutoff=50000, keep_valid=False, device=None):
     """Stage 1 on the device.  obs: every spectrum's peaks (spectrum g:
@@ -102,6 +140,7 @@ class DeviceFixpoint:
     n_rounds: int
 
 
+@_one_stream
 def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=None, record=False):
     """Stage 2 on the device: Predictor.filter_by_explanation (prediction.py:
     170-202) for every spectrum, one sst_fix_round_device + one
@@ -204,6 +243,7 @@ class DeviceBins:
     alpha_dev: object = None  # torch int64 [S, 2] the alphabets they were answered on
 
 
+@_one_stream
 def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=None, max_len=None):
     """Stage 3 on the device (SkeletonBuilder._predict_skeleton's bins,
     skeleton_building.py:114-160) over the rows the fixpoint kept
@@ -349,6 +389,7 @@ class DeviceDict:
     thr: object    # torch f64
 
 
+@_one_stream
 def final_dict_device(dp_table, rows: DeviceRows, alpha_dev, tolerance=None):
     """filter_by_explanation's final explanation dict of every spectrum
     (prediction.py:261-329 over the fixpoint's rows and alphabets), as
@@ -433,6 +474,7 @@ class DeviceSkeleton:
     results: list         # the masked explain results the references point into
 
 
+@_one_stream
 def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, tolerance=None, caps=(64, 32),
                     big_caps=(8192, 8192)):
     """Stage 4 on the device: SkeletonBuilder._predict_skeleton for the START
@@ -615,6 +657,7 @@ class DeviceLength:
     reach_batches: int
 
 
+@_one_stream
 def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=8 << 30):
     """Stage 5: each spectrum's skeleton alphabet (the canonical rows and the
     modifications its START / END skeletons name), both length bounds on it
@@ -712,3 +755,72 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     eng.synchronize()
     return DeviceLength(alpha_sk, lower, upper, lb_st, seq_len.cpu().numpy()[:S], jst.cpu().numpy()[:S], comb_off,
                         comb, n_batches)
+
+
+# ---------------------------------------------------------------------------
+# Per-spectrum outcomes, packed for the gather to rank 0 (config 5 on N GPUs)
+# ---------------------------------------------------------------------------
+OUTCOME_MAGIC = 0x35435453  # "STC5"
+
+
+def pack_outcomes(rows: DeviceRows, fx, sk: DeviceSkeleton, ln: DeviceLength):
+    """One rank's config-5 outcome per spectrum as one uint8 device tensor:
+    the fixpoint's and the skeleton's alphabets, both length bounds and their
+    status, the Jaccard length and status, the walk's per-side status, the
+    rows each side's walk kept (a bit per row slot), and the combined
+    skeleton (max_len positions reserved per spectrum, seq_len used)."""
+    import torch
+
+    dev = sk.skel.device
+    S = len(sk.max_len)
+    u8 = lambda t: t.contiguous().view(torch.uint8).reshape(-1)  # noqa: E731
+    host = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=dev)  # noqa: E731
+    kept = (sk.kept & rows.alive.view(1, -1)).reshape(-1)
+    pad = (-kept.numel()) % 8
+    if pad:
+        kept = torch.cat([kept, torch.zeros(pad, dtype=torch.uint8, device=dev)])
+    weights = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.int32, device=dev)
+    kept_bits = (kept.view(-1, 8).to(torch.int32) * weights).sum(dim=1).to(torch.uint8)
+    head = np.array([OUTCOME_MAGIC, S, int(rows.su.numel()), int(sk.skel_off[-1]), int(ln.comb_off[-1]),
+                     int(kept_bits.numel()), 0, 0], dtype=np.int64)
+    parts = [host(head), host(np.asarray(fx.alpha, dtype=np.uint64).view(np.int64)),
+             host(ln.alpha.view(np.int64)), host(ln.lower), host(ln.upper), host(ln.lb_status),
+             host(ln.seq_len.astype(np.int32)), host(ln.status), host(sk.status), host(sk.max_len.astype(np.int32)),
+             ln.comb[:int(ln.comb_off[-1])], kept_bits]
+    return torch.cat([u8(p) for p in parts])
+
+
+def unpack_outcomes(buf):
+    """pack_outcomes' bytes (host numpy uint8) -> dict of numpy arrays."""
+    b = np.asarray(buf, dtype=np.uint8)
+    head = b[:64].view(np.int64)
+    if int(head[0]) != OUTCOME_MAGIC:
+        raise ValueError("not a config-5 outcome buffer")
+    S, slots, _, n_comb, n_kept = (int(x) for x in head[1:6])
+    o = 64
+    out = {}
+
+    def take(name, dtype, count):
+        nonlocal o
+        nb = np.dtype(dtype).itemsize * count
+        out[name] = b[o:o + nb].view(dtype).copy()
+        o += nb
+
+    take("alpha", np.uint64, 2 * S)
+    take("alpha_skeleton", np.uint64, 2 * S)
+    take("lower", np.int64, S)
+    take("upper", np.int64, S)
+    take("lb_status", np.int8, S)
+    take("seq_len", np.int32, S)
+    take("status", np.int8, S)
+    take("walk_status", np.uint8, 2 * S)
+    take("max_len", np.int32, S)
+    take("combined", np.uint64, 2 * n_comb)
+    take("kept_bits", np.uint8, n_kept)
+    out["kept"] = np.unpackbits(out.pop("kept_bits"), bitorder="little")[:2 * slots].reshape(2, slots)
+    out["alpha"] = out["alpha"].reshape(S, 2)
+    out["alpha_skeleton"] = out["alpha_skeleton"].reshape(S, 2)
+    out["combined"] = out["combined"].reshape(-1, 2)
+    if o != len(b):
+        raise ValueError("outcome buffer size mismatch")
+    return out

@@ -75,3 +75,32 @@ def test_two_rank_gathered_step_vs_oracle(tmp_path):
         for i in rng.choice(np.flatnonzero(some), 1500, replace=False):
             _, sols, _, _ = oracle.explain_table(host, 32, alph, inp["a8_mass"][i], inp["a8_thr"][i], 1e-5, A)
             assert candidates(pay, cnt, off, i) == sols, (r, i)
+
+
+def test_two_rank_pipeline_outcomes_vs_single_rank(tmp_path):
+    """Config 5 sharded: tools/pipeline_bench.py as two ranks on GPU 0 (gloo),
+    every stage device-resident through the skeleton walk and the length
+    selection, each rank's per-spectrum outcomes gathered to rank 0; each
+    rank's gathered bytes equal a single-process run on that rank's spectra."""
+    from spectrseqtools_amd.pipeline_device import unpack_outcomes
+
+    multi, single = str(tmp_path / "multi"), str(tmp_path / "single")
+    env = dict(os.environ, SST_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    bench = os.path.join(REPO, "tools", "pipeline_bench.py")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), bench, "--spectra", "400", "--backend", "gloo",
+           "--dump-outcomes", multi]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=REPO)
+    assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
+    assert '"n_gpus": 2' in line and '"gather"' in line
+    for r in range(2):
+        p = subprocess.run([sys.executable, bench, "--spectra", "400", "--as-rank", str(r), "--dump-outcomes", single],
+                           env=dict(os.environ, SST_DEVICE="0"), capture_output=True, text=True, timeout=250,
+                           cwd=REPO)
+        assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
+        got = np.load(os.path.join(multi, f"outcome_rank{r}.npy"))
+        want = np.load(os.path.join(single, f"outcome_rank{r}.npy"))
+        assert np.array_equal(got, want), r
+        o = unpack_outcomes(got)
+        assert len(o["seq_len"]) == 400 and (o["status"] == 0).sum() > 200 and (o["walk_status"] == 0).all()

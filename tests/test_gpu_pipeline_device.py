@@ -10,6 +10,8 @@ sst_classify_rows_device, sst_fix_round_device, sst_valid_rows_alpha_device):
     mirrors in the CPU suite), and the device skeleton-bin answers equal the
     host-built bin queries (pipeline.bin_queries) answered on the same
     alphabets."""
+import os
+
 import numpy as np
 import pytest
 
@@ -205,3 +207,210 @@ def test_device_skeleton_walk_vs_reference(tc):
                        capture_output=True, text=True, timeout=250)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert f"skeleton ok {tc} device" in p.stdout
+
+
+def _mirror_outcome(obs, su_seq, obs_seq, max_len, engine):
+    """The per-spectrum host mirrors (pinned to the reference on its own test
+    spectra): classify_fragments, Predictor.filter_by_explanation,
+    SkeletonBuilder._predict_skeleton per side and
+    select_sequence_length_with_jaccard with combine_skeleton_sequences."""
+    from spectrseqtools_amd.fragment_classification import classify_fragments
+    from spectrseqtools_amd.frame import Frame
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict
+    from spectrseqtools_amd.prediction import Predictor
+    from spectrseqtools_amd.skeleton_building import SkeletonBuilder, combine_skeleton_sequences
+
+    seq = SequenceInformation(max_len=int(max_len), su_mass=float(su_seq), obs_mass=float(obs_seq),
+                              modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=engine)
+    bd = build_breakage_dict(555.1294, 455.1491)
+    fr = classify_fragments(Frame({"observed_mass": list(map(float, obs))}), dp, bd)
+    f = C.prepared(fr)
+    pred = Predictor(dp, EXPLANATION_MASSES)
+    frags, expl = pred.filter_by_explanation(f)
+    sb = SkeletonBuilder(explanations=expl, dp_table=dp)
+    out, sks = {}, {}
+    for side in ("START", "END"):
+        sub = frags.filter_mask([side in b for b in frags.get_column("breakage").to_list()])
+        sk, fs = sb._predict_skeleton(Frame(sub.to_dict()), [set() for _ in range(dp.seq.max_len)])
+        out[side] = {"skeleton": [sorted(p) for p in sk], "kept_index": fs.get_column("index").to_list(),
+                     "min_end": fs.get_column("min_end").to_list(), "max_end": fs.get_column("max_end").to_list()}
+        sks[side] = sk
+    try:
+        seq_len = sb.select_sequence_length_with_jaccard(start_skeleton=sks["START"], end_skeleton=sks["END"][::-1])
+        out["seq_len"] = seq_len
+        out["combined"] = [sorted(p) for p in combine_skeleton_sequences(seq_len, sks["START"], sks["END"][::-1])]
+    except IndexError:
+        out["seq_len"], out["combined"] = "IndexError", None
+    except Exception:  # noqa: BLE001 -- the reference raises a bare Exception when no length fits
+        out["seq_len"], out["combined"] = None, None
+    out["masses"] = [m.mass for m in dp.masses]
+    return out
+
+
+@pytest.mark.parametrize("variant", ["full_ladders", "short_fragments_missing"])
+def test_device_skeleton_and_length_vs_mirror(engine, variant):
+    """Stages 4-5 on the device over synthetic spectra against the
+    per-spectrum host mirrors in this process (same interpreter, same hash
+    seed): each side's skeleton, kept rows, min_end / max_end, the skeleton
+    alphabet, the Jaccard length and the combined skeleton.  Without their
+    short fragments, spectra need first bins of whole masses of 3+ nucleotides
+    and re-queries against older bins (the masked explain, suspended lanes)."""
+    from spectrseqtools_amd import _native, pipeline, pipeline_device as PD
+    from spectrseqtools_amd.mass_explanation import MASS_NAMES
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict
+    from spectrseqtools_amd.synthetic import make_spectra
+
+    n = 48
+    b = make_spectra(n, seed=41 if variant == "full_ladders" else 43, len_range=(6, 14))
+    spec = np.repeat(np.arange(n), np.diff(b.offsets))
+    keep = np.ones(len(b.observed), bool)
+    if variant != "full_ladders":
+        keep = (spec % 3 == 0) | (b.observed > 1300.0)
+    obs = b.observed[keep]
+    offsets = np.concatenate([[0], np.cumsum(np.bincount(spec[keep], minlength=n))])
+    bd = build_breakage_dict(555.1294, 455.1491)
+    w_full = [k for k, v in bd.items() if "START_END" in v][0]
+    su_seq = b.seq_mass - w_full * TOLERANCE
+    seq = SequenceInformation(max_len=20, su_mass=float(su_seq[0]), obs_mass=float(b.seq_mass[0]),
+                              modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=engine)
+    max_len = pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:]))
+    rows = PD.classify_device(dp, obs, offsets, su_seq, bd)
+    fx = PD.fixpoint_device(dp, rows, max_len)
+    bins = PD.bins_device(dp, rows, fx.alpha, max_len=max_len)
+    sk = PD.skeleton_device(dp, rows, fx.alpha, max_len, bins=bins)
+    ln = PD.length_device(dp, sk, bins.alpha_dev, su_seq, b.seq_mass)
+    names = [None] + [MASS_NAMES[m.mass][0] for m in dp.masses[1:]]
+    n_len = n_err = 0
+    for g in range(n):
+        want = _mirror_outcome(obs[offsets[g]:offsets[g + 1]], su_seq[g], b.seq_mass[g], max_len[g], engine)
+        assert (sk.status[2 * g:2 * g + 2] == _native.WALK_DONE).all(), (g, sk.status[2 * g:2 * g + 2])
+        got = PD.skeleton_frames(dp, rows, sk, g)
+        for side in ("START", "END"):
+            assert got[side] == want[side], (g, side)
+        kept = pipeline.mask_rows(ln.alpha[g:g + 1], len(dp.masses))[0]
+        assert [0] + [dp.masses[r].mass for r in range(1, len(dp.masses)) if kept[r]] == want["masses"], g
+        if want["seq_len"] is None:
+            assert int(ln.status[g]) == _native.JAC_NO_LENGTH, (g, int(ln.status[g]))
+            n_err += 1
+        elif want["seq_len"] == "IndexError":
+            assert int(ln.status[g]) == _native.JAC_INDEX, g
+            n_err += 1
+        else:
+            assert int(ln.status[g]) == _native.JAC_OK and int(ln.seq_len[g]) == want["seq_len"], \
+                (g, int(ln.status[g]), int(ln.seq_len[g]), want["seq_len"], int(ln.lower[g]), int(ln.upper[g]))
+            L = int(ln.seq_len[g])
+            comb = ln.comb[int(ln.comb_off[g]):int(ln.comb_off[g]) + L].cpu().numpy().view(np.uint64)
+            got_c = [sorted(names[r] for r in range(1, len(names)) if (int(c[r >> 6]) >> (r & 63)) & 1) for c in comb]
+            assert got_c == want["combined"], g
+            n_len += 1
+    assert n_len >= n // 2
+    if variant != "full_ladders":
+        assert sk.requeries > 0 or bins.deferred["queries"] > 0
+
+
+def test_device_fixpoint_rounds_vs_oracle_rebuilt_tables(engine):
+    """Every filter_by_explanation round of the device fixpoint (k_fix_round:
+    the round's window / singleton answers on the spectrum's alphabet, the
+    dict's last-writer semantics, the reduced alphabet; k_valid_alpha: the
+    rows is_valid_mass keeps on the reduced table) on 600 synthetic spectra
+    against the CPU oracle on each round's REBUILT reduced table
+    (set_up_bit_table over the kept rows, mass_table.py:94-121), the queries
+    produced by the host-native sliding window (prediction.py:261-329)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import _oracle as oracle
+    from spectrseqtools_amd import pipeline, pipeline_device as PD
+    from spectrseqtools_amd._native import su_diff_queries
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import (EXPLANATION_MASSES, MATCHING_THRESHOLD, PHOSPHATE_LINK_MASS, TOLERANCE,
+                                           build_breakage_dict)
+    from spectrseqtools_amd.synthetic import make_spectra
+
+    n = 600
+    b = make_spectra(n, seed=53)
+    bd = build_breakage_dict(555.1294, 455.1491)
+    w_full = [k for k, v in bd.items() if "START_END" in v][0]
+    su_seq = b.seq_mass - w_full * TOLERANCE
+    seq = SequenceInformation(max_len=20, su_mass=float(su_seq[0]), obs_mass=float(b.seq_mass[0]),
+                              modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=engine)
+    tol = dp.tolerance
+    max_len = pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:]))
+    rows = PD.classify_device(dp, b.observed, b.offsets, su_seq, bd)
+    fx = PD.fixpoint_device(dp, rows, max_len, record=True)
+    c = PD.to_classified(rows, alive_only=False)  # every classified row, spectrum-major in SU order
+    off = rows.peak_off.cpu().numpy()
+    slot = 4 * off[:-1][c.spec] + (np.arange(len(c.spec)) - c.offsets[c.spec])
+    ms_all = [m.mass for m in dp.masses]
+    N = len(ms_all)
+    is_mod = np.array([m.is_modification for m in dp.masses])
+    rate = [m.modification_rate for m in dp.masses]
+    canon = pipeline.row_masks((~is_mod & (np.arange(N) > 0))[None, :])[0]
+    max_w = max(EXPLANATION_MASSES.get_column("monoisotopic_mass").to_list()) + PHOSPHATE_LINK_MASS
+    side = np.array([("START" in nm) | (("END" in nm) << 1) for nm in c.names], dtype=np.uint8)
+    flags = side[c.brk] | (c.singleton.astype(np.uint8) << 2)
+    tables = {}
+
+    def table(mask):
+        key = (int(mask[0]), int(mask[1]))
+        if key not in tables:
+            rows_k = pipeline.mask_rows(np.asarray(mask, np.uint64)[None, :], N)[0]
+            keep = [0] + [r for r in range(1, N) if rows_k[r]]
+            ms = [ms_all[r] for r in keep]
+            tables[key] = (keep, oracle.build_table(ms, max(ms) * 35, 32))
+        return tables[key]
+
+    def check(task):
+        k, g, alpha_in, alive_in, alpha_out, alive_out = task
+        keep, tab = table(alpha_in)
+        alph = oracle.Alphabet([ms_all[r] for r in keep], [bool(is_mod[r]) for r in keep],
+                               [round(int(max_len[g]) * rate[r]) for r in keep])
+        A = round(dp.seq.modification_rate * int(max_len[g]))
+        idx = np.arange(c.offsets[g], c.offsets[g + 1])[alive_in]
+        d, t, _, kind = su_diff_queries(c.su[idx], c.obs[idx], flags[idx], np.array([0, len(idx)]), max_w, tol)
+        last = {}  # the dict: key -> last writer's answer (rows of its candidates) or None / []
+        for i in range(len(d)):
+            st, sols, n_e, _ = oracle.explain_table(tab, 32, alph, d[i], t[i], tol, A)
+            assert st >= 0, (k, g, i)
+            if kind[i] == 2 or sols:  # singletons always, side pairs with >= 1 explanation
+                last[float(d[i])] = [tuple(keep[x] for x in s) for s in sols]
+        used = np.zeros(N, bool)
+        for v in last.values():
+            for s in v:
+                used[list(s)] = True
+        want = canon | (np.asarray(alpha_in, np.uint64) & pipeline.row_masks(used[None, :])[0])
+        assert np.array_equal(want, alpha_out), (k, g)
+        changed = pipeline.mask_rows(want[None, :], N).sum() != pipeline.mask_rows(
+            np.asarray(alpha_in, np.uint64)[None, :], N).sum()
+        exp_alive = alive_in.copy()
+        if changed:
+            keep2, tab2 = table(want)
+            v = oracle.is_valid_batch(tab2, 32, c.su[idx], tol * c.obs[idx], tol)
+            assert (v >= 0).all(), (k, g)
+            exp_alive[alive_in] = v == 1
+        assert np.array_equal(exp_alive, alive_out), (k, g)
+        return len(d)
+
+    full = pipeline.row_masks((np.arange(N) > 0)[None, :])[0]
+    alpha_prev = np.repeat(full[None, :], n, axis=0)
+    alive_prev = np.ones(len(c.spec), bool)
+    tasks = []
+    for k, (act, alpha_k, alive_k) in enumerate(fx.history):
+        alive_now = alive_k[slot]
+        for g in np.flatnonzero(act):
+            sl = slice(c.offsets[g], c.offsets[g + 1])
+            tasks.append((k, int(g), alpha_prev[g].copy(), alive_prev[sl].copy(), alpha_k[g].copy(),
+                          alive_now[sl].copy()))
+        alpha_prev = alpha_k.copy()
+        alive_prev = alive_now.copy()
+    table(full)  # shared by every first round
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
+        n_q = sum(ex.map(check, tasks))
+    assert len(fx.history) >= 3 and n_q > 100_000 and len(tasks) >= 2 * n

@@ -18,6 +18,17 @@ stages over many synthetic spectra, batched on the GPU engine
            differences -- through the masked explain's DFS roles on each
            spectrum's alphabet, one pass per max_len group; the host-driven
            path counts them)
+  stage 4  SkeletonBuilder._predict_skeleton per side (device-resident path):
+           filter_by_explanation's final dict (k_dict), the walk (k_skel_walk:
+           bins, re-queries against older bins through the masked explain,
+           update_skeleton_for_given_explanations in CPython's set order,
+           min_end / max_end, rejected rows)
+  stage 5  select_sequence_length_with_jaccard: the skeleton alphabet, both
+           compute_sequence_length_bound directions on it (k_reach_rows + one
+           k_length_exact replay per spectrum), the Jaccard length and the
+           combined skeleton (k_jaccard)
+  gather   (N > 1) every rank's per-spectrum outcomes to rank 0
+           (pipeline_device.pack_outcomes, one agreed-size gather)
 
 One process per GPU (torch.distributed.run for N > 1, spectra sharded by
 rank, no collective in the data path); every stage is timed over all of this
@@ -38,6 +49,7 @@ k_pairs_alpha).  Every stage reports its event-timed kernel time and the
 GPU-busy share of its wall time.
 
 Usage: python tools/pipeline_bench.py [--spectra 100000] [--seed 7] [--host-driven]
+       [--backend nccl|gloo] [--dump-outcomes DIR] [--as-rank R]
 """
 import argparse
 import json
@@ -58,6 +70,11 @@ def main():
     ap.add_argument("--host-driven", action="store_true",
                     help="stages 1-2 through the host-driven batched path (pipeline.classify / filter_fixpoint) "
                          "instead of the device-resident one (pipeline_device)")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
+    ap.add_argument("--dump-outcomes", default=None,
+                    help="rank 0 saves the gathered per-spectrum outcomes (one .npy per rank) here")
+    ap.add_argument("--as-rank", type=int, default=None,
+                    help="single process: generate the spectra rank R of a multi-rank run would get")
     args = ap.parse_args()
 
     import torch
@@ -75,7 +92,10 @@ def main():
         import torch.distributed as dist
 
         torch.cuda.set_device(gpu)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
     engine = _native.get_engine(gpu)
 
     def barrier():
@@ -85,12 +105,14 @@ def main():
     def tmax(x):
         if not dist:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=torch.device("cuda", gpu))
+        t = torch.tensor([x], dtype=torch.float64, device=comm_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    comm_dev = torch.device("cuda", gpu) if args.backend == "nccl" else torch.device("cpu")
     t0 = time.perf_counter()
-    batch = make_spectra(args.spectra, seed=args.seed + 1_000_003 * rank)
+    data_rank = rank if args.as_rank is None else args.as_rank
+    batch = make_spectra(args.spectra, seed=args.seed + 1_000_003 * data_rank)
     gen_s = time.perf_counter() - t0
     bd = build_breakage_dict(555.1294, 455.1491)
     w_full = [k for k, v in bd.items() if "START_END" in v][0]
@@ -125,6 +147,8 @@ def main():
         bw = pd.bins_device(dp, rw, fw.alpha, max_len=m0)
         sw = bw.status == 2
         int(sw.sum().item()), int((bw.status == -10).sum().item()), int(bw.count[sw].sum().item())
+        kw = pd.skeleton_device(dp, rw, fw.alpha, m0, bins=bw)
+        pd.length_device(dp, kw, bw.alpha_dev, su_seq[:S0], batch.seq_mass[:S0])
     engine.synchronize()
 
     stages = {}
@@ -217,6 +241,47 @@ def main():
         stages["bins"]["masked_explain_groups"] = [list(x) for x in db.deferred["groups"]]
     stages["bins"]["kernels"] = kernels()
     busy(stages["bins"])
+    outcome = None
+    if rows is not None:  # stages 4-5 (device-resident path)
+        barrier()
+        t0 = time.perf_counter()
+        sk = pd.skeleton_device(dp, rows, fx_alpha, max_len, bins=db)
+        barrier()
+        wst = {int(k): int(v) for k, v in zip(*np.unique(sk.status, return_counts=True))}
+        stages["skeleton"] = {"s": tmax(time.perf_counter() - t0), "sides": 2 * len(max_len),
+                              "walk_status": wst, "walk_launches": sk.launches, "requery_windows": sk.requeries,
+                              "dict_entries": sk.dict_entries, "kernels": kernels()}
+        busy(stages["skeleton"])
+        barrier()
+        t0 = time.perf_counter()
+        ln = pd.length_device(dp, sk, db.alpha_dev, su_seq, batch.seq_mass)
+        barrier()
+        stages["length"] = {"s": tmax(time.perf_counter() - t0), "reach_batches": ln.reach_batches,
+                            "jaccard_status": {int(k): int(v) for k, v in zip(*np.unique(ln.status,
+                                                                                         return_counts=True))},
+                            "lb_status": {int(k): int(v) for k, v in zip(*np.unique(ln.lb_status,
+                                                                                   return_counts=True))},
+                            "mean_seq_len": float(ln.seq_len[ln.status == 0].mean()) if (ln.status == 0).any() else 0,
+                            "kernels": kernels()}
+        busy(stages["length"])
+        barrier()
+        t0 = time.perf_counter()
+        buf = pd.pack_outcomes(rows, fx, sk, ln)
+        if dist:
+            from spectrseqtools_amd.parallel import Gatherer
+
+            gth = Gatherer(dist, comm_dev)
+            sizes = gth.agree(buf.numel())
+            got = gth.gather(buf.to(comm_dev))
+            if rank == 0:
+                outcome = [x.cpu().numpy() for x in got]
+        else:
+            sizes = [int(buf.numel())]
+            outcome = [buf.cpu().numpy()]
+        barrier()
+        stages["gather"] = {"s": tmax(time.perf_counter() - t0), "bytes_per_rank": sizes,
+                            "path": "pack_outcomes + one agreed-size gather to rank 0"
+                                    + (f" ({'RCCL' if args.backend == 'nccl' else 'gloo'})" if dist else " (local)")}
     engine.profile(False)
 
     # per-spectrum alphabet reduction = a table rebuild (canonical + 3 mods)
@@ -240,11 +305,17 @@ def main():
         peaks_all, spectra_all = peaks, args.spectra
     ref_est = (n_valid_q + valid_q_rounds) / 70e3 + (explain_q + stages["bins"]["queries"]) / 4.0e3
     gpu_s = sum(sum(v[0] for v in st["kernels"].values()) / 1e3 for st in stages.values())
+    if rank == 0 and args.dump_outcomes and outcome is not None:
+        os.makedirs(args.dump_outcomes, exist_ok=True)
+        for r, o in enumerate(outcome):
+            np.save(os.path.join(args.dump_outcomes, f"outcome_rank{r if args.as_rank is None else args.as_rank}.npy"),
+                    o)
     if rank == 0:
         print(json.dumps({
-            "workload": "config5: explanation stages of the prediction pipeline (classify_fragments, the "
-                        "filter_by_explanation fixpoint with per-spectrum alphabets, skeleton bin queries on the "
-                        "reduced alphabets) over synthetic spectra",
+            "workload": "config5: the prediction pipeline's explanation stages (classify_fragments, the "
+                        "filter_by_explanation fixpoint with per-spectrum alphabets, skeleton bin queries, the "
+                        "skeleton walk, both length bounds and the Jaccard length on the skeleton alphabets; "
+                        "MILP stages excluded) over synthetic spectra",
             "n_gpus": world, "spectra": spectra_all, "peaks": peaks_all,
             "path": "host-driven" if args.host_driven else "device-resident",
             "stages": stages, "total_s": total_s, "gpu_busy_frac": gpu_s / total_s,
