@@ -454,6 +454,33 @@ int sst_classify_rows_device(sst_table* t, const double* d_obs, const int64_t* d
                              double max_weight, double tolerance, double precision, int8_t* d_valid_out,
                              double* d_rows_su, double* d_rows_ob, uint32_t* d_rows_meta, uint8_t* d_alive,
                              uint32_t* d_rows, uint32_t* d_err);
+/* Budget-binding ("exact mode") spectra of the device pipeline: a spectrum
+ * whose max_modifications or modification caps are < 2 (a small
+ * --modification_rate, or max_len <= 2: mass_explanation.py:158-172) can have
+ * its budgets bind on pair-class windows, where the pair list's answers are
+ * not the reference's.  With x->pair_ok[g] == 0 the stage lists the
+ * spectrum's queries instead of answering them: x->xq_mass / xq_thr /
+ * xq_spec / xq_single[...] in one block per spectrum (x->xq_block[g] = start
+ * << 32 | count; *x->xq_count the list length, x->xq_cap its capacity, d_err
+ * bit 64 on overflow); the caller answers the list with the exact masked
+ * explain (sst_explain_alpha_batch_device, per max_len group) and
+ * sst_result_refs_device into x->xa_st / xa_n / xa_ptr, then runs the stage's
+ * second half (sst_fix_finish_device, sst_dict_build_device).  x may be NULL:
+ * every spectrum's pair-class answers are exact. */
+typedef struct sst_exact_io {
+  const uint8_t* pair_ok;  /* [n_spec] */
+  double* xq_mass;
+  double* xq_thr;
+  int32_t* xq_spec;
+  uint8_t* xq_single;      /* 1: a singleton's query (stored in the dict even when empty) */
+  uint32_t* xq_count;
+  uint64_t xq_cap;
+  uint64_t* xq_block;      /* [n_spec] */
+  const int8_t* xa_st;
+  const uint32_t* xa_n;
+  const uint64_t* xa_ptr;
+} sst_exact_io;
+
 /* One filter_by_explanation round (prediction.py:170-202) of the spectra with
  * d_active[g]: their alive rows' window pairs and singletons explained
  * against d_alpha[2g..2g+1] (row masks of t; the caller keeps budgets from
@@ -467,7 +494,12 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
                          const uint32_t* d_rows, const uint64_t* d_alpha, uint64_t* d_alpha_next,
                          const uint8_t* d_active, uint8_t* d_active_next, uint32_t* d_rounds, uint32_t* d_queries,
                          uint32_t* d_n_active, double max_weight, double tolerance, double precision,
-                         uint32_t* d_err);
+                         uint32_t* d_err, const sst_exact_io* x);
+/* The exact-mode spectra's half of the round, after their listed queries
+ * were answered (same arrays as the round; x required). */
+int sst_fix_finish_device(sst_table* t, int64_t n_spec, const uint64_t* d_alpha, uint64_t* d_alpha_next,
+                          const uint8_t* d_active, uint8_t* d_active_next, uint32_t* d_rounds, uint32_t* d_queries,
+                          uint32_t* d_n_active, uint32_t* d_err, const sst_exact_io* x);
 /* SkeletonBuilder._predict_skeleton's speculative bin queries
  * (skeleton_building.py:114-160; replaces the per-bin explain calls of
  * :131-160 for every spectrum at once) over the rows a fixpoint kept
@@ -494,7 +526,7 @@ int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
                          const uint32_t* d_rows, const uint64_t* d_alpha, double tol, double prec,
                          const uint64_t* d_q_off, int8_t* d_status, uint32_t* d_count, double* d_def_mass,
                          double* d_def_thr, int32_t* d_def_spec, uint64_t* d_def_q, uint32_t* d_n_def,
-                         uint32_t* d_err);
+                         uint32_t* d_err, const uint8_t* d_pair_ok /* may be NULL; 0: list every window */);
 
 /* _reduce_alphabet's filter (prediction.py:211-227): is_valid_mass of the
  * alive rows of the d_active spectra against their reduced tables (d_alpha),
@@ -622,7 +654,13 @@ int sst_dict_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spe
 int sst_dict_build_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                           const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
                           const uint32_t* d_rows, const uint64_t* d_alpha, double max_weight, double tol, double prec,
-                          const uint64_t* d_off, uint64_t* d_key, double* d_thr, uint32_t* d_n_ent, uint32_t* d_err);
+                          const uint64_t* d_off, uint64_t* d_key, double* d_thr, uint32_t* d_n_ent, uint32_t* d_err,
+                          const sst_exact_io* x);
+/* The exact-mode spectra's final-round queries listed for the masked
+ * explain (before sst_dict_build_device, which then reads x->xa_*). */
+int sst_dict_list_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                         const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                         const uint32_t* d_rows, double max_weight, double tol, uint32_t* d_err, const sst_exact_io* x);
 
 /* select_sequence_length_with_jaccard (skeleton_building.py:315-370) and
  * combine_skeleton_sequences (:494-516) per spectrum, one lane each: the

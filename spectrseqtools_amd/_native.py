@@ -36,6 +36,7 @@ EXPORTS = (
     "sst_py_tuple_hash", "sst_pyset_order", "sst_pyset_table_size", "sst_walk_scratch_bytes",
     "sst_skel_walk_device", "sst_result_refs_device", "sst_dict_count_device", "sst_dict_build_device",
     "sst_reach_rows_device", "sst_length_bounds_reach_device", "sst_jaccard_device", "sst_skeleton_alpha_device",
+    "sst_dict_list_device", "sst_fix_finish_device",
 )
 
 # kernel ids of sst_profile_read
@@ -69,6 +70,14 @@ WALK_MAX_ROUNDS = 16  # SST_WALK_MAX_ROUNDS
 
 
 JAC_OK, JAC_NO_LENGTH, JAC_INDEX, JAC_BOUNDS = range(4)
+
+
+class ExactIO(ctypes.Structure):
+    """sst_exact_io (include/sst.h): budget-binding spectra's query lists."""
+    _fields_ = [("pair_ok", ctypes.c_void_p), ("xq_mass", ctypes.c_void_p), ("xq_thr", ctypes.c_void_p),
+                ("xq_spec", ctypes.c_void_p), ("xq_single", ctypes.c_void_p), ("xq_count", ctypes.c_void_p),
+                ("xq_cap", ctypes.c_uint64), ("xq_block", ctypes.c_void_p), ("xa_st", ctypes.c_void_p),
+                ("xa_n", ctypes.c_void_p), ("xa_ptr", ctypes.c_void_p)]
 
 
 class JaccardArgs(ctypes.Structure):
@@ -210,14 +219,15 @@ def load_library(path=LIB_PATH):
     lib.sst_classify_rows_device.argtypes = [_P, _P, _P, _I64, _I64, _P, _D, _D, _P, _P, _P, _I, _D, _D, _D, _P, _P,
                                              _P, _P, _P, _P, _P]
     lib.sst_classify_rows_device.restype = _I
-    lib.sst_fix_round_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _D, _D, _D, _P]
+    lib.sst_fix_round_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _D, _D, _D, _P,
+                                         ctypes.POINTER(ExactIO)]
     lib.sst_fix_round_device.restype = _I
     lib.sst_valid_rows_alpha_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _P]
     lib.sst_valid_rows_alpha_device.restype = _I
     lib.sst_bins_count_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _D, _P, _P, _P, _P]
     lib.sst_bins_count_device.restype = _I
     lib.sst_bins_emit_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _P, _P, _P, _P, _P, _P, _P,
-                                         _P, _P]
+                                         _P, _P, _P]
     lib.sst_bins_emit_device.restype = _I
     lib.sst_pyset_table_size.argtypes = [ctypes.c_uint32]
     lib.sst_pyset_table_size.restype = ctypes.c_uint32
@@ -229,7 +239,12 @@ def load_library(path=LIB_PATH):
     lib.sst_result_refs_device.restype = _I
     lib.sst_dict_count_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _D, _D, _P, _P, _P]
     lib.sst_dict_count_device.restype = _I
-    lib.sst_dict_build_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _D, _P, _P, _P, _P, _P]
+    lib.sst_dict_build_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _P, _D, _D, _D, _P, _P, _P, _P, _P,
+                                          ctypes.POINTER(ExactIO)]
+    lib.sst_dict_list_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _D, _D, _P, ctypes.POINTER(ExactIO)]
+    lib.sst_dict_list_device.restype = _I
+    lib.sst_fix_finish_device.argtypes = [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(ExactIO)]
+    lib.sst_fix_finish_device.restype = _I
     lib.sst_dict_build_device.restype = _I
     lib.sst_reach_rows_device.argtypes = [_P, _P, _P, _P, _I64, _P]
     lib.sst_reach_rows_device.restype = _I

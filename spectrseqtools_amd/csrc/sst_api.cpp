@@ -2092,11 +2092,31 @@ int sst_classify_rows_device(sst_table* t, const double* d_obs, const int64_t* d
   return SST_OK;
 }
 
+// the exact-mode arrays (sst_exact_io) into the stage's arguments
+static int exact_io(sst_ctx* c, const sst_exact_io* x, sst::PipeArgs& a) {
+  if (!x) return SST_OK;
+  if (!x->pair_ok || !x->xq_mass || !x->xq_thr || !x->xq_spec || !x->xq_single || !x->xq_count || !x->xq_block)
+    return fail(c, SST_E_ARG, "exact-mode arrays");
+  a.pair_ok = x->pair_ok;
+  a.xq_mass = x->xq_mass;
+  a.xq_thr = x->xq_thr;
+  a.xq_spec = x->xq_spec;
+  a.xq_single = x->xq_single;
+  a.xq_count = x->xq_count;
+  a.xq_cap = x->xq_cap;
+  a.xq_block = x->xq_block;
+  a.xa_st = x->xa_st;
+  a.xa_n = x->xa_n;
+  a.xa_ptr = x->xa_ptr;
+  return SST_OK;
+}
+
 int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                          const double* d_rows_ob, const uint32_t* d_rows_meta, uint8_t* d_alive,
                          const uint32_t* d_rows, const uint64_t* d_alpha, uint64_t* d_alpha_next,
                          const uint8_t* d_active, uint8_t* d_active_next, uint32_t* d_rounds, uint32_t* d_queries,
-                         uint32_t* d_n_active, double max_weight, double tol, double prec, uint32_t* d_err) {
+                         uint32_t* d_n_active, double max_weight, double tol, double prec, uint32_t* d_err,
+                         const sst_exact_io* x) {
   const double zero_shift = 0.0;
   const uint8_t zero_side = 0;
   PipeArgs a;
@@ -2123,6 +2143,7 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
   a.queries = d_queries;
   a.n_active = d_n_active;
   a.err = d_err;
+  if (int rc = exact_io(c, x, a)) return rc;
   if (n_spec > 0) HIP_OK(c, hipMemsetAsync(d_n_active, 0, sizeof(uint32_t), c->stream));  // this round's count
   Prof p(c, SST_K_FIX_ROUND);
   HIP_OK(c, launch_fix_round(t->args, a, c->n_cu, c->stream));
@@ -2176,7 +2197,7 @@ int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
                          const uint32_t* d_rows, const uint64_t* d_alpha, double tol, double prec,
                          const uint64_t* d_q_off, int8_t* d_status, uint32_t* d_count, double* d_def_mass,
                          double* d_def_thr, int32_t* d_def_spec, uint64_t* d_def_q, uint32_t* d_n_def,
-                         uint32_t* d_err) {
+                         uint32_t* d_err, const uint8_t* d_pair_ok) {
   PipeArgs a;
   if (int rc = bins_args(t, d_peak_off, n_spec, d_rows_su, d_rows_ob, d_rows_meta, d_alive, d_rows, tol, prec,
                          const_cast<uint64_t*>(d_q_off), d_err, a))
@@ -2191,6 +2212,7 @@ int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
   a.def_spec = d_def_spec;
   a.def_q = d_def_q;
   a.n_def = d_n_def;
+  a.pair_ok = d_pair_ok;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
@@ -2654,7 +2676,7 @@ extern "C" int sst_dict_count_device(sst_table* t, const int64_t* d_peak_off, in
   sst::DictArgs d{};
   d.n_q = d_n_q;
   Prof p(c, SST_K_DICT);
-  HIP_OK(c, sst::launch_dict(t->args, a, d, true, c->n_cu, c->stream));
+  HIP_OK(c, sst::launch_dict(t->args, a, d, 1, c->n_cu, c->stream));
   HIP_OK(c, sst::launch_scan_u32(d_n_q, d_off, n_spec, c->stream));
   return SST_OK;
 }
@@ -2663,7 +2685,7 @@ extern "C" int sst_dict_build_device(sst_table* t, const int64_t* d_peak_off, in
                                      const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
                                      const uint32_t* d_rows, const uint64_t* d_alpha, double max_weight, double tol,
                                      double prec, const uint64_t* d_off, uint64_t* d_key, double* d_thr,
-                                     uint32_t* d_n_ent, uint32_t* d_err) {
+                                     uint32_t* d_n_ent, uint32_t* d_err, const sst_exact_io* x) {
   if (!t || n_spec < 0 || n_spec > INT32_MAX ||
       (n_spec > 0 && (!d_peak_off || !d_rows_su || !d_rows_ob || !d_rows_meta || !d_alive || !d_rows || !d_alpha ||
                       !d_off || !d_n_ent || !d_err)))
@@ -2692,8 +2714,67 @@ extern "C" int sst_dict_build_device(sst_table* t, const int64_t* d_peak_off, in
   d.key = d_key;
   d.thr = d_thr;
   d.n_ent = d_n_ent;
+  if (int rc = exact_io(c, x, a)) return rc;
+  if (x && (!x->xa_st || !x->xa_n || !x->xa_ptr)) return fail(c, SST_E_ARG, "final dict: the exact-mode answers");
   Prof p(c, SST_K_DICT);
-  HIP_OK(c, sst::launch_dict(t->args, a, d, false, c->n_cu, c->stream));
+  HIP_OK(c, sst::launch_dict(t->args, a, d, 0, c->n_cu, c->stream));
+  return SST_OK;
+}
+
+extern "C" int sst_dict_list_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
+                                    const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
+                                    const uint32_t* d_rows, double max_weight, double tol, uint32_t* d_err,
+                                    const sst_exact_io* x) {
+  if (!t || !x || n_spec < 0 || n_spec > INT32_MAX ||
+      (n_spec > 0 && (!d_peak_off || !d_rows_su || !d_rows_ob || !d_rows_meta || !d_alive || !d_rows || !d_err)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  sst::PipeArgs a{};
+  a.peak_off = d_peak_off;
+  a.n_spec = n_spec;
+  a.r_su = const_cast<double*>(d_rows_su);
+  a.r_ob = const_cast<double*>(d_rows_ob);
+  a.r_meta = const_cast<uint32_t*>(d_rows_meta);
+  a.alive = const_cast<uint8_t*>(d_alive);
+  a.cnt = const_cast<uint32_t*>(d_rows);
+  a.max_weight = max_weight;
+  a.tol = tol;
+  a.err = d_err;
+  if (int rc = exact_io(c, x, a)) return rc;
+  sst::DictArgs d{};
+  Prof p(c, SST_K_DICT);
+  HIP_OK(c, sst::launch_dict(t->args, a, d, 2, c->n_cu, c->stream));
+  return SST_OK;
+}
+
+extern "C" int sst_fix_finish_device(sst_table* t, int64_t n_spec, const uint64_t* d_alpha, uint64_t* d_alpha_next,
+                                     const uint8_t* d_active, uint8_t* d_active_next, uint32_t* d_rounds,
+                                     uint32_t* d_queries, uint32_t* d_n_active, uint32_t* d_err,
+                                     const sst_exact_io* x) {
+  if (!t || !x || n_spec < 0 || n_spec > INT32_MAX ||
+      (n_spec > 0 && (!d_alpha || !d_alpha_next || !d_active || !d_active_next || !d_rounds || !d_queries ||
+                      !d_n_active || !d_err || !x->xa_st || !x->xa_n || !x->xa_ptr)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  sst::PipeArgs a{};
+  a.n_spec = n_spec;
+  a.alpha = d_alpha;
+  a.alpha_next = d_alpha_next;
+  a.active = d_active;
+  a.active_next = d_active_next;
+  a.rounds = d_rounds;
+  a.queries = d_queries;
+  a.n_active = d_n_active;
+  a.err = d_err;
+  for (int r = 1; r < t->n_rows; ++r)
+    if (!t->is_mod[r]) a.canon[r >> 6] |= 1ull << (r & 63);
+  if (int rc = exact_io(c, x, a)) return rc;
+  Prof p(c, SST_K_FIX_ROUND);
+  HIP_OK(c, sst::launch_fix_finish(a, c->n_cu, c->stream));
   return SST_OK;
 }
 

@@ -451,7 +451,25 @@ struct PipeArgs {
   uint64_t* def_q;
   uint32_t* n_def;
   uint32_t* err;
+  // spectra whose budgets can bind on pair-class windows (pair_ok[g] == 0;
+  // null: none): their windows need the exact masked explain.  k_fix_round /
+  // k_dict list such a spectrum's queries (xq_*, a block per spectrum in
+  // xq_block[g] = start << 32 | count) instead of answering them; the caller
+  // answers the list (sst_explain_alpha_batch_device, sst_result_refs_device
+  // into xa_*) and k_fix_finish / k_dict's build pass read the answers
+  const uint8_t* pair_ok;
+  double* xq_mass;
+  double* xq_thr;
+  int32_t* xq_spec;
+  uint8_t* xq_single;
+  uint32_t* xq_count;
+  uint64_t xq_cap;
+  uint64_t* xq_block;
+  const int8_t* xa_st;
+  const uint32_t* xa_n;
+  const uint64_t* xa_ptr;
 };
+hipError_t launch_fix_finish(const PipeArgs& a, int n_wg, hipStream_t st);
 // filter_by_explanation's final explanation dict per spectrum (sst_pipe.hip,
 // k_dict): the dict the last round built (prediction.py:261-329: a side pair
 // is stored only with >= 1 explanation, a singleton always, a later equal key
@@ -466,7 +484,9 @@ struct DictArgs {
   double* thr;           // [total] the last writer's threshold
   uint32_t* n_ent;       // [n_spec] entries
 };
-hipError_t launch_dict(const TableArgs& t, const PipeArgs& a, const DictArgs& d, bool count_only, int n_wg,
+// mode 1: count, 2: list the exact-mode spectra's queries (PipeArgs xq_*),
+// 0: build (exact-mode spectra read their listed answers xa_*)
+hipError_t launch_dict(const TableArgs& t, const PipeArgs& a, const DictArgs& d, int mode, int n_wg,
                        hipStream_t st);
 hipError_t launch_scan_u32(const uint32_t* in, uint64_t* out, int64_t n, hipStream_t st);
 // the skeleton walk (sst_skel.hip, k_skel_walk): the public sst_walk_args

@@ -318,6 +318,109 @@ __device__ __forceinline__ uint32_t key_hash(uint64_t x) {
 
 }  // namespace
 
+// exact mode: the round's queries (START pairs, END pairs, singletons) of
+// spectrum g listed for the masked explain, in order (one block per spectrum)
+__device__ void fix_list(const FixLds& L, const PipeArgs& a, int64_t g, uint32_t q0, uint32_t q1, uint32_t Q) {
+  __shared__ uint32_t s_start;
+  if (threadIdx.x == 0) {
+    s_start = atomicAdd(a.xq_count, Q);
+    if ((uint64_t)s_start + Q > a.xq_cap) atomicOr(a.err, 64u);
+  }
+  __syncthreads();
+  const uint32_t start = s_start;
+  if ((uint64_t)start + Q <= a.xq_cap) {
+    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+      double mass, thr;
+      bool single;
+      fix_query(L, o, q0, q1, a.tol, mass, thr, single);
+      a.xq_mass[start + o] = mass;
+      a.xq_thr[start + o] = thr;
+      a.xq_spec[start + o] = (int32_t)g;
+      a.xq_single[start + o] = single;
+    }
+    if (threadIdx.x == 0) a.xq_block[g] = ((uint64_t)start << 32) | Q;
+  } else if (threadIdx.x == 0) {
+    a.xq_block[g] = 0;
+  }
+  __syncthreads();
+}
+
+// the rest of an exact-mode round (after the caller answered the list): the
+// dict's last writer per key (a side pair only with >= 1 explanation, a
+// singleton always), the rows its surviving answers name (their candidates'
+// payload records), the reduced alphabet and the round's counters
+__global__ __launch_bounds__(kPipeWG) void k_fix_finish(PipeArgs a) {
+  __shared__ uint64_t hkey[kHashSlots];
+  __shared__ uint32_t hidx[kHashSlots];
+  __shared__ unsigned long long su0, su1;
+  __shared__ uint32_t writers;
+  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
+    if (!a.active[g] || !a.pair_ok || a.pair_ok[g]) continue;  // k_fix_round settled it
+    const uint64_t blk = a.xq_block[g];
+    const uint32_t start = (uint32_t)(blk >> 32), Q = (uint32_t)blk;
+    for (int k = threadIdx.x; k < kHashSlots; k += blockDim.x) {
+      hkey[k] = kEmptyKey;
+      hidx[k] = 0;
+    }
+    if (threadIdx.x == 0) {
+      su0 = su1 = 0;
+      writers = 0;
+    }
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+      const int8_t st = a.xa_st[start + o];
+      if (st != SST_NONE && st != SST_EMPTY && st != SST_SOME) atomicOr(a.err, 128u);  // raised / capped
+      if (!(a.xq_single[start + o] || st == SST_SOME)) continue;
+      const uint64_t key = key_bits(a.xq_mass[start + o]);
+      uint32_t h = key_hash(key);
+      for (int probe = 0; probe < kHashSlots; ++probe, h = (h + 1) & (kHashSlots - 1)) {
+        const unsigned long long prev = atomicCAS((unsigned long long*)&hkey[h], kEmptyKey, key);
+        if (prev == kEmptyKey || prev == key) {
+          atomicMax(&hidx[h], o + 1);
+          if (prev == kEmptyKey) atomicAdd(&writers, 1u);
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (writers > kHashSlots * 3 / 4 && threadIdx.x == 0) atomicOr(a.err, 16u);
+    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+      if (a.xa_st[start + o] != SST_SOME) continue;  // None / set() entries name no nucleotide
+      const uint64_t key = key_bits(a.xq_mass[start + o]);
+      uint32_t h = key_hash(key);
+      for (int probe = 0; probe < kHashSlots && hkey[h] != key; ++probe) h = (h + 1) & (kHashSlots - 1);
+      if (hkey[h] != key || hidx[h] != o + 1) continue;
+      const uint8_t* p = (const uint8_t*)a.xa_ptr[start + o];
+      uint64_t u0 = 0, u1 = 0;
+      for (uint32_t c = 0; c < a.xa_n[start + o]; ++c) {
+        const int k = p[0];
+        for (int j = 0; j < k; ++j) {
+          const int r = p[1 + j];
+          if (r < 64) u0 |= 1ull << r;
+          else u1 |= 1ull << (r - 64);
+        }
+        p += 1 + k;
+      }
+      if (u0) atomicOr(&su0, (unsigned long long)u0);
+      if (u1) atomicOr(&su1, (unsigned long long)u1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+      const uint64_t n0 = a.canon[0] | (m0 & su0), n1 = a.canon[1] | (m1 & su1);
+      a.alpha_next[2 * g] = n0;
+      a.alpha_next[2 * g + 1] = n1;
+      const bool changed = __builtin_popcountll(n0) + __builtin_popcountll(n1) !=
+                           __builtin_popcountll(m0) + __builtin_popcountll(m1);
+      a.active_next[g] = changed;
+      a.rounds[g] += 1;
+      a.queries[g] += Q;
+      if (changed) atomicAdd(a.n_active, 1u);
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(kPipeWG) void k_fix_round(TableArgs t, PipeArgs a) {
   __shared__ FixLds L;
   for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
@@ -378,6 +481,10 @@ __global__ __launch_bounds__(kPipeWG) void k_fix_round(TableArgs t, PipeArgs a) 
     const uint32_t q1 = fix_side_pairs(L, 1, a.max_weight);
     const uint32_t Q = q0 + q1 + L.n_single;
     const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+    if (a.pair_ok && !a.pair_ok[g]) {  // budgets can bind: list the round's queries for the exact explain
+      fix_list(L, a, g, q0, q1, Q);
+      continue;
+    }
     // pass A: every query's answer; writers insert their key, the last (largest order) wins
     for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
       double mass, thr;
@@ -492,18 +599,24 @@ __global__ __launch_bounds__(kPipeWG) void k_dict(TableArgs t, PipeArgs a, DictA
     const uint32_t q0 = fix_side_pairs(L, 0, a.max_weight);
     const uint32_t q1 = fix_side_pairs(L, 1, a.max_weight);
     const uint32_t Q = q0 + q1 + L.n_single;
-    if (count_only) {
+    const bool exact = a.pair_ok && !a.pair_ok[g];  // budgets can bind: the listed answers
+    if (count_only == 1) {
       if (threadIdx.x == 0) d.n_q[g] = Q;
       __syncthreads();
       continue;
     }
+    if (count_only == 2) {  // list the exact-mode spectra's queries for the masked explain
+      if (exact) fix_list(L, a, g, q0, q1, Q);
+      continue;
+    }
     const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+    const uint32_t xstart = exact ? (uint32_t)(a.xq_block[g] >> 32) : 0u;
     for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
       double mass, thr;
-      bool single, pc;
+      bool single, pc = true;
       fix_query(L, o, q0, q1, a.tol, mass, thr, single);
       uint64_t u0, u1;
-      const int8_t st = masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
+      const int8_t st = exact ? a.xa_st[xstart + o] : masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
       if (!pc) atomicOr(a.err, 4u);
       if (!(single || st == SST_SOME)) continue;
       const uint64_t key = key_bits(mass);
@@ -687,7 +800,8 @@ __global__ __launch_bounds__(kPipeWG) void k_bins_emit(TableArgs t, PipeArgs a) 
       quantise_lean(mass, thr, a.prec, a.rprec, lof, hif);
       int8_t st = SST_NONE;
       uint32_t cnt = 0;
-      const bool pend = !(hif < (double)t.pair_hi);
+      // off the pair class, or budgets that can bind: listed for the masked explain
+      const bool pend = !(hif < (double)t.pair_hi) || (a.pair_ok && !a.pair_ok[g]);
       if (pend) {
         st = (int8_t)kStatusPending;  // not a pair-class window: listed for the masked explain
       } else if (hif >= 0.0) {
@@ -769,10 +883,10 @@ __global__ __launch_bounds__(kPipeWG) void k_scan_u32(const uint32_t* in, uint64
   if (threadIdx.x == 0) out[n] = carry;
 }
 
-hipError_t launch_dict(const TableArgs& t, const PipeArgs& a, const DictArgs& d, bool count_only, int n_wg,
+hipError_t launch_dict(const TableArgs& t, const PipeArgs& a, const DictArgs& d, int mode, int n_wg,
                        hipStream_t st) {
   if (a.n_spec <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_dict, dim3(n_wg), dim3(kPipeWG), 0, st, t, a, d, count_only ? 1 : 0);
+  hipLaunchKernelGGL(k_dict, dim3(n_wg), dim3(kPipeWG), 0, st, t, a, d, mode);
   return hipGetLastError();
 }
 hipError_t launch_scan_u32(const uint32_t* in, uint64_t* out, int64_t n, hipStream_t st) {
@@ -794,6 +908,11 @@ hipError_t launch_bins_emit(const TableArgs& t, const PipeArgs& a, int n_wg, hip
 hipError_t launch_classify_rows(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st) {
   if (a.n_spec <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_classify_rows, dim3(n_wg), dim3(kPipeWG), 0, st, t, a);
+  return hipGetLastError();
+}
+hipError_t launch_fix_finish(const PipeArgs& a, int n_wg, hipStream_t st) {
+  if (a.n_spec <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fix_finish, dim3(n_wg), dim3(kPipeWG), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_fix_round(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st) {

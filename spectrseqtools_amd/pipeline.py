@@ -260,18 +260,15 @@ def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolera
     S = len(c.offsets) - 1
     max_len = np.broadcast_to(np.asarray(max_len, dtype=np.int64), (S,))
     is_mod = np.array([m.is_modification for m in masses])
-    rate = np.array([m.modification_rate for m in masses], dtype=np.float64)
     rows_all = np.zeros((1, N), bool)
     rows_all[0, 1:] = True
     alpha = np.repeat(row_masks(rows_all), S, axis=0)
     canon = row_masks((~is_mod & (np.arange(N) > 0))[None, :])[0]
     # budgets: max_modifications = round(0.5 max_len) (common.py:55) and the
     # modification rows' caps round(max_len * rate) (mass_explanation.py:158-172)
-    A = np.round(dp_table.seq.modification_rate * max_len.astype(np.float64)).astype(np.int64)  # ties to even
-    cap_min = (np.round(np.outer(max_len.astype(np.float64), rate[is_mod])).min(axis=1).astype(np.int64)
-               if is_mod.any() else np.full(S, 2, dtype=np.int64))
-    if (A < 2).any() or (cap_min < 2).any():
-        raise NotImplementedError("filter_fixpoint: budgets that can bind on pair windows (max_len too small)")
+    from .pipeline_device import budgets_pair_ok
+
+    pair_ok = budgets_pair_ok(dp_table, max_len)  # else: the exact masked explain answers the spectrum's windows
     max_w = max(explanation_masses.get_column("monoisotopic_mass").to_list()) + PHOSPHATE_LINK_MASS
     side = np.array([("START" in n) | (("END" in n) << 1) for n in c.names], dtype=np.uint8)
     flags = side[c.brk] | (np.asarray(c.singleton, dtype=np.uint8) << 2)
@@ -287,6 +284,9 @@ def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolera
         off = np.searchsorted(c.spec[rows], np.arange(S + 1))
         d, t, g, k = _su_diff_queries(c.su[rows], c.obs[rows], flags[rows], off, max_w, tolerance)
         st, cnt, rm, rg = dev.explain_pairs_alpha(d, t, g, alpha, tolerance, dp_table.precision)
+        ex = ~pair_ok[g]
+        if ex.any():  # budgets can bind: the exact replay on each spectrum's alphabet
+            st[ex], cnt[ex], rm[ex] = _exact_answers(dp_table, d[ex], t[ex], g[ex], alpha, max_len, tolerance)
         if (st == -10).any():
             raise NotImplementedError("filter_fixpoint: a window outside the pair class")
         q_off = np.searchsorted(g, np.arange(S + 1))
@@ -310,6 +310,31 @@ def filter_fixpoint(c: Classified, dp_table, max_len, explanation_masses, tolera
             history.append((active.copy(), alpha.copy(), alive.copy()))
         active &= changed
     return Fixpoint(alpha, alive, rounds, history, _final_round(parts, S), n_queries)
+
+
+def _exact_answers(dp_table, diff, thr, spec, alpha, max_len, tolerance):
+    """Windows of budget-binding spectra through the exact masked explain
+    (sst_explain_alpha_batch_device, one pass per max_len group): status,
+    candidate count and the union of the candidates' rows."""
+    dev = dp_table.device_table
+    masses = dp_table.masses
+    is_mod = [m.is_modification for m in masses]
+    st = np.zeros(len(diff), np.int8)
+    cnt = np.zeros(len(diff), np.uint32)
+    rm = np.zeros((len(diff), 2), np.uint64)
+    ml = np.asarray(max_len, dtype=np.int64)[spec]
+    for L in np.unique(ml):
+        sel = np.flatnonzero(ml == L)
+        dev.set_budgets(is_mod, [round(int(L) * m.modification_rate) for m in masses])
+        res = dev.explain_alpha(diff[sel], thr[sel], spec[sel].astype(np.int32), alpha, tolerance,
+                                dp_table.precision, round(dp_table.seq.modification_rate * int(L)))
+        st[sel] = res.status
+        cnt[sel] = res.count
+        for j, i in enumerate(sel):
+            for c in res.candidates(j):
+                for r in c:
+                    rm[i, r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    return st, cnt, rm
 
 
 def _final_round(parts, S):

@@ -131,6 +131,88 @@ def _max_weight(explanation_masses=None):
     return max(em.get_column("monoisotopic_mass").to_list()) + PHOSPHATE_LINK_MASS
 
 
+class _ExactLists:
+    """Exact-mode (budget-binding) spectra's query lists and their answers
+    (sst_exact_io): capacity for a round's queries, the masked explain per
+    max_len group, the answers' references."""
+
+    def __init__(self, dp_table, rows, pair_ok, max_len, cap=None):
+        import torch
+
+        self.dp = dp_table
+        self.rows = rows
+        self.max_len = np.asarray(max_len, dtype=np.int64)
+        self.dev = rows.su.device
+        S = len(rows.rows)
+        self.ok = torch.as_tensor(np.asarray(pair_ok, dtype=np.uint8), device=self.dev)
+        self.exact = torch.as_tensor(~np.asarray(pair_ok, bool), device=self.dev)
+        self.block = torch.zeros(max(1, S), dtype=torch.int64, device=self.dev)
+        self.count = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.cap = 0
+        self.results = []
+        self.io = _native.ExactIO()
+        self.io.pair_ok = self.ok.data_ptr()
+        self.io.xq_count = self.count.data_ptr()
+        self.io.xq_block = self.block.data_ptr()
+        self._alloc(max(1024, int(cap or 0)))
+
+    def _alloc(self, cap):
+        import torch
+
+        self.cap = cap
+        self.mass = torch.empty(cap, dtype=torch.float64, device=self.dev)
+        self.thr = torch.empty(cap, dtype=torch.float64, device=self.dev)
+        self.spec = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        self.single = torch.empty(cap, dtype=torch.uint8, device=self.dev)
+        self.st = torch.empty(cap, dtype=torch.int8, device=self.dev)
+        self.n = torch.empty(cap, dtype=torch.int32, device=self.dev)
+        self.ptr = torch.empty(cap, dtype=torch.int64, device=self.dev)
+        io = self.io
+        io.xq_mass, io.xq_thr, io.xq_spec = self.mass.data_ptr(), self.thr.data_ptr(), self.spec.data_ptr()
+        io.xq_single, io.xq_cap = self.single.data_ptr(), cap
+        io.xa_st, io.xa_n, io.xa_ptr = self.st.data_ptr(), self.n.data_ptr(), self.ptr.data_ptr()
+
+    def reset(self):
+        self.count.zero_()
+        self.results = []
+
+    def prepare(self, active):
+        """Before a fixpoint round: room for the exact-mode active spectra's
+        queries (their count from sst_dict_count_device on the current rows)."""
+        import torch
+
+        dp, r = self.dp, self.rows
+        eng = dp.device_table.engine
+        S = len(r.rows)
+        n_q = torch.zeros(max(1, S), dtype=torch.int32, device=self.dev)
+        off = torch.zeros(S + 1, dtype=torch.int64, device=self.dev)
+        err = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        eng.check(eng._lib.sst_dict_count_device(dp.device_table.handle, r.peak_off.data_ptr(), S, r.su.data_ptr(),
+                                                 r.obs.data_ptr(), r.meta.data_ptr(), r.alive.data_ptr(),
+                                                 r.rows.data_ptr(), float(_max_weight()), float(dp.tolerance),
+                                                 n_q.data_ptr(), off.data_ptr(), err.data_ptr()),
+                  "sst_dict_count_device")
+        need = int((n_q[:S].to(torch.int64) * (active[:S].to(torch.bool) & self.exact[:S])).sum().item())
+        if need > self.cap:
+            self._alloc(need)
+        self.reset()
+
+    def answer(self, alpha_dev):
+        """The listed queries through the exact masked explain (one pass per
+        max_len group), their references into xa_*."""
+        import torch
+
+        n = int(self.count.item())
+        if n > self.cap:
+            raise _native.EngineError("exact-mode query list overflow")
+        if n == 0:
+            return
+        self.st[:n].fill_(-10)
+        dst = torch.arange(n, dtype=torch.int64, device=self.dev)
+        self.results = _masked_explain_refs(self.dp, alpha_dev, self.mass, self.thr, self.spec, n, self.max_len, dst,
+                                            self.ptr, self.n, self.st)
+
+
 @dataclass
 class DeviceFixpoint:
     alpha: np.ndarray     # [S, 2] u64 final alphabets (row masks of the full table)
@@ -155,13 +237,11 @@ def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=None, record=
     dev = rows.su.device
     is_mod = np.array([m.is_modification for m in masses])
     rate = np.array([m.modification_rate for m in masses], dtype=np.float64)
-    max_len = np.broadcast_to(np.asarray(max_len, dtype=np.int64), (S,))
-    # round() on the same f64 products, ties to even like Python's round (vectorised over spectra)
-    A = np.round(dp_table.seq.modification_rate * max_len.astype(np.float64)).astype(np.int64)
-    cap_min = (np.round(np.outer(max_len.astype(np.float64), rate[is_mod])).min(axis=1).astype(np.int64)
-               if is_mod.any() else np.full(S, 2, dtype=np.int64))
-    if (A < 2).any() or (cap_min < 2).any():
-        raise NotImplementedError("fixpoint_device: budgets that can bind on pair windows (max_len too small)")
+    max_len = np.ascontiguousarray(np.broadcast_to(np.asarray(max_len, dtype=np.int64), (S,)))
+    # spectra whose budgets can bind on pair windows run in exact mode: their
+    # queries go to the exact masked explain (sst_exact_io)
+    ok = budgets_pair_ok(dp_table, max_len)
+    xio = None if ok.all() else _ExactLists(dp_table, rows, ok, max_len)
     full = np.zeros((1, N), bool)
     full[0, 1:] = True
     alpha = torch.as_tensor(np.repeat(row_masks(full), S, axis=0).view(np.int64), device=dev).contiguous()
@@ -180,12 +260,21 @@ def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=None, record=
     max_w = _max_weight()
     torch.cuda.synchronize(dev)
     while True:  # per round: two launches, one synchronize, one 8-byte read
+        xp = None
+        if xio is not None:  # list capacity: the round's queries of the exact-mode spectra
+            xio.prepare(active)
+            xp = ctypes.byref(xio.io)
         eng.check(L.sst_fix_round_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(), rows.obs.data_ptr(),
                                          rows.meta.data_ptr(), rows.alive.data_ptr(), rows.rows.data_ptr(),
                                          alpha.data_ptr(), alpha_next.data_ptr(), active.data_ptr(),
                                          active_next.data_ptr(), rounds.data_ptr(), queries.data_ptr(),
                                          n_active.data_ptr(), float(max_w), float(tolerance),
-                                         float(dp_table.precision), err.data_ptr()), "sst_fix_round_device")
+                                         float(dp_table.precision), err.data_ptr(), xp), "sst_fix_round_device")
+        if xio is not None:  # the listed queries answered exactly, then the exact-mode half of the round
+            xio.answer(alpha)
+            eng.check(L.sst_fix_finish_device(h, S, alpha.data_ptr(), alpha_next.data_ptr(), active.data_ptr(),
+                                              active_next.data_ptr(), rounds.data_ptr(), queries.data_ptr(),
+                                              n_active.data_ptr(), err.data_ptr(), xp), "sst_fix_finish_device")
         # re-filter only the spectra whose alphabet shrank: an unchanged alphabet is
         # the table the rows already passed (round 1: classify's full table)
         eng.check(L.sst_valid_rows_alpha_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(),
@@ -279,7 +368,11 @@ def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=None, max_len=None)
     status = torch.empty(max(1, total), dtype=torch.int8, device=dev)
     count = torch.empty(max(1, total), dtype=torch.int32, device=dev)
     defer = max_len is not None
+    pok = None
     if defer:
+        ok = budgets_pair_ok(dp_table, np.broadcast_to(np.asarray(max_len, dtype=np.int64), (S,)))
+        if not ok.all():  # exact-mode spectra: every window to the masked explain
+            pok = torch.as_tensor(ok.astype(np.uint8), device=dev)
         d_mass = torch.empty(max(1, total), dtype=torch.float64, device=dev)
         d_thr = torch.empty_like(d_mass)
         d_spec = torch.empty(max(1, total), dtype=torch.int32, device=dev)
@@ -291,7 +384,8 @@ def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=None, max_len=None)
                                      float(tolerance), float(dp_table.precision), q_off.data_ptr(),
                                      status.data_ptr(), count.data_ptr(), ptr(d_mass) if defer else None,
                                      ptr(d_thr) if defer else None, ptr(d_spec) if defer else None,
-                                     ptr(d_q) if defer else None, ptr(n_def) if defer else None, err.data_ptr()),
+                                     ptr(d_q) if defer else None, ptr(n_def) if defer else None, err.data_ptr(),
+                                     pok.data_ptr() if pok is not None else None),
               "sst_bins_emit_device")
     eng.synchronize()
     _check_err(err)
@@ -390,7 +484,7 @@ class DeviceDict:
 
 
 @_one_stream
-def final_dict_device(dp_table, rows: DeviceRows, alpha_dev, tolerance=None):
+def final_dict_device(dp_table, rows: DeviceRows, alpha_dev, tolerance=None, max_len=None):
     """filter_by_explanation's final explanation dict of every spectrum
     (prediction.py:261-329 over the fixpoint's rows and alphabets), as
     sorted (key, last writer's threshold) lists on the device."""
@@ -416,9 +510,19 @@ def final_dict_device(dp_table, rows: DeviceRows, alpha_dev, tolerance=None):
     key = torch.empty(max(1, total), dtype=torch.int64, device=dev)
     thr = torch.empty(max(1, total), dtype=torch.float64, device=dev)
     n_ent = torch.zeros(max(1, S), dtype=torch.int32, device=dev)
+    xp = None
+    if max_len is not None:
+        ok = budgets_pair_ok(dp_table, np.broadcast_to(np.asarray(max_len, dtype=np.int64), (S,)))
+        if not ok.all():  # exact-mode spectra: their final-round queries answered by the exact masked explain
+            xio = _ExactLists(dp_table, rows, ok, max_len, cap=total)
+            xio.reset()
+            xp = ctypes.byref(xio.io)
+            eng.check(L.sst_dict_list_device(*args, float(max_w), float(tolerance), err.data_ptr(), xp),
+                      "sst_dict_list_device")
+            xio.answer(alpha_dev)
     eng.check(L.sst_dict_build_device(*args, alpha_dev.data_ptr(), float(max_w), float(tolerance),
                                       float(dp_table.precision), off.data_ptr(), key.data_ptr(), thr.data_ptr(),
-                                      n_ent.data_ptr(), err.data_ptr()), "sst_dict_build_device")
+                                      n_ent.data_ptr(), err.data_ptr(), xp), "sst_dict_build_device")
     eng.synchronize()
     _check_err(err)
     return DeviceDict(off, n_ent, key, thr)
@@ -495,7 +599,7 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
     if bins is None:
         bins = bins_device(dp_table, rows, alpha, tolerance=tolerance, max_len=max_len)
     alpha_dev = bins.alpha_dev
-    dct = final_dict_device(dp_table, rows, alpha_dev, tolerance)
+    dct = final_dict_device(dp_table, rows, alpha_dev, tolerance, max_len=max_len)
     Q = int(bins.q_off[-1])
     s_ptr = torch.zeros(max(1, Q), dtype=torch.int64, device=dev)
     s_n = torch.zeros(max(1, Q), dtype=torch.int32, device=dev)

@@ -209,7 +209,7 @@ def test_device_skeleton_walk_vs_reference(tc):
     assert f"skeleton ok {tc} device" in p.stdout
 
 
-def _mirror_outcome(obs, su_seq, obs_seq, max_len, engine):
+def _mirror_outcome(obs, su_seq, obs_seq, max_len, engine, mod_rate=0.5):
     """The per-spectrum host mirrors (pinned to the reference on its own test
     spectra): classify_fragments, Predictor.filter_by_explanation,
     SkeletonBuilder._predict_skeleton per side and
@@ -222,7 +222,7 @@ def _mirror_outcome(obs, su_seq, obs_seq, max_len, engine):
     from spectrseqtools_amd.skeleton_building import SkeletonBuilder, combine_skeleton_sequences
 
     seq = SequenceInformation(max_len=int(max_len), su_mass=float(su_seq), obs_mass=float(obs_seq),
-                              modification_rate=0.5)
+                              modification_rate=mod_rate)
     dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
                                  precision=TOLERANCE, seq=seq, engine=engine)
     bd = build_breakage_dict(555.1294, 455.1491)
@@ -231,7 +231,7 @@ def _mirror_outcome(obs, su_seq, obs_seq, max_len, engine):
     pred = Predictor(dp, EXPLANATION_MASSES)
     frags, expl = pred.filter_by_explanation(f)
     sb = SkeletonBuilder(explanations=expl, dp_table=dp)
-    out, sks = {}, {}
+    out, sks = {"filter_masses": [m.mass for m in dp.masses], "filter_kept": frags.get_column("index").to_list()}, {}
     for side in ("START", "END"):
         sub = frags.filter_mask([side in b for b in frags.get_column("breakage").to_list()])
         sk, fs = sb._predict_skeleton(Frame(sub.to_dict()), [set() for _ in range(dp.seq.max_len)])
@@ -250,14 +250,17 @@ def _mirror_outcome(obs, su_seq, obs_seq, max_len, engine):
     return out
 
 
-@pytest.mark.parametrize("variant", ["full_ladders", "short_fragments_missing"])
+@pytest.mark.parametrize("variant", ["full_ladders", "short_fragments_missing", "low_modification_rate"])
 def test_device_skeleton_and_length_vs_mirror(engine, variant):
     """Stages 4-5 on the device over synthetic spectra against the
     per-spectrum host mirrors in this process (same interpreter, same hash
     seed): each side's skeleton, kept rows, min_end / max_end, the skeleton
     alphabet, the Jaccard length and the combined skeleton.  Without their
     short fragments, spectra need first bins of whole masses of 3+ nucleotides
-    and re-queries against older bins (the masked explain, suspended lanes)."""
+    and re-queries against older bins (the masked explain, suspended lanes).
+    At --modification_rate 0.05 (cli.py:35) the budgets bind on pair windows
+    (max_modifications and caps < 2): every stage runs its spectra in exact
+    mode (sst_exact_io: the exact masked replay answers their windows)."""
     from spectrseqtools_amd import _native, pipeline, pipeline_device as PD
     from spectrseqtools_amd.mass_explanation import MASS_NAMES
     from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
@@ -265,7 +268,9 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
     from spectrseqtools_amd.synthetic import make_spectra
 
     n = 48
-    b = make_spectra(n, seed=41 if variant == "full_ladders" else 43, len_range=(6, 14))
+    mod_rate = 0.05 if variant == "low_modification_rate" else 0.5
+    b = make_spectra(n, seed={"full_ladders": 41, "short_fragments_missing": 43}.get(variant, 47), len_range=(6, 14),
+                     mod_rate=0.3 if variant == "low_modification_rate" else 0.5)
     spec = np.repeat(np.arange(n), np.diff(b.offsets))
     keep = np.ones(len(b.observed), bool)
     if variant != "full_ladders":
@@ -276,10 +281,12 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
     w_full = [k for k, v in bd.items() if "START_END" in v][0]
     su_seq = b.seq_mass - w_full * TOLERANCE
     seq = SequenceInformation(max_len=20, su_mass=float(su_seq[0]), obs_mass=float(b.seq_mass[0]),
-                              modification_rate=0.5)
+                              modification_rate=mod_rate)
     dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
                                  precision=TOLERANCE, seq=seq, engine=engine)
     max_len = pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:]))
+    if variant == "low_modification_rate":
+        assert not PD.budgets_pair_ok(dp, max_len).any()
     rows = PD.classify_device(dp, obs, offsets, su_seq, bd)
     fx = PD.fixpoint_device(dp, rows, max_len)
     bins = PD.bins_device(dp, rows, fx.alpha, max_len=max_len)
@@ -288,7 +295,13 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
     names = [None] + [MASS_NAMES[m.mass][0] for m in dp.masses[1:]]
     n_len = n_err = 0
     for g in range(n):
-        want = _mirror_outcome(obs[offsets[g]:offsets[g + 1]], su_seq[g], b.seq_mass[g], max_len[g], engine)
+        want = _mirror_outcome(obs[offsets[g]:offsets[g + 1]], su_seq[g], b.seq_mass[g], max_len[g], engine,
+                               mod_rate)
+        fm = pipeline.mask_rows(fx.alpha[g:g + 1], len(dp.masses))[0]
+        assert [0] + [dp.masses[r].mass for r in range(1, len(dp.masses)) if fm[r]] == want["filter_masses"], g
+        o4 = int(rows.peak_off[g].item()) * 4
+        al = rows.alive[o4:o4 + int(rows.rows[g].item())].cpu().numpy().astype(bool)
+        assert np.flatnonzero(al).tolist() == want["filter_kept"], g
         assert (sk.status[2 * g:2 * g + 2] == _native.WALK_DONE).all(), (g, sk.status[2 * g:2 * g + 2])
         got = PD.skeleton_frames(dp, rows, sk, g)
         for side in ("START", "END"):
