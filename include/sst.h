@@ -441,11 +441,19 @@ int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* 
  * 4 * d_peak_off[g] + i, i < d_rows[g] (d_rows_* arrays of 4 * n_peaks):
  * su, observed mass, meta = breakage | sides << 2 | is_singleton << 4 | peak
  * position << 8, alive.  Peaks in any order (ranked by mass on the device, equal
- * masses in their given order), <= 1024 per spectrum;
- * shifts / sides as sst_step_rows_device.  d_err collects | 1 a spectrum over
- * 1024 peaks, 2 over 2048 rows, 4 a window outside the pair class, 8 a window
- * past a table's end (the reference raises), 16 a dict too large for the LDS
- * hash, 32 rows out of mass order; the caller checks it. */
+ * masses in their given order), <= 4096 per spectrum;
+ * shifts / sides as sst_step_rows_device.  A spectrum of more than 2048 rows
+ * is held in HBM slices the table's context reserves (sst_pipe_reserve_rows,
+ * before the stages run); without them it is an error.  d_err collects | 1 a
+ * spectrum over 4096 peaks, 2 over 2048 rows with no slices reserved (or over
+ * the reserved rows), 4 a window outside the pair class, 8 a window past a
+ * table's end (the reference raises), 16 a dict too large for its hash, 32
+ * rows out of mass order; the caller checks it. */
+/* Reserve the context's slices for spectra of up to max_rows rows (<= 16384:
+ * 4 breakages x 4096 peaks) in the row stages (fix rounds, final dict, bins);
+ * a no-op for max_rows <= 2048 or at most what is reserved.  Synchronises the
+ * context's stream when it grows. */
+int sst_pipe_reserve_rows(sst_table* t, int64_t max_rows);
 /* classify_fragments (fragment_classification.py:17-101): A7 into d_valid_out
  * (may be NULL), the filters, is_singleton against t's masses, SU order. */
 int sst_classify_rows_device(sst_table* t, const double* d_obs, const int64_t* d_peak_off, int64_t n_spec,
@@ -497,7 +505,8 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
                          uint32_t* d_err, const sst_exact_io* x);
 /* The exact-mode spectra's half of the round, after their listed queries
  * were answered (same arrays as the round; x required). */
-int sst_fix_finish_device(sst_table* t, int64_t n_spec, const uint64_t* d_alpha, uint64_t* d_alpha_next,
+int sst_fix_finish_device(sst_table* t, int64_t n_spec, const uint32_t* d_rows, const uint64_t* d_alpha,
+                          uint64_t* d_alpha_next,
                           const uint8_t* d_active, uint8_t* d_active_next, uint32_t* d_rounds, uint32_t* d_queries,
                           uint32_t* d_n_active, uint32_t* d_err, const sst_exact_io* x);
 /* SkeletonBuilder._predict_skeleton's speculative bin queries
@@ -516,7 +525,8 @@ int sst_fix_finish_device(sst_table* t, int64_t n_spec, const uint64_t* d_alpha,
  * those windows are also listed, in any order, for
  * sst_explain_alpha_batch_device: d_def_mass / d_def_thr / d_def_spec /
  * d_def_q[*d_n_def] = window mass, threshold, spectrum and index into
- * d_status (capacity: the total).  d_err bit 2: a spectrum over 2048 rows. */
+ * d_status (capacity: the total).  d_err bit 2: a spectrum over 2048 rows
+ * with no slices reserved (sst_pipe_reserve_rows). */
 int sst_bins_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                           const double* d_rows_ob, const uint32_t* d_rows_meta, const uint8_t* d_alive,
                           const uint32_t* d_rows, double tol, uint32_t* d_n_q, uint64_t* d_q_off, uint32_t* d_err,

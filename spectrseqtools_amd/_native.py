@@ -36,7 +36,7 @@ EXPORTS = (
     "sst_py_tuple_hash", "sst_pyset_order", "sst_pyset_table_size", "sst_walk_scratch_bytes",
     "sst_skel_walk_device", "sst_result_refs_device", "sst_dict_count_device", "sst_dict_build_device",
     "sst_reach_rows_device", "sst_length_bounds_reach_device", "sst_jaccard_device", "sst_skeleton_alpha_device",
-    "sst_dict_list_device", "sst_fix_finish_device",
+    "sst_dict_list_device", "sst_fix_finish_device", "sst_pipe_reserve_rows",
 )
 
 # kernel ids of sst_profile_read
@@ -243,7 +243,9 @@ def load_library(path=LIB_PATH):
                                           ctypes.POINTER(ExactIO)]
     lib.sst_dict_list_device.argtypes = [_P, _P, _I64, _P, _P, _P, _P, _P, _D, _D, _P, ctypes.POINTER(ExactIO)]
     lib.sst_dict_list_device.restype = _I
-    lib.sst_fix_finish_device.argtypes = [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(ExactIO)]
+    lib.sst_fix_finish_device.argtypes = [_P, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(ExactIO)]
+    lib.sst_pipe_reserve_rows.argtypes = [_P, _I64]
+    lib.sst_pipe_reserve_rows.restype = _I
     lib.sst_fix_finish_device.restype = _I
     lib.sst_dict_build_device.restype = _I
     lib.sst_reach_rows_device.argtypes = [_P, _P, _P, _P, _I64, _P]

@@ -25,8 +25,9 @@
 //                   the three chunks before it (w_max < 3 * 2^18), in a ring of
 //                   four 32 KB chunks.  The spectrum's windows (in mass order)
 //                   are answered as soon as the chunk holding them is done; a
-//                   run of >= w_max reachable masses ends the closure (every
-//                   later mass is reachable).  The reduced table's extent and
+//                   run of >= w_min reachable masses (the alphabet's lightest
+//                   row) ends the closure: every later mass m is reachable, as
+//                   m - w_min is.  The reduced table's extent and
 //                   its last-column mask (mass_table.py:212, :246) bound the
 //                   reachable masses exactly as in set_up_bit_table.
 #include <hip/hip_runtime.h>
@@ -94,8 +95,10 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   __shared__ int s_w[kMaxRows];
   __shared__ int s_n;
   __shared__ int64_t s_done;   // queries [q0, s_done) answered
-  __shared__ int s_full;       // a run of >= w_max reachable masses seen
-  __shared__ int s_chunk_full[kRing];
+  __shared__ int s_full;       // a run of >= w_min reachable masses seen: every later mass is reachable
+  __shared__ int s_zmax;       // the chunk's highest unreachable mass (chunk-relative), -1: none
+  __shared__ int64_t s_run;    // reachable masses ending at the last chunk's end
+  __shared__ int s_wmin_all;
   const int64_t g = blockIdx.x;
   if (a.active && !a.active[g]) return;
   const int64_t q0 = a.counts ? 4 * a.offsets[g] : a.offsets[g];
@@ -106,9 +109,12 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   // L2) and only the other rows are added per spectrum
   __shared__ int s_wmax_all, s_use_c;
   if (threadIdx.x == 0) {
-    int n = 0, wmax_all = 0;
+    int n = 0, wmax_all = 0, wmin_all = INT32_MAX;
     for (int r = 1; r < a.n_rows; ++r)
-      if (row_in(m0, m1, r)) wmax_all = a.w[r] > wmax_all ? a.w[r] : wmax_all;
+      if (row_in(m0, m1, r)) {
+        wmax_all = a.w[r] > wmax_all ? a.w[r] : wmax_all;
+        wmin_all = a.w[r] < wmin_all ? a.w[r] : wmin_all;
+      }
     // the reduced table ends below ceil((35 w_max + 1) / 32) * 32: the shared
     // closure must cover it
     const int64_t lim = ((int64_t)wmax_all * 35 + 32) / 32 * 32;
@@ -121,6 +127,9 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
     s_use_c = uc;
     s_done = q0;
     s_full = 0;
+    s_zmax = -1;
+    s_run = 0;
+    s_wmin_all = wmin_all;
   }
   __syncthreads();
   const bool use_c = s_use_c;
@@ -164,7 +173,7 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   for (int64_t j = 0; j < n_chunks && guard_ok; ++j) {
     uint32_t* cur = ring + (j & (kRing - 1)) * kChunkWords;
     const int64_t base = j * kChunkBits;
-    bool all_ones = true;
+    int zmax = -1;  // this lane's highest unreachable mass in the chunk
     // Each wave writes 63 consecutive words per pass: a row's shifted word
     // for output word o needs ring words wi and wi + 1, and wi + 1 is the next
     // lane's wi (a DPP lane shift), so the 64 lanes read 64 words and the
@@ -183,19 +192,26 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
         // the wave's first output mass (masses < limit < 2^31), wave-uniform: the
         // shifts and ring offsets below are scalar arithmetic
         const int m0 = (int)base + 32 * __builtin_amdgcn_readfirstlane(o0);
-        // two rows per step: their LDS reads are in flight together
-        for (int r = 0; r < n_w; r += 2) {
+        // four rows per step: their LDS reads are in flight together (a tail
+        // repeats the last row: the same bits again)
+        for (int r = 0; r < n_w; r += 4) {
           // the rows' masses from the lanes that hold the list (no LDS round trip)
-          const int x0 = m0 - __builtin_amdgcn_readlane(r < 64 ? w_lo : w_hi, r & 63);
-          const int r1 = r + 1 < n_w ? r + 1 : r;
-          const int x1 = m0 - __builtin_amdgcn_readlane(r1 < 64 ? w_lo : w_hi, r1 & 63);
+          int x[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int rk = r + k < n_w ? r + k : n_w - 1;
+            x[k] = m0 - __builtin_amdgcn_readlane(rk < 64 ? w_lo : w_hi, rk & 63);
+          }
           // ring words from the wave's first shifted word (negative masses: the
           // zeroed slots of chunks not yet filled; past the end: the copy of slot 0)
-          const uint32_t lo0 = ring[((x0 >> 5) & kRingMask) + lane], lo1 = ring[((x1 >> 5) & kRingMask) + lane];
-          const uint32_t nx0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo0, 0x130, 0xF, 0xF, false);  // wave_shl:1
-          const uint32_t nx1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo1, 0x130, 0xF, 0xF, false);
-          v |= __builtin_amdgcn_alignbit(nx0, lo0, (uint32_t)x0 & 31u);  // ({nx, lo} >> shift) low word
-          v |= __builtin_amdgcn_alignbit(nx1, lo1, (uint32_t)x1 & 31u);  // (r1 == r at an odd tail: same bits)
+          uint32_t lo[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) lo[k] = ring[((x[k] >> 5) & kRingMask) + lane];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo[k], 0x130, 0xF, 0xF, false);  // wave_shl:1
+            v |= __builtin_amdgcn_alignbit(nx, lo[k], (uint32_t)x[k] & 31u);  // ({nx, lo} >> shift) low word
+          }
         }
       } else {
         v = ~0u;
@@ -203,16 +219,18 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
       if (lane < 63 && o < kChunkWords) {
         cur[o] = v;
         if ((j & (kRing - 1)) == 0 && o < 64) ring[kRing * kChunkWords + o] = v;
-        all_ones &= (v == ~0u);
+        if (v != ~0u) zmax = 32 * o + 31 - __builtin_clz(~v);  // o ascends: the lane's last one is its highest
       }
     }
-    const bool chunk_full = __syncthreads_and(all_ones);
+    if (zmax >= 0) atomicMax(&s_zmax, zmax);
+    __syncthreads();
     if (threadIdx.x == 0) {
-      s_chunk_full[j & (kRing - 1)] = chunk_full;
-      // the last three chunks all set: a run of 3 * 2^18 > w_max masses, so
-      // every later mass is reachable
-      if (j >= 2 && chunk_full && s_chunk_full[(j - 1) & (kRing - 1)] && s_chunk_full[(j - 2) & (kRing - 1)])
-        s_full = 1;
+      // a run of >= w_min reachable masses [x, x + w_min): every m beyond is
+      // reachable (m - w_min is, by induction), so the closure is full from here
+      const int zm = s_zmax;
+      s_zmax = -1;
+      s_run = zm < 0 ? s_run + kChunkBits : kChunkBits - 1 - zm;
+      if (s_run >= s_wmin_all) s_full = 1;
     }
     __syncthreads();
     // answer the queries whose windows lie below the end of this chunk (the

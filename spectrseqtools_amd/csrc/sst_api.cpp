@@ -81,6 +81,10 @@ struct sst_ctx {
   int64_t prof_n[SST_K_COUNT] = {0};
   uint32_t prof_every = 1;                // bracket every n-th launch of a selected kernel
   uint64_t prof_seen[SST_K_COUNT] = {0};  // launches of each kernel id since selection
+  // the pipeline's big-spectrum slices (sst_pipe_reserve_rows, pipe_big_layout)
+  DevBuf pipe_big;
+  uint32_t pipe_big_rows = 0, pipe_big_slots = 0;
+  int pipe_big_wg = 0;
 };
 
 struct sst_table {
@@ -2111,6 +2115,38 @@ static int exact_io(sst_ctx* c, const sst_exact_io* x, sst::PipeArgs& a) {
   return SST_OK;
 }
 
+// the context's big-spectrum slices into the stage's arguments (none reserved:
+// a spectrum of more than kPipeMaxRows rows is reported, bit 2)
+static void big_args(sst_ctx* c, sst::PipeArgs& a) {
+  if (!c->pipe_big_rows) return;
+  a.big = (uint8_t*)c->pipe_big.p;
+  a.big_rows = c->pipe_big_rows;
+  a.big_slots = c->pipe_big_slots;
+  a.big_stride = sst::pipe_big_layout(a.big_rows, a.big_slots).stride;
+  a.big_wg = c->pipe_big_wg;
+}
+
+int sst_pipe_reserve_rows(sst_table* t, int64_t max_rows) {
+  if (!t || max_rows < 0) return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (max_rows <= kPipeMaxRows || (uint32_t)max_rows <= c->pipe_big_rows) return SST_OK;
+  if (max_rows > kPipeBigRows)
+    return fail(c, SST_E_ARG, "pipeline: more than " + std::to_string(kPipeBigRows) + " rows per spectrum");
+  if (int rc = set_device(c)) return rc;
+  const uint32_t rows = (uint32_t)max_rows;
+  uint32_t slots = 1u << 15;  // the dict hash: >= 16 slots per row (writers <= 3/4 of them)
+  while (slots < 16u * rows) slots <<= 1;
+  const int wg = std::max(1, std::min(c->n_cu, 32));
+  const uint64_t bytes = sst::pipe_big_layout(rows, slots).stride * (uint64_t)wg;
+  HIP_OK(c, hipStreamSynchronize(c->stream));  // earlier launches may still read the old slices
+  if (!c->pipe_big.ensure(bytes)) return fail(c, SST_E_NOMEM, "device allocation failed");
+  c->pipe_big_rows = rows;
+  c->pipe_big_slots = slots;
+  c->pipe_big_wg = wg;
+  return SST_OK;
+}
+
 int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec, const double* d_rows_su,
                          const double* d_rows_ob, const uint32_t* d_rows_meta, uint8_t* d_alive,
                          const uint32_t* d_rows, const uint64_t* d_alpha, uint64_t* d_alpha_next,
@@ -2145,6 +2181,7 @@ int sst_fix_round_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
   a.err = d_err;
   if (int rc = exact_io(c, x, a)) return rc;
   if (n_spec > 0) HIP_OK(c, hipMemsetAsync(d_n_active, 0, sizeof(uint32_t), c->stream));  // this round's count
+  big_args(c, a);
   Prof p(c, SST_K_FIX_ROUND);
   HIP_OK(c, launch_fix_round(t->args, a, c->n_cu, c->stream));
   return SST_OK;
@@ -2187,6 +2224,7 @@ int sst_bins_count_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spe
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
+  big_args(c, a);
   Prof p(c, SST_K_BINS_COUNT);
   HIP_OK(c, launch_bins_count(a, c->n_cu, c->stream));
   return SST_OK;
@@ -2217,6 +2255,7 @@ int sst_bins_emit_device(sst_table* t, const int64_t* d_peak_off, int64_t n_spec
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (int rc = set_device(c)) return rc;
   if (int rc = check_masks(t)) return rc;
+  big_args(c, a);
   Prof p(c, SST_K_BINS_EMIT);
   HIP_OK(c, launch_bins_emit(t->args, a, c->n_cu, c->stream));
   return SST_OK;
@@ -2675,6 +2714,7 @@ extern "C" int sst_dict_count_device(sst_table* t, const int64_t* d_peak_off, in
   a.err = d_err;
   sst::DictArgs d{};
   d.n_q = d_n_q;
+  big_args(c, a);
   Prof p(c, SST_K_DICT);
   HIP_OK(c, sst::launch_dict(t->args, a, d, 1, c->n_cu, c->stream));
   HIP_OK(c, sst::launch_scan_u32(d_n_q, d_off, n_spec, c->stream));
@@ -2716,6 +2756,7 @@ extern "C" int sst_dict_build_device(sst_table* t, const int64_t* d_peak_off, in
   d.n_ent = d_n_ent;
   if (int rc = exact_io(c, x, a)) return rc;
   if (x && (!x->xa_st || !x->xa_n || !x->xa_ptr)) return fail(c, SST_E_ARG, "final dict: the exact-mode answers");
+  big_args(c, a);
   Prof p(c, SST_K_DICT);
   HIP_OK(c, sst::launch_dict(t->args, a, d, 0, c->n_cu, c->stream));
   return SST_OK;
@@ -2744,17 +2785,19 @@ extern "C" int sst_dict_list_device(sst_table* t, const int64_t* d_peak_off, int
   a.err = d_err;
   if (int rc = exact_io(c, x, a)) return rc;
   sst::DictArgs d{};
+  big_args(c, a);
   Prof p(c, SST_K_DICT);
   HIP_OK(c, sst::launch_dict(t->args, a, d, 2, c->n_cu, c->stream));
   return SST_OK;
 }
 
-extern "C" int sst_fix_finish_device(sst_table* t, int64_t n_spec, const uint64_t* d_alpha, uint64_t* d_alpha_next,
+extern "C" int sst_fix_finish_device(sst_table* t, int64_t n_spec, const uint32_t* d_rows, const uint64_t* d_alpha,
+                                     uint64_t* d_alpha_next,
                                      const uint8_t* d_active, uint8_t* d_active_next, uint32_t* d_rounds,
                                      uint32_t* d_queries, uint32_t* d_n_active, uint32_t* d_err,
                                      const sst_exact_io* x) {
   if (!t || !x || n_spec < 0 || n_spec > INT32_MAX ||
-      (n_spec > 0 && (!d_alpha || !d_alpha_next || !d_active || !d_active_next || !d_rounds || !d_queries ||
+      (n_spec > 0 && (!d_rows || !d_alpha || !d_alpha_next || !d_active || !d_active_next || !d_rounds || !d_queries ||
                       !d_n_active || !d_err || !x->xa_st || !x->xa_n || !x->xa_ptr)))
     return SST_E_ARG;
   sst_ctx* c = t->ctx;
@@ -2762,6 +2805,7 @@ extern "C" int sst_fix_finish_device(sst_table* t, int64_t n_spec, const uint64_
   if (int rc = set_device(c)) return rc;
   sst::PipeArgs a{};
   a.n_spec = n_spec;
+  a.cnt = const_cast<uint32_t*>(d_rows);
   a.alpha = d_alpha;
   a.alpha_next = d_alpha_next;
   a.active = d_active;
@@ -2773,6 +2817,7 @@ extern "C" int sst_fix_finish_device(sst_table* t, int64_t n_spec, const uint64_
   for (int r = 1; r < t->n_rows; ++r)
     if (!t->is_mod[r]) a.canon[r >> 6] |= 1ull << (r & 63);
   if (int rc = exact_io(c, x, a)) return rc;
+  big_args(c, a);
   Prof p(c, SST_K_FIX_ROUND);
   HIP_OK(c, sst::launch_fix_finish(a, c->n_cu, c->stream));
   return SST_OK;

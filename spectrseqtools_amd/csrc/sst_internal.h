@@ -409,8 +409,40 @@ struct RowsArgs {
 hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, size_t dyn, hipStream_t st);
 
 // config 5 on the device (sst_pipe.hip)
-constexpr int kPipeMaxPeaks = 1024;  // peaks per spectrum the classify workgroup holds
-constexpr int kPipeMaxRows = 2048;   // rows per spectrum (4 breakages)
+constexpr int kPipeMaxPeaks = 4096;  // peaks per spectrum the classify workgroup holds (77 KB of LDS)
+constexpr int kPipeMaxRows = 2048;   // rows per spectrum the LDS variants of the row kernels hold
+constexpr int kPipeBigRows = 4 * kPipeMaxPeaks;  // rows per spectrum in the HBM-scratch variants
+// A spectrum of more than kPipeMaxRows rows is handled by the *_big variants
+// of k_fix_round / k_dict / k_fix_finish / k_bins_*: the same code over a
+// workgroup's slice of HBM scratch (PipeArgs big*) instead of LDS arrays,
+// with a dict hash of big_slots entries.  Layout of one slice:
+struct PipeBigLayout {
+  uint64_t su, ob, q0, q1, hkey, hidx, sk, si, s0, s1, single, b0, b1, stride;
+};
+__host__ __device__ inline PipeBigLayout pipe_big_layout(uint32_t rows, uint32_t slots) {
+  PipeBigLayout L{};
+  uint64_t o = 0;
+  auto take = [&o](uint64_t bytes) {
+    const uint64_t at = o;
+    o += (bytes + 255) & ~255ull;
+    return at;
+  };
+  L.su = take(8ull * rows);
+  L.ob = take(8ull * rows);
+  L.q0 = take(4ull * (rows + 1));
+  L.q1 = take(4ull * (rows + 1));
+  L.hkey = take(8ull * slots);
+  L.hidx = take(4ull * slots);
+  L.sk = take(8ull * slots);  // the dict's entries sorted by key (bitonic, k_dict_big)
+  L.si = take(4ull * slots);
+  L.s0 = take(2ull * rows);
+  L.s1 = take(2ull * rows);
+  L.single = take(2ull * rows);
+  L.b0 = take(2ull * (rows + 1));
+  L.b1 = take(2ull * (rows + 1));
+  L.stride = o;
+  return L;
+}
 struct PipeArgs {
   const double* obs;          // [n_peaks], any order within each spectrum
   const int64_t* peak_off;    // [n_spec + 1]; rows of spectrum g live at slots 4 * peak_off[g] + i
@@ -468,6 +500,12 @@ struct PipeArgs {
   const int8_t* xa_st;
   const uint32_t* xa_n;
   const uint64_t* xa_ptr;
+  // HBM scratch of the big-spectrum variants (null: a spectrum of more than
+  // kPipeMaxRows rows is an error, bit 2); big_wg slices of big_stride bytes
+  uint8_t* big;
+  uint64_t big_stride;
+  uint32_t big_rows, big_slots;
+  int big_wg;
 };
 hipError_t launch_fix_finish(const PipeArgs& a, int n_wg, hipStream_t st);
 // filter_by_explanation's final explanation dict per spectrum (sst_pipe.hip,

@@ -223,32 +223,143 @@ __global__ __launch_bounds__(kPipeWG) void k_classify_rows(TableArgs t, PipeArgs
 
 namespace {
 
-struct FixLds {
+// One spectrum's alive rows, a round's query offsets and the explanation
+// dict's hash, as views: of LDS arrays for a spectrum of <= kPipeMaxRows
+// rows, of the workgroup's HBM slice (pipe_big_layout) in the *_big variants.
+// Both instantiate the same code; the LDS views stay in the LDS address space
+// after inlining (ds_* instructions), the HBM ones are global accesses.
+struct FixView {
+  double* su;
+  double* ob;
+  uint16_t* s0;      // alive rows of the START side (indices into su / ob), SU order
+  uint16_t* s1;      // ... of the END side
+  uint16_t* single;  // alive singleton rows
+  uint32_t* q0;      // per side: exclusive prefix of each row's pair queries
+  uint32_t* q1;
+  uint64_t* hkey;
+  uint32_t* hidx;
+  uint32_t hmask;    // hash slots - 1
+  __device__ __forceinline__ uint16_t* side(int sd) const { return sd ? s1 : s0; }
+  __device__ __forceinline__ uint32_t* qoff(int sd) const { return sd ? q1 : q0; }
+};
+struct FixLdsArrays {
   double su[kPipeMaxRows];
   double ob[kPipeMaxRows];
-  uint16_t side[2][kPipeMaxRows];   // alive rows of each side (indices into su / ob), SU order
-  uint16_t single[kPipeMaxRows];    // alive singleton rows
+  uint16_t side[2][kPipeMaxRows];
+  uint16_t single[kPipeMaxRows];
   uint32_t qoff[2][kPipeMaxRows + 1];
   uint64_t hkey[kHashSlots];
   uint32_t hidx[kHashSlots];
+};
+struct FixMeta {
   uint32_t n_side[2], n_single, n_alive;
   int sstar[2];
   uint32_t w[16];
   unsigned long long u0, u1;
-  uint32_t writers;
+  uint32_t writers, n_ent;
 };
 
-__device__ __forceinline__ double side_su(const FixLds& L, int sd, uint32_t r) { return L.su[L.side[sd][r]]; }
+__device__ __forceinline__ FixView lds_view(FixLdsArrays& S) {
+  return FixView{S.su, S.ob, S.side[0], S.side[1], S.single, S.qoff[0], S.qoff[1], S.hkey, S.hidx,
+                 (uint32_t)kHashSlots - 1};
+}
+__device__ __forceinline__ uint8_t* big_slice(const PipeArgs& a) { return a.big + (uint64_t)blockIdx.x * a.big_stride; }
+__device__ __forceinline__ FixView big_view(const PipeArgs& a) {
+  const PipeBigLayout B = pipe_big_layout(a.big_rows, a.big_slots);
+  uint8_t* p = big_slice(a);
+  return FixView{(double*)(p + B.su),     (double*)(p + B.ob),   (uint16_t*)(p + B.s0),
+                 (uint16_t*)(p + B.s1),   (uint16_t*)(p + B.single), (uint32_t*)(p + B.q0),
+                 (uint32_t*)(p + B.q1),   (uint64_t*)(p + B.hkey), (uint32_t*)(p + B.hidx),
+                 a.big_slots - 1};
+}
+
+// the big variants' spectra: rows > kPipeMaxRows; spectrum g goes to
+// workgroup g % gridDim.x, found by a coalesced scan of the row counts
+template <class F>
+__device__ __forceinline__ void for_big_spectra(const PipeArgs& a, F&& f) {
+  __shared__ uint32_t s_list[kPipeWG];
+  __shared__ uint32_t s_n;
+  const int64_t G = gridDim.x;
+  for (int64_t c0 = 0; (int64_t)blockIdx.x + c0 * G < a.n_spec; c0 += blockDim.x) {
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    const int64_t gi = (int64_t)blockIdx.x + (c0 + threadIdx.x) * G;
+    if (gi < a.n_spec && a.cnt[gi] > (uint32_t)kPipeMaxRows) s_list[atomicAdd(&s_n, 1u)] = threadIdx.x;
+    __syncthreads();
+    const uint32_t n = s_n;
+    for (uint32_t k = 0; k < n; ++k) {
+      const int64_t g = (int64_t)blockIdx.x + (c0 + s_list[k]) * G;
+      f(g, a.cnt[g]);
+      __syncthreads();
+    }
+  }
+}
+// a spectrum neither variant holds (more rows than the big slices, or no slices)
+__device__ __forceinline__ bool pipe_too_big(const PipeArgs& a, uint32_t nr) {
+  return nr > (uint32_t)kPipeMaxRows && (a.big == nullptr || nr > a.big_rows);
+}
+
+// reads of hash slots written by atomics (device-scope loads: the slots may be HBM)
+__device__ __forceinline__ uint64_t ld_key(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_idx(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the alive rows of a spectrum (SU order) and each side's / the singletons' lists
+__device__ __forceinline__ void fix_load(FixMeta& M, const FixView& V, const PipeArgs& a, int64_t base,
+                                         uint32_t nr) {
+  uint32_t carry[4] = {0, 0, 0, 0};
+  for (uint32_t r0 = 0; r0 < nr; r0 += blockDim.x) {
+    const uint32_t r = r0 + threadIdx.x;
+    const bool al = r < nr && a.alive[base + r];
+    const uint32_t meta = al ? a.r_meta[base + r] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl(al ? 1u : 0u, M.w, tot);
+    const uint32_t i = carry[0] + ex;
+    if (al) {
+      V.su[i] = a.r_su[base + r];
+      V.ob[i] = a.r_ob[base + r];
+    }
+    carry[0] += tot;
+    for (int c = 0; c < 3; ++c) {
+      const bool f = al && ((meta >> (2 + c)) & 1u);  // START, END, singleton
+      const uint32_t x = block_excl(f ? 1u : 0u, M.w, tot);
+      if (f) (c == 0 ? V.s0 : c == 1 ? V.s1 : V.single)[carry[c + 1] + x] = (uint16_t)i;
+      carry[c + 1] += tot;
+    }
+  }
+  if (threadIdx.x == 0) {
+    M.n_alive = carry[0];
+    M.n_side[0] = carry[1];
+    M.n_side[1] = carry[2];
+    M.n_single = carry[3];
+    M.u0 = M.u1 = 0;
+    M.writers = 0;
+    M.n_ent = 0;
+  }
+}
+
+__device__ __forceinline__ void hash_clear(const FixView& V) {
+  for (uint32_t k = threadIdx.x; k <= V.hmask; k += blockDim.x) {
+    V.hkey[k] = kEmptyKey;
+    V.hidx[k] = 0;
+  }
+}
+
+__device__ __forceinline__ double side_su(const FixView& V, int sd, uint32_t r) { return V.su[V.side(sd)[r]]; }
 
 // s* and the per-row pair counts' prefix of side sd (the rows step's closed form)
-__device__ uint32_t fix_side_pairs(FixLds& L, int sd, double mw) {
-  const uint32_t n = L.n_side[sd];
-  if (threadIdx.x == 0) L.sstar[sd] = n ? (int)n - 1 : 0;
+__device__ __forceinline__ uint32_t fix_side_pairs(FixMeta& M, const FixView& V, int sd, double mw) {
+  const uint32_t n = M.n_side[sd];
+  if (threadIdx.x == 0) M.sstar[sd] = n ? (int)n - 1 : 0;
   __syncthreads();
   for (uint32_t r = threadIdx.x; r + 1 < n; r += blockDim.x)
-    if (!(side_su(L, sd, n - 1) - side_su(L, sd, r) > mw)) atomicMin(&L.sstar[sd], (int)r);
+    if (!(side_su(V, sd, n - 1) - side_su(V, sd, r) > mw)) atomicMin(&M.sstar[sd], (int)r);
   __syncthreads();
-  const uint32_t ss = (uint32_t)L.sstar[sd];
+  const uint32_t ss = (uint32_t)M.sstar[sd];
+  uint32_t* qoff = V.qoff(sd);
   uint32_t carry = 0;
   for (uint32_t r0 = 0; r0 < n; r0 += blockDim.x) {
     const uint32_t r = r0 + threadIdx.x;
@@ -256,10 +367,10 @@ __device__ uint32_t fix_side_pairs(FixLds& L, int sd, double mw) {
     if (r + 1 < n) {
       if (r < ss) {
         uint32_t lo = r + 1, hi = n - 1;
-        const double sr = side_su(L, sd, r);
+        const double sr = side_su(V, sd, r);
         while (lo < hi) {
           const uint32_t mid = (lo + hi) >> 1;
-          if (side_su(L, sd, mid) - sr > mw) hi = mid;
+          if (side_su(V, sd, mid) - sr > mw) hi = mid;
           else lo = mid + 1;
         }
         c = lo - r - 1;
@@ -270,39 +381,41 @@ __device__ uint32_t fix_side_pairs(FixLds& L, int sd, double mw) {
       }
     }
     uint32_t tot;
-    const uint32_t ex = block_excl(c, L.w, tot);
-    if (r < n) L.qoff[sd][r] = carry + ex;
+    const uint32_t ex = block_excl(c, M.w, tot);
+    if (r < n) qoff[r] = carry + ex;
     carry += tot;
   }
-  if (threadIdx.x == 0) L.qoff[sd][n] = carry;
+  if (threadIdx.x == 0) qoff[n] = carry;
   __syncthreads();
   return carry;
 }
 
 // query o of the round (START pairs, END pairs, singletons): its key, mass and threshold
-__device__ __forceinline__ void fix_query(const FixLds& L, uint32_t o, uint32_t q0, uint32_t q1, double tol,
-                                          double& mass, double& thr, bool& single) {
+__device__ __forceinline__ void fix_query(const FixMeta& M, const FixView& V, uint32_t o, uint32_t q0, uint32_t q1,
+                                          double tol, double& mass, double& thr, bool& single) {
   single = o >= q0 + q1;
   if (single) {
-    const uint32_t r = L.single[o - q0 - q1];
-    mass = L.su[r];
-    thr = tol * L.ob[r];  // prediction.py:280
+    const uint32_t r = V.single[o - q0 - q1];
+    mass = V.su[r];
+    thr = tol * V.ob[r];  // prediction.py:280
     return;
   }
   const int sd = o >= q0;
   const uint32_t q = sd ? o - q0 : o;
-  const uint32_t n = L.n_side[sd];
+  const uint32_t n = M.n_side[sd];
+  const uint32_t* qoff = V.qoff(sd);
   uint32_t lo = 0, hi = n;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (L.qoff[sd][mid] <= q) lo = mid;
+    if (qoff[mid] <= q) lo = mid;
     else hi = mid;
   }
   const uint32_t s = lo;
-  const uint32_t e = s <= (uint32_t)L.sstar[sd] ? s + 1 + (q - L.qoff[sd][s]) : n - 1;
-  const uint32_t rs = L.side[sd][s], re = L.side[sd][e];
-  mass = L.su[re] - L.su[rs];
-  thr = tol * (L.ob[rs] + L.ob[re]);  // calculate_error_threshold, l1 (common.py:37-44)
+  const uint32_t e = s <= (uint32_t)M.sstar[sd] ? s + 1 + (q - qoff[s]) : n - 1;
+  const uint16_t* rows = V.side(sd);
+  const uint32_t rs = rows[s], re = rows[e];
+  mass = V.su[re] - V.su[rs];
+  thr = tol * (V.ob[rs] + V.ob[re]);  // calculate_error_threshold, l1 (common.py:37-44)
 }
 
 __device__ __forceinline__ uint64_t key_bits(double k) {
@@ -313,14 +426,40 @@ __device__ __forceinline__ uint32_t key_hash(uint64_t x) {
   x ^= x >> 33;
   x *= 0xff51afd7ed558ccdull;
   x ^= x >> 33;
-  return (uint32_t)x & (kHashSlots - 1);
+  return (uint32_t)x;
 }
 
-}  // namespace
+// the dict's writers: insert the key, the last (largest order) writer wins
+__device__ __forceinline__ void hash_put(const FixView& V, uint32_t* writers, uint64_t key, uint32_t o) {
+  uint32_t h = key_hash(key) & V.hmask;
+  for (uint32_t probe = 0; probe <= V.hmask; ++probe, h = (h + 1) & V.hmask) {
+    const unsigned long long prev = atomicCAS((unsigned long long*)&V.hkey[h], kEmptyKey, key);
+    if (prev == kEmptyKey || prev == key) {
+      atomicMax(&V.hidx[h], o + 1);
+      if (prev == kEmptyKey) atomicAdd(writers, 1u);
+      return;
+    }
+  }
+}
+// query o is the last writer of its key
+__device__ __forceinline__ bool hash_last(const FixView& V, uint64_t key, uint32_t o) {
+  uint32_t h = key_hash(key) & V.hmask;
+  uint64_t k = ld_key(&V.hkey[h]);
+  for (uint32_t probe = 0; probe < V.hmask && k != key; ++probe) {
+    h = (h + 1) & V.hmask;
+    k = ld_key(&V.hkey[h]);
+  }
+  return k == key && ld_idx(&V.hidx[h]) == o + 1;
+}
+__device__ __forceinline__ void hash_check(const FixMeta& M, const FixView& V, const PipeArgs& a) {
+  // too full to trust the probe bound: reported
+  if (threadIdx.x == 0 && (uint64_t)M.writers * 4 > 3ull * (V.hmask + 1ull)) atomicOr(a.err, 16u);
+}
 
 // exact mode: the round's queries (START pairs, END pairs, singletons) of
 // spectrum g listed for the masked explain, in order (one block per spectrum)
-__device__ void fix_list(const FixLds& L, const PipeArgs& a, int64_t g, uint32_t q0, uint32_t q1, uint32_t Q) {
+__device__ __forceinline__ void fix_list(const FixMeta& M, const FixView& V, const PipeArgs& a, int64_t g,
+                                         uint32_t q0, uint32_t q1, uint32_t Q) {
   __shared__ uint32_t s_start;
   if (threadIdx.x == 0) {
     s_start = atomicAdd(a.xq_count, Q);
@@ -332,7 +471,7 @@ __device__ void fix_list(const FixLds& L, const PipeArgs& a, int64_t g, uint32_t
     for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
       double mass, thr;
       bool single;
-      fix_query(L, o, q0, q1, a.tol, mass, thr, single);
+      fix_query(M, V, o, q0, q1, a.tol, mass, thr, single);
       a.xq_mass[start + o] = mass;
       a.xq_thr[start + o] = thr;
       a.xq_spec[start + o] = (int32_t)g;
@@ -345,6 +484,119 @@ __device__ void fix_list(const FixLds& L, const PipeArgs& a, int64_t g, uint32_t
   __syncthreads();
 }
 
+// the round's outcome: canonical rows stay, a modification stays iff a
+// surviving explanation names it (adapt_individual_modification_rates_by_
+// alphabet_reduction, mass_table.py:94-121); the spectrum stays active while
+// its alphabet shrinks
+__device__ __forceinline__ void fix_outcome(const FixMeta& M, const PipeArgs& a, int64_t g, uint32_t Q) {
+  if (threadIdx.x == 0) {
+    const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+    const uint64_t n0 = a.canon[0] | (m0 & M.u0), n1 = a.canon[1] | (m1 & M.u1);
+    a.alpha_next[2 * g] = n0;
+    a.alpha_next[2 * g + 1] = n1;
+    const bool changed = __builtin_popcountll(n0) + __builtin_popcountll(n1) !=
+                         __builtin_popcountll(m0) + __builtin_popcountll(m1);
+    a.active_next[g] = changed;
+    a.rounds[g] += 1;
+    a.queries[g] += Q;
+    if (changed) atomicAdd(a.n_active, 1u);
+  }
+  __syncthreads();
+}
+
+// one filter_by_explanation round of spectrum g (nr row slots)
+__device__ __forceinline__ void fix_round_spec(const TableArgs& t, const PipeArgs& a, FixMeta& M, const FixView& V,
+                                               int64_t g, uint32_t nr) {
+  fix_load(M, V, a, 4 * a.peak_off[g], nr);
+  hash_clear(V);
+  __syncthreads();
+  const uint32_t q0 = fix_side_pairs(M, V, 0, a.max_weight);
+  const uint32_t q1 = fix_side_pairs(M, V, 1, a.max_weight);
+  const uint32_t Q = q0 + q1 + M.n_single;
+  const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+  if (a.pair_ok && !a.pair_ok[g]) {  // budgets can bind: list the round's queries for the exact explain
+    fix_list(M, V, a, g, q0, q1, Q);
+    return;
+  }
+  // pass A: every query's answer; writers insert their key, the last (largest order) wins
+  for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+    double mass, thr;
+    bool single, pc;
+    fix_query(M, V, o, q0, q1, a.tol, mass, thr, single);
+    uint64_t u0, u1;
+    const int8_t st = masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
+    if (!pc) atomicOr(a.err, 4u);  // not pair-class: never for these windows (the host checks)
+    if (single || st == SST_SOME) hash_put(V, &M.writers, key_bits(mass), o);
+  }
+  __syncthreads();
+  hash_check(M, V, a);
+  // pass B: the dict's surviving entries -> the observed rows
+  for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+    double mass, thr;
+    bool single, pc;
+    fix_query(M, V, o, q0, q1, a.tol, mass, thr, single);
+    uint64_t u0, u1;
+    const int8_t st = masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
+    if (st != SST_SOME) continue;  // None / set() entries name no nucleotide
+    if (hash_last(V, key_bits(mass), o)) {
+      if (u0) atomicOr(&M.u0, (unsigned long long)u0);
+      if (u1) atomicOr(&M.u1, (unsigned long long)u1);
+    }
+  }
+  __syncthreads();
+  fix_outcome(M, a, g, Q);
+}
+
+// a spectrum no variant holds: reported, its alphabet carried over
+__device__ __forceinline__ void fix_reject(const PipeArgs& a, int64_t g) {
+  if (threadIdx.x == 0) {
+    atomicOr(a.err, 2u);
+    a.alpha_next[2 * g] = a.alpha[2 * g];
+    a.alpha_next[2 * g + 1] = a.alpha[2 * g + 1];
+    a.active_next[g] = 0;
+  }
+}
+
+// the rest of an exact-mode round after the caller answered the list (see k_fix_finish)
+__device__ __forceinline__ void fix_finish_spec(const PipeArgs& a, FixMeta& M, const FixView& V, int64_t g) {
+  const uint64_t blk = a.xq_block[g];
+  const uint32_t start = (uint32_t)(blk >> 32), Q = (uint32_t)blk;
+  hash_clear(V);
+  if (threadIdx.x == 0) {
+    M.u0 = M.u1 = 0;
+    M.writers = 0;
+  }
+  __syncthreads();
+  for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+    const int8_t st = a.xa_st[start + o];
+    if (st != SST_NONE && st != SST_EMPTY && st != SST_SOME) atomicOr(a.err, 128u);  // raised / capped
+    if (a.xq_single[start + o] || st == SST_SOME) hash_put(V, &M.writers, key_bits(a.xq_mass[start + o]), o);
+  }
+  __syncthreads();
+  hash_check(M, V, a);
+  for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+    if (a.xa_st[start + o] != SST_SOME) continue;  // None / set() entries name no nucleotide
+    if (!hash_last(V, key_bits(a.xq_mass[start + o]), o)) continue;
+    const uint8_t* p = (const uint8_t*)a.xa_ptr[start + o];
+    uint64_t u0 = 0, u1 = 0;
+    for (uint32_t c = 0; c < a.xa_n[start + o]; ++c) {
+      const int k = p[0];
+      for (int j = 0; j < k; ++j) {
+        const int r = p[1 + j];
+        if (r < 64) u0 |= 1ull << r;
+        else u1 |= 1ull << (r - 64);
+      }
+      p += 1 + k;
+    }
+    if (u0) atomicOr(&M.u0, (unsigned long long)u0);
+    if (u1) atomicOr(&M.u1, (unsigned long long)u1);
+  }
+  __syncthreads();
+  fix_outcome(M, a, g, Q);
+}
+
+}  // namespace
+
 // the rest of an exact-mode round (after the caller answered the list): the
 // dict's last writer per key (a side pair only with >= 1 explanation, a
 // singleton always), the rows its surviving answers name (their candidates'
@@ -352,77 +604,27 @@ __device__ void fix_list(const FixLds& L, const PipeArgs& a, int64_t g, uint32_t
 __global__ __launch_bounds__(kPipeWG) void k_fix_finish(PipeArgs a) {
   __shared__ uint64_t hkey[kHashSlots];
   __shared__ uint32_t hidx[kHashSlots];
-  __shared__ unsigned long long su0, su1;
-  __shared__ uint32_t writers;
+  __shared__ FixMeta M;
+  const FixView V{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, hkey, hidx, (uint32_t)kHashSlots - 1};
   for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
     if (!a.active[g] || !a.pair_ok || a.pair_ok[g]) continue;  // k_fix_round settled it
-    const uint64_t blk = a.xq_block[g];
-    const uint32_t start = (uint32_t)(blk >> 32), Q = (uint32_t)blk;
-    for (int k = threadIdx.x; k < kHashSlots; k += blockDim.x) {
-      hkey[k] = kEmptyKey;
-      hidx[k] = 0;
-    }
-    if (threadIdx.x == 0) {
-      su0 = su1 = 0;
-      writers = 0;
-    }
-    __syncthreads();
-    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
-      const int8_t st = a.xa_st[start + o];
-      if (st != SST_NONE && st != SST_EMPTY && st != SST_SOME) atomicOr(a.err, 128u);  // raised / capped
-      if (!(a.xq_single[start + o] || st == SST_SOME)) continue;
-      const uint64_t key = key_bits(a.xq_mass[start + o]);
-      uint32_t h = key_hash(key);
-      for (int probe = 0; probe < kHashSlots; ++probe, h = (h + 1) & (kHashSlots - 1)) {
-        const unsigned long long prev = atomicCAS((unsigned long long*)&hkey[h], kEmptyKey, key);
-        if (prev == kEmptyKey || prev == key) {
-          atomicMax(&hidx[h], o + 1);
-          if (prev == kEmptyKey) atomicAdd(&writers, 1u);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    if (writers > kHashSlots * 3 / 4 && threadIdx.x == 0) atomicOr(a.err, 16u);
-    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
-      if (a.xa_st[start + o] != SST_SOME) continue;  // None / set() entries name no nucleotide
-      const uint64_t key = key_bits(a.xq_mass[start + o]);
-      uint32_t h = key_hash(key);
-      for (int probe = 0; probe < kHashSlots && hkey[h] != key; ++probe) h = (h + 1) & (kHashSlots - 1);
-      if (hkey[h] != key || hidx[h] != o + 1) continue;
-      const uint8_t* p = (const uint8_t*)a.xa_ptr[start + o];
-      uint64_t u0 = 0, u1 = 0;
-      for (uint32_t c = 0; c < a.xa_n[start + o]; ++c) {
-        const int k = p[0];
-        for (int j = 0; j < k; ++j) {
-          const int r = p[1 + j];
-          if (r < 64) u0 |= 1ull << r;
-          else u1 |= 1ull << (r - 64);
-        }
-        p += 1 + k;
-      }
-      if (u0) atomicOr(&su0, (unsigned long long)u0);
-      if (u1) atomicOr(&su1, (unsigned long long)u1);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
-      const uint64_t n0 = a.canon[0] | (m0 & su0), n1 = a.canon[1] | (m1 & su1);
-      a.alpha_next[2 * g] = n0;
-      a.alpha_next[2 * g + 1] = n1;
-      const bool changed = __builtin_popcountll(n0) + __builtin_popcountll(n1) !=
-                           __builtin_popcountll(m0) + __builtin_popcountll(m1);
-      a.active_next[g] = changed;
-      a.rounds[g] += 1;
-      a.queries[g] += Q;
-      if (changed) atomicAdd(a.n_active, 1u);
-    }
-    __syncthreads();
+    const uint32_t nr = a.cnt[g];
+    if (nr > (uint32_t)kPipeMaxRows) continue;  // k_fix_finish_big's, or rejected by k_fix_round
+    fix_finish_spec(a, M, V, g);
   }
+}
+__global__ __launch_bounds__(kPipeWG) void k_fix_finish_big(PipeArgs a) {
+  __shared__ FixMeta M;
+  const FixView V = big_view(a);
+  for_big_spectra(a, [&](int64_t g, uint32_t nr) {
+    if (a.active[g] && a.pair_ok && !a.pair_ok[g] && !pipe_too_big(a, nr)) fix_finish_spec(a, M, V, g);
+  });
 }
 
 __global__ __launch_bounds__(kPipeWG) void k_fix_round(TableArgs t, PipeArgs a) {
-  __shared__ FixLds L;
+  __shared__ FixLdsArrays S;
+  __shared__ FixMeta M;
+  const FixView V = lds_view(S);
   for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
     if (!a.active[g]) {  // settled earlier: its alphabet carries over
       if (threadIdx.x == 0) {
@@ -432,290 +634,254 @@ __global__ __launch_bounds__(kPipeWG) void k_fix_round(TableArgs t, PipeArgs a) 
       }
       continue;
     }
-    const int64_t base = 4 * a.peak_off[g];
     const uint32_t nr = a.cnt[g];
-    if (nr > (uint32_t)kPipeMaxRows) {
-      if (threadIdx.x == 0) {
-        atomicOr(a.err, 2u);
-        a.alpha_next[2 * g] = a.alpha[2 * g];
-        a.alpha_next[2 * g + 1] = a.alpha[2 * g + 1];
-        a.active_next[g] = 0;
-      }
+    if (nr > (uint32_t)kPipeMaxRows) {  // k_fix_round_big's
+      if (pipe_too_big(a, nr)) fix_reject(a, g);
       continue;
     }
-    // the alive rows (SU order) and each side's / the singletons' lists
-    uint32_t carry[4] = {0, 0, 0, 0};
-    for (uint32_t r0 = 0; r0 < nr; r0 += blockDim.x) {
-      const uint32_t r = r0 + threadIdx.x;
-      const bool al = r < nr && a.alive[base + r];
-      const uint32_t meta = al ? a.r_meta[base + r] : 0u;
-      uint32_t tot;
-      const uint32_t ex = block_excl(al ? 1u : 0u, L.w, tot);
-      const uint32_t i = carry[0] + ex;
-      if (al) {
-        L.su[i] = a.r_su[base + r];
-        L.ob[i] = a.r_ob[base + r];
-      }
-      carry[0] += tot;
-      for (int c = 0; c < 3; ++c) {
-        const bool f = al && ((meta >> (2 + c)) & 1u);  // START, END, singleton
-        const uint32_t x = block_excl(f ? 1u : 0u, L.w, tot);
-        if (f) (c < 2 ? L.side[c] : L.single)[carry[c + 1] + x] = (uint16_t)i;
-        carry[c + 1] += tot;
-      }
-    }
-    if (threadIdx.x == 0) {
-      L.n_alive = carry[0];
-      L.n_side[0] = carry[1];
-      L.n_side[1] = carry[2];
-      L.n_single = carry[3];
-      L.u0 = L.u1 = 0;
-      L.writers = 0;
-    }
-    for (int k = threadIdx.x; k < kHashSlots; k += blockDim.x) {
-      L.hkey[k] = kEmptyKey;
-      L.hidx[k] = 0;
-    }
-    __syncthreads();
-    const uint32_t q0 = fix_side_pairs(L, 0, a.max_weight);
-    const uint32_t q1 = fix_side_pairs(L, 1, a.max_weight);
-    const uint32_t Q = q0 + q1 + L.n_single;
-    const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
-    if (a.pair_ok && !a.pair_ok[g]) {  // budgets can bind: list the round's queries for the exact explain
-      fix_list(L, a, g, q0, q1, Q);
-      continue;
-    }
-    // pass A: every query's answer; writers insert their key, the last (largest order) wins
-    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
-      double mass, thr;
-      bool single, pc;
-      fix_query(L, o, q0, q1, a.tol, mass, thr, single);
-      uint64_t u0, u1;
-      const int8_t st = masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
-      if (!pc) atomicOr(a.err, 4u);  // not pair-class: never for these windows (the host checks)
-      if (!(single || st == SST_SOME)) continue;
-      const uint64_t key = key_bits(mass);
-      uint32_t h = key_hash(key);
-      for (int probe = 0; probe < kHashSlots; ++probe, h = (h + 1) & (kHashSlots - 1)) {
-        const unsigned long long prev = atomicCAS((unsigned long long*)&L.hkey[h], kEmptyKey, key);
-        if (prev == kEmptyKey || prev == key) {
-          atomicMax(&L.hidx[h], o + 1);
-          if (prev == kEmptyKey) atomicAdd(&L.writers, 1u);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    if (L.writers > kHashSlots * 3 / 4) {  // too full to trust the probe bound: reported
-      if (threadIdx.x == 0) atomicOr(a.err, 16u);
-    }
-    // pass B: the dict's surviving entries -> the observed rows
-    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
-      double mass, thr;
-      bool single, pc;
-      fix_query(L, o, q0, q1, a.tol, mass, thr, single);
-      uint64_t u0, u1;
-      const int8_t st = masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
-      if (st != SST_SOME) continue;  // None / set() entries name no nucleotide
-      const uint64_t key = key_bits(mass);
-      uint32_t h = key_hash(key);
-      for (int probe = 0; probe < kHashSlots && L.hkey[h] != key; ++probe) h = (h + 1) & (kHashSlots - 1);
-      if (L.hkey[h] == key && L.hidx[h] == o + 1) {
-        if (u0) atomicOr(&L.u0, (unsigned long long)u0);
-        if (u1) atomicOr(&L.u1, (unsigned long long)u1);
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      // adapt_individual_modification_rates_by_alphabet_reduction: canonical
-      // rows stay, a modification stays iff an explanation names it
-      const uint64_t n0 = a.canon[0] | (m0 & L.u0), n1 = a.canon[1] | (m1 & L.u1);
-      a.alpha_next[2 * g] = n0;
-      a.alpha_next[2 * g + 1] = n1;
-      const bool changed = __builtin_popcountll(n0) + __builtin_popcountll(n1) !=
-                           __builtin_popcountll(m0) + __builtin_popcountll(m1);
-      a.active_next[g] = changed;
-      a.rounds[g] += 1;
-      a.queries[g] += Q;
-      if (changed) atomicAdd(a.n_active, 1u);
-    }
-    __syncthreads();
+    fix_round_spec(t, a, M, V, g, nr);
   }
 }
-
-// filter_by_explanation's final dict (DictArgs): the last round's queries
-// over the final alive rows, answered on the final alphabet; count pass: the
-// query count per spectrum; build pass: the last writer per key (LDS hash, as
-// k_fix_round), then the entries sorted by key into the spectrum's region.
-__global__ __launch_bounds__(kPipeWG) void k_dict(TableArgs t, PipeArgs a, DictArgs d, int count_only) {
-  __shared__ FixLds L;
-  __shared__ uint32_t ent[kHashSlots];
-  __shared__ uint32_t n_ent;
-  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
-    const int64_t base = 4 * a.peak_off[g];
-    const uint32_t nr = a.cnt[g];
-    if (nr > (uint32_t)kPipeMaxRows) {
-      if (threadIdx.x == 0) {
-        atomicOr(a.err, 2u);
-        if (count_only) d.n_q[g] = 0;
-        else d.n_ent[g] = 0;
-      }
-      continue;
-    }
-    uint32_t carry[4] = {0, 0, 0, 0};
-    for (uint32_t r0 = 0; r0 < nr; r0 += blockDim.x) {
-      const uint32_t r = r0 + threadIdx.x;
-      const bool al = r < nr && a.alive[base + r];
-      const uint32_t meta = al ? a.r_meta[base + r] : 0u;
-      uint32_t tot;
-      const uint32_t ex = block_excl(al ? 1u : 0u, L.w, tot);
-      const uint32_t i = carry[0] + ex;
-      if (al) {
-        L.su[i] = a.r_su[base + r];
-        L.ob[i] = a.r_ob[base + r];
-      }
-      carry[0] += tot;
-      for (int c = 0; c < 3; ++c) {
-        const bool f = al && ((meta >> (2 + c)) & 1u);  // START, END, singleton
-        const uint32_t x = block_excl(f ? 1u : 0u, L.w, tot);
-        if (f) (c < 2 ? L.side[c] : L.single)[carry[c + 1] + x] = (uint16_t)i;
-        carry[c + 1] += tot;
-      }
-    }
-    if (threadIdx.x == 0) {
-      L.n_alive = carry[0];
-      L.n_side[0] = carry[1];
-      L.n_side[1] = carry[2];
-      L.n_single = carry[3];
-      L.writers = 0;
-      n_ent = 0;
-    }
-    if (!count_only)
-      for (int k = threadIdx.x; k < kHashSlots; k += blockDim.x) {
-        L.hkey[k] = kEmptyKey;
-        L.hidx[k] = 0;
-      }
-    __syncthreads();
-    const uint32_t q0 = fix_side_pairs(L, 0, a.max_weight);
-    const uint32_t q1 = fix_side_pairs(L, 1, a.max_weight);
-    const uint32_t Q = q0 + q1 + L.n_single;
-    const bool exact = a.pair_ok && !a.pair_ok[g];  // budgets can bind: the listed answers
-    if (count_only == 1) {
-      if (threadIdx.x == 0) d.n_q[g] = Q;
-      __syncthreads();
-      continue;
-    }
-    if (count_only == 2) {  // list the exact-mode spectra's queries for the masked explain
-      if (exact) fix_list(L, a, g, q0, q1, Q);
-      continue;
-    }
-    const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
-    const uint32_t xstart = exact ? (uint32_t)(a.xq_block[g] >> 32) : 0u;
-    for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
-      double mass, thr;
-      bool single, pc = true;
-      fix_query(L, o, q0, q1, a.tol, mass, thr, single);
-      uint64_t u0, u1;
-      const int8_t st = exact ? a.xa_st[xstart + o] : masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
-      if (!pc) atomicOr(a.err, 4u);
-      if (!(single || st == SST_SOME)) continue;
-      const uint64_t key = key_bits(mass);
-      uint32_t h = key_hash(key);
-      for (int probe = 0; probe < kHashSlots; ++probe, h = (h + 1) & (kHashSlots - 1)) {
-        const unsigned long long prev = atomicCAS((unsigned long long*)&L.hkey[h], kEmptyKey, key);
-        if (prev == kEmptyKey || prev == key) {
-          atomicMax(&L.hidx[h], o + 1);
-          if (prev == kEmptyKey) atomicAdd(&L.writers, 1u);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    if (L.writers > kHashSlots * 3 / 4 && threadIdx.x == 0) atomicOr(a.err, 16u);
-    // the occupied slots, then each entry's rank by key (entries are few)
-    for (int k = threadIdx.x; k < kHashSlots; k += blockDim.x)
-      if (L.hkey[k] != kEmptyKey) ent[atomicAdd(&n_ent, 1u)] = (uint32_t)k;
-    __syncthreads();
-    const uint32_t E = n_ent;
-    const uint64_t out0 = d.off[g];
-    for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) {
-      const uint64_t key = L.hkey[ent[e]];
-      uint32_t rank = 0;
-      for (uint32_t f = 0; f < E; ++f) rank += L.hkey[ent[f]] < key;  // keys are distinct
-      double mass, thr;
-      bool single;
-      fix_query(L, L.hidx[ent[e]] - 1, q0, q1, a.tol, mass, thr, single);
-      d.key[out0 + rank] = key;
-      d.thr[out0 + rank] = thr;
-    }
-    if (threadIdx.x == 0) d.n_ent[g] = E;
-    __syncthreads();
-  }
+__global__ __launch_bounds__(kPipeWG) void k_fix_round_big(TableArgs t, PipeArgs a) {
+  __shared__ FixMeta M;
+  const FixView V = big_view(a);
+  for_big_spectra(a, [&](int64_t g, uint32_t nr) {
+    if (a.active[g] && !pipe_too_big(a, nr)) fix_round_spec(t, a, M, V, g, nr);
+  });
 }
 
 namespace {
 
-struct BinLds {
+// k_dict's entries of one spectrum by key into its region: few in the LDS
+// variant (a rank count over the occupied slots), a bitonic sort of (key,
+// slot) pairs in the HBM slice in the big one
+__device__ __forceinline__ void dict_emit_lds(FixMeta& M, const FixView& V, const PipeArgs& a, const DictArgs& d,
+                                              int64_t g, uint32_t q0, uint32_t q1, uint32_t* ent) {
+  for (uint32_t k = threadIdx.x; k <= V.hmask; k += blockDim.x)
+    if (ld_key(&V.hkey[k]) != kEmptyKey) ent[atomicAdd(&M.n_ent, 1u)] = k;
+  __syncthreads();
+  const uint32_t E = M.n_ent;
+  const uint64_t out0 = d.off[g];
+  for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) {
+    const uint64_t key = ld_key(&V.hkey[ent[e]]);
+    uint32_t rank = 0;
+    for (uint32_t f = 0; f < E; ++f) rank += ld_key(&V.hkey[ent[f]]) < key;  // keys are distinct
+    double mass, thr;
+    bool single;
+    fix_query(M, V, ld_idx(&V.hidx[ent[e]]) - 1, q0, q1, a.tol, mass, thr, single);
+    d.key[out0 + rank] = key;
+    d.thr[out0 + rank] = thr;
+  }
+  if (threadIdx.x == 0) d.n_ent[g] = E;
+}
+__device__ __forceinline__ void dict_emit_big(FixMeta& M, const FixView& V, const PipeArgs& a, const DictArgs& d,
+                                              int64_t g, uint32_t q0, uint32_t q1) {
+  const PipeBigLayout B = pipe_big_layout(a.big_rows, a.big_slots);
+  uint64_t* sk = (uint64_t*)(big_slice(a) + B.sk);
+  uint32_t* si = (uint32_t*)(big_slice(a) + B.si);
+  for (uint32_t k = threadIdx.x; k <= V.hmask; k += blockDim.x) {
+    const uint64_t key = ld_key(&V.hkey[k]);
+    if (key != kEmptyKey) {
+      const uint32_t e = atomicAdd(&M.n_ent, 1u);
+      sk[e] = key;
+      si[e] = k;
+    }
+  }
+  __syncthreads();
+  const uint32_t E = M.n_ent;
+  uint32_t N = 1;
+  while (N < E) N <<= 1;
+  for (uint32_t e = E + threadIdx.x; e < N; e += blockDim.x) {
+    sk[e] = kEmptyKey;  // never a key (no mass has these bits): sorts last
+    si[e] = 0;
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= N; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+        const uint32_t l = i ^ j;
+        if (l <= i) continue;
+        const uint64_t x = sk[i], y = sk[l];
+        if ((x > y) == ((i & k) == 0)) {
+          sk[i] = y;
+          sk[l] = x;
+          const uint32_t t = si[i];
+          si[i] = si[l];
+          si[l] = t;
+        }
+      }
+      __syncthreads();
+    }
+  const uint64_t out0 = d.off[g];
+  for (uint32_t e = threadIdx.x; e < E; e += blockDim.x) {
+    double mass, thr;
+    bool single;
+    fix_query(M, V, ld_idx(&V.hidx[si[e]]) - 1, q0, q1, a.tol, mass, thr, single);
+    d.key[out0 + e] = sk[e];
+    d.thr[out0 + e] = thr;
+  }
+  if (threadIdx.x == 0) d.n_ent[g] = E;
+}
+
+// k_dict on one spectrum (mode as launch_dict)
+template <bool BIG>
+__device__ __forceinline__ void dict_spec(const TableArgs& t, const PipeArgs& a, const DictArgs& d, int mode,
+                                          FixMeta& M, const FixView& V, int64_t g, uint32_t nr, uint32_t* ent) {
+  fix_load(M, V, a, 4 * a.peak_off[g], nr);
+  if (mode == 0) hash_clear(V);
+  __syncthreads();
+  const uint32_t q0 = fix_side_pairs(M, V, 0, a.max_weight);
+  const uint32_t q1 = fix_side_pairs(M, V, 1, a.max_weight);
+  const uint32_t Q = q0 + q1 + M.n_single;
+  const bool exact = a.pair_ok && !a.pair_ok[g];  // budgets can bind: the listed answers
+  if (mode == 1) {
+    if (threadIdx.x == 0) d.n_q[g] = Q;
+    __syncthreads();
+    return;
+  }
+  if (mode == 2) {  // list the exact-mode spectra's queries for the masked explain
+    if (exact) fix_list(M, V, a, g, q0, q1, Q);
+    return;
+  }
+  const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+  const uint32_t xstart = exact ? (uint32_t)(a.xq_block[g] >> 32) : 0u;
+  for (uint32_t o = threadIdx.x; o < Q; o += blockDim.x) {
+    double mass, thr;
+    bool single, pc = true;
+    fix_query(M, V, o, q0, q1, a.tol, mass, thr, single);
+    uint64_t u0, u1;
+    const int8_t st = exact ? a.xa_st[xstart + o] : masked_answer(t, mass, thr, a.prec, a.rprec, m0, m1, u0, u1, pc);
+    if (!pc) atomicOr(a.err, 4u);
+    if (single || st == SST_SOME) hash_put(V, &M.writers, key_bits(mass), o);
+  }
+  __syncthreads();
+  hash_check(M, V, a);
+  if constexpr (BIG) dict_emit_big(M, V, a, d, g, q0, q1);
+  else dict_emit_lds(M, V, a, d, g, q0, q1, ent);
+  __syncthreads();
+}
+
+}  // namespace
+
+// filter_by_explanation's final dict (DictArgs): the last round's queries
+// over the final alive rows, answered on the final alphabet; count pass: the
+// query count per spectrum; build pass: the last writer per key (the hash of
+// k_fix_round), then the entries sorted by key into the spectrum's region.
+__global__ __launch_bounds__(kPipeWG) void k_dict(TableArgs t, PipeArgs a, DictArgs d, int mode) {
+  __shared__ FixLdsArrays S;
+  __shared__ FixMeta M;
+  __shared__ uint32_t ent[kHashSlots];
+  const FixView V = lds_view(S);
+  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
+    const uint32_t nr = a.cnt[g];
+    if (nr > (uint32_t)kPipeMaxRows) {  // k_dict_big's
+      if (pipe_too_big(a, nr) && threadIdx.x == 0) {
+        atomicOr(a.err, 2u);
+        if (mode == 1) d.n_q[g] = 0;
+        else if (mode == 0) d.n_ent[g] = 0;
+        else if (a.pair_ok && !a.pair_ok[g]) a.xq_block[g] = 0;
+      }
+      continue;
+    }
+    dict_spec<false>(t, a, d, mode, M, V, g, nr, ent);
+  }
+}
+__global__ __launch_bounds__(kPipeWG) void k_dict_big(TableArgs t, PipeArgs a, DictArgs d, int mode) {
+  __shared__ FixMeta M;
+  const FixView V = big_view(a);
+  for_big_spectra(a, [&](int64_t g, uint32_t nr) {
+    if (!pipe_too_big(a, nr)) dict_spec<true>(t, a, d, mode, M, V, g, nr, nullptr);
+  });
+}
+
+namespace {
+
+// SkeletonBuilder's bins over one spectrum's alive rows (views as FixView)
+struct BinView {
+  double* su;
+  double* ob;
+  uint16_t* s0;  // alive rows of each side, SU order
+  uint16_t* s1;
+  uint16_t* b0;  // per side: first row of each bin, then the row count
+  uint16_t* b1;
+  uint32_t* q0;  // per side: exclusive prefix of each bin's queries
+  uint32_t* q1;
+  __device__ __forceinline__ uint16_t* side(int sd) const { return sd ? s1 : s0; }
+  __device__ __forceinline__ uint16_t* bstart(int sd) const { return sd ? b1 : b0; }
+  __device__ __forceinline__ uint32_t* qoff(int sd) const { return sd ? q1 : q0; }
+};
+struct BinLdsArrays {
   double su[kPipeMaxRows];
   double ob[kPipeMaxRows];
-  uint16_t side[2][kPipeMaxRows];        // alive rows of each side, SU order
-  uint16_t bstart[2][kPipeMaxRows + 1];  // per side: first row of each bin, then the row count
-  uint32_t qoff[2][kPipeMaxRows + 1];    // per side: exclusive prefix of each bin's queries
+  uint16_t side[2][kPipeMaxRows];
+  uint16_t bstart[2][kPipeMaxRows + 1];
+  uint32_t qoff[2][kPipeMaxRows + 1];
+};
+struct BinMeta {
   uint32_t n_side[2], nb[2];
   uint32_t w[16];
 };
+__device__ __forceinline__ BinView lds_bin_view(BinLdsArrays& S) {
+  return BinView{S.su, S.ob, S.side[0], S.side[1], S.bstart[0], S.bstart[1], S.qoff[0], S.qoff[1]};
+}
+__device__ __forceinline__ BinView big_bin_view(const PipeArgs& a) {
+  const PipeBigLayout B = pipe_big_layout(a.big_rows, a.big_slots);
+  uint8_t* p = big_slice(a);
+  return BinView{(double*)(p + B.su),   (double*)(p + B.ob),   (uint16_t*)(p + B.s0), (uint16_t*)(p + B.s1),
+                 (uint16_t*)(p + B.b0), (uint16_t*)(p + B.b1), (uint32_t*)(p + B.q0), (uint32_t*)(p + B.q1)};
+}
 
-// the alive rows of spectrum g and each side's list (false: too many rows)
-__device__ bool bins_load(BinLds& L, const PipeArgs& a, int64_t g) {
+// the alive rows of spectrum g and each side's list
+__device__ __forceinline__ void bins_load(BinMeta& M, const BinView& V, const PipeArgs& a, int64_t g, uint32_t nr) {
   const int64_t base = 4 * a.peak_off[g];
-  const uint32_t nr = a.cnt[g];
-  if (nr > (uint32_t)kPipeMaxRows) return false;
   uint32_t carry[3] = {0, 0, 0};
   for (uint32_t r0 = 0; r0 < nr; r0 += blockDim.x) {
     const uint32_t r = r0 + threadIdx.x;
     const bool al = r < nr && a.alive[base + r];
     const uint32_t meta = al ? a.r_meta[base + r] : 0u;
     uint32_t tot;
-    const uint32_t ex = block_excl(al ? 1u : 0u, L.w, tot);
+    const uint32_t ex = block_excl(al ? 1u : 0u, M.w, tot);
     const uint32_t i = carry[0] + ex;
     if (al) {
-      L.su[i] = a.r_su[base + r];
-      L.ob[i] = a.r_ob[base + r];
+      V.su[i] = a.r_su[base + r];
+      V.ob[i] = a.r_ob[base + r];
     }
     carry[0] += tot;
     for (int c = 0; c < 2; ++c) {
       const bool f = al && ((meta >> (2 + c)) & 1u);  // START, END
-      const uint32_t x = block_excl(f ? 1u : 0u, L.w, tot);
-      if (f) L.side[c][carry[c + 1] + x] = (uint16_t)i;
+      const uint32_t x = block_excl(f ? 1u : 0u, M.w, tot);
+      if (f) V.side(c)[carry[c + 1] + x] = (uint16_t)i;
       carry[c + 1] += tot;
     }
   }
   if (threadIdx.x == 0) {
-    L.n_side[0] = carry[1];
-    L.n_side[1] = carry[2];
+    M.n_side[0] = carry[1];
+    M.n_side[1] = carry[2];
   }
   __syncthreads();
-  return true;
 }
 
 // side sd's bins and each bin's query count prefix; returns the side's queries
-__device__ uint32_t bins_side(BinLds& L, int sd, double tol) {
-  const uint32_t n = L.n_side[sd];
-  const uint16_t* rs = L.side[sd];
+__device__ __forceinline__ uint32_t bins_side(BinMeta& M, const BinView& V, int sd, double tol) {
+  const uint32_t n = M.n_side[sd];
+  const uint16_t* rs = V.side(sd);
+  uint16_t* bs = V.bstart(sd);
+  uint32_t* qoff = V.qoff(sd);
   uint32_t carry = 0;
   for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {
     const uint32_t i = i0 + threadIdx.x;
     // row i joins row i - 1's bin when their SU step is within the pair threshold (:130-136)
-    const bool starts = i < n && (i == 0 || !(L.su[rs[i]] - L.su[rs[i - 1]] <= tol * (L.ob[rs[i - 1]] + L.ob[rs[i]])));
+    const bool starts =
+        i < n && (i == 0 || !(V.su[rs[i]] - V.su[rs[i - 1]] <= tol * (V.ob[rs[i - 1]] + V.ob[rs[i]])));
     uint32_t tot;
-    const uint32_t ex = block_excl(starts ? 1u : 0u, L.w, tot);
-    if (starts) L.bstart[sd][carry + ex] = (uint16_t)i;
+    const uint32_t ex = block_excl(starts ? 1u : 0u, M.w, tot);
+    if (starts) bs[carry + ex] = (uint16_t)i;
     carry += tot;
   }
   const uint32_t nb = carry;
   if (threadIdx.x == 0) {
-    L.bstart[sd][nb] = (uint16_t)n;
-    L.nb[sd] = nb;
+    bs[nb] = (uint16_t)n;
+    M.nb[sd] = nb;
   }
   __syncthreads();
   carry = 0;
@@ -723,111 +889,145 @@ __device__ uint32_t bins_side(BinLds& L, int sd, double tol) {
     const uint32_t b = b0 + threadIdx.x;
     uint32_t c = 0;
     if (b < nb) {
-      const uint32_t size = (uint32_t)L.bstart[sd][b + 1] - L.bstart[sd][b];
+      const uint32_t size = (uint32_t)bs[b + 1] - bs[b];
       const bool closed = b + 1 < nb || size > 1;  // a later row closes it, or the side's last row joined it
-      if (closed) c = b == 0 ? size : ((uint32_t)L.bstart[sd][b] - L.bstart[sd][b - 1]) * size;
+      if (closed) c = b == 0 ? size : ((uint32_t)bs[b] - bs[b - 1]) * size;
     }
     uint32_t tot;
-    const uint32_t ex = block_excl(c, L.w, tot);
-    if (b < nb) L.qoff[sd][b] = carry + ex;
+    const uint32_t ex = block_excl(c, M.w, tot);
+    if (b < nb) qoff[b] = carry + ex;
     carry += tot;
   }
-  if (threadIdx.x == 0) L.qoff[sd][nb] = carry;
+  if (threadIdx.x == 0) qoff[nb] = carry;
   __syncthreads();
   return carry;
 }
 
 // query q of side sd: the first bin's whole mass against 0, a later bin's
 // (predecessor row, row) difference; threshold as calculate_error_threshold
-__device__ __forceinline__ void bins_query(const BinLds& L, int sd, uint32_t q, double tol, double& mass,
-                                           double& thr) {
-  uint32_t lo = 0, hi = L.nb[sd];  // last bin with qoff <= q (empty bins share their successor's offset)
+__device__ __forceinline__ void bins_query(const BinMeta& M, const BinView& V, int sd, uint32_t q, double tol,
+                                           double& mass, double& thr) {
+  const uint32_t* qoff = V.qoff(sd);
+  const uint16_t* bs = V.bstart(sd);
+  uint32_t lo = 0, hi = M.nb[sd];  // last bin with qoff <= q (empty bins share their successor's offset)
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (L.qoff[sd][mid] <= q) lo = mid;
+    if (qoff[mid] <= q) lo = mid;
     else hi = mid;
   }
-  const uint32_t b = lo, local = q - L.qoff[sd][b];
-  const uint16_t* rs = L.side[sd];
+  const uint32_t b = lo, local = q - qoff[b];
+  const uint16_t* rs = V.side(sd);
   if (b == 0) {
-    const uint32_t m = rs[L.bstart[sd][0] + local];
-    mass = L.su[m];
-    thr = tol * (0.0 + L.ob[m]);
+    const uint32_t m = rs[bs[0] + local];
+    mass = V.su[m];
+    thr = tol * (0.0 + V.ob[m]);
     return;
   }
-  const uint32_t csz = (uint32_t)L.bstart[sd][b + 1] - L.bstart[sd][b];
-  const uint32_t p = rs[L.bstart[sd][b - 1] + local / csz], r = rs[L.bstart[sd][b] + local % csz];
-  mass = L.su[r] - L.su[p];
-  thr = tol * (L.ob[p] + L.ob[r]);
+  const uint32_t csz = (uint32_t)bs[b + 1] - bs[b];
+  const uint32_t p = rs[bs[b - 1] + local / csz], r = rs[bs[b] + local % csz];
+  mass = V.su[r] - V.su[p];
+  thr = tol * (V.ob[p] + V.ob[r]);
+}
+
+__device__ __forceinline__ void bins_count_spec(const PipeArgs& a, BinMeta& M, const BinView& V, int64_t g,
+                                                uint32_t nr) {
+  bins_load(M, V, a, g, nr);
+  const uint32_t q0 = bins_side(M, V, 0, a.tol);
+  const uint32_t q1 = bins_side(M, V, 1, a.tol);
+  if (threadIdx.x == 0) {
+    a.n_q[g] = q0 + q1;
+    if (a.n_q0) a.n_q0[g] = q0;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void bins_emit_spec(const TableArgs& t, const PipeArgs& a, BinMeta& M, const BinView& V,
+                                               int64_t g, uint32_t nr) {
+  bins_load(M, V, a, g, nr);
+  const uint32_t q0 = bins_side(M, V, 0, a.tol);
+  const uint32_t q1 = bins_side(M, V, 1, a.tol);
+  const uint64_t base = a.q_off[g];
+  const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
+  for (uint32_t o = threadIdx.x; o < q0 + q1; o += blockDim.x) {
+    const int sd = o >= q0;
+    double mass, thr;
+    bins_query(M, V, sd, sd ? o - q0 : o, a.tol, mass, thr);
+    double lof, hif;
+    quantise_lean(mass, thr, a.prec, a.rprec, lof, hif);
+    int8_t st = SST_NONE;
+    uint32_t cnt = 0;
+    // off the pair class, or budgets that can bind: listed for the masked explain
+    const bool pend = !(hif < (double)t.pair_hi) || (a.pair_ok && !a.pair_ok[g]);
+    if (pend) {
+      st = (int8_t)kStatusPending;
+    } else if (hif >= 0.0) {
+      const double af = lof < 1.0 ? 1.0 : lof;
+      uint64_t u0 = 0, u1 = 0;
+      if (af <= hif) cnt = masked_walk(t, (uint32_t)af, (uint32_t)hif, m0, m1, u0, u1);
+      st = cnt ? (int8_t)SST_SOME : lof <= 0.0 ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;
+    }
+    a.q_status[base + o] = st;
+    a.q_count[base + o] = cnt;
+    if (a.n_def) {  // one returning atomic per wave instruction
+      const uint64_t bal = __ballot(pend);
+      if (pend) {
+        const int lane = threadIdx.x & 63, leader = __builtin_ctzll(bal);
+        uint32_t pos = 0;
+        if (lane == leader) pos = atomicAdd(a.n_def, (uint32_t)__builtin_popcountll(bal));
+        pos = __shfl(pos, leader, 64) + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+        a.def_mass[pos] = mass;
+        a.def_thr[pos] = thr;
+        a.def_spec[pos] = (int32_t)g;
+        a.def_q[pos] = base + o;
+      }
+    }
+  }
+  __syncthreads();
 }
 
 }  // namespace
 
 __global__ __launch_bounds__(kPipeWG) void k_bins_count(PipeArgs a) {
-  __shared__ BinLds L;
+  __shared__ BinLdsArrays S;
+  __shared__ BinMeta M;
+  const BinView V = lds_bin_view(S);
   for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
-    if (!bins_load(L, a, g)) {
-      if (threadIdx.x == 0) {
+    const uint32_t nr = a.cnt[g];
+    if (nr > (uint32_t)kPipeMaxRows) {  // k_bins_count_big's
+      if (pipe_too_big(a, nr) && threadIdx.x == 0) {
         atomicOr(a.err, 2u);
         a.n_q[g] = 0;
         if (a.n_q0) a.n_q0[g] = 0;
       }
       continue;
     }
-    const uint32_t q0 = bins_side(L, 0, a.tol);
-    const uint32_t q1 = bins_side(L, 1, a.tol);
-    if (threadIdx.x == 0) {
-      a.n_q[g] = q0 + q1;
-      if (a.n_q0) a.n_q0[g] = q0;
-    }
-    __syncthreads();
+    bins_count_spec(a, M, V, g, nr);
   }
+}
+__global__ __launch_bounds__(kPipeWG) void k_bins_count_big(PipeArgs a) {
+  __shared__ BinMeta M;
+  const BinView V = big_bin_view(a);
+  for_big_spectra(a, [&](int64_t g, uint32_t nr) {
+    if (!pipe_too_big(a, nr)) bins_count_spec(a, M, V, g, nr);
+  });
 }
 
 __global__ __launch_bounds__(kPipeWG) void k_bins_emit(TableArgs t, PipeArgs a) {
-  __shared__ BinLds L;
+  __shared__ BinLdsArrays S;
+  __shared__ BinMeta M;
+  const BinView V = lds_bin_view(S);
   for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
-    if (!bins_load(L, a, g)) continue;
-    const uint32_t q0 = bins_side(L, 0, a.tol);
-    const uint32_t q1 = bins_side(L, 1, a.tol);
-    const uint64_t base = a.q_off[g];
-    const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
-    for (uint32_t o = threadIdx.x; o < q0 + q1; o += blockDim.x) {
-      const int sd = o >= q0;
-      double mass, thr;
-      bins_query(L, sd, sd ? o - q0 : o, a.tol, mass, thr);
-      double lof, hif;
-      quantise_lean(mass, thr, a.prec, a.rprec, lof, hif);
-      int8_t st = SST_NONE;
-      uint32_t cnt = 0;
-      // off the pair class, or budgets that can bind: listed for the masked explain
-      const bool pend = !(hif < (double)t.pair_hi) || (a.pair_ok && !a.pair_ok[g]);
-      if (pend) {
-        st = (int8_t)kStatusPending;  // not a pair-class window: listed for the masked explain
-      } else if (hif >= 0.0) {
-        const double af = lof < 1.0 ? 1.0 : lof;
-        uint64_t u0 = 0, u1 = 0;
-        if (af <= hif) cnt = masked_walk(t, (uint32_t)af, (uint32_t)hif, m0, m1, u0, u1);
-        st = cnt ? (int8_t)SST_SOME : lof <= 0.0 ? (int8_t)SST_EMPTY : (int8_t)SST_NONE;
-      }
-      a.q_status[base + o] = st;
-      a.q_count[base + o] = cnt;
-      if (a.n_def) {  // one returning atomic per wave instruction
-        const uint64_t bal = __ballot(pend);
-        if (pend) {
-          const int lane = threadIdx.x & 63, leader = __builtin_ctzll(bal);
-          uint32_t pos = 0;
-          if (lane == leader) pos = atomicAdd(a.n_def, (uint32_t)__builtin_popcountll(bal));
-          pos = __shfl(pos, leader, 64) + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-          a.def_mass[pos] = mass;
-          a.def_thr[pos] = thr;
-          a.def_spec[pos] = (int32_t)g;
-          a.def_q[pos] = base + o;
-        }
-      }
-    }
-    __syncthreads();
+    const uint32_t nr = a.cnt[g];
+    if (nr > (uint32_t)kPipeMaxRows) continue;  // k_bins_emit_big's (or no queries: rejected)
+    bins_emit_spec(t, a, M, V, g, nr);
   }
+}
+__global__ __launch_bounds__(kPipeWG) void k_bins_emit_big(TableArgs t, PipeArgs a) {
+  __shared__ BinMeta M;
+  const BinView V = big_bin_view(a);
+  for_big_spectra(a, [&](int64_t g, uint32_t nr) {
+    if (!pipe_too_big(a, nr)) bins_emit_spec(t, a, M, V, g, nr);
+  });
 }
 
 // exclusive prefix of n u32 counts into n + 1 u64 offsets (one workgroup,
@@ -887,6 +1087,7 @@ hipError_t launch_dict(const TableArgs& t, const PipeArgs& a, const DictArgs& d,
                        hipStream_t st) {
   if (a.n_spec <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_dict, dim3(n_wg), dim3(kPipeWG), 0, st, t, a, d, mode);
+  if (a.big) hipLaunchKernelGGL(k_dict_big, dim3(a.big_wg), dim3(kPipeWG), 0, st, t, a, d, mode);
   return hipGetLastError();
 }
 hipError_t launch_scan_u32(const uint32_t* in, uint64_t* out, int64_t n, hipStream_t st) {
@@ -896,12 +1097,14 @@ hipError_t launch_scan_u32(const uint32_t* in, uint64_t* out, int64_t n, hipStre
 
 hipError_t launch_bins_count(const PipeArgs& a, int n_wg, hipStream_t st) {
   if (a.n_spec > 0) hipLaunchKernelGGL(k_bins_count, dim3(n_wg), dim3(kPipeWG), 0, st, a);
+  if (a.n_spec > 0 && a.big) hipLaunchKernelGGL(k_bins_count_big, dim3(a.big_wg), dim3(kPipeWG), 0, st, a);
   hipLaunchKernelGGL(k_scan_u32, dim3(1), dim3(kPipeWG), 0, st, (const uint32_t*)a.n_q, a.q_off, a.n_spec);
   return hipGetLastError();
 }
 hipError_t launch_bins_emit(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st) {
   if (a.n_spec <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_bins_emit, dim3(n_wg), dim3(kPipeWG), 0, st, t, a);
+  if (a.big) hipLaunchKernelGGL(k_bins_emit_big, dim3(a.big_wg), dim3(kPipeWG), 0, st, t, a);
   return hipGetLastError();
 }
 
@@ -913,11 +1116,13 @@ hipError_t launch_classify_rows(const TableArgs& t, const PipeArgs& a, int n_wg,
 hipError_t launch_fix_finish(const PipeArgs& a, int n_wg, hipStream_t st) {
   if (a.n_spec <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_fix_finish, dim3(n_wg), dim3(kPipeWG), 0, st, a);
+  if (a.big) hipLaunchKernelGGL(k_fix_finish_big, dim3(a.big_wg), dim3(kPipeWG), 0, st, a);
   return hipGetLastError();
 }
 hipError_t launch_fix_round(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st) {
   if (a.n_spec <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_fix_round, dim3(n_wg), dim3(kPipeWG), 0, st, t, a);
+  if (a.big) hipLaunchKernelGGL(k_fix_round_big, dim3(a.big_wg), dim3(kPipeWG), 0, st, t, a);
   return hipGetLastError();
 }
 

@@ -264,7 +264,7 @@ __global__ __launch_bounds__(256) void k_skel_walk(TableArgs t, WalkArgs a) {
   }
   uint64_t* sk = a.skel + 2 * (a.skel_off[g] + (sd ? (uint64_t)ML : 0));
   for (int i = 0; i < 2 * ML; ++i) sk[i] = 0;
-  if (nr > (uint32_t)kPipeMaxRows || ML + 2 > (int)a.len_cap) {
+  if (nr > (uint32_t)kPipeBigRows || ML + 2 > (int)a.len_cap) {
     a.side_status[sid] = kWalkLimit;
     return;
   }

@@ -21,7 +21,7 @@ from . import _native
 from .masses import PHOSPHATE_LINK_MASS
 from .pipeline import mask_rows, row_masks
 
-ERR_BITS = {1: "a spectrum has more than 1024 peaks", 2: "a spectrum has more than 2048 rows",
+ERR_BITS = {1: "a spectrum has more than 4096 peaks", 2: "a spectrum has more rows than the reserved slices hold",
             4: "a window outside the pair class", 8: "is_valid_mass raised (a window past a table's end)",
             16: "an explanation dict too large for the LDS hash", 32: "rows out of mass order"}
 
@@ -104,6 +104,12 @@ def classify_device(dp_table, obs, offsets, su_seq, breakage_dict, intensity=Non
     shifts = np.array([w * dp_table.precision for w in weights], dtype=np.float64)
     sides = np.array([("START" in n) | (("END" in n) << 1) for n in names], dtype=np.uint8)
     max_w = _max_weight()
+    eng = dp_table.device_table.engine
+    # spectra of more than 2048 rows run in the context's HBM slices (sst_pipe_reserve_rows)
+    peaks = np.diff(np.asarray(offsets, dtype=np.int64))
+    if len(peaks):
+        eng.check(eng._lib.sst_pipe_reserve_rows(dp_table.device_table.handle, min(int(peaks.max()), 4096) * len(shifts)),
+                  "sst_pipe_reserve_rows")
     su = torch.empty(max(1, 4 * P), dtype=torch.float64, device=dev)
     ob = torch.empty_like(su)
     meta = torch.empty(max(1, 4 * P), dtype=torch.int32, device=dev)
@@ -111,7 +117,6 @@ def classify_device(dp_table, obs, offsets, su_seq, breakage_dict, intensity=Non
     rows = torch.zeros(max(1, S), dtype=torch.int32, device=dev)
     valid = torch.empty(max(1, len(weights) * P), dtype=torch.int8, device=dev) if keep_valid else None
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    eng = dp_table.device_table.engine
     torch.cuda.synchronize(dev)
     eng.check(eng._lib.sst_classify_rows_device(
         dp_table.device_table.handle, obs_t.data_ptr(), off_t.data_ptr(), S, P,
@@ -272,7 +277,7 @@ def fixpoint_device(dp_table, rows: DeviceRows, max_len, tolerance=None, record=
                                          float(dp_table.precision), err.data_ptr(), xp), "sst_fix_round_device")
         if xio is not None:  # the listed queries answered exactly, then the exact-mode half of the round
             xio.answer(alpha)
-            eng.check(L.sst_fix_finish_device(h, S, alpha.data_ptr(), alpha_next.data_ptr(), active.data_ptr(),
+            eng.check(L.sst_fix_finish_device(h, S, rows.rows.data_ptr(), alpha.data_ptr(), alpha_next.data_ptr(), active.data_ptr(),
                                               active_next.data_ptr(), rounds.data_ptr(), queries.data_ptr(),
                                               n_active.data_ptr(), err.data_ptr(), xp), "sst_fix_finish_device")
         # re-filter only the spectra whose alphabet shrank: an unchanged alphabet is

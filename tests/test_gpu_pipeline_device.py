@@ -327,6 +327,86 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
         assert sk.requeries > 0 or bins.deferred["queries"] > 0
 
 
+def test_device_pipeline_big_spectra(engine):
+    """Spectra of ~3000 peaks (more than 2048 rows: the *_big variants of the
+    row kernels in HBM slices, sst_pipe_reserve_rows) batched with ordinary
+    ones: classify / fixpoint / bins against the host-driven stages (host
+    sliding windows answered by explain_pairs_alpha), and the big spectra's
+    skeleton walk, Jaccard length and combined skeleton against the
+    per-spectrum host mirrors."""
+    from spectrseqtools_amd import _native, pipeline, pipeline_device as PD
+    from spectrseqtools_amd.mass_explanation import MASS_NAMES
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict
+    from spectrseqtools_amd.synthetic import make_spectra
+
+    small = make_spectra(40, seed=59, len_range=(6, 14))
+    big = make_spectra(2, seed=61, len_range=(60, 60), noise_frac=7.5)
+    parts, seq_mass = [], []
+    for i in range(42):  # the big spectra at positions 7 and 30
+        src, g = (big, 0) if i == 7 else (big, 1) if i == 30 else (small, i - (i > 7) - (i > 30))
+        parts.append(src.observed[src.offsets[g]:src.offsets[g + 1]])
+        seq_mass.append(src.seq_mass[g])
+    obs = np.concatenate(parts)
+    offsets = np.concatenate([[0], np.cumsum([len(x) for x in parts])])
+    seq_mass = np.asarray(seq_mass)
+    n = len(parts)
+    assert max(len(x) for x in parts) > 2500
+    bd = build_breakage_dict(555.1294, 455.1491)
+    w_full = [k for k, v in bd.items() if "START_END" in v][0]
+    su_seq = seq_mass - w_full * TOLERANCE
+    seq = SequenceInformation(max_len=20, su_mass=float(su_seq[0]), obs_mass=float(seq_mass[0]),
+                              modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=engine)
+    max_len = pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:]))
+    c = pipeline.classify(obs, offsets, su_seq, dp, bd)
+    rows = PD.classify_device(dp, obs, offsets, su_seq, bd)
+    cnt = rows.rows.cpu().numpy()
+    assert np.array_equal(cnt, np.diff(c.offsets))
+    assert cnt[7] > 2048 and cnt[30] > 2048, cnt[[7, 30]]
+    slot = (4 * offsets[:-1])[c.spec] + (np.arange(len(c.spec)) - c.offsets[c.spec])
+    assert np.array_equal(rows.su.cpu().numpy()[slot], c.su)
+    fx_h = pipeline.filter_fixpoint(c, dp, max_len, EXPLANATION_MASSES)
+    fx_d = PD.fixpoint_device(dp, rows, max_len)
+    assert np.array_equal(fx_d.alpha, fx_h.alpha)
+    assert np.array_equal(fx_d.rounds, fx_h.rounds)
+    assert np.array_equal(rows.alive.cpu().numpy()[slot].astype(bool), fx_h.alive)
+    c3 = pipeline.subset(c, fx_h.alive)
+    q3 = pipeline.bin_queries(c3)
+    st3, cnt3, _, _ = dp.device_table.explain_pairs_alpha(q3.diff, q3.thr, q3.spec, fx_h.alpha, dp.tolerance,
+                                                          dp.precision)
+    order = np.lexsort((q3.side, q3.spec))
+    db = PD.bins_device(dp, rows, fx_d.alpha)
+    assert np.array_equal(np.diff(db.q_off), np.bincount(q3.spec, minlength=n))
+    assert np.array_equal(db.status.cpu().numpy(), st3[order])
+    assert np.array_equal(db.count.cpu().numpy().astype(np.int64), cnt3[order].astype(np.int64))
+    # stages 4-5 for the big spectra (and a few ordinary ones) against the mirrors
+    bins = PD.bins_device(dp, rows, fx_d.alpha, max_len=max_len)
+    sk = PD.skeleton_device(dp, rows, fx_d.alpha, max_len, bins=bins)
+    ln = PD.length_device(dp, sk, bins.alpha_dev, su_seq, seq_mass)
+    names = [None] + [MASS_NAMES[m.mass][0] for m in dp.masses[1:]]
+    for g in (7, 30, 0, 41):
+        want = _mirror_outcome(obs[offsets[g]:offsets[g + 1]], su_seq[g], seq_mass[g], max_len[g], engine)
+        assert (sk.status[2 * g:2 * g + 2] == _native.WALK_DONE).all(), (g, sk.status[2 * g:2 * g + 2])
+        got = PD.skeleton_frames(dp, rows, sk, g)
+        for side in ("START", "END"):
+            assert got[side] == want[side], (g, side)
+        kept = pipeline.mask_rows(ln.alpha[g:g + 1], len(dp.masses))[0]
+        assert [0] + [dp.masses[r].mass for r in range(1, len(dp.masses)) if kept[r]] == want["masses"], g
+        if want["seq_len"] is None:
+            assert int(ln.status[g]) == _native.JAC_NO_LENGTH, g
+        elif want["seq_len"] == "IndexError":
+            assert int(ln.status[g]) == _native.JAC_INDEX, g
+        else:
+            assert int(ln.status[g]) == _native.JAC_OK and int(ln.seq_len[g]) == want["seq_len"], g
+            L = int(ln.seq_len[g])
+            comb = ln.comb[int(ln.comb_off[g]):int(ln.comb_off[g]) + L].cpu().numpy().view(np.uint64)
+            got_c = [sorted(names[r] for r in range(1, len(names)) if (int(c_[r >> 6]) >> (r & 63)) & 1)
+                     for c_ in comb]
+            assert got_c == want["combined"], g
+
+
 def test_device_fixpoint_rounds_vs_oracle_rebuilt_tables(engine):
     """Every filter_by_explanation round of the device fixpoint (k_fix_round:
     the round's window / singleton answers on the spectrum's alphabet, the
