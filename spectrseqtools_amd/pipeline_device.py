@@ -585,13 +585,15 @@ class DeviceSkeleton:
 
 @_one_stream
 def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, tolerance=None, caps=(64, 32),
-                    big_caps=(8192, 8192)):
+                    big_caps=(8192, 8192), max_rounds=4096):
     """Stage 4 on the device: SkeletonBuilder._predict_skeleton for the START
     and END rows of every spectrum (the rows the fixpoint kept, its final
     alphabets `alpha` [S, 2] u64), with filter_by_explanation's final dict.
     `bins`: stage 3's bins_device(..., max_len=max_len) result (computed here
     when None).  caps = (explanations per bin, candidates per query) of the
-    lanes' scratch; sides that outgrow them are walked again with big_caps."""
+    lanes' scratch; sides that outgrow them are walked again with big_caps.
+    max_rounds bounds the re-query rounds (each answers every suspended side's
+    next re-query bin)."""
     import torch
 
     tolerance = dp_table.tolerance if tolerance is None else tolerance
@@ -658,7 +660,17 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
     a.min_end, a.max_end, a.kept = min_end.data_ptr(), max_end.data_ptr(), kept.data_ptr()
     a.side_status, a.n_suspended, a.n_big = status.data_ptr(), ctl.data_ptr(), ctl.data_ptr() + 4
     a.pos_cap, a.len_cap = pos_cap, len_cap
-    rounds = []  # per re-query round: (block, ptr, n, st) tensors
+    # every re-query answer so far, merged per side in round order (block =
+    # start << 32 | count per side, then ptr / n / st): the lanes see one
+    # round, so the number of re-query rounds is not bounded by the ABI's
+    # SST_WALK_MAX_ROUNDS (exact-mode spectra re-query every bin whose
+    # predecessor had no explanations through the host)
+    merged = None
+    m_sid = torch.zeros(0, dtype=torch.int64, device=dev)
+    m_ptr = torch.zeros(0, dtype=torch.int64, device=dev)
+    m_n = torch.zeros(0, dtype=torch.int32, device=dev)
+    m_st = torch.zeros(0, dtype=torch.int8, device=dev)
+    n_rounds = 0
     keep_alive = []
     mode = {}  # side -> big
     run = np.arange(2 * S, dtype=np.int32)
@@ -669,10 +681,9 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
     while len(run) or len(big):
         req_block = torch.zeros(max(1, 2 * S), dtype=torch.int64, device=dev)
         a.req_block = req_block.data_ptr()
-        a.n_rounds = len(rounds)
-        for r, (blk, p_, n_, s_) in enumerate(rounds):
-            a.rq_block[r], a.rq_ptr[r], a.rq_n[r], a.rq_st[r] = (blk.data_ptr(), p_.data_ptr(), n_.data_ptr(),
-                                                                  s_.data_ptr())
+        a.n_rounds = 0 if merged is None else 1
+        if merged is not None:
+            a.rq_block[0], a.rq_ptr[0], a.rq_n[0], a.rq_st[0] = (t.data_ptr() for t in merged)
         ctl.zero_()
         for sides, (e_cap, c_cap) in ((run, caps), (big, big_caps)):
             if not len(sides):
@@ -701,8 +712,8 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
         run = susp[~was_big[susp]]
         big = np.concatenate([susp[was_big[susp]], new_big]).astype(np.int32)
         if n_req:
-            if len(rounds) >= _native.WALK_MAX_ROUNDS:
-                break
+            if n_rounds >= max_rounds:
+                break  # the sides still suspended keep SST_WALK_SUSPENDED
             if n_req > req_cap:
                 raise _native.EngineError("skeleton walk: re-query list overflow")
             p_ = torch.zeros(n_req, dtype=torch.int64, device=dev)
@@ -712,7 +723,26 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
             res = _masked_explain_refs(dp_table, alpha_dev, req_mass, req_thr, req_spec, n_req, max_len, dst, p_, n_,
                                        s_)
             results.extend(res)
-            rounds.append((req_block, p_, n_, s_))
+            # this round's entries per side (each side's block is contiguous, in
+            # its lane's order), appended after the earlier rounds' and ordered
+            # by side with a stable sort: per side, round-major
+            blk = req_block[:2 * S]
+            cnt_s = (blk & 0xFFFFFFFF)
+            sides_nz = torch.nonzero(cnt_s).flatten()
+            c_nz = cnt_s[sides_nz]
+            first = torch.cumsum(c_nz, 0) - c_nz
+            idx = torch.repeat_interleave(blk[sides_nz] >> 32, c_nz) + (
+                torch.arange(int(c_nz.sum().item()), device=dev) - torch.repeat_interleave(first, c_nz))
+            m_sid = torch.cat([m_sid, torch.repeat_interleave(sides_nz, c_nz)])
+            m_ptr = torch.cat([m_ptr, p_[idx]])
+            m_n = torch.cat([m_n, n_[idx]])
+            m_st = torch.cat([m_st, s_[idx]])
+            order = torch.sort(m_sid, stable=True).indices
+            m_sid, m_ptr, m_n, m_st = m_sid[order], m_ptr[order], m_n[order], m_st[order]
+            per = torch.bincount(m_sid, minlength=2 * S)
+            start = torch.cumsum(per, 0) - per
+            merged = ((start << 32) | per, m_ptr, m_n, m_st)
+            n_rounds += 1
             n_req_total += n_req
     return DeviceSkeleton(max_len, skel_off, skel, min_end, max_end, kept, status.cpu().numpy()[:2 * S], launches,
                           n_req_total, int(dct.n.sum().item()), results)

@@ -341,7 +341,9 @@ def test_device_pipeline_big_spectra(engine):
     from spectrseqtools_amd.synthetic import make_spectra
 
     small = make_spectra(40, seed=59, len_range=(6, 14))
-    big = make_spectra(2, seed=61, len_range=(60, 60), noise_frac=7.5)
+    # 20-nt sequences with ~2 900 noise peaks each (most of them valid below
+    # the sequence mass: > 2 048 rows)
+    big = make_spectra(2, seed=61, len_range=(20, 20), noise_frac=24.0)
     parts, seq_mass = [], []
     for i in range(42):  # the big spectra at positions 7 and 30
         src, g = (big, 0) if i == 7 else (big, 1) if i == 30 else (small, i - (i > 7) - (i > 30))
