@@ -98,6 +98,11 @@ class DynamicProgrammingTable:
                                                            engine=self._engine))
 
     # -- device table ---------------------------------------------------------
+    def close(self):
+        """Free the device table now (HBM is not Python memory: a table held
+        by a reference cycle would otherwise wait for a full GC pass)."""
+        self._set_device(None)
+
     def _set_device(self, dev):
         if self._device is not None:
             self._device.close()

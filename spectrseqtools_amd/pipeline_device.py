@@ -13,6 +13,8 @@ SU order of its classify_fragments frame, so a row's slot offset is the
 the device memory only; every computation is the library's.
 """
 import ctypes
+import os
+import sys
 from dataclasses import dataclass
 
 import numpy as np
@@ -21,6 +23,7 @@ from . import _native
 from .masses import PHOSPHATE_LINK_MASS
 from .pipeline import mask_rows, row_masks
 
+_PROGRESS = os.environ.get("SST_PIPE_PROGRESS") == "1"  # per-launch lines of the long stages on stderr
 ERR_BITS = {1: "a spectrum has more than 4096 peaks", 2: "a spectrum has more rows than the reserved slices hold",
             4: "a window outside the pair class", 8: "is_valid_mass raised (a window past a table's end)",
             16: "an explanation dict too large for the LDS hash", 32: "rows out of mass order"}
@@ -701,6 +704,9 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
         eng.synchronize()
         keep_alive.clear()
         n_susp, n_big, n_req = (int(x) for x in ctl.cpu().tolist())
+        if _PROGRESS:
+            print(f"[skeleton walk] launch {launches}: {n_susp} suspended, {n_big} big, {n_req} re-queries",
+                  file=sys.stderr, flush=True)
         st_h = status.cpu().numpy()
         was_big = np.zeros(2 * S, bool)
         was_big[big] = True
@@ -794,10 +800,12 @@ class DeviceLength:
     comb_off: np.ndarray  # [S + 1]
     comb: object          # torch int64 [total, 2] the combined skeleton (masks)
     reach_batches: int
+    distinct_alphabets: int = 0  # skeleton alphabets (each one's row bitsets built once)
 
 
 @_one_stream
-def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=8 << 30):
+def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=8 << 30,
+                  share_alphabets=True):
     """Stage 5: each spectrum's skeleton alphabet (the canonical rows and the
     modifications its START / END skeletons name), both length bounds on it
     (sst_reach_rows_device + sst_length_bounds_reach_device: the reduced
@@ -827,32 +835,52 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     from .pipeline import mask_rows
 
     n_rows = len(dp_table.masses)
-    K = mask_rows(alpha_sk, n_rows)[:, 1:].sum(axis=1).astype(np.int64)
-    need = 4 * K * words
+    # spectra with one skeleton alphabet share its rows' bitsets (built up to
+    # the heaviest of their windows): few distinct alphabets among many spectra
+    if share_alphabets:
+        uniq, inv = np.unique(alpha_sk, axis=0, return_inverse=True)
+        inv = inv.reshape(-1)
+    else:
+        uniq, inv = alpha_sk, np.arange(S)
+    U = len(uniq)
+    words_u = np.zeros(U, np.int64)
+    np.maximum.at(words_u, inv, words)
+    K_u = mask_rows(uniq, n_rows)[:, 1:].sum(axis=1).astype(np.int64)
+    need_u = 4 * K_u * words_u
     lower = np.zeros(S, np.int64)
     upper = np.zeros(S, np.int64)
     lb_st = np.zeros(S, np.int8)
     masses = dp_table.masses
     is_mod = [m.is_modification for m in masses]
+    by_u = np.argsort(inv, kind="stable")  # spectra grouped by alphabet
+    u_first = np.concatenate([[0], np.cumsum(np.bincount(inv, minlength=U))])
     n_batches = 0
-    g0 = 0
-    while g0 < S:
-        g1, tot = g0, 0
-        while g1 < S and (g1 == g0 or tot + need[g1] <= reach_budget_bytes):
-            tot += int(need[g1])
-            g1 += 1
-        n = g1 - g0
-        off = np.concatenate([[0], np.cumsum(need[g0:g1] // 4)[:-1]]).astype(np.int64)
+    u0 = 0
+    while u0 < U:
+        u1, tot = u0, 0
+        while u1 < U and (u1 == u0 or tot + need_u[u1] <= reach_budget_bytes):
+            tot += int(need_u[u1])
+            u1 += 1
+        nu = u1 - u0
+        off_u = np.concatenate([[0], np.cumsum(need_u[u0:u1] // 4)[:-1]]).astype(np.int64)
         bits = torch.empty(max(1, int(tot // 4)), dtype=torch.int32, device=dev)
-        al_t = torch.as_tensor(alpha_sk[g0:g1].view(np.int64), device=dev).contiguous()
-        w_t = torch.as_tensor(words[g0:g1], device=dev)
-        o_t = torch.as_tensor(off, device=dev)
-        eng.check(L.sst_reach_rows_device(h, al_t.data_ptr(), w_t.data_ptr(), o_t.data_ptr(), n, bits.data_ptr()),
+        # (every device array stays referenced until the batch is done: a
+        # temporary's block can be handed to the next allocation at once)
+        alu_t = torch.as_tensor(uniq[u0:u1].view(np.int64), device=dev).contiguous()
+        wu_t = torch.as_tensor(words_u[u0:u1], device=dev)
+        ou_t = torch.as_tensor(off_u, device=dev)
+        eng.check(L.sst_reach_rows_device(h, alu_t.data_ptr(), wu_t.data_ptr(), ou_t.data_ptr(), nu, bits.data_ptr()),
                   "sst_reach_rows_device")
-        order = np.argsort(ml[g0:g1], kind="stable")
-        ml_s = ml[g0:g1][order]
-        su_t = torch.as_tensor(su[g0:g1][order], device=dev)
-        ob_t = torch.as_tensor(ob[g0:g1][order], device=dev)
+        members = by_u[u_first[u0]:u_first[u1]]  # this batch's spectra
+        n = len(members)
+        lu = inv[members] - u0  # their alphabets within the batch
+        al_t = torch.as_tensor(uniq[u0:u1][lu].view(np.int64), device=dev).contiguous()
+        w_t = torch.as_tensor(words_u[u0:u1][lu], device=dev)
+        o_t = torch.as_tensor(off_u[lu], device=dev)
+        order = np.argsort(ml[members], kind="stable")
+        ml_s = ml[members][order]
+        su_t = torch.as_tensor(su[members][order], device=dev)
+        ob_t = torch.as_tensor(ob[members][order], device=dev)
         sp_t = torch.as_tensor(order.astype(np.int32), device=dev)
         lo_t = torch.zeros(n, dtype=torch.int64, device=dev)
         up_t = torch.zeros(n, dtype=torch.int64, device=dev)
@@ -867,13 +895,13 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
                 bits.data_ptr(), o_t.data_ptr(), w_t.data_ptr(), s1 - s0, float(tol), float(prec), Lm, A,
                 lo_t.data_ptr() + 8 * s0, up_t.data_ptr() + 8 * s0, st_t.data_ptr() + s0),
                 "sst_length_bounds_reach_device")
-        idx = g0 + order
+        idx = members[order]
         lower[idx] = lo_t.cpu().numpy()
         upper[idx] = up_t.cpu().numpy()
         lb_st[idx] = st_t.cpu().numpy()
         del bits
         n_batches += 1
-        g0 = g1
+        u0 = u1
     # Jaccard + combine
     comb_off = np.concatenate([[0], np.cumsum(ml)]).astype(np.int64)
     comb = torch.zeros((max(1, int(comb_off[-1])), 2), dtype=torch.int64, device=dev)
@@ -893,7 +921,7 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     eng.check(L.sst_jaccard_device(h, ctypes.byref(ja)), "sst_jaccard_device")
     eng.synchronize()
     return DeviceLength(alpha_sk, lower, upper, lb_st, seq_len.cpu().numpy()[:S], jst.cpu().numpy()[:S], comb_off,
-                        comb, n_batches)
+                        comb, n_batches, U)
 
 
 # ---------------------------------------------------------------------------

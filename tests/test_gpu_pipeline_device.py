@@ -214,17 +214,27 @@ def _mirror_outcome(obs, su_seq, obs_seq, max_len, engine, mod_rate=0.5):
     spectra): classify_fragments, Predictor.filter_by_explanation,
     SkeletonBuilder._predict_skeleton per side and
     select_sequence_length_with_jaccard with combine_skeleton_sequences."""
-    from spectrseqtools_amd.fragment_classification import classify_fragments
-    from spectrseqtools_amd.frame import Frame
     from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
-    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict
-    from spectrseqtools_amd.prediction import Predictor
-    from spectrseqtools_amd.skeleton_building import SkeletonBuilder, combine_skeleton_sequences
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
 
     seq = SequenceInformation(max_len=int(max_len), su_mass=float(su_seq), obs_mass=float(obs_seq),
                               modification_rate=mod_rate)
     dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
                                  precision=TOLERANCE, seq=seq, engine=engine)
+    try:
+        return _mirror_run(dp, obs)
+    finally:
+        dp.close()  # a table per spectrum: free its HBM now, not at the next full GC pass
+
+
+def _mirror_run(dp, obs):
+    from spectrseqtools_amd import _native
+    from spectrseqtools_amd.fragment_classification import classify_fragments
+    from spectrseqtools_amd.frame import Frame
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, build_breakage_dict
+    from spectrseqtools_amd.prediction import Predictor
+    from spectrseqtools_amd.skeleton_building import SkeletonBuilder, combine_skeleton_sequences
+
     bd = build_breakage_dict(555.1294, 455.1491)
     fr = classify_fragments(Frame({"observed_mass": list(map(float, obs))}), dp, bd)
     f = C.prepared(fr)
@@ -244,6 +254,8 @@ def _mirror_outcome(obs, su_seq, obs_seq, max_len, engine, mod_rate=0.5):
         out["combined"] = [sorted(p) for p in combine_skeleton_sequences(seq_len, sks["START"], sks["END"][::-1])]
     except IndexError:
         out["seq_len"], out["combined"] = "IndexError", None
+    except _native.EngineError:
+        raise  # the engine failing (out of HBM, say) is not the reference's "no length" exception
     except Exception:  # noqa: BLE001 -- the reference raises a bare Exception when no length fits
         out["seq_len"], out["combined"] = None, None
     out["masses"] = [m.mass for m in dp.masses]

@@ -11,8 +11,8 @@ step() {  # step NAME TIMEOUT CMD...
   echo "[$name] rc=$rc"; tail -2 "gpurun_out/${TAG}_${name}.log" | cut -c1-800
   if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-step pipe 600 python -u tools/pipeline_bench.py --spectra $N
-step stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_stats -o trace -- python3 tools/pipeline_bench.py --spectra $N
+SST_PIPE_PROGRESS=1 step pipe 600 python -u tools/pipeline_bench.py --spectra $N
+SST_PIPE_PROGRESS=1 step stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_stats -o trace -- python3 tools/pipeline_bench.py --spectra $N
 find gpurun_out/${TAG}_stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_kernel_stats.csv \;
 [ "$PMC" = "0" ] && exit 0
 i=0

@@ -127,6 +127,10 @@ def main():
     def kernels():
         return {_native.KERNEL_NAMES.get(k, str(k)): v for k, v in engine.profile_read().items()}
 
+    def progress(*names):  # one line per finished stage on stderr (a long run shows it is alive)
+        if rank == 0:
+            print(" ".join(f"[{n}] {stages[n]['s']:.3f}s" for n in names), file=sys.stderr, flush=True)
+
     def busy(st):  # GPU-busy share of a stage: event-timed kernel time over its wall time
         st["gpu_busy_frac"] = sum(v[0] for v in st["kernels"].values()) / 1e3 / st["s"]
 
@@ -150,6 +154,8 @@ def main():
         kw = pd.skeleton_device(dp, rw, fw.alpha, m0, bins=bw)
         pd.length_device(dp, kw, bw.alpha_dev, su_seq[:S0], batch.seq_mass[:S0])
     engine.synchronize()
+    if rank == 0:
+        print(f"[warm-up] {S0} spectra done", file=sys.stderr, flush=True)
 
     stages = {}
     engine.profile(True)
@@ -212,6 +218,7 @@ def main():
 
     busy(stages["classify"])
     busy(stages["fixpoint"])
+    progress("classify", "fixpoint")
 
     barrier()
     t0 = time.perf_counter()
@@ -241,6 +248,7 @@ def main():
         stages["bins"]["masked_explain_groups"] = [list(x) for x in db.deferred["groups"]]
     stages["bins"]["kernels"] = kernels()
     busy(stages["bins"])
+    progress("bins")
     outcome = None
     if rows is not None:  # stages 4-5 (device-resident path)
         barrier()
@@ -252,11 +260,13 @@ def main():
                               "walk_status": wst, "walk_launches": sk.launches, "requery_windows": sk.requeries,
                               "dict_entries": sk.dict_entries, "kernels": kernels()}
         busy(stages["skeleton"])
+        progress("skeleton")
         barrier()
         t0 = time.perf_counter()
         ln = pd.length_device(dp, sk, db.alpha_dev, su_seq, batch.seq_mass)
         barrier()
         stages["length"] = {"s": tmax(time.perf_counter() - t0), "reach_batches": ln.reach_batches,
+                            "distinct_skeleton_alphabets": ln.distinct_alphabets,
                             "jaccard_status": {int(k): int(v) for k, v in zip(*np.unique(ln.status,
                                                                                          return_counts=True))},
                             "lb_status": {int(k): int(v) for k, v in zip(*np.unique(ln.lb_status,
@@ -264,6 +274,7 @@ def main():
                             "mean_seq_len": float(ln.seq_len[ln.status == 0].mean()) if (ln.status == 0).any() else 0,
                             "kernels": kernels()}
         busy(stages["length"])
+        progress("length")
         barrier()
         t0 = time.perf_counter()
         buf = pd.pack_outcomes(rows, fx, sk, ln)
