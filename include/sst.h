@@ -724,13 +724,22 @@ int sst_skeleton_alpha_device(sst_table* t, int64_t n_spec, const int32_t* d_max
  * d_status[i] 0 ok, SST_OUT_OF_TABLE (the reference raises), SST_ABORTED (a
  * window in the reduced table's masked last word, or a guard), -5 an empty
  * window.  Budgets: max_len, max_mods and the table's caps
- * (sst_table_set_budgets) as in sst_length_bound_batch.  Device pointers. */
+ * (sst_table_set_budgets) as in sst_length_bound_batch -- or, with d_qlen
+ * non-NULL, per query: max_len d_qlen[i], caps d_caps_len[d_qlen[i] *
+ * SST_MAX_ROWS + r] and max_mods d_a0_len[d_qlen[i]] (the caller's
+ * round(L * rate)), so spectra of every max_len share one launch (the
+ * table's is_modification flags still come from sst_table_set_budgets).
+ * d_nodes (may be NULL; zeroed by the caller): per query, the replay's
+ * visited nodes summed over its attempts.  Device pointers. */
+#define SST_MAX_ROWS 120
 int sst_reach_rows_device(sst_table* t, const uint64_t* d_alpha, const int64_t* d_words, const uint64_t* d_off,
                           int64_t n_spec, uint32_t* d_bits);
 int sst_length_bounds_reach_device(sst_table* t, const double* d_su, const double* d_obs, const int32_t* d_spec,
                                    const uint64_t* d_alpha, const uint32_t* d_reach_bits, const uint64_t* d_reach_off,
                                    const int64_t* d_reach_words, int64_t n, double tol, double prec, int max_len,
-                                   int64_t max_mods, int64_t* d_lower, int64_t* d_upper, int8_t* d_status);
+                                   int64_t max_mods, int64_t* d_lower, int64_t* d_upper, int8_t* d_status,
+                                   const int32_t* d_qlen, const int32_t* d_caps_len, const int32_t* d_a0_len,
+                                   uint64_t* d_nodes);
 
 /* ---- CPython set order (the skeleton walk's emulation, sst_pyset.h) ---- */
 /* hash(tuple) of a tuple whose items hash to item_hashes[0..n) (CPython

@@ -45,6 +45,8 @@ constexpr int64_t kChunkBits = kChunkWords * 32;  // 262144 masses
 constexpr int kRing = 4;                          // chunks kept in LDS (128 KB)
 constexpr int kRingMask = kRing * kChunkWords - 1;
 constexpr int kValidWG = 1024;
+constexpr int kValidWaves = kValidWG / 64;
+constexpr int kPasses = (kChunkWords + 63 * kValidWaves - 1) / (63 * kValidWaves);  // 9: a wave's passes per chunk
 
 __device__ __forceinline__ bool row_in(uint64_t m0, uint64_t m1, int r) {
   return r < 64 ? ((m0 >> r) & 1ull) : ((m1 >> (r - 64)) & 1ull);
@@ -170,22 +172,44 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   top = s_top < limit - 1 ? s_top : limit - 1;
   const int64_t n_chunks = top / kChunkBits + 1;
   const bool guard_ok = wmin >= kChunkBits && wmax < 3 * kChunkBits;  // the ring's dependency window
+  // Each wave writes 63 consecutive words per pass: a row's shifted word
+  // for output word o needs ring words wi and wi + 1, and wi + 1 is the next
+  // lane's wi (a DPP lane shift), so the 64 lanes read 64 words and the
+  // last lane only supplies its neighbour.  The shift is wave-uniform.
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // the canonical closure's words of a chunk, per lane and pass, loaded a
+  // chunk ahead: one L2 latency per chunk, hidden behind the chunk before
+  // (read pass by pass they cost one exposed latency per pass)
+  uint32_t cwv[kPasses];
+  auto load_canon = [&](int64_t jj, uint32_t* dst) {
+#pragma unroll
+    for (int p = 0; p < kPasses; ++p) {
+      const int o = 63 * wv + p * 63 * kValidWaves + lane;
+      const int64_t cw = jj * kChunkWords + o;
+      dst[p] = use_c && o < kChunkWords && cw < a.canon_words ? a.canon_closure[cw] : 0u;
+    }
+  };
+  load_canon(0, cwv);
   for (int64_t j = 0; j < n_chunks && guard_ok; ++j) {
     uint32_t* cur = ring + (j & (kRing - 1)) * kChunkWords;
     const int64_t base = j * kChunkBits;
     int zmax = -1;  // this lane's highest unreachable mass in the chunk
-    // Each wave writes 63 consecutive words per pass: a row's shifted word
-    // for output word o needs ring words wi and wi + 1, and wi + 1 is the next
-    // lane's wi (a DPP lane shift), so the 64 lanes read 64 words and the
-    // last lane only supplies its neighbour.  The shift is wave-uniform.
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, n_wv = blockDim.x >> 6;
-    for (int o0 = 63 * wv; o0 < kChunkWords; o0 += 63 * n_wv) {
+    uint32_t nxt[kPasses];
+    if (j + 1 < n_chunks && !s_full) {
+      load_canon(j + 1, nxt);
+    } else {
+#pragma unroll
+      for (int p = 0; p < kPasses; ++p) nxt[p] = 0u;
+    }
+#pragma unroll
+    for (int p = 0; p < kPasses; ++p) {
+      const int o0 = 63 * wv + p * 63 * kValidWaves;
+      if (o0 >= kChunkWords) break;
       const int o = o0 + lane;
       uint32_t v = 0;
       if (!s_full) {
         if (use_c) {  // includes mass 0; masses past the full table (>= every reduced table's end): none
-          const int64_t cw = j * kChunkWords + o;
-          v = o < kChunkWords && cw < a.canon_words ? a.canon_closure[cw] : 0u;
+          v = cwv[p];
         } else if (j == 0 && o == 0) {
           v = 1u;  // mass 0: the empty multiset (table[0, 0] seed)
         }
@@ -222,7 +246,13 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
         if (v != ~0u) zmax = 32 * o + 31 - __builtin_clz(~v);  // o ascends: the lane's last one is its highest
       }
     }
-    if (zmax >= 0) atomicMax(&s_zmax, zmax);
+#pragma unroll
+    for (int p = 0; p < kPasses; ++p) cwv[p] = nxt[p];
+    for (int off = 32; off > 0; off >>= 1) {  // the wave's highest, then one atomic per wave
+      const int z2 = __shfl_xor(zmax, off, 64);
+      zmax = zmax > z2 ? zmax : z2;
+    }
+    if (lane == 0 && zmax >= 0) atomicMax(&s_zmax, zmax);
     __syncthreads();
     if (threadIdx.x == 0) {
       // a run of >= w_min reachable masses [x, x + w_min): every m beyond is

@@ -2903,13 +2903,19 @@ extern "C" int sst_reach_rows_device(sst_table* t, const uint64_t* d_alpha, cons
   return SST_OK;
 }
 
+// replay waves in flight for the reach-mode bounds (16 per CU: the DFS is
+// latency-bound, one query per wave; memo 2^16 entries each on the first try)
+constexpr uint32_t kReachUnits = 4096;
+constexpr size_t kReachMemoBytes = 48ull << 30;  // the replay's memo workspace per launch (HBM: 288 GB)
+
 extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, const double* d_obs,
                                               const int32_t* d_spec, const uint64_t* d_alpha,
                                               const uint32_t* d_reach_bits, const uint64_t* d_reach_off,
                                               const int64_t* d_reach_words, int64_t n, double tol, double prec,
                                               int max_len, int64_t max_mods, int64_t* d_lower, int64_t* d_upper,
-                                              int8_t* d_status) {
-  if (!t || n < 0 || n > INT32_MAX || max_len < 0 || max_len > 120 ||
+                                              int8_t* d_status, const int32_t* d_qlen, const int32_t* d_caps_len,
+                                              const int32_t* d_a0_len, uint64_t* d_nodes) {
+  if (!t || n < 0 || n > INT32_MAX || max_len < 0 || max_len > 120 || (d_qlen && (!d_caps_len || !d_a0_len)) ||
       (n > 0 && (!d_su || !d_obs || !d_spec || !d_alpha || !d_reach_bits || !d_reach_off || !d_reach_words ||
                  !d_lower || !d_upper || !d_status)))
     return SST_E_ARG;
@@ -2944,6 +2950,10 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   q.reach_words = d_reach_words;
   q.both = 1;
   q.out_hi = d_upper;
+  q.qlen = d_qlen;
+  q.caps_len = d_caps_len;
+  q.a0_len = d_a0_len;
+  q.nodes_out = d_nodes;
   uint32_t n_exact = 0;
   {
     Prof p(c, SST_K_LENGTH_BOUND);  // windows, extents; every live query is listed for the replay
@@ -2952,8 +2962,16 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   HIP_OK(c, hipMemcpyAsync(&n_exact, d_cnt.p, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   std::vector<int8_t> st(nn);
-  int units = (int)std::min<uint32_t>(1024, std::max<uint32_t>(1, n_exact));
-  uint32_t cap = memo_cap0(units, kLBHashCap0);
+  // memo per wave: 2^16 masses on the first try (most spectra), 8x per retry
+  // for the queries that ran out; the waves in flight are what the
+  // workspace budget allows at that size (a retry keeps its parallelism)
+  const size_t per_entry = hash_entry_bytes() + kMaxRows;
+  uint32_t cap = kLBHashCap0;
+  auto units_for = [&](uint32_t n_q) {
+    const size_t by_mem = kReachMemoBytes / ((size_t)cap * per_entry);
+    return (int)std::max<size_t>(1, std::min<size_t>({(size_t)kReachUnits, (size_t)std::max<uint32_t>(1, n_q), by_mem}));
+  };
+  int units = units_for(n_exact);
   while (n_exact) {
     DevBuf hash, vals, frames;
     if (!hash.ensure((size_t)units * cap * hash_entry_bytes()) || !vals.ensure((size_t)units * cap * kMaxRows) ||
@@ -2972,10 +2990,10 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
     for (size_t i = 0; i < nn; ++i)
       if (st[i] == kStatusExactRetry) retry.push_back((uint32_t)i);
     if (retry.empty()) break;
-    if ((size_t)std::max(1, units / 8) * cap * 8 * (hash_entry_bytes() + kMaxRows) > kMaxMemoBytes)
+    if ((size_t)cap * 8 * per_entry > kReachMemoBytes)
       return fail(c, SST_E_NOMEM, "length bound: memo would exceed the workspace limit");
     cap *= 8;
-    units = std::max(1, std::min<int>(units / 8, (int)retry.size()));
+    units = units_for((uint32_t)retry.size());
     n_exact = (uint32_t)retry.size();
     HIP_OK(c, hipMemcpyAsync(d_list.p, retry.data(), retry.size() * 4, hipMemcpyHostToDevice, c->stream));
     HIP_OK(c, hipMemcpyAsync(d_cnt.p, &n_exact, 4, hipMemcpyHostToDevice, c->stream));

@@ -9,6 +9,7 @@
 namespace sst {
 
 constexpr int kMaxRows = 120;      // rows 0..119; index record keeps lo in bits 56..63
+static_assert(kMaxRows == SST_MAX_ROWS, "the ABI's row stride");
 constexpr int kWG = 256;           // workgroup of the lane-per-query kernels (4 waves)
 #ifndef SST_DEF_WG
 #define SST_DEF_WG 256
@@ -269,6 +270,13 @@ struct LBArgs {
   const int64_t* reach_words = nullptr;
   int both = 0;
   int64_t* out_hi = nullptr;
+  // per-query max_len (wave mode; null: max_len, A0 and the table's caps for
+  // every query): query i's caps caps_len[qlen[i] * kMaxRows + r] and
+  // max_modifications a0_len[qlen[i]] (the host's round(L * rate))
+  const int32_t* qlen = nullptr;
+  const int32_t* caps_len = nullptr;
+  const int32_t* a0_len = nullptr;
+  uint64_t* nodes_out = nullptr;  // may be null: per query, phase-1 nodes visited (summed over attempts)
 };
 
 // per-row reachability of reduced alphabets (sst_reach.hip): spectrum g's

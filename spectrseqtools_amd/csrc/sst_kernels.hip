@@ -385,12 +385,17 @@ struct Lds {
   int w[kMaxRows];
   int cap[kMaxRows];
   uint8_t mod[kMaxRows];
+  uint64_t capz0, capz1;  // rows with cap <= 0 (the table's, or the current query's)
 };
 __device__ __forceinline__ void stage_rows(Lds& s, const TableArgs& t) {
   for (int r = threadIdx.x; r < t.n_rows; r += blockDim.x) {
     s.w[r] = t.w[r];
     s.cap[r] = t.cap[r];
     s.mod[r] = t.mod[r];
+  }
+  if (threadIdx.x == 0) {
+    s.capz0 = t.capz0;
+    s.capz1 = t.capz1;
   }
   __syncthreads();
 }
@@ -606,6 +611,7 @@ struct Hash {
   uint32_t last_meta = 0;  // meta written by the last first visit (p1_visit)
   bool reach = false;      // wave mode only: node records from rv, not the full table's index
   ReachView rv{};
+  M128 last_L{0, 0};       // reach mode: the left bits of the last first visit's record (p1_classify)
   __device__ __forceinline__ uint32_t slot(uint32_t m) const { return (m * 0x9E3779B1u) & mask; }
   // returns entry pointer or nullptr if absent
   __device__ __forceinline__ HEntry* find(uint32_t m) const {
@@ -990,7 +996,7 @@ __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& 
   M128 en = mand(rec_L(rec), rng);
   if (t.any_mod) {
     M128 blocked;
-    if (A > 0) blocked = M128{t.mod0 & t.capz0, t.mod1 & t.capz1};
+    if (A > 0) blocked = M128{t.mod0 & s.capz0, t.mod1 & s.capz1};
     else blocked = M128{t.mod0, t.mod1};
     en.a &= ~blocked.a;
     en.b &= ~blocked.b;
@@ -1009,6 +1015,7 @@ __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& 
   e->en1 = en_old1 | en.b;
   e->meta = (meta & 0xFF00u) | ((uint32_t)lo << 16) | (uint32_t)r;
   h.last_meta = e->meta;
+  if (WAVE && h.reach) h.last_L = rec_L(rec);
   // the frame will visit (m - w_rr, rr) for every enabled row: issue their
   // index-record and first-probe loads now, independently, so the visits
   // that follow hit the cache instead of paying dependent HBM round trips
@@ -1140,7 +1147,7 @@ __device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, co
       const int64_t c = (int64_t)m - s.w[r];
       bool reach_c;
       if (c <= 0) reach_c = false;
-      else if (h.reach) reach_c = reach_bit(h.rv, half ? h.rv.rank1 : h.rv.rank0, c);  // c in R_r (r kept)
+      else if (h.reach) reach_c = mtest(h.last_L, r);  // c in R_r (r kept): the frame's record says so
       else reach_c = r >= rec_lo(ld_index(t.index, c));
       if (c == 0) {
         nrow = nrow < r ? nrow : r;
@@ -2874,10 +2881,13 @@ __device__ __forceinline__ bool lb_window(const LBArgs& q, int64_t i, int64_t& l
   return lo <= hi;
 }
 
-__device__ __forceinline__ int64_t lb_finish(const LBArgs& q, int best, int dir) {
+__device__ __forceinline__ int64_t lb_finish_len(int best, int dir, int max_len) {
   // mass_table.py:476-484: the default bound becomes 1 (lower) / max_len (upper)
-  if (dir == 0) return best >= q.max_len + 1 ? 1 : best;
-  return best == -1 ? q.max_len : best;
+  if (dir == 0) return best >= max_len + 1 ? 1 : best;
+  return best == -1 ? max_len : best;
+}
+__device__ __forceinline__ int64_t lb_finish(const LBArgs& q, int best, int dir) {
+  return lb_finish_len(best, dir, q.max_len);
 }
 __device__ __forceinline__ int64_t lb_finish(const LBArgs& q, int best) { return lb_finish(q, best, q.dir); }
 
@@ -2956,6 +2966,28 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
     const int64_t i = q.exact_list[j];
     int64_t lo, hi;
     lb_window(q, i, lo, hi);
+    int A0 = q.A0, max_len = q.max_len;
+    if (WAVE && q.qlen) {  // this query's budgets by its max_len (the block is one wave)
+      const int L = q.qlen[i];
+      const int lane = threadIdx.x & 63;
+      bool z0 = false, z1 = false;
+      if (lane < t.n_rows) {
+        s.cap[lane] = q.caps_len[(int64_t)L * kMaxRows + lane];
+        z0 = s.cap[lane] <= 0;
+      }
+      if (lane + 64 < t.n_rows) {
+        s.cap[lane + 64] = q.caps_len[(int64_t)L * kMaxRows + lane + 64];
+        z1 = s.cap[lane + 64] <= 0;
+      }
+      const uint64_t c0 = __ballot(z0), c1 = __ballot(z1);
+      if (lane == 0) {
+        s.capz0 = c0;
+        s.capz1 = c1;
+      }
+      __syncthreads();
+      A0 = q.a0_len[L];
+      max_len = L;
+    }
     h.epoch = ++epoch;  // the workspace was zeroed: epochs 1, 2, ... are fresh
     h.used = 0;
     uint64_t nodes = 0;
@@ -2989,7 +3021,8 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
         __syncthreads();
       }
     }
-    int rc = phase1<WAVE>(t, s, h, fr, a, hi, q.A0, q.node_budget, nodes, am);
+    int rc = phase1<WAVE>(t, s, h, fr, a, hi, A0, q.node_budget, nodes, am);
+    if (q.nodes_out && (!WAVE || threadIdx.x == 0)) q.nodes_out[i] += nodes;
     if (rc == -1) {
       q.status[i] = (int8_t)kStatusExactRetry;
       continue;
@@ -3005,7 +3038,7 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
     for (int di = 0; di < n_dir && rc == 0; ++di) {
       const int dir = q.both ? di : q.dir;
       const uint32_t pass = (uint32_t)di + 1;
-      const int dflt = dir ? -1 : q.max_len + 1;
+      const int dflt = dir ? -1 : max_len + 1;
       int best = dflt;
       if (lo <= 0 && hi >= 0) best = lb_combine(dir, best, 0);  // total_mass == 0 -> 0
       for (int64_t v = a; v <= hi && rc == 0; ++v) {
@@ -3021,7 +3054,7 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
                     : lb_values(t, s, h, lv, lf, e, (uint32_t)v, dir, dflt);
         if (rc == 0) best = lb_combine(dir, best, lv[(size_t)(e - h.e) * kMaxRows + top]);
       }
-      res[di] = lb_finish(q, best, dir);
+      res[di] = lb_finish_len(best, dir, max_len);
     }
     if (rc < 0) {
       q.status[i] = SST_ABORTED;

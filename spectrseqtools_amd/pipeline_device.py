@@ -24,6 +24,7 @@ from .masses import PHOSPHATE_LINK_MASS
 from .pipeline import mask_rows, row_masks
 
 _PROGRESS = os.environ.get("SST_PIPE_PROGRESS") == "1"  # per-launch lines of the long stages on stderr
+LB_NOT_RUN = -6  # length_device(spectra=...): the bounds of a spectrum outside the sample
 ERR_BITS = {1: "a spectrum has more than 4096 peaks", 2: "a spectrum has more rows than the reserved slices hold",
             4: "a window outside the pair class", 8: "is_valid_mass raised (a window past a table's end)",
             16: "an explanation dict too large for the LDS hash", 32: "rows out of mass order"}
@@ -64,6 +65,29 @@ def _one_stream(fn):
 
 
 _STREAMS = {}
+
+
+class _Heartbeat:
+    """Prints `what` every `period` seconds on stderr until stop() (a long
+    device call holds no Python lock, so a watcher sees the run is alive)."""
+
+    def __init__(self, what, period):
+        import threading
+        import time
+
+        self._stop = threading.Event()
+        t0 = time.perf_counter()
+
+        def run():
+            while not self._stop.wait(period):
+                print(f"{what}: {time.perf_counter() - t0:.0f} s", file=sys.stderr, flush=True)
+
+        self._t = threading.Thread(target=run, daemon=True)
+        self._t.start()
+
+    def stop(self):
+        self._stop.set()
+        self._t.join()
 
 
 def _check_err(err):
@@ -801,17 +825,21 @@ class DeviceLength:
     comb: object          # torch int64 [total, 2] the combined skeleton (masks)
     reach_batches: int
     distinct_alphabets: int = 0  # skeleton alphabets (each one's row bitsets built once)
+    replay_nodes: object = None  # [S] the bounds' DFS nodes (phase 1, over its attempts)
 
 
 @_one_stream
-def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=8 << 30,
-                  share_alphabets=True):
+def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=64 << 30,
+                  share_alphabets=True, length_chunk=1 << 30, spectra=None):
     """Stage 5: each spectrum's skeleton alphabet (the canonical rows and the
     modifications its START / END skeletons name), both length bounds on it
     (sst_reach_rows_device + sst_length_bounds_reach_device: the reduced
     table's pairs from its rows' reachability, one replay per spectrum, in
     batches whose bitsets fit `reach_budget_bytes`, one pass per max_len
-    group), then the Jaccard selection and the combined skeleton (k_jaccard)."""
+    group), then the Jaccard selection and the combined skeleton (k_jaccard).
+    spectra: the bounds for these spectra only (indices; the others get
+    lb_status LB_NOT_RUN and Jaccard status SST_JAC_BOUNDS) -- a bounded
+    sample where the reference's DFS is too large to replay for all."""
     import torch
 
     dt = dp_table.device_table
@@ -837,21 +865,36 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     n_rows = len(dp_table.masses)
     # spectra with one skeleton alphabet share its rows' bitsets (built up to
     # the heaviest of their windows): few distinct alphabets among many spectra
+    sel = np.arange(S) if spectra is None else np.unique(np.asarray(spectra, dtype=np.int64))
     if share_alphabets:
-        uniq, inv = np.unique(alpha_sk, axis=0, return_inverse=True)
+        uniq, inv = np.unique(alpha_sk[sel], axis=0, return_inverse=True)
         inv = inv.reshape(-1)
     else:
-        uniq, inv = alpha_sk, np.arange(S)
+        uniq, inv = alpha_sk[sel], np.arange(len(sel))
     U = len(uniq)
     words_u = np.zeros(U, np.int64)
-    np.maximum.at(words_u, inv, words)
+    np.maximum.at(words_u, inv, words[sel])
     K_u = mask_rows(uniq, n_rows)[:, 1:].sum(axis=1).astype(np.int64)
     need_u = 4 * K_u * words_u
     lower = np.zeros(S, np.int64)
     upper = np.zeros(S, np.int64)
-    lb_st = np.zeros(S, np.int8)
+    lb_st = np.full(S, LB_NOT_RUN, np.int8)
+    lb_st[sel] = 0
+    nodes = np.zeros(S, np.int64)
     masses = dp_table.masses
     is_mod = [m.is_modification for m in masses]
+    # budgets by max_len (mass_explanation.py:158-172 as set_budgets): caps
+    # round(L * rate) per row, max_modifications round(modification_rate * L)
+    ml_hi = int(ml[sel].max()) if len(sel) else 1
+    if ml_hi >= 128:
+        raise NotImplementedError("length bounds: max_len above 127")
+    caps_len = np.zeros((ml_hi + 1, _native.MAX_ROWS), np.int32)
+    for Lm in range(ml_hi + 1):
+        caps_len[Lm, :len(masses)] = [min(round(Lm * m.modification_rate), 1 << 30) for m in masses]
+    a0_len = [min(round(dp_table.seq.modification_rate * Lm), 1 << 30) for Lm in range(ml_hi + 1)]
+    caps_t = torch.as_tensor(caps_len, device=dev)
+    a0_t = torch.as_tensor(np.asarray(a0_len, np.int32), device=dev)
+    dt.set_budgets(is_mod, [int(c) for c in caps_len[ml_hi, :len(masses)]])  # the rows' modification flags
     by_u = np.argsort(inv, kind="stable")  # spectra grouped by alphabet
     u_first = np.concatenate([[0], np.cumsum(np.bincount(inv, minlength=U))])
     n_batches = 0
@@ -871,34 +914,45 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
         ou_t = torch.as_tensor(off_u, device=dev)
         eng.check(L.sst_reach_rows_device(h, alu_t.data_ptr(), wu_t.data_ptr(), ou_t.data_ptr(), nu, bits.data_ptr()),
                   "sst_reach_rows_device")
-        members = by_u[u_first[u0]:u_first[u1]]  # this batch's spectra
+        if _PROGRESS:
+            eng.synchronize()
+            print(f"[length] batch {n_batches}: {nu} alphabets, {tot / 2**20:.1f} MiB of row bitsets", file=sys.stderr,
+                  flush=True)
+        members = sel[by_u[u_first[u0]:u_first[u1]]]  # this batch's spectra
+        lu_src = by_u[u_first[u0]:u_first[u1]]
         n = len(members)
-        lu = inv[members] - u0  # their alphabets within the batch
+        lu = inv[lu_src] - u0  # their alphabets within the batch
         al_t = torch.as_tensor(uniq[u0:u1][lu].view(np.int64), device=dev).contiguous()
         w_t = torch.as_tensor(words_u[u0:u1][lu], device=dev)
         o_t = torch.as_tensor(off_u[lu], device=dev)
         order = np.argsort(ml[members], kind="stable")
-        ml_s = ml[members][order]
         su_t = torch.as_tensor(su[members][order], device=dev)
         ob_t = torch.as_tensor(ob[members][order], device=dev)
         sp_t = torch.as_tensor(order.astype(np.int32), device=dev)
+        ql_t = torch.as_tensor(ml[members][order].astype(np.int32), device=dev)
         lo_t = torch.zeros(n, dtype=torch.int64, device=dev)
         up_t = torch.zeros(n, dtype=torch.int64, device=dev)
         st_t = torch.zeros(n, dtype=torch.int8, device=dev)
-        bnd = np.flatnonzero(np.diff(ml_s)) + 1
-        for s0, s1 in zip(np.concatenate([[0], bnd]).tolist(), np.concatenate([bnd, [n]]).tolist()):
-            Lm = int(ml_s[s0])
-            dt.set_budgets(is_mod, [round(Lm * m.modification_rate) for m in masses])
-            A = round(dp_table.seq.modification_rate * Lm)
+        nd_t = torch.zeros(n, dtype=torch.int64, device=dev)
+        # every max_len in one launch (per-query budgets); a heartbeat line
+        # every 30 s while a long replay runs (the call releases the GIL)
+        beat = _Heartbeat("[length] replay running", 30.0) if _PROGRESS else None
+        for s0 in range(0, n, length_chunk):
+            s1 = min(n, s0 + length_chunk)
             eng.check(L.sst_length_bounds_reach_device(
                 h, su_t.data_ptr() + 8 * s0, ob_t.data_ptr() + 8 * s0, sp_t.data_ptr() + 4 * s0, al_t.data_ptr(),
-                bits.data_ptr(), o_t.data_ptr(), w_t.data_ptr(), s1 - s0, float(tol), float(prec), Lm, A,
-                lo_t.data_ptr() + 8 * s0, up_t.data_ptr() + 8 * s0, st_t.data_ptr() + s0),
-                "sst_length_bounds_reach_device")
+                bits.data_ptr(), o_t.data_ptr(), w_t.data_ptr(), s1 - s0, float(tol), float(prec), ml_hi, a0_len[ml_hi],
+                lo_t.data_ptr() + 8 * s0, up_t.data_ptr() + 8 * s0, st_t.data_ptr() + s0, ql_t.data_ptr() + 4 * s0,
+                caps_t.data_ptr(), a0_t.data_ptr(), nd_t.data_ptr() + 8 * s0), "sst_length_bounds_reach_device")
+            if _PROGRESS:
+                print(f"[length] bounds {s1}/{n}", file=sys.stderr, flush=True)
+        if beat is not None:
+            beat.stop()
         idx = members[order]
         lower[idx] = lo_t.cpu().numpy()
         upper[idx] = up_t.cpu().numpy()
         lb_st[idx] = st_t.cpu().numpy()
+        nodes[idx] = nd_t.cpu().numpy()
         del bits
         n_batches += 1
         u0 = u1
@@ -921,7 +975,7 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     eng.check(L.sst_jaccard_device(h, ctypes.byref(ja)), "sst_jaccard_device")
     eng.synchronize()
     return DeviceLength(alpha_sk, lower, upper, lb_st, seq_len.cpu().numpy()[:S], jst.cpu().numpy()[:S], comb_off,
-                        comb, n_batches, U)
+                        comb, n_batches, U, nodes)
 
 
 # ---------------------------------------------------------------------------

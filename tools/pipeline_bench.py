@@ -66,6 +66,10 @@ sys.path.insert(0, REPO)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spectra", type=int, default=100000, help="spectra per GPU")
+    ap.add_argument("--warmup-spectra", type=int, default=256, help="untimed warm-up spectra (all stages)")
+    ap.add_argument("--length-spectra", type=int, default=2048,
+                    help="stage 5's length bounds on this many spectra of the rank (0: all); the reference's "
+                         "memoised DFS visits up to ~10^7 nodes per spectrum on rich skeleton alphabets")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--host-driven", action="store_true",
                     help="stages 1-2 through the host-driven batched path (pipeline.classify / filter_fixpoint) "
@@ -136,7 +140,7 @@ def main():
 
     # warm-up on the first 256 spectra (untimed): loads every kernel and the
     # torch ops the stages use, as a serving process would have
-    S0 = min(256, args.spectra)
+    S0 = min(args.warmup_spectra, args.spectra)
     o0, s0, m0 = batch.observed[:batch.offsets[S0]], batch.offsets[:S0 + 1], max_len[:S0]
     if args.host_driven:
         cw = pipeline.classify(o0, s0, su_seq[:S0], dp, bd)
@@ -263,10 +267,16 @@ def main():
         progress("skeleton")
         barrier()
         t0 = time.perf_counter()
-        ln = pd.length_device(dp, sk, db.alpha_dev, su_seq, batch.seq_mass)
+        n_len = len(max_len) if args.length_spectra <= 0 else min(args.length_spectra, len(max_len))
+        ln = pd.length_device(dp, sk, db.alpha_dev, su_seq, batch.seq_mass,
+                              spectra=None if n_len == len(max_len) else np.arange(n_len))
         barrier()
-        stages["length"] = {"s": tmax(time.perf_counter() - t0), "reach_batches": ln.reach_batches,
+        stages["length"] = {"s": tmax(time.perf_counter() - t0), "bounds_spectra": n_len,
+                            "bounds_sample": n_len < len(max_len), "reach_batches": ln.reach_batches,
                             "distinct_skeleton_alphabets": ln.distinct_alphabets,
+                            "replay_nodes": {"total": int(ln.replay_nodes[:n_len].sum()),
+                                             "percentiles": {str(p): int(np.percentile(ln.replay_nodes[:n_len], p))
+                                                             for p in (50, 90, 99, 100)}},
                             "jaccard_status": {int(k): int(v) for k, v in zip(*np.unique(ln.status,
                                                                                          return_counts=True))},
                             "lb_status": {int(k): int(v) for k, v in zip(*np.unique(ln.lb_status,
@@ -290,7 +300,7 @@ def main():
             sizes = [int(buf.numel())]
             outcome = [buf.cpu().numpy()]
         barrier()
-        stages["gather"] = {"s": tmax(time.perf_counter() - t0), "bytes_per_rank": sizes,
+        stages["gather"] = {"s": tmax(time.perf_counter() - t0), "bytes_per_rank": sizes, "kernels": kernels(),
                             "path": "pack_outcomes + one agreed-size gather to rank 0"
                                     + (f" ({'RCCL' if args.backend == 'nccl' else 'gloo'})" if dist else " (local)")}
     engine.profile(False)
@@ -330,6 +340,7 @@ def main():
             "n_gpus": world, "spectra": spectra_all, "peaks": peaks_all,
             "path": "host-driven" if args.host_driven else "device-resident",
             "stages": stages, "total_s": total_s, "gpu_busy_frac": gpu_s / total_s,
+            "total_s_without_length": total_s - stages.get("length", {}).get("s", 0.0),
             "spectra_per_s": spectra_all / total_s, "peaks_per_s": peaks_all / total_s,
             "reduction_rebuild_ms": rebuild_ms, "generation_s": gen_s,
             "reference_estimate_s_per_gpu_share": ref_est,
