@@ -2954,6 +2954,7 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   q.caps_len = d_caps_len;
   q.a0_len = d_a0_len;
   q.nodes_out = d_nodes;
+  q.fuse = 1;
   uint32_t n_exact = 0;
   {
     Prof p(c, SST_K_LENGTH_BOUND);  // windows, extents; every live query is listed for the replay
@@ -2965,7 +2966,7 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   // memo per wave: 2^16 masses on the first try (most spectra), 8x per retry
   // for the queries that ran out; the waves in flight are what the
   // workspace budget allows at that size (a retry keeps its parallelism)
-  const size_t per_entry = hash_entry_bytes() + kMaxRows;
+  const size_t per_entry = hash_entry_bytes() + 2 * kMaxRows;  // two value slices (q.fuse)
   uint32_t cap = kLBHashCap0;
   auto units_for = [&](uint32_t n_q) {
     const size_t by_mem = kReachMemoBytes / ((size_t)cap * per_entry);
@@ -2974,7 +2975,7 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   int units = units_for(n_exact);
   while (n_exact) {
     DevBuf hash, vals, frames;
-    if (!hash.ensure((size_t)units * cap * hash_entry_bytes()) || !vals.ensure((size_t)units * cap * kMaxRows) ||
+    if (!hash.ensure((size_t)units * cap * hash_entry_bytes()) || !vals.ensure((size_t)units * cap * 2 * kMaxRows) ||
         !frames.ensure((size_t)units * lb_frame_bytes()))
       return fail(c, SST_E_NOMEM, "device allocation failed (length-bound memo)");
     HIP_OK(c, hipMemsetAsync(hash.p, 0, hash.bytes, c->stream));

@@ -277,6 +277,7 @@ struct LBArgs {
   const int32_t* caps_len = nullptr;
   const int32_t* a0_len = nullptr;
   uint64_t* nodes_out = nullptr;  // may be null: per query, phase-1 nodes visited (summed over attempts)
+  int fuse = 0;  // wave mode with both: the values computed inside phase 1 (vals holds 2 slices per wave)
 };
 
 // per-row reachability of reduced alphabets (sst_reach.hip): spectrum g's

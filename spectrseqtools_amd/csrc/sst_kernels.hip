@@ -612,6 +612,13 @@ struct Hash {
   bool reach = false;      // wave mode only: node records from rv, not the full table's index
   ReachView rv{};
   M128 last_L{0, 0};       // reach mode: the left bits of the last first visit's record (p1_classify)
+  uint32_t last_rlo = 0;   // the rows [last_rlo, r] the last first visit covered (p1_visit)
+  // fused values (length bounds, both directions): a frame's rows get their
+  // lower / upper values when the frame completes -- every child is final by
+  // then -- instead of in separate passes over the DAG
+  int8_t* vals_lo = nullptr;
+  int8_t* vals_hi = nullptr;
+  int dflt_lo = 0;
   __device__ __forceinline__ uint32_t slot(uint32_t m) const { return (m * 0x9E3779B1u) & mask; }
   // returns entry pointer or nullptr if absent
   __device__ __forceinline__ HEntry* find(uint32_t m) const {
@@ -904,6 +911,18 @@ __device__ __forceinline__ void shallow_window(const TableArgs& t, const Lds& s,
   }
 }
 
+// min (dir 0) / max (dir 1) of the length bound's values, and its prefix over the 64 lanes
+__device__ __forceinline__ int lb_combine(int dir, int x, int y) { return dir ? (x > y ? x : y) : (x < y ? x : y); }
+__device__ __forceinline__ int lb_scan(int dir, int x) {  // inclusive prefix combine over the 64 lanes
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x = lb_combine(dir, x, y);
+  }
+  return x;
+}
+
 // ---------------------------------------------------------------------------
 // exact path phase 1: replay the memoised DFS (first-visit budgets)
 // ---------------------------------------------------------------------------
@@ -1015,6 +1034,7 @@ __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& 
   e->en1 = en_old1 | en.b;
   e->meta = (meta & 0xFF00u) | ((uint32_t)lo << 16) | (uint32_t)r;
   h.last_meta = e->meta;
+  h.last_rlo = (uint32_t)rlo;
   if (WAVE && h.reach) h.last_L = rec_L(rec);
   // the frame will visit (m - w_rr, rr) for every enabled row: issue their
   // index-record and first-probe loads now, independently, so the visits
@@ -1173,6 +1193,50 @@ __device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, co
   return M128{(uint64_t)__ballot(desc[0]), (uint64_t)__ballot(desc[1])};
 }
 
+// Both length-bound values of a completed frame's rows [rlo, rtop] of mass m
+// (lb_values_wave's recurrence, one frame at a time): row r's value combines
+// the default, the row below (the up chain; the entry's earlier rows are
+// final) and, when its left branch was enabled at the first visit, the
+// child's value at row r plus one.
+__device__ __forceinline__ void p1_values(const TableArgs& t, const Lds& s, const Hash& h, const HEntry* e, uint32_t m,
+                                          int rlo, int rtop) {
+  const int lane = threadIdx.x & 63;
+  const int lo = (int)((e->meta >> 16) & 0xFF);
+  const M128 en{e->en0, e->en1};
+  int cl[2] = {127, 127}, ch[2] = {-128, -128};
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lane + 64 * half;
+    if (r < t.n_rows && r >= rlo && r <= rtop && mtest(en, r)) {
+      const uint32_t c = m - (uint32_t)s.w[r];
+      int vl = 0, vh = 0;  // total_mass == 0 -> 0 (mass_table.py:378-379)
+      if (c != 0) {
+        const HEntry* ce = h.find(c);
+        if (ce) {
+          const size_t at = (size_t)(ce - h.e) * kMaxRows + r;
+          vl = h.vals_lo[at];
+          vh = h.vals_hi[at];
+        }
+      }
+      cl[half] = vl + 1;
+      ch[half] = vh + 1;
+    }
+  }
+  const size_t base = (size_t)(e - h.e) * kMaxRows;
+  const int seed_lo = rlo > lo ? h.vals_lo[base + rlo - 1] : h.dflt_lo;
+  const int seed_hi = rlo > lo ? h.vals_hi[base + rlo - 1] : -1;
+  const int l0 = lb_scan(0, cl[0]), l1 = lb_combine(0, lb_scan(0, cl[1]), __shfl(l0, 63, 64));
+  const int u0 = lb_scan(1, ch[0]), u1 = lb_combine(1, lb_scan(1, ch[1]), __shfl(u0, 63, 64));
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lane + 64 * half;
+    if (r < kMaxRows && r >= rlo && r <= rtop) {
+      h.vals_lo[base + r] = (int8_t)lb_combine(0, seed_lo, half ? l1 : l0);
+      h.vals_hi[base + r] = (int8_t)lb_combine(1, seed_hi, half ? u1 : u0);
+    }
+  }
+}
+
 // phase1_body for one query per wave: the same replay, with the saved frames
 // in LDS and the current frame's lowest non-empty row in a register (written
 // to its memo entry once, when the frame completes -- no other node can read
@@ -1192,11 +1256,13 @@ __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Fra
     if (pr == 0) continue;
     uint32_t m = (uint32_t)v, meta = h.last_meta;
     int A = A0, B = s.cap[top], rtop = top, d = 0;
+    int rlo = (int)h.last_rlo;
     int ne = (int)((meta >> 8) & 0xFF);
     rest = p1_classify(t, s, h, m, rest, ne);
     for (;;) {
       if (mzero(rest)) {  // frame done: publish its non-empty row, report to the parent
         e->meta = (meta & ~0xFF00u) | ((uint32_t)ne << 8);
+        if (h.vals_lo) p1_values(t, s, h, e, m, rlo, rtop);
         if (d == 0) break;
         const int cne = ne;
         const P1Frame f = fr[--d];
@@ -1206,6 +1272,7 @@ __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Fra
         A = f.A;
         B = f.B;
         rtop = f.rtop;
+        rlo = f.pad1;
         ne = f.ne;
         meta = f.meta;
         const int rr = f.rnext - 1;
@@ -1229,13 +1296,15 @@ __device__ int phase1_body_wave(const TableArgs& t, const Lds& s, Hash& h, P1Fra
             p1_visit<true>(t, s, h, (uint32_t)child, rr, A - md, Bv - md, nonempty, nodes, cen, cent, am);
         if (pushed < 0) return -1;
         if (pushed) {  // descend: save this frame (its pending row is rr)
-          fr[d++] = P1Frame{rest.a, rest.b, e, m, A, B, (uint8_t)rtop, (uint8_t)(rr + 1), (uint8_t)ne, 0, meta};
+          fr[d++] = P1Frame{rest.a, rest.b, e, m, A, B, (uint8_t)rtop, (uint8_t)(rr + 1), (uint8_t)ne, (uint8_t)rlo,
+                            meta};
           rest = cen;
           e = cent;
           m = (uint32_t)child;
           A -= md;
           B = Bv - md;
           rtop = rr;
+          rlo = (int)h.last_rlo;
           meta = h.last_meta;
           ne = (int)((meta >> 8) & 0xFF);
           rest = p1_classify(t, s, h, m, rest, ne);
@@ -2708,7 +2777,6 @@ __global__ void k_layer_step(const uint64_t* __restrict__ prev, uint64_t* __rest
   next[j] = acc;
 }
 
-__device__ __forceinline__ int lb_combine(int dir, int x, int y) { return dir ? (x > y ? x : y) : (x < y ? x : y); }
 
 // saved ancestors of the value DP (the current frame is in registers)
 struct LBFrame {
@@ -2779,15 +2847,6 @@ struct LBWFrame {
   uint32_t m;
   uint32_t pad;
 };
-__device__ __forceinline__ int lb_scan(int dir, int x) {  // inclusive prefix combine over the 64 lanes
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(x, off, 64);
-    if (lane >= off) x = lb_combine(dir, x, y);
-  }
-  return x;
-}
 __device__ __forceinline__ M128 lb_uncomputed(const TableArgs& t, const Lds& s, const Hash& h, const HEntry* e,
                                               uint32_t m, bool& bad, uint32_t pass) {
   const int lane = threadIdx.x & 63;
@@ -2959,7 +3018,12 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
   h.e = (HEntry*)(hash + (size_t)gid * hash_cap * sizeof(HEntry));
   h.mask = hash_cap - 1;
   h.limit = hash_cap / 4;  // load factor <= 1/4: a wave waits for its longest probe chain
-  int8_t* lv = vals + (size_t)gid * hash_cap * kMaxRows;
+  const bool fuse = WAVE && q.fuse;  // both bounds' values in phase 1 (two value slices per wave)
+  int8_t* lv = vals + (size_t)gid * hash_cap * kMaxRows * (fuse ? 2 : 1);
+  if (fuse) {
+    h.vals_lo = lv;
+    h.vals_hi = lv + (size_t)hash_cap * kMaxRows;
+  }
   uint64_t epoch = 0;
   const int top = t.n_rows - 1;
   for (int64_t j = gid; j < (int64_t)n_list; j += nthreads) {
@@ -2990,6 +3054,7 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
     }
     h.epoch = ++epoch;  // the workspace was zeroed: epochs 1, 2, ... are fresh
     h.used = 0;
+    h.dflt_lo = max_len + 1;
     uint64_t nodes = 0;
     const int64_t a = lo < 1 ? 1 : lo;
     M128 am{~0ull, ~0ull};
@@ -3032,10 +3097,31 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
       continue;
     }
     // the value DP over phase 1's DAG: one direction, or (both) the lower
-    // bound then the upper from the same first visits (pass 1, 2)
+    // bound then the upper from the same first visits (pass 1, 2); fused:
+    // phase 1 already wrote both, the roots' top rows are combined here
     const int n_dir = WAVE && q.both ? 2 : 1;
     int64_t res[2] = {0, 0};
-    for (int di = 0; di < n_dir && rc == 0; ++di) {
+    if (fuse) {
+      int bl = max_len + 1, bh = -1;
+      if (lo <= 0 && hi >= 0) {  // total_mass == 0 -> 0
+        bl = lb_combine(0, bl, 0);
+        bh = lb_combine(1, bh, 0);
+      }
+      for (int64_t v = a; v <= hi && rc == 0; ++v) {
+        if (h.reach ? !reach_bit(h.rv, h.rv.K - 1, v) : !((t.valid[v >> 6] >> (v & 63)) & 1ull)) continue;
+        const HEntry* e = h.find((uint32_t)v);
+        if (!e) {
+          rc = -3;
+          break;
+        }
+        const size_t at = (size_t)(e - h.e) * kMaxRows + top;
+        bl = lb_combine(0, bl, h.vals_lo[at]);
+        bh = lb_combine(1, bh, h.vals_hi[at]);
+      }
+      res[0] = lb_finish_len(bl, 0, max_len);
+      res[1] = lb_finish_len(bh, 1, max_len);
+    }
+    for (int di = 0; di < n_dir && rc == 0 && !fuse; ++di) {
       const int dir = q.both ? di : q.dir;
       const uint32_t pass = (uint32_t)di + 1;
       const int dflt = dir ? -1 : max_len + 1;
