@@ -67,6 +67,7 @@ class EngineError(RuntimeError):
 
 WALK_MAX_ROUNDS = 16  # SST_WALK_MAX_ROUNDS
 MAX_ROWS = 120  # SST_MAX_ROWS (row stride of per-length cap tables)
+LB_HEAVY = -7  # SST_LB_HEAVY
 (WALK_DONE, WALK_SUSPENDED, WALK_BIG, WALK_RAISE, WALK_LIMIT, WALK_ROUNDS, WALK_MISSING) = range(7)
 
 
@@ -252,7 +253,7 @@ def load_library(path=LIB_PATH):
     lib.sst_reach_rows_device.argtypes = [_P, _P, _P, _P, _I64, _P]
     lib.sst_reach_rows_device.restype = _I
     lib.sst_length_bounds_reach_device.argtypes = [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _D, _D, _I, _I64, _P, _P, _P,
-                                                   _P, _P, _P, _P]
+                                                   _P, _P, _P, _P, _I64, ctypes.c_uint32]
     lib.sst_length_bounds_reach_device.restype = _I
     lib.sst_jaccard_device.argtypes = [_P, ctypes.POINTER(JaccardArgs)]
     lib.sst_jaccard_device.restype = _I

@@ -2914,7 +2914,8 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
                                               const int64_t* d_reach_words, int64_t n, double tol, double prec,
                                               int max_len, int64_t max_mods, int64_t* d_lower, int64_t* d_upper,
                                               int8_t* d_status, const int32_t* d_qlen, const int32_t* d_caps_len,
-                                              const int32_t* d_a0_len, uint64_t* d_nodes) {
+                                              const int32_t* d_a0_len, uint64_t* d_nodes, int64_t soft_nodes,
+                                              uint32_t memo_first) {
   if (!t || n < 0 || n > INT32_MAX || max_len < 0 || max_len > 120 || (d_qlen && (!d_caps_len || !d_a0_len)) ||
       (n > 0 && (!d_su || !d_obs || !d_spec || !d_alpha || !d_reach_bits || !d_reach_off || !d_reach_words ||
                  !d_lower || !d_upper || !d_status)))
@@ -2955,6 +2956,11 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   q.a0_len = d_a0_len;
   q.nodes_out = d_nodes;
   q.fuse = 1;
+  if (soft_nodes > 0) {
+    q.node_budget = (uint64_t)soft_nodes;
+    q.soft = 1;
+  }
+  if (memo_first && (memo_first & (memo_first - 1))) return fail(c, SST_E_ARG, "length bound: memo_first not a power of two");
   uint32_t n_exact = 0;
   {
     Prof p(c, SST_K_LENGTH_BOUND);  // windows, extents; every live query is listed for the replay
@@ -2967,7 +2973,7 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   // for the queries that ran out; the waves in flight are what the
   // workspace budget allows at that size (a retry keeps its parallelism)
   const size_t per_entry = hash_entry_bytes() + 2 * kMaxRows;  // two value slices (q.fuse)
-  uint32_t cap = kLBHashCap0;
+  uint32_t cap = memo_first ? std::max<uint32_t>(memo_first, 64) : kLBHashCap0;
   auto units_for = [&](uint32_t n_q) {
     const size_t by_mem = kReachMemoBytes / ((size_t)cap * per_entry);
     return (int)std::max<size_t>(1, std::min<size_t>({(size_t)kReachUnits, (size_t)std::max<uint32_t>(1, n_q), by_mem}));

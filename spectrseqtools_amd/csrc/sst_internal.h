@@ -32,6 +32,7 @@ constexpr int kStatusPending = -10;
 constexpr int kStatusArenaRetry = -11;
 constexpr int kStatusExactRetry = -12;
 constexpr int kLBEmptyWindow = -5;  // length bound: empty window (the reference's min([]) raises ValueError)
+constexpr int kLBHeavy = SST_LB_HEAVY;  // length bound: over the caller's soft node budget (replayed later)
 
 enum {
   kStatShallow = 0,
@@ -278,6 +279,7 @@ struct LBArgs {
   const int32_t* a0_len = nullptr;
   uint64_t* nodes_out = nullptr;  // may be null: per query, phase-1 nodes visited (summed over attempts)
   int fuse = 0;  // wave mode with both: the values computed inside phase 1 (vals holds 2 slices per wave)
+  int soft = 0;  // node_budget is the caller's soft budget: a query over it gets kLBHeavy, not SST_ABORTED
 };
 
 // per-row reachability of reduced alphabets (sst_reach.hip): spectrum g's

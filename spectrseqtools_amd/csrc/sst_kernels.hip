@@ -1154,7 +1154,7 @@ __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* f
 // Only those children are descended (ascending rows, as the reference).  The
 // frame's lowest non-empty row is the minimum over its rows (the sequential
 // replay meets them in ascending order, so "first found" is the minimum).
-__device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, const Hash& h, uint32_t m, M128 rows,
+__device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, Hash& h, uint32_t m, M128 rows,
                                             int& ne) {
   const int lane = threadIdx.x & 63;
   bool desc[2];
@@ -1190,7 +1190,26 @@ __device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, co
     nrow = nrow < o ? nrow : o;
   }
   ne = ne < nrow ? ne : nrow;
-  return M128{(uint64_t)__ballot(desc[0]), (uint64_t)__ballot(desc[1])};
+  const M128 d{(uint64_t)__ballot(desc[0]), (uint64_t)__ballot(desc[1])};
+  if (h.reach && !mzero(d)) {
+    // the replay descends into the lowest such child next: issue its record's
+    // reach words now (reach_rec reads them), behind this frame's probes
+    const int64_t c0 = (int64_t)m - s.w[mlow(d)];
+    const ReachView& rv = h.rv;
+    uint32_t sink = 0;
+    if (lane < rv.K) {
+      const int64_t x0 = c0 >> 5, x1 = (c0 - rv.w0) >> 5;
+      if (x0 >= 0 && x0 < rv.W) sink ^= rv.bits[(int64_t)lane * rv.W + x0];
+      if (x1 >= 0 && x1 < rv.W) sink ^= rv.bits[(int64_t)lane * rv.W + x1];
+    }
+    if (lane + 64 < rv.K) {
+      const int64_t x0 = c0 >> 5, x1 = (c0 - rv.w1) >> 5;
+      if (x0 >= 0 && x0 < rv.W) sink ^= rv.bits[(int64_t)(lane + 64) * rv.W + x0];
+      if (x1 >= 0 && x1 < rv.W) sink ^= rv.bits[(int64_t)(lane + 64) * rv.W + x1];
+    }
+    h.sink ^= sink;
+  }
+  return d;
 }
 
 // Both length-bound values of a completed frame's rows [rlo, rtop] of mass m
@@ -3090,6 +3109,10 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
     if (q.nodes_out && (!WAVE || threadIdx.x == 0)) q.nodes_out[i] += nodes;
     if (rc == -1) {
       q.status[i] = (int8_t)kStatusExactRetry;
+      continue;
+    }
+    if (rc == -3 && q.soft) {
+      q.status[i] = (int8_t)kLBHeavy;
       continue;
     }
     if (rc < 0) {

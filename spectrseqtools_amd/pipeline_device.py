@@ -830,7 +830,8 @@ class DeviceLength:
 
 @_one_stream
 def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=64 << 30,
-                  share_alphabets=True, length_chunk=1 << 30, spectra=None):
+                  share_alphabets=True, length_chunk=1 << 30, spectra=None, soft_nodes=1 << 20,
+                  heavy_memo=1 << 20):
     """Stage 5: each spectrum's skeleton alphabet (the canonical rows and the
     modifications its START / END skeletons name), both length bounds on it
     (sst_reach_rows_device + sst_length_bounds_reach_device: the reduced
@@ -866,16 +867,6 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     # spectra with one skeleton alphabet share its rows' bitsets (built up to
     # the heaviest of their windows): few distinct alphabets among many spectra
     sel = np.arange(S) if spectra is None else np.unique(np.asarray(spectra, dtype=np.int64))
-    if share_alphabets:
-        uniq, inv = np.unique(alpha_sk[sel], axis=0, return_inverse=True)
-        inv = inv.reshape(-1)
-    else:
-        uniq, inv = alpha_sk[sel], np.arange(len(sel))
-    U = len(uniq)
-    words_u = np.zeros(U, np.int64)
-    np.maximum.at(words_u, inv, words[sel])
-    K_u = mask_rows(uniq, n_rows)[:, 1:].sum(axis=1).astype(np.int64)
-    need_u = 4 * K_u * words_u
     lower = np.zeros(S, np.int64)
     upper = np.zeros(S, np.int64)
     lb_st = np.full(S, LB_NOT_RUN, np.int8)
@@ -895,67 +886,95 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     caps_t = torch.as_tensor(caps_len, device=dev)
     a0_t = torch.as_tensor(np.asarray(a0_len, np.int32), device=dev)
     dt.set_budgets(is_mod, [int(c) for c in caps_len[ml_hi, :len(masses)]])  # the rows' modification flags
-    by_u = np.argsort(inv, kind="stable")  # spectra grouped by alphabet
-    u_first = np.concatenate([[0], np.cumsum(np.bincount(inv, minlength=U))])
-    n_batches = 0
-    u0 = 0
-    while u0 < U:
-        u1, tot = u0, 0
-        while u1 < U and (u1 == u0 or tot + need_u[u1] <= reach_budget_bytes):
-            tot += int(need_u[u1])
-            u1 += 1
-        nu = u1 - u0
-        off_u = np.concatenate([[0], np.cumsum(need_u[u0:u1] // 4)[:-1]]).astype(np.int64)
-        bits = torch.empty(max(1, int(tot // 4)), dtype=torch.int32, device=dev)
-        # (every device array stays referenced until the batch is done: a
-        # temporary's block can be handed to the next allocation at once)
-        alu_t = torch.as_tensor(uniq[u0:u1].view(np.int64), device=dev).contiguous()
-        wu_t = torch.as_tensor(words_u[u0:u1], device=dev)
-        ou_t = torch.as_tensor(off_u, device=dev)
-        eng.check(L.sst_reach_rows_device(h, alu_t.data_ptr(), wu_t.data_ptr(), ou_t.data_ptr(), nu, bits.data_ptr()),
-                  "sst_reach_rows_device")
-        if _PROGRESS:
-            eng.synchronize()
-            print(f"[length] batch {n_batches}: {nu} alphabets, {tot / 2**20:.1f} MiB of row bitsets", file=sys.stderr,
-                  flush=True)
-        members = sel[by_u[u_first[u0]:u_first[u1]]]  # this batch's spectra
-        lu_src = by_u[u_first[u0]:u_first[u1]]
-        n = len(members)
-        lu = inv[lu_src] - u0  # their alphabets within the batch
-        al_t = torch.as_tensor(uniq[u0:u1][lu].view(np.int64), device=dev).contiguous()
-        w_t = torch.as_tensor(words_u[u0:u1][lu], device=dev)
-        o_t = torch.as_tensor(off_u[lu], device=dev)
-        order = np.argsort(ml[members], kind="stable")
-        su_t = torch.as_tensor(su[members][order], device=dev)
-        ob_t = torch.as_tensor(ob[members][order], device=dev)
-        sp_t = torch.as_tensor(order.astype(np.int32), device=dev)
-        ql_t = torch.as_tensor(ml[members][order].astype(np.int32), device=dev)
-        lo_t = torch.zeros(n, dtype=torch.int64, device=dev)
-        up_t = torch.zeros(n, dtype=torch.int64, device=dev)
-        st_t = torch.zeros(n, dtype=torch.int8, device=dev)
-        nd_t = torch.zeros(n, dtype=torch.int64, device=dev)
-        # every max_len in one launch (per-query budgets); a heartbeat line
-        # every 30 s while a long replay runs (the call releases the GIL)
-        beat = _Heartbeat("[length] replay running", 30.0) if _PROGRESS else None
-        for s0 in range(0, n, length_chunk):
-            s1 = min(n, s0 + length_chunk)
-            eng.check(L.sst_length_bounds_reach_device(
-                h, su_t.data_ptr() + 8 * s0, ob_t.data_ptr() + 8 * s0, sp_t.data_ptr() + 4 * s0, al_t.data_ptr(),
-                bits.data_ptr(), o_t.data_ptr(), w_t.data_ptr(), s1 - s0, float(tol), float(prec), ml_hi, a0_len[ml_hi],
-                lo_t.data_ptr() + 8 * s0, up_t.data_ptr() + 8 * s0, st_t.data_ptr() + s0, ql_t.data_ptr() + 4 * s0,
-                caps_t.data_ptr(), a0_t.data_ptr(), nd_t.data_ptr() + 8 * s0), "sst_length_bounds_reach_device")
+    stats = {"batches": 0, "distinct": 0}
+
+    def bounds_pass(sel, soft_nodes, memo_first):
+        """Both bounds of spectra `sel`, in batches whose row bitsets fit
+        the budget; returns the spectra left SST_LB_HEAVY (over soft_nodes)."""
+        # spectra with one skeleton alphabet share its rows' bitsets (built up
+        # to the heaviest of their windows)
+        if share_alphabets:
+            uniq, inv = np.unique(alpha_sk[sel], axis=0, return_inverse=True)
+            inv = inv.reshape(-1)
+        else:
+            uniq, inv = alpha_sk[sel], np.arange(len(sel))
+        U = len(uniq)
+        stats["distinct"] = max(stats["distinct"], U)
+        words_u = np.zeros(U, np.int64)
+        np.maximum.at(words_u, inv, words[sel])
+        K_u = mask_rows(uniq, n_rows)[:, 1:].sum(axis=1).astype(np.int64)
+        need_u = 4 * K_u * words_u
+        by_u = np.argsort(inv, kind="stable")  # spectra grouped by alphabet
+        u_first = np.concatenate([[0], np.cumsum(np.bincount(inv, minlength=U))])
+        u0 = 0
+        while u0 < U:
+            u1, tot = u0, 0
+            while u1 < U and (u1 == u0 or tot + need_u[u1] <= reach_budget_bytes):
+                tot += int(need_u[u1])
+                u1 += 1
+            nu = u1 - u0
+            off_u = np.concatenate([[0], np.cumsum(need_u[u0:u1] // 4)[:-1]]).astype(np.int64)
+            bits = torch.empty(max(1, int(tot // 4)), dtype=torch.int32, device=dev)
+            # (every device array stays referenced until the batch is done: a
+            # temporary's block can be handed to the next allocation at once)
+            alu_t = torch.as_tensor(uniq[u0:u1].view(np.int64), device=dev).contiguous()
+            wu_t = torch.as_tensor(words_u[u0:u1], device=dev)
+            ou_t = torch.as_tensor(off_u, device=dev)
+            eng.check(L.sst_reach_rows_device(h, alu_t.data_ptr(), wu_t.data_ptr(), ou_t.data_ptr(), nu,
+                                              bits.data_ptr()), "sst_reach_rows_device")
+            lu_src = by_u[u_first[u0]:u_first[u1]]
+            members = sel[lu_src]  # this batch's spectra
+            n = len(members)
             if _PROGRESS:
-                print(f"[length] bounds {s1}/{n}", file=sys.stderr, flush=True)
-        if beat is not None:
-            beat.stop()
-        idx = members[order]
-        lower[idx] = lo_t.cpu().numpy()
-        upper[idx] = up_t.cpu().numpy()
-        lb_st[idx] = st_t.cpu().numpy()
-        nodes[idx] = nd_t.cpu().numpy()
-        del bits
-        n_batches += 1
-        u0 = u1
+                eng.synchronize()
+                print(f"[length] batch {stats['batches']}: {n} spectra, {nu} alphabets, {tot / 2**20:.1f} MiB of row "
+                      f"bitsets, soft node budget {soft_nodes}", file=sys.stderr, flush=True)
+            lu = inv[lu_src] - u0  # their alphabets within the batch
+            al_t = torch.as_tensor(uniq[u0:u1][lu].view(np.int64), device=dev).contiguous()
+            w_t = torch.as_tensor(words_u[u0:u1][lu], device=dev)
+            o_t = torch.as_tensor(off_u[lu], device=dev)
+            order = np.argsort(ml[members], kind="stable")
+            su_t = torch.as_tensor(su[members][order], device=dev)
+            ob_t = torch.as_tensor(ob[members][order], device=dev)
+            sp_t = torch.as_tensor(order.astype(np.int32), device=dev)
+            ql_t = torch.as_tensor(ml[members][order].astype(np.int32), device=dev)
+            lo_t = torch.zeros(n, dtype=torch.int64, device=dev)
+            up_t = torch.zeros(n, dtype=torch.int64, device=dev)
+            st_t = torch.zeros(n, dtype=torch.int8, device=dev)
+            nd_t = torch.zeros(n, dtype=torch.int64, device=dev)
+            # every max_len in one launch (per-query budgets); a heartbeat line
+            # every 30 s while a long replay runs (the call releases the GIL)
+            beat = _Heartbeat("[length] replay running", 30.0) if _PROGRESS else None
+            for s0 in range(0, n, length_chunk):
+                s1 = min(n, s0 + length_chunk)
+                eng.check(L.sst_length_bounds_reach_device(
+                    h, su_t.data_ptr() + 8 * s0, ob_t.data_ptr() + 8 * s0, sp_t.data_ptr() + 4 * s0, al_t.data_ptr(),
+                    bits.data_ptr(), o_t.data_ptr(), w_t.data_ptr(), s1 - s0, float(tol), float(prec), ml_hi,
+                    a0_len[ml_hi], lo_t.data_ptr() + 8 * s0, up_t.data_ptr() + 8 * s0, st_t.data_ptr() + s0,
+                    ql_t.data_ptr() + 4 * s0, caps_t.data_ptr(), a0_t.data_ptr(), nd_t.data_ptr() + 8 * s0,
+                    int(soft_nodes), int(memo_first)), "sst_length_bounds_reach_device")
+            if beat is not None:
+                beat.stop()
+            idx = members[order]
+            lower[idx] = lo_t.cpu().numpy()
+            upper[idx] = up_t.cpu().numpy()
+            lb_st[idx] = st_t.cpu().numpy()
+            nodes[idx] += nd_t.cpu().numpy()
+            del bits
+            stats["batches"] += 1
+            u0 = u1
+        return sel[lb_st[sel] == _native.LB_HEAVY]
+
+    # light spectra first, under a soft node budget, so that no batch waits
+    # for its few heavy spectra; then the heavy ones together, with a larger
+    # first memo
+    heavy = bounds_pass(sel, soft_nodes, 0) if soft_nodes else sel
+    if len(heavy):
+        if _PROGRESS:
+            print(f"[length] {len(heavy)} spectra over {soft_nodes} nodes: replayed together", file=sys.stderr,
+                  flush=True)
+        bounds_pass(heavy, 0, heavy_memo if soft_nodes else 0)
+    n_batches, U = stats["batches"], stats["distinct"]
     # Jaccard + combine
     comb_off = np.concatenate([[0], np.cumsum(ml)]).astype(np.int64)
     comb = torch.zeros((max(1, int(comb_off[-1])), 2), dtype=torch.int64, device=dev)

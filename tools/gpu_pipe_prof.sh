@@ -11,15 +11,15 @@ step() {  # step NAME TIMEOUT CMD...
   echo "[$name] rc=$rc"; tail -2 "gpurun_out/${TAG}_${name}.log" | cut -c1-800
   if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
-SST_PIPE_PROGRESS=1 step pipe 600 python -u tools/pipeline_bench.py --spectra $N
-SST_PIPE_PROGRESS=1 step stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_stats -o trace -- python3 tools/pipeline_bench.py --spectra $N
+SST_PIPE_PROGRESS=1 step pipe 600 python -u tools/pipeline_bench.py --spectra $N --warmup-spectra 64 --length-spectra ${LS:-256}
+SST_PIPE_PROGRESS=1 step stats 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_stats -o trace -- python3 tools/pipeline_bench.py --spectra $N --warmup-spectra 64 --length-spectra ${LS:-256}
 find gpurun_out/${TAG}_stats -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_kernel_stats.csv \;
 [ "$PMC" = "0" ] && exit 0
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${TAG}_p$i -o pmc -- python3 tools/pipeline_bench.py --spectra 20000 > gpurun_out/${TAG}_p$i.log 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/${TAG}_p$i -o pmc -- python3 tools/pipeline_bench.py --spectra 20000 --warmup-spectra 16 --length-spectra 16 > gpurun_out/${TAG}_p$i.log 2>&1
   rc=$?; echo "[pmc $i: $grp] rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done < tools/pmc_groups.txt
