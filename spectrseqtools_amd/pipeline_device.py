@@ -594,6 +594,33 @@ def _masked_explain_refs(dp_table, alpha_dev, mass, thr, spec, n, max_len, dst, 
     return out
 
 
+def merge_requery_round(m_sid, m_ptr, m_n, m_st, block, p_, n_, s_, n_sides):
+    """Append one re-query round's answers to the merged per-side lists the
+    walk reads as a single round.  block[sid] = start << 32 | count: side
+    sid's entries of this round, contiguous in its lane's order, in p_ / n_ /
+    s_.  Returns the merged (sid, ptr, n, st) ordered by side and, per side,
+    round-major (a stable sort of the concatenation), and the walk's view
+    (start << 32 | count per side, ptr, n, st)."""
+    import torch
+
+    dev = block.device
+    cnt_s = block & 0xFFFFFFFF
+    sides_nz = torch.nonzero(cnt_s).flatten()
+    c_nz = cnt_s[sides_nz]
+    first = torch.cumsum(c_nz, 0) - c_nz
+    idx = torch.repeat_interleave(block[sides_nz] >> 32, c_nz) + (
+        torch.arange(int(c_nz.sum().item()), device=dev) - torch.repeat_interleave(first, c_nz))
+    m_sid = torch.cat([m_sid, torch.repeat_interleave(sides_nz, c_nz)])
+    m_ptr = torch.cat([m_ptr, p_[idx]])
+    m_n = torch.cat([m_n, n_[idx]])
+    m_st = torch.cat([m_st, s_[idx]])
+    order = torch.sort(m_sid, stable=True).indices
+    m_sid, m_ptr, m_n, m_st = m_sid[order], m_ptr[order], m_n[order], m_st[order]
+    per = torch.bincount(m_sid, minlength=n_sides)
+    start = torch.cumsum(per, 0) - per
+    return m_sid, m_ptr, m_n, m_st, ((start << 32) | per, m_ptr, m_n, m_st)
+
+
 @dataclass
 class DeviceSkeleton:
     """_predict_skeleton of both sides of every spectrum (device arrays)."""
@@ -753,25 +780,8 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
             res = _masked_explain_refs(dp_table, alpha_dev, req_mass, req_thr, req_spec, n_req, max_len, dst, p_, n_,
                                        s_)
             results.extend(res)
-            # this round's entries per side (each side's block is contiguous, in
-            # its lane's order), appended after the earlier rounds' and ordered
-            # by side with a stable sort: per side, round-major
-            blk = req_block[:2 * S]
-            cnt_s = (blk & 0xFFFFFFFF)
-            sides_nz = torch.nonzero(cnt_s).flatten()
-            c_nz = cnt_s[sides_nz]
-            first = torch.cumsum(c_nz, 0) - c_nz
-            idx = torch.repeat_interleave(blk[sides_nz] >> 32, c_nz) + (
-                torch.arange(int(c_nz.sum().item()), device=dev) - torch.repeat_interleave(first, c_nz))
-            m_sid = torch.cat([m_sid, torch.repeat_interleave(sides_nz, c_nz)])
-            m_ptr = torch.cat([m_ptr, p_[idx]])
-            m_n = torch.cat([m_n, n_[idx]])
-            m_st = torch.cat([m_st, s_[idx]])
-            order = torch.sort(m_sid, stable=True).indices
-            m_sid, m_ptr, m_n, m_st = m_sid[order], m_ptr[order], m_n[order], m_st[order]
-            per = torch.bincount(m_sid, minlength=2 * S)
-            start = torch.cumsum(per, 0) - per
-            merged = ((start << 32) | per, m_ptr, m_n, m_st)
+            m_sid, m_ptr, m_n, m_st, merged = merge_requery_round(m_sid, m_ptr, m_n, m_st, req_block[:2 * S], p_,
+                                                                  n_, s_, 2 * S)
             n_rounds += 1
             n_req_total += n_req
     return DeviceSkeleton(max_len, skel_off, skel, min_end, max_end, kept, status.cpu().numpy()[:2 * S], launches,
