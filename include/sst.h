@@ -734,7 +734,10 @@ int sst_skeleton_alpha_device(sst_table* t, int64_t n_spec, const int32_t* d_max
  * replay passes that many nodes stops with status SST_LB_HEAVY (the caller
  * replays such queries together later, with soft_nodes 0), so that a few
  * heavy spectra do not hold up a batch.  memo_first: the first attempt's
- * memo masses per query (0: 2^16; a power of two).  Device pointers. */
+ * memo masses per query (0: 2^16; a power of two).  fuse: both bounds'
+ * values computed inside the replay, in dense per-mass slots (allowed when
+ * every alphabet has <= 64 kept rows; 0: the separate value passes).
+ * Device pointers. */
 #define SST_MAX_ROWS 120
 #define SST_LB_HEAVY (-7)
 int sst_reach_rows_device(sst_table* t, const uint64_t* d_alpha, const int64_t* d_words, const uint64_t* d_off,
@@ -744,7 +747,7 @@ int sst_length_bounds_reach_device(sst_table* t, const double* d_su, const doubl
                                    const int64_t* d_reach_words, int64_t n, double tol, double prec, int max_len,
                                    int64_t max_mods, int64_t* d_lower, int64_t* d_upper, int8_t* d_status,
                                    const int32_t* d_qlen, const int32_t* d_caps_len, const int32_t* d_a0_len,
-                                   uint64_t* d_nodes, int64_t soft_nodes, uint32_t memo_first);
+                                   uint64_t* d_nodes, int64_t soft_nodes, uint32_t memo_first, int fuse);
 
 /* ---- CPython set order (the skeleton walk's emulation, sst_pyset.h) ---- */
 /* hash(tuple) of a tuple whose items hash to item_hashes[0..n) (CPython

@@ -253,7 +253,7 @@ def load_library(path=LIB_PATH):
     lib.sst_reach_rows_device.argtypes = [_P, _P, _P, _P, _I64, _P]
     lib.sst_reach_rows_device.restype = _I
     lib.sst_length_bounds_reach_device.argtypes = [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _D, _D, _I, _I64, _P, _P, _P,
-                                                   _P, _P, _P, _P, _I64, ctypes.c_uint32]
+                                                   _P, _P, _P, _P, _I64, ctypes.c_uint32, _I]
     lib.sst_length_bounds_reach_device.restype = _I
     lib.sst_jaccard_device.argtypes = [_P, ctypes.POINTER(JaccardArgs)]
     lib.sst_jaccard_device.restype = _I

@@ -2915,7 +2915,7 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
                                               int max_len, int64_t max_mods, int64_t* d_lower, int64_t* d_upper,
                                               int8_t* d_status, const int32_t* d_qlen, const int32_t* d_caps_len,
                                               const int32_t* d_a0_len, uint64_t* d_nodes, int64_t soft_nodes,
-                                              uint32_t memo_first) {
+                                              uint32_t memo_first, int fuse) {
   if (!t || n < 0 || n > INT32_MAX || max_len < 0 || max_len > 120 || (d_qlen && (!d_caps_len || !d_a0_len)) ||
       (n > 0 && (!d_su || !d_obs || !d_spec || !d_alpha || !d_reach_bits || !d_reach_off || !d_reach_words ||
                  !d_lower || !d_upper || !d_status)))
@@ -2955,7 +2955,7 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   q.caps_len = d_caps_len;
   q.a0_len = d_a0_len;
   q.nodes_out = d_nodes;
-  q.fuse = 1;
+  q.fuse = fuse ? 1 : 0;  // the caller checks every alphabet has <= 64 kept rows
   if (soft_nodes > 0) {
     q.node_budget = (uint64_t)soft_nodes;
     q.soft = 1;
@@ -2972,7 +2972,9 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   // memo per wave: 2^16 masses on the first try (most spectra), 8x per retry
   // for the queries that ran out; the waves in flight are what the
   // workspace budget allows at that size (a retry keeps its parallelism)
-  const size_t per_entry = hash_entry_bytes() + 2 * kMaxRows;  // two value slices (q.fuse)
+  // per memo slot: the hash entry, plus (fused) 2 x 64 value bytes per
+  // inserted mass at load factor 1/4, or (not fused) 120 value bytes per slot
+  const size_t per_entry = hash_entry_bytes() + (fuse ? 2 * 64 / 4 : kMaxRows);
   uint32_t cap = memo_first ? std::max<uint32_t>(memo_first, 64) : kLBHashCap0;
   auto units_for = [&](uint32_t n_q) {
     const size_t by_mem = kReachMemoBytes / ((size_t)cap * per_entry);
@@ -2981,7 +2983,8 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   int units = units_for(n_exact);
   while (n_exact) {
     DevBuf hash, vals, frames;
-    if (!hash.ensure((size_t)units * cap * hash_entry_bytes()) || !vals.ensure((size_t)units * cap * 2 * kMaxRows) ||
+    if (!hash.ensure((size_t)units * cap * hash_entry_bytes()) ||
+        !vals.ensure(fuse ? (size_t)units * (cap / 4) * 2 * 64 : (size_t)units * cap * kMaxRows) ||
         !frames.ensure((size_t)units * lb_frame_bytes()))
       return fail(c, SST_E_NOMEM, "device allocation failed (length-bound memo)");
     HIP_OK(c, hipMemsetAsync(hash.p, 0, hash.bytes, c->stream));

@@ -593,6 +593,7 @@ struct ReachView {
   const uint32_t* bits;  // R_k at bits + k * W
   int64_t W;             // words per row: masses [0, 32 W)
   int K;
+  M128 kept;             // the kept rows (row 0 excluded)
   int row0, row1, w0, w1;
   int rank0, rank1;
 };
@@ -619,6 +620,7 @@ struct Hash {
   int8_t* vals_lo = nullptr;
   int8_t* vals_hi = nullptr;
   int dflt_lo = 0;
+  bool dense = false;  // fused values: entry i's values at slot pad (its insertion order) x kValSlots + kept rank
   __device__ __forceinline__ uint32_t slot(uint32_t m) const { return (m * 0x9E3779B1u) & mask; }
   // returns entry pointer or nullptr if absent
   __device__ __forceinline__ HEntry* find(uint32_t m) const {
@@ -643,7 +645,7 @@ struct Hash {
         ++used;
         e[i].key = key;
         e[i].meta = 0xFFFFu;
-        e[i].pad = 0;
+        e[i].pad = dense ? used - 1 : 0;
         e[i].en0 = 0;
         e[i].en1 = 0;
         return &e[i];
@@ -1216,23 +1218,27 @@ __device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, Ha
 // (lb_values_wave's recurrence, one frame at a time): row r's value combines
 // the default, the row below (the up chain; the entry's earlier rows are
 // final) and, when its left branch was enabled at the first visit, the
-// child's value at row r plus one.
+// child's value at row r plus one.  Values are kept for the alphabet's rows
+// only, at slot kept-rank (a dropped row's value is the nearest kept row's
+// below it), per entry in insertion order: 2 x kValSlots bytes per mass.
+constexpr int kValSlots = 64;  // kept rows a fused replay holds (the caller checks K <= 64)
 __device__ __forceinline__ void p1_values(const TableArgs& t, const Lds& s, const Hash& h, const HEntry* e, uint32_t m,
                                           int rlo, int rtop) {
   const int lane = threadIdx.x & 63;
   const int lo = (int)((e->meta >> 16) & 0xFF);
   const M128 en{e->en0, e->en1};
   int cl[2] = {127, 127}, ch[2] = {-128, -128};
+  int rk[2] = {h.rv.rank0, h.rv.rank1};
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int r = lane + 64 * half;
-    if (r < t.n_rows && r >= rlo && r <= rtop && mtest(en, r)) {
+    if (r < t.n_rows && r >= rlo && r <= rtop && mtest(en, r)) {  // enabled rows are kept rows
       const uint32_t c = m - (uint32_t)s.w[r];
       int vl = 0, vh = 0;  // total_mass == 0 -> 0 (mass_table.py:378-379)
       if (c != 0) {
         const HEntry* ce = h.find(c);
         if (ce) {
-          const size_t at = (size_t)(ce - h.e) * kMaxRows + r;
+          const size_t at = (size_t)ce->pad * kValSlots + rk[half];
           vl = h.vals_lo[at];
           vh = h.vals_hi[at];
         }
@@ -1241,17 +1247,23 @@ __device__ __forceinline__ void p1_values(const TableArgs& t, const Lds& s, cons
       ch[half] = vh + 1;
     }
   }
-  const size_t base = (size_t)(e - h.e) * kMaxRows;
-  const int seed_lo = rlo > lo ? h.vals_lo[base + rlo - 1] : h.dflt_lo;
-  const int seed_hi = rlo > lo ? h.vals_hi[base + rlo - 1] : -1;
+  const size_t base = (size_t)e->pad * kValSlots;
+  // the seed: the value at row rlo - 1, i.e. at the highest kept row below rlo (if >= lo)
+  const uint64_t below0 = rlo >= 64 ? ~0ull : ((1ull << rlo) - 1ull);
+  const uint64_t below1 = rlo <= 64 ? 0ull : (rlo >= 128 ? ~0ull : ((1ull << (rlo - 64)) - 1ull));
+  const M128 keptm = h.rv.kept;
+  const int nb = __builtin_popcountll(keptm.a & below0) + __builtin_popcountll(keptm.b & below1);
+  const bool has_seed = rlo > lo && nb > 0;  // lo is a kept row: rows in [lo, rlo) hold a kept one
+  const int seed_lo = has_seed ? h.vals_lo[base + nb - 1] : h.dflt_lo;
+  const int seed_hi = has_seed ? h.vals_hi[base + nb - 1] : -1;
   const int l0 = lb_scan(0, cl[0]), l1 = lb_combine(0, lb_scan(0, cl[1]), __shfl(l0, 63, 64));
   const int u0 = lb_scan(1, ch[0]), u1 = lb_combine(1, lb_scan(1, ch[1]), __shfl(u0, 63, 64));
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int r = lane + 64 * half;
-    if (r < kMaxRows && r >= rlo && r <= rtop) {
-      h.vals_lo[base + r] = (int8_t)lb_combine(0, seed_lo, half ? l1 : l0);
-      h.vals_hi[base + r] = (int8_t)lb_combine(1, seed_hi, half ? u1 : u0);
+    if (r < t.n_rows && r >= rlo && r <= rtop && rk[half] >= 0) {
+      h.vals_lo[base + rk[half]] = (int8_t)lb_combine(0, seed_lo, half ? l1 : l0);
+      h.vals_hi[base + rk[half]] = (int8_t)lb_combine(1, seed_hi, half ? u1 : u0);
     }
   }
 }
@@ -3037,11 +3049,12 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
   h.e = (HEntry*)(hash + (size_t)gid * hash_cap * sizeof(HEntry));
   h.mask = hash_cap - 1;
   h.limit = hash_cap / 4;  // load factor <= 1/4: a wave waits for its longest probe chain
-  const bool fuse = WAVE && q.fuse;  // both bounds' values in phase 1 (two value slices per wave)
-  int8_t* lv = vals + (size_t)gid * hash_cap * kMaxRows * (fuse ? 2 : 1);
+  const bool fuse = WAVE && q.fuse;  // both bounds' values in phase 1 (two dense value slices per wave)
+  int8_t* lv = fuse ? vals + (size_t)gid * (hash_cap / 4) * kValSlots * 2 : vals + (size_t)gid * hash_cap * kMaxRows;
   if (fuse) {
     h.vals_lo = lv;
-    h.vals_hi = lv + (size_t)hash_cap * kMaxRows;
+    h.vals_hi = lv + (size_t)(hash_cap / 4) * kValSlots;
+    h.dense = true;
   }
   uint64_t epoch = 0;
   const int top = t.n_rows - 1;
@@ -3096,6 +3109,11 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
         h.rv.bits = q.reach_bits + q.reach_off[g];
         h.rv.W = q.reach_words[g];
         h.rv.K = n_lo + __builtin_popcountll(kept.b);
+        h.rv.kept = kept;
+        if (fuse && h.rv.K > kValSlots) {  // the dense value slots hold 64 kept rows: reported, not guessed
+          q.status[i] = SST_ABORTED;
+          continue;
+        }
         h.rv.row0 = lane < h.rv.K ? s_krow[lane] : 0;
         h.rv.row1 = lane + 64 < h.rv.K ? s_krow[lane + 64] : 0;
         h.rv.w0 = s.w[h.rv.row0];
@@ -3137,7 +3155,7 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
           rc = -3;
           break;
         }
-        const size_t at = (size_t)(e - h.e) * kMaxRows + top;
+        const size_t at = (size_t)e->pad * kValSlots + (h.rv.K - 1);  // the top row's value: the highest kept row's
         bl = lb_combine(0, bl, h.vals_lo[at]);
         bh = lb_combine(1, bh, h.vals_hi[at]);
       }

@@ -841,7 +841,7 @@ class DeviceLength:
 @_one_stream
 def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=64 << 30,
                   share_alphabets=True, length_chunk=1 << 30, spectra=None, soft_nodes=1 << 20,
-                  heavy_memo=1 << 20):
+                  heavy_memo=1 << 22):
     """Stage 5: each spectrum's skeleton alphabet (the canonical rows and the
     modifications its START / END skeletons name), both length bounds on it
     (sst_reach_rows_device + sst_length_bounds_reach_device: the reduced
@@ -962,7 +962,7 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
                     bits.data_ptr(), o_t.data_ptr(), w_t.data_ptr(), s1 - s0, float(tol), float(prec), ml_hi,
                     a0_len[ml_hi], lo_t.data_ptr() + 8 * s0, up_t.data_ptr() + 8 * s0, st_t.data_ptr() + s0,
                     ql_t.data_ptr() + 4 * s0, caps_t.data_ptr(), a0_t.data_ptr(), nd_t.data_ptr() + 8 * s0,
-                    int(soft_nodes), int(memo_first)), "sst_length_bounds_reach_device")
+                    int(soft_nodes), int(memo_first), int(K_u.max() <= 64)), "sst_length_bounds_reach_device")
             if beat is not None:
                 beat.stop()
             idx = members[order]
