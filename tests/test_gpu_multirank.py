@@ -77,6 +77,7 @@ def test_two_rank_gathered_step_vs_oracle(tmp_path):
             assert candidates(pay, cnt, off, i) == sols, (r, i)
 
 
+@pytest.mark.timeout(600)  # three pipeline runs (two ranks, then each rank alone)
 def test_two_rank_pipeline_outcomes_vs_single_rank(tmp_path):
     """Config 5 sharded: tools/pipeline_bench.py as two ranks on GPU 0 (gloo),
     every stage device-resident through the skeleton walk and the length
@@ -88,14 +89,15 @@ def test_two_rank_pipeline_outcomes_vs_single_rank(tmp_path):
     env = dict(os.environ, SST_DEVICE="0", MASTER_ADDR="127.0.0.1")
     bench = os.path.join(REPO, "tools", "pipeline_bench.py")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), bench, "--spectra", "400", "--backend", "gloo",
+           "127.0.0.1", "--master-port", str(_free_port()), bench, "--spectra", "400", "--warmup-spectra", "16", "--length-spectra", "48", "--backend", "gloo",
            "--dump-outcomes", multi]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=REPO)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
     assert '"n_gpus": 2' in line and '"gather"' in line
     for r in range(2):
-        p = subprocess.run([sys.executable, bench, "--spectra", "400", "--as-rank", str(r), "--dump-outcomes", single],
+        p = subprocess.run([sys.executable, bench, "--spectra", "400", "--warmup-spectra", "16", "--length-spectra", "48",
+                            "--as-rank", str(r), "--dump-outcomes", single],
                            env=dict(os.environ, SST_DEVICE="0"), capture_output=True, text=True, timeout=250,
                            cwd=REPO)
         assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
