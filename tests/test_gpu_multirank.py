@@ -86,7 +86,8 @@ def test_two_rank_pipeline_outcomes_vs_single_rank(tmp_path):
     from spectrseqtools_amd.pipeline_device import unpack_outcomes
 
     multi, single = str(tmp_path / "multi"), str(tmp_path / "single")
-    env = dict(os.environ, SST_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    env = dict(os.environ, SST_DEVICE="0", MASTER_ADDR="127.0.0.1",
+               PYTHONHASHSEED="0")  # the walk orders explanations as CPython sets do: one seed for all runs
     bench = os.path.join(REPO, "tools", "pipeline_bench.py")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), bench, "--spectra", "400", "--warmup-spectra", "16", "--length-spectra", "48", "--backend", "gloo",
@@ -98,7 +99,7 @@ def test_two_rank_pipeline_outcomes_vs_single_rank(tmp_path):
     for r in range(2):
         p = subprocess.run([sys.executable, bench, "--spectra", "400", "--warmup-spectra", "16", "--length-spectra", "48",
                             "--as-rank", str(r), "--dump-outcomes", single],
-                           env=dict(os.environ, SST_DEVICE="0"), capture_output=True, text=True, timeout=250,
+                           env=dict(os.environ, SST_DEVICE="0", PYTHONHASHSEED="0"), capture_output=True, text=True, timeout=250,
                            cwd=REPO)
         assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
         got = np.load(os.path.join(multi, f"outcome_rank{r}.npy"))
