@@ -12,7 +12,11 @@ step() {  # step NAME TIMEOUT CMD...
   if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+( while sleep 50; do date +%s >> gpurun_out/${TAG}_heartbeat.log; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 step gputests 900 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 170 --timeout-method thread --durations=12
+kill $HB 2>/dev/null
 export SST_PIPE_PROGRESS=1
 step pipeprof 420 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_pipeprof -o trace -- python3 tools/pipeline_bench.py --spectra 100000 --warmup-spectra 64 --length-spectra 256
 find gpurun_out/${TAG}_pipeprof -name "*kernel_stats.csv" -exec cp {} gpurun_out/${TAG}_pipe_kernel_stats.csv \;
