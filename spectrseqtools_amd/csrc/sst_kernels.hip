@@ -602,6 +602,7 @@ __device__ __forceinline__ bool reach_bit(const ReachView& rv, int k, int64_t x)
   return (rv.bits[(int64_t)k * rv.W + (x >> 5)] >> (x & 31)) & 1u;
 }
 
+constexpr int kValSlots = 64;  // kept rows a fused replay holds (the caller checks K <= 64)
 struct Hash {
   HEntry* e;
   uint32_t mask;  // capacity - 1
@@ -1180,6 +1181,11 @@ __device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, Ha
         if (r <= hv) {
           const int nec = (int)((meta >> 8) & 0xFF);
           if (nec != 0xFF && r >= nec) nrow = nrow < r ? nrow : r;
+          if (h.vals_lo) {  // fused values: this final child's values are read when the frame completes
+            const int rk = half ? h.rv.rank1 : h.rv.rank0;
+            const size_t at = (size_t)ce->pad * kValSlots + (rk < 0 ? 0 : rk);
+            h.sink ^= (uint64_t)h.vals_lo[at] ^ ((uint64_t)h.vals_hi[at] << 8);
+          }
         } else {
           desc[half] = true;
         }
@@ -1221,7 +1227,6 @@ __device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, Ha
 // child's value at row r plus one.  Values are kept for the alphabet's rows
 // only, at slot kept-rank (a dropped row's value is the nearest kept row's
 // below it), per entry in insertion order: 2 x kValSlots bytes per mass.
-constexpr int kValSlots = 64;  // kept rows a fused replay holds (the caller checks K <= 64)
 __device__ __forceinline__ void p1_values(const TableArgs& t, const Lds& s, const Hash& h, const HEntry* e, uint32_t m,
                                           int rlo, int rtop) {
   const int lane = threadIdx.x & 63;
