@@ -2906,7 +2906,7 @@ extern "C" int sst_reach_rows_device(sst_table* t, const uint64_t* d_alpha, cons
 // replay waves in flight for the reach-mode bounds (16 per CU: the DFS is
 // latency-bound, one query per wave; memo 2^16 entries each on the first try)
 constexpr uint32_t kReachUnits = 4096;
-constexpr size_t kReachMemoBytes = 48ull << 30;  // the replay's memo workspace per launch (HBM: 288 GB)
+constexpr size_t kReachMemoBytes = 96ull << 30;  // the replay's memo workspace per launch (HBM: 288 GB)
 
 extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, const double* d_obs,
                                               const int32_t* d_spec, const uint64_t* d_alpha,
