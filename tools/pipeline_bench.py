@@ -67,6 +67,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spectra", type=int, default=100000, help="spectra per GPU")
     ap.add_argument("--warmup-spectra", type=int, default=256, help="untimed warm-up spectra (all stages)")
+    ap.add_argument("--length-soft-nodes", type=int, default=1 << 20,
+                    help="stage 5's light pass: replays over this many nodes are deferred to the heavy pass")
     ap.add_argument("--length-spectra", type=int, default=2048,
                     help="stage 5's length bounds on this many spectra of the rank (0: all); the reference's "
                          "memoised DFS visits up to ~10^7 nodes per spectrum on rich skeleton alphabets")
@@ -269,7 +271,8 @@ def main():
         t0 = time.perf_counter()
         n_len = len(max_len) if args.length_spectra <= 0 else min(args.length_spectra, len(max_len))
         ln = pd.length_device(dp, sk, db.alpha_dev, su_seq, batch.seq_mass,
-                              spectra=None if n_len == len(max_len) else np.arange(n_len))
+                              spectra=None if n_len == len(max_len) else np.arange(n_len),
+                              soft_nodes=args.length_soft_nodes)
         barrier()
         stages["length"] = {"s": tmax(time.perf_counter() - t0), "bounds_spectra": n_len,
                             "bounds_sample": n_len < len(max_len), "reach_batches": ln.reach_batches,
