@@ -917,12 +917,21 @@ __device__ __forceinline__ void shallow_window(const TableArgs& t, const Lds& s,
 // min (dir 0) / max (dir 1) of the length bound's values, and its prefix over the 64 lanes
 __device__ __forceinline__ int lb_combine(int dir, int x, int y) { return dir ? (x > y ? x : y) : (x < y ? x : y); }
 __device__ __forceinline__ int lb_scan(int dir, int x) {  // inclusive prefix combine over the 64 lanes
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int y = __shfl_up(x, off, 64);
-    if (lane >= off) x = lb_combine(dir, x, y);
+  // DPP: row_shr 1, 2, 4, 8 inside each 16-lane row, then row_bcast 15 / 31
+  // across rows; lanes whose source is out of range read the identity
+  const int id = dir ? -128 : 127;
+#define SST_SCAN_STEP(ctrl, rmask)                                                 \
+  {                                                                                \
+    const int t = __builtin_amdgcn_update_dpp(id, x, ctrl, rmask, 0xF, false);     \
+    x = lb_combine(dir, x, t);                                                     \
   }
+  SST_SCAN_STEP(0x111, 0xF)
+  SST_SCAN_STEP(0x112, 0xF)
+  SST_SCAN_STEP(0x114, 0xF)
+  SST_SCAN_STEP(0x118, 0xF)
+  SST_SCAN_STEP(0x142, 0xA)
+  SST_SCAN_STEP(0x143, 0xC)
+#undef SST_SCAN_STEP
   return x;
 }
 
