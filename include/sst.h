@@ -749,6 +749,46 @@ int sst_length_bounds_reach_device(sst_table* t, const double* d_su, const doubl
                                    const int32_t* d_qlen, const int32_t* d_caps_len, const int32_t* d_a0_len,
                                    uint64_t* d_nodes, int64_t soft_nodes, uint32_t memo_first, int fuse);
 
+/* The same bounds WITHOUT replaying the DFS (sst_frontier.hip, DESIGN §3
+ * "first-visit frontier"): the reference's memo is keyed by (mass, row) and
+ * ignores the budgets, so each node's memoised value is fixed by its first
+ * visit; which visit comes first is the lexicographic minimum over the node's
+ * up and left parents (mass_table.py:373-457: up before left, window values
+ * ascending), computed in bands of the lightest row mass over descending
+ * masses, then the values by a DP over ascending masses.  Same result as the
+ * replay for every query, in time linear in the memo's size and independent of
+ * any one spectrum's depth.
+ * sst_reach_lowest_device first turns sst_reach_rows_device's bitsets into one
+ * byte per mass: d_lr[d_lr_off[g] + m] = the lowest kept rank k with m in
+ * R_k (0xFF: none), m < 32 d_words[g] (d_lr_off[g] a multiple of 32).
+ * sst_length_bounds_frontier_device: arguments as sst_length_bounds_reach_device
+ * (d_lr / d_lr_off instead of the bitsets); d_nodes (may be NULL; zeroed by the
+ * caller) = per query, the memo entries (distinct (mass, row) nodes) its DFS
+ * creates.  workspace_bytes: the device workspace (0: half the free memory, at
+ * most 48 GB); queries are processed in chunks that fit it (a chunk that
+ * overflows is split; a single query beyond the workspace gets SST_ABORTED).
+ * stats may be NULL. */
+typedef struct sst_lbf_stats {
+  int64_t live;            /* queries the list pass handed to the frontier */
+  int64_t nodes;           /* memo entries created */
+  int64_t chunks;          /* chunks run to completion */
+  int64_t splits;          /* chunks that overflowed the workspace and were split */
+  int64_t aborted;         /* single queries beyond the workspace (SST_ABORTED) */
+  int64_t bands;           /* mass bands of the largest chunk */
+  int64_t key_words;       /* 64-bit words per first-visit key (4, 8 or 16) */
+  int64_t max_band_groups; /* (query, mass) groups of the fullest band */
+  int64_t table_slots;     /* slots per hash table of the ring */
+  int64_t node_cap;        /* node capacity per chunk */
+} sst_lbf_stats;
+int sst_reach_lowest_device(sst_table* t, const uint64_t* d_alpha, const int64_t* d_words, const uint64_t* d_off,
+                            int64_t n_spec, const uint32_t* d_bits, const uint64_t* d_lr_off, uint8_t* d_lr);
+int sst_length_bounds_frontier_device(sst_table* t, const double* d_su, const double* d_obs, const int32_t* d_spec,
+                                      const uint64_t* d_alpha, const uint8_t* d_lr, const uint64_t* d_lr_off, int64_t n,
+                                      double tol, double prec, int max_len, int64_t max_mods, int64_t* d_lower,
+                                      int64_t* d_upper, int8_t* d_status, const int32_t* d_qlen,
+                                      const int32_t* d_caps_len, const int32_t* d_a0_len, uint64_t* d_nodes,
+                                      uint64_t workspace_bytes, sst_lbf_stats* stats);
+
 /* ---- CPython set order (the skeleton walk's emulation, sst_pyset.h) ---- */
 /* hash(tuple) of a tuple whose items hash to item_hashes[0..n) (CPython
  * 3.8+ tuplehash, 64-bit): the hash of an explanation's name tuple

@@ -36,7 +36,8 @@ EXPORTS = (
     "sst_py_tuple_hash", "sst_pyset_order", "sst_pyset_table_size", "sst_walk_scratch_bytes",
     "sst_skel_walk_device", "sst_result_refs_device", "sst_dict_count_device", "sst_dict_build_device",
     "sst_reach_rows_device", "sst_length_bounds_reach_device", "sst_jaccard_device", "sst_skeleton_alpha_device",
-    "sst_dict_list_device", "sst_fix_finish_device", "sst_pipe_reserve_rows",
+    "sst_dict_list_device", "sst_fix_finish_device", "sst_pipe_reserve_rows", "sst_reach_lowest_device",
+    "sst_length_bounds_frontier_device",
 )
 
 # kernel ids of sst_profile_read
@@ -80,6 +81,15 @@ class ExactIO(ctypes.Structure):
                 ("xq_spec", ctypes.c_void_p), ("xq_single", ctypes.c_void_p), ("xq_count", ctypes.c_void_p),
                 ("xq_cap", ctypes.c_uint64), ("xq_block", ctypes.c_void_p), ("xa_st", ctypes.c_void_p),
                 ("xa_n", ctypes.c_void_p), ("xa_ptr", ctypes.c_void_p)]
+
+
+class LbfStats(ctypes.Structure):
+    """sst_lbf_stats (include/sst.h): the first-visit frontier's record."""
+    _fields_ = [(n, ctypes.c_int64) for n in ("live", "nodes", "chunks", "splits", "aborted", "bands", "key_words",
+                                             "max_band_groups", "table_slots", "node_cap")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
 class JaccardArgs(ctypes.Structure):
@@ -255,6 +265,11 @@ def load_library(path=LIB_PATH):
     lib.sst_length_bounds_reach_device.argtypes = [_P, _P, _P, _P, _P, _P, _P, _P, _I64, _D, _D, _I, _I64, _P, _P, _P,
                                                    _P, _P, _P, _P, _I64, ctypes.c_uint32, _I]
     lib.sst_length_bounds_reach_device.restype = _I
+    lib.sst_reach_lowest_device.argtypes = [_P, _P, _P, _P, _I64, _P, _P, _P]
+    lib.sst_reach_lowest_device.restype = _I
+    lib.sst_length_bounds_frontier_device.argtypes = [_P, _P, _P, _P, _P, _P, _P, _I64, _D, _D, _I, _I64, _P, _P,
+                                                      _P, _P, _P, _P, _P, _U64, ctypes.POINTER(LbfStats)]
+    lib.sst_length_bounds_frontier_device.restype = _I
     lib.sst_jaccard_device.argtypes = [_P, ctypes.POINTER(JaccardArgs)]
     lib.sst_jaccard_device.restype = _I
     lib.sst_skeleton_alpha_device.argtypes = [_P, _I64, _P, _P, _P, _P, _P]

@@ -3014,6 +3014,227 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   return SST_OK;
 }
 
+// ---- the first-visit frontier (sst_frontier.hip) ---------------------------
+extern "C" int sst_reach_lowest_device(sst_table* t, const uint64_t* d_alpha, const int64_t* d_words,
+                                       const uint64_t* d_off, int64_t n_spec, const uint32_t* d_bits,
+                                       const uint64_t* d_lr_off, uint8_t* d_lr) {
+  if (!t || n_spec < 0 || (n_spec > 0 && (!d_alpha || !d_words || !d_off || !d_bits || !d_lr_off || !d_lr)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  sst::ReachArgs a{d_alpha, d_words, d_off, const_cast<uint32_t*>(d_bits), t->args.w, t->n_rows, n_spec};
+  Prof p(c, SST_K_REACH_ROWS);
+  HIP_OK(c, sst::launch_reach_lowest(a, d_lr_off, d_lr, c->stream));
+  return SST_OK;
+}
+
+namespace {
+int bits_for(uint64_t x) {  // bits needed to hold 0..x
+  int b = 0;
+  while (b < 64 && (x >> b)) ++b;
+  return b;
+}
+uint64_t pow2_floor(uint64_t x) {
+  uint64_t p = 1;
+  while (p <= x / 2) p <<= 1;
+  return p;
+}
+}  // namespace
+
+extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_su, const double* d_obs,
+                                                 const int32_t* d_spec, const uint64_t* d_alpha, const uint8_t* d_lr,
+                                                 const uint64_t* d_lr_off, int64_t n, double tol, double prec,
+                                                 int max_len, int64_t max_mods, int64_t* d_lower, int64_t* d_upper,
+                                                 int8_t* d_status, const int32_t* d_qlen, const int32_t* d_caps_len,
+                                                 const int32_t* d_a0_len, uint64_t* d_nodes, uint64_t workspace_bytes,
+                                                 sst_lbf_stats* stats) {
+  if (!t || n < 0 || n > INT32_MAX || max_len < 0 || (d_qlen && (!d_caps_len || !d_a0_len)) ||
+      (n > 0 && (!d_su || !d_obs || !d_spec || !d_alpha || !d_lr || !d_lr_off || !d_lower || !d_upper || !d_status)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  if (stats) *stats = sst_lbf_stats{};
+  if (n == 0) return SST_OK;
+  for (int r = 1; r < t->n_rows; ++r)
+    if (t->masses[r] >= (1 << 20)) return fail(c, SST_E_ARG, "length bounds (frontier): a row mass of 2^20 or more");
+  const int wb = (int)t->args.w_min;
+  int64_t w_max = 0;
+  for (int r = 1; r < t->n_rows; ++r) w_max = std::max<int64_t>(w_max, t->masses[r]);
+  if (wb < 1) return fail(c, SST_E_ARG, "length bounds (frontier): no row mass");
+  const int jump = (int)((w_max + wb - 1) / wb);  // bands one left move can cross
+  int ring = 1;
+  while (ring <= jump) ring <<= 1;
+  if (ring > 8) return fail(c, SST_E_ARG, "length bounds (frontier): row masses span more than 7 bands");
+  const size_t nn = (size_t)n;
+  DevBuf d_list, d_cnt;
+  if (!d_list.ensure(nn * 4) || !d_cnt.ensure(4)) return fail(c, SST_E_NOMEM, "device allocation failed (length bound)");
+  HIP_OK(c, hipMemsetAsync(d_cnt.p, 0, 4, c->stream));
+  // the list pass: windows, the reduced table's extent (SST_OUT_OF_TABLE /
+  // SST_ABORTED in its last word), empty windows; every live query listed
+  LBArgs q{};
+  q.su = d_su;
+  q.obs = d_obs;
+  q.n = n;
+  q.tol = tol;
+  q.prec = prec;
+  q.rprec = 1.0 / prec;
+  q.A0 = (int)std::max<int64_t>(0, std::min<int64_t>(max_mods, kInfBudget));
+  q.max_len = max_len;
+  q.out = d_lower;
+  q.status = d_status;
+  q.exact_list = (uint32_t*)d_list.p;
+  q.exact_count = (uint32_t*)d_cnt.p;
+  q.node_budget = kLBNodeBudget;
+  q.alpha = d_alpha;
+  q.spec = d_spec;
+  q.comp = (int)t->C;
+  uint32_t n_live = 0;
+  {
+    Prof p(c, SST_K_LENGTH_BOUND);
+    HIP_OK(c, launch_length_bound(t->args, q, nullptr, nullptr, nullptr, 0, 0, true, c->stream));
+  }
+  HIP_OK(c, hipMemcpyAsync(&n_live, d_cnt.p, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  if (stats) stats->live = n_live;
+  if (n_live == 0) return SST_OK;
+  // workspace: nodes 7 B each, per ring table S group slots (32 B + a 4-B list
+  // entry) and S candidate slots (48 B with 256-bit keys); nodes = 8 S
+  size_t budget = workspace_bytes;
+  if (budget == 0) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+      (void)hipGetLastError();
+      fr = 16ull << 30;
+    }
+    budget = std::min<size_t>(48ull << 30, fr / 2);
+  }
+  const size_t per_slot = 8 * 7 + (size_t)ring * (lbf_group_bytes() + 4 + lbf_cand_bytes(4));
+  uint64_t S = pow2_floor(std::max<size_t>(1024, budget / per_slot));
+  if (S > (1ull << 31)) S = 1ull << 31;
+  const uint64_t ncap = std::min<uint64_t>(8 * S, 0xFFFFFFF0ull);
+  DevBuf flags, lchild, vlo, vhi, gtab, ctab, glist, ctl, bstart, bgroups, qi, qrow, roots;
+  if (!flags.ensure(ncap) || !lchild.ensure(ncap * 4) || !vlo.ensure(ncap) || !vhi.ensure(ncap) ||
+      !gtab.ensure((size_t)ring * S * lbf_group_bytes()) || !ctab.ensure((size_t)ring * S * lbf_cand_bytes(4)) ||
+      !glist.ensure((size_t)ring * S * 4) || !ctl.ensure(sizeof(FCtl)))
+    return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier workspace)");
+  constexpr uint32_t kChunkMax = 1u << 20;  // the keys' query field
+  std::vector<std::pair<uint32_t, uint32_t>> todo;
+  for (uint32_t c0 = 0; c0 < n_live; c0 += kChunkMax) todo.push_back({c0, std::min(n_live, c0 + kChunkMax)});
+  std::reverse(todo.begin(), todo.end());
+  std::vector<uint32_t> band_groups;
+  while (!todo.empty()) {
+    const auto [c0, c1] = todo.back();
+    todo.pop_back();
+    const uint32_t nc = c1 - c0;
+    FrontierArgs a{};
+    a.list = (const uint32_t*)d_list.p;
+    a.chunk0 = c0;
+    a.n_chunk = nc;
+    a.su = d_su;
+    a.obs = d_obs;
+    a.tol = tol;
+    a.prec = prec;
+    a.rprec = 1.0 / prec;
+    a.spec = d_spec;
+    a.alpha = d_alpha;
+    a.lr = d_lr;
+    a.lr_off = d_lr_off;
+    a.qlen = d_qlen;
+    a.caps_len = d_caps_len;
+    a.a0_len = d_a0_len;
+    a.A0 = q.A0;
+    a.max_len = max_len;
+    a.wb = wb;
+    a.ring = ring;
+    a.jump = jump;
+    a.lower = d_lower;
+    a.upper = d_upper;
+    a.status = d_status;
+    a.nodes_out = d_nodes;
+    if (!qi.ensure((size_t)nc * sizeof(FQInfo)) || !qrow.ensure((size_t)nc * 128 * 4))
+      return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier queries)");
+    a.qi = (FQInfo*)qi.p;
+    a.qrow = (uint32_t*)qrow.p;
+    a.ctl = (FCtl*)ctl.p;
+    HIP_OK(c, hipMemsetAsync(ctl.p, 0, sizeof(FCtl), c->stream));
+    {
+      Prof p(c, SST_K_LENGTH_BOUND);
+      HIP_OK(c, launch_lbf_setup(t->args, a, c->stream));
+    }
+    FCtl h{};
+    HIP_OK(c, hipMemcpyAsync(&h, ctl.p, sizeof(FCtl), hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    const int n_bands = h.max_hi >= 1 ? (int)h.max_band + 1 : 0;
+    if (n_bands > 4094) return fail(c, SST_E_ARG, "length bounds (frontier): a window beyond 4094 bands");
+    if (h.max_hi >= (1ull << 25)) return fail(c, SST_E_ARG, "length bounds (frontier): a window at 2^25 or beyond");
+    a.rb = bits_for(h.max_win > 0 ? h.max_win - 1 : 0);
+    a.cb = std::max(1, bits_for(h.max_hi / (uint64_t)wb));
+    const int need = a.rb + (int)h.max_k * a.cb;
+    const int kw = need <= 256 ? 4 : need <= 512 ? 8 : need <= 1024 ? 16 : 0;
+    if (!kw || a.rb > 32) return fail(c, SST_E_ARG, "length bounds (frontier): first-visit keys beyond 1024 bits");
+    a.rstride = (int)std::max<uint32_t>(1, h.max_win);
+    if (!roots.ensure((size_t)nc * a.rstride * 4))
+      return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier roots)");
+    a.root_node = (uint32_t*)roots.p;
+    a.flags = (uint8_t*)flags.p;
+    a.lchild = (uint32_t*)lchild.p;
+    a.vlo = (uint8_t*)vlo.p;
+    a.vhi = (int8_t*)vhi.p;
+    a.ncap = ncap;
+    a.gtab = (char*)gtab.p;
+    a.gmask = (uint32_t)(S - 1);
+    const uint64_t cslots = pow2_floor(ctab.bytes / ((size_t)ring * lbf_cand_bytes(kw)));
+    a.ctab = (char*)ctab.p;
+    a.cmask = (uint32_t)(cslots - 1);
+    a.glist = (uint32_t*)glist.p;
+    if (!bstart.ensure((size_t)(n_bands + 2) * 4) || !bgroups.ensure((size_t)(n_bands + 2) * 4))
+      return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier bands)");
+    a.band_start = (uint32_t*)bstart.p;
+    a.band_groups = (uint32_t*)bgroups.p;
+    HIP_OK(c, hipMemsetAsync(gtab.p, 0, gtab.bytes, c->stream));  // empty tables: tag 0 matches no band
+    HIP_OK(c, hipMemsetAsync(ctab.p, 0, ctab.bytes, c->stream));
+    {
+      Prof p(c, SST_K_LENGTH_BOUND);
+      HIP_OK(c, launch_lbf_sweep(a, kw, n_bands, c->n_cu * 8, c->stream));
+    }
+    HIP_OK(c, hipMemcpyAsync(&h, ctl.p, sizeof(FCtl), hipMemcpyDeviceToHost, c->stream));
+    band_groups.assign((size_t)n_bands, 0);
+    if (n_bands)
+      HIP_OK(c, hipMemcpyAsync(band_groups.data(), bgroups.p, (size_t)n_bands * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    if (h.overflow & 24u) return fail(c, SST_E_INTERNAL, "length bounds (frontier): inconsistent first-visit tables");
+    if (h.overflow) {
+      if (stats) stats->splits++;
+      if (nc == 1) {  // one query beyond the whole workspace: reported, not guessed
+        FQInfo one{};
+        HIP_OK(c, hipMemcpyAsync(&one, qi.p, sizeof(FQInfo), hipMemcpyDeviceToHost, c->stream));
+        HIP_OK(c, hipStreamSynchronize(c->stream));
+        const int8_t ab = SST_ABORTED;
+        HIP_OK(c, hipMemcpyAsync(d_status + one.i, &ab, 1, hipMemcpyHostToDevice, c->stream));
+        if (stats) stats->aborted++;
+        continue;
+      }
+      const uint32_t mid = c0 + nc / 2;
+      todo.push_back({mid, c1});
+      todo.push_back({c0, mid});
+      continue;
+    }
+    if (stats) {
+      stats->chunks++;
+      stats->nodes += h.node_ctr;
+      stats->bands = std::max<int64_t>(stats->bands, n_bands);
+      stats->key_words = std::max<int64_t>(stats->key_words, kw);
+      for (uint32_t x : band_groups) stats->max_band_groups = std::max<int64_t>(stats->max_band_groups, x);
+      stats->table_slots = (int64_t)S;
+      stats->node_cap = (int64_t)ncap;
+    }
+  }
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  return SST_OK;
+}
+
 extern "C" int sst_jaccard_device(sst_table* t, const sst_jaccard_args* a) {
   if (!t || !a || a->n_spec < 0) return SST_E_ARG;
   if (a->n_spec == 0) return SST_OK;

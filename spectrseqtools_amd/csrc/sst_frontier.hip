@@ -1,0 +1,610 @@
+// sst_frontier.hip -- compute_sequence_length_bound (mass_table.py:343-487)
+// on the skeleton's reduced alphabets, both directions, WITHOUT replaying the
+// reference's memoised DFS (gfx950).
+//
+// The reference walks backtrack(m, r, A, B) depth-first: memo check, up
+// branch (m, r-1) before left branch (m - w_r, r), one memo shared by every
+// window value (ascending).  The memo key (m, r) ignores the budgets (A, B), so
+// a node's memoised value is fixed by its FIRST visit's budgets -- the only
+// order-dependent thing in the whole computation.  That first visit is not a
+// property of the DFS order alone: it is the lexicographically smallest path
+//     (root index, c_{K-1}, c_{K-2}, ..., c_r)      c_s = left moves in row s
+// among the paths the DFS actually expands, and a node is expanded exactly
+// once, at its own first visit.  So
+//     FV(m, r) = lexmin( FV(m, r+1) . up,  FV(m + w_r, r) . left )
+// over the two possible parents (the up parent only if m is in R_{r-1}..R_r,
+// the left parent only if ITS first-visit budgets allow the move), a
+// recurrence over descending masses: a left parent is heavier by w_r >= w_min,
+// an up parent has the same mass.  Masses are therefore processed in bands of
+// w_min (every band depends only on earlier bands and, within a mass, on the
+// row above), one launch per band; the values (min / max path length, the
+// reference's defaults and its -1 + 1 = 0 quirk included) then follow by a DP
+// over ascending masses, one launch per band in reverse.  Nodes = the
+// reference's memo entries; no node is ever revisited.  DESIGN §3.
+//
+// Data (per chunk of queries, HBM):
+//   lr        per alphabet: byte per mass, the lowest kept rank k with the mass
+//             in R_k (0xFF: none) -- pair(k, m) != 0 <=> lr[m] <= k, bit0 <=>
+//             lr[m] <= k-1, bit1 <=> m - w_k == 0 or lr[m - w_k] <= k
+//   groups    one per (query, mass) with at least one visited row: hash ring
+//             of R tables (band mod R), 32-B entries {key, 128-bit rank mask
+//             of the left candidates}; each band's fresh groups listed
+//   cands     one per left edge (child (query, mass, rank)): hash ring, entry
+//             {key, parent node, child budgets A B, the child's FV key}
+//   nodes     ids allocated per group (ranks lo..hv ascending): flags, left
+//             child id, lower / upper value
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sst_internal.h"
+#include "sst_quant.h"
+
+namespace sst {
+
+namespace {
+
+constexpr int kProbeMax = 4096;
+constexpr uint32_t kRootBit = 0x80000000u;
+constexpr uint8_t kFLeft = 1, kFUp = 2, kFZero = 4;
+
+struct alignas(32) FGroup {
+  uint64_t key;
+  uint64_t mask[2];
+  uint64_t pad;
+};
+
+template <int KW>
+struct alignas(16) FCand {
+  uint64_t key;
+  uint32_t parent;
+  uint8_t A, B;
+  uint16_t pad;
+  uint64_t fk[KW];
+};
+
+__device__ __forceinline__ uint64_t fkey(uint32_t band, uint32_t j, uint32_t m, uint32_t k) {
+  return ((uint64_t)(band + 1) << 52) | ((uint64_t)j << 32) | ((uint64_t)m << 7) | (uint64_t)k;
+}
+__device__ __forceinline__ uint32_t ftag(uint64_t key) { return (uint32_t)(key >> 52); }
+__device__ __forceinline__ uint32_t fhash(uint64_t key, uint32_t mask) {
+  uint64_t x = key * 0x9E3779B97F4A7C15ull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 17) & mask;
+}
+
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const int o = __shfl_xor(v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_u(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(v, d, 64);
+    if (lane >= d) v += y;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int lane = threadIdx.x & 63;
+  return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+// find-or-insert (band-tagged; a slot whose tag is not this band's is free)
+__device__ __forceinline__ uint32_t group_get(FGroup* T, uint32_t mask, uint64_t key, bool& fresh) {
+  const uint32_t tag = ftag(key);
+  uint32_t h = fhash(key, mask);
+  for (int p = 0; p < kProbeMax; ++p) {
+    const uint64_t cur = __hip_atomic_load(&T[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) {
+      fresh = false;
+      return h;
+    }
+    if (ftag(cur) != tag) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&T[h].key, (unsigned long long)cur, (unsigned long long)key);
+      if (prev == cur) {
+        fresh = true;
+        return h;
+      }
+      if (prev == key) {
+        fresh = false;
+        return h;
+      }
+    }
+    h = (h + 1) & mask;
+  }
+  return UINT32_MAX;
+}
+
+// insert a key known to be new (a left edge has one parent)
+template <int KW>
+__device__ __forceinline__ uint32_t cand_put(FCand<KW>* T, uint32_t mask, uint64_t key) {
+  const uint32_t tag = ftag(key);
+  uint32_t h = fhash(key, mask);
+  for (int p = 0; p < kProbeMax; ++p) {
+    const uint64_t cur = __hip_atomic_load(&T[h].key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ftag(cur) != tag) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&T[h].key, (unsigned long long)cur, (unsigned long long)key);
+      if (prev == cur) return h;
+    }
+    h = (h + 1) & mask;
+  }
+  return UINT32_MAX;
+}
+
+template <int KW>
+__device__ __forceinline__ uint32_t cand_find(const FCand<KW>* T, uint32_t mask, uint64_t key) {
+  const uint32_t tag = ftag(key);
+  uint32_t h = fhash(key, mask);
+  for (int p = 0; p < kProbeMax; ++p) {
+    const uint64_t cur = T[h].key;
+    if (cur == key) return h;
+    if (ftag(cur) != tag) return UINT32_MAX;
+    h = (h + 1) & mask;
+  }
+  return UINT32_MAX;
+}
+
+// first-visit keys: a KW x 64-bit big-endian integer (word 0 most
+// significant): the root index in the top rb bits, then cb bits per kept
+// rank from the top rank down; lexicographic order of the reference's DFS
+template <int KW>
+__device__ __forceinline__ bool key_less(const uint64_t (&a)[KW], const uint64_t (&b)[KW]) {
+  bool lt = false, decided = false;
+#pragma unroll
+  for (int i = 0; i < KW; ++i) {
+    if (!decided && a[i] != b[i]) {
+      lt = a[i] < b[i];
+      decided = true;
+    }
+  }
+  return lt;
+}
+template <int KW>
+__device__ __forceinline__ void key_add_bit(uint64_t (&k)[KW], int p) {  // k += 2^p (p from the LSB)
+  const int wi = KW - 1 - (p >> 6);
+  const uint64_t add = 1ull << (p & 63);
+  uint64_t carry = 0;
+#pragma unroll
+  for (int i = KW - 1; i >= 0; --i) {
+    const uint64_t a = i == wi ? add : 0ull;
+    const uint64_t s = k[i] + a;
+    const uint64_t c1 = s < a;
+    const uint64_t s2 = s + carry;
+    const uint64_t c2 = s2 < carry;
+    k[i] = s2;
+    carry = c1 | c2;
+  }
+}
+
+__device__ __forceinline__ uint32_t qrow_w(uint32_t x) { return x & 0xFFFFFu; }
+__device__ __forceinline__ int qrow_cap(uint32_t x) { return (int)((x >> 20) & 0xFFu); }
+__device__ __forceinline__ bool qrow_mod(uint32_t x) { return (x >> 28) & 1u; }
+
+__device__ __forceinline__ void set_overflow(FrontierArgs& a, uint32_t why) { atomicOr(&a.ctl->overflow, why); }
+
+}  // namespace
+
+// per listed query (one wave each): its window, budgets, alphabet rank table
+__global__ __launch_bounds__(256) void k_lbf_setup(TableArgs t, FrontierArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t jj = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (jj >= a.n_chunk) return;
+  const uint32_t i = a.list[a.chunk0 + jj];
+  int64_t lo, hi;
+  quantise(a.su[i], a.tol * a.obs[i], false, a.tol, a.prec, a.rprec, lo, hi);  // mass_table.py:354-359
+  const uint32_t u = (uint32_t)a.spec[i];
+  const int L = a.qlen ? a.qlen[i] : a.max_len;
+  const int A0 = a.qlen ? a.a0_len[L] : a.A0;
+  const uint64_t top = t.n_rows >= 64 ? (t.n_rows - 64 >= 64 ? ~0ull : ((1ull << (t.n_rows - 64)) - 1ull)) : 0ull;
+  const uint64_t m0 = a.alpha[2 * u] & ~1ull & (t.n_rows >= 64 ? ~0ull : ((1ull << t.n_rows) - 1ull));
+  const uint64_t m1 = a.alpha[2 * u + 1] & top;
+  const int n_lo = __builtin_popcountll(m0);
+  const int K = n_lo + __builtin_popcountll(m1);
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const int r = lane + 64 * half;
+    const uint64_t mm = half ? m1 : m0;
+    if (r < t.n_rows && ((mm >> lane) & 1ull)) {
+      const int rank = (half ? n_lo : 0) + __builtin_popcountll(mm & ((1ull << lane) - 1ull));
+      int cap = a.qlen ? a.caps_len[(int64_t)L * kMaxRows + r] : t.cap[r];
+      cap = cap < 0 ? 0 : (cap > 255 ? 255 : cap);
+      a.qrow[(size_t)jj * 128 + rank] = (uint32_t)t.w[r] | ((uint32_t)cap << 20) | ((uint32_t)(t.mod[r] ? 1 : 0) << 28);
+    }
+  }
+  if (lane == 0) {
+    FQInfo q;
+    q.hi = hi;
+    q.lo = lo;
+    q.lr_off = a.lr_off[u];
+    q.i = i;
+    q.K = (uint16_t)K;
+    q.L = (uint16_t)(L > 65535 ? 65535 : L);
+    q.A0 = (uint16_t)(A0 < 0 ? 0 : (A0 > 255 ? 255 : A0));
+    a.qi[jj] = q;
+    if (hi >= 1) {
+      atomicMax(&a.ctl->max_band, (uint32_t)((hi - 1) / a.wb));
+      atomicMax((unsigned long long*)&a.ctl->max_hi, (unsigned long long)hi);
+    }
+    const int64_t win = hi - lo + 1;
+    atomicMax(&a.ctl->max_win, (uint32_t)(win < 1 ? 1 : (win > 0x7FFFFFFF ? 0x7FFFFFFF : win)));
+    atomicMax(&a.ctl->max_k, (uint32_t)K);
+  }
+}
+
+// the roots: window values v >= 1 in R_{K-1}, band 0, key (v - lo, 0, ...)
+template <int KW>
+__global__ __launch_bounds__(256) void k_lbf_roots(FrontierArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t jj = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = jj < a.n_chunk;
+  FQInfo q{};
+  int64_t win = 0;
+  if (act) {
+    q = a.qi[jj];
+    win = q.hi - q.lo + 1;
+    if (win < 0) win = 0;
+  }
+  const int steps = wave_max_i((int)win);
+  FGroup* G = (FGroup*)a.gtab;
+  FCand<KW>* C = (FCand<KW>*)a.ctab;
+  const int top = (int)q.K - 1;
+  const uint32_t rtop = act && top >= 0 ? a.qrow[(size_t)jj * 128 + top] : 0u;
+  for (int s = 0; s < steps; ++s) {
+    const int64_t v = q.lo + s;
+    bool pred = act && s < win && v >= 1 && top >= 0 && (int)a.lr[q.lr_off + v] <= top;
+    bool fresh = false;
+    uint32_t gs = 0;
+    if (pred) {
+      gs = group_get(G, a.gmask, fkey(0, jj, (uint32_t)v, 0), fresh);
+      if (gs == UINT32_MAX) {
+        set_overflow(a, 2);
+        pred = false;
+        fresh = false;
+      } else {
+        atomicOr((unsigned long long*)&G[gs].mask[top >> 6], 1ull << (top & 63));
+      }
+    }
+    const uint64_t bm = __ballot(fresh);
+    if (bm) {
+      const int leader = __builtin_ctzll(bm);
+      uint32_t b0 = 0;
+      if (lane == leader) b0 = atomicAdd(&a.ctl->list_cnt[0], (uint32_t)__builtin_popcountll(bm));
+      b0 = __shfl(b0, leader, 64);
+      if (fresh) {
+        const uint32_t at = b0 + (uint32_t)__builtin_popcountll(bm & lanemask_lt());
+        if (at > a.gmask) set_overflow(a, 4);
+        else a.glist[at] = gs;
+      }
+    }
+    if (pred) {
+      const uint32_t cs = cand_put<KW>(C, a.cmask, fkey(0, jj, (uint32_t)v, (uint32_t)top));
+      if (cs == UINT32_MAX) {
+        set_overflow(a, 2);
+      } else {
+        FCand<KW>& e = C[cs];
+        e.parent = kRootBit | (uint32_t)(jj * a.rstride + s);
+        e.A = (uint8_t)q.A0;
+        e.B = (uint8_t)qrow_cap(rtop);
+#pragma unroll
+        for (int w = 0; w < KW; ++w) e.fk[w] = 0;
+        if (a.rb > 0) e.fk[0] = (uint64_t)s << (64 - a.rb);
+      }
+    }
+  }
+}
+
+// band b: every group (query, mass) of the band walks its ranks hv .. lo,
+// choosing each node's first visit among its up and left candidates
+template <int KW>
+__global__ __launch_bounds__(256) void k_lbf_band(FrontierArgs a, int band) {
+  if (__hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t rmask = (uint32_t)a.ring - 1u;
+  const uint32_t slot = (uint32_t)band & rmask;
+  const uint32_t ng = a.ctl->list_cnt[slot];
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.band_groups[band] = ng;
+  const size_t gstride = (size_t)a.gmask + 1, cstride = (size_t)a.cmask + 1;
+  FGroup* G = (FGroup*)a.gtab + slot * gstride;
+  const FCand<KW>* Cb = (const FCand<KW>*)a.ctab + slot * cstride;
+  const uint32_t* Lst = a.glist + slot * gstride;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t base = wave * 64u; base < ng; base += nwaves * 64u) {
+    const uint32_t gi = base + lane;
+    const bool act = gi < ng;
+    uint32_t jj = 0, m = 0;
+    int hv = -1, lo = 0, n = 0;
+    uint64_t mk0 = 0, mk1 = 0;
+    FQInfo q{};
+    if (act) {
+      const uint32_t gs = Lst[gi];
+      const FGroup g = G[gs];
+      G[gs].mask[0] = 0;  // consumed: the slot's next band starts from empty masks
+      G[gs].mask[1] = 0;
+      jj = (uint32_t)(g.key >> 32) & 0xFFFFFu;
+      m = (uint32_t)(g.key >> 7) & 0x1FFFFFFu;
+      mk0 = g.mask[0];
+      mk1 = g.mask[1];
+      hv = mk1 ? 127 - __builtin_clzll(mk1) : 63 - __builtin_clzll(mk0 | 1ull);
+      q = a.qi[jj];
+      lo = a.lr[q.lr_off + m];
+      n = hv >= lo ? hv - lo + 1 : 0;
+      if (hv < lo || !(mk0 | mk1)) set_overflow(a, 8);  // cannot happen: a candidate's mass is in R_hv
+    }
+    const uint32_t incl = wave_incl_u((uint32_t)n);
+    const uint32_t total = __shfl(incl, 63, 64);
+    uint32_t wbase = 0;
+    if (lane == 0) wbase = atomicAdd(&a.ctl->node_ctr, total);
+    wbase = __shfl(wbase, 0, 64);
+    if ((uint64_t)wbase + total > a.ncap) {
+      if (lane == 0) set_overflow(a, 1);
+      return;
+    }
+    const uint32_t id0 = wbase + incl - (uint32_t)n;  // rank lo; rank k at id0 + k - lo
+    if (a.nodes_out && act) atomicAdd((unsigned long long*)&a.nodes_out[q.i], (unsigned long long)n);
+    const int steps = wave_max_i(n);
+    uint64_t uk[KW];
+#pragma unroll
+    for (int w = 0; w < KW; ++w) uk[w] = 0;
+    int uA = 0;
+    bool have_u = false;
+    const uint32_t* qrow = a.qrow + (size_t)jj * 128;
+    const int field0 = KW * 64 - a.rb - (int)q.K * a.cb;  // LSB of rank 0's count field
+    for (int s = 0; s < steps; ++s) {
+      const bool live = s < n;
+      const int k = hv - s;
+      const uint32_t id = id0 + (uint32_t)(k - lo);
+      const uint32_t rw = live ? qrow[k] : 0u;
+      const int64_t wk = qrow_w(rw);
+      const bool mod = qrow_mod(rw);
+      uint64_t key[KW];
+      int A = 0, B = 0;
+      bool from_l = false;
+      const bool has_c = live && (k < 64 ? ((mk0 >> k) & 1ull) : ((mk1 >> (k - 64)) & 1ull));
+      if (has_c) {
+        const uint32_t cs = cand_find<KW>(Cb, a.cmask, fkey((uint32_t)band, jj, m, (uint32_t)k));
+        if (cs == UINT32_MAX) {
+          set_overflow(a, 16);  // cannot happen: the mask bit follows the insertion
+        } else {
+          const FCand<KW>& e = Cb[cs];
+          const uint32_t par = e.parent;
+          uint64_t ck[KW];
+#pragma unroll
+          for (int w = 0; w < KW; ++w) ck[w] = e.fk[w];
+          if (par & kRootBit) a.root_node[par & ~kRootBit] = id;
+          else a.lchild[par] = id;
+          if (!(have_u && key_less<KW>(uk, ck))) {  // the left parent's path comes first (or is the only one)
+            from_l = true;
+#pragma unroll
+            for (int w = 0; w < KW; ++w) key[w] = ck[w];
+            A = e.A;
+            B = e.B;
+          }
+        }
+      }
+      if (!from_l) {  // up from (m, k + 1): same path, B = cap of this row (mass_table.py:411-420)
+#pragma unroll
+        for (int w = 0; w < KW; ++w) key[w] = uk[w];
+        A = uA;
+        B = qrow_cap(rw);
+      }
+      // the left branch (mass_table.py:424-441): bit1 <=> m - w_k in R_k
+      const int64_t m2 = (int64_t)m - wk;
+      const bool b1 = live && m2 >= 0 && (m2 == 0 || (int)a.lr[q.lr_off + m2] <= k);
+      const bool latt = b1 && (!mod || (A > 0 && B > 0));
+      if (live) a.flags[id] = (uint8_t)((latt ? kFLeft : 0) | (k > lo ? kFUp : 0) | (latt && m2 == 0 ? kFZero : 0));
+      bool emit = latt && m2 > 0;
+      const uint32_t band2 = emit ? (uint32_t)((q.hi - m2) / a.wb) : 0u;
+      const uint32_t slot2 = band2 & rmask;
+      uint32_t gs2 = 0;
+      bool fresh = false;
+      if (emit) {
+        FGroup* G2 = (FGroup*)a.gtab + slot2 * gstride;
+        gs2 = group_get(G2, a.gmask, fkey(band2, jj, (uint32_t)m2, 0), fresh);
+        if (gs2 == UINT32_MAX) {
+          set_overflow(a, 2);
+          emit = false;
+          fresh = false;
+        } else {
+          atomicOr((unsigned long long*)&G2[gs2].mask[k >> 6], 1ull << (k & 63));
+        }
+      }
+      for (int d = 1; d <= a.jump; ++d) {  // fresh groups join their band's list: one atomic per wave and band
+        const bool pd = fresh && band2 == (uint32_t)band + (uint32_t)d;
+        const uint64_t bm = __ballot(pd);
+        if (bm) {
+          const int leader = __builtin_ctzll(bm);
+          const uint32_t sl = ((uint32_t)band + (uint32_t)d) & rmask;
+          uint32_t b0 = 0;
+          if (lane == leader) b0 = atomicAdd(&a.ctl->list_cnt[sl], (uint32_t)__builtin_popcountll(bm));
+          b0 = __shfl(b0, leader, 64);
+          if (pd) {
+            const uint32_t at = b0 + (uint32_t)__builtin_popcountll(bm & lanemask_lt());
+            if (at > a.gmask) set_overflow(a, 4);
+            else a.glist[sl * gstride + at] = gs2;
+          }
+        }
+      }
+      if (emit) {
+        FCand<KW>* C2 = (FCand<KW>*)a.ctab + slot2 * cstride;
+        const uint32_t cs = cand_put<KW>(C2, a.cmask, fkey(band2, jj, (uint32_t)m2, (uint32_t)k));
+        if (cs == UINT32_MAX) {
+          set_overflow(a, 2);
+        } else {
+          uint64_t k2[KW];
+#pragma unroll
+          for (int w = 0; w < KW; ++w) k2[w] = key[w];
+          key_add_bit<KW>(k2, field0 + k * a.cb);
+          FCand<KW>& e = C2[cs];
+          e.parent = id;
+          e.A = (uint8_t)(mod ? A - 1 : A);
+          e.B = (uint8_t)(mod ? B - 1 : B);
+#pragma unroll
+          for (int w = 0; w < KW; ++w) e.fk[w] = k2[w];
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < KW; ++w) uk[w] = key[w];
+      uA = A;
+      have_u = live;
+    }
+  }
+}
+
+// between bands: record where band b's nodes start; free the list slot the
+// next band's heaviest children will fill
+__global__ void k_lbf_mark(FrontierArgs a, int band) {
+  a.band_start[band] = a.ctl->node_ctr;
+  a.ctl->list_cnt[((uint32_t)band + (uint32_t)a.jump) & ((uint32_t)a.ring - 1u)] = 0;
+}
+
+// the memoised values of band b's nodes (mass_table.py:407-457): a lane per
+// group (its lowest rank, whose id starts the group), ranks ascending; lower
+// with 255 as "no path" (min(default, x) at the roots), upper from -1
+__global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
+  if (__hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const uint32_t s0 = a.band_start[band], s1 = a.band_start[band + 1];
+  const uint32_t nth = gridDim.x * blockDim.x;
+  for (uint32_t x0 = s0 + blockIdx.x * blockDim.x + threadIdx.x; x0 < s1; x0 += nth) {
+    uint8_t f = a.flags[x0];
+    if (f & kFUp) continue;  // not the lowest rank of its group
+    int plo = 255, phi = -1;
+    for (uint32_t x = x0; x < s1; ++x) {
+      if (x != x0) {
+        f = a.flags[x];
+        if (!(f & kFUp)) break;
+      }
+      int vl = 255, vh = -1;
+      if (f & kFUp) {  // (m, k - 1): the node below in this group
+        vl = plo;
+        vh = phi;
+      }
+      if (f & kFLeft) {
+        int cl = 1, ch = 1;  // a left move onto mass 0: 0 + 1
+        if (!(f & kFZero)) {
+          const uint32_t c = a.lchild[x];
+          const int l = (int)a.vlo[c] + 1;
+          cl = l > 255 ? 255 : l;
+          ch = (int)a.vhi[c] + 1;  // -1 + 1 = 0 (the reference's default feeds the max)
+        }
+        vl = cl < vl ? cl : vl;
+        vh = ch > vh ? ch : vh;
+      }
+      a.vlo[x] = (uint8_t)vl;
+      a.vhi[x] = (int8_t)vh;
+      plo = vl;
+      phi = vh;
+    }
+  }
+}
+
+// per query: min / max over the window's roots (mass_table.py:459-487)
+__global__ __launch_bounds__(256) void k_lbf_out(FrontierArgs a) {
+  const uint32_t jj = blockIdx.x * blockDim.x + threadIdx.x;
+  if (jj >= a.n_chunk) return;
+  const FQInfo q = a.qi[jj];
+  const bool bad = __hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (bad) return;  // the host splits the chunk and runs it again
+  const int dl = (int)q.L + 1;
+  int bl = dl, bh = -1;
+  if (q.lo <= 0 && q.hi >= 0) {  // total_mass == 0 -> 0
+    bl = 0 < bl ? 0 : bl;
+    bh = 0 > bh ? 0 : bh;
+  }
+  const int top = (int)q.K - 1;
+  for (int64_t v = q.lo < 1 ? 1 : q.lo; v <= q.hi; ++v) {
+    if (top < 0 || (int)a.lr[q.lr_off + v] > top) continue;  // pair(top, v) == 0: the default
+    const uint32_t id = a.root_node[(size_t)jj * a.rstride + (size_t)(v - q.lo)];
+    const int l = a.vlo[id], h = a.vhi[id];
+    bl = l < bl ? l : bl;
+    bh = h > bh ? h : bh;
+  }
+  a.lower[q.i] = bl >= dl ? 1 : bl;  // the default becomes 1 / max_len (:476-484)
+  a.upper[q.i] = bh == -1 ? (int64_t)q.L : bh;
+  a.status[q.i] = 0;
+}
+
+// the lowest kept rank reaching each mass, from sst_reach_rows' row bitsets
+__global__ __launch_bounds__(256) void k_reach_lowest(ReachArgs r, const uint64_t* lr_off, uint8_t* lr) {
+  for (int64_t g = blockIdx.y; g < r.n_spec; g += gridDim.y) {
+    const uint64_t m0 = r.alpha[2 * g], m1 = r.alpha[2 * g + 1];
+    int K = 0;
+    for (int row = 1; row < r.n_rows; ++row) K += row < 64 ? (int)((m0 >> row) & 1ull) : (int)((m1 >> (row - 64)) & 1ull);
+    const int64_t W = r.words[g];
+    const uint32_t* bits = r.bits + r.off[g];
+    uint4* out = (uint4*)(lr + lr_off[g]);
+    for (int64_t jw = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; jw < W; jw += (int64_t)gridDim.x * blockDim.x) {
+      uint32_t o[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = 0xFFFFFFFFu;
+      uint32_t acc = 0;
+      for (int k = 0; k < K && acc != 0xFFFFFFFFu; ++k) {
+        const uint32_t x = bits[(int64_t)k * W + jw];
+        const uint32_t nw = x & ~acc;
+        if (!nw) continue;
+        acc |= x;
+        const uint32_t kk = (uint32_t)k * 0x01010101u;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const uint32_t nib = (nw >> (4 * q)) & 0xFu;
+          const uint32_t bm = ((nib & 1u) ? 0xFFu : 0u) | ((nib & 2u) ? 0xFF00u : 0u) | ((nib & 4u) ? 0xFF0000u : 0u) |
+                              ((nib & 8u) ? 0xFF000000u : 0u);
+          o[q] = (o[q] & ~bm) | (kk & bm);
+        }
+      }
+      out[2 * jw] = make_uint4(o[0], o[1], o[2], o[3]);
+      out[2 * jw + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+    }
+  }
+}
+
+hipError_t launch_reach_lowest(const ReachArgs& r, const uint64_t* lr_off, uint8_t* lr, hipStream_t st) {
+  if (r.n_spec <= 0) return hipSuccess;
+  const int gy = (int)(r.n_spec < 65535 ? r.n_spec : 65535);
+  hipLaunchKernelGGL(k_reach_lowest, dim3(16, gy), dim3(256), 0, st, r, lr_off, lr);
+  return hipGetLastError();
+}
+
+hipError_t launch_lbf_setup(const TableArgs& t, const FrontierArgs& a, hipStream_t st) {
+  const uint32_t blocks = (a.n_chunk + 3) / 4;  // four 64-lane waves per block
+  hipLaunchKernelGGL(k_lbf_setup, dim3(blocks), dim3(256), 0, st, t, a);
+  return hipGetLastError();
+}
+
+template <int KW>
+static hipError_t sweep(const FrontierArgs& a, int n_bands, int band_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_lbf_roots<KW>, dim3((a.n_chunk + 255) / 256), dim3(256), 0, st, a);
+  for (int b = 0; b < n_bands; ++b) {
+    hipLaunchKernelGGL(k_lbf_mark, dim3(1), dim3(1), 0, st, a, b);
+    hipLaunchKernelGGL(k_lbf_band<KW>, dim3(band_blocks), dim3(256), 0, st, a, b);
+  }
+  hipLaunchKernelGGL(k_lbf_mark, dim3(1), dim3(1), 0, st, a, n_bands);
+  for (int b = n_bands - 1; b >= 0; --b) hipLaunchKernelGGL(k_lbf_values, dim3(band_blocks), dim3(256), 0, st, a, b);
+  hipLaunchKernelGGL(k_lbf_out, dim3((a.n_chunk + 255) / 256), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_lbf_sweep(const FrontierArgs& a, int key_words, int n_bands, int band_blocks, hipStream_t st) {
+  switch (key_words) {
+    case 4: return sweep<4>(a, n_bands, band_blocks, st);
+    case 8: return sweep<8>(a, n_bands, band_blocks, st);
+    case 16: return sweep<16>(a, n_bands, band_blocks, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+size_t lbf_cand_bytes(int key_words) {
+  switch (key_words) {
+    case 4: return sizeof(FCand<4>);
+    case 8: return sizeof(FCand<8>);
+    default: return sizeof(FCand<16>);
+  }
+}
+size_t lbf_group_bytes() { return sizeof(FGroup); }
+
+}  // namespace sst

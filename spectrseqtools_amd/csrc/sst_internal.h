@@ -295,6 +295,70 @@ struct ReachArgs {
   int64_t n_spec;
 };
 hipError_t launch_reach_rows(const ReachArgs& a, int n_wg, hipStream_t st);
+// lr[lr_off[g] + m] = the lowest kept rank k with m in R_k (0xFF: none)
+hipError_t launch_reach_lowest(const ReachArgs& r, const uint64_t* lr_off, uint8_t* lr, hipStream_t st);
+
+// the first-visit frontier (sst_frontier.hip): length bounds on reduced
+// alphabets without replaying the DFS
+struct FQInfo {       // per listed query of a chunk
+  int64_t hi, lo;     // quantised window
+  uint64_t lr_off;    // its alphabet's lowest-rank bytes
+  uint32_t i;         // query index
+  uint16_t K;         // kept rows (row 0 excluded)
+  uint16_t L;         // max_len
+  uint16_t A0;        // max_modifications (clamped to 255)
+  uint16_t pad;
+};
+struct FCtl {
+  uint32_t node_ctr;
+  uint32_t overflow;  // bit 0 nodes, 1 a hash table, 2 a band list, 3/4 internal
+  uint32_t list_cnt[8];
+  uint32_t max_band, max_win, max_k, pad;
+  uint64_t max_hi;
+};
+struct FrontierArgs {
+  const uint32_t* list;  // the list pass's live queries
+  uint32_t chunk0, n_chunk;
+  const double* su;
+  const double* obs;
+  double tol, prec, rprec;
+  const int32_t* spec;
+  const uint64_t* alpha;
+  const uint8_t* lr;
+  const uint64_t* lr_off;
+  const int32_t* qlen;
+  const int32_t* caps_len;
+  const int32_t* a0_len;
+  int A0, max_len;
+  int wb;          // band width: the table's lightest row (every left move crosses >= 1 band)
+  int ring, jump;  // hash / list ring size (power of two > jump), max bands one left move crosses
+  int rb, cb;      // key fields: root index bits, bits per rank count
+  int rstride;     // root slots per query
+  FQInfo* qi;
+  uint32_t* qrow;  // [n_chunk][128]: rank -> w | cap << 20 | is_mod << 28
+  uint32_t* root_node;
+  uint8_t* flags;
+  uint32_t* lchild;
+  uint8_t* vlo;
+  int8_t* vhi;
+  uint64_t ncap;
+  char* gtab;
+  uint32_t gmask;
+  char* ctab;
+  uint32_t cmask;
+  uint32_t* glist;
+  FCtl* ctl;
+  uint32_t* band_start;
+  uint32_t* band_groups;
+  int64_t* lower;
+  int64_t* upper;
+  int8_t* status;
+  uint64_t* nodes_out;
+};
+hipError_t launch_lbf_setup(const TableArgs& t, const FrontierArgs& a, hipStream_t st);
+hipError_t launch_lbf_sweep(const FrontierArgs& a, int key_words, int n_bands, int band_blocks, hipStream_t st);
+size_t lbf_cand_bytes(int key_words);
+size_t lbf_group_bytes();
 
 struct ExactWs {
   char* hash;

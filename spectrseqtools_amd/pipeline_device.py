@@ -27,7 +27,8 @@ _PROGRESS = os.environ.get("SST_PIPE_PROGRESS") == "1"  # per-launch lines of th
 LB_NOT_RUN = -6  # length_device(spectra=...): the bounds of a spectrum outside the sample
 ERR_BITS = {1: "a spectrum has more than 4096 peaks", 2: "a spectrum has more rows than the reserved slices hold",
             4: "a window outside the pair class", 8: "is_valid_mass raised (a window past a table's end)",
-            16: "an explanation dict too large for the LDS hash", 32: "rows out of mass order"}
+            16: "an explanation dict too large for the LDS hash", 32: "rows out of mass order",
+            64: "an exact-mode query list overflowed", 128: "an exact-mode answer raised or was capped"}
 
 
 def _one_stream(fn):
@@ -93,7 +94,11 @@ class _Heartbeat:
 def _check_err(err):
     e = int(err.item())
     if e:
-        raise _native.EngineError("device pipeline: " + "; ".join(v for k, v in ERR_BITS.items() if e & k))
+        known = [v for k, v in ERR_BITS.items() if e & k]
+        rest = e & ~sum(ERR_BITS)
+        if rest:
+            known.append(f"unknown error bits {rest:#x}")
+        raise _native.EngineError("device pipeline: " + "; ".join(known))
 
 
 @dataclass
@@ -835,39 +840,34 @@ class DeviceLength:
     comb: object          # torch int64 [total, 2] the combined skeleton (masks)
     reach_batches: int
     distinct_alphabets: int = 0  # skeleton alphabets (each one's row bitsets built once)
-    replay_nodes: object = None  # [S] the bounds' DFS nodes (phase 1, over its attempts)
+    replay_nodes: object = None  # [S] frontier: memo entries of the bounds' DFS; replay: phase-1 nodes over attempts
+    engine: str = "frontier"
+    frontier: dict = None  # sst_lbf_stats summed over the batches (frontier engine)
 
 
 @_one_stream
-def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=64 << 30,
-                  share_alphabets=True, length_chunk=1 << 30, spectra=None, soft_nodes=1 << 20,
-                  heavy_memo=1 << 22):
-    """Stage 5: each spectrum's skeleton alphabet (the canonical rows and the
-    modifications its START / END skeletons name), both length bounds on it
-    (sst_reach_rows_device + sst_length_bounds_reach_device: the reduced
-    table's pairs from its rows' reachability, one replay per spectrum, in
-    batches whose bitsets fit `reach_budget_bytes`, one pass per max_len
-    group), then the Jaccard selection and the combined skeleton (k_jaccard).
-    spectra: the bounds for these spectra only (indices; the others get
-    lb_status LB_NOT_RUN and Jaccard status SST_JAC_BOUNDS) -- a bounded
-    sample where the reference's DFS is too large to replay for all."""
+def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0_len, sel=None, engine="frontier",
+                               reach_budget_bytes=64 << 30, share_alphabets=True, length_chunk=1 << 30,
+                               soft_nodes=1 << 20, heavy_memo=1 << 22, frontier_workspace=0):
+    """compute_sequence_length_bound(dir="lower") and (dir="upper")
+    (mass_table.py:343-487) for spectra on reduced alphabets (alpha_sk [S, 2]
+    u64 row masks; su / ob the SequenceInformation masses; max_len [S]), with
+    the budgets per max_len: caps_len[L, r] = round(L * rate_r) (row stride
+    MAX_ROWS) and a0_len[L] = round(modification_rate * L).  Only spectra
+    `sel` are computed (the others keep lb_status LB_NOT_RUN).  engine:
+    "frontier" (the first-visit frontier) or "replay" (the round-4
+    per-spectrum DFS replay).  Returns (lower, upper, lb_status, nodes, stats)."""
     import torch
 
     dt = dp_table.device_table
     eng = dt.engine
     L = eng._lib
     h = dt.handle
-    S = len(sk.max_len)
-    dev = sk.skel.device
-    ml = sk.max_len.astype(np.int64)
-    ml_t = torch.as_tensor(ml.astype(np.int32), device=dev)
-    skel_off_t = torch.as_tensor(sk.skel_off, device=dev)
-    a_sk = torch.empty((max(1, S), 2), dtype=torch.int64, device=dev)
-    eng.check(L.sst_skeleton_alpha_device(h, S, ml_t.data_ptr(), skel_off_t.data_ptr(), sk.skel.data_ptr(),
-                                          alpha_dev.data_ptr(), a_sk.data_ptr()), "sst_skeleton_alpha_device")
-    alpha_sk = a_sk.cpu().numpy().view(np.uint64)[:S].copy()
-    su = np.asarray(su_seq, dtype=np.float64)
-    ob = np.asarray(obs_seq, dtype=np.float64)
+    S = len(alpha_sk)
+    dev = torch.device("cuda", eng.device) if hasattr(eng, "device") else torch.device("cuda")
+    su = np.asarray(su, dtype=np.float64)
+    ob = np.asarray(ob, dtype=np.float64)
+    ml = np.asarray(max_len, dtype=np.int64)
     prec, tol = dp_table.precision, dp_table.tolerance
     hi = np.rint(su / prec) + np.ceil(tol * ob / prec)  # the window's top (mass_table.py:354-359)
     words = (np.maximum(hi, 0).astype(np.int64) >> 5) + 2
@@ -876,7 +876,7 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     n_rows = len(dp_table.masses)
     # spectra with one skeleton alphabet share its rows' bitsets (built up to
     # the heaviest of their windows): few distinct alphabets among many spectra
-    sel = np.arange(S) if spectra is None else np.unique(np.asarray(spectra, dtype=np.int64))
+    sel = np.arange(S) if sel is None else np.asarray(sel, dtype=np.int64)
     lower = np.zeros(S, np.int64)
     upper = np.zeros(S, np.int64)
     lb_st = np.full(S, LB_NOT_RUN, np.int8)
@@ -884,19 +884,15 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     nodes = np.zeros(S, np.int64)
     masses = dp_table.masses
     is_mod = [m.is_modification for m in masses]
-    # budgets by max_len (mass_explanation.py:158-172 as set_budgets): caps
-    # round(L * rate) per row, max_modifications round(modification_rate * L)
+    caps_len = np.ascontiguousarray(caps_len, dtype=np.int32)
+    a0_len = [int(x) for x in a0_len]
     ml_hi = int(ml[sel].max()) if len(sel) else 1
-    if ml_hi >= 128:
-        raise NotImplementedError("length bounds: max_len above 127")
-    caps_len = np.zeros((ml_hi + 1, _native.MAX_ROWS), np.int32)
-    for Lm in range(ml_hi + 1):
-        caps_len[Lm, :len(masses)] = [min(round(Lm * m.modification_rate), 1 << 30) for m in masses]
-    a0_len = [min(round(dp_table.seq.modification_rate * Lm), 1 << 30) for Lm in range(ml_hi + 1)]
+    if caps_len.shape[0] <= ml_hi or len(a0_len) <= ml_hi or caps_len.shape[1] != _native.MAX_ROWS:
+        raise ValueError("length bounds: caps_len / a0_len must cover every max_len")
     caps_t = torch.as_tensor(caps_len, device=dev)
     a0_t = torch.as_tensor(np.asarray(a0_len, np.int32), device=dev)
     dt.set_budgets(is_mod, [int(c) for c in caps_len[ml_hi, :len(masses)]])  # the rows' modification flags
-    stats = {"batches": 0, "distinct": 0}
+    stats = {"batches": 0, "distinct": 0, "frontier": {}}
 
     def bounds_pass(sel, soft_nodes, memo_first):
         """Both bounds of spectra `sel`, in batches whose row bitsets fit
@@ -975,15 +971,155 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
             u0 = u1
         return sel[lb_st[sel] == _native.LB_HEAVY]
 
-    # light spectra first, under a soft node budget, so that no batch waits
-    # for its few heavy spectra; then the heavy ones together, with a larger
-    # first memo
-    heavy = bounds_pass(sel, soft_nodes, 0) if soft_nodes else sel
+    def frontier_pass(sel):
+        """Both bounds of spectra `sel` by the first-visit frontier
+        (sst_length_bounds_frontier_device): per batch of alphabets, the row
+        bitsets, then one byte per mass (the lowest kept rank reaching it),
+        then every spectrum of the batch in one call."""
+        if share_alphabets:
+            uniq, inv = np.unique(alpha_sk[sel], axis=0, return_inverse=True)
+            inv = inv.reshape(-1)
+        else:
+            uniq, inv = alpha_sk[sel], np.arange(len(sel))
+        U = len(uniq)
+        stats["distinct"] = max(stats["distinct"], U)
+        words_u = np.zeros(U, np.int64)
+        np.maximum.at(words_u, inv, words[sel])
+        K_u = mask_rows(uniq, n_rows)[:, 1:].sum(axis=1).astype(np.int64)
+        need_u = 4 * K_u * words_u + 32 * words_u
+        by_u = np.argsort(inv, kind="stable")
+        u_first = np.concatenate([[0], np.cumsum(np.bincount(inv, minlength=U))])
+        u0 = 0
+        while u0 < U:
+            u1, tot = u0, 0
+            while u1 < U and (u1 == u0 or tot + need_u[u1] <= reach_budget_bytes):
+                tot += int(need_u[u1])
+                u1 += 1
+            nu = u1 - u0
+            wb = words_u[u0:u1]
+            off_u = np.concatenate([[0], np.cumsum(K_u[u0:u1] * wb)[:-1]]).astype(np.int64)
+            lr_off = np.concatenate([[0], np.cumsum(32 * wb)[:-1]]).astype(np.int64)
+            bits = torch.empty(max(1, int((K_u[u0:u1] * wb).sum())), dtype=torch.int32, device=dev)
+            lr = torch.empty(max(1, int(32 * wb.sum())), dtype=torch.uint8, device=dev)
+            alu_t = torch.as_tensor(uniq[u0:u1].view(np.int64), device=dev).contiguous()
+            wu_t = torch.as_tensor(wb, device=dev)
+            ou_t = torch.as_tensor(off_u, device=dev)
+            lo_u_t = torch.as_tensor(lr_off, device=dev)
+            eng.check(L.sst_reach_rows_device(h, alu_t.data_ptr(), wu_t.data_ptr(), ou_t.data_ptr(), nu,
+                                              bits.data_ptr()), "sst_reach_rows_device")
+            eng.check(L.sst_reach_lowest_device(h, alu_t.data_ptr(), wu_t.data_ptr(), ou_t.data_ptr(), nu,
+                                                bits.data_ptr(), lo_u_t.data_ptr(), lr.data_ptr()),
+                      "sst_reach_lowest_device")
+            eng.synchronize()
+            del bits
+            torch.cuda.empty_cache()
+            lu_src = by_u[u_first[u0]:u_first[u1]]
+            members = sel[lu_src]
+            n = len(members)
+            lu = (inv[lu_src] - u0).astype(np.int32)
+            su_t = torch.as_tensor(su[members], device=dev)
+            ob_t = torch.as_tensor(ob[members], device=dev)
+            sp_t = torch.as_tensor(lu, device=dev)
+            ql_t = torch.as_tensor(ml[members].astype(np.int32), device=dev)
+            lo_t = torch.zeros(n, dtype=torch.int64, device=dev)
+            up_t = torch.zeros(n, dtype=torch.int64, device=dev)
+            st_t = torch.zeros(n, dtype=torch.int8, device=dev)
+            nd_t = torch.zeros(n, dtype=torch.int64, device=dev)
+            fs = _native.LbfStats()
+            beat = _Heartbeat("[length] frontier running", 30.0) if _PROGRESS else None
+            eng.check(L.sst_length_bounds_frontier_device(
+                h, su_t.data_ptr(), ob_t.data_ptr(), sp_t.data_ptr(), alu_t.data_ptr(), lr.data_ptr(),
+                lo_u_t.data_ptr(), n, float(tol), float(prec), ml_hi, a0_len[ml_hi], lo_t.data_ptr(), up_t.data_ptr(),
+                st_t.data_ptr(), ql_t.data_ptr(), caps_t.data_ptr(), a0_t.data_ptr(), nd_t.data_ptr(),
+                int(frontier_workspace), ctypes.byref(fs)), "sst_length_bounds_frontier_device")
+            if beat is not None:
+                beat.stop()
+            lower[members] = lo_t.cpu().numpy()
+            upper[members] = up_t.cpu().numpy()
+            lb_st[members] = st_t.cpu().numpy()
+            nodes[members] += nd_t.cpu().numpy()
+            fd = fs.as_dict()
+            for k_, v_ in fd.items():
+                if k_ in ("bands", "key_words", "max_band_groups", "table_slots", "node_cap"):
+                    stats["frontier"][k_] = max(stats["frontier"].get(k_, 0), v_)
+                else:
+                    stats["frontier"][k_] = stats["frontier"].get(k_, 0) + v_
+            if _PROGRESS:
+                print(f"[length] frontier batch {stats['batches']}: {n} spectra, {nu} alphabets: {fd}",
+                      file=sys.stderr, flush=True)
+            del lr
+            stats["batches"] += 1
+            u0 = u1
+
+    if engine == "frontier":
+        frontier_pass(sel)
+        heavy = []
+    elif engine == "replay":
+        # light spectra first, under a soft node budget, so that no batch waits
+        # for its few heavy spectra; then the heavy ones together, with a larger
+        # first memo
+        heavy = bounds_pass(sel, soft_nodes, 0) if soft_nodes else sel
+    else:
+        raise ValueError(f"length_device: engine {engine!r}")
     if len(heavy):
         if _PROGRESS:
             print(f"[length] {len(heavy)} spectra over {soft_nodes} nodes: replayed together", file=sys.stderr,
                   flush=True)
         bounds_pass(heavy, 0, heavy_memo if soft_nodes else 0)
+    return lower, upper, lb_st, nodes, stats
+
+
+@_one_stream
+def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=64 << 30,
+                  share_alphabets=True, length_chunk=1 << 30, spectra=None, soft_nodes=1 << 20,
+                  heavy_memo=1 << 22, engine="frontier", frontier_workspace=0):
+    """Stage 5: each spectrum's skeleton alphabet (the canonical rows and the
+    modifications its START / END skeletons name), both length bounds on it,
+    then the Jaccard selection and the combined skeleton (k_jaccard).
+    engine="frontier" (default): sst_reach_rows_device + sst_reach_lowest_device
+    + sst_length_bounds_frontier_device -- the reduced table's pairs from its
+    rows' reachability, every node's first visit computed band by band over
+    descending masses, no DFS replay; batches of alphabets whose
+    bitsets fit `reach_budget_bytes`, every max_len in one call
+    (frontier_workspace: the call's device workspace, 0 = its default).
+    engine="replay": sst_length_bounds_reach_device, one replay of the
+    reference's DFS per spectrum (the round-4 engine, kept for comparison).
+    spectra: the bounds for these spectra only (indices; the others get
+    lb_status LB_NOT_RUN and Jaccard status SST_JAC_BOUNDS) -- a bounded
+    sample where the reference's DFS is too large to replay for all."""
+    import torch
+
+    dt = dp_table.device_table
+    eng = dt.engine
+    L = eng._lib
+    h = dt.handle
+    S = len(sk.max_len)
+    dev = sk.skel.device
+    ml = sk.max_len.astype(np.int64)
+    ml_t = torch.as_tensor(ml.astype(np.int32), device=dev)
+    skel_off_t = torch.as_tensor(sk.skel_off, device=dev)
+    a_sk = torch.empty((max(1, S), 2), dtype=torch.int64, device=dev)
+    eng.check(L.sst_skeleton_alpha_device(h, S, ml_t.data_ptr(), skel_off_t.data_ptr(), sk.skel.data_ptr(),
+                                          alpha_dev.data_ptr(), a_sk.data_ptr()), "sst_skeleton_alpha_device")
+    alpha_sk = a_sk.cpu().numpy().view(np.uint64)[:S].copy()
+    su = np.asarray(su_seq, dtype=np.float64)
+    ob = np.asarray(obs_seq, dtype=np.float64)
+    prec = dp_table.precision
+    sel = np.arange(S) if spectra is None else np.unique(np.asarray(spectra, dtype=np.int64))
+    masses = dp_table.masses
+    # budgets by max_len (mass_explanation.py:158-172 as set_budgets): caps
+    # round(L * rate) per row, max_modifications round(modification_rate * L)
+    ml_hi = int(ml[sel].max()) if len(sel) else 1
+    if ml_hi >= 128:
+        raise NotImplementedError("length bounds: max_len above 127")
+    caps_len = np.zeros((ml_hi + 1, _native.MAX_ROWS), np.int32)
+    for Lm in range(ml_hi + 1):
+        caps_len[Lm, :len(masses)] = [min(round(Lm * m.modification_rate), 1 << 30) for m in masses]
+    a0_len = [min(round(dp_table.seq.modification_rate * Lm), 1 << 30) for Lm in range(ml_hi + 1)]
+    lower, upper, lb_st, nodes, stats = length_bounds_alpha_device(
+        dp_table, alpha_sk, su, ob, ml, caps_len, a0_len, sel=sel, engine=engine,
+        reach_budget_bytes=reach_budget_bytes, share_alphabets=share_alphabets, length_chunk=length_chunk,
+        soft_nodes=soft_nodes, heavy_memo=heavy_memo, frontier_workspace=frontier_workspace)
     n_batches, U = stats["batches"], stats["distinct"]
     # Jaccard + combine
     comb_off = np.concatenate([[0], np.cumsum(ml)]).astype(np.int64)
@@ -1004,7 +1140,7 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     eng.check(L.sst_jaccard_device(h, ctypes.byref(ja)), "sst_jaccard_device")
     eng.synchronize()
     return DeviceLength(alpha_sk, lower, upper, lb_st, seq_len.cpu().numpy()[:S], jst.cpu().numpy()[:S], comb_off,
-                        comb, n_batches, U, nodes)
+                        comb, n_batches, U, nodes, engine, stats["frontier"])
 
 
 # ---------------------------------------------------------------------------

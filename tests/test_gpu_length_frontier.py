@@ -1,0 +1,180 @@
+"""GPU parity of config 5's stage-5 engines against the CPU oracle on each
+skeleton alphabet's REBUILT table (set_up_bit_table over the kept rows,
+max_mass = max(kept) * 35, mass_table.py:94-121, skeleton_building.py:315-336):
+compute_sequence_length_bound (mass_table.py:343-487) in both directions for
+~200 synthetic spectra of 5..20 nucleotides, per-spectrum max_len, random
+modification rates (caps round(L * rate)) and max_modifications from 0 up
+to round(0.5 L), so that budgets bind.
+
+  * the first-visit frontier (sst_length_bounds_frontier_device, what
+    pipeline_device.length_device runs): alphabets of 4..104 kept rows, so
+    that first-visit keys of 256, 512 and 1024 bits all run; then again in a
+    workspace too small for the batch (chunks split and rerun, counted) and
+    in one too small for the heaviest spectra (those report SST_ABORTED,
+    every other spectrum unchanged);
+  * the round-4 DFS replay (sst_length_bounds_reach_device) on the same
+    spectra with a small soft node budget (the heavy second pass runs) and a
+    small first memo (memo retries run), fused (<= 64 kept rows) and unfused.
+"""
+import concurrent.futures as cf
+
+import numpy as np
+import pytest
+
+import _oracle as oracle
+from conftest import load_golden
+from spectrseqtools_amd import _native
+
+pytestmark = pytest.mark.gpu
+TOL, PREC = 1e-5, 1e-3
+CANONICAL = (305042, 306026, 329053, 345048)
+RATES = (0.02, 0.05, 0.1, 0.25, 0.5)
+
+
+@pytest.fixture(scope="module")
+def setup():
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
+
+    eng = _native.get_engine(0)
+    seq = SequenceInformation(max_len=20, su_mass=2000.0, obs_mass=2000.0, modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=eng)
+    rows = [m.mass for m in dp.masses]
+    g = load_golden("alphabet.json")
+    assert rows == sorted({r["tolerated_integer_masses"] for r in g["rows"]} | {0})
+    rng = np.random.default_rng(2025)
+    n_rows = len(rows)
+    # per max_len budgets: caps round(L * rate_r) with random per-row rates,
+    # max_modifications drawn per L from {0, 1, 2, 3, round(0.5 L)}
+    rate = np.array([0.0] + [float(rng.choice(RATES)) if m.is_modification else 1.0 for m in dp.masses[1:]])
+    caps_len = np.zeros((21, _native.MAX_ROWS), np.int32)
+    for L in range(21):
+        caps_len[L, :n_rows] = [round(L * r) for r in rate]
+    a0_len = np.array([int(rng.choice([0, 1, 2, 3, round(0.5 * L)])) for L in range(21)], np.int32)
+    return dp, rows, caps_len, a0_len
+
+
+def _spectra(rows, dp, rng):
+    canon = [i for i, m in enumerate(rows) if m in CANONICAL]
+    mods = [i for i in range(1, len(rows)) if rows[i] not in CANONICAL]
+    plan = [(0, 4, 10, 20)] * 40 + [(1, 8, 10, 20)] * 60 + [(9, 16, 10, 16)] * 60 + [(40, 60, 7, 9)] * 24 + \
+        [(100, 100, 5, 6)] * 16
+    alphas, su, ob, ml = [], [], [], []
+    for lo_m, hi_m, lo_k, hi_k in plan:
+        nm = int(rng.integers(lo_m, hi_m + 1))
+        a = sorted(set(canon + rng.choice(mods, size=min(nm, len(mods)), replace=False).tolist()))
+        w = np.array([rows[r] for r in a])
+        k = int(rng.integers(lo_k, hi_k + 1))
+        s = float(w[rng.integers(0, len(w), k)].sum()) * PREC + rng.normal(0, 0.002)
+        alphas.append(a)
+        su.append(s)
+        ob.append(s + 912.303)  # a START_END fragment's observed mass
+        ml.append(int(np.clip(k + rng.integers(-2, 3), 3, 20)))
+    masks = np.zeros((len(alphas), 2), np.uint64)
+    for g, a in enumerate(alphas):
+        for r in a:
+            masks[g, r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    return alphas, masks, np.array(su), np.array(ob), np.array(ml)
+
+
+def _oracle_bounds(rows, dp, caps_len, a0_len, alphas, su, ob, ml):
+    def one(g):
+        full = [0] + alphas[g]
+        ms = [rows[r] for r in full]
+        L = int(ml[g])
+        tab = oracle.build_table(ms, max(ms) * 35, 32)
+        alph = oracle.Alphabet(ms, [dp.masses[r].is_modification for r in full], [int(caps_len[L, r]) for r in full])
+        return tuple(oracle.length_bound(tab, 32, alph, su[g], ob[g], TOL, L, int(a0_len[L]), d)
+                     for d in ("lower", "upper"))
+
+    with cf.ThreadPoolExecutor(16) as ex:  # ctypes releases the GIL: the oracle calls run in parallel
+        return list(ex.map(one, range(len(alphas))))
+
+
+@pytest.fixture(scope="module")
+def cases(setup):
+    dp, rows, caps_len, a0_len = setup
+    rng = np.random.default_rng(77)
+    alphas, masks, su, ob, ml = _spectra(rows, dp, rng)
+    want = _oracle_bounds(rows, dp, caps_len, a0_len, alphas, su, ob, ml)
+    return alphas, masks, su, ob, ml, want
+
+
+def _check(want, lower, upper, st, skip=()):
+    n_ok = 0
+    for g, (wl, wu) in enumerate(want):
+        if g in skip:
+            continue
+        if wl is None:  # the reference raises (a window past the reduced table)
+            assert int(st[g]) != 0, g
+            continue
+        assert int(st[g]) == 0 and (int(lower[g]), int(upper[g])) == (wl, wu), \
+            (g, int(st[g]), int(lower[g]), int(upper[g]), wl, wu)
+        n_ok += 1
+    return n_ok
+
+
+def test_frontier_vs_oracle_rebuilt_tables(setup, cases):
+    from spectrseqtools_amd import pipeline_device as PD
+
+    dp, rows, caps_len, a0_len = setup
+    alphas, masks, su, ob, ml, want = cases
+    lower, upper, st, nodes, stats = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len)
+    fr = stats["frontier"]
+    assert _check(want, lower, upper, st) >= 190
+    assert fr["key_words"] == 16 and fr["splits"] == 0 and fr["aborted"] == 0, fr
+    assert fr["nodes"] == int(nodes.sum()) > 10 ** 6, fr  # memo entries, summed over the spectra
+    # binding budgets: some spectra's bounds differ from their budget-free ones
+    free = np.full((21, _native.MAX_ROWS), 255, np.int32)
+    lo2, up2, st2, _, _ = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, free, np.full(21, 255, np.int32))
+    assert ((lo2 != lower) | (up2 != upper)).sum() >= 10
+
+
+def test_frontier_split_and_abort(setup, cases):
+    """A workspace far smaller than the batch: chunks overflow and are split
+    until they fit (same results); one smaller than the heaviest spectra:
+    those alone report SST_ABORTED."""
+    from spectrseqtools_amd import pipeline_device as PD
+
+    dp, rows, caps_len, a0_len = setup
+    alphas, masks, su, ob, ml, want = cases
+    _, _, _, nodes, _ = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len)
+    per_slot = 392  # workspace bytes per hash-ring slot (sst_api.cpp: 8 nodes of 7 B + 4 x (32 + 4 + 48) B)
+    big, tot = int(nodes.max()), int(nodes.sum())
+    S = 1 << int(np.ceil(np.log2(max(big, 1024))))  # ring tables of >= the heaviest spectrum's nodes
+    assert 8 * S < tot, (big, tot)  # ... but node capacity below the batch's
+    lower, upper, st, _, stats = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len,
+                                                               frontier_workspace=per_slot * S)
+    fr = stats["frontier"]
+    assert fr["splits"] > 0 and fr["aborted"] == 0 and fr["node_cap"] == 8 * S, fr
+    assert _check(want, lower, upper, st) >= 190
+    small = int(np.sort(nodes)[-8])  # node capacity below the 8 heaviest spectra's
+    S2 = 1 << int(np.floor(np.log2(small // 8)))
+    lower, upper, st, _, stats = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len,
+                                                               frontier_workspace=per_slot * S2)
+    fr = stats["frontier"]
+    ab = set(np.flatnonzero(st == _native.SST_ABORTED).tolist())
+    assert fr["aborted"] == len(ab) >= 8 and fr["node_cap"] == 8 * S2, fr
+    assert all(nodes[g] >= S2 // 2 for g in ab), sorted(int(nodes[g]) for g in ab)
+    assert _check(want, lower, upper, st, skip=ab) >= 150
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_replay_heavy_pass_and_retries_vs_oracle(setup, cases, fused):
+    """The round-4 engine: a soft node budget of 2^12 (every spectrum above it
+    is replayed again in the heavy pass) and a 2^8-mass first memo (memo
+    retries), on the spectra of <= 64 kept rows (fused values) or all of
+    them at <= 9 nucleotides (unfused)."""
+    from spectrseqtools_amd import pipeline_device as PD
+
+    dp, rows, caps_len, a0_len = setup
+    alphas, masks, su, ob, ml, want = cases
+    K = np.array([len(a) for a in alphas])
+    sel = np.flatnonzero(K <= 64) if fused else np.flatnonzero((K > 64) | (np.arange(len(K)) % 4 == 0))
+    lower, upper, st, nodes, _ = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len, sel=sel,
+                                                               engine="replay", soft_nodes=1 << 12,
+                                                               heavy_memo=1 << 8)
+    assert (nodes[sel] > (1 << 12)).sum() >= 10  # the heavy pass ran
+    skip = set(range(len(alphas))) - set(sel.tolist())
+    assert _check(want, lower, upper, st, skip=skip) >= len(sel) - 2

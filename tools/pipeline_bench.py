@@ -63,15 +63,90 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
+def length_cpu_baseline(dp, ln, su_seq, obs_seq, max_len, n_len, budget_s):
+    """Stage 5 on the host: for spectra of the stage (in order, until about
+    budget_s seconds of wall time), what the reference does per spectrum
+    after the skeleton -- rebuild the table on the skeleton alphabet
+    (skeleton_building.py:324, mass_table.py:94-121) and run
+    compute_sequence_length_bound both ways (:335-336) -- by the CPU oracle
+    (oracle/sst_oracle.c, the literal restatement; TEST INFRASTRUCTURE, used
+    here as the baseline only, after the GPU timing), one spectrum per host
+    thread.  Every sampled spectrum's bounds are also compared with the GPU's."""
+    import concurrent.futures as cf
+
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle as oracle
+    from spectrseqtools_amd.pipeline import mask_rows
+
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))  # the box's CPU share for one GPU
+    masses = dp.masses
+    kept = mask_rows(ln.alpha[:n_len], len(masses))
+    tol, prec = dp.tolerance, dp.precision
+
+    def one(g):
+        full = [0] + [r for r in range(1, len(masses)) if kept[g, r]]
+        ms = [masses[r].mass for r in full]
+        L = int(max_len[g])
+        t0 = time.perf_counter()
+        tab = oracle.build_table(ms, max(ms) * 35, 32)
+        t1 = time.perf_counter()
+        alph = oracle.Alphabet(ms, [masses[r].is_modification for r in full],
+                               [round(L * masses[r].modification_rate) for r in full])
+        a0 = round(dp.seq.modification_rate * L)
+        b = [oracle.length_bound(tab, 32, alph, float(su_seq[g]), float(obs_seq[g]), tol, L, a0, d, precision=prec)
+             for d in ("lower", "upper")]
+        return g, t1 - t0, time.perf_counter() - t1, b
+
+    done, build_s, dfs_s, mism = [], 0.0, 0.0, 0
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL
+        it = iter(range(n_len))
+        futs = set()
+        for _ in range(2 * threads):
+            g = next(it, None)
+            if g is not None:
+                futs.add(ex.submit(one, g))
+        while futs:
+            fin, futs = cf.wait(futs, return_when=cf.FIRST_COMPLETED)
+            for f in fin:
+                g, tb, td, b = f.result()
+                done.append(g)
+                build_s += tb
+                dfs_s += td
+                if b[0] is None:
+                    mism += int(ln.lb_status[g]) == 0
+                else:
+                    mism += (int(ln.lb_status[g]), int(ln.lower[g]), int(ln.upper[g])) != (0, b[0], b[1])
+            if time.perf_counter() - t0 < budget_s:
+                for _ in range(len(fin)):
+                    g = next(it, None)
+                    if g is not None:
+                        futs.add(ex.submit(one, g))
+    wall = time.perf_counter() - t0
+    n = len(done)
+    return {"kind": "port", "what": "oracle table rebuild + length_bound lower and upper per spectrum",
+            "threads": threads, "spectra": n, "sample": f"the first {n} of the stage's {n_len} spectra (in order)",
+            "wall_s": wall, "spectra_per_s": n / wall if wall > 0 else 0.0,
+            "thread_s_table_rebuild": build_s, "thread_s_length_bounds": dfs_s,
+            "est_s_all_spectra": n_len * wall / n if n else None,
+            "mismatches_vs_gpu": int(mism)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spectra", type=int, default=100000, help="spectra per GPU")
     ap.add_argument("--warmup-spectra", type=int, default=256, help="untimed warm-up spectra (all stages)")
     ap.add_argument("--length-soft-nodes", type=int, default=1 << 20,
                     help="stage 5's light pass: replays over this many nodes are deferred to the heavy pass")
-    ap.add_argument("--length-spectra", type=int, default=2048,
+    ap.add_argument("--length-spectra", type=int, default=0,
                     help="stage 5's length bounds on this many spectra of the rank (0: all); the reference's "
                          "memoised DFS visits up to ~10^7 nodes per spectrum on rich skeleton alphabets")
+    ap.add_argument("--length-engine", default="frontier", choices=("frontier", "replay"),
+                    help="stage 5: the first-visit frontier (default) or the round-4 per-spectrum DFS replay")
+    ap.add_argument("--cpu-baseline-s", type=float, default=20.0,
+                    help="stage 5's CPU baseline: the oracle's table rebuild + both length bounds per spectrum on "
+                         "the host's cores, for about this many seconds (0: skip)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--host-driven", action="store_true",
                     help="stages 1-2 through the host-driven batched path (pipeline.classify / filter_fixpoint) "
@@ -272,7 +347,7 @@ def main():
         n_len = len(max_len) if args.length_spectra <= 0 else min(args.length_spectra, len(max_len))
         ln = pd.length_device(dp, sk, db.alpha_dev, su_seq, batch.seq_mass,
                               spectra=None if n_len == len(max_len) else np.arange(n_len),
-                              soft_nodes=args.length_soft_nodes)
+                              soft_nodes=args.length_soft_nodes, engine=args.length_engine)
         barrier()
         stages["length"] = {"s": tmax(time.perf_counter() - t0), "bounds_spectra": n_len,
                             "bounds_sample": n_len < len(max_len), "reach_batches": ln.reach_batches,
@@ -285,7 +360,7 @@ def main():
                             "lb_status": {int(k): int(v) for k, v in zip(*np.unique(ln.lb_status,
                                                                                    return_counts=True))},
                             "mean_seq_len": float(ln.seq_len[ln.status == 0].mean()) if (ln.status == 0).any() else 0,
-                            "kernels": kernels()}
+                            "engine": ln.engine, "frontier": ln.frontier, "kernels": kernels()}
         busy(stages["length"])
         progress("length")
         barrier()
@@ -307,6 +382,9 @@ def main():
                             "path": "pack_outcomes + one agreed-size gather to rank 0"
                                     + (f" ({'RCCL' if args.backend == 'nccl' else 'gloo'})" if dist else " (local)")}
     engine.profile(False)
+    if rows is not None and rank == 0 and args.cpu_baseline_s > 0:
+        stages["length"]["cpu_baseline"] = length_cpu_baseline(dp, ln, su_seq, batch.seq_mass, max_len, n_len,
+                                                               args.cpu_baseline_s)
 
     # per-spectrum alphabet reduction = a table rebuild (canonical + 3 mods)
     keep = {m.names[0] for m in dp.masses[1:5]} | {m.names[0] for m in dp.masses[-3:]}
