@@ -711,6 +711,44 @@ int sst_jaccard_device(sst_table* t, const sst_jaccard_args* a);
 int sst_skeleton_alpha_device(sst_table* t, int64_t n_spec, const int32_t* d_max_len, const uint64_t* d_skel_off,
                               const uint64_t* d_skel, const uint64_t* d_alpha, uint64_t* d_out);
 
+/* After the skeleton (Predictor.predict, prediction.py:88-103), for the
+ * spectra whose Jaccard length stands (status SST_JAC_OK; the others get
+ * active 0 and no rows: predict returns Prediction.default()):
+ * build_skeleton's fragments (skeleton_building.py:67-109) -- rows the START
+ * walk kept (min_end - 1, max_end - 1), rows the END walk kept that START did
+ * not (len - min_end, len - max_end), the alive internal rows whose peak no kept
+ * terminal row shares (0, -1), every end index outside [0, len) clamped to
+ * len - 1 -- in alive_out / min_end_out / max_end_out per row slot, and the
+ * alphabet _reduce_alphabet sets (:99-103): alpha (the Jaccard stage's, as
+ * sst_skeleton_alpha_device gives it) without the modifications the combined
+ * skeleton's positions 0 .. seq_len - 1 do not name.  The caller applies the
+ * reduction's is_valid filter with sst_valid_rows_alpha_device(alpha_out,
+ * active, alive_out).  kept / min_end / max_end are sst_walk_args' [2][slots]
+ * arrays (side-major).  err bit 0: a spectrum of more than 4096 peaks. */
+typedef struct sst_post_args {
+  int64_t n_spec;
+  const int64_t* peak_off;   /* [n_spec + 1] */
+  const uint32_t* rows;      /* [n_spec] */
+  const uint32_t* meta;      /* row slots, as sst_classify_rows_device writes them */
+  const uint8_t* alive;      /* the fixpoint's survivors */
+  const uint8_t* kept;       /* [2][slots] */
+  const int32_t* min_end;    /* [2][slots] */
+  const int32_t* max_end;
+  int64_t slots;
+  const int32_t* seq_len;    /* [n_spec] sst_jaccard_device's */
+  const int8_t* jac_status;  /* [n_spec] */
+  const uint64_t* comb_off;  /* [n_spec] */
+  const uint64_t* comb;
+  const uint64_t* alpha;     /* [2 n_spec] the Jaccard stage's alphabets */
+  uint64_t* alpha_out;       /* [2 n_spec] */
+  uint8_t* active;           /* [n_spec] */
+  uint8_t* alive_out;        /* row slots */
+  int32_t* min_end_out;
+  int32_t* max_end_out;
+  uint32_t* err;
+} sst_post_args;
+int sst_post_skeleton_device(sst_table* t, const sst_post_args* a);
+
 /* compute_sequence_length_bound (mass_table.py:343-487) after the skeleton's
  * alphabet reduction (skeleton_building.py:315-336), both directions, for
  * queries on per-spectrum reduced alphabets, exact without a table rebuild:

@@ -37,7 +37,7 @@ EXPORTS = (
     "sst_skel_walk_device", "sst_result_refs_device", "sst_dict_count_device", "sst_dict_build_device",
     "sst_reach_rows_device", "sst_length_bounds_reach_device", "sst_jaccard_device", "sst_skeleton_alpha_device",
     "sst_dict_list_device", "sst_fix_finish_device", "sst_pipe_reserve_rows", "sst_reach_lowest_device",
-    "sst_length_bounds_frontier_device",
+    "sst_length_bounds_frontier_device", "sst_post_skeleton_device",
 )
 
 # kernel ids of sst_profile_read
@@ -81,6 +81,17 @@ class ExactIO(ctypes.Structure):
                 ("xq_spec", ctypes.c_void_p), ("xq_single", ctypes.c_void_p), ("xq_count", ctypes.c_void_p),
                 ("xq_cap", ctypes.c_uint64), ("xq_block", ctypes.c_void_p), ("xa_st", ctypes.c_void_p),
                 ("xa_n", ctypes.c_void_p), ("xa_ptr", ctypes.c_void_p)]
+
+
+class PostArgs(ctypes.Structure):
+    """sst_post_args (include/sst.h): build_skeleton's fragments and the skeleton-based reduction."""
+    _fields_ = [("n_spec", ctypes.c_int64), ("peak_off", ctypes.c_void_p), ("rows", ctypes.c_void_p),
+                ("meta", ctypes.c_void_p), ("alive", ctypes.c_void_p), ("kept", ctypes.c_void_p),
+                ("min_end", ctypes.c_void_p), ("max_end", ctypes.c_void_p), ("slots", ctypes.c_int64),
+                ("seq_len", ctypes.c_void_p), ("jac_status", ctypes.c_void_p), ("comb_off", ctypes.c_void_p),
+                ("comb", ctypes.c_void_p), ("alpha", ctypes.c_void_p), ("alpha_out", ctypes.c_void_p),
+                ("active", ctypes.c_void_p), ("alive_out", ctypes.c_void_p), ("min_end_out", ctypes.c_void_p),
+                ("max_end_out", ctypes.c_void_p), ("err", ctypes.c_void_p)]
 
 
 class LbfStats(ctypes.Structure):
@@ -270,6 +281,8 @@ def load_library(path=LIB_PATH):
     lib.sst_length_bounds_frontier_device.argtypes = [_P, _P, _P, _P, _P, _P, _P, _I64, _D, _D, _I, _I64, _P, _P,
                                                       _P, _P, _P, _P, _P, _U64, ctypes.POINTER(LbfStats)]
     lib.sst_length_bounds_frontier_device.restype = _I
+    lib.sst_post_skeleton_device.argtypes = [_P, ctypes.POINTER(PostArgs)]
+    lib.sst_post_skeleton_device.restype = _I
     lib.sst_jaccard_device.argtypes = [_P, ctypes.POINTER(JaccardArgs)]
     lib.sst_jaccard_device.restype = _I
     lib.sst_skeleton_alpha_device.argtypes = [_P, _I64, _P, _P, _P, _P, _P]

@@ -2916,14 +2916,23 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
                                               int8_t* d_status, const int32_t* d_qlen, const int32_t* d_caps_len,
                                               const int32_t* d_a0_len, uint64_t* d_nodes, int64_t soft_nodes,
                                               uint32_t memo_first, int fuse) {
-  if (!t || n < 0 || n > INT32_MAX || max_len < 0 || max_len > 120 || (d_qlen && (!d_caps_len || !d_a0_len)) ||
+  if (!t || n < 0 || n > INT32_MAX || max_len < 0 || (d_qlen && (!d_caps_len || !d_a0_len)) ||
       (n > 0 && (!d_su || !d_obs || !d_spec || !d_alpha || !d_reach_bits || !d_reach_off || !d_reach_words ||
                  !d_lower || !d_upper || !d_status)))
     return SST_E_ARG;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (max_len > 120) return fail(c, SST_E_ARG, "length bounds (replay): max_len above 120 (the int8 value slots)");
   if (int rc = set_device(c)) return rc;
   if (n == 0) return SST_OK;
+  // the memo workspace: at most kReachMemoBytes, and at most 60 % of what the
+  // device has free now (a smaller or shared device runs fewer waves)
+  size_t memo_bytes = kReachMemoBytes;
+  {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) memo_bytes = std::min(memo_bytes, fr / 10 * 6);
+    else (void)hipGetLastError();
+  }
   const size_t nn = (size_t)n;
   DevBuf d_list, d_cnt;
   if (!d_list.ensure(nn * 4) || !d_cnt.ensure(4)) return fail(c, SST_E_NOMEM, "device allocation failed (length bound)");
@@ -2977,7 +2986,7 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
   const size_t per_entry = hash_entry_bytes() + (fuse ? 2 * 64 / 4 : kMaxRows);
   uint32_t cap = memo_first ? std::max<uint32_t>(memo_first, 64) : kLBHashCap0;
   auto units_for = [&](uint32_t n_q) {
-    const size_t by_mem = kReachMemoBytes / ((size_t)cap * per_entry);
+    const size_t by_mem = memo_bytes / ((size_t)cap * per_entry);
     return (int)std::max<size_t>(1, std::min<size_t>({(size_t)kReachUnits, (size_t)std::max<uint32_t>(1, n_q), by_mem}));
   };
   int units = units_for(n_exact);
@@ -3000,7 +3009,7 @@ extern "C" int sst_length_bounds_reach_device(sst_table* t, const double* d_su, 
     for (size_t i = 0; i < nn; ++i)
       if (st[i] == kStatusExactRetry) retry.push_back((uint32_t)i);
     if (retry.empty()) break;
-    if ((size_t)cap * 8 * per_entry > kReachMemoBytes)
+    if ((size_t)cap * 8 * per_entry > memo_bytes)
       return fail(c, SST_E_NOMEM, "length bound: memo would exceed the workspace limit");
     cap *= 8;
     units = units_for((uint32_t)retry.size());
@@ -3175,6 +3184,7 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
     const int kw = need <= 256 ? 4 : need <= 512 ? 8 : need <= 1024 ? 16 : 0;
     if (!kw || a.rb > 32) return fail(c, SST_E_ARG, "length bounds (frontier): first-visit keys beyond 1024 bits");
     a.rstride = (int)std::max<uint32_t>(1, h.max_win);
+    a.n_bands = n_bands;
     if (!roots.ensure((size_t)nc * a.rstride * 4))
       return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier roots)");
     a.root_node = (uint32_t*)roots.p;
@@ -3204,7 +3214,7 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
     if (n_bands)
       HIP_OK(c, hipMemcpyAsync(band_groups.data(), bgroups.p, (size_t)n_bands * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
-    if (h.overflow & 24u) return fail(c, SST_E_INTERNAL, "length bounds (frontier): inconsistent first-visit tables");
+    if (h.overflow & 56u) return fail(c, SST_E_INTERNAL, "length bounds (frontier): inconsistent first-visit tables");
     if (h.overflow) {
       if (stats) stats->splits++;
       if (nc == 1) {  // one query beyond the whole workspace: reported, not guessed
@@ -3246,6 +3256,24 @@ extern "C" int sst_jaccard_device(sst_table* t, const sst_jaccard_args* a) {
   if (int rc = set_device(c)) return rc;
   Prof p(c, SST_K_JACCARD);
   HIP_OK(c, sst::launch_jaccard(*a, c->stream));
+  return SST_OK;
+}
+
+extern "C" int sst_post_skeleton_device(sst_table* t, const sst_post_args* a) {
+  if (!t || !a || a->n_spec < 0) return SST_E_ARG;
+  if (a->n_spec == 0) return SST_OK;
+  if (!a->peak_off || !a->rows || !a->meta || !a->alive || !a->kept || !a->min_end || !a->max_end || a->slots < 0 ||
+      !a->seq_len || !a->jac_status || !a->comb_off || !a->comb || !a->alpha || !a->alpha_out || !a->active ||
+      !a->alive_out || !a->min_end_out || !a->max_end_out || !a->err)
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  uint64_t canon[2] = {0, 0};
+  for (int r = 1; r < t->n_rows; ++r)
+    if (!t->is_mod[r]) canon[r >> 6] |= 1ull << (r & 63);
+  Prof p(c, SST_K_JACCARD);
+  HIP_OK(c, sst::launch_post_skel(*a, canon[0], canon[1], 4 * c->n_cu, c->stream));
   return SST_OK;
 }
 

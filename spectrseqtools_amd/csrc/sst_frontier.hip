@@ -469,6 +469,7 @@ __global__ void k_lbf_mark(FrontierArgs a, int band) {
 __global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
   if (__hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const uint32_t s0 = a.band_start[band], s1 = a.band_start[band + 1];
+  const uint32_t n_nodes = a.band_start[a.n_bands];  // every id below is a node of this chunk
   const uint32_t nth = gridDim.x * blockDim.x;
   for (uint32_t x0 = s0 + blockIdx.x * blockDim.x + threadIdx.x; x0 < s1; x0 += nth) {
     uint8_t f = a.flags[x0];
@@ -487,7 +488,11 @@ __global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
       if (f & kFLeft) {
         int cl = 1, ch = 1;  // a left move onto mass 0: 0 + 1
         if (!(f & kFZero)) {
-          const uint32_t c = a.lchild[x];
+          uint32_t c = a.lchild[x];
+          if (c >= n_nodes || c < s1) {  // a left child lies in a later band: never unset or stale
+            set_overflow(a, 32);
+            c = x;
+          }
           const int l = (int)a.vlo[c] + 1;
           cl = l > 255 ? 255 : l;
           ch = (int)a.vhi[c] + 1;  // -1 + 1 = 0 (the reference's default feeds the max)
@@ -519,7 +524,11 @@ __global__ __launch_bounds__(256) void k_lbf_out(FrontierArgs a) {
   const int top = (int)q.K - 1;
   for (int64_t v = q.lo < 1 ? 1 : q.lo; v <= q.hi; ++v) {
     if (top < 0 || (int)a.lr[q.lr_off + v] > top) continue;  // pair(top, v) == 0: the default
-    const uint32_t id = a.root_node[(size_t)jj * a.rstride + (size_t)(v - q.lo)];
+    uint32_t id = a.root_node[(size_t)jj * a.rstride + (size_t)(v - q.lo)];
+    if (id >= a.band_start[a.n_bands]) {  // every reachable root is a band-0 node
+      set_overflow(a, 32);
+      return;
+    }
     const int l = a.vlo[id], h = a.vhi[id];
     bl = l < bl ? l : bl;
     bh = h > bh ? h : bh;

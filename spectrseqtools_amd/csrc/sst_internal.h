@@ -311,7 +311,7 @@ struct FQInfo {       // per listed query of a chunk
 };
 struct FCtl {
   uint32_t node_ctr;
-  uint32_t overflow;  // bit 0 nodes, 1 a hash table, 2 a band list, 3/4 internal
+  uint32_t overflow;  // bit 0 nodes, 1 a hash table, 2 a band list, 3/4/5 internal
   uint32_t list_cnt[8];
   uint32_t max_band, max_win, max_k, pad;
   uint64_t max_hi;
@@ -334,6 +334,7 @@ struct FrontierArgs {
   int ring, jump;  // hash / list ring size (power of two > jump), max bands one left move crosses
   int rb, cb;      // key fields: root index bits, bits per rank count
   int rstride;     // root slots per query
+  int n_bands;     // band_start[n_bands] = the chunk's node count (after the last band)
   FQInfo* qi;
   uint32_t* qrow;  // [n_chunk][128]: rank -> w | cap << 20 | is_mod << 28
   uint32_t* root_node;
@@ -610,6 +611,7 @@ enum { kWalkDone = SST_WALK_DONE, kWalkSuspended = SST_WALK_SUSPENDED, kWalkBig 
 using WalkArgs = sst_walk_args;
 hipError_t launch_skel_walk(const TableArgs& t, const WalkArgs& a, hipStream_t st);
 hipError_t launch_jaccard(const sst_jaccard_args& a, hipStream_t st);
+hipError_t launch_post_skel(const sst_post_args& a, uint64_t canon0, uint64_t canon1, int n_wg, hipStream_t st);
 hipError_t launch_skel_alpha(int64_t n_spec, const int32_t* max_len, const uint64_t* skel_off, const uint64_t* skel,
                              const uint64_t* alpha, uint64_t canon0, uint64_t canon1, uint64_t* out, hipStream_t st);
 hipError_t launch_result_refs(const int8_t* status, int64_t n, const uint4* hits, uint64_t n_hits,

@@ -621,6 +621,7 @@ struct Hash {
   int8_t* vals_lo = nullptr;
   int8_t* vals_hi = nullptr;
   int dflt_lo = 0;
+  bool vals_bad = false;  // fused values: a visited child had no memo entry (reported as SST_ABORTED)
   bool dense = false;  // fused values: entry i's values at slot pad (its insertion order) x kValSlots + kept rank
   __device__ __forceinline__ uint32_t slot(uint32_t m) const { return (m * 0x9E3779B1u) & mask; }
   // returns entry pointer or nullptr if absent
@@ -1236,13 +1237,14 @@ __device__ __forceinline__ M128 p1_classify(const TableArgs& t, const Lds& s, Ha
 // child's value at row r plus one.  Values are kept for the alphabet's rows
 // only, at slot kept-rank (a dropped row's value is the nearest kept row's
 // below it), per entry in insertion order: 2 x kValSlots bytes per mass.
-__device__ __forceinline__ void p1_values(const TableArgs& t, const Lds& s, const Hash& h, const HEntry* e, uint32_t m,
+__device__ __forceinline__ void p1_values(const TableArgs& t, const Lds& s, Hash& h, const HEntry* e, uint32_t m,
                                           int rlo, int rtop) {
   const int lane = threadIdx.x & 63;
   const int lo = (int)((e->meta >> 16) & 0xFF);
   const M128 en{e->en0, e->en1};
   int cl[2] = {127, 127}, ch[2] = {-128, -128};
   int rk[2] = {h.rv.rank0, h.rv.rank1};
+  bool miss = false;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int r = lane + 64 * half;
@@ -1255,12 +1257,15 @@ __device__ __forceinline__ void p1_values(const TableArgs& t, const Lds& s, cons
           const size_t at = (size_t)ce->pad * kValSlots + rk[half];
           vl = h.vals_lo[at];
           vh = h.vals_hi[at];
+        } else {
+          miss = true;  // phase 1 memoises every child it enters: reported, not guessed (lb_uncomputed's -3)
         }
       }
       cl[half] = vl + 1;
       ch[half] = vh + 1;
     }
   }
+  if (__ballot(miss)) h.vals_bad = true;
   const size_t base = (size_t)e->pad * kValSlots;
   // the seed: the value at row rlo - 1, i.e. at the highest kept row below rlo (if >= lo)
   const uint64_t below0 = rlo >= 64 ? ~0ull : ((1ull << rlo) - 1ull);
@@ -3137,7 +3142,9 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
         __syncthreads();
       }
     }
+    h.vals_bad = false;
     int rc = phase1<WAVE>(t, s, h, fr, a, hi, A0, q.node_budget, nodes, am);
+    if (rc == 0 && h.vals_bad) rc = -4;  // SST_ABORTED below
     if (q.nodes_out && (!WAVE || threadIdx.x == 0)) q.nodes_out[i] += nodes;
     if (rc == -1) {
       q.status[i] = (int8_t)kStatusExactRetry;

@@ -324,11 +324,26 @@ __global__ __launch_bounds__(256) void k_skel_walk(TableArgs t, WalkArgs a) {
     const int e0 = cur0, e1 = joined ? (int)f + 1 : (int)f;
     const int ne = e1 - e0;
     const bool first = pb0 < 0;
-    const bool spec = first ? lv0 < 0 : lv0 == pb0;  // the bin pair stage 3 answered
+    bool spec = first ? lv0 < 0 : lv0 == pb0;  // the bin pair stage 3 answered
     const uint32_t spec_base = spec_ctr;
     spec_ctr += first ? (uint32_t)ne : (uint32_t)((pb1 - pb0) * ne);
     const int p0 = lv0, p1 = lv1;
     const uint32_t nq = p0 < 0 ? (uint32_t)ne : (uint32_t)((p1 - p0) * ne);
+    // stage 3 answered each window at the bin's own threshold; a difference
+    // the final dict holds is answered at the dict writer's threshold
+    // (explain_mass_difference, skeleton_building.py:429-430).  Where the two
+    // differ and the walk does not answer the window itself (not pair class:
+    // exact-mode spectra), stage 3's answer is not the reference's: the bin
+    // is re-queried instead
+    for (uint32_t j = 0; j < nq && spec; ++j) {
+      double diff, thr, te;
+      bin_query(R, p0, p1, e0, e1, j, a.tol, diff, thr);
+      if (dict_thr(a, g, diff, te) && te != thr) {
+        double lof, hif;
+        quantise_lean(diff, te, a.prec, a.rprec, lof, hif);
+        if (!(pair_ok && hif < pair_hi)) spec = false;
+      }
+    }
     // re-query: its DFS windows must have been answered
     int res = kBinNone;
     if (!spec) {
@@ -697,6 +712,96 @@ hipError_t launch_skel_alpha(int64_t n_spec, const int32_t* max_len, const uint6
   if (n_spec <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_skel_alpha, dim3((unsigned)((n_spec + 255) / 256)), dim3(256), 0, st, n_spec, max_len,
                      skel_off, skel, alpha, canon0, canon1, out);
+  return hipGetLastError();
+}
+
+// After the skeleton (prediction.py:88-103): build_skeleton's fragment
+// bookkeeping (skeleton_building.py:67-109) -- the START walk's kept rows
+// (min_end / max_end - 1), the END walk's kept rows not already kept at START
+// (len - min_end / len - max_end), the internal rows whose peak no kept
+// terminal row shares, every end index outside [0, len) clamped to len - 1
+// -- and the alphabet _reduce_alphabet then sets: the Jaccard stage's
+// alphabet with the modifications the combined skeleton does not name dropped
+// (mass_table.py:94-100).  One workgroup per spectrum; the peaks of kept
+// terminal rows as an LDS bitmap.  The caller then runs is_valid on that
+// alphabet (sst_valid_rows_alpha_device) over alive_out.
+constexpr int kPostPeaks = 4096;
+__global__ __launch_bounds__(256) void k_post_skel(sst_post_args a, uint64_t canon0, uint64_t canon1) {
+  __shared__ uint32_t peaks[kPostPeaks / 32];
+  __shared__ uint64_t names[2];
+  for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
+    const int64_t off = 4 * a.peak_off[g];
+    const int n = (int)a.rows[g];
+    const int64_t np = a.peak_off[g + 1] - a.peak_off[g];
+    const bool ok = a.jac_status[g] == SST_JAC_OK && np <= kPostPeaks;
+    if (threadIdx.x == 0) {
+      if (a.jac_status[g] == SST_JAC_OK && np > kPostPeaks) atomicOr(a.err, 1u);
+      a.active[g] = ok ? 1 : 0;
+      names[0] = names[1] = 0;
+    }
+    if (!ok) {  // build_skeleton raised: predict returns Prediction.default() (:89-94)
+      for (int i = threadIdx.x; i < n; i += blockDim.x) a.alive_out[off + i] = 0;
+      if (threadIdx.x == 0) {
+        a.alpha_out[2 * g] = a.alpha[2 * g];
+        a.alpha_out[2 * g + 1] = a.alpha[2 * g + 1];
+      }
+      __syncthreads();
+      continue;
+    }
+    const int L = a.seq_len[g];
+    for (int w = threadIdx.x; w < kPostPeaks / 32; w += blockDim.x) peaks[w] = 0;
+    __syncthreads();
+    const uint8_t* kept_s = a.kept;
+    const uint8_t* kept_e = a.kept + a.slots;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t m = a.meta[off + i];
+      const bool al = a.alive[off + i] != 0;
+      const bool st = al && ((m >> 2) & 1u) && kept_s[off + i];
+      const bool en = al && ((m >> 3) & 1u) && kept_e[off + i] && !st;
+      if (st || en) atomicOr(&peaks[(m >> 8) >> 5], 1u << ((m >> 8) & 31u));
+    }
+    // the combined skeleton's names (positions 0 .. len - 1)
+    const uint64_t* cb = a.comb + 2 * a.comb_off[g];
+    uint64_t u0 = 0, u1 = 0;
+    for (int i = threadIdx.x; i < L; i += blockDim.x) {
+      u0 |= cb[2 * i];
+      u1 |= cb[2 * i + 1];
+    }
+    if (u0) atomicOr((unsigned long long*)&names[0], (unsigned long long)u0);
+    if (u1) atomicOr((unsigned long long*)&names[1], (unsigned long long)u1);
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint32_t m = a.meta[off + i];
+      const bool al = a.alive[off + i] != 0;
+      const bool st = al && ((m >> 2) & 1u) && kept_s[off + i];
+      const bool en = al && ((m >> 3) & 1u) && kept_e[off + i] && !st;
+      const bool internal = al && !((m >> 2) & 3u);
+      const bool fin = st || en || (internal && !((peaks[(m >> 8) >> 5] >> ((m >> 8) & 31u)) & 1u));
+      int lo = 0, hi = -1;  // Predictor.predict's initial columns (prediction.py:76-79)
+      if (st) {
+        lo = a.min_end[off + i] - 1;
+        hi = a.max_end[off + i] - 1;
+      } else if (en) {
+        lo = L - a.min_end[a.slots + off + i];
+        hi = L - a.max_end[a.slots + off + i];
+      }
+      if (lo < 0 || lo >= L) lo = L - 1;
+      if (hi < 0 || hi >= L) hi = L - 1;
+      a.alive_out[off + i] = fin ? 1 : 0;
+      a.min_end_out[off + i] = lo;
+      a.max_end_out[off + i] = hi;
+    }
+    if (threadIdx.x == 0) {
+      a.alpha_out[2 * g] = a.alpha[2 * g] & (canon0 | names[0]);
+      a.alpha_out[2 * g + 1] = a.alpha[2 * g + 1] & (canon1 | names[1]);
+    }
+    __syncthreads();
+  }
+}
+hipError_t launch_post_skel(const sst_post_args& a, uint64_t canon0, uint64_t canon1, int n_wg, hipStream_t st) {
+  if (a.n_spec <= 0) return hipSuccess;
+  const int64_t g = a.n_spec < (int64_t)n_wg ? a.n_spec : (int64_t)n_wg;
+  hipLaunchKernelGGL(k_post_skel, dim3((unsigned)g), dim3(256), 0, st, a, canon0, canon1);
   return hipGetLastError();
 }
 

@@ -644,7 +644,7 @@ class DeviceSkeleton:
 
 @_one_stream
 def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, tolerance=None, caps=(64, 32),
-                    big_caps=(8192, 8192), max_rounds=4096):
+                    big_caps=(8192, 8192), max_rounds=4096, name_hash=None):
     """Stage 4 on the device: SkeletonBuilder._predict_skeleton for the START
     and END rows of every spectrum (the rows the fixpoint kept, its final
     alphabets `alpha` [S, 2] u64), with filter_by_explanation's final dict.
@@ -652,7 +652,10 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
     when None).  caps = (explanations per bin, candidates per query) of the
     lanes' scratch; sides that outgrow them are walked again with big_caps.
     max_rounds bounds the re-query rounds (each answers every suspended side's
-    next re-query bin)."""
+    next re-query bin).  name_hash: hash() of each row's nucleoside name (the
+    reference's set order, common.py:60-65); None = this interpreter's
+    (name_hashes).  A sharded run passes rank 0's to every rank, so that
+    every spectrum's walk follows one interpreter's order."""
     import torch
 
     tolerance = dp_table.tolerance if tolerance is None else tolerance
@@ -692,7 +695,9 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
     side_rows = torch.zeros(2 * slots, dtype=torch.int16, device=dev)
     status = torch.zeros(max(1, 2 * S), dtype=torch.uint8, device=dev)
     ctl = torch.zeros(3, dtype=torch.int32, device=dev)  # suspended, big, request count
-    nh = torch.as_tensor(name_hashes(dp_table), device=dev)
+    # the names' str hashes fix the explanation sets' iteration order: this
+    # interpreter's, or the caller's (a sharded run uses rank 0's on every rank)
+    nh = torch.as_tensor(name_hashes(dp_table) if name_hash is None else np.asarray(name_hash, np.int64), device=dev)
     ml_max = int(max_len.max()) if S else 1
     len_cap = ml_max + 2
     if len_cap > 128:
@@ -889,6 +894,10 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
     ml_hi = int(ml[sel].max()) if len(sel) else 1
     if caps_len.shape[0] <= ml_hi or len(a0_len) <= ml_hi or caps_len.shape[1] != _native.MAX_ROWS:
         raise ValueError("length bounds: caps_len / a0_len must cover every max_len")
+    # value ranges: the replay's int8 value slots hold max_len + 1 for max_len <= 120 (sst_api.cpp), the
+    # frontier's u8 lower values max_len + 1 <= 254
+    if ml_hi > (120 if engine == "replay" else 253):
+        raise NotImplementedError(f"length bounds ({engine}): max_len {ml_hi} above the engine's limit")
     caps_t = torch.as_tensor(caps_len, device=dev)
     a0_t = torch.as_tensor(np.asarray(a0_len, np.int32), device=dev)
     dt.set_budgets(is_mod, [int(c) for c in caps_len[ml_hi, :len(masses)]])  # the rows' modification flags
@@ -1110,8 +1119,6 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     # budgets by max_len (mass_explanation.py:158-172 as set_budgets): caps
     # round(L * rate) per row, max_modifications round(modification_rate * L)
     ml_hi = int(ml[sel].max()) if len(sel) else 1
-    if ml_hi >= 128:
-        raise NotImplementedError("length bounds: max_len above 127")
     caps_len = np.zeros((ml_hi + 1, _native.MAX_ROWS), np.int32)
     for Lm in range(ml_hi + 1):
         caps_len[Lm, :len(masses)] = [min(round(Lm * m.modification_rate), 1 << 30) for m in masses]
@@ -1144,17 +1151,88 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
 
 
 # ---------------------------------------------------------------------------
+# After the skeleton: build_skeleton's fragments and the skeleton-based
+# alphabet reduction (prediction.py:88-103, skeleton_building.py:67-109)
+# ---------------------------------------------------------------------------
+@dataclass
+class DevicePost:
+    alpha: np.ndarray   # [S, 2] u64 the alphabet after _reduce_alphabet(skeleton nucleotides)
+    active: np.ndarray  # [S] 1: the spectrum reached the reduction (its Jaccard length stands)
+    alive: object       # torch uint8 row slots: the fragments after the reduction's is_valid filter
+    alive_skeleton: object  # torch uint8 row slots: build_skeleton's fragments (before the filter)
+    min_end: object     # torch int32 row slots (build_skeleton's, clamped to [0, len))
+    max_end: object
+    rows_before: int    # fragments build_skeleton returned (all spectra)
+    rows_after: int     # after the is_valid filter
+
+
+@_one_stream
+def post_skeleton_device(dp_table, rows: DeviceRows, sk: DeviceSkeleton, ln: DeviceLength, tolerance=None):
+    """Predictor.predict after build_skeleton (prediction.py:88-103), every
+    spectrum at once: build_skeleton's fragments -- the START walk's kept
+    rows, the END walk's kept rows START did not keep, the internal rows no
+    kept terminal row shares a peak with, min_end / max_end as
+    skeleton_building.py:67-109 sets them (sst_post_skeleton_device) -- then
+    _reduce_alphabet on the combined skeleton's nucleotides: the alphabet
+    without the modifications the skeleton does not name, and is_valid_mass of
+    every remaining fragment on it (sst_valid_rows_alpha_device, :204-227)."""
+    import torch
+
+    dt = dp_table.device_table
+    eng = dt.engine
+    L = eng._lib
+    h = dt.handle
+    S = len(sk.max_len)
+    dev = sk.skel.device
+    tol = dp_table.tolerance if tolerance is None else tolerance
+    slots = int(rows.alive.numel())
+    i32 = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.int32), device=dev)  # noqa: E731
+    seq_len = i32(ln.seq_len)
+    jst = torch.as_tensor(np.ascontiguousarray(ln.status, dtype=np.int8), device=dev)
+    comb_off = torch.as_tensor(np.ascontiguousarray(ln.comb_off[:-1] if len(ln.comb_off) > S else ln.comb_off,
+                                                    dtype=np.int64), device=dev)
+    alpha = torch.as_tensor(np.ascontiguousarray(ln.alpha).view(np.int64), device=dev)
+    alpha_out = torch.empty_like(alpha)
+    active = torch.zeros(max(1, S), dtype=torch.uint8, device=dev)
+    alive_out = torch.zeros_like(rows.alive)
+    min_out = torch.zeros(slots, dtype=torch.int32, device=dev)
+    max_out = torch.zeros(slots, dtype=torch.int32, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    a = _native.PostArgs(S, rows.peak_off.data_ptr(), rows.rows.data_ptr(), rows.meta.data_ptr(),
+                         rows.alive.data_ptr(), sk.kept.data_ptr(), sk.min_end.data_ptr(), sk.max_end.data_ptr(), slots,
+                         seq_len.data_ptr(), jst.data_ptr(), comb_off.data_ptr(), ln.comb.data_ptr(), alpha.data_ptr(),
+                         alpha_out.data_ptr(), active.data_ptr(), alive_out.data_ptr(), min_out.data_ptr(),
+                         max_out.data_ptr(), err.data_ptr())
+    eng.check(L.sst_post_skeleton_device(h, ctypes.byref(a)), "sst_post_skeleton_device")
+    alive_skel = alive_out.clone()
+    before = int(alive_out.sum().item())
+    err2 = torch.zeros(1, dtype=torch.int32, device=dev)
+    eng.check(L.sst_valid_rows_alpha_device(h, rows.peak_off.data_ptr(), S, rows.su.data_ptr(), rows.obs.data_ptr(),
+                                            rows.rows.data_ptr(), alpha_out.data_ptr(), active.data_ptr(),
+                                            alive_out.data_ptr(), float(tol), float(dp_table.precision),
+                                            err2.data_ptr()), "sst_valid_rows_alpha_device")
+    eng.synchronize()
+    if int(err.item()):
+        raise _native.EngineError("post-skeleton stage: a spectrum of more than 4096 peaks")
+    _check_err(err2)
+    return DevicePost(alpha_out.cpu().numpy().view(np.uint64)[:S].copy(), active.cpu().numpy()[:S].copy(),
+                      alive_out, alive_skel, min_out, max_out, before, int(alive_out.sum().item()))
+
+
+# ---------------------------------------------------------------------------
 # Per-spectrum outcomes, packed for the gather to rank 0 (config 5 on N GPUs)
 # ---------------------------------------------------------------------------
 OUTCOME_MAGIC = 0x35435453  # "STC5"
 
 
-def pack_outcomes(rows: DeviceRows, fx, sk: DeviceSkeleton, ln: DeviceLength):
+def pack_outcomes(rows: DeviceRows, fx, sk: DeviceSkeleton, ln: DeviceLength, post=None):
     """One rank's config-5 outcome per spectrum as one uint8 device tensor:
     the fixpoint's and the skeleton's alphabets, both length bounds and their
     status, the Jaccard length and status, the walk's per-side status, the
-    rows each side's walk kept (a bit per row slot), and the combined
-    skeleton (max_len positions reserved per spectrum, seq_len used)."""
+    rows each side's walk kept (a bit per row slot), the combined skeleton
+    (max_len positions reserved per spectrum, seq_len used), and with `post`
+    (post_skeleton_device) the alphabet after the skeleton-based reduction
+    and the fragments that survive it (a bit per row slot)."""
     import torch
 
     dev = sk.skel.device
@@ -1167,12 +1245,22 @@ def pack_outcomes(rows: DeviceRows, fx, sk: DeviceSkeleton, ln: DeviceLength):
         kept = torch.cat([kept, torch.zeros(pad, dtype=torch.uint8, device=dev)])
     weights = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.int32, device=dev)
     kept_bits = (kept.view(-1, 8).to(torch.int32) * weights).sum(dim=1).to(torch.uint8)
+    def bits(flags):
+        f = flags.reshape(-1)
+        pad = (-f.numel()) % 8
+        if pad:
+            f = torch.cat([f, torch.zeros(pad, dtype=torch.uint8, device=dev)])
+        return (f.view(-1, 8).to(torch.int32) * weights).sum(dim=1).to(torch.uint8)
+
+    post_bits = bits(post.alive & rows.alive) if post is not None else None
     head = np.array([OUTCOME_MAGIC, S, int(rows.su.numel()), int(sk.skel_off[-1]), int(ln.comb_off[-1]),
-                     int(kept_bits.numel()), 0, 0], dtype=np.int64)
+                     int(kept_bits.numel()), 0 if post is None else int(post_bits.numel()), 0], dtype=np.int64)
     parts = [host(head), host(np.asarray(fx.alpha, dtype=np.uint64).view(np.int64)),
              host(ln.alpha.view(np.int64)), host(ln.lower), host(ln.upper), host(ln.lb_status),
              host(ln.seq_len.astype(np.int32)), host(ln.status), host(sk.status), host(sk.max_len.astype(np.int32)),
              ln.comb[:int(ln.comb_off[-1])], kept_bits]
+    if post is not None:
+        parts += [host(post.alpha.view(np.int64)), host(post.active.astype(np.uint8)), post_bits]
     return torch.cat([u8(p) for p in parts])
 
 
@@ -1182,7 +1270,7 @@ def unpack_outcomes(buf):
     head = b[:64].view(np.int64)
     if int(head[0]) != OUTCOME_MAGIC:
         raise ValueError("not a config-5 outcome buffer")
-    S, slots, _, n_comb, n_kept = (int(x) for x in head[1:6])
+    S, slots, _, n_comb, n_kept, n_post = (int(x) for x in head[1:7])
     o = 64
     out = {}
 
@@ -1204,6 +1292,12 @@ def unpack_outcomes(buf):
     take("combined", np.uint64, 2 * n_comb)
     take("kept_bits", np.uint8, n_kept)
     out["kept"] = np.unpackbits(out.pop("kept_bits"), bitorder="little")[:2 * slots].reshape(2, slots)
+    if n_post:
+        take("alpha_post", np.uint64, 2 * S)
+        take("post_active", np.uint8, S)
+        take("post_bits", np.uint8, n_post)
+        out["alpha_post"] = out["alpha_post"].reshape(S, 2)
+        out["post_alive"] = np.unpackbits(out.pop("post_bits"), bitorder="little")[:slots]
     out["alpha"] = out["alpha"].reshape(S, 2)
     out["alpha_skeleton"] = out["alpha_skeleton"].reshape(S, 2)
     out["combined"] = out["combined"].reshape(-1, 2)

@@ -12,13 +12,15 @@ insertion order and overwrite semantics; each value is the list
 calculate_explanations returns (its order is the reference's set iteration
 order, i.e. hash-seed dependent in the reference too).
 
-predict() and filter_with_lp() need the MILP (linear_program.py: pulp/CBC),
-which is outside the hot path and absent from this image.
+predict()'s MILP stages -- filter_with_lp() and the final
+LinearProgramInstance (linear_program.py: pulp/CBC) -- are outside the hot
+path and absent from this image; predict_skeleton_stage() runs predict up to
+them (:63-103).
 """
 import numpy as np
 
 from .common import calculate_explanations_batch
-from .frame import as_columns, like
+from .frame import Frame, as_columns, like
 from .mass_explanation import is_valid_masses
 from .masses import PHOSPHATE_LINK_MASS
 from ._native import window_pairs
@@ -99,6 +101,31 @@ class Predictor:
             }
             fragments = self._reduce_alphabet(observed_nucleotides, fragments)
         return fragments, explanations
+
+    def predict_skeleton_stage(self, fragments, solver_params=None, record=None):
+        """Predictor.predict up to its MILP stages (prediction.py:63-103): the
+        framing (index, min_end 0, max_end -1), filter_by_explanation,
+        SkeletonBuilder.build_skeleton (the MILP-free path, see
+        skeleton_building), then _reduce_alphabet on the combined skeleton's
+        nucleotides.  Returns (skeleton_seq, fragments), or None where predict
+        returns Prediction.default() because build_skeleton raised (:89-94).
+        filter_with_lp and the final LinearProgramInstance need pulp/CBC.
+        record (a dict, optional) receives build_skeleton's fragments."""
+        from .skeleton_building import SkeletonBuilder
+
+        f = Frame(as_columns(fragments)).with_row_index("orig_index").sort("standard_unit_mass")
+        f = f.with_row_index("index")
+        f = f.with_columns(min_end=[0] * len(f), max_end=[-1] * len(f))
+        f, explanations = self.filter_by_explanation(f)
+        try:
+            skeleton_seq, f = SkeletonBuilder(explanations=explanations, dp_table=self.dp_table).build_skeleton(
+                f, solver_params)
+        except Exception:  # noqa: BLE001 -- prediction.py:93-94
+            return None
+        if record is not None:
+            record["build_skeleton"] = f
+        nucleotides = {nuc for skeleton_pos in skeleton_seq for nuc in skeleton_pos}
+        return skeleton_seq, self._reduce_alphabet(nucleotide_list=nucleotides, fragments=f)
 
     def _reduce_alphabet(self, nucleotide_list, fragments):
         """prediction.py:204-227: alphabet reduction (a GPU table rebuild when

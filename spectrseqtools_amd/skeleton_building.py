@@ -19,8 +19,12 @@ explanation (the reference then pairs it with an older bin).  Whole-fragment
 masses of the first bin and wide differences leave the LDS pair path: these
 are the engine's deferred DFS kernels (k_explain_deferred).
 
-build_skeleton / select_sequence_length_with_lp / determine_lp_score need the
-MILP (pulp/CBC), outside the hot path and absent from this image.
+select_sequence_length_with_lp / determine_lp_score need the MILP (pulp/CBC),
+outside the hot path and absent from this image.  build_skeleton (:26-112)
+is mirrored with the length the reference selects when no LP instance can be
+built -- determine_lp_score's `except Exception: return np.inf` (:279-286)
+for every candidate length, so select_sequence_length_with_lp returns -1 and
+the Jaccard selection decides (:52-57) -- which is config 5's MILP-free path.
 """
 from dataclasses import dataclass, field
 from itertools import chain, groupby
@@ -38,6 +42,47 @@ class SkeletonBuilder:
     explanations: dict  # diff -> explanation list (Predictor.filter_by_explanation); the reference's cache
     dp_table: DynamicProgrammingTable
     engine_calls: int = field(default=0, repr=False)  # batched explain calls made (measurement)
+
+    def build_skeleton(self, fragments, solver_params=None):
+        """skeleton_building.py:26-112 on the MILP-free path (module note):
+        both sides' skeletons, the Jaccard length, the combined skeleton, and
+        the fragments: the START walk's kept rows (min_end / max_end - 1), the
+        END walk's kept rows START did not keep (len - min_end / len -
+        max_end), the internal rows whose fragment_index no kept terminal row
+        has, end indices outside [0, len) clamped to len - 1, sorted by index.
+        Raises as the reference does when no length fits (predict then returns
+        its default prediction)."""
+        if not isinstance(fragments, Frame):
+            sk, fr = self.build_skeleton(Frame(as_columns(fragments)), solver_params)
+            return sk, like(fragments, fr.to_dict())
+        brk = fragments["breakage"]
+        start_sk, start_fr = self._predict_skeleton(
+            fragments.filter_mask(["START" in b for b in brk]),
+            skeleton_seq=[set() for _ in range(self.dp_table.seq.max_len)])
+        end_sk, end_fr = self._predict_skeleton(
+            fragments.filter_mask(["END" in b for b in brk]),
+            skeleton_seq=[set() for _ in range(self.dp_table.seq.max_len)])
+        end_sk = end_sk[::-1]
+        seq_len = self.select_sequence_length_with_jaccard(start_skeleton=start_sk, end_skeleton=end_sk)
+        skeleton_seq = combine_skeleton_sequences(seq_len=seq_len, start_skeleton=start_sk, end_skeleton=end_sk)
+        n = len(skeleton_seq)
+        start_idx = set(start_fr["index"])
+        end_fr = end_fr.filter_mask([i not in start_idx for i in end_fr["index"]])
+        start_fr = start_fr.with_columns(min_end=[x - 1 for x in start_fr["min_end"]],
+                                         max_end=[x - 1 for x in start_fr["max_end"]])
+        end_fr = end_fr.with_columns(min_end=[n - x for x in end_fr["min_end"]],
+                                     max_end=[n - x for x in end_fr["max_end"]])
+        terminal = {k: start_fr[k].to_list() + end_fr[k].to_list() for k in fragments.columns}
+        term_peaks = set(terminal["fragment_index"])
+        internal = fragments.filter_mask([("START" not in b and "END" not in b) and fi not in term_peaks
+                                          for b, fi in zip(brk, fragments["fragment_index"])])
+        merged = Frame({k: internal[k].to_list() + terminal[k] for k in fragments.columns}).sort("index")
+
+        def clamp(v):
+            return [n - 1 if (x < 0 or x >= n) else x for x in v]
+
+        merged = merged.with_columns(min_end=clamp(merged["min_end"]), max_end=clamp(merged["max_end"]))
+        return skeleton_seq, merged
 
     # -- single queries, as the reference -----------------------------------
     def explain_mass_difference(self, diff: float, prev_mass: float, current_mass: float) -> List[Explanation]:

@@ -268,6 +268,31 @@ def check_skeleton_vs_reference(rec, dp, frags, expl):
     return seq_len
 
 
+def check_predict_skeleton_stage(rec, dp, classified):
+    """Predictor.predict_skeleton_stage (the mirror of predict up to its MILP
+    stages) == the reference's predict observed at the skeleton-based
+    reduction (post_skeleton.json.gz): build_skeleton's fragments, then the
+    alphabet and the fragments after _reduce_alphabet (prediction.py:88-103)."""
+    from conftest import load_golden
+    from spectrseqtools_amd.prediction import Predictor
+
+    want = load_golden("post_skeleton.json.gz")[rec["_tc"]]
+    rec_ = {}
+    out = Predictor(dp, EXPLANATION_MASSES).predict_skeleton_stage(classified, record=rec_)
+    if want["default"]:
+        assert out is None
+        return None
+    sk, fr = out
+    assert [sorted(p) for p in sk] == want["build_skeleton"]["skeleton"]
+    for key, frame in (("build_skeleton", rec_["build_skeleton"]), ("reduction", fr)):
+        w = want[key]["fragments"]
+        assert frame.get_column("index").to_list() == w["index"], key
+        assert frame.get_column("min_end").to_list() == w["min_end"], key
+        assert frame.get_column("max_end").to_list() == w["max_end"], key
+    assert [m.mass for m in dp.masses] == want["reduction"]["masses"]
+    return out
+
+
 def device_pipeline_skeleton(rec, dp):
     """The device-resident stages on one reference spectrum, in its own peak
     order: classify_device -> fixpoint_device -> bins_device (with the masked
@@ -326,4 +351,33 @@ def check_skeleton_device_vs_reference(rec, dp):
         assert got_c == j["combined"]
     else:
         assert int(ln.status[0]) == _native.JAC_NO_LENGTH, (int(ln.status[0]), j["error"])
+    check_post_skeleton_vs_reference(rec, dp, rows, sk, ln)
     return sk
+
+
+def check_post_skeleton_vs_reference(rec, dp, rows, sk, ln):
+    """post_skeleton_device == the reference's Predictor.predict after the
+    skeleton (post_skeleton.json.gz, tests/golden/make_post_golden.py):
+    build_skeleton's fragments (index, min_end, max_end) and, after
+    _reduce_alphabet on the combined skeleton's nucleotides, the alphabet and
+    the kept fragments (prediction.py:88-103)."""
+    from conftest import load_golden
+    from spectrseqtools_amd import pipeline_device as PD
+    from spectrseqtools_amd.pipeline import mask_rows
+
+    want = load_golden("post_skeleton.json.gz")[rec["_tc"]]
+    post = PD.post_skeleton_device(dp, rows, sk, ln)
+    if want["default"]:  # build_skeleton raised: Prediction.default()
+        assert int(post.active[0]) == 0
+        return post
+    assert int(post.active[0]) == 1
+    n = int(rows.rows[0].item())
+    for key, alive in (("build_skeleton", post.alive_skeleton), ("reduction", post.alive)):
+        fr = want[key]["fragments"]
+        idx = np.flatnonzero(alive[:n].cpu().numpy())
+        assert idx.tolist() == fr["index"], (key, idx.tolist(), fr["index"])
+        assert post.min_end[idx].cpu().numpy().tolist() == fr["min_end"], key
+        assert post.max_end[idx].cpu().numpy().tolist() == fr["max_end"], key
+    kept = mask_rows(post.alpha, len(dp.masses))[0]
+    assert [0] + [dp.masses[r].mass for r in range(1, len(dp.masses)) if kept[r]] == want["reduction"]["masses"]
+    return post

@@ -36,14 +36,17 @@ def main():
 
         engine = _native.get_engine(0)
     rec = load_golden("callers.json.gz")[tc]
+    rec["_tc"] = tc
     dp = C.make_dp(rec["ctx"], engine=engine)
     if mode == "device":  # the device-resident pipeline (k_skel_walk)
         sk = C.check_skeleton_device_vs_reference(rec, dp)
         print(f"skeleton ok {tc} device launches={sk.launches} requeries={sk.requeries}")
         return
-    C.check_classify(rec, dp)
+    classified = C.check_classify(rec, dp)
     frags, expl = C.check_filter(rec, dp)
     C.check_skeleton_vs_reference(rec, dp, frags, expl)
+    # Predictor.predict up to the skeleton-based reduction, from a fresh table
+    C.check_predict_skeleton_stage(rec, C.make_dp(rec["ctx"], engine=engine), classified)
     print(f"skeleton ok {tc}")
 
 

@@ -4,7 +4,8 @@ time and in `DynamicProgrammingTable`, plus the frame plumbing of
 fragment_classification.classify_fragments (lit, struct.map_elements, concat,
 with_row_index, rename, drop, comparisons, str.contains), and of the reference's
 Predictor.filter_by_explanation and SkeletonBuilder._predict_skeleton
-(DataFrame.item, row/column assignment).
+(DataFrame.item, row/column assignment) and build_skeleton's fragment
+bookkeeping (clone, vstack, when/then/otherwise, reverse subtraction).
 
 TEST INFRASTRUCTURE ONLY.  polars is not installed in this image and there is no
 network.  This module is put on sys.path solely by tests/golden/make_golden.py
@@ -46,6 +47,9 @@ class Expr:
     def __sub__(self, v):
         return self._map(lambda x: x - v)
 
+    def __rsub__(self, v):  # int - Expr (build_skeleton's reverse end indices)
+        return self._map(lambda x: v - x)
+
     def __truediv__(self, v):
         return self._map(lambda x: x / v)
 
@@ -57,6 +61,12 @@ class Expr:
 
     def __lt__(self, v):
         return self._map(lambda x: x < v)
+
+    def __ge__(self, v):
+        return self._map(lambda x: x >= v)
+
+    def __le__(self, v):
+        return self._map(lambda x: x <= v)
 
     def __and__(self, o):
         return Expr(lambda df: self.fn(df) & o.fn(df), self.name)
@@ -113,6 +123,33 @@ def lit(value, dtype=None):
 
 def struct(*names):
     return Expr(lambda df: [dict(zip(names, r)) for r in df._d[list(names)].itertuples(index=False)], names[0])
+
+
+def _values(e, df):
+    return np.asarray(e.fn(df)) if isinstance(e, Expr) else np.full(len(df._d), e)
+
+
+class _Then:
+    def __init__(self, cond, value):
+        self.cond, self.value = cond, value
+
+    def otherwise(self, other):
+        c, a, b = self.cond, self.value, other
+        name = a.name if isinstance(a, Expr) else "literal"
+        return Expr(lambda df: pd.Series(np.where(np.asarray(c.fn(df), dtype=bool), _values(a, df), _values(b, df))),
+                    name)
+
+
+class _When:
+    def __init__(self, cond):
+        self.cond = cond
+
+    def then(self, value):
+        return _Then(self.cond, value)
+
+
+def when(cond):
+    return _When(cond)
 
 
 def concat(frames):
@@ -221,6 +258,12 @@ class DataFrame:
 
     def __len__(self):
         return len(self._d)
+
+    def clone(self):
+        return DataFrame(self._d.copy())
+
+    def vstack(self, other):
+        return DataFrame(pd.concat([self._d, other._d], ignore_index=True))
 
     def replace_column(self, index, series):
         d = self._d.copy()

@@ -142,7 +142,7 @@ def test_frontier_split_and_abort(setup, cases):
     _, _, _, nodes, _ = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len)
     per_slot = 392  # workspace bytes per hash-ring slot (sst_api.cpp: 8 nodes of 7 B + 4 x (32 + 4 + 48) B)
     big, tot = int(nodes.max()), int(nodes.sum())
-    S = 1 << int(np.ceil(np.log2(max(big, 1024))))  # ring tables of >= the heaviest spectrum's nodes
+    S = 1 << int(np.ceil(np.log2(max(big // 2, 1024))))  # ring tables of >= half the heaviest spectrum's nodes
     assert 8 * S < tot, (big, tot)  # ... but node capacity below the batch's
     lower, upper, st, _, stats = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len,
                                                                frontier_workspace=per_slot * S)

@@ -82,16 +82,19 @@ def test_two_rank_pipeline_outcomes_vs_single_rank(tmp_path):
     """Config 5 sharded: tools/pipeline_bench.py as two ranks on GPU 0 (gloo),
     every stage device-resident through the skeleton walk and the length
     selection, each rank's per-spectrum outcomes gathered to rank 0; each
-    rank's gathered bytes equal a single-process run on that rank's spectra."""
+    rank's gathered bytes equal a single-process run on that rank's spectra.
+    The ranks run with PYTHONHASHSEED unset (each interpreter its own str
+    hashes): the walk must follow rank 0's name hashes on both ranks, and the
+    single-rank runs are given those (--name-hashes)."""
     from spectrseqtools_amd import _native
     from spectrseqtools_amd.pipeline_device import unpack_outcomes
 
     multi, single = str(tmp_path / "multi"), str(tmp_path / "single")
-    env = dict(os.environ, SST_DEVICE="0", MASTER_ADDR="127.0.0.1",
-               PYTHONHASHSEED="0")  # the walk orders explanations as CPython sets do: one seed for all runs
+    env = dict(os.environ, SST_DEVICE="0", MASTER_ADDR="127.0.0.1")
+    env.pop("PYTHONHASHSEED", None)  # random per interpreter: rank 0's name hashes must rule
     bench = os.path.join(REPO, "tools", "pipeline_bench.py")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), bench, "--spectra", "400", "--warmup-spectra", "16", "--length-spectra", "48", "--backend", "gloo",
+           "127.0.0.1", "--master-port", str(_free_port()), bench, "--spectra", "400", "--warmup-spectra", "16", "--length-spectra", "48", "--backend", "gloo", "--cpu-baseline-s", "0",
            "--dump-outcomes", multi]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=REPO)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
@@ -99,8 +102,9 @@ def test_two_rank_pipeline_outcomes_vs_single_rank(tmp_path):
     assert '"n_gpus": 2' in line and '"gather"' in line
     for r in range(2):
         p = subprocess.run([sys.executable, bench, "--spectra", "400", "--warmup-spectra", "16", "--length-spectra", "48",
-                            "--as-rank", str(r), "--dump-outcomes", single],
-                           env=dict(os.environ, SST_DEVICE="0", PYTHONHASHSEED="0"), capture_output=True, text=True, timeout=250,
+                            "--cpu-baseline-s", "0", "--as-rank", str(r), "--dump-outcomes", single, "--name-hashes",
+                            os.path.join(multi, "name_hashes.npy")],
+                           env=env, capture_output=True, text=True, timeout=250,
                            cwd=REPO)
         assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-5000:]
         got = np.load(os.path.join(multi, f"outcome_rank{r}.npy"))

@@ -154,6 +154,9 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--dump-outcomes", default=None,
                     help="rank 0 saves the gathered per-spectrum outcomes (one .npy per rank) here")
+    ap.add_argument("--name-hashes", default=None,
+                    help="a .npy of the rows' name hashes (the skeleton walk's set order) to use instead of this "
+                         "interpreter's; a multi-rank run always uses rank 0's (saved with --dump-outcomes)")
     ap.add_argument("--as-rank", type=int, default=None,
                     help="single process: generate the spectra rank R of a multi-rank run would get")
     args = ap.parse_args()
@@ -203,6 +206,18 @@ def main():
     dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
                                  precision=TOLERANCE, seq=seq0, engine=engine)
     min_int = min(m.mass for m in dp.masses[1:])
+    # the skeleton walk orders explanations as the reference's CPython sets do,
+    # by the names' str hashes: one interpreter's for every rank (rank 0's)
+    from spectrseqtools_amd.pipeline_device import name_hashes
+
+    nh = name_hashes(dp) if args.name_hashes is None else np.load(args.name_hashes)
+    if dist:
+        t = torch.as_tensor(nh, device=comm_dev)
+        dist.broadcast(t, src=0)
+        nh = t.cpu().numpy()
+    if rank == 0 and args.dump_outcomes:
+        os.makedirs(args.dump_outcomes, exist_ok=True)
+        np.save(os.path.join(args.dump_outcomes, "name_hashes.npy"), nh)
     max_len = pipeline.max_len_of(su_seq, TOLERANCE, min_int)  # cli.py:158-170
 
     def kernels():
@@ -232,8 +247,9 @@ def main():
         bw = pd.bins_device(dp, rw, fw.alpha, max_len=m0)
         sw = bw.status == 2
         int(sw.sum().item()), int((bw.status == -10).sum().item()), int(bw.count[sw].sum().item())
-        kw = pd.skeleton_device(dp, rw, fw.alpha, m0, bins=bw)
-        pd.length_device(dp, kw, bw.alpha_dev, su_seq[:S0], batch.seq_mass[:S0])
+        kw = pd.skeleton_device(dp, rw, fw.alpha, m0, bins=bw, name_hash=nh)
+        lw = pd.length_device(dp, kw, bw.alpha_dev, su_seq[:S0], batch.seq_mass[:S0])
+        pd.post_skeleton_device(dp, rw, kw, lw)
     engine.synchronize()
     if rank == 0:
         print(f"[warm-up] {S0} spectra done", file=sys.stderr, flush=True)
@@ -334,7 +350,7 @@ def main():
     if rows is not None:  # stages 4-5 (device-resident path)
         barrier()
         t0 = time.perf_counter()
-        sk = pd.skeleton_device(dp, rows, fx_alpha, max_len, bins=db)
+        sk = pd.skeleton_device(dp, rows, fx_alpha, max_len, bins=db, name_hash=nh)
         barrier()
         wst = {int(k): int(v) for k, v in zip(*np.unique(sk.status, return_counts=True))}
         stages["skeleton"] = {"s": tmax(time.perf_counter() - t0), "sides": 2 * len(max_len),
@@ -365,7 +381,18 @@ def main():
         progress("length")
         barrier()
         t0 = time.perf_counter()
-        buf = pd.pack_outcomes(rows, fx, sk, ln)
+        post = pd.post_skeleton_device(dp, rows, sk, ln)
+        barrier()
+        stages["post_skeleton"] = {"s": tmax(time.perf_counter() - t0), "spectra": int(post.active.sum()),
+                                   "fragments_after_skeleton": post.rows_before,
+                                   "fragments_after_reduction": post.rows_after,
+                                   "path": "device (sst_post_skeleton_device + sst_valid_rows_alpha_device)",
+                                   "kernels": kernels()}
+        busy(stages["post_skeleton"])
+        progress("post_skeleton")
+        barrier()
+        t0 = time.perf_counter()
+        buf = pd.pack_outcomes(rows, fx, sk, ln, post)
         if dist:
             from spectrseqtools_amd.parallel import Gatherer
 
