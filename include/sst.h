@@ -803,8 +803,9 @@ int sst_length_bounds_reach_device(sst_table* t, const double* d_su, const doubl
  * (d_lr / d_lr_off instead of the bitsets); d_nodes (may be NULL; zeroed by the
  * caller) = per query, the memo entries (distinct (mass, row) nodes) its DFS
  * creates.  workspace_bytes: the device workspace (0: half the free memory, at
- * most 48 GB); queries are processed in chunks that fit it (a chunk that
- * overflows is split; a single query beyond the workspace gets SST_ABORTED).
+ * most 48 GB); queries are processed in chunks sized from the memo entries
+ * per query seen so far (a chunk that overflows is split; a single query
+ * beyond the workspace gets SST_ABORTED).
  * stats may be NULL. */
 typedef struct sst_lbf_stats {
   int64_t live;            /* queries the list pass handed to the frontier */
@@ -813,8 +814,9 @@ typedef struct sst_lbf_stats {
   int64_t splits;          /* chunks that overflowed the workspace and were split */
   int64_t aborted;         /* single queries beyond the workspace (SST_ABORTED) */
   int64_t bands;           /* mass bands of the largest chunk */
-  int64_t key_words;       /* 64-bit words per first-visit key (4, 8 or 16) */
+  int64_t key_words;       /* 64-bit words per first-visit key (1, 2 or 4) */
   int64_t max_band_groups; /* (query, mass) groups of the fullest band */
+  int64_t max_band_nodes;  /* memo entries of the fullest band */
   int64_t table_slots;     /* slots per hash table of the ring */
   int64_t node_cap;        /* node capacity per chunk */
 } sst_lbf_stats;

@@ -533,10 +533,23 @@ static int64_t lb_backtrack(LCtx* l, int64_t total_mass, int row, int64_t A, int
     return best;
 }
 
-/* returns the bound, or INT64_MIN on the NameError raise. */
+/* returns the bound, or INT64_MIN on the NameError raise; *memo_entries (may
+ * be NULL) = the memo's size when the call returns (the (mass, row) nodes the
+ * DFS expanded) */
+int64_t ora_length_bound_memo(const void* table, int nrows, int64_t cols, int C, const int64_t* w,
+                              const uint8_t* is_mod, const int64_t* cap, double su_mass, double obs_mass,
+                              double tolerance, double precision, int64_t max_len, int64_t max_mods, int dir,
+                              int64_t* memo_entries);
 int64_t ora_length_bound(const void* table, int nrows, int64_t cols, int C, const int64_t* w, const uint8_t* is_mod,
                          const int64_t* cap, double su_mass, double obs_mass, double tolerance, double precision,
                          int64_t max_len, int64_t max_mods, int dir) {
+    return ora_length_bound_memo(table, nrows, cols, C, w, is_mod, cap, su_mass, obs_mass, tolerance, precision,
+                                 max_len, max_mods, dir, NULL);
+}
+int64_t ora_length_bound_memo(const void* table, int nrows, int64_t cols, int C, const int64_t* w,
+                              const uint8_t* is_mod, const int64_t* cap, double su_mass, double obs_mass,
+                              double tolerance, double precision, int64_t max_len, int64_t max_mods, int dir,
+                              int64_t* memo_entries) {
     LCtx l;
     memset(&l, 0, sizeof(l));
     Ctx* c = &l.base;
@@ -558,6 +571,7 @@ int64_t ora_length_bound(const void* table, int nrows, int64_t cols, int C, cons
         if (c->error) break;
         res = dir ? (b > res ? b : res) : (b < res ? b : res);
     }
+    if (memo_entries) *memo_entries = (int64_t)c->memo.n;
     memo_free(&c->memo);
     if (c->error) return INT64_MIN;
     if (res == l.dflt) res = dir ? max_len : 1;

@@ -3108,8 +3108,8 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
   HIP_OK(c, hipStreamSynchronize(c->stream));
   if (stats) stats->live = n_live;
   if (n_live == 0) return SST_OK;
-  // workspace: nodes 7 B each, per ring table S group slots (32 B + a 4-B list
-  // entry) and S candidate slots (48 B with 256-bit keys); nodes = 8 S
+  // workspace: nodes 7 B each (8 per ring slot), per ring table S group slots
+  // (32 B + a 4-B list entry) and S candidate slots (24 B with 64-bit keys)
   size_t budget = workspace_bytes;
   if (budget == 0) {
     size_t fr = 0, tot = 0;
@@ -3119,23 +3119,20 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
     }
     budget = std::min<size_t>(48ull << 30, fr / 2);
   }
-  const size_t per_slot = 8 * 7 + (size_t)ring * (lbf_group_bytes() + 4 + lbf_cand_bytes(4));
+  constexpr uint64_t kNodesPerSlot = 8;
+  const size_t per_slot = kNodesPerSlot * 7 + (size_t)ring * (lbf_group_bytes() + 4 + lbf_cand_bytes(1));
   uint64_t S = pow2_floor(std::max<size_t>(1024, budget / per_slot));
   if (S > (1ull << 31)) S = 1ull << 31;
-  const uint64_t ncap = std::min<uint64_t>(8 * S, 0xFFFFFFF0ull);
-  DevBuf flags, lchild, vlo, vhi, gtab, ctab, glist, ctl, bstart, bgroups, qi, qrow, roots;
+  const uint64_t ncap = std::min<uint64_t>(kNodesPerSlot * S, 0xFFFFFFF0ull);
+  DevBuf flags, lchild, vlo, vhi, gtab, ctab, glist, ctl, bstart, bgroups, qi, qrow, roots, ncnt;
   if (!flags.ensure(ncap) || !lchild.ensure(ncap * 4) || !vlo.ensure(ncap) || !vhi.ensure(ncap) ||
-      !gtab.ensure((size_t)ring * S * lbf_group_bytes()) || !ctab.ensure((size_t)ring * S * lbf_cand_bytes(4)) ||
+      !gtab.ensure((size_t)ring * S * lbf_group_bytes()) || !ctab.ensure((size_t)ring * S * lbf_cand_bytes(1)) ||
       !glist.ensure((size_t)ring * S * 4) || !ctl.ensure(sizeof(FCtl)))
     return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier workspace)");
   constexpr uint32_t kChunkMax = 1u << 20;  // the keys' query field
-  std::vector<std::pair<uint32_t, uint32_t>> todo;
-  for (uint32_t c0 = 0; c0 < n_live; c0 += kChunkMax) todo.push_back({c0, std::min(n_live, c0 + kChunkMax)});
-  std::reverse(todo.begin(), todo.end());
-  std::vector<uint32_t> band_groups;
-  while (!todo.empty()) {
-    const auto [c0, c1] = todo.back();
-    todo.pop_back();
+  // one sweep over list entries [c0, c1): 1 done, 0 overflow (split and rerun), < 0 error
+  uint64_t last_nodes = 0;
+  auto run_chunk = [&](uint32_t c0, uint32_t c1) -> int {
     const uint32_t nc = c1 - c0;
     FrontierArgs a{};
     a.list = (const uint32_t*)d_list.p;
@@ -3162,12 +3159,14 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
     a.upper = d_upper;
     a.status = d_status;
     a.nodes_out = d_nodes;
-    if (!qi.ensure((size_t)nc * sizeof(FQInfo)) || !qrow.ensure((size_t)nc * 128 * 4))
+    if (!qi.ensure((size_t)nc * sizeof(FQInfo)) || !qrow.ensure((size_t)nc * 128 * 4) || !ncnt.ensure((size_t)nc * 4))
       return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier queries)");
     a.qi = (FQInfo*)qi.p;
     a.qrow = (uint32_t*)qrow.p;
+    a.node_cnt = (uint32_t*)ncnt.p;
     a.ctl = (FCtl*)ctl.p;
     HIP_OK(c, hipMemsetAsync(ctl.p, 0, sizeof(FCtl), c->stream));
+    HIP_OK(c, hipMemsetAsync(ncnt.p, 0, (size_t)nc * 4, c->stream));
     {
       Prof p(c, SST_K_LENGTH_BOUND);
       HIP_OK(c, launch_lbf_setup(t->args, a, c->stream));
@@ -3179,10 +3178,10 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
     if (n_bands > 4094) return fail(c, SST_E_ARG, "length bounds (frontier): a window beyond 4094 bands");
     if (h.max_hi >= (1ull << 25)) return fail(c, SST_E_ARG, "length bounds (frontier): a window at 2^25 or beyond");
     a.rb = bits_for(h.max_win > 0 ? h.max_win - 1 : 0);
-    a.cb = std::max(1, bits_for(h.max_hi / (uint64_t)wb));
-    const int need = a.rb + (int)h.max_k * a.cb;
-    const int kw = need <= 256 ? 4 : need <= 512 ? 8 : need <= 1024 ? 16 : 0;
-    if (!kw || a.rb > 32) return fail(c, SST_E_ARG, "length bounds (frontier): first-visit keys beyond 1024 bits");
+    // unary keys: root bits, one zero per kept rank, one 1 per left move (<= hi / w_min)
+    const int need = a.rb + (int)h.max_k + (int)(h.max_hi / (uint64_t)wb);
+    const int kw = need <= 64 ? 1 : need <= 128 ? 2 : need <= 256 ? 4 : 0;
+    if (!kw || a.rb > 32) return fail(c, SST_E_ARG, "length bounds (frontier): first-visit keys beyond 256 bits");
     a.rstride = (int)std::max<uint32_t>(1, h.max_win);
     a.n_bands = n_bands;
     if (!roots.ensure((size_t)nc * a.rstride * 4))
@@ -3210,9 +3209,12 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
       HIP_OK(c, launch_lbf_sweep(a, kw, n_bands, c->n_cu * 8, c->stream));
     }
     HIP_OK(c, hipMemcpyAsync(&h, ctl.p, sizeof(FCtl), hipMemcpyDeviceToHost, c->stream));
-    band_groups.assign((size_t)n_bands, 0);
-    if (n_bands)
+    std::vector<uint32_t> band_groups((size_t)n_bands, 0), band_start((size_t)n_bands + 1, 0);
+    if (n_bands) {
       HIP_OK(c, hipMemcpyAsync(band_groups.data(), bgroups.p, (size_t)n_bands * 4, hipMemcpyDeviceToHost, c->stream));
+      HIP_OK(c, hipMemcpyAsync(band_start.data(), bstart.p, ((size_t)n_bands + 1) * 4, hipMemcpyDeviceToHost,
+                               c->stream));
+    }
     HIP_OK(c, hipStreamSynchronize(c->stream));
     if (h.overflow & 56u) return fail(c, SST_E_INTERNAL, "length bounds (frontier): inconsistent first-visit tables");
     if (h.overflow) {
@@ -3224,22 +3226,53 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
         const int8_t ab = SST_ABORTED;
         HIP_OK(c, hipMemcpyAsync(d_status + one.i, &ab, 1, hipMemcpyHostToDevice, c->stream));
         if (stats) stats->aborted++;
-        continue;
+        return 1;
       }
-      const uint32_t mid = c0 + nc / 2;
-      todo.push_back({mid, c1});
-      todo.push_back({c0, mid});
-      continue;
+      return 0;
     }
+    last_nodes = h.node_ctr;
     if (stats) {
       stats->chunks++;
       stats->nodes += h.node_ctr;
       stats->bands = std::max<int64_t>(stats->bands, n_bands);
       stats->key_words = std::max<int64_t>(stats->key_words, kw);
       for (uint32_t x : band_groups) stats->max_band_groups = std::max<int64_t>(stats->max_band_groups, x);
+      for (int b = 0; b < n_bands; ++b)
+        stats->max_band_nodes = std::max<int64_t>(stats->max_band_nodes, band_start[b + 1] - band_start[b]);
       stats->table_slots = (int64_t)S;
       stats->node_cap = (int64_t)ncap;
     }
+    return 1;
+  };
+  // chunks sized from the nodes per query seen so far (a first chunk of 256),
+  // aiming at half the node capacity; a chunk that overflows is split in halves
+  uint64_t done_q = 0, done_nodes = 0;
+  uint32_t c0 = 0;
+  while (c0 < n_live) {
+    uint32_t nc = std::min<uint32_t>(n_live - c0, 256);
+    if (done_q && done_nodes) {
+      const double per_q = (double)done_nodes / (double)done_q;
+      nc = (uint32_t)std::max<double>(1.0, std::min<double>({(double)(n_live - c0), (double)kChunkMax,
+                                                              0.5 * (double)ncap / per_q}));
+    } else if (done_q) {
+      nc = std::min<uint32_t>(n_live - c0, kChunkMax);
+    }
+    std::vector<std::pair<uint32_t, uint32_t>> todo{{c0, c0 + nc}};
+    while (!todo.empty()) {
+      const auto [a0, a1] = todo.back();
+      todo.pop_back();
+      const int rc = run_chunk(a0, a1);
+      if (rc < 0) return rc;
+      if (rc == 0) {
+        const uint32_t mid = a0 + (a1 - a0) / 2;
+        todo.push_back({mid, a1});
+        todo.push_back({a0, mid});
+        continue;
+      }
+      done_q += a1 - a0;
+      done_nodes += last_nodes;
+    }
+    c0 += nc;
   }
   HIP_OK(c, hipStreamSynchronize(c->stream));
   return SST_OK;

@@ -54,7 +54,7 @@ struct alignas(32) FGroup {
 };
 
 template <int KW>
-struct alignas(16) FCand {
+struct FCand {
   uint64_t key;
   uint32_t parent;
   uint8_t A, B;
@@ -150,8 +150,14 @@ __device__ __forceinline__ uint32_t cand_find(const FCand<KW>* T, uint32_t mask,
 }
 
 // first-visit keys: a KW x 64-bit big-endian integer (word 0 most
-// significant): the root index in the top rb bits, then cb bits per kept
-// rank from the top rank down; lexicographic order of the reference's DFS
+// significant) whose lexicographic order is the reference's DFS preorder: the
+// root index in the top rb bits, then each kept rank from the top down in
+// unary -- c_s ones and a zero.  (Unary keeps the order: at the first rank
+// where two count vectors differ, the smaller count meets its zero where the
+// larger has a one.)  A path in row k has zero counts below k, so every bit
+// after its current position is zero, and one more left move in row k sets the
+// bit at rb + d + (K - 1 - k) from the top (d = the path's left moves so far:
+// the ones already set).  rb + max d + K bits; max d <= hi / w_min.
 template <int KW>
 __device__ __forceinline__ bool key_less(const uint64_t (&a)[KW], const uint64_t (&b)[KW]) {
   bool lt = false, decided = false;
@@ -165,20 +171,17 @@ __device__ __forceinline__ bool key_less(const uint64_t (&a)[KW], const uint64_t
   return lt;
 }
 template <int KW>
-__device__ __forceinline__ void key_add_bit(uint64_t (&k)[KW], int p) {  // k += 2^p (p from the LSB)
-  const int wi = KW - 1 - (p >> 6);
-  const uint64_t add = 1ull << (p & 63);
-  uint64_t carry = 0;
+__device__ __forceinline__ int key_ones(const uint64_t (&k)[KW], int rb) {  // left moves on the path
+  int d = rb > 0 ? -__builtin_popcountll(k[0] >> (64 - rb)) : 0;
 #pragma unroll
-  for (int i = KW - 1; i >= 0; --i) {
-    const uint64_t a = i == wi ? add : 0ull;
-    const uint64_t s = k[i] + a;
-    const uint64_t c1 = s < a;
-    const uint64_t s2 = s + carry;
-    const uint64_t c2 = s2 < carry;
-    k[i] = s2;
-    carry = c1 | c2;
-  }
+  for (int i = 0; i < KW; ++i) d += __builtin_popcountll(k[i]);
+  return d;
+}
+template <int KW>
+__device__ __forceinline__ void key_set_msb(uint64_t (&k)[KW], int p) {  // bit p counted from the most significant
+#pragma unroll
+  for (int i = 0; i < KW; ++i)
+    if (i == (p >> 6)) k[i] |= 1ull << (63 - (p & 63));
 }
 
 __device__ __forceinline__ uint32_t qrow_w(uint32_t x) { return x & 0xFFFFFu; }
@@ -346,7 +349,7 @@ __global__ __launch_bounds__(256) void k_lbf_band(FrontierArgs a, int band) {
       return;
     }
     const uint32_t id0 = wbase + incl - (uint32_t)n;  // rank lo; rank k at id0 + k - lo
-    if (a.nodes_out && act) atomicAdd((unsigned long long*)&a.nodes_out[q.i], (unsigned long long)n);
+    if (act && n) atomicAdd(&a.node_cnt[jj], (uint32_t)n);
     const int steps = wave_max_i(n);
     uint64_t uk[KW];
 #pragma unroll
@@ -354,7 +357,6 @@ __global__ __launch_bounds__(256) void k_lbf_band(FrontierArgs a, int band) {
     int uA = 0;
     bool have_u = false;
     const uint32_t* qrow = a.qrow + (size_t)jj * 128;
-    const int field0 = KW * 64 - a.rb - (int)q.K * a.cb;  // LSB of rank 0's count field
     for (int s = 0; s < steps; ++s) {
       const bool live = s < n;
       const int k = hv - s;
@@ -439,7 +441,7 @@ __global__ __launch_bounds__(256) void k_lbf_band(FrontierArgs a, int band) {
           uint64_t k2[KW];
 #pragma unroll
           for (int w = 0; w < KW; ++w) k2[w] = key[w];
-          key_add_bit<KW>(k2, field0 + k * a.cb);
+          key_set_msb<KW>(k2, a.rb + key_ones<KW>(key, a.rb) + ((int)q.K - 1 - k));
           FCand<KW>& e = C2[cs];
           e.parent = id;
           e.A = (uint8_t)(mod ? A - 1 : A);
@@ -533,6 +535,7 @@ __global__ __launch_bounds__(256) void k_lbf_out(FrontierArgs a) {
     bl = l < bl ? l : bl;
     bh = h > bh ? h : bh;
   }
+  if (a.nodes_out) a.nodes_out[q.i] += a.node_cnt[jj];
   a.lower[q.i] = bl >= dl ? 1 : bl;  // the default becomes 1 / max_len (:476-484)
   a.upper[q.i] = bh == -1 ? (int64_t)q.L : bh;
   a.status[q.i] = 0;
@@ -601,17 +604,17 @@ static hipError_t sweep(const FrontierArgs& a, int n_bands, int band_blocks, hip
 hipError_t launch_lbf_sweep(const FrontierArgs& a, int key_words, int n_bands, int band_blocks, hipStream_t st) {
   switch (key_words) {
     case 4: return sweep<4>(a, n_bands, band_blocks, st);
-    case 8: return sweep<8>(a, n_bands, band_blocks, st);
-    case 16: return sweep<16>(a, n_bands, band_blocks, st);
+    case 1: return sweep<1>(a, n_bands, band_blocks, st);
+    case 2: return sweep<2>(a, n_bands, band_blocks, st);
     default: return hipErrorInvalidValue;
   }
 }
 
 size_t lbf_cand_bytes(int key_words) {
   switch (key_words) {
-    case 4: return sizeof(FCand<4>);
-    case 8: return sizeof(FCand<8>);
-    default: return sizeof(FCand<16>);
+    case 1: return sizeof(FCand<1>);
+    case 2: return sizeof(FCand<2>);
+    default: return sizeof(FCand<4>);
   }
 }
 size_t lbf_group_bytes() { return sizeof(FGroup); }

@@ -332,7 +332,7 @@ struct FrontierArgs {
   int A0, max_len;
   int wb;          // band width: the table's lightest row (every left move crosses >= 1 band)
   int ring, jump;  // hash / list ring size (power of two > jump), max bands one left move crosses
-  int rb, cb;      // key fields: root index bits, bits per rank count
+  int rb;          // key: root index bits (then the ranks in unary)
   int rstride;     // root slots per query
   int n_bands;     // band_start[n_bands] = the chunk's node count (after the last band)
   FQInfo* qi;
@@ -355,6 +355,7 @@ struct FrontierArgs {
   int64_t* upper;
   int8_t* status;
   uint64_t* nodes_out;
+  uint32_t* node_cnt;  // [n_chunk] memo entries per listed query (added to nodes_out when the chunk completes)
 };
 hipError_t launch_lbf_setup(const TableArgs& t, const FrontierArgs& a, hipStream_t st);
 hipError_t launch_lbf_sweep(const FrontierArgs& a, int key_words, int n_bands, int band_blocks, hipStream_t st);

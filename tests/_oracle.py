@@ -44,6 +44,8 @@ def _load():
     lib.ora_result_free.argtypes = [ctypes.POINTER(_Res)]
     lib.ora_length_bound.restype = I64
     lib.ora_length_bound.argtypes = [P, I, I64, I, P, P, P, D, D, D, D, I64, I64, I]
+    lib.ora_length_bound_memo.restype = I64
+    lib.ora_length_bound_memo.argtypes = [P, I, I64, I, P, P, P, D, D, D, D, I64, I64, I, ctypes.POINTER(I64)]
     lib.ora_is_valid_batch.restype = I64
     lib.ora_is_valid_batch.argtypes = [P, I, I64, I, P, P, I64, D, D, I, P]
     lib.ora_explain_batch.restype = I64
@@ -127,6 +129,15 @@ def length_bound(table, C, alph, su_mass, obs_mass, tolerance, max_len, max_mods
                              int(max_len), int(max_mods), 1 if direction == "upper" else 0)
     return None if v == -(2 ** 63) else int(v)
 
+
+def length_bound_memo(table, C, alph, su_mass, obs_mass, tolerance, max_len, max_mods, direction, precision=1e-3):
+    """length_bound and the memo's size when the reference's call returns
+    (the (mass, row) nodes its DFS expanded), or (None, n) where it raises."""
+    n = ctypes.c_int64(0)
+    v = LIB.ora_length_bound_memo(_p(table), table.shape[0], table.shape[1], C, _p(alph.w), _p(alph.is_mod),
+                                  _p(alph.cap), float(su_mass), float(obs_mass), float(tolerance), float(precision),
+                                  int(max_len), int(max_mods), 1 if direction == "upper" else 0, ctypes.byref(n))
+    return (None if v == -(2 ** 63) else int(v)), int(n.value)
 
 def explain_batch(table, C, alph, masses, thrs, A, tolerance, with_memo=True, nthreads=1, precision=1e-3):
     n = len(masses)

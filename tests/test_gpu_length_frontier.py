@@ -8,7 +8,7 @@ to round(0.5 L), so that budgets bind.
 
   * the first-visit frontier (sst_length_bounds_frontier_device, what
     pipeline_device.length_device runs): alphabets of 4..104 kept rows, so
-    that first-visit keys of 256, 512 and 1024 bits all run; then again in a
+    that first-visit keys of 64, 128 and 256 bits all run; then again in a
     workspace too small for the batch (chunks split and rerun, counted) and
     in one too small for the heaviest spectra (those report SST_ABORTED,
     every other spectrum unchanged);
@@ -85,8 +85,10 @@ def _oracle_bounds(rows, dp, caps_len, a0_len, alphas, su, ob, ml):
         L = int(ml[g])
         tab = oracle.build_table(ms, max(ms) * 35, 32)
         alph = oracle.Alphabet(ms, [dp.masses[r].is_modification for r in full], [int(caps_len[L, r]) for r in full])
-        return tuple(oracle.length_bound(tab, 32, alph, su[g], ob[g], TOL, L, int(a0_len[L]), d)
-                     for d in ("lower", "upper"))
+        lo, n_lo = oracle.length_bound_memo(tab, 32, alph, su[g], ob[g], TOL, L, int(a0_len[L]), "lower")
+        up, n_up = oracle.length_bound_memo(tab, 32, alph, su[g], ob[g], TOL, L, int(a0_len[L]), "upper")
+        assert n_lo == n_up  # the visits do not depend on the direction
+        return lo, up, n_lo
 
     with cf.ThreadPoolExecutor(16) as ex:  # ctypes releases the GIL: the oracle calls run in parallel
         return list(ex.map(one, range(len(alphas))))
@@ -101,9 +103,12 @@ def cases(setup):
     return alphas, masks, su, ob, ml, want
 
 
-def _check(want, lower, upper, st, skip=()):
+def _check(want, lower, upper, st, skip=(), nodes=None):
+    """Bounds and status against the oracle; with nodes, every completed
+    spectrum's memo entries too (the same (mass, row) nodes as the
+    reference's memo: the first-visit structure itself, not only its result)."""
     n_ok = 0
-    for g, (wl, wu) in enumerate(want):
+    for g, (wl, wu, wn) in enumerate(want):
         if g in skip:
             continue
         if wl is None:  # the reference raises (a window past the reduced table)
@@ -111,6 +116,8 @@ def _check(want, lower, upper, st, skip=()):
             continue
         assert int(st[g]) == 0 and (int(lower[g]), int(upper[g])) == (wl, wu), \
             (g, int(st[g]), int(lower[g]), int(upper[g]), wl, wu)
+        if nodes is not None:
+            assert int(nodes[g]) == wn, (g, int(nodes[g]), wn)
         n_ok += 1
     return n_ok
 
@@ -122,9 +129,18 @@ def test_frontier_vs_oracle_rebuilt_tables(setup, cases):
     alphas, masks, su, ob, ml, want = cases
     lower, upper, st, nodes, stats = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len)
     fr = stats["frontier"]
-    assert _check(want, lower, upper, st) >= 190
-    assert fr["key_words"] == 16 and fr["splits"] == 0 and fr["aborted"] == 0, fr
+    assert _check(want, lower, upper, st, nodes=nodes) >= 190
+    assert fr["key_words"] == 4 and fr["splits"] == 0 and fr["aborted"] == 0, fr  # 104 rows and 20-mers: > 128 bits
     assert fr["nodes"] == int(nodes.sum()) > 10 ** 6, fr  # memo entries, summed over the spectra
+    # the same spectra with narrower keys: the <= 12-row alphabets (64-bit
+    # keys) and the 41..64-row ones of <= 9 nucleotides (128-bit keys)
+    K = np.array([len(a) for a in alphas])
+    for sel, kw in ((np.flatnonzero(K <= 12), 1), (np.flatnonzero((K > 40) & (K <= 64)), 2)):
+        lo1, up1, st1, nd1, s1 = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len, sel=sel)
+        assert np.array_equal(nd1[sel], nodes[sel])
+        assert s1["frontier"]["key_words"] == kw and len(sel) >= 20, (kw, s1["frontier"])
+        assert np.array_equal(lo1[sel], lower[sel]) and np.array_equal(up1[sel], upper[sel])
+        assert np.array_equal(st1[sel], st[sel])
     # binding budgets: some spectra's bounds differ from their budget-free ones
     free = np.full((21, _native.MAX_ROWS), 255, np.int32)
     lo2, up2, st2, _, _ = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, free, np.full(21, 255, np.int32))
@@ -140,15 +156,15 @@ def test_frontier_split_and_abort(setup, cases):
     dp, rows, caps_len, a0_len = setup
     alphas, masks, su, ob, ml, want = cases
     _, _, _, nodes, _ = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len)
-    per_slot = 392  # workspace bytes per hash-ring slot (sst_api.cpp: 8 nodes of 7 B + 4 x (32 + 4 + 48) B)
+    per_slot = 296  # workspace bytes per hash-ring slot (sst_api.cpp: 8 nodes of 7 B + 4 x (32 + 4 + 24) B)
     big, tot = int(nodes.max()), int(nodes.sum())
     S = 1 << int(np.ceil(np.log2(max(big // 2, 1024))))  # ring tables of >= half the heaviest spectrum's nodes
     assert 8 * S < tot, (big, tot)  # ... but node capacity below the batch's
-    lower, upper, st, _, stats = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len,
-                                                               frontier_workspace=per_slot * S)
+    lower, upper, st, nd, stats = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len,
+                                                                frontier_workspace=per_slot * S)
     fr = stats["frontier"]
     assert fr["splits"] > 0 and fr["aborted"] == 0 and fr["node_cap"] == 8 * S, fr
-    assert _check(want, lower, upper, st) >= 190
+    assert _check(want, lower, upper, st, nodes=nd) >= 190  # failed chunks' nodes are not counted
     small = int(np.sort(nodes)[-8])  # node capacity below the 8 heaviest spectra's
     S2 = 1 << int(np.floor(np.log2(small // 8)))
     lower, upper, st, _, stats = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len,
