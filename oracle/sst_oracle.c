@@ -497,6 +497,7 @@ typedef struct LCtx {
     Ctx base;
     int dir; /* 0 lower, 1 upper */
     int64_t dflt;
+    int64_t live; /* memo entries whose own pair bits are non-zero (diagnostic, see ora_length_bound_memo) */
 } LCtx;
 
 static int64_t lb_backtrack(LCtx* l, int64_t total_mass, int row, int64_t A, int64_t B) {
@@ -529,13 +530,18 @@ static int64_t lb_backtrack(LCtx* l, int64_t total_mass, int row, int64_t A, int
             best = l->dir ? (v > best ? v : best) : (v < best ? v : best);
         }
     }
+    if (cv & 3u) l->live++;
     memo_put(&c->memo, mkey(total_mass, row), NULL, best);
     return best;
 }
 
 /* returns the bound, or INT64_MIN on the NameError raise; *memo_entries (may
- * be NULL) = the memo's size when the call returns (the (mass, row) nodes the
- * DFS expanded) */
+ * be NULL) = the memo entries whose own pair bits are non-zero when the call
+ * returns (the (mass, row) nodes the DFS expanded).  The reference's memo
+ * also holds "dead" entries: a window value whose pair is 0 passes the
+ * `current_value % C == 0` early exit (mass_table.py:403) when a lower
+ * neighbour's bits are set in the same shifted word, and is memoised with
+ * the default bound; such entries never change a value. */
 int64_t ora_length_bound_memo(const void* table, int nrows, int64_t cols, int C, const int64_t* w,
                               const uint8_t* is_mod, const int64_t* cap, double su_mass, double obs_mass,
                               double tolerance, double precision, int64_t max_len, int64_t max_mods, int dir,
@@ -571,7 +577,7 @@ int64_t ora_length_bound_memo(const void* table, int nrows, int64_t cols, int C,
         if (c->error) break;
         res = dir ? (b > res ? b : res) : (b < res ? b : res);
     }
-    if (memo_entries) *memo_entries = (int64_t)c->memo.n;
+    if (memo_entries) *memo_entries = l.live;
     memo_free(&c->memo);
     if (c->error) return INT64_MIN;
     if (res == l.dflt) res = dir ? max_len : 1;

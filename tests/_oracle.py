@@ -131,8 +131,11 @@ def length_bound(table, C, alph, su_mass, obs_mass, tolerance, max_len, max_mods
 
 
 def length_bound_memo(table, C, alph, su_mass, obs_mass, tolerance, max_len, max_mods, direction, precision=1e-3):
-    """length_bound and the memo's size when the reference's call returns
-    (the (mass, row) nodes its DFS expanded), or (None, n) where it raises."""
+    """length_bound and the memo entries with non-zero pair bits when the
+    reference's call returns (the (mass, row) nodes its DFS expanded; the
+    memo's dead entries -- window values whose pair is 0, memoised with the
+    default through the %C quirk of mass_table.py:403 -- are not counted), or
+    (None, n) where it raises."""
     n = ctypes.c_int64(0)
     v = LIB.ora_length_bound_memo(_p(table), table.shape[0], table.shape[1], C, _p(alph.w), _p(alph.is_mod),
                                   _p(alph.cap), float(su_mass), float(obs_mass), float(tolerance), float(precision),

@@ -117,12 +117,15 @@ def test_frontier_model_equals_oracle(seed):
         wv = np.array(ms[1:])
         su = float(wv[rng.integers(0, len(wv), int(rng.integers(2, 12)))].sum()) * PREC + rng.normal(0, 0.002)
         obs = su + 912.303
-        want = [oracle.length_bound(tab, 32, alph, su, obs, TOL, max_len, A0, d) for d in ("lower", "upper")]
+        (w_lo, n_memo), (w_up, _) = (oracle.length_bound_memo(tab, 32, alph, su, obs, TOL, max_len, A0, d)
+                                     for d in ("lower", "upper"))
+        want = [w_lo, w_up]
         lo, up, nn = frontier_bounds(tab, 32, ms, is_mod, cap, su, obs, max_len, A0)
         if want[0] is None:
             assert lo is None
             continue
         assert [lo, up] == want, (lo, up, want, A0, max_len)
+        assert nn == n_memo, (nn, n_memo)  # the same (mass, row) nodes as the reference's memo
         free = [oracle.length_bound(tab, 32, oracle.Alphabet(ms, is_mod, [99] * len(ms)), su, obs, TOL, max_len, 99, d)
                 for d in ("lower", "upper")]
         n_bind += free != want
