@@ -3108,8 +3108,10 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
   HIP_OK(c, hipStreamSynchronize(c->stream));
   if (stats) stats->live = n_live;
   if (n_live == 0) return SST_OK;
-  // workspace: nodes 7 B each (8 per ring slot), per ring table S group slots
-  // (32 B + a 4-B list entry) and S candidate slots (24 B with 64-bit keys)
+  // workspace per "slot": 8 nodes of 7 B, a 4-B node -> group entry for the
+  // band in hand, per ring table a group entry (32 B) + its list entry (4 B)
+  // and a candidate entry (32 B: 128-bit keys), and the band's group record
+  // (20 B) and candidate record (24 B); S slots, S a power of two (hashing)
   size_t budget = workspace_bytes;
   if (budget == 0) {
     size_t fr = 0, tot = 0;
@@ -3117,21 +3119,25 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
       (void)hipGetLastError();
       fr = 16ull << 30;
     }
-    budget = std::min<size_t>(48ull << 30, fr / 2);
+    budget = std::min<size_t>(96ull << 30, fr / 2);
   }
   constexpr uint64_t kNodesPerSlot = 8;
-  const size_t per_slot = kNodesPerSlot * 7 + (size_t)ring * (lbf_group_bytes() + 4 + lbf_cand_bytes(1));
+  const size_t per_slot = kNodesPerSlot * 7 + 4 + (size_t)ring * (lbf_group_bytes() + 4 + lbf_cand_bytes(2)) +
+                          lbf_grec_bytes() + lbf_crec_bytes(2);
   uint64_t S = pow2_floor(std::max<size_t>(1024, budget / per_slot));
   if (S > (1ull << 31)) S = 1ull << 31;
   const uint64_t ncap = std::min<uint64_t>(kNodesPerSlot * S, 0xFFFFFFF0ull);
-  DevBuf flags, lchild, vlo, vhi, gtab, ctab, glist, ctl, bstart, bgroups, qi, qrow, roots, ncnt;
+  DevBuf flags, lchild, vlo, vhi, gtab, ctab, glist, ctl, bstart, bgroups, qi, qrow, roots, ncnt, grec, crec, ngrp;
   if (!flags.ensure(ncap) || !lchild.ensure(ncap * 4) || !vlo.ensure(ncap) || !vhi.ensure(ncap) ||
-      !gtab.ensure((size_t)ring * S * lbf_group_bytes()) || !ctab.ensure((size_t)ring * S * lbf_cand_bytes(1)) ||
-      !glist.ensure((size_t)ring * S * 4) || !ctl.ensure(sizeof(FCtl)))
+      !gtab.ensure((size_t)ring * S * lbf_group_bytes()) || !ctab.ensure((size_t)ring * S * lbf_cand_bytes(2)) ||
+      !glist.ensure((size_t)ring * S * 4) || !ctl.ensure(sizeof(FCtl)) || !grec.ensure(S * lbf_grec_bytes()) ||
+      !crec.ensure(S * lbf_crec_bytes(2)) || !ngrp.ensure(S * 4))
     return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier workspace)");
   constexpr uint32_t kChunkMax = 1u << 20;  // the keys' query field
   // one sweep over list entries [c0, c1): 1 done, 0 overflow (split and rerun), < 0 error
   uint64_t last_nodes = 0;
+  int epoch = 0;          // hash tags per chunk: tables are cleared only when the epoch wraps
+  bool dirty = true;      // or after an overflowed chunk (its groups' masks were not consumed)
   auto run_chunk = [&](uint32_t c0, uint32_t c1) -> int {
     const uint32_t nc = c1 - c0;
     FrontierArgs a{};
@@ -3175,7 +3181,7 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
     HIP_OK(c, hipMemcpyAsync(&h, ctl.p, sizeof(FCtl), hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
     const int n_bands = h.max_hi >= 1 ? (int)h.max_band + 1 : 0;
-    if (n_bands > 4094) return fail(c, SST_E_ARG, "length bounds (frontier): a window beyond 4094 bands");
+    if (n_bands > 126) return fail(c, SST_E_ARG, "length bounds (frontier): a window beyond 126 bands");
     if (h.max_hi >= (1ull << 25)) return fail(c, SST_E_ARG, "length bounds (frontier): a window at 2^25 or beyond");
     a.rb = bits_for(h.max_win > 0 ? h.max_win - 1 : 0);
     // unary keys: root bits, one zero per kept rank, one 1 per left move (<= hi / w_min)
@@ -3202,8 +3208,20 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
       return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier bands)");
     a.band_start = (uint32_t*)bstart.p;
     a.band_groups = (uint32_t*)bgroups.p;
-    HIP_OK(c, hipMemsetAsync(gtab.p, 0, gtab.bytes, c->stream));  // empty tables: tag 0 matches no band
-    HIP_OK(c, hipMemsetAsync(ctab.p, 0, ctab.bytes, c->stream));
+    a.grec = (char*)grec.p;
+    a.grec_cap = S;
+    a.crec = (char*)crec.p;
+    a.crec_cap = crec.bytes / lbf_crec_bytes(kw);
+    a.node_group = (uint32_t*)ngrp.p;
+    a.ngrp_cap = S;
+    if (dirty || epoch == 0) {  // empty tables: tag 0 matches no band
+      HIP_OK(c, hipMemsetAsync(gtab.p, 0, gtab.bytes, c->stream));
+      HIP_OK(c, hipMemsetAsync(ctab.p, 0, ctab.bytes, c->stream));
+      epoch = 0;
+      dirty = false;
+    }
+    a.epoch = epoch;
+    epoch = (epoch + 1) & 31;
     {
       Prof p(c, SST_K_LENGTH_BOUND);
       HIP_OK(c, launch_lbf_sweep(a, kw, n_bands, c->n_cu * 8, c->stream));
@@ -3218,6 +3236,7 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
     HIP_OK(c, hipStreamSynchronize(c->stream));
     if (h.overflow & 56u) return fail(c, SST_E_INTERNAL, "length bounds (frontier): inconsistent first-visit tables");
     if (h.overflow) {
+      dirty = true;
       if (stats) stats->splits++;
       if (nc == 1) {  // one query beyond the whole workspace: reported, not guessed
         FQInfo one{};

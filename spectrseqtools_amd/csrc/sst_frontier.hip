@@ -62,8 +62,14 @@ struct FCand {
   uint64_t fk[KW];
 };
 
-__device__ __forceinline__ uint64_t fkey(uint32_t band, uint32_t j, uint32_t m, uint32_t k) {
-  return ((uint64_t)(band + 1) << 52) | ((uint64_t)j << 32) | ((uint64_t)m << 7) | (uint64_t)k;
+// hash keys: tag (12 bits: the chunk's epoch mod 32, band + 1 <= 127) | listed
+// query (20) | mass (25) | rank (7).  A slot whose tag is not the current one
+// is free: stale entries of earlier bands and chunks need no clearing.
+__device__ __forceinline__ uint64_t fkey(uint32_t tagb, uint32_t j, uint32_t m, uint32_t k) {
+  return ((uint64_t)tagb << 52) | ((uint64_t)j << 32) | ((uint64_t)m << 7) | (uint64_t)k;
+}
+__device__ __forceinline__ uint32_t ftagb(const FrontierArgs& a, uint32_t band) {
+  return ((uint32_t)a.epoch << 7) | (band + 1u);
 }
 __device__ __forceinline__ uint32_t ftag(uint64_t key) { return (uint32_t)(key >> 52); }
 __device__ __forceinline__ uint32_t fhash(uint64_t key, uint32_t mask) {
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(256) void k_lbf_roots(FrontierArgs a) {
     bool fresh = false;
     uint32_t gs = 0;
     if (pred) {
-      gs = group_get(G, a.gmask, fkey(0, jj, (uint32_t)v, 0), fresh);
+      gs = group_get(G, a.gmask, fkey(ftagb(a, 0), jj, (uint32_t)v, 0), fresh);
       if (gs == UINT32_MAX) {
         set_overflow(a, 2);
         pred = false;
@@ -285,7 +291,7 @@ __global__ __launch_bounds__(256) void k_lbf_roots(FrontierArgs a) {
       }
     }
     if (pred) {
-      const uint32_t cs = cand_put<KW>(C, a.cmask, fkey(0, jj, (uint32_t)v, (uint32_t)top));
+      const uint32_t cs = cand_put<KW>(C, a.cmask, fkey(ftagb(a, 0), jj, (uint32_t)v, (uint32_t)top));
       if (cs == UINT32_MAX) {
         set_overflow(a, 2);
       } else {
@@ -301,29 +307,57 @@ __global__ __launch_bounds__(256) void k_lbf_roots(FrontierArgs a) {
   }
 }
 
-// band b: every group (query, mass) of the band walks its ranks hv .. lo,
-// choosing each node's first visit among its up and left candidates
+// Band b in two launches.  Within a group (query, mass) the up move keeps
+// the path's key, so the first visit of rank k is the smallest left candidate
+// at ranks k .. hv: FV(m, k) = min_{j >= k} L_j (the up chain carries the
+// winner down; its budgets: A from the winning candidate, B = cap[k] unless
+// the winner is rank k's own).  Every node of the band is then independent:
+//   k_lbf_groups  a lane per group: the group's entry (its masks consumed),
+//                 lo, node ids (ranks lo .. hv ascending), its left
+//                 candidates copied out of the hash (rank descending) with
+//                 their parents' child links, node -> group for the band
+//   k_lbf_nodes   a lane per node: its first visit from the group's
+//                 candidates, the left attempt (mass_table.py:424-441), the
+//                 left child's group and candidate in the band it falls in
 template <int KW>
-__global__ __launch_bounds__(256) void k_lbf_band(FrontierArgs a, int band) {
+struct FCRec {  // a group's left candidate, copied for the node lanes
+  uint64_t fk[KW];
+  uint8_t A, B, rank, pad[5];
+};
+struct FGRec {
+  uint32_t base;   // node id of rank lo
+  uint32_t j;      // listed query (chunk index)
+  uint32_t m;      // mass
+  uint32_t cbase;  // its first candidate record (ranks descending)
+  uint8_t lo, hv, nc, pad;
+};
+
+template <int KW>
+__global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
   if (__hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int lane = threadIdx.x & 63;
-  const uint32_t rmask = (uint32_t)a.ring - 1u;
-  const uint32_t slot = (uint32_t)band & rmask;
+  const uint32_t slot = (uint32_t)band & ((uint32_t)a.ring - 1u);
   const uint32_t ng = a.ctl->list_cnt[slot];
   if (blockIdx.x == 0 && threadIdx.x == 0) a.band_groups[band] = ng;
+  if (ng > a.grec_cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) set_overflow(a, 4);
+    return;
+  }
   const size_t gstride = (size_t)a.gmask + 1, cstride = (size_t)a.cmask + 1;
   FGroup* G = (FGroup*)a.gtab + slot * gstride;
   const FCand<KW>* Cb = (const FCand<KW>*)a.ctab + slot * cstride;
   const uint32_t* Lst = a.glist + slot * gstride;
+  FGRec* GR = (FGRec*)a.grec;
+  FCRec<KW>* CR = (FCRec<KW>*)a.crec;
+  const uint32_t band0 = a.band_start[band];
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   for (uint32_t base = wave * 64u; base < ng; base += nwaves * 64u) {
     const uint32_t gi = base + lane;
     const bool act = gi < ng;
-    uint32_t jj = 0, m = 0;
-    int hv = -1, lo = 0, n = 0;
+    uint32_t jj = 0, m = 0, n = 0, nc = 0;
+    int hv = 0, lo = 0;
     uint64_t mk0 = 0, mk1 = 0;
-    FQInfo q{};
     if (act) {
       const uint32_t gs = Lst[gi];
       const FGroup g = G[gs];
@@ -334,126 +368,174 @@ __global__ __launch_bounds__(256) void k_lbf_band(FrontierArgs a, int band) {
       mk0 = g.mask[0];
       mk1 = g.mask[1];
       hv = mk1 ? 127 - __builtin_clzll(mk1) : 63 - __builtin_clzll(mk0 | 1ull);
-      q = a.qi[jj];
-      lo = a.lr[q.lr_off + m];
-      n = hv >= lo ? hv - lo + 1 : 0;
+      lo = a.lr[a.qi[jj].lr_off + m];
       if (hv < lo || !(mk0 | mk1)) set_overflow(a, 8);  // cannot happen: a candidate's mass is in R_hv
+      else n = (uint32_t)(hv - lo + 1);
+      nc = (uint32_t)(__builtin_popcountll(mk0) + __builtin_popcountll(mk1));
     }
-    const uint32_t incl = wave_incl_u((uint32_t)n);
-    const uint32_t total = __shfl(incl, 63, 64);
-    uint32_t wbase = 0;
-    if (lane == 0) wbase = atomicAdd(&a.ctl->node_ctr, total);
+    // node ids and candidate records: one atomic each per wave
+    const uint32_t incl = wave_incl_u(n), total = __shfl(incl, 63, 64);
+    const uint32_t cincl = wave_incl_u(nc), ctotal = __shfl(cincl, 63, 64);
+    uint32_t wbase = 0, cwbase = 0;
+    if (lane == 0) {
+      wbase = atomicAdd(&a.ctl->node_ctr, total);
+      cwbase = atomicAdd(&a.ctl->crec_ctr, ctotal);
+    }
     wbase = __shfl(wbase, 0, 64);
-    if ((uint64_t)wbase + total > a.ncap) {
+    cwbase = __shfl(cwbase, 0, 64);
+    if ((uint64_t)wbase + total > a.ncap || (uint64_t)wbase + total - band0 > a.ngrp_cap ||
+        (uint64_t)cwbase + ctotal > a.crec_cap) {
       if (lane == 0) set_overflow(a, 1);
       return;
     }
-    const uint32_t id0 = wbase + incl - (uint32_t)n;  // rank lo; rank k at id0 + k - lo
-    if (act && n) atomicAdd(&a.node_cnt[jj], (uint32_t)n);
-    const int steps = wave_max_i(n);
-    uint64_t uk[KW];
-#pragma unroll
-    for (int w = 0; w < KW; ++w) uk[w] = 0;
-    int uA = 0;
-    bool have_u = false;
-    const uint32_t* qrow = a.qrow + (size_t)jj * 128;
-    for (int s = 0; s < steps; ++s) {
-      const bool live = s < n;
-      const int k = hv - s;
-      const uint32_t id = id0 + (uint32_t)(k - lo);
-      const uint32_t rw = live ? qrow[k] : 0u;
-      const int64_t wk = qrow_w(rw);
-      const bool mod = qrow_mod(rw);
-      uint64_t key[KW];
-      int A = 0, B = 0;
-      bool from_l = false;
-      const bool has_c = live && (k < 64 ? ((mk0 >> k) & 1ull) : ((mk1 >> (k - 64)) & 1ull));
-      if (has_c) {
-        const uint32_t cs = cand_find<KW>(Cb, a.cmask, fkey((uint32_t)band, jj, m, (uint32_t)k));
+    if (!act) continue;
+    const uint32_t id0 = wbase + incl - n, c0 = cwbase + cincl - nc;
+    if (n) atomicAdd(&a.node_cnt[jj], n);
+    FGRec r;
+    r.base = id0;
+    r.j = jj;
+    r.m = m;
+    r.cbase = c0;
+    r.lo = (uint8_t)lo;
+    r.hv = (uint8_t)hv;
+    r.nc = (uint8_t)nc;
+    r.pad = 0;
+    GR[gi] = r;
+    for (uint32_t x = 0; x < n; ++x) a.node_group[id0 - band0 + x] = gi;
+    // the left candidates, highest rank first
+    uint32_t t = 0;
+    for (int half = 1; half >= 0; --half) {
+      uint64_t mk = half ? mk1 : mk0;
+      while (mk) {
+        const int k = 64 * half + 63 - __builtin_clzll(mk);
+        mk &= ~(1ull << (k & 63));
+        const uint32_t cs = cand_find<KW>(Cb, a.cmask, fkey(ftagb(a, (uint32_t)band), jj, m, (uint32_t)k));
         if (cs == UINT32_MAX) {
           set_overflow(a, 16);  // cannot happen: the mask bit follows the insertion
-        } else {
-          const FCand<KW>& e = Cb[cs];
-          const uint32_t par = e.parent;
-          uint64_t ck[KW];
+          continue;
+        }
+        const FCand<KW>& e = Cb[cs];
+        const uint32_t par = e.parent, id = id0 + (uint32_t)(k - lo);
+        if (par & kRootBit) a.root_node[par & ~kRootBit] = id;
+        else a.lchild[par] = id;
+        FCRec<KW> cr;
 #pragma unroll
-          for (int w = 0; w < KW; ++w) ck[w] = e.fk[w];
-          if (par & kRootBit) a.root_node[par & ~kRootBit] = id;
-          else a.lchild[par] = id;
-          if (!(have_u && key_less<KW>(uk, ck))) {  // the left parent's path comes first (or is the only one)
-            from_l = true;
+        for (int w = 0; w < KW; ++w) cr.fk[w] = e.fk[w];
+        cr.A = e.A;
+        cr.B = e.B;
+        cr.rank = (uint8_t)k;
+        CR[c0 + t++] = cr;
+      }
+    }
+  }
+}
+
+template <int KW>
+__global__ __launch_bounds__(256) void k_lbf_nodes(FrontierArgs a, int band) {
+  if (__hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int lane = threadIdx.x & 63;
+  const uint32_t rmask = (uint32_t)a.ring - 1u;
+  const uint32_t band0 = a.band_start[band];
+  const uint32_t nn = a.ctl->node_ctr - band0;  // this band's nodes (k_lbf_groups allocated them)
+  const size_t gstride = (size_t)a.gmask + 1, cstride = (size_t)a.cmask + 1;
+  const FGRec* GR = (const FGRec*)a.grec;
+  const FCRec<KW>* CR = (const FCRec<KW>*)a.crec;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t base = wave * 64u; base < nn; base += nwaves * 64u) {
+    const uint32_t x = base + lane;
+    const bool live = x < nn;
+    const uint32_t id = band0 + x;
+    uint32_t jj = 0, m = 0;
+    int k = 0, lo = 0;
+    uint64_t key[KW];
 #pragma unroll
-            for (int w = 0; w < KW; ++w) key[w] = ck[w];
-            A = e.A;
-            B = e.B;
-          }
+    for (int w = 0; w < KW; ++w) key[w] = 0;
+    int A = 0, B = 0;
+    uint32_t rw = 0;
+    FQInfo q{};
+    if (live) {
+      const FGRec r = GR[a.node_group[x]];
+      jj = r.j;
+      m = r.m;
+      lo = r.lo;
+      k = lo + (int)(id - r.base);
+      q = a.qi[jj];
+      rw = a.qrow[(size_t)jj * 128 + k];
+      // the smallest left candidate at ranks >= k (ranks descending: stop below k)
+      int win = -1;
+      for (uint32_t t = 0; t < r.nc; ++t) {
+        const FCRec<KW>& c = CR[r.cbase + t];
+        if ((int)c.rank < k) break;
+        uint64_t ck[KW];
+#pragma unroll
+        for (int w = 0; w < KW; ++w) ck[w] = c.fk[w];
+        if (win < 0 || key_less<KW>(ck, key)) {
+#pragma unroll
+          for (int w = 0; w < KW; ++w) key[w] = ck[w];
+          A = c.A;
+          B = c.B;
+          win = c.rank;
         }
       }
-      if (!from_l) {  // up from (m, k + 1): same path, B = cap of this row (mass_table.py:411-420)
-#pragma unroll
-        for (int w = 0; w < KW; ++w) key[w] = uk[w];
-        A = uA;
-        B = qrow_cap(rw);
+      if (win != k) B = qrow_cap(rw);  // reached by the up chain: B = cap of this row (mass_table.py:411-420)
+    }
+    const int64_t wk = qrow_w(rw);
+    const bool mod = qrow_mod(rw);
+    // the left branch (mass_table.py:424-441): bit1 <=> m - w_k in R_k
+    const int64_t m2 = (int64_t)m - wk;
+    const bool b1 = live && m2 >= 0 && (m2 == 0 || (int)a.lr[q.lr_off + m2] <= k);
+    const bool latt = b1 && (!mod || (A > 0 && B > 0));
+    if (live) a.flags[id] = (uint8_t)((latt ? kFLeft : 0) | (k > lo ? kFUp : 0) | (latt && m2 == 0 ? kFZero : 0));
+    bool emit = latt && m2 > 0;
+    const uint32_t band2 = emit ? (uint32_t)((q.hi - m2) / a.wb) : 0u;
+    const uint32_t slot2 = band2 & rmask;
+    uint32_t gs2 = 0;
+    bool fresh = false;
+    if (emit) {
+      FGroup* G2 = (FGroup*)a.gtab + slot2 * gstride;
+      gs2 = group_get(G2, a.gmask, fkey(ftagb(a, band2), jj, (uint32_t)m2, 0), fresh);
+      if (gs2 == UINT32_MAX) {
+        set_overflow(a, 2);
+        emit = false;
+        fresh = false;
+      } else {
+        atomicOr((unsigned long long*)&G2[gs2].mask[k >> 6], 1ull << (k & 63));
       }
-      // the left branch (mass_table.py:424-441): bit1 <=> m - w_k in R_k
-      const int64_t m2 = (int64_t)m - wk;
-      const bool b1 = live && m2 >= 0 && (m2 == 0 || (int)a.lr[q.lr_off + m2] <= k);
-      const bool latt = b1 && (!mod || (A > 0 && B > 0));
-      if (live) a.flags[id] = (uint8_t)((latt ? kFLeft : 0) | (k > lo ? kFUp : 0) | (latt && m2 == 0 ? kFZero : 0));
-      bool emit = latt && m2 > 0;
-      const uint32_t band2 = emit ? (uint32_t)((q.hi - m2) / a.wb) : 0u;
-      const uint32_t slot2 = band2 & rmask;
-      uint32_t gs2 = 0;
-      bool fresh = false;
-      if (emit) {
-        FGroup* G2 = (FGroup*)a.gtab + slot2 * gstride;
-        gs2 = group_get(G2, a.gmask, fkey(band2, jj, (uint32_t)m2, 0), fresh);
-        if (gs2 == UINT32_MAX) {
-          set_overflow(a, 2);
-          emit = false;
-          fresh = false;
-        } else {
-          atomicOr((unsigned long long*)&G2[gs2].mask[k >> 6], 1ull << (k & 63));
+    }
+    for (int d = 1; d <= a.jump; ++d) {  // fresh groups join their band's list: one atomic per wave and band
+      const bool pd = fresh && band2 == (uint32_t)band + (uint32_t)d;
+      const uint64_t bm = __ballot(pd);
+      if (bm) {
+        const int leader = __builtin_ctzll(bm);
+        const uint32_t sl = ((uint32_t)band + (uint32_t)d) & rmask;
+        uint32_t b0 = 0;
+        if (lane == leader) b0 = atomicAdd(&a.ctl->list_cnt[sl], (uint32_t)__builtin_popcountll(bm));
+        b0 = __shfl(b0, leader, 64);
+        if (pd) {
+          const uint32_t at = b0 + (uint32_t)__builtin_popcountll(bm & lanemask_lt());
+          if (at > a.gmask) set_overflow(a, 4);
+          else a.glist[sl * gstride + at] = gs2;
         }
       }
-      for (int d = 1; d <= a.jump; ++d) {  // fresh groups join their band's list: one atomic per wave and band
-        const bool pd = fresh && band2 == (uint32_t)band + (uint32_t)d;
-        const uint64_t bm = __ballot(pd);
-        if (bm) {
-          const int leader = __builtin_ctzll(bm);
-          const uint32_t sl = ((uint32_t)band + (uint32_t)d) & rmask;
-          uint32_t b0 = 0;
-          if (lane == leader) b0 = atomicAdd(&a.ctl->list_cnt[sl], (uint32_t)__builtin_popcountll(bm));
-          b0 = __shfl(b0, leader, 64);
-          if (pd) {
-            const uint32_t at = b0 + (uint32_t)__builtin_popcountll(bm & lanemask_lt());
-            if (at > a.gmask) set_overflow(a, 4);
-            else a.glist[sl * gstride + at] = gs2;
-          }
-        }
+    }
+    if (emit) {
+      FCand<KW>* C2 = (FCand<KW>*)a.ctab + slot2 * cstride;
+      const uint32_t cs = cand_put<KW>(C2, a.cmask, fkey(ftagb(a, band2), jj, (uint32_t)m2, (uint32_t)k));
+      if (cs == UINT32_MAX) {
+        set_overflow(a, 2);
+      } else {
+        uint64_t k2[KW];
+#pragma unroll
+        for (int w = 0; w < KW; ++w) k2[w] = key[w];
+        key_set_msb<KW>(k2, a.rb + key_ones<KW>(key, a.rb) + ((int)q.K - 1 - k));
+        FCand<KW>& e = C2[cs];
+        e.parent = id;
+        e.A = (uint8_t)(mod ? A - 1 : A);
+        e.B = (uint8_t)(mod ? B - 1 : B);
+#pragma unroll
+        for (int w = 0; w < KW; ++w) e.fk[w] = k2[w];
       }
-      if (emit) {
-        FCand<KW>* C2 = (FCand<KW>*)a.ctab + slot2 * cstride;
-        const uint32_t cs = cand_put<KW>(C2, a.cmask, fkey(band2, jj, (uint32_t)m2, (uint32_t)k));
-        if (cs == UINT32_MAX) {
-          set_overflow(a, 2);
-        } else {
-          uint64_t k2[KW];
-#pragma unroll
-          for (int w = 0; w < KW; ++w) k2[w] = key[w];
-          key_set_msb<KW>(k2, a.rb + key_ones<KW>(key, a.rb) + ((int)q.K - 1 - k));
-          FCand<KW>& e = C2[cs];
-          e.parent = id;
-          e.A = (uint8_t)(mod ? A - 1 : A);
-          e.B = (uint8_t)(mod ? B - 1 : B);
-#pragma unroll
-          for (int w = 0; w < KW; ++w) e.fk[w] = k2[w];
-        }
-      }
-#pragma unroll
-      for (int w = 0; w < KW; ++w) uk[w] = key[w];
-      uA = A;
-      have_u = live;
     }
   }
 }
@@ -462,6 +544,7 @@ __global__ __launch_bounds__(256) void k_lbf_band(FrontierArgs a, int band) {
 // next band's heaviest children will fill
 __global__ void k_lbf_mark(FrontierArgs a, int band) {
   a.band_start[band] = a.ctl->node_ctr;
+  a.ctl->crec_ctr = 0;  // the candidate records are per band
   a.ctl->list_cnt[((uint32_t)band + (uint32_t)a.jump) & ((uint32_t)a.ring - 1u)] = 0;
 }
 
@@ -593,7 +676,8 @@ static hipError_t sweep(const FrontierArgs& a, int n_bands, int band_blocks, hip
   hipLaunchKernelGGL(k_lbf_roots<KW>, dim3((a.n_chunk + 255) / 256), dim3(256), 0, st, a);
   for (int b = 0; b < n_bands; ++b) {
     hipLaunchKernelGGL(k_lbf_mark, dim3(1), dim3(1), 0, st, a, b);
-    hipLaunchKernelGGL(k_lbf_band<KW>, dim3(band_blocks), dim3(256), 0, st, a, b);
+    hipLaunchKernelGGL(k_lbf_groups<KW>, dim3(band_blocks), dim3(256), 0, st, a, b);
+    hipLaunchKernelGGL(k_lbf_nodes<KW>, dim3(band_blocks), dim3(256), 0, st, a, b);
   }
   hipLaunchKernelGGL(k_lbf_mark, dim3(1), dim3(1), 0, st, a, n_bands);
   for (int b = n_bands - 1; b >= 0; --b) hipLaunchKernelGGL(k_lbf_values, dim3(band_blocks), dim3(256), 0, st, a, b);
@@ -618,5 +702,13 @@ size_t lbf_cand_bytes(int key_words) {
   }
 }
 size_t lbf_group_bytes() { return sizeof(FGroup); }
+size_t lbf_grec_bytes() { return sizeof(FGRec); }
+size_t lbf_crec_bytes(int key_words) {
+  switch (key_words) {
+    case 1: return sizeof(FCRec<1>);
+    case 2: return sizeof(FCRec<2>);
+    default: return sizeof(FCRec<4>);
+  }
+}
 
 }  // namespace sst

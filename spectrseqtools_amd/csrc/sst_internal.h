@@ -313,7 +313,7 @@ struct FCtl {
   uint32_t node_ctr;
   uint32_t overflow;  // bit 0 nodes, 1 a hash table, 2 a band list, 3/4/5 internal
   uint32_t list_cnt[8];
-  uint32_t max_band, max_win, max_k, pad;
+  uint32_t max_band, max_win, max_k, crec_ctr;
   uint64_t max_hi;
 };
 struct FrontierArgs {
@@ -333,6 +333,7 @@ struct FrontierArgs {
   int wb;          // band width: the table's lightest row (every left move crosses >= 1 band)
   int ring, jump;  // hash / list ring size (power of two > jump), max bands one left move crosses
   int rb;          // key: root index bits (then the ranks in unary)
+  int epoch;       // hash tags of this chunk (0..31; the tables are cleared when it wraps)
   int rstride;     // root slots per query
   int n_bands;     // band_start[n_bands] = the chunk's node count (after the last band)
   FQInfo* qi;
@@ -356,11 +357,21 @@ struct FrontierArgs {
   int8_t* status;
   uint64_t* nodes_out;
   uint32_t* node_cnt;  // [n_chunk] memo entries per listed query (added to nodes_out when the chunk completes)
+  // the band being processed: its groups' records (list order), their left
+  // candidates, and node (id - band start) -> group
+  char* grec;
+  uint64_t grec_cap;
+  char* crec;
+  uint64_t crec_cap;
+  uint32_t* node_group;
+  uint64_t ngrp_cap;
 };
 hipError_t launch_lbf_setup(const TableArgs& t, const FrontierArgs& a, hipStream_t st);
 hipError_t launch_lbf_sweep(const FrontierArgs& a, int key_words, int n_bands, int band_blocks, hipStream_t st);
 size_t lbf_cand_bytes(int key_words);
 size_t lbf_group_bytes();
+size_t lbf_grec_bytes();
+size_t lbf_crec_bytes(int key_words);
 
 struct ExactWs {
   char* hash;
