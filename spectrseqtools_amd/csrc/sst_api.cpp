@@ -83,6 +83,19 @@ struct sst_ctx {
   DevBuf ws_deep;
   DevBuf ws_hash, ws_frames, ws_stacks, ws_epochs;
   DevBuf singleton_masses;  // sorted, de-duplicated integer masses of the last is_singleton call
+  // the first-visit frontier's workspace (sst_length_bounds_frontier_device):
+  // kept across calls (a config-5 run makes one call per batch of alphabets;
+  // allocating tens of GB per call costs seconds), with its hash epoch and the
+  // memo entries per query seen so far (the next call's first chunk size)
+  struct LbfWs {
+    DevBuf flags, lchild, vlo, vhi, gtab, ctab, glist, ctl, bstart, bgroups, qi, qrow, roots, ncnt, grec, crec, ngrp;
+    uint64_t S = 0, ncap = 0, budget = 0;
+    bool by_default = false;
+    int epoch = 0;
+    bool dirty = true;
+    uint64_t done_q = 0, done_nodes = 0;
+    double band_frac = 0.3;  // the largest band's share of a chunk's nodes seen so far
+  } lbf;
   uint32_t hash_cap = 0;
   int exact_blocks = 0;
   int n_cu = 256;       // compute units (persistent grid sizing)
@@ -3113,7 +3126,9 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
   // and a candidate entry (32 B: 128-bit keys), and the band's group record
   // (20 B) and candidate record (24 B); S slots, S a power of two (hashing)
   size_t budget = workspace_bytes;
-  if (budget == 0) {
+  if (budget == 0 && c->lbf.S && c->lbf.by_default) {
+    budget = c->lbf.budget;  // the default workspace of an earlier call
+  } else if (budget == 0) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
       (void)hipGetLastError();
@@ -3124,20 +3139,31 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
   constexpr uint64_t kNodesPerSlot = 8;
   const size_t per_slot = kNodesPerSlot * 7 + 4 + (size_t)ring * (lbf_group_bytes() + 4 + lbf_cand_bytes(2)) +
                           lbf_grec_bytes() + lbf_crec_bytes(2);
-  uint64_t S = pow2_floor(std::max<size_t>(1024, budget / per_slot));
-  if (S > (1ull << 31)) S = 1ull << 31;
-  const uint64_t ncap = std::min<uint64_t>(kNodesPerSlot * S, 0xFFFFFFF0ull);
-  DevBuf flags, lchild, vlo, vhi, gtab, ctab, glist, ctl, bstart, bgroups, qi, qrow, roots, ncnt, grec, crec, ngrp;
+  auto& W = c->lbf;
+  if (W.budget != budget) {  // (re)size the ctx's workspace: the first call, or another budget
+    W = sst_ctx::LbfWs{};
+    W.budget = budget;
+    W.by_default = workspace_bytes == 0;
+    W.S = pow2_floor(std::max<size_t>(1024, budget / per_slot));
+    if (W.S > (1ull << 31)) W.S = 1ull << 31;
+    W.ncap = std::min<uint64_t>(kNodesPerSlot * W.S, 0xFFFFFFF0ull);
+  }
+  const uint64_t S = W.S, ncap = W.ncap;
+  DevBuf &flags = W.flags, &lchild = W.lchild, &vlo = W.vlo, &vhi = W.vhi, &gtab = W.gtab, &ctab = W.ctab,
+         &glist = W.glist, &ctl = W.ctl, &bstart = W.bstart, &bgroups = W.bgroups, &qi = W.qi, &qrow = W.qrow,
+         &roots = W.roots, &ncnt = W.ncnt, &grec = W.grec, &crec = W.crec, &ngrp = W.ngrp;
   if (!flags.ensure(ncap) || !lchild.ensure(ncap * 4) || !vlo.ensure(ncap) || !vhi.ensure(ncap) ||
       !gtab.ensure((size_t)ring * S * lbf_group_bytes()) || !ctab.ensure((size_t)ring * S * lbf_cand_bytes(2)) ||
       !glist.ensure((size_t)ring * S * 4) || !ctl.ensure(sizeof(FCtl)) || !grec.ensure(S * lbf_grec_bytes()) ||
-      !crec.ensure(S * lbf_crec_bytes(2)) || !ngrp.ensure(S * 4))
+      !crec.ensure(S * lbf_crec_bytes(2)) || !ngrp.ensure(S * 4)) {
+    c->lbf = sst_ctx::LbfWs{};
     return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier workspace)");
+  }
   constexpr uint32_t kChunkMax = 1u << 20;  // the keys' query field
   // one sweep over list entries [c0, c1): 1 done, 0 overflow (split and rerun), < 0 error
   uint64_t last_nodes = 0;
-  int epoch = 0;          // hash tags per chunk: tables are cleared only when the epoch wraps
-  bool dirty = true;      // or after an overflowed chunk (its groups' masks were not consumed)
+  int& epoch = W.epoch;  // hash tags per chunk: tables are cleared only when the epoch wraps
+  bool& dirty = W.dirty;  // or after an overflowed chunk (its groups' masks were not consumed)
   auto run_chunk = [&](uint32_t c0, uint32_t c1) -> int {
     const uint32_t nc = c1 - c0;
     FrontierArgs a{};
@@ -3250,6 +3276,11 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
       return 0;
     }
     last_nodes = h.node_ctr;
+    if (h.node_ctr > (1u << 24)) {  // the bands' shape: sizes the next chunks against the per-band capacities
+      uint32_t mb = 0;
+      for (int b = 0; b < n_bands; ++b) mb = std::max<uint32_t>(mb, band_start[b + 1] - band_start[b]);
+      W.band_frac = std::max(W.band_frac * 0.9, (double)mb / (double)h.node_ctr);
+    }
     if (stats) {
       stats->chunks++;
       stats->nodes += h.node_ctr;
@@ -3263,16 +3294,19 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
     }
     return 1;
   };
-  // chunks sized from the nodes per query seen so far (a first chunk of 256),
-  // aiming at half the node capacity; a chunk that overflows is split in halves
-  uint64_t done_q = 0, done_nodes = 0;
+  // chunks sized from the nodes per query seen so far (this ctx's earlier
+  // calls included; a first chunk of 256), aiming at half the node capacity;
+  // a chunk that overflows is split in halves
+  uint64_t &done_q = W.done_q, &done_nodes = W.done_nodes;
   uint32_t c0 = 0;
   while (c0 < n_live) {
     uint32_t nc = std::min<uint32_t>(n_live - c0, 256);
     if (done_q && done_nodes) {
+      // nodes per chunk: half the node capacity, and a largest band of at most
+      // 40 % of the per-band capacities (S node -> group entries, hash slots)
       const double per_q = (double)done_nodes / (double)done_q;
-      nc = (uint32_t)std::max<double>(1.0, std::min<double>({(double)(n_live - c0), (double)kChunkMax,
-                                                              0.5 * (double)ncap / per_q}));
+      const double target = std::min(0.5 * (double)ncap, 0.4 * (double)S / std::max(0.02, W.band_frac));
+      nc = (uint32_t)std::max<double>(1.0, std::min<double>({(double)(n_live - c0), (double)kChunkMax, target / per_q}));
     } else if (done_q) {
       nc = std::min<uint32_t>(n_live - c0, kChunkMax);
     }

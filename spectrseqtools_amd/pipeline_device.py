@@ -15,6 +15,7 @@ the device memory only; every computation is the library's.
 import ctypes
 import os
 import sys
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -1014,6 +1015,7 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
             wu_t = torch.as_tensor(wb, device=dev)
             ou_t = torch.as_tensor(off_u, device=dev)
             lo_u_t = torch.as_tensor(lr_off, device=dev)
+            t_batch = time.perf_counter()
             eng.check(L.sst_reach_rows_device(h, alu_t.data_ptr(), wu_t.data_ptr(), ou_t.data_ptr(), nu,
                                               bits.data_ptr()), "sst_reach_rows_device")
             eng.check(L.sst_reach_lowest_device(h, alu_t.data_ptr(), wu_t.data_ptr(), ou_t.data_ptr(), nu,
@@ -1022,6 +1024,7 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
             eng.synchronize()
             del bits
             torch.cuda.empty_cache()
+            t_reach = time.perf_counter() - t_batch
             lu_src = by_u[u_first[u0]:u_first[u1]]
             members = sel[lu_src]
             n = len(members)
@@ -1054,8 +1057,8 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
                 else:
                     stats["frontier"][k_] = stats["frontier"].get(k_, 0) + v_
             if _PROGRESS:
-                print(f"[length] frontier batch {stats['batches']}: {n} spectra, {nu} alphabets: {fd}",
-                      file=sys.stderr, flush=True)
+                print(f"[length] frontier batch {stats['batches']}: {n} spectra, {nu} alphabets, reach "
+                      f"{t_reach:.3f}s, batch {time.perf_counter() - t_batch:.3f}s: {fd}", file=sys.stderr, flush=True)
             del lr
             stats["batches"] += 1
             u0 = u1
