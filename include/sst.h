@@ -819,6 +819,7 @@ typedef struct sst_lbf_stats {
   int64_t max_band_nodes;  /* memo entries of the fullest band */
   int64_t table_slots;     /* slots per hash table of the ring */
   int64_t node_cap;        /* node capacity per chunk */
+  int64_t overflow_bits;   /* why chunks were split: 1 nodes / a band's records, 2 a hash table, 4 a band list */
 } sst_lbf_stats;
 int sst_reach_lowest_device(sst_table* t, const uint64_t* d_alpha, const int64_t* d_words, const uint64_t* d_off,
                             int64_t n_spec, const uint32_t* d_bits, const uint64_t* d_lr_off, uint8_t* d_lr);

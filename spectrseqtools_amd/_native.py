@@ -97,7 +97,8 @@ class PostArgs(ctypes.Structure):
 class LbfStats(ctypes.Structure):
     """sst_lbf_stats (include/sst.h): the first-visit frontier's record."""
     _fields_ = [(n, ctypes.c_int64) for n in ("live", "nodes", "chunks", "splits", "aborted", "bands", "key_words",
-                                             "max_band_groups", "max_band_nodes", "table_slots", "node_cap")]
+                                             "max_band_groups", "max_band_nodes", "table_slots", "node_cap",
+                                             "overflow_bits")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

@@ -3263,7 +3263,10 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
     if (h.overflow & 56u) return fail(c, SST_E_INTERNAL, "length bounds (frontier): inconsistent first-visit tables");
     if (h.overflow) {
       dirty = true;
-      if (stats) stats->splits++;
+      if (stats) {
+        stats->splits++;
+        stats->overflow_bits |= h.overflow;
+      }
       if (nc == 1) {  // one query beyond the whole workspace: reported, not guessed
         FQInfo one{};
         HIP_OK(c, hipMemcpyAsync(&one, qi.p, sizeof(FQInfo), hipMemcpyDeviceToHost, c->stream));
@@ -3297,14 +3300,16 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
   // chunks sized from the nodes per query seen so far (this ctx's earlier
   // calls included; a first chunk of 256), aiming at half the node capacity;
   // a chunk that overflows is split in halves
-  uint64_t &done_q = W.done_q, &done_nodes = W.done_nodes;
+  // (this call's queries once it has some: alphabets differ between calls)
+  uint64_t done_q = 0, done_nodes = 0;
   uint32_t c0 = 0;
   while (c0 < n_live) {
     uint32_t nc = std::min<uint32_t>(n_live - c0, 256);
-    if (done_q && done_nodes) {
+    if ((done_q && done_nodes) || (W.done_q && W.done_nodes)) {
       // nodes per chunk: half the node capacity, and a largest band of at most
       // 40 % of the per-band capacities (S node -> group entries, hash slots)
-      const double per_q = (double)done_nodes / (double)done_q;
+      const double per_q = done_q && done_nodes ? (double)done_nodes / (double)done_q
+                                                : 4.0 * (double)W.done_nodes / (double)W.done_q;
       const double target = std::min(0.5 * (double)ncap, 0.4 * (double)S / std::max(0.02, W.band_frac));
       nc = (uint32_t)std::max<double>(1.0, std::min<double>({(double)(n_live - c0), (double)kChunkMax, target / per_q}));
     } else if (done_q) {
@@ -3324,6 +3329,8 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
       }
       done_q += a1 - a0;
       done_nodes += last_nodes;
+      W.done_q += a1 - a0;
+      W.done_nodes += last_nodes;
     }
     c0 += nc;
   }

@@ -1054,6 +1054,8 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
             for k_, v_ in fd.items():
                 if k_ in ("bands", "key_words", "max_band_groups", "max_band_nodes", "table_slots", "node_cap"):
                     stats["frontier"][k_] = max(stats["frontier"].get(k_, 0), v_)
+                elif k_ == "overflow_bits":
+                    stats["frontier"][k_] = stats["frontier"].get(k_, 0) | v_
                 else:
                     stats["frontier"][k_] = stats["frontier"].get(k_, 0) + v_
             if _PROGRESS:
