@@ -342,10 +342,16 @@ int sst_result_stats(const sst_result* r, uint64_t* stats_out /* [8] */);
  * batched over (su_mass, obs_mass) pairs: window = round(su/precision) +-
  * ceil(tolerance*obs/precision); max_mods = round(seq.modification_rate *
  * seq.max_len) (:351); per-row caps from sst_table_set_budgets; direction 0 =
- * "lower", 1 = "upper", optionally | SST_LB_EXACT_ONLY.  out[i] = the bound; status[i]: 0 ok, SST_OUT_OF_TABLE
- * (the reference raises NotImplementedError), SST_LB_EMPTY_WINDOW (its
- * min([]) raises ValueError), SST_ABORTED (DFS node budget exhausted: no
- * bound).  Synchronous, host buffers. */
+ * "lower", 1 = "upper", optionally | SST_LB_EXACT_ONLY | SST_LB_REPLAY.
+ * Windows whose budgets provably never bind come from layered reachability;
+ * the others, on a table built here (a closure of its rows), from the
+ * first-visit frontier (as sst_length_bounds_frontier_device, with the
+ * table's own rows; a 4 GB workspace kept in the ctx), or from the replay
+ * of the memoised DFS (windows in the table's last packed word, tables
+ * uploaded as they are, SST_LB_REPLAY).  out[i] = the bound; status[i]: 0
+ * ok, SST_OUT_OF_TABLE (the reference raises NotImplementedError),
+ * SST_LB_EMPTY_WINDOW (its min([]) raises ValueError), SST_ABORTED (DFS node
+ * budget exhausted: no bound).  Synchronous, host buffers. */
 #define SST_LB_EMPTY_WINDOW (-5)
 /* sst_length_bound_batch on per-query reduced alphabets (the table
  * adapt_individual_modification_rates_by_alphabet_reduction would rebuild,
@@ -365,6 +371,7 @@ int sst_length_bound_alpha_batch(sst_table* t, const double* su_mass, const doub
                                  double precision, int max_len, int64_t max_mods, int direction, int64_t* out,
                                  int8_t* status);
 #define SST_LB_EXACT_ONLY 2 /* direction flag: skip the layered fast path (tests) */
+#define SST_LB_REPLAY 4     /* direction flag: the replay instead of the first-visit frontier (tests) */
 int sst_length_bound_batch(sst_table* t, const double* su_mass, const double* obs_mass, int64_t n, double tolerance,
                            double precision, int max_len, int64_t max_mods, int direction, int64_t* out,
                            int8_t* status);

@@ -701,9 +701,10 @@ class DeviceTable:
         return out
 
     def length_bound(self, su_masses, obs_masses, tolerance, precision, max_len, max_mods, direction,
-                     exact_only=False):
+                     exact_only=False, replay=False):
         """compute_sequence_length_bound for each (su, obs) pair: (bounds int64[n], status int8[n]).
-        exact_only: skip the layered fast path (cross-checks in tests)."""
+        exact_only: skip the layered fast path; replay: the DFS replay instead of
+        the first-visit frontier (cross-checks in tests)."""
         su = np.ascontiguousarray(su_masses, dtype=np.float64)
         ob = np.ascontiguousarray(obs_masses, dtype=np.float64)
         if su.shape != ob.shape:
@@ -712,6 +713,7 @@ class DeviceTable:
         st = np.zeros(len(su), np.int8)
         d = {"lower": 0, "upper": 1}[direction] if isinstance(direction, str) else int(direction)
         d |= 2 if exact_only else 0  # SST_LB_EXACT_ONLY
+        d |= 4 if replay else 0  # SST_LB_REPLAY
         self.engine.check(self.engine._lib.sst_length_bound_batch(self.handle, _ptr(su), _ptr(ob), len(su),
                                                                   float(tolerance), float(precision), int(max_len),
                                                                   int(max_mods), d, _ptr(out), _ptr(st)),

@@ -95,7 +95,7 @@ struct sst_ctx {
     bool dirty = true;
     uint64_t done_q = 0, done_nodes = 0;
     double band_frac = 0.3;  // the largest band's share of a chunk's nodes seen so far
-  } lbf;
+  } lbf, lbf_small;  // lbf_small: sst_length_bound_batch's (one table, few queries; 4 GB)
   uint32_t hash_cap = 0;
   int exact_blocks = 0;
   int n_cu = 256;       // compute units (persistent grid sizing)
@@ -2352,12 +2352,20 @@ int sst_is_valid_alpha(sst_table* t, const double* mass, const double* thr, cons
 }
 
 }  // extern "C"
+static int lbf_frontier(sst_table* t, sst_ctx::LbfWs& W, const double* d_su, const double* d_obs,
+                        const int32_t* d_spec, const uint64_t* d_alpha, const uint8_t* d_lr, const uint64_t* d_lr_off,
+                        int64_t n, double tol, double prec, int max_len, int64_t max_mods, int64_t* d_lower,
+                        int64_t* d_upper, int8_t* d_status, const int32_t* d_qlen, const int32_t* d_caps_len,
+                        const int32_t* d_a0_len, uint64_t* d_nodes, uint64_t workspace_bytes, sst_lbf_stats* stats);
 namespace {
+constexpr uint64_t kBatchFrontierBytes = 4ull << 30;  // sst_length_bound_batch's frontier workspace
+
 static int length_bound_batch(sst_table* t, const double* su, const double* obs, int64_t n, double tol, double prec,
                               int max_len, int64_t max_mods, int direction, int64_t* out, int8_t* status,
                               const int32_t* spec, const uint64_t* alpha, int64_t n_alpha) {
   const bool exact_only = (direction & SST_LB_EXACT_ONLY) != 0;
-  direction &= ~SST_LB_EXACT_ONLY;
+  const bool replay_only = (direction & SST_LB_REPLAY) != 0;
+  direction &= ~(SST_LB_EXACT_ONLY | SST_LB_REPLAY);
   if (!t || n < 0 || n > INT32_MAX || (n > 0 && (!su || !obs || !out || !status)) || (direction != 0 && direction != 1) ||
       max_len < 0 || max_len > 120)
     return SST_E_ARG;
@@ -2434,6 +2442,58 @@ static int length_bound_batch(sst_table* t, const double* su, const double* obs,
   HIP_OK(c, hipMemcpyAsync(&n_exact, d_cnt.p, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(c, hipStreamSynchronize(c->stream));
   std::vector<int8_t> st(nn);
+  DevBuf f_alpha, f_words, f_off, f_bits, f_lr, f_lro, f_spec, f_lo, f_hi, f_st;
+  bool frontier_ok = t->closure && !alpha && !replay_only && t->args.w_min >= 1024;  // (the reach rows' LDS ring)
+  for (int r = 1; r < t->n_rows && frontier_ok; ++r) frontier_ok = t->masses[r] < (1 << 20);
+  if (n_exact && frontier_ok) {
+    // the first-visit frontier on the table's own rows, both
+    // directions for every query of the call (the fast path's answers are the
+    // same); a window in the table's last packed word, where the frontier's
+    // reachability cannot see the last-column mask (SST_ABORTED there), goes
+    // on to the replay below
+    int64_t hmax = 1;
+    for (int64_t i = 0; i < n; ++i)
+      hmax = std::max<int64_t>(hmax, (int64_t)((su[i] + tol * std::fabs(obs[i])) / prec) + 4);
+    hmax = std::min<int64_t>(hmax, t->n_cols * t->C);
+    const int64_t words = hmax / 32 + 2;
+    uint64_t am[2] = {0, 0};
+    for (int r = 1; r < t->n_rows; ++r) am[r >> 6] |= 1ull << (r & 63);
+    const int64_t zero = 0;
+    const size_t K = (size_t)(t->n_rows - 1);
+    if (!f_alpha.ensure(16) || !f_words.ensure(8) || !f_off.ensure(8) || !f_bits.ensure(K * words * 4) ||
+        !f_lr.ensure((size_t)words * 32) || !f_lro.ensure(8) || !f_spec.ensure(nn * 4) || !f_lo.ensure(nn * 8) ||
+        !f_hi.ensure(nn * 8) || !f_st.ensure(nn))
+      return fail(c, SST_E_NOMEM, "device allocation failed (length bound, frontier)");
+    HIP_OK(c, hipMemcpyAsync(f_alpha.p, am, 16, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipMemcpyAsync(f_words.p, &words, 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipMemcpyAsync(f_off.p, &zero, 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipMemcpyAsync(f_lro.p, &zero, 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipMemsetAsync(f_spec.p, 0, nn * 4, c->stream));
+    if (int rc = sst_reach_rows_device(t, (const uint64_t*)f_alpha.p, (const int64_t*)f_words.p,
+                                       (const uint64_t*)f_off.p, 1, (uint32_t*)f_bits.p))
+      return rc;
+    if (int rc = sst_reach_lowest_device(t, (const uint64_t*)f_alpha.p, (const int64_t*)f_words.p,
+                                         (const uint64_t*)f_off.p, 1, (const uint32_t*)f_bits.p,
+                                         (const uint64_t*)f_lro.p, (uint8_t*)f_lr.p))
+      return rc;
+    if (int rc = lbf_frontier(t, c->lbf_small, q.su, q.obs, (const int32_t*)f_spec.p, (const uint64_t*)f_alpha.p,
+                              (const uint8_t*)f_lr.p, (const uint64_t*)f_lro.p, n, tol, prec, max_len, max_mods,
+                              (int64_t*)f_lo.p, (int64_t*)f_hi.p, (int8_t*)f_st.p, nullptr, nullptr, nullptr, nullptr,
+                              kBatchFrontierBytes, nullptr))
+      return rc;
+    HIP_OK(c, hipMemcpyAsync(d_out.p, direction ? f_hi.p : f_lo.p, nn * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIP_OK(c, hipMemcpyAsync(d_st.p, f_st.p, nn, hipMemcpyDeviceToDevice, c->stream));
+    HIP_OK(c, hipMemcpyAsync(st.data(), f_st.p, nn, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> rest;
+    for (size_t i = 0; i < nn; ++i)
+      if (st[i] == SST_ABORTED) rest.push_back((uint32_t)i);
+    n_exact = (uint32_t)rest.size();
+    if (n_exact) {
+      HIP_OK(c, hipMemcpyAsync(d_list.p, rest.data(), rest.size() * 4, hipMemcpyHostToDevice, c->stream));
+      HIP_OK(c, hipMemcpyAsync(d_cnt.p, &n_exact, 4, hipMemcpyHostToDevice, c->stream));
+    }
+  }
   if (n_exact) {
     // one 64-lane block per query in flight (k_length_exact<WAVE>), each with
     // its own memo slice: up to 1 024 at once (4 waves per CU; the memo slices
@@ -3064,13 +3124,11 @@ uint64_t pow2_floor(uint64_t x) {
 }
 }  // namespace
 
-extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_su, const double* d_obs,
-                                                 const int32_t* d_spec, const uint64_t* d_alpha, const uint8_t* d_lr,
-                                                 const uint64_t* d_lr_off, int64_t n, double tol, double prec,
-                                                 int max_len, int64_t max_mods, int64_t* d_lower, int64_t* d_upper,
-                                                 int8_t* d_status, const int32_t* d_qlen, const int32_t* d_caps_len,
-                                                 const int32_t* d_a0_len, uint64_t* d_nodes, uint64_t workspace_bytes,
-                                                 sst_lbf_stats* stats) {
+static int lbf_frontier(sst_table* t, sst_ctx::LbfWs& W, const double* d_su, const double* d_obs,
+                        const int32_t* d_spec, const uint64_t* d_alpha, const uint8_t* d_lr, const uint64_t* d_lr_off,
+                        int64_t n, double tol, double prec, int max_len, int64_t max_mods, int64_t* d_lower,
+                        int64_t* d_upper, int8_t* d_status, const int32_t* d_qlen, const int32_t* d_caps_len,
+                        const int32_t* d_a0_len, uint64_t* d_nodes, uint64_t workspace_bytes, sst_lbf_stats* stats) {
   if (!t || n < 0 || n > INT32_MAX || max_len < 0 || (d_qlen && (!d_caps_len || !d_a0_len)) ||
       (n > 0 && (!d_su || !d_obs || !d_spec || !d_alpha || !d_lr || !d_lr_off || !d_lower || !d_upper || !d_status)))
     return SST_E_ARG;
@@ -3126,8 +3184,8 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
   // and a candidate entry (32 B: 128-bit keys), and the band's group record
   // (20 B) and candidate record (24 B); S slots, S a power of two (hashing)
   size_t budget = workspace_bytes;
-  if (budget == 0 && c->lbf.S && c->lbf.by_default) {
-    budget = c->lbf.budget;  // the default workspace of an earlier call
+  if (budget == 0 && W.S && W.by_default) {
+    budget = W.budget;  // the default workspace of an earlier call
   } else if (budget == 0) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
@@ -3139,7 +3197,6 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
   constexpr uint64_t kNodesPerSlot = 8;
   const size_t per_slot = kNodesPerSlot * 7 + 4 + (size_t)ring * (lbf_group_bytes() + 4 + lbf_cand_bytes(2)) +
                           lbf_grec_bytes() + lbf_crec_bytes(2);
-  auto& W = c->lbf;
   if (W.budget != budget) {  // (re)size the ctx's workspace: the first call, or another budget
     W = sst_ctx::LbfWs{};
     W.budget = budget;
@@ -3156,7 +3213,7 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
       !gtab.ensure((size_t)ring * S * lbf_group_bytes()) || !ctab.ensure((size_t)ring * S * lbf_cand_bytes(2)) ||
       !glist.ensure((size_t)ring * S * 4) || !ctl.ensure(sizeof(FCtl)) || !grec.ensure(S * lbf_grec_bytes()) ||
       !crec.ensure(S * lbf_crec_bytes(2)) || !ngrp.ensure(S * 4)) {
-    c->lbf = sst_ctx::LbfWs{};
+    W = sst_ctx::LbfWs{};
     return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier workspace)");
   }
   constexpr uint32_t kChunkMax = 1u << 20;  // the keys' query field
@@ -3336,6 +3393,18 @@ extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_s
   }
   HIP_OK(c, hipStreamSynchronize(c->stream));
   return SST_OK;
+}
+
+extern "C" int sst_length_bounds_frontier_device(sst_table* t, const double* d_su, const double* d_obs,
+                                                 const int32_t* d_spec, const uint64_t* d_alpha, const uint8_t* d_lr,
+                                                 const uint64_t* d_lr_off, int64_t n, double tol, double prec,
+                                                 int max_len, int64_t max_mods, int64_t* d_lower, int64_t* d_upper,
+                                                 int8_t* d_status, const int32_t* d_qlen, const int32_t* d_caps_len,
+                                                 const int32_t* d_a0_len, uint64_t* d_nodes, uint64_t workspace_bytes,
+                                                 sst_lbf_stats* stats) {
+  if (!t) return SST_E_ARG;
+  return lbf_frontier(t, t->ctx->lbf, d_su, d_obs, d_spec, d_alpha, d_lr, d_lr_off, n, tol, prec, max_len, max_mods,
+                      d_lower, d_upper, d_status, d_qlen, d_caps_len, d_a0_len, d_nodes, workspace_bytes, stats);
 }
 
 extern "C" int sst_jaccard_device(sst_table* t, const sst_jaccard_args* a) {

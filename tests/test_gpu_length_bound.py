@@ -53,10 +53,10 @@ def test_golden_length_bounds(engine, golden_cases):
         su = c.get("su_mass", ctx["su_mass"])
         obs = c.get("obs_mass", ctx["obs_mass"])
         A = round(ctx["mod_rate"] * ctx["max_len"])
-        for exact_only in (False, True):
+        for exact_only, replay in ((False, False), (True, False), (True, True)):
             got, st = dev.length_bound([su], [obs], ctx["tolerance"], ctx["precision"], ctx["max_len"], A, c["dir"],
-                                       exact_only=exact_only)
-            assert int(st[0]) == 0 and int(got[0]) == c["result"], (c, exact_only)
+                                       exact_only=exact_only, replay=replay)
+            assert int(st[0]) == 0 and int(got[0]) == c["result"], (c, exact_only, replay)
 
 
 def _alph(ms, max_len, rate=0.5):
@@ -74,12 +74,14 @@ def _check(engine, ms, max_len, su, obs, tol=1e-5):
     A = round(0.5 * max_len)
     for d in ("lower", "upper"):
         got, st = dev.length_bound(su, obs, tol, 1e-3, max_len, A, d)
-        got_x, st_x = dev.length_bound(su, obs, tol, 1e-3, max_len, A, d, exact_only=True)
-        assert (st == 0).all() and (st_x == 0).all()
+        got_x, st_x = dev.length_bound(su, obs, tol, 1e-3, max_len, A, d, exact_only=True)  # the frontier
+        got_r, st_r = dev.length_bound(su, obs, tol, 1e-3, max_len, A, d, exact_only=True, replay=True)
+        assert (st == 0).all() and (st_x == 0).all() and (st_r == 0).all()
         for i in range(len(su)):
             want = oracle.length_bound(host, 32, alph, su[i], obs[i], tol, max_len, A, d)
             assert int(got[i]) == want, (d, i, su[i], max_len)
-            assert int(got_x[i]) == want, ("exact", d, i, su[i], max_len)
+            assert int(got_x[i]) == want, ("frontier", d, i, su[i], max_len)
+            assert int(got_r[i]) == want, ("replay", d, i, su[i], max_len)
 
 
 @pytest.mark.parametrize("max_len", [8, 14, 20])
@@ -129,3 +131,27 @@ def test_full_alphabet_6mer_vs_oracle(engine, alphabet_rows):
     ms = alphabet_rows
     su = np.array([rng.choice(ms[1:], 6).sum() * 1e-3 for _ in range(2)])
     _check(engine, ms, 6, su, su)
+
+
+def test_last_word_windows_go_to_the_replay(engine):
+    """A window in the table's last packed word: the reference's last-column
+    mask (mass_table.py:246) may clear pair bits the closure has, so the
+    frontier reports SST_ABORTED there and the batch call answers those
+    windows by the replay (the table's real bits); equal to the oracle."""
+    ms = [0, 1100, 1500, 2200]
+    dev = dev_for(engine, ms)
+    host = _host(ms)
+    is_mod, caps = [False, False, True, True], [0, 20, 2, 1]
+    dev.set_budgets(is_mod, caps)
+    alph = oracle.Alphabet(ms, is_mod, caps)
+    limit = dev.n_cols * 32
+    su = np.array([(limit - 20) * 1e-3, (limit - 40) * 1e-3, (limit - 5) * 1e-3, 30.0, 21.5])
+    obs = np.full(len(su), 0.5)  # windows of +-5 masses
+    for d in ("lower", "upper"):
+        got, st = dev.length_bound(su, obs, 1e-5, 1e-3, 40, 3, d, exact_only=True)
+        for i in range(len(su)):
+            want = oracle.length_bound(host, 32, alph, su[i], obs[i], 1e-5, 40, 3, d)
+            if want is None:
+                assert int(st[i]) == _native.SST_OUT_OF_TABLE, (d, i)
+            else:
+                assert int(st[i]) == 0 and int(got[i]) == want, (d, i, int(st[i]), int(got[i]), want)
