@@ -20,10 +20,10 @@
 //                   last row), computed as a bitset closure in LDS, one
 //                   workgroup per spectrum.  Every row mass is >= w_min (C, a
 //                   canonical row, is never dropped), so bit m depends only on
-//                   bits m - w_r <= m - w_min: chunks of 2^18 masses (< w_min)
-//                   are filled in order, each word an OR of shifted words of
-//                   the three chunks before it (w_max < 3 * 2^18), in a ring of
-//                   four 32 KB chunks.  The spectrum's windows (in mass order)
+//                   bits m - w_r <= m - w_min: chunks of 8064 words (258048
+//                   masses < w_min) are filled in order, each word an OR of
+//                   shifted words of the ones before it (w_max < 3 * 2^18), in
+//                   a 128 KB ring of 2^15 words.  The spectrum's windows (in mass order)
 //                   are answered as soon as the chunk holding them is done; a
 //                   run of >= w_min reachable masses (the alphabet's lightest
 //                   row) ends the closure: every later mass m is reachable, as
@@ -40,13 +40,21 @@ namespace sst {
 
 namespace {
 
-constexpr int kChunkWords = 8192;                 // 32-bit words per chunk
-constexpr int64_t kChunkBits = kChunkWords * 32;  // 262144 masses
-constexpr int kRing = 4;                          // chunks kept in LDS (128 KB)
-constexpr int kRingMask = kRing * kChunkWords - 1;
+// A wave fills kParts runs of 63 consecutive words per chunk (lane 63 only
+// supplies its neighbour's word), one wave-segment of 504 words: a row's
+// scalar work (its mass, ring offset and shift) serves the wave's whole
+// segment, and a chunk is one segment per wave.
 constexpr int kValidWG = 1024;
 constexpr int kValidWaves = kValidWG / 64;
-constexpr int kPasses = (kChunkWords + 63 * kValidWaves - 1) / (63 * kValidWaves);  // 9: a wave's passes per chunk
+constexpr int kParts = 8;
+constexpr int kSegWords = 63 * kParts;                  // 504
+constexpr int kChunkWords = kSegWords * kValidWaves;    // 8064 words per chunk
+constexpr int64_t kChunkBits = kChunkWords * 32;        // 258048 masses (< w_min)
+constexpr int kRingWords = 32768;                       // a chunk + the w_max / 32 words before it
+constexpr int kRingMask = kRingWords - 1;
+constexpr int kRingPad = 512;                           // the ring's first words again: reads past the end
+static_assert(kChunkWords + 3 * 262144 / 32 + 2 <= kRingWords, "ring too small");
+static_assert(kSegWords + 1 <= kRingPad, "ring pad too small");
 
 __device__ __forceinline__ bool row_in(uint64_t m0, uint64_t m1, int r) {
   return r < 64 ? ((m0 >> r) & 1ull) : ((m1 >> (r - 64)) & 1ull);
@@ -93,7 +101,7 @@ __device__ __forceinline__ void alpha_put(const AlphaArgs& a, int64_t i, int8_t 
 }
 
 __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
-  __shared__ uint32_t ring[kRing * kChunkWords + 64];  // + slot 0's first 64 words again (reads past the end)
+  __shared__ uint32_t ring[kRingWords + kRingPad];  // word i of the closure at i & kRingMask
   __shared__ int s_w[kMaxRows];
   __shared__ int s_n;
   __shared__ int64_t s_done;   // queries [q0, s_done) answered
@@ -140,8 +148,8 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
     for (int64_t i = q0 + threadIdx.x; i < q1; i += blockDim.x) alpha_put(a, i, 0);
     return;
   }
-  // chunks below mass 0 read as empty: zero the ring (slots are reused across spectra)
-  for (int i = threadIdx.x; i < kRing * kChunkWords + 64; i += blockDim.x) ring[i] = 0u;
+  // words below mass 0 read as empty: zero the ring (slots are reused across spectra)
+  for (int i = threadIdx.x; i < kRingWords + kRingPad; i += blockDim.x) ring[i] = 0u;
   // the row masses, lane r of every wave holding rows r and r + 64
   const int w_lo = (int)(threadIdx.x & 63) < n_w ? s_w[threadIdx.x & 63] : 0;
   const int w_hi = (int)(threadIdx.x & 63) + 64 < n_w ? s_w[(threadIdx.x & 63) + 64] : 0;
@@ -150,7 +158,7 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
     wmax = s_w[k] > wmax ? s_w[k] : wmax;
     wmin = s_w[k] < wmin ? s_w[k] : wmin;
   }
-  if (n_w == 0) wmin = wmax = kChunkBits;  // the canonical closure alone
+  if (n_w == 0) wmin = wmax = (int)kChunkBits + 1;  // the canonical closure alone
   // the reduced table (set_up_bit_table with max_mass = max(kept) * 35):
   // masses < limit exist, the last-column mask leaves masses <= vtop reachable
   const int64_t max_mass = (int64_t)s_wmax_all * 35;
@@ -171,84 +179,95 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
   __syncthreads();
   top = s_top < limit - 1 ? s_top : limit - 1;
   const int64_t n_chunks = top / kChunkBits + 1;
-  const bool guard_ok = wmin >= kChunkBits && wmax < 3 * kChunkBits;  // the ring's dependency window
-  // Each wave writes 63 consecutive words per pass: a row's shifted word
-  // for output word o needs ring words wi and wi + 1, and wi + 1 is the next
-  // lane's wi (a DPP lane shift), so the 64 lanes read 64 words and the
-  // last lane only supplies its neighbour.  The shift is wave-uniform.
+  // a chunk's words depend only on words before it (every row is heavier than
+  // a chunk), and on none more than 3 * 2^18 masses back (the ring holds them)
+  const bool guard_ok = wmin > kChunkBits && wmax < 3 * 262144;
+  // A row's shifted word for output word o needs ring words wi and wi + 1,
+  // and wi + 1 is the next lane's wi (a DPP lane shift): each of the wave's
+  // kParts runs reads 64 words and writes 63.  The shift is wave-uniform.
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // the canonical closure's words of a chunk, per lane and pass, loaded a
+  const int seg0 = wv * kSegWords;  // the wave's first word in a chunk
+  // the canonical closure's words of a chunk, per lane and part, loaded a
   // chunk ahead: one L2 latency per chunk, hidden behind the chunk before
-  // (read pass by pass they cost one exposed latency per pass)
-  uint32_t cwv[kPasses];
+  uint32_t cwv[kParts];
   auto load_canon = [&](int64_t jj, uint32_t* dst) {
 #pragma unroll
-    for (int p = 0; p < kPasses; ++p) {
-      const int o = 63 * wv + p * 63 * kValidWaves + lane;
-      const int64_t cw = jj * kChunkWords + o;
-      dst[p] = use_c && o < kChunkWords && cw < a.canon_words ? a.canon_closure[cw] : 0u;
+    for (int k = 0; k < kParts; ++k) {
+      const int64_t cw = jj * kChunkWords + seg0 + 63 * k + lane;
+      dst[k] = use_c && lane < 63 && cw < a.canon_words ? a.canon_closure[cw] : 0u;
     }
   };
   load_canon(0, cwv);
   for (int64_t j = 0; j < n_chunks && guard_ok; ++j) {
-    uint32_t* cur = ring + (j & (kRing - 1)) * kChunkWords;
-    const int64_t base = j * kChunkBits;
+    const int64_t cs = j * kChunkWords;  // the chunk's first word
+    const int64_t base = cs * 32;
     int zmax = -1;  // this lane's highest unreachable mass in the chunk
-    uint32_t nxt[kPasses];
+    uint32_t nxt[kParts];
     if (j + 1 < n_chunks && !s_full) {
       load_canon(j + 1, nxt);
     } else {
 #pragma unroll
-      for (int p = 0; p < kPasses; ++p) nxt[p] = 0u;
+      for (int k = 0; k < kParts; ++k) nxt[k] = 0u;
     }
+    uint32_t v[kParts];
+    if (!s_full) {
 #pragma unroll
-    for (int p = 0; p < kPasses; ++p) {
-      const int o0 = 63 * wv + p * 63 * kValidWaves;
-      if (o0 >= kChunkWords) break;
-      const int o = o0 + lane;
-      uint32_t v = 0;
-      if (!s_full) {
-        if (use_c) {  // includes mass 0; masses past the full table (>= every reduced table's end): none
-          v = cwv[p];
-        } else if (j == 0 && o == 0) {
-          v = 1u;  // mass 0: the empty multiset (table[0, 0] seed)
-        }
-        // the wave's first output mass (masses < limit < 2^31), wave-uniform: the
-        // shifts and ring offsets below are scalar arithmetic
-        const int m0 = (int)base + 32 * __builtin_amdgcn_readfirstlane(o0);
-        // two rows per step: their LDS reads are in flight together (a tail
-        // repeats the last row: the same bits again; 4 and 8 rows per step
-        // measured 1.6 % and 8 % slower)
-        for (int r = 0; r < n_w; r += 2) {
-          // the rows' masses from the lanes that hold the list (no LDS round trip)
+      for (int k = 0; k < kParts; ++k) v[k] = cwv[k];  // includes mass 0 (use_c); past the full table: none
+      if (!use_c && j == 0 && wv == 0 && lane == 0) v[0] = 1u;  // mass 0: the empty multiset (table[0, 0] seed)
+      // the wave's first output mass (masses < limit < 2^31), wave-uniform:
+      // the shifts and ring offsets below are scalar arithmetic
+      const int mw = __builtin_amdgcn_readfirstlane((int)(32 * (cs + seg0)));
+      // rows [r0, r1), lane r - r0 holding row r's mass (read by readlane: no
+      // LDS round trip); two rows per step, their LDS reads in flight together
+      // (a tail repeats the last row: the same bits again)
+      auto add_rows = [&](int wsrc, int r0, int r1) {
+        for (int r = r0; r < r1; r += 2) {
           int x[2];
 #pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const int rk = r + k < n_w ? r + k : n_w - 1;
-            x[k] = m0 - __builtin_amdgcn_readlane(rk < 64 ? w_lo : w_hi, rk & 63);
+          for (int kk = 0; kk < 2; ++kk) {
+            const int rk = r + kk < r1 ? r + kk : r1 - 1;
+            x[kk] = mw - __builtin_amdgcn_readlane(wsrc, rk - r0);
           }
           // ring words from the wave's first shifted word (negative masses: the
-          // zeroed slots of chunks not yet filled; past the end: the copy of slot 0)
-          uint32_t lo[2];
+          // zeroed slots not yet filled; past the end: the pad copy of the start)
+          uint32_t lo[2][kParts];
 #pragma unroll
-          for (int k = 0; k < 2; ++k) lo[k] = ring[((x[k] >> 5) & kRingMask) + lane];
+          for (int kk = 0; kk < 2; ++kk) {
+            const uint32_t* src = ring + ((x[kk] >> 5) & kRingMask) + lane;
 #pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const uint32_t nx = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo[k], 0x130, 0xF, 0xF, false);  // wave_shl:1
-            v |= __builtin_amdgcn_alignbit(nx, lo[k], (uint32_t)x[k] & 31u);  // ({nx, lo} >> shift) low word
+            for (int k = 0; k < kParts; ++k) lo[kk][k] = src[63 * k];
+          }
+#pragma unroll
+          for (int k = 0; k < kParts; ++k) {
+            uint32_t t[2];
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+              // the next lane's word (wave_shl:1; lane 63's result is unused)
+              const uint32_t nx = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo[kk][k], 0x130, 0xF, 0xF, true);
+              t[kk] = __builtin_amdgcn_alignbit(nx, lo[kk][k], (uint32_t)x[kk] & 31u);  // ({nx, lo} >> shift) low word
+            }
+            v[k] |= t[0] | t[1];
           }
         }
-      } else {
-        v = ~0u;
-      }
-      if (lane < 63 && o < kChunkWords) {
-        cur[o] = v;
-        if ((j & (kRing - 1)) == 0 && o < 64) ring[kRing * kChunkWords + o] = v;
-        if (v != ~0u) zmax = 32 * o + 31 - __builtin_clz(~v);  // o ascends: the lane's last one is its highest
+      };
+      add_rows(w_lo, 0, n_w < 64 ? n_w : 64);
+      if (n_w > 64) add_rows(w_hi, 64, n_w);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kParts; ++k) v[k] = ~0u;
+    }
+    if (lane < 63) {
+#pragma unroll
+      for (int k = 0; k < kParts; ++k) {
+        const int o = seg0 + 63 * k + lane;  // chunk-relative; o ascends with k
+        const int ri = (int)((cs + o) & kRingMask);
+        ring[ri] = v[k];
+        if (ri < kRingPad) ring[ri + kRingWords] = v[k];
+        if (v[k] != ~0u) zmax = 32 * o + 31 - __builtin_clz(~v[k]);
       }
     }
 #pragma unroll
-    for (int p = 0; p < kPasses; ++p) cwv[p] = nxt[p];
+    for (int k = 0; k < kParts; ++k) cwv[k] = nxt[k];
     for (int off = 32; off > 0; off >>= 1) {  // the wave's highest, then one atomic per wave
       const int z2 = __shfl_xor(zmax, off, 64);
       zmax = zmax > z2 ? zmax : z2;
@@ -283,7 +302,7 @@ __global__ __launch_bounds__(kValidWG) void k_valid_alpha(AlphaArgs a) {
           const int64_t x0 = lo < 1 ? 1 : lo;
           const int64_t x1 = hi < vtop ? hi : vtop;
           bool any = false;
-          if (x0 <= x1 && x0 < base - 3 * kChunkBits) {
+          if (x0 <= x1 && (x0 >> 5) < cs + kChunkWords - kRingWords) {
             res = (int8_t)kStatusPending;  // below the ring (rows not in mass order): reported, not guessed
           } else {
             if (x0 <= x1) any = ring_any(ring, x0, x1);

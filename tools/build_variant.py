@@ -27,7 +27,7 @@ os.makedirs(os.path.dirname(out), exist_ok=True)
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
                 "-fno-fast-math", "-DSST_DIAG", "-I" + os.path.join(REPO, "include"), "-I" + src, "-shared", "-o", out,
                 *[os.path.join(src, f) for f in ("sst_kernels.hip", "sst_alpha.hip", "sst_rows.hip", "sst_pipe.hip",
-                                                  "sst_skel.hip", "sst_reach.hip", "sst_api.cpp")]],
+                                                  "sst_skel.hip", "sst_reach.hip", "sst_frontier.hip", "sst_api.cpp")]],
                check=True)
 shutil.rmtree(tmp)
 print(out)
