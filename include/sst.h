@@ -185,6 +185,22 @@ int sst_explain_alpha_batch_device(sst_table* t, const double* d_mass, const dou
                                    const int64_t* d_max_mods, int64_t max_mods_scalar, int with_memo,
                                    uint64_t cap_per_query, sst_result** out);
 
+/* sst_explain_alpha_batch_device with per-query budgets: query i's row caps
+ * are row d_qlen[i] of caps_by_len (host, [n_lens][n_rows]: the caps
+ * sst_table_set_budgets would set for that length, round(L * rate)), its
+ * max_modifications d_mods[i]; the table's is_modification flags (set by
+ * sst_table_set_budgets) are kept.  Every query is answered as one
+ * sst_explain_alpha_batch_device call with those budgets set would answer it
+ * (the exact memo path: with_memo = 1), so windows of many max_len values
+ * go in one pass instead of one pass per value (skeleton_building.py:212 ->
+ * :436 per spectrum, each spectrum's SequenceInformation.max_len).  Results,
+ * reuse and settling as for sst_explain_batch_device; d_qlen / d_mods must
+ * stay valid until the pass is settled. */
+int sst_explain_alpha_lens_batch_device(sst_table* t, const double* d_mass, const double* d_thr, const int32_t* d_spec,
+                                        const uint64_t* d_alpha, const int32_t* d_qlen, const int64_t* caps_by_len,
+                                        int n_lens, int64_t n, double tolerance, double precision,
+                                        const int64_t* d_mods, uint64_t cap_per_query, sst_result** out);
+
 /* One step of both predicates on device buffers, as classify_fragments and
  * the explanation stage issue them: sst_is_valid_peaks_device(d_obs, n_peaks,
  * shifts, n_shifts -> d_valid_out) and sst_explain_batch_device(d_mass, ...,
@@ -586,7 +602,9 @@ int sst_sort_rows(const int64_t* group, const double* key, int64_t n, int64_t n_
  * their answers are missing -- the side is then SST_WALK_SUSPENDED, and the
  * caller answers req_* (sst_explain_alpha_batch_device), adds them as round
  * n_rounds (rq_*: per side its block start << 32 | count in the round's
- * lists) and walks the suspended sides again (they replay from the start).
+ * lists) and walks the suspended sides again: with resume set and the same
+ * scratch slots, each resumes at the bin that suspended it (its loop state
+ * is kept at the head of its slot), otherwise it replays from the start.
  * SST_WALK_BIG: a bin outgrew the lane's scratch capacities (walk that side
  * again with larger ones).  All pointers are device pointers. */
 #define SST_WALK_MAX_ROUNDS 16
@@ -633,7 +651,7 @@ typedef struct sst_walk_args {
   const int64_t* name_hash;  /* [n_rows] hash() of each row's nucleoside name */
   const uint32_t* sides;     /* side ids 2 g + (0 START, 1 END) to walk */
   uint32_t n_sides;
-  uint8_t* scratch;          /* n_sides * scratch_stride bytes (sst_walk_scratch_bytes) */
+  uint8_t* scratch;          /* scratch_stride bytes per slot (sst_walk_scratch_bytes) */
   uint64_t scratch_stride;
   uint32_t pos_cap, len_cap, expl_cap, cand_cap, tset_cap;
   uint16_t* side_rows;       /* [2 slots] */
@@ -645,6 +663,9 @@ typedef struct sst_walk_args {
   uint8_t* side_status;      /* [2 n_spec] SST_WALK_* */
   uint32_t* n_suspended;
   uint32_t* n_big;
+  const uint32_t* slot;      /* [n_sides] each walked side's scratch slot (NULL: its index in sides) */
+  int resume;                /* a side whose slot holds its suspended state resumes there (else it
+                                walks from the start; slots of a first launch hold no state) */
 } sst_walk_args;
 /* Scratch bytes per walked side for the given capacities (pos_cap, tset_cap:
  * powers of two >= the set tables the positions / a query's candidates need,

@@ -23,7 +23,7 @@ EXPORTS = (
     "sst_device_count", "sst_ctx_create", "sst_ctx_destroy", "sst_last_error", "sst_ctx_stream",
     "sst_ctx_synchronize", "sst_table_build", "sst_table_upload", "sst_table_set_budgets", "sst_table_shape",
     "sst_table_download", "sst_table_destroy", "sst_is_valid_batch", "sst_is_valid_batch_device",
-    "sst_explain_batch", "sst_explain_batch_device", "sst_explain_alpha_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
+    "sst_explain_batch", "sst_explain_batch_device", "sst_explain_alpha_batch_device", "sst_explain_alpha_lens_batch_device", "sst_result_host", "sst_result_device", "sst_result_fetch",
     "sst_result_free", "sst_result_stats", "sst_profile_enable", "sst_profile_select",
     "sst_profile_sample", "sst_profile_read", "sst_length_bound_batch", "sst_explain_recursion_batch", "sst_is_singleton_batch",
     "sst_is_singleton_batch_device", "sst_ctx_set_stream", "sst_result_hit_list", "sst_result_settle",
@@ -133,7 +133,8 @@ class WalkArgs(ctypes.Structure):
                 ("expl_cap", ctypes.c_uint32), ("cand_cap", ctypes.c_uint32), ("tset_cap", ctypes.c_uint32),
                 ("side_rows", ctypes.c_void_p), ("skel_off", ctypes.c_void_p), ("skel", ctypes.c_void_p),
                 ("min_end", ctypes.c_void_p), ("max_end", ctypes.c_void_p), ("kept", ctypes.c_void_p),
-                ("side_status", ctypes.c_void_p), ("n_suspended", ctypes.c_void_p), ("n_big", ctypes.c_void_p)]
+                ("side_status", ctypes.c_void_p), ("n_suspended", ctypes.c_void_p), ("n_big", ctypes.c_void_p),
+                ("slot", ctypes.c_void_p), ("resume", ctypes.c_int)]
 
 
 def _share_hip_runtime_with_torch():
@@ -186,6 +187,7 @@ def load_library(path=LIB_PATH):
     lib.sst_explain_batch.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
     lib.sst_explain_batch_device.argtypes = [_P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
     lib.sst_explain_alpha_batch_device.argtypes = [_P, _P, _P, _P, _P, _I64, _D, _D, _P, _I64, _I, _U64, _PP]
+    lib.sst_explain_alpha_lens_batch_device.argtypes = [_P, _P, _P, _P, _P, _P, _P, _I, _I64, _D, _D, _P, _U64, _PP]
     lib.sst_result_host.argtypes = [_P, _PP, _PP, _PP, _PP, ctypes.POINTER(_U64)]
     lib.sst_result_device.argtypes = [_P, _PP, _PP, _PP, _PP, ctypes.POINTER(_U64)]
     lib.sst_result_hit_list.argtypes = [_P, _PP, ctypes.POINTER(_U64)]
@@ -846,6 +848,19 @@ class DeviceTable:
             return reuse
         return ExplainResult(self.engine, h, n)
 
+    def explain_alpha_lens_device(self, d_mass, d_thr, d_spec, d_alpha, d_qlen, caps_by_len, n, tolerance,
+                                  precision, d_mods, cap=2 ** 32):
+        """sst_explain_alpha_lens_batch_device: explain_alpha_device with
+        per-query budgets -- query i's row caps caps_by_len[d_qlen[i]] (host
+        [n_lens, n_rows] ints), its max_modifications d_mods[i]."""
+        caps = np.ascontiguousarray(caps_by_len, dtype=np.int64)
+        h = ctypes.c_void_p(None)
+        self.engine.check(self.engine._lib.sst_explain_alpha_lens_batch_device(
+            self.handle, d_mass, d_thr, d_spec, d_alpha, d_qlen, caps.ctypes.data, int(caps.shape[0]), int(n),
+            float(tolerance), float(precision), d_mods, int(cap), ctypes.byref(h)),
+            "sst_explain_alpha_lens_batch_device")
+        return ExplainResult(self.engine, h, n)
+
     def explain_alpha(self, masses, thresholds, spec, alpha, tolerance, precision, max_mods, with_memo=True,
                       cap=2 ** 32):
         """Host-buffer form of explain_alpha_device (tests, small batches):
@@ -865,6 +880,27 @@ class DeviceTable:
                                         precision, 0, d_mods=dmods.data_ptr(), with_memo=with_memo, cap=cap)
         res.fetch_device()
         del dm, dt, ds, da, dmods
+        return res
+
+    def explain_alpha_lens(self, masses, thresholds, spec, alpha, qlen, caps_by_len, max_mods, tolerance, precision):
+        """Host-buffer form of explain_alpha_lens_device (tests): query i with
+        row caps caps_by_len[qlen[i]] and max_mods[i]; settles and fetches."""
+        import torch
+
+        dev = torch.device("cuda", self.engine.device)
+        n = len(masses)
+        dm = torch.as_tensor(np.ascontiguousarray(masses, dtype=np.float64), device=dev)
+        dt = torch.as_tensor(np.ascontiguousarray(thresholds, dtype=np.float64), device=dev)
+        ds = torch.as_tensor(np.ascontiguousarray(spec, dtype=np.int32), device=dev)
+        da = torch.as_tensor(np.ascontiguousarray(alpha, dtype=np.uint64).view(np.int64), device=dev)
+        dq = torch.as_tensor(np.ascontiguousarray(qlen, dtype=np.int32), device=dev)
+        dmods = torch.as_tensor(np.ascontiguousarray(np.broadcast_to(np.asarray(max_mods, np.int64), (n,))),
+                                device=dev)
+        torch.cuda.synchronize(dev)
+        res = self.explain_alpha_lens_device(dm.data_ptr(), dt.data_ptr(), ds.data_ptr(), da.data_ptr(),
+                                             dq.data_ptr(), caps_by_len, n, tolerance, precision, dmods.data_ptr())
+        res.fetch_device()
+        del dm, dt, ds, da, dq, dmods
         return res
 
     def step_rows_device(self, d_obs, d_peak_off, n_spec, n_peaks, d_su_seq, shifts, sides, d_valid_out, max_weight,

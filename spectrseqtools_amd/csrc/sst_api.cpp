@@ -137,6 +137,15 @@ struct sst_table {
   TableArgs args{};
 };
 
+// per-query budgets of an explain pass (QueryArgs::qlen ...): query i's caps
+// row qlen[i] of the tables
+struct LenBudgets {
+  const int32_t* qlen = nullptr;
+  const int32_t* caps = nullptr;
+  const uint64_t* capz = nullptr;
+  const uint32_t* never = nullptr;
+};
+
 struct sst_result {
   sst_ctx* ctx = nullptr;
   int64_t n = 0;
@@ -148,6 +157,7 @@ struct sst_result {
   // blocks, class lists, scan worklists / hit records, tallies, deferred hits
   DevBuf payload, ctl, lists, wave_stats, work, work_count, tally, wg_tally, dhits, hdr, agg, refs, stage;
   DevBuf count, offset;  // per-query arrays: only built for sst_result_device callers that ask for them
+  DevBuf lb_caps, lb_capz, lb_never;  // per-query budgets' tables (sst_explain_alpha_lens_batch_device)
   uint64_t* hdr_host = nullptr;  // host-mapped copy of the pack kernel's header (host address)
   uint64_t* hdr_host_dev = nullptr;  // its device address
   // control block (spill cursor, class counters, stats) of the current pass;
@@ -177,6 +187,7 @@ struct sst_result {
     uint64_t cap;
     const uint64_t* alpha;  // per-query alphabets (sst_explain_alpha_batch_device) or null
     const int32_t* spec;
+    LenBudgets lb;          // per-query budgets or none
   } pass{};
   uint64_t arena_bytes = 0;
   uint64_t n_hits = 0, payload_bytes = 0;
@@ -821,7 +832,8 @@ constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses pe
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->hits, &r->dense, &r->payload, &r->ctl, &r->lists, &r->wave_stats, &r->work,
                     &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->refs, &r->stage, &r->count,
-                    &r->offset, &r->rows_su, &r->rows_ob, &r->rows_side, &r->rows_tot, &r->rows_chunk, &r->rows_ctl, &r->rows_big, &r->rows_ans, &r->rows_aq})
+                    &r->offset, &r->rows_su, &r->rows_ob, &r->rows_side, &r->rows_tot, &r->rows_chunk, &r->rows_ctl, &r->rows_big, &r->rows_ans, &r->rows_aq,
+                    &r->lb_caps, &r->lb_capz, &r->lb_never})
     b->release();
   if (r->hdr_host) (void)hipHostFree(r->hdr_host);
   r->hdr_host = nullptr;
@@ -936,6 +948,10 @@ int launch_tail(sst_table* t, sst_result* r) {
   q.alpha = ps.alpha;
   q.spec = ps.spec;
   q.comp = (int)t->C;
+  q.qlen = ps.lb.qlen;
+  q.caps_len = ps.lb.caps;
+  q.capz_len = ps.lb.capz;
+  q.never_len = ps.lb.never;
   OutArgs o = out_args(r);
 #ifdef SST_DIAG  // diagnostic builds only (make DIAG=1): roles switched off, results invalid
   {
@@ -1011,9 +1027,11 @@ struct PeaksJob {
 
 int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double* d_thr, const int64_t* d_mods,
                  int64_t mods_scalar, double tol, double prec, int with_memo, uint64_t cap_count, bool eager_tail,
-                 const PeaksJob* peaks = nullptr, const uint64_t* d_alpha = nullptr, const int32_t* d_spec = nullptr) {
+                 const PeaksJob* peaks = nullptr, const uint64_t* d_alpha = nullptr, const int32_t* d_spec = nullptr,
+                 const LenBudgets* lens = nullptr) {
   sst_ctx* c = t->ctx;
-  r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count, d_alpha, d_spec};
+  const LenBudgets lb = lens ? *lens : LenBudgets{};
+  r->pass = {t, d_mass, d_thr, d_mods, mods_scalar, tol, prec, with_memo, cap_count, d_alpha, d_spec, lb};
   r->pass_stream = c->stream;
   r->settle_ev_pending = false;
   r->rows_pass = false;
@@ -1071,6 +1089,10 @@ int explain_pass(sst_table* t, sst_result* r, const double* d_mass, const double
   q.alpha = d_alpha;
   q.spec = d_spec;
   q.comp = (int)t->C;
+  q.qlen = lb.qlen;
+  q.caps_len = lb.caps;
+  q.capz_len = lb.capz;
+  q.never_len = lb.never;
   OutArgs o = out_args(r);
   // the pair scan packs its own result (and writes the header) when no
   // deferred-class launch follows it in this pass
@@ -1251,9 +1273,9 @@ int settle(sst_result* r) {
     if (attempt == 6) return fail(c, SST_E_INTERNAL, "explain: retries exhausted");
     HIP_OK(c, hipStreamSynchronize(c->stream));  // the pack may still run: buffers are about to be replaced
     if (int rc = grow_for_retry(r, regions, spill, exact, h[kHdrCursor], h[kHdrRegionNeed])) return rc;
-    const auto& p = r->pass;
+    const auto p = r->pass;  // a copy: the pass rewrites it
     if (int rc = explain_pass(p.t, r, p.mass, p.thr, p.mods, p.mods_scalar, p.tol, p.prec, p.with_memo, p.cap, true,
-                              nullptr, p.alpha, p.spec))
+                              nullptr, p.alpha, p.spec, &p.lb))
       return rc;
     launched = true;
   }
@@ -1381,6 +1403,71 @@ int sst_explain_alpha_batch_device(sst_table* t, const double* d_mass, const dou
     }
     return rc;
   }
+  *out = r;
+  return SST_OK;
+}
+
+int sst_explain_alpha_lens_batch_device(sst_table* t, const double* d_mass, const double* d_thr, const int32_t* d_spec,
+                                        const uint64_t* d_alpha, const int32_t* d_qlen, const int64_t* caps_by_len,
+                                        int n_lens, int64_t n, double tol, double prec, const int64_t* d_mods,
+                                        uint64_t cap_count, sst_result** out) {
+  if (!t || !out || n < 0 || n > SST_MAX_EXPLAIN_BATCH || n_lens < 1 || n_lens > 4096 || !caps_by_len ||
+      (n > 0 && (!d_mass || !d_alpha || !d_qlen || !d_mods)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  const int N = t->n_rows;
+  if ((int)t->is_mod.size() != N) return fail(c, SST_E_ARG, "explain (per-query budgets): the table has no budgets set");
+  // per length: the caps (clamped as sst_table_set_budgets), the rows with
+  // cap <= 0 and the fast-path limit (no per-row cap can bind below it)
+  std::vector<int32_t> caps((size_t)n_lens * kMaxRows, 0);
+  std::vector<uint64_t> capz(2 * (size_t)n_lens, 0);
+  std::vector<uint32_t> never(n_lens);
+  const int64_t u32max = (int64_t)UINT32_MAX;
+  for (int L = 0; L < n_lens; ++L) {
+    int64_t lim = INT64_MAX;
+    bool any_mod = false;
+    for (int r = 0; r < N; ++r) {
+      const int64_t cp = caps_by_len[(int64_t)L * N + r];
+      caps[(size_t)L * kMaxRows + r] = (int32_t)std::max<int64_t>(std::min<int64_t>(cp, kInfBudget), -1);
+      if (cp <= 0) capz[2 * L + (r >> 6)] |= 1ull << (r & 63);
+      if (t->is_mod[r]) {
+        any_mod = true;
+        const int64_t w = t->masses[r], cpp = std::max<int64_t>(cp, 0);
+        const int64_t l = (w <= 0) ? (cpp > 0 ? INT64_MAX : -1)
+                                   : (cpp + 1 > INT64_MAX / std::max<int64_t>(w, 1) ? INT64_MAX : (cpp + 1) * w - 1);
+        lim = std::min(lim, l);
+      }
+    }
+    never[L] = (uint32_t)(!any_mod ? u32max : (lim < 0 ? 0 : std::min(lim, u32max - 1) + 1));
+  }
+  sst_result* r = *out;
+  const bool reuse = r != nullptr;
+  if (reuse) {
+    if (r->ctx != c || n > r->cap_n) return fail(c, SST_E_ARG, "result reuse: other ctx or capacity < n");
+    r->n = n;
+  } else if (int rc = alloc_result(t, n, &r)) {
+    return rc;
+  }
+  auto drop = [&](int rc) {
+    if (!reuse) {
+      free_result_bufs(r);
+      delete r;
+    }
+    return rc;
+  };
+  // the result's own copies (a retry of the pass reads them again); a reused
+  // result's previous pass is settled by its consumer before it is reused
+  if (!r->lb_caps.ensure(caps.size() * 4) || !r->lb_capz.ensure(capz.size() * 8) || !r->lb_never.ensure(never.size() * 4))
+    return drop(fail(c, SST_E_NOMEM, "device allocation failed (result)"));
+  if (hipMemcpy(r->lb_caps.p, caps.data(), caps.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(r->lb_capz.p, capz.data(), capz.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(r->lb_never.p, never.data(), never.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+    return drop(fail(c, SST_E_HIP, "hipMemcpy (per-query budgets)"));
+  LenBudgets lb{d_qlen, (const int32_t*)r->lb_caps.p, (const uint64_t*)r->lb_capz.p, (const uint32_t*)r->lb_never.p};
+  int rc = explain_pass(t, r, d_mass, d_thr, d_mods, 0, tol, prec, 1, cap_count, false, nullptr, d_alpha, d_spec, &lb);
+  if (rc) return drop(rc);
   *out = r;
   return SST_OK;
 }

@@ -112,6 +112,15 @@ struct QueryArgs {
   const uint64_t* alpha = nullptr;
   const int32_t* spec = nullptr;
   int comp = 32;  // the table's compression (masses per packed word)
+  // per-query budgets (sst_explain_alpha_lens_batch_device; null: the
+  // table's caps for every query): query i's row caps caps_len[qlen[i] *
+  // kMaxRows + r], the rows with cap <= 0 capz_len[2 qlen[i]], [+ 1], and its
+  // fast-path limit never_len[qlen[i]] (never_lim for those caps); its
+  // max_modifications come in max_mods[i]
+  const int32_t* qlen = nullptr;
+  const int32_t* caps_len = nullptr;
+  const uint64_t* capz_len = nullptr;
+  const uint32_t* never_len = nullptr;
 };
 
 // Arena layout of one explain pass:

@@ -623,6 +623,10 @@ struct Hash {
   int dflt_lo = 0;
   bool vals_bad = false;  // fused values: a visited child had no memo entry (reported as SST_ABORTED)
   bool dense = false;  // fused values: entry i's values at slot pad (its insertion order) x kValSlots + kept rank
+  // the query's row caps and the rows with cap <= 0 (the table's in LDS, or
+  // the query's own: per-query budgets), set by the caller before phase 1
+  const int* cap = nullptr;
+  uint64_t capz0 = 0, capz1 = 0;
   __device__ __forceinline__ uint32_t slot(uint32_t m) const { return (m * 0x9E3779B1u) & mask; }
   // returns entry pointer or nullptr if absent
   __device__ __forceinline__ HEntry* find(uint32_t m) const {
@@ -1028,7 +1032,7 @@ __device__ __forceinline__ int p1_visit(const TableArgs& t, const Lds& s, Hash& 
   M128 en = mand(rec_L(rec), rng);
   if (t.any_mod) {
     M128 blocked;
-    if (A > 0) blocked = M128{t.mod0 & s.capz0, t.mod1 & s.capz1};
+    if (A > 0) blocked = M128{t.mod0 & h.capz0, t.mod1 & h.capz1};
     else blocked = M128{t.mod0, t.mod1};
     en.a &= ~blocked.a;
     en.b &= ~blocked.b;
@@ -1102,11 +1106,11 @@ __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* f
     bool ne_dummy;
     M128 rest;
     HEntry* e;
-    int pr = p1_visit<WAVE>(t, s, h, (uint32_t)v, top, A0, s.cap[top], ne_dummy, nodes, rest, e, am);
+    int pr = p1_visit<WAVE>(t, s, h, (uint32_t)v, top, A0, h.cap[top], ne_dummy, nodes, rest, e, am);
     if (pr < 0) return -1;
     if (pr == 0) continue;
     uint32_t m = (uint32_t)v;
-    int A = A0, B = s.cap[top], rtop = top, d = 0;
+    int A = A0, B = h.cap[top], rtop = top, d = 0;
     for (;;) {
       if (mzero(rest)) {  // frame done: report to the parent (its pending row)
         if (d == 0) break;
@@ -1126,7 +1130,7 @@ __device__ int phase1_body(const TableArgs& t, const Lds& s, Hash& h, P1Frame* f
       const int rr = mlow(rest);
       rest = mclear(rest, rr);
       const int md = s.mod[rr];
-      const int Bv = (rr == rtop) ? B : s.cap[rr];
+      const int Bv = (rr == rtop) ? B : h.cap[rr];
       const int64_t child = (int64_t)m - s.w[rr];
       bool nonempty = false;
       if (child == 0) {
@@ -1840,7 +1844,9 @@ __device__ __forceinline__ void explain_scan_wg(const TableArgs& t, const QueryA
       const bool a0ok =
           !t.any_mod || A0 >= kInfBudget || (uint64_t)hi < (uint64_t)(A0 + 1) * (uint64_t)t.w_min_mod;
       pair = active && a0ok && hi < t.pair_lim;
-      never = a0ok && hi < t.never_lim;
+      // per-query budgets: the fast-path limit of the query's caps
+      const uint32_t nl = q.qlen ? q.never_len[q.qlen[live ? i : n - 1]] : t.never_lim;
+      never = a0ok && hi < nl;
     } else {
       pair = active && hi < q.pair_hi_lim;
       never = hi < q.never_hi_lim;
@@ -2152,7 +2158,8 @@ __global__ __launch_bounds__(kScanWG, 8) void k_bitset_scan(TableArgs t, QueryAr
     const uint32_t a = active ? (uint32_t)af : 0u, hi = active ? (uint32_t)hif : 0u;
     const int A0 = clamp_budget(mm);
     const bool a0ok = !t.any_mod || A0 >= kInfBudget || (uint64_t)hi < (uint64_t)(A0 + 1) * (uint64_t)t.w_min_mod;
-    const bool never = hi < t.never_lim && a0ok;
+    const uint32_t nl = q.qlen && live ? q.never_len[q.qlen[i]] : t.never_lim;  // per-query budgets
+    const bool never = hi < nl && a0ok;
     int8_t status = oot ? (int8_t)SST_OUT_OF_TABLE : (zero ? (int8_t)SST_EMPTY : (int8_t)SST_NONE);
     bool work = false;
     uint4 item = make_uint4(0, 0, 0, 0);
@@ -2694,6 +2701,9 @@ __device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs
   h.e = (HEntry*)(ws.hash + (size_t)gid * ws.hash_cap * sizeof(HEntry));
   h.mask = ws.hash_cap - 1;
   h.limit = (uint32_t)(ws.hash_cap * 0.7);
+  h.cap = s.cap;
+  h.capz0 = s.capz0;
+  h.capz1 = s.capz1;
   uint64_t st_n = 0, st_nodes = 0;
   const int lane = threadIdx.x & 63;
   for (int64_t j0 = gid - lane; j0 < (int64_t)n_list; j0 += nthreads) {  // wave-uniform (see deep_body)
@@ -2708,6 +2718,12 @@ __device__ void exact_body(const TableArgs& t, const QueryArgs& q, const OutArgs
     if (live) {
       i = out.lists[(int64_t)kClassExact * q.n + j];
       am = query_alpha(q, i);
+      if (q.qlen) {  // this query's own budgets
+        const int L = q.qlen[i];
+        h.cap = q.caps_len + (int64_t)L * kMaxRows;
+        h.capz0 = q.capz_len[2 * L];
+        h.capz1 = q.capz_len[2 * L + 1];
+      }
       int64_t lo, hi;
       quantise(q.mass[i], q.thr ? q.thr[i] : 0.0, q.thr == nullptr, q.tol, q.prec, q.rprec, lo, hi);
       A0 = clamp_budget(q.max_mods ? q.max_mods[i] : q.max_mods_scalar);
@@ -3068,6 +3084,9 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
   h.e = (HEntry*)(hash + (size_t)gid * hash_cap * sizeof(HEntry));
   h.mask = hash_cap - 1;
   h.limit = hash_cap / 4;  // load factor <= 1/4: a wave waits for its longest probe chain
+  h.cap = s.cap;
+  h.capz0 = s.capz0;
+  h.capz1 = s.capz1;
   const bool fuse = WAVE && q.fuse;  // both bounds' values in phase 1 (two dense value slices per wave)
   int8_t* lv = fuse ? vals + (size_t)gid * (hash_cap / 4) * kValSlots * 2 : vals + (size_t)gid * hash_cap * kMaxRows;
   if (fuse) {
@@ -3102,6 +3121,8 @@ __global__ __launch_bounds__(64) void k_length_exact(TableArgs t, LBArgs q, char
       __syncthreads();
       A0 = q.a0_len[L];
       max_len = L;
+      h.capz0 = s.capz0;
+      h.capz1 = s.capz1;
     }
     h.epoch = ++epoch;  // the workspace was zeroed: epochs 1, 2, ... are fresh
     h.used = 0;

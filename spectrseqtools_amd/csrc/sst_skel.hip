@@ -69,7 +69,32 @@ struct Lane {
   uint64_t* cref;        // [cand_cap] the current query's candidates
   int64_t* chash;
   pyset::Table ts;       // their name-tuple set
+  uint64_t* xi;          // [xmask + 1] the bin's list by tuple hash: xepoch << 32 | (index + 1)
+  uint32_t xmask;
+  uint32_t xepoch;       // one per bin: slots of other epochs are empty
 };
+
+// A suspended side's loop state, at the head of its scratch: a relaunch
+// resumes at the bin that listed the re-queries instead of replaying.
+struct WalkState {
+  uint32_t tag;  // side id + 1: valid
+  uint32_t f, n, spec_ctr, consumed, xepoch;
+  int32_t lv0, lv1, pb0, pb1, cur0, cur;
+  uint32_t pmask, pfill;
+  int32_t pcur;
+  uint32_t povf;
+};
+static_assert(sizeof(WalkState) <= 64, "walk state");
+constexpr uint64_t kWalkStateBytes = 64;
+__host__ __device__ inline uint32_t walk_index_slots(uint32_t expl_cap) {
+  uint32_t x = 16;
+  while (x < 2 * expl_cap) x <<= 1;
+  return x;
+}
+__device__ __forceinline__ uint32_t xi_slot(int64_t h, uint32_t mask) {
+  const uint64_t u = (uint64_t)h;
+  return (uint32_t)(u ^ (u >> 29) ^ (u >> 47)) & mask;
+}
 
 __device__ __forceinline__ double key_of(double k) { return k == 0.0 ? 0.0 : k; }
 
@@ -174,19 +199,28 @@ __device__ bool merge_query(const TableArgs& t, const WalkArgs& a, Lane& L, uint
     const uint64_t ref = L.cref[c];
     const int64_t h = L.chash[c];
     const int len = ref_len(ref);
+    // `not in` the bin's list: equal name tuples have equal hashes, so only
+    // the entries filed under this hash are compared
+    uint32_t x = xi_slot(h, L.xmask);
     bool dup = false;
-    for (uint32_t u = 0; u < L.n_ex && !dup; ++u) {
-      const uint64_t* e = L.ex + 4 * u;
+    for (;; x = (x + 1) & L.xmask) {
+      const uint64_t v = L.xi[x];
+      if ((uint32_t)(v >> 32) != L.xepoch) break;  // empty
+      const uint64_t* e = L.ex + 4 * ((uint32_t)v - 1u);
       if ((int64_t)e[0] != h || ref_len(e[3]) != len) continue;
       bool same = true;
       for (int j = 0; j < len && same; ++j) same = ref_row(t, e[3], j) == ref_row(t, ref, j);
-      dup = same;
+      if (same) {
+        dup = true;
+        break;
+      }
     }
     if (dup) continue;
     if (L.n_ex == a.expl_cap) return false;
     int64_t hh;
     uint64_t m0, m1;
     cand_props(t, a, ref, hh, m0, m1);
+    L.xi[x] = ((uint64_t)L.xepoch << 32) | (L.n_ex + 1u);
     uint64_t* e = L.ex + 4 * L.n_ex++;
     e[0] = (uint64_t)h;
     e[1] = m0;
@@ -249,27 +283,34 @@ __global__ __launch_bounds__(256) void k_skel_walk(TableArgs t, WalkArgs a) {
   const int ML = a.max_len[g];
   const uint64_t m0 = a.alpha[2 * g], m1 = a.alpha[2 * g + 1];
   const bool pair_ok = a.pair_ok[g] != 0;
+  // lane scratch: the side's slot (a relaunch finds its state there)
+  uint8_t* sc = a.scratch + (uint64_t)(a.slot ? a.slot[li] : li) * a.scratch_stride;
+  WalkState* wst = (WalkState*)sc;
+  const bool resume = a.resume && wst->tag == sid + 1u;
+  sc += kWalkStateBytes;
   // the side's rows (alive, side bit), SU order, as slot indices
   uint16_t* rows = a.side_rows + (sd ? a.slots : 0) + base;
-  uint32_t n = 0;
-  for (uint32_t r = 0; r < nr; ++r)
-    if (a.alive[base + r] && ((a.r_meta[base + r] >> (2 + sd)) & 1u)) rows[n++] = (uint16_t)r;
   int32_t* mn = a.min_end + (sd ? a.slots : 0) + base;
   int32_t* mx = a.max_end + (sd ? a.slots : 0) + base;
   uint8_t* kp = a.kept + (sd ? a.slots : 0) + base;
-  for (uint32_t f = 0; f < n; ++f) {  // Predictor.predict's initial min_end / max_end (prediction.py:76-79)
-    mn[rows[f]] = 0;
-    mx[rows[f]] = -1;
-    kp[rows[f]] = 1;
-  }
   uint64_t* sk = a.skel + 2 * (a.skel_off[g] + (sd ? (uint64_t)ML : 0));
-  for (int i = 0; i < 2 * ML; ++i) sk[i] = 0;
-  if (nr > (uint32_t)kPipeBigRows || ML + 2 > (int)a.len_cap) {
-    a.side_status[sid] = kWalkLimit;
-    return;
+  uint32_t n = 0;
+  if (resume) {
+    n = wst->n;
+  } else {
+    for (uint32_t r = 0; r < nr; ++r)
+      if (a.alive[base + r] && ((a.r_meta[base + r] >> (2 + sd)) & 1u)) rows[n++] = (uint16_t)r;
+    for (uint32_t f = 0; f < n; ++f) {  // Predictor.predict's initial min_end / max_end (prediction.py:76-79)
+      mn[rows[f]] = 0;
+      mx[rows[f]] = -1;
+      kp[rows[f]] = 1;
+    }
+    for (int i = 0; i < 2 * ML; ++i) sk[i] = 0;
+    if (nr > (uint32_t)kPipeBigRows || ML + 2 > (int)a.len_cap) {
+      a.side_status[sid] = kWalkLimit;
+      return;
+    }
   }
-  // lane scratch
-  uint8_t* sc = a.scratch + (uint64_t)li * a.scratch_stride;
   Lane L;
   for (int s2 = 0; s2 < 2; ++s2) {
     for (int k = 0; k < 2; ++k) {
@@ -295,24 +336,42 @@ __global__ __launch_bounds__(256) void k_skel_walk(TableArgs t, WalkArgs a) {
     sc += 8ull * a.tset_cap;
   }
   L.ts.cap = a.tset_cap;
+  L.xi = (uint64_t*)sc;
+  L.xmask = walk_index_slots(a.expl_cap) - 1u;
+  sc += 8ull * (L.xmask + 1u);
   L.lkeys = sc;
   sc += a.len_cap;
   L.lseen = sc;
-  for (uint32_t k = 0; k < a.len_cap; ++k) L.lseen[k] = 0;
-  L.cur = 0;
-  pyset::clear(L.pos[0]);
-  pyset::add(L.pos[0], 0, 0);  // pos = {0} (:126)
-
-  SideRows R{rows, a.r_su + base, a.r_ob + base};
-  const uint64_t spec_q0 = a.q_off[g] + (sd ? a.q0[g] : 0u);  // this side's speculative queries
-  uint32_t spec_ctr = 0;    // speculative queries of the closed bins so far
-  uint32_t consumed = 0;    // re-query answers used
+  uint32_t f0 = 1, spec_ctr = 0, consumed = 0;  // speculative queries of the closed bins so far, re-query answers used
   int lv0 = -1, lv1 = -1;   // last bin with explanations
   int pb0 = -1, pb1 = -1;   // the previous closed bin
   int cur0 = 0;
+  if (resume) {
+    f0 = wst->f;
+    spec_ctr = wst->spec_ctr;
+    consumed = wst->consumed;
+    lv0 = wst->lv0, lv1 = wst->lv1, pb0 = wst->pb0, pb1 = wst->pb1, cur0 = wst->cur0;
+    L.cur = wst->cur;
+    pyset::Table& P = L.pos[L.cur];
+    P.mask = wst->pmask;
+    P.fill = wst->pfill;
+    P.cur = wst->pcur;
+    P.overflow = wst->povf != 0;
+    L.xepoch = wst->xepoch;
+  } else {
+    for (uint32_t k = 0; k < a.len_cap; ++k) L.lseen[k] = 0;
+    for (uint32_t k = 0; k <= L.xmask; ++k) L.xi[k] = 0;
+    L.xepoch = 0;
+    L.cur = 0;
+    pyset::clear(L.pos[0]);
+    pyset::add(L.pos[0], 0, 0);  // pos = {0} (:126)
+  }
+
+  SideRows R{rows, a.r_su + base, a.r_ob + base};
+  const uint64_t spec_q0 = a.q_off[g] + (sd ? a.q0[g] : 0u);  // this side's speculative queries
   int status = kWalkDone;
   const double pair_hi = (double)t.pair_hi;
-  for (uint32_t f = 1; f < n && status == kWalkDone; ++f) {
+  for (uint32_t f = f0; f < n && status == kWalkDone; ++f) {
     if (L.pos[L.cur].fill == 0) {  // no positions left (:132-135)
       kp[rows[f]] = 0;
       continue;
@@ -386,12 +445,18 @@ __global__ __launch_bounds__(256) void k_skel_walk(TableArgs t, WalkArgs a) {
         }
         a.req_block[sid] = ((uint64_t)start << 32) | n_off;
         status = kWalkSuspended;
+        // the loop state at this bin's start, for the relaunch
+        const pyset::Table& P = L.pos[L.cur];
+        WalkState w{sid + 1u, f, n, spec_base, consumed, L.xepoch, lv0, lv1, pb0, pb1, cur0, L.cur,
+                    P.mask, P.fill, P.cur, P.overflow ? 1u : 0u};
+        *wst = w;
         break;
       }
     }
     // the bin's explanation list
     bool all_none = true;
     L.n_ex = 0;
+    ++L.xepoch;  // empties the list's index
     uint32_t off_j = 0;
     for (uint32_t j = 0; j < nq && res == kBinNone; ++j) {
       double diff, thr;
@@ -574,8 +639,8 @@ hipError_t launch_result_refs(const int8_t* status, int64_t n, const uint4* hits
 
 uint64_t walk_scratch_bytes(uint32_t pos_cap, uint32_t len_cap, uint32_t expl_cap, uint32_t cand_cap,
                             uint32_t tset_cap) {
-  const uint64_t b = 2ull * 2 * 12 * pos_cap + 16ull * len_cap + 32ull * expl_cap + 16ull * cand_cap +
-                     2ull * 12 * tset_cap + 2ull * len_cap;
+  const uint64_t b = kWalkStateBytes + 2ull * 2 * 12 * pos_cap + 16ull * len_cap + 32ull * expl_cap +
+                     16ull * cand_cap + 2ull * 12 * tset_cap + 8ull * walk_index_slots(expl_cap) + 2ull * len_cap;
   return (b + 15) & ~15ull;
 }
 

@@ -567,8 +567,11 @@ def final_dict_device(dp_table, rows: DeviceRows, alpha_dev, tolerance=None, max
 
 
 def _masked_explain_refs(dp_table, alpha_dev, mass, thr, spec, n, max_len, dst, ptr, cnt, st):
-    """Windows answered by the masked explain on their spectra's alphabets,
-    one pass per max_len group (budgets follow max_len); each window's
+    """Windows answered by the masked explain on their spectra's alphabets
+    with their spectra's budgets (round(max_len * rate) per row,
+    round(seq.modification_rate * max_len) modifications: the budgets the
+    rebuilt table of skeleton_building.py:212 / prediction.py:207 carries),
+    in one pass (sst_explain_alpha_lens_batch_device); each window's
     candidate reference lands at dst[i] of (ptr, cnt, st).  Returns the
     results (their payload backs the references)."""
     import torch
@@ -577,27 +580,21 @@ def _masked_explain_refs(dp_table, alpha_dev, mass, thr, spec, n, max_len, dst, 
     eng = dt.engine
     if n == 0:
         return []
-    sp_h = spec[:n].cpu().numpy()
-    ml = np.asarray(max_len, dtype=np.int64)[sp_h]
-    order = np.argsort(ml, kind="stable")
-    o = torch.as_tensor(order, device=mass.device)
-    ms, th, sp = mass[:n][o].contiguous(), thr[:n][o].contiguous(), spec[:n][o].contiguous()
-    ds = dst[:n][o].contiguous()
-    ml_s = ml[order]
-    bounds = np.flatnonzero(np.diff(ml_s)) + 1
+    dev = mass.device
     masses = dp_table.masses
-    is_mod = [m.is_modification for m in masses]
-    out = []
-    for s0, s1 in zip(np.concatenate([[0], bounds]).tolist(), np.concatenate([bounds, [n]]).tolist()):
-        Lm = int(ml_s[s0])
-        dt.set_budgets(is_mod, [round(Lm * m.modification_rate) for m in masses])
-        res = dt.explain_alpha_device(ms.data_ptr() + 8 * s0, th.data_ptr() + 8 * s0, sp.data_ptr() + 4 * s0,
-                                      alpha_dev.data_ptr(), s1 - s0, dp_table.tolerance, dp_table.precision,
-                                      round(dp_table.seq.modification_rate * Lm))
-        eng.check(eng._lib.sst_result_refs_device(res.handle, ds.data_ptr() + 8 * s0, ptr.data_ptr(),
-                                                  cnt.data_ptr(), st.data_ptr()), "sst_result_refs_device")
-        out.append(res)
-    return out
+    lens = np.unique(np.asarray(max_len, dtype=np.int64))
+    caps = np.array([[round(int(L) * m.modification_rate) for m in masses] for L in lens], dtype=np.int64)
+    mods_l = torch.as_tensor(np.array([round(dp_table.seq.modification_rate * int(L)) for L in lens], np.int64),
+                             device=dev)
+    ml_q = torch.as_tensor(np.asarray(max_len, dtype=np.int64), device=dev)[spec[:n].long()]
+    qlen = torch.searchsorted(torch.as_tensor(lens, device=dev), ml_q).to(torch.int32).contiguous()
+    mods = mods_l[qlen.long()].contiguous()
+    res = dt.explain_alpha_lens_device(mass.data_ptr(), thr.data_ptr(), spec.data_ptr(), alpha_dev.data_ptr(),
+                                       qlen.data_ptr(), caps, n, dp_table.tolerance, dp_table.precision,
+                                       mods.data_ptr())
+    eng.check(eng._lib.sst_result_refs_device(res.handle, dst.data_ptr(), ptr.data_ptr(), cnt.data_ptr(),
+                                              st.data_ptr()), "sst_result_refs_device")
+    return [res]
 
 
 def merge_requery_round(m_sid, m_ptr, m_n, m_st, block, p_, n_, s_, n_sides):
@@ -731,17 +728,25 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
     # SST_WALK_MAX_ROUNDS (exact-mode spectra re-query every bin whose
     # predecessor had no explanations through the host)
     merged = None
+    keep_alive = []
     m_sid = torch.zeros(0, dtype=torch.int64, device=dev)
     m_ptr = torch.zeros(0, dtype=torch.int64, device=dev)
     m_n = torch.zeros(0, dtype=torch.int32, device=dev)
     m_st = torch.zeros(0, dtype=torch.int8, device=dev)
     n_rounds = 0
-    keep_alive = []
-    mode = {}  # side -> big
     run = np.arange(2 * S, dtype=np.int32)
     big = np.zeros(0, np.int32)
     launches = 0
     n_req_total = 0
+    # scratch slots: every side's at the small caps (slot = side id), the
+    # sides that outgrew them at the big caps (slots in the order they did);
+    # a suspended side's state stays in its slot and the relaunch resumes it
+    t_small, t_big = _native.pyset_table_size(caps[1]), _native.pyset_table_size(big_caps[1])
+    stride_small = _native.walk_scratch_bytes(pos_cap, len_cap, caps[0], caps[1], t_small)
+    stride_big = _native.walk_scratch_bytes(pos_cap, len_cap, big_caps[0], big_caps[1], t_big)
+    scratch_small = torch.empty(max(1, 2 * S) * stride_small, dtype=torch.uint8, device=dev)
+    scratch_big = torch.zeros(0, dtype=torch.uint8, device=dev)  # zeroed: a new slot holds no state
+    big_slot = {}
     torch.cuda.synchronize(dev)
     while len(run) or len(big):
         req_block = torch.zeros(max(1, 2 * S), dtype=torch.int64, device=dev)
@@ -750,18 +755,26 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
         if merged is not None:
             a.rq_block[0], a.rq_ptr[0], a.rq_n[0], a.rq_st[0] = (t.data_ptr() for t in merged)
         ctl.zero_()
-        for sides, (e_cap, c_cap) in ((run, caps), (big, big_caps)):
+        for b in big.tolist():
+            big_slot.setdefault(b, len(big_slot))
+        need = len(big_slot) * stride_big
+        if need > scratch_big.numel():
+            grown = torch.zeros(max(need, 2 * scratch_big.numel()), dtype=torch.uint8, device=dev)
+            grown[:scratch_big.numel()].copy_(scratch_big)
+            scratch_big = grown
+        for sides, (e_cap, c_cap), t_cap, stride, scr in ((run, caps, t_small, stride_small, scratch_small),
+                                                          (big, big_caps, t_big, stride_big, scratch_big)):
             if not len(sides):
                 continue
-            t_cap = _native.pyset_table_size(c_cap)
-            stride = _native.walk_scratch_bytes(pos_cap, len_cap, e_cap, c_cap, t_cap)
-            scratch = torch.empty(len(sides) * stride, dtype=torch.uint8, device=dev)
             sides_t = torch.as_tensor(sides, device=dev)
+            slots_t = sides_t if scr is scratch_small else torch.as_tensor(
+                np.array([big_slot[b] for b in sides.tolist()], np.int32), device=dev)
             a.sides, a.n_sides = sides_t.data_ptr(), len(sides)
-            a.scratch, a.scratch_stride = scratch.data_ptr(), stride
+            a.slot, a.resume = slots_t.data_ptr(), int(launches > 0)
+            a.scratch, a.scratch_stride = scr.data_ptr(), stride
             a.expl_cap, a.cand_cap, a.tset_cap = e_cap, c_cap, t_cap
             eng.check(L.sst_skel_walk_device(h, ctypes.byref(a)), "sst_skel_walk_device")
-            keep_alive.append((scratch, sides_t))
+            keep_alive.append((sides_t, slots_t))
             launches += 1
         eng.synchronize()
         keep_alive.clear()

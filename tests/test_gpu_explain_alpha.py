@@ -208,3 +208,50 @@ def test_explain_alpha_rootless_window_past_reduced_extent():
             if int(res.status[i]) == want_st == _native.SST_SOME:
                 assert res.candidates(i) == want
     assert n_oot >= 2
+
+
+def test_explain_alpha_lens_vs_rebuilt_tables(setup):
+    """Per-query budgets (sst_explain_alpha_lens_batch_device): every query
+    with the caps round(L * rate) of its own max_len L and its own
+    max_modifications, in one pass, against the oracle on its alphabet's
+    rebuilt table with those budgets -- windows of many max_len values, as the
+    skeleton walk's re-queries carry them."""
+    rows, dev, is_mod, _ = setup
+    rng = np.random.default_rng(76)
+    alphas = _alphabets(rows, rng, 8)
+    mass, thr, spec = _queries(rows, alphas, rng, 90, 10)
+    rate = [float(rng.choice(RATES)) if md else (1.0 if m else 0.0) for m, md in zip(rows, is_mod)]
+    lens = [2, 4, 7, 12, 20]
+    caps_by_len = np.array([[round(L * r) for r in rate] for L in lens], np.int64)
+    qlen = rng.integers(0, len(lens), len(mass))
+    A = np.array([round(0.5 * lens[k]) if rng.random() < 0.7 else int(rng.integers(0, 4)) for k in qlen])
+    masks = row_masks(np.array([[r in a for r in range(len(rows))] for a in alphas]))
+    res = dev.explain_alpha_lens(mass, thr, spec, masks, qlen, caps_by_len, A, TOL, PREC)
+    tabs = {}
+    n_some = n_bind = 0
+    for i in range(len(mass)):
+        a = alphas[spec[i]]
+        full = [0] + a
+        ms = [rows[r] for r in full]
+        lim = (max(ms) * 35 + 32) // 32 * 32
+        whi = np.rint(mass[i] / PREC) + np.ceil(thr[i] / PREC)
+        if whi >= 1 and lim - 32 <= whi < lim:
+            assert int(res.status[i]) == _native.SST_ABORTED, i
+            continue
+        if spec[i] not in tabs:
+            tabs[spec[i]] = oracle.build_table(ms, max(ms) * 35, 32)
+        tab = tabs[spec[i]]
+        caps = caps_by_len[qlen[i]]
+        alph = oracle.Alphabet(ms, [is_mod[r] for r in full], [int(caps[r]) for r in full])
+        st, sols, n_e, _ = oracle.explain_table(tab, 32, alph, mass[i], thr[i], TOL, int(A[i]))
+        if st < 0:
+            assert int(res.status[i]) == _native.SST_OUT_OF_TABLE, i
+            continue
+        want = [tuple(full[x] for x in t) for t in sols]
+        want_st = _native.SST_SOME if want else (_native.SST_EMPTY if n_e else _native.SST_NONE)
+        assert int(res.status[i]) == want_st, (i, mass[i], thr[i], int(A[i]), lens[qlen[i]])
+        assert res.candidates(i) == want, (i, lens[qlen[i]])
+        n_some += want_st == _native.SST_SOME
+        free = oracle.Alphabet(ms, [is_mod[r] for r in full], [99] * len(full))
+        n_bind += oracle.explain_table(tab, 32, free, mass[i], thr[i], TOL, 99)[1] != sols
+    assert n_some > 150 and n_bind > 20

@@ -337,6 +337,16 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
     assert n_len >= n // 2
     if variant != "full_ladders":
         assert sk.requeries > 0 or bins.deferred["queries"] > 0
+        import torch
+
+        # tiny lane capacities: most sides outgrow them and walk again at the
+        # big ones (fresh slots), suspended sides resume in either slot kind
+        sk2 = PD.skeleton_device(dp, rows, fx.alpha, max_len, bins=bins, caps=(4, 2), big_caps=(64, 32))
+        assert sk2.launches > sk.launches
+        assert (sk2.status == sk.status).all()
+        for x, y in ((sk.skel, sk2.skel), (sk.min_end, sk2.min_end), (sk.max_end, sk2.max_end),
+                     (sk.kept, sk2.kept)):
+            assert torch.equal(x, y)
 
 
 def test_device_pipeline_big_spectra(engine):
