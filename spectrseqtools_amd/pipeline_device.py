@@ -436,45 +436,28 @@ def bins_device(dp_table, rows: DeviceRows, alpha, tolerance=None, max_len=None)
 
 
 def answer_deferred(dp_table, alpha, d_mass, d_thr, d_spec, d_q, n, max_len, status, count):
-    """The listed off-pair-class windows through the masked explain, one pass
-    per max_len group (the rows' caps follow max_len); statuses and counts
-    scattered into the bin-query arrays.  Returns the per-group results."""
+    """The listed off-pair-class windows through the masked explain with
+    their spectra's budgets (one pass, per-query budgets: the rows' caps
+    follow max_len); statuses and counts scattered into the bin-query
+    arrays.  Returns the pass's result and the list (in its order)."""
     import torch
 
-    dt = dp_table.device_table
-    eng = dt.engine
     info = {"queries": n, "groups": [], "results": []}
     if n == 0:
         return info
     spec = d_spec[:n].cpu().numpy()
     ml = np.asarray(max_len, dtype=np.int64)[spec]
-    order = np.argsort(ml, kind="stable")
-    o = torch.as_tensor(order, device=d_mass.device)
-    mass, thr = d_mass[:n][o].contiguous(), d_thr[:n][o].contiguous()
-    sp, qi = d_spec[:n][o].contiguous(), d_q[:n][o].contiguous()
-    ml_s = ml[order]
-    info["spec"], info["mass"], info["thr"] = sp.cpu().numpy(), mass.cpu().numpy(), thr.cpu().numpy()
-    bounds = np.flatnonzero(np.diff(ml_s)) + 1
-    starts = np.concatenate([[0], bounds])
-    ends = np.concatenate([bounds, [n]])
-    masses = dp_table.masses
-    is_mod = [m.is_modification for m in masses]
-    A_rate = dp_table.seq.modification_rate
-    for s0, s1 in zip(starts.tolist(), ends.tolist()):
-        L = int(ml_s[s0])
-        dt.set_budgets(is_mod, [round(L * m.modification_rate) for m in masses])
-        k = int(s1 - s0)
-        res = dt.explain_alpha_device(mass.data_ptr() + 8 * s0, thr.data_ptr() + 8 * s0, sp.data_ptr() + 4 * s0,
-                                      alpha.data_ptr(), k, dp_table.tolerance, dp_table.precision,
-                                      round(A_rate * L))
-        res.fetch_device()
-        idx = qi[s0:s1]
-        status[idx] = torch.as_tensor(res.status, device=status.device)
-        count[idx] = torch.as_tensor(res.count.astype(np.int32), device=count.device)
-        info["groups"].append((L, k))
-        info["results"].append((int(s0), res))
-    info["order"] = order
-    info["dst"] = qi  # sorted position -> bin-query index
+    info["spec"], info["mass"], info["thr"] = spec, d_mass[:n].cpu().numpy(), d_thr[:n].cpu().numpy()
+    res = _lens_pass(dp_table, alpha, d_mass, d_thr, d_spec, n, max_len)
+    res.fetch_device()
+    idx = d_q[:n]
+    status[idx] = torch.as_tensor(res.status, device=status.device)
+    count[idx] = torch.as_tensor(res.count.astype(np.int32), device=count.device)
+    Ls, ks = np.unique(ml, return_counts=True)
+    info["groups"] = [(int(L), int(k)) for L, k in zip(Ls, ks)]
+    info["results"].append((0, res))
+    info["order"] = np.arange(n)
+    info["dst"] = idx.contiguous()  # list position -> bin-query index
     return info
 
 
@@ -566,20 +549,15 @@ def final_dict_device(dp_table, rows: DeviceRows, alpha_dev, tolerance=None, max
     return DeviceDict(off, n_ent, key, thr)
 
 
-def _masked_explain_refs(dp_table, alpha_dev, mass, thr, spec, n, max_len, dst, ptr, cnt, st):
-    """Windows answered by the masked explain on their spectra's alphabets
-    with their spectra's budgets (round(max_len * rate) per row,
+def _lens_pass(dp_table, alpha_dev, mass, thr, spec, n, max_len):
+    """The masked explain of windows [0, n) on their spectra's alphabets with
+    their spectra's budgets (round(max_len * rate) per row,
     round(seq.modification_rate * max_len) modifications: the budgets the
     rebuilt table of skeleton_building.py:212 / prediction.py:207 carries),
-    in one pass (sst_explain_alpha_lens_batch_device); each window's
-    candidate reference lands at dst[i] of (ptr, cnt, st).  Returns the
-    results (their payload backs the references)."""
+    in one pass (sst_explain_alpha_lens_batch_device)."""
     import torch
 
     dt = dp_table.device_table
-    eng = dt.engine
-    if n == 0:
-        return []
     dev = mass.device
     masses = dp_table.masses
     lens = np.unique(np.asarray(max_len, dtype=np.int64))
@@ -592,6 +570,18 @@ def _masked_explain_refs(dp_table, alpha_dev, mass, thr, spec, n, max_len, dst, 
     res = dt.explain_alpha_lens_device(mass.data_ptr(), thr.data_ptr(), spec.data_ptr(), alpha_dev.data_ptr(),
                                        qlen.data_ptr(), caps, n, dp_table.tolerance, dp_table.precision,
                                        mods.data_ptr())
+    res.keep_alive = (qlen, mods)  # read by the pass until it settles
+    return res
+
+
+def _masked_explain_refs(dp_table, alpha_dev, mass, thr, spec, n, max_len, dst, ptr, cnt, st):
+    """Windows answered by the masked explain (_lens_pass); each window's
+    candidate reference lands at dst[i] of (ptr, cnt, st).  Returns the
+    results (their payload backs the references)."""
+    if n == 0:
+        return []
+    res = _lens_pass(dp_table, alpha_dev, mass, thr, spec, n, max_len)
+    eng = dp_table.device_table.engine
     eng.check(eng._lib.sst_result_refs_device(res.handle, dst.data_ptr(), ptr.data_ptr(), cnt.data_ptr(),
                                               st.data_ptr()), "sst_result_refs_device")
     return [res]
