@@ -527,6 +527,7 @@ struct WaveLds {
   uint8_t ord[kWP];  // peaks in (mass, position) order when they do not come sorted
   uint32_t kcnt[4];
   uint32_t sstar;
+  uint32_t hist[64];  // wave_pair_window: starts per position of a 64-query window
 };
 
 // LDS written by some lanes of the wave, read by others: order the accesses
@@ -695,6 +696,39 @@ __device__ __forceinline__ void wave_pair(const WaveLds& L, uint32_t n, uint32_t
   e = s <= L.sstar ? s + 1 + (q - L.qoff[s]) : n - 1;
 }
 
+// The pairs of queries q0 + lane (q0 a multiple of 64; qoff[s0] <= q0):
+// lane j looks at start r = s0 + 1 + j, whose first query sits at position
+// qoff[r] - q0 of the window; a histogram of those positions and its prefix
+// give each lane its start, the last r with qoff[r] <= q (as wave_pair's
+// binary search, without one per lane).  Returns the start of query q0 + 64;
+// a window whose 64 looked-at starts all begin in it (starts without pairs)
+// falls back to the binary search.
+__device__ __forceinline__ uint32_t wave_pair_window(WaveLds& L, uint32_t n, uint32_t q0, uint32_t s0, uint32_t& s,
+                                                     uint32_t& e) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t r = s0 + 1u + (uint32_t)lane;
+  const uint32_t pos = r < n ? L.qoff[r] - q0 : 0xFFFFFFFFu;
+  L.hist[lane] = 0u;
+  wsync();
+  if (pos < 64u) atomicAdd(&L.hist[pos], 1u);
+  wsync();
+  uint32_t tot;
+  const uint32_t cnt = wave_excl(L.hist[lane], tot) + L.hist[lane];  // starts at positions <= lane
+  const uint64_t at64 = __ballot(pos == 64u);
+  const bool full = __shfl(pos, 63, 64) <= 64u;  // lane 63's start begins by q0 + 64: maybe more beyond it
+  const uint32_t q = q0 + (uint32_t)lane;
+  wsync();  // the histogram is rewritten by the next window
+  if (!full) {
+    s = s0 + cnt;
+    e = s <= L.sstar ? s + 1u + (q - L.qoff[s]) : n - 1u;
+    return s0 + tot + (uint32_t)__builtin_popcountll(at64);
+  }
+  wave_pair(L, n, q, s, e);
+  uint32_t s1, e1;
+  wave_pair(L, n, q0 + 64u, s1, e1);
+  return s1;
+}
+
 // the pair-list entries with sums in [a, hi] (1 <= a <= hi < pair_hi) from the census: two independent loads
 __device__ __forceinline__ uint32_t census_walk(const TableArgs& t, uint32_t a, uint32_t hi, uint32_t& first,
                                                 uint32_t& bytes) {
@@ -782,9 +816,12 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
           ro[r] = L.ob[r];
         }
       }
-      for (uint32_t q = lane; q < Q; q += 64) {
+      uint32_t s0 = 0;  // the start of query q0
+      for (uint32_t q0 = 0; q0 < Q; q0 += 64) {
+        const uint32_t q = q0 + lane;
         uint32_t s, e;
-        wave_pair(L, n, q, s, e);
+        s0 = wave_pair_window(L, n, q0, s0, s, e);
+        if (q >= Q) continue;
         const QAns r = wave_answer(L, t, a, s, e);
         nh += (r.status == SST_SOME || r.status == SST_OVERFLOW);
         nb += r.status == SST_SOME ? r.bytes + 2u : 0u;
@@ -996,10 +1033,13 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
   b.chunk = (a.n_spec + b.n_chunks - 1) / b.n_chunks;
   if (b.n_chunks > a.chunk_cap) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_rows_count_w, dim3(wave_wg), dim3(64 * kWavesPerWG), 0, st, t, b);
-  hipLaunchKernelGGL(k_rows_count, dim3(n_wg), dim3(kRowsWG), dyn, st, t, b);
+  // the workgroup kernels take the few spectra over kWP peaks (none in most
+  // batches: a small grid keeps their launches cheap when idle)
+  const int big_wg = n_wg < 64 ? n_wg : 64;
+  hipLaunchKernelGGL(k_rows_count, dim3(big_wg), dim3(kRowsWG), dyn, st, t, b);
   hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kRowsWG), 0, st, b);
   hipLaunchKernelGGL(k_rows_emit_w, dim3(wave_wg), dim3(64 * kWavesPerWG), wdyn, st, t, b);
-  hipLaunchKernelGGL(k_rows_emit, dim3(n_wg), dim3(kRowsWG), dyn, st, t, b);  // last: writes the header
+  hipLaunchKernelGGL(k_rows_emit, dim3(big_wg), dim3(kRowsWG), dyn, st, t, b);  // last: writes the header
   return hipGetLastError();
 }
 
