@@ -335,14 +335,16 @@ def main():
         engine.set_stream(packer.cuda_stream)
         r.wire_pack(outs7[j & 1].data_ptr(), n7s[b], wbuf[j & 1].data_ptr(), wbuf[j & 1].numel())
         engine.set_stream(None)
+        # this step's wire size (the packed header: fixed part + its list),
+        # agreed with one all_gather of an int64 per rank inside the timed loop
+        # (RCCL has no gatherv: the gather then moves the largest rank's size);
+        # the event follows the header's copy, so the host reads this step's
+        # header, not the previous one's
+        with torch.cuda.stream(packer):
+            hdr_host.copy_(wbuf[j & 1][:WIRE_HEADER], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(packer)
         copied[j & 1] = ev
-        # this step's wire size (the packed header: fixed part + its list),
-        # agreed with one all_gather of an int64 per rank inside the timed loop
-        # (RCCL has no gatherv: the gather then moves the largest rank's size)
-        with torch.cuda.stream(packer):
-            hdr_host.copy_(wbuf[j & 1][:WIRE_HEADER], non_blocking=True)
         ev.synchronize()
         sizes = gath.agree(wire_used_bytes(hdr_host.numpy()), capacity=wbuf[j & 1].numel())
         wire_sizes.append(sizes)

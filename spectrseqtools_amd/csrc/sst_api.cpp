@@ -1546,11 +1546,14 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   const bool fresh = !r->rows_ctl.p;
   if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, (uint64_t)16 * r->cap_n + (1u << 20))) ||
       !r->rows_su.ensure(std::max<size_t>(1, 4 * P) * 8) || !r->rows_ob.ensure(std::max<size_t>(1, 4 * P) * 8) ||
-      !r->rows_side.ensure(2 * S * 4) || !r->rows_tot.ensure(3 * S * 4) || !r->rows_chunk.ensure(2 * 3 * NC * 8) ||
+      !r->rows_side.ensure(2 * S * 4) || !r->rows_tot.ensure(3 * S * 4) || !r->rows_chunk.ensure(2 * 3 * NC * 8 + 4 * 16 * 8) ||
       !r->rows_big.ensure(S * 4) || !r->rows_ctl.ensure(64) ||
       !r->rows_ans.ensure(std::max<size_t>(1, 2 * kRowsAnsPerPeak * P) * 8) || !r->rows_aq.ensure(2 * S * 4))
     return bail(fail(c, SST_E_NOMEM, "device allocation failed (rows step)"));
-  if (fresh) HIP_OK(c, hipMemsetAsync(r->rows_ctl.p, 0, 64, c->stream));
+  if (fresh) {
+    HIP_OK(c, hipMemsetAsync(r->rows_ctl.p, 0, 64, c->stream));
+    HIP_OK(c, hipMemsetAsync((uint64_t*)r->rows_chunk.p + 6 * NC, 0, 4 * 16 * 8, c->stream));  // scan flags: no pass id
+  }
   r->pass = {t, nullptr, nullptr, nullptr, max_mods_scalar, tol, prec, 1, cap_per_query, nullptr, nullptr};
   r->pass_stream = c->stream;
   r->settle_ev_pending = false;
@@ -1593,6 +1596,7 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   a.chunk_tot = (unsigned long long*)r->rows_chunk.p;
   a.chunk_off = (uint64_t*)r->rows_chunk.p + 3 * NC;
   a.chunk_cap = (int64_t)NC;
+  a.scan_agg = (uint64_t*)r->rows_chunk.p + 6 * NC;
   a.ctl = (uint64_t*)r->rows_ctl.p;
   a.err = (uint32_t*)((char*)r->rows_ctl.p + 32);
   a.done = (uint32_t*)((char*)r->rows_ctl.p + 40);

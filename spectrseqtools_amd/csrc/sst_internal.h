@@ -487,6 +487,7 @@ struct RowsArgs {
   uint32_t* totals;           // [3 n_spec] queries, hits, payload bytes
   unsigned long long* chunk_tot;  // [3 n_chunks] totals of each wave's contiguous chunk of spectra
   uint64_t* chunk_off;        // [3 n_chunks] their exclusive offsets (k_rows_scan)
+  uint64_t* scan_agg;         // [4 x 16] k_rows_scan's tile sums and their pass id (the look-back)
   int64_t chunk, n_chunks;    // spectra per chunk, chunks (= waves of the wave kernels' grid; set at launch)
   int64_t chunk_cap;          // chunk arrays' capacity (chunks)
   uint64_t* ctl;              // [4] totals

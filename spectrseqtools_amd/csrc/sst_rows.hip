@@ -349,13 +349,13 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_count(TableArgs t, RowsArgs a)
   }
 }
 
-// exclusive offsets of the wave kernels' chunks (each wave's contiguous run of
-// spectra; the workgroup kernels add the big spectra's totals to their chunk)
-// and the pass totals: one workgroup, each thread a contiguous run of kScanPer
-// chunks.  A spectrum's own offset is its chunk's plus the totals of the
-// chunk's earlier spectra (the emitting wave walks them in order).
-constexpr int kScanPer = 4;
-constexpr int kScanChunk = kScanPer * kRowsWG;
+// exclusive offsets of the wave kernels' chunks (the workgroup kernels add
+// the big spectra's totals to their chunk) and the pass totals: one thread per
+// chunk, a workgroup per 1 024 chunks, the tiles chained by a look-back over
+// the earlier tiles' published sums (<= kScanTiles workgroups, all resident).
+// A spectrum's own offset is its chunk's plus the totals of the chunk's
+// earlier spectra (the emitting wave walks them in order).
+constexpr int kScanTiles = 16;
 
 __device__ __forceinline__ uint64_t block_excl64(uint64_t v, uint64_t* s_w, uint64_t& total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -380,29 +380,37 @@ __device__ __forceinline__ uint64_t block_excl64(uint64_t v, uint64_t* s_w, uint
 
 __global__ __launch_bounds__(kRowsWG) void k_rows_scan(RowsArgs a) {
   __shared__ uint64_t s_w[16];
+  __shared__ uint64_t s_pre[3];
   const int64_t nb = a.n_chunks;
-  uint64_t carry[3] = {0, 0, 0};
-  for (int64_t c0 = 0; c0 < nb; c0 += kScanChunk) {
-    const int64_t j0 = c0 + (int64_t)threadIdx.x * kScanPer;
-    uint64_t v[3 * kScanPer], run[3] = {0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 3 * kScanPer; ++k) v[k] = j0 + k / 3 < nb ? a.chunk_tot[3 * j0 + k] : 0ull;
-#pragma unroll
-    for (int k = 0; k < 3 * kScanPer; ++k) run[k % 3] += v[k];
-    uint64_t base[3], tot[3];
-    for (int c = 0; c < 3; ++c) base[c] = carry[c] + block_excl64(run[c], s_w, tot[c]);
-#pragma unroll
-    for (int k = 0; k < 3 * kScanPer; ++k) {
-      if (j0 + k / 3 < nb) a.chunk_off[3 * j0 + k] = base[k % 3];
-      base[k % 3] += v[k];
-    }
-    for (int c = 0; c < 3; ++c) carry[c] += tot[c];
+  const int b = blockIdx.x;
+  const int64_t j = (int64_t)b * kRowsWG + threadIdx.x;
+  uint64_t v[3], ex[3], tot[3];
+  for (int c = 0; c < 3; ++c) v[c] = j < nb ? a.chunk_tot[3 * j + c] : 0ull;
+  for (int c = 0; c < 3; ++c) ex[c] = block_excl64(v[c], s_w, tot[c]);
+  if (threadIdx.x == 0) {  // publish the tile's sums
+    for (int c = 0; c < 3; ++c) a.scan_agg[4 * b + c] = tot[c];
+    __threadfence();
+    __hip_atomic_store(&a.scan_agg[4 * b + 3], a.pass_id, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (threadIdx.x == 0) {
-    a.ctl[0] = carry[0];
-    a.ctl[1] = carry[1];
-    a.ctl[2] = carry[2];
-    if (carry[0] > a.cap_queries || carry[1] > a.cap_queries || carry[2] > a.cap_bytes) atomicOr(a.err, 4u);
+  if (threadIdx.x < 3) {  // this tile's offset: the earlier tiles' sums
+    const int c = threadIdx.x;
+    uint64_t pre = 0;
+    for (int k = 0; k < b; ++k) {
+      while (__hip_atomic_load(&a.scan_agg[4 * k + 3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != a.pass_id) {
+      }
+      pre += __hip_atomic_load(&a.scan_agg[4 * k + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_pre[c] = pre;
+  }
+  __syncthreads();
+  if (j < nb)
+    for (int c = 0; c < 3; ++c) a.chunk_off[3 * j + c] = s_pre[c] + ex[c];
+  if (b == (int)gridDim.x - 1 && threadIdx.x == 0) {  // the pass totals
+    const uint64_t q = s_pre[0] + tot[0], h = s_pre[1] + tot[1], by = s_pre[2] + tot[2];
+    a.ctl[0] = q;
+    a.ctl[1] = h;
+    a.ctl[2] = by;
+    if (q > a.cap_queries || h > a.cap_queries || by > a.cap_bytes) atomicOr(a.err, 4u);
   }
 }
 
@@ -1027,18 +1035,23 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
     return e;
   }
   const int wave_wg = n_wg * (occ > 0 ? occ : 1);
-  // contiguous chunks of spectra, one per wave of the wave kernels' grid
+  // one spectrum per wave where the chunk arrays allow (the dispatcher then
+  // balances the waves: a resident-only grid of contiguous chunks left the
+  // kernel waiting for its 3-spectrum waves), contiguous chunks beyond
   RowsArgs b = a;
-  b.n_chunks = (int64_t)wave_wg * kWavesPerWG;
+  b.n_chunks = a.n_spec < a.chunk_cap ? a.n_spec : a.chunk_cap;
   b.chunk = (a.n_spec + b.n_chunks - 1) / b.n_chunks;
-  if (b.n_chunks > a.chunk_cap) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_rows_count_w, dim3(wave_wg), dim3(64 * kWavesPerWG), 0, st, t, b);
+  b.n_chunks = (a.n_spec + b.chunk - 1) / b.chunk;
+  if (b.n_chunks > a.chunk_cap || b.n_chunks > (int64_t)kScanTiles * kRowsWG) return hipErrorInvalidValue;
+  const int wgrid = (int)((b.n_chunks + kWavesPerWG - 1) / kWavesPerWG);
+  (void)wave_wg;
+  hipLaunchKernelGGL(k_rows_count_w, dim3(wgrid), dim3(64 * kWavesPerWG), 0, st, t, b);
   // the workgroup kernels take the few spectra over kWP peaks (none in most
   // batches: a small grid keeps their launches cheap when idle)
   const int big_wg = n_wg < 64 ? n_wg : 64;
   hipLaunchKernelGGL(k_rows_count, dim3(big_wg), dim3(kRowsWG), dyn, st, t, b);
-  hipLaunchKernelGGL(k_rows_scan, dim3(1), dim3(kRowsWG), 0, st, b);
-  hipLaunchKernelGGL(k_rows_emit_w, dim3(wave_wg), dim3(64 * kWavesPerWG), wdyn, st, t, b);
+  hipLaunchKernelGGL(k_rows_scan, dim3((unsigned)((b.n_chunks + kRowsWG - 1) / kRowsWG)), dim3(kRowsWG), 0, st, b);
+  hipLaunchKernelGGL(k_rows_emit_w, dim3(wgrid), dim3(64 * kWavesPerWG), wdyn, st, t, b);
   hipLaunchKernelGGL(k_rows_emit, dim3(big_wg), dim3(kRowsWG), dyn, st, t, b);  // last: writes the header
   return hipGetLastError();
 }
