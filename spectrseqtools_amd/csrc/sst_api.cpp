@@ -206,7 +206,7 @@ struct sst_result {
   // the step from the peaks (sst_step_rows_device): its pass writes the dense
   // result in query order and produces its own queries (n from the header)
   bool rows_pass = false;
-  DevBuf rows_su, rows_ob, rows_side, rows_tot, rows_chunk, rows_ctl, rows_big, rows_ans, rows_aq;
+  DevBuf rows_su, rows_ob, rows_side, rows_tot, rows_chunk, rows_ctl, rows_big, rows_redo, rows_ans, rows_aq;
   std::vector<int8_t> h_status;
   std::vector<uint64_t> h_count, h_offset;
   std::vector<uint8_t> h_payload;
@@ -832,7 +832,7 @@ constexpr uint32_t kLBHashCap0 = 1u << 16;       // length bound: memo masses pe
 void free_result_bufs(sst_result* r) {
   for (DevBuf* b : {&r->status, &r->hits, &r->dense, &r->payload, &r->ctl, &r->lists, &r->wave_stats, &r->work,
                     &r->work_count, &r->tally, &r->wg_tally, &r->dhits, &r->hdr, &r->agg, &r->refs, &r->stage, &r->count,
-                    &r->offset, &r->rows_su, &r->rows_ob, &r->rows_side, &r->rows_tot, &r->rows_chunk, &r->rows_ctl, &r->rows_big, &r->rows_ans, &r->rows_aq,
+                    &r->offset, &r->rows_su, &r->rows_ob, &r->rows_side, &r->rows_tot, &r->rows_chunk, &r->rows_ctl, &r->rows_big, &r->rows_redo, &r->rows_ans, &r->rows_aq,
                     &r->lb_caps, &r->lb_capz, &r->lb_never})
     b->release();
   if (r->hdr_host) (void)hipHostFree(r->hdr_host);
@@ -1547,7 +1547,7 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, (uint64_t)16 * r->cap_n + (1u << 20))) ||
       !r->rows_su.ensure(std::max<size_t>(1, 4 * P) * 8) || !r->rows_ob.ensure(std::max<size_t>(1, 4 * P) * 8) ||
       !r->rows_side.ensure(2 * S * 4) || !r->rows_tot.ensure(3 * S * 4) || !r->rows_chunk.ensure(2 * 3 * NC * 8 + 4 * 16 * 8) ||
-      !r->rows_big.ensure(S * 4) || !r->rows_ctl.ensure(64) ||
+      !r->rows_big.ensure(S * 4) || !r->rows_redo.ensure(S * 4) || !r->rows_ctl.ensure(64) ||
       !r->rows_ans.ensure(std::max<size_t>(1, 2 * kRowsAnsPerPeak * P) * 8) || !r->rows_aq.ensure(2 * S * 4))
     return bail(fail(c, SST_E_NOMEM, "device allocation failed (rows step)"));
   if (fresh) {
@@ -1602,6 +1602,7 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   a.done = (uint32_t*)((char*)r->rows_ctl.p + 40);
   a.tickets = (uint32_t*)((char*)r->rows_ctl.p + 48);
   a.big = (uint32_t*)r->rows_big.p;
+  a.redo = (uint32_t*)r->rows_redo.p;
   a.cap_queries = (uint64_t)r->cap_n;
   a.cap_bytes = r->dense.bytes;
   a.status = (int8_t*)r->status.p;

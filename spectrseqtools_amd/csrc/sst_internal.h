@@ -460,7 +460,7 @@ constexpr int kRowsMaxSide = 2048;    // rows per side (two breakages per side a
 constexpr int kRowsWaveMaxPeaks = 160;  // spectra up to this many peaks: one wave each (k_rows_*_w)
 // answer slots per peak and side of the rows step's count pass (config 3:
 // 10 queries per peak over both sides)
-constexpr int kRowsAnsPerPeak = 12;
+constexpr int kRowsAnsPerPeak = 24;
 struct RowsArgs {
   const double* obs;          // [n_peaks] sorted within each spectrum
   const int64_t* peak_off;    // [n_spec + 1]
@@ -493,8 +493,9 @@ struct RowsArgs {
   uint64_t* ctl;              // [4] totals
   uint32_t* err;
   uint32_t* done;
-  uint32_t* tickets;          // [3]: [2] spectra listed in `big` ([0], [1] spare)
+  uint32_t* tickets;          // [3]: [2] spectra listed in `big`, [1] in `redo` ([0] spare)
   uint32_t* big;              // [n_spec] spectra over kRowsWaveMaxPeaks peaks (the block kernels')
+  uint32_t* redo;             // [n_spec] the wave kernels' spectra with a side past its answer slots (tickets[1])
   uint64_t cap_queries, cap_bytes;
   int8_t* status;
   uint4* hits;

@@ -417,12 +417,16 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_scan(RowsArgs a) {
 __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) {
   extern __shared__ uint32_t dyn[];
   __shared__ SpecLds L;
-  const uint32_t n_big = a.tickets[2];
+  // the spectra over kWP peaks (both sides from the rows the workgroup count
+  // left in scratch) and the wave kernels' spectra with a side past its answer
+  // slots (that side from its scratch rows, the other's stored answers)
+  const uint32_t n_big = a.tickets[2], n_all = n_big + a.tickets[1];
   PairImg img;
-  if (n_big) stage_img(t, dyn, img);
+  if (n_all) stage_img(t, dyn, img);
   const bool room = !(*(volatile uint32_t*)a.err & 4u);
-  for (uint32_t i = blockIdx.x; i < n_big && room; i += gridDim.x) {
-    const int64_t g = a.big[i];
+  for (uint32_t i = blockIdx.x; i < n_all && room; i += gridDim.x) {
+    const bool redo = i >= n_big;
+    const int64_t g = redo ? a.redo[i - n_big] : a.big[i];
     if (a.peak_off[g + 1] - a.peak_off[g] > kRowsMaxPeaks) continue;
     // its offsets: its chunk's plus the chunk's earlier spectra's totals
     __shared__ unsigned long long s_off[3];
@@ -435,23 +439,39 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
     __syncthreads();
     uint64_t qb = s_off[0], hb = s_off[1], bb = s_off[2];
     __syncthreads();
+    const int64_t P = a.peak_off[g + 1] - a.peak_off[g];
     for (int sd = 0; sd < 2; ++sd) {
       const uint32_t n = a.side_rows[2 * g + sd];
-      const double* rs = a.rows_su + 4 * a.peak_off[g] + (sd ? 2 * (a.peak_off[g + 1] - a.peak_off[g]) : 0);
-      const double* ro = a.rows_ob + 4 * a.peak_off[g] + (sd ? 2 * (a.peak_off[g + 1] - a.peak_off[g]) : 0);
-      for (uint32_t r = threadIdx.x; r < n; r += blockDim.x) {
-        L.su[r] = rs[r];
-        L.ob[r] = ro[r];
+      const bool stored = redo && a.ans_q[2 * g + sd] != 0xFFFFFFFFu;  // the count pass's answers, in query order
+      const uint64_t* ans = a.ans + (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)a.peak_off[g] + (uint64_t)sd * P);
+      uint32_t Q;
+      if (stored) {
+        Q = a.ans_q[2 * g + sd];
+      } else {
+        const double* rs = a.rows_su + 4 * a.peak_off[g] + (sd ? 2 * P : 0);
+        const double* ro = a.rows_ob + 4 * a.peak_off[g] + (sd ? 2 * P : 0);
+        for (uint32_t r = threadIdx.x; r < n; r += blockDim.x) {
+          L.su[r] = rs[r];
+          L.ob[r] = ro[r];
+        }
+        __syncthreads();
+        Q = side_pairs(L, n, a.max_weight);
       }
-      __syncthreads();
-      const uint32_t Q = side_pairs(L, n, a.max_weight);
       for (uint32_t q0 = 0; q0 < Q; q0 += blockDim.x) {
         const uint32_t q = q0 + threadIdx.x;
         QAns r{SST_NONE, 0, 0, 0};
         if (q < Q) {
-          uint32_t s, e;
-          pair_of(L, n, q, s, e);
-          r = answer(L, img, a, s, e);
+          if (stored) {
+            const uint64_t v = ans[q];
+            r.status = (int8_t)(uint8_t)v;
+            r.cnt = (uint32_t)(v >> 8) & 0xFFFFu;
+            r.first = (uint32_t)(v >> 24) & 0xFFFFu;
+            r.bytes = (uint32_t)(v >> 40);
+          } else {
+            uint32_t s, e;
+            pair_of(L, n, q, s, e);
+            r = answer(L, img, a, s, e);
+          }
           a.status[qb + q] = r.status;
         }
         const bool hit = r.status == SST_SOME || r.status == SST_OVERFLOW;
@@ -515,7 +535,7 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
 // One wave per spectrum (spectra of <= kRowsWaveMaxPeaks peaks, i.e. every
 // spectrum of a 10..20-mer): a spectrum's phases are short dependent chains
 // (bitset loads, LDS binary searches, pair-list walks), so many spectra must
-// be in flight per CU -- four waves per workgroup, several workgroups per CU,
+// be in flight per CU -- one wave per workgroup, many workgroups per CU,
 // each wave its own spectrum, wave-level prefix sums (no barriers).  The
 // pair list is read through L2 (40 KB, resident); the block kernels above
 // take the larger spectra.
@@ -523,7 +543,8 @@ namespace {
 
 constexpr int kWP = kRowsWaveMaxPeaks;
 constexpr int kWS = 2 * kRowsWaveMaxPeaks;  // rows per side: two breakages per side
-constexpr int kWavesPerWG = 4;
+constexpr int kWavesPerWG = 1;  // one wave per workgroup: a finished spectrum frees its slot at once
+                                 // (4-wave workgroups held theirs until the slowest of the four: 168 vs 140 us)
 
 struct WaveLds {
   double obs[kWP];
@@ -816,6 +837,8 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
       const uint64_t base = (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P);
       const bool fits = Q <= (uint32_t)kRowsAnsPerPeak * P;
       if (lane == 0) a.ans_q[2 * g + sd] = fits ? Q : 0xFFFFFFFFu;
+      // a side past its slots: the workgroup emit answers it again (listed once per spectrum)
+      if (!fits && lane == 0 && (sd == 0 || a.ans_q[2 * g] != 0xFFFFFFFFu)) a.redo[atomicAdd(&a.tickets[1], 1u)] = (uint32_t)g;
       if (!fits) {
         double* rs = a.rows_su + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
         double* ro = a.rows_ob + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
@@ -876,16 +899,11 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
 }
 
 __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, RowsArgs a) {
-  __shared__ WaveLds Ls[kWavesPerWG];
-  WaveLds& L = Ls[threadIdx.x >> 6];
+  // the answers the count pass stored, streamed back in query order (a
+  // spectrum with a side past its slots, or over kWP peaks, is the workgroup
+  // emit's): no LDS, so the waves per CU are set by registers alone
   const int lane = threadIdx.x & 63;
-#ifndef SST_ROWS_IMG_LDS  // records through L2: 16 waves per CU (staged in LDS: 8, measured slower)
   const PairImg img = global_img(t);
-#else
-  extern __shared__ uint32_t dyn[];
-  PairImg img;
-  stage_img(t, dyn, img);
-#endif
   const bool room = !(*(volatile uint32_t*)a.err & 4u);
   const int64_t w = (int64_t)blockIdx.x * kWavesPerWG + (threadIdx.x >> 6);
   const int64_t g_end = (w + 1) * a.chunk < a.n_spec ? (w + 1) * a.chunk : a.n_spec;
@@ -896,81 +914,30 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, R
     off[2] = a.chunk_off[3 * w + 2];
   }
   for (int64_t g = w * a.chunk; g < g_end && room; ++g) {
-    RPROF_T(e0);
-    RPROF_T(e1);
-    RPROF_ADD(6, e1 - e0);
     const int64_t p0 = a.peak_off[g];
     const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
+    const uint32_t Q0 = a.ans_q[2 * g], Q1 = a.ans_q[2 * g + 1];
     uint64_t qb = off[0], hb = off[1], bb = off[2];
     // the next spectrum's offsets (this one's totals: the count kernels')
     off[0] += a.totals[3 * g];
     off[1] += a.totals[3 * g + 1];
     off[2] += a.totals[3 * g + 2];
-    if (P > (uint32_t)kWP) continue;  // the workgroup kernel's
+    if (P > (uint32_t)kWP || Q0 == 0xFFFFFFFFu || Q1 == 0xFFFFFFFFu) continue;  // the workgroup kernel's
     for (int sd = 0; sd < 2; ++sd) {
-      uint32_t Q = a.ans_q[2 * g + sd];
-      const bool stored = Q != 0xFFFFFFFFu;  // the count pass's answers, in query order
-      const uint64_t base = (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P);
-      const uint32_t n = a.side_rows[2 * g + sd];
-      if (!stored) {  // too many queries for the side's slots: the rows back from scratch, answered again
-        const double* rs = a.rows_su + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
-        const double* ro = a.rows_ob + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
-        for (uint32_t r = lane; r < n; r += 64) {
-          L.su[r] = rs[r];
-          L.ob[r] = ro[r];
-        }
-        wsync();
-        uint32_t ss = n ? n - 1 : 0;
-        for (uint32_t r = lane; r + 1 < n; r += 64)
-          if (!(L.su[n - 1] - L.su[r] > a.max_weight)) ss = r < ss ? r : ss;
-        ss = wave_min(ss);
-        uint32_t carry = 0;
-        for (uint32_t r0 = 0; r0 < n; r0 += 64) {
-          const uint32_t r = r0 + lane;
-          uint32_t c = 0;
-          if (r + 1 < n) {
-            if (r < ss) {
-              uint32_t lo = r + 1, hi = n - 1;
-              const double sr = L.su[r];
-              while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (L.su[mid] - sr > a.max_weight) hi = mid;
-                else lo = mid + 1;
-              }
-              c = lo - r - 1;
-            } else if (r == ss) {
-              c = n - 1 - r;
-            } else {
-              c = 1;
-            }
-          }
-          uint32_t tot;
-          const uint32_t ex = wave_excl(c, tot);
-          if (r < n) L.qoff[r] = carry + ex;
-          carry += tot;
-        }
-        if (lane == 0) {
-          L.qoff[n] = carry;
-          L.sstar = ss;
-        }
-        wsync();
-        Q = carry;
-      }
+      const uint32_t Q = sd ? Q1 : Q0;
+      const uint64_t* ans = a.ans + (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P);
+      // one window ahead: its answers are in flight while this one is emitted
+      uint64_t nv = lane < (int)Q ? __builtin_nontemporal_load(&ans[lane]) : 0ull;
       for (uint32_t q0 = 0; q0 < Q; q0 += 64) {
         const uint32_t q = q0 + lane;
+        const uint64_t v = nv;
+        if (q0 + 64 < Q) nv = q + 64 < Q ? __builtin_nontemporal_load(&ans[q + 64]) : 0ull;
         QAns r{SST_NONE, 0, 0, 0};
         if (q < Q) {
-          if (stored) {
-            const uint64_t v = __builtin_nontemporal_load(&a.ans[base + q]);
-            r.status = (int8_t)(uint8_t)v;
-            r.cnt = (uint32_t)(v >> 8) & 0xFFFFu;
-            r.first = (uint32_t)(v >> 24) & 0xFFFFu;
-            r.bytes = (uint32_t)(v >> 40);
-          } else {
-            uint32_t s, e;
-            wave_pair(L, n, q, s, e);
-            r = wave_answer(L, t, a, s, e);
-          }
+          r.status = (int8_t)(uint8_t)v;
+          r.cnt = (uint32_t)(v >> 8) & 0xFFFFu;
+          r.first = (uint32_t)(v >> 24) & 0xFFFFu;
+          r.bytes = (uint32_t)(v >> 40);
           a.status[qb + q] = r.status;
         }
         const bool hit = r.status == SST_SOME || r.status == SST_OVERFLOW;
@@ -978,12 +945,12 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, R
         const uint32_t xh = wave_excl(hit ? 1u : 0u, th);
         const uint32_t xb = wave_excl(r.status == SST_SOME ? r.bytes + 2u : 0u, tb);
         if (hit) {
-          const uint64_t off = bb + xb;
-          const uint64_t word = r.status == SST_SOME ? off : (uint64_t)r.cnt;
+          const uint64_t o = bb + xb;
+          const uint64_t word = r.status == SST_SOME ? o : (uint64_t)r.cnt;
           a.hits[hb + xh] = make_uint4((uint32_t)(qb + q), r.cnt, (uint32_t)word, (uint32_t)(word >> 32));
           a.refs[hb + xh] = (uint16_t)(r.first | (r.status == SST_OVERFLOW ? 0x8000u : 0u));
           if (r.status == SST_SOME) {
-            uint8_t* dst = a.dense + off;
+            uint8_t* dst = a.dense + o;
             for (uint32_t k = r.first; k < r.first + r.cnt; ++k) {
               const uint32_t rec = img.recs[k];
               *(u32_unal*)dst = rec;
@@ -995,10 +962,7 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, R
         bb += tb;
       }
       qb += Q;
-      wsync();
     }
-    RPROF_T(e2);
-    RPROF_ADD(7, e2 - e1);
   }
 }
 

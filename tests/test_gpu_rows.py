@@ -120,6 +120,8 @@ def test_rows_step_edge_spectra(dp):
             o = np.concatenate([o, rng.uniform(15000.0, 21000.0, 3)])  # heavy peaks (near the table's end)
         elif s % 10 == 4:  # over 160 peaks: the workgroup-per-spectrum kernels
             o = np.concatenate([o] + [b.observed[b.offsets[t]:b.offsets[t + 1]] for t in (s + 1, s + 2)])
+        elif s % 10 == 6:  # every peak within max_weight of the others: more pairs than a side's answer slots
+            o = rng.uniform(3000.0, 3250.0, 40)
         o = np.sort(o)
         if s % 10 == 5:
             o = np.concatenate([o, o[:3]])[rng.permutation(len(o) + 3)]  # unsorted, with ties: ranked on the device
