@@ -162,6 +162,12 @@ def load_library(path=LIB_PATH):
         raise ImportError(
             f"{path} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()' "
             "or make -C spectrseqtools_amd/csrc)")
+    if path == LIB_PATH and not os.environ.get("SST_LIBRARY"):
+        from . import build_record
+
+        why = build_record.check(path)
+        if why:
+            raise ImportError(f"{path}: {why}; rebuild it (make -C spectrseqtools_amd/csrc)")
     _share_hip_runtime_with_torch()
     lib = ctypes.CDLL(path)
     lib.sst_device_count.restype = _I

@@ -73,3 +73,20 @@ def test_budget_conversion():
     assert _native._budget(-np.inf) == 0
     arr, s = _native._mods([1, np.inf, 0], 3)
     assert arr.tolist() == [1, -1, 0] and s == 0
+
+
+def test_library_matches_its_build_record():
+    """The shipped libsstgpu.so is the one built from this tree's sources
+    (spectrseqtools_amd/build_record.json: the Makefile writes it after every
+    link; the loader refuses a library or sources that no longer match)."""
+    import json
+    import os
+
+    from spectrseqtools_amd import build_record
+
+    if not os.path.exists(build_record.LIB):
+        pytest.skip("libsstgpu.so not built")
+    assert build_record.check() is None, build_record.check()
+    rec = json.load(open(build_record.RECORD))
+    assert rec["arch"] == "gfx950" and rec["library"]["bytes"] == os.path.getsize(build_record.LIB)
+    assert set(rec["sources"]) >= {"spectrseqtools_amd/csrc/sst_kernels.hip", "include/sst.h"}
