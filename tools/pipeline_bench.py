@@ -144,6 +144,8 @@ def main():
                          "memoised DFS visits up to ~10^7 nodes per spectrum on rich skeleton alphabets")
     ap.add_argument("--length-engine", default="frontier", choices=("frontier", "replay"),
                     help="stage 5: the first-visit frontier (default) or the round-4 per-spectrum DFS replay")
+    ap.add_argument("--frontier-workspace-gb", type=float, default=0.0,
+                    help="stage 5: the frontier's device workspace per call in GiB (0: its default, min(96, free/2))")
     ap.add_argument("--cpu-baseline-s", type=float, default=20.0,
                     help="stage 5's CPU baseline: the oracle's table rebuild + both length bounds per spectrum on "
                          "the host's cores, for about this many seconds (0: skip)")
@@ -363,7 +365,8 @@ def main():
         n_len = len(max_len) if args.length_spectra <= 0 else min(args.length_spectra, len(max_len))
         ln = pd.length_device(dp, sk, db.alpha_dev, su_seq, batch.seq_mass,
                               spectra=None if n_len == len(max_len) else np.arange(n_len),
-                              soft_nodes=args.length_soft_nodes, engine=args.length_engine)
+                              soft_nodes=args.length_soft_nodes, engine=args.length_engine,
+                              frontier_workspace=int(args.frontier_workspace_gb * (1 << 30)))
         barrier()
         stages["length"] = {"s": tmax(time.perf_counter() - t0), "bounds_spectra": n_len,
                             "bounds_sample": n_len < len(max_len), "reach_batches": ln.reach_batches,
