@@ -9,7 +9,7 @@ rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/${TAG}_t.log; [ $rc -ne 0 ] && ex
 for r in 1 2; do
   for v in main "$@"; do
     if [ $v = main ]; then unset SST_LIBRARY; else export SST_LIBRARY=$PWD/build/ab/$v.so; fi
-    timeout -k 10 300 python -u tools/pipeline_bench.py --spectra $N --warmup-spectra 16 --cpu-baseline-s 0 > gpurun_out/${TAG}_${v}_$r.json 2> gpurun_out/${TAG}_${v}_$r.err
+    timeout -k 10 300 python -u tools/pipeline_bench.py --spectra $N --warmup-spectra 16 --cpu-baseline-s 0 ${AB_ARGS:-} > gpurun_out/${TAG}_${v}_$r.json 2> gpurun_out/${TAG}_${v}_$r.err
     rc=$?; [ $rc -ne 0 ] && { echo "$v rc=$rc"; tail -3 gpurun_out/${TAG}_${v}_$r.err; exit $rc; }
     python3 - gpurun_out/${TAG}_${v}_$r.json $v <<'PY'
 import json, sys
