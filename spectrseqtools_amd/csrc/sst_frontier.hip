@@ -100,6 +100,28 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
+// the lane owning item q of a wave's items laid out by lane (incl: the
+// inclusive count up to each lane): the first lane whose count exceeds q
+__device__ __forceinline__ int wave_owner(uint32_t incl, uint32_t q) {
+  int g = 0;
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1)
+    if (__shfl(incl, g + s - 1, 64) <= q) g += s;
+  return g;
+}
+
+// the t-th highest set bit (t from 0) of the 128-bit mask (h1:h0)
+__device__ __forceinline__ int mask_select_top(uint64_t h1, uint64_t h0, uint32_t t) {
+  const uint32_t c1 = (uint32_t)__builtin_popcountll(h1);
+  const uint64_t x = t < c1 ? h1 : h0;
+  const uint32_t need = (t < c1 ? t : t - c1) + 1u;
+  int b = 0;
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1)
+    if ((uint32_t)__builtin_popcountll(x >> (b + s)) >= need) b += s;
+  return (t < c1 ? 64 : 0) + b;
+}
+
 // find-or-insert (band-tagged; a slot whose tag is not this band's is free)
 __device__ __forceinline__ uint32_t group_get(FGroup* T, uint32_t mask, uint64_t key, bool& fresh) {
   const uint32_t tag = ftag(key);
@@ -388,44 +410,54 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
       if (lane == 0) set_overflow(a, 1);
       return;
     }
-    if (!act) continue;
-    const uint32_t id0 = wbase + incl - n, c0 = cwbase + cincl - nc;
-    if (n) atomicAdd(&a.node_cnt[jj], n);
-    FGRec r;
-    r.base = id0;
-    r.j = jj;
-    r.m = m;
-    r.cbase = c0;
-    r.lo = (uint8_t)lo;
-    r.hv = (uint8_t)hv;
-    r.nc = (uint8_t)nc;
-    r.pad = 0;
-    GR[gi] = r;
-    for (uint32_t x = 0; x < n; ++x) a.node_group[id0 - band0 + x] = gi;
-    // the left candidates, highest rank first
-    uint32_t t = 0;
-    for (int half = 1; half >= 0; --half) {
-      uint64_t mk = half ? mk1 : mk0;
-      while (mk) {
-        const int k = 64 * half + 63 - __builtin_clzll(mk);
-        mk &= ~(1ull << (k & 63));
-        const uint32_t cs = cand_find<KW>(Cb, a.cmask, fkey(ftagb(a, (uint32_t)band), jj, m, (uint32_t)k));
-        if (cs == UINT32_MAX) {
-          set_overflow(a, 16);  // cannot happen: the mask bit follows the insertion
-          continue;
-        }
-        const FCand<KW>& e = Cb[cs];
-        const uint32_t par = e.parent, id = id0 + (uint32_t)(k - lo);
-        if (par & kRootBit) a.root_node[par & ~kRootBit] = id;
-        else a.lchild[par] = id;
-        FCRec<KW> cr;
-#pragma unroll
-        for (int w = 0; w < KW; ++w) cr.fk[w] = e.fk[w];
-        cr.A = e.A;
-        cr.B = e.B;
-        cr.rank = (uint8_t)k;
-        CR[c0 + t++] = cr;
+    const uint32_t id0 = wbase + incl - n;
+    if (act) {
+      if (n) atomicAdd(&a.node_cnt[jj], n);
+      FGRec r;
+      r.base = id0;
+      r.j = jj;
+      r.m = m;
+      r.cbase = cwbase + cincl - nc;
+      r.lo = (uint8_t)lo;
+      r.hv = (uint8_t)hv;
+      r.nc = (uint8_t)nc;
+      r.pad = 0;
+      GR[gi] = r;
+    }
+    // node -> group, the wave's nodes 64 at a time (ids are the wave's
+    // items in lane order: coalesced, no lane waits for the largest group)
+    for (uint32_t q0 = 0; q0 < total; q0 += 64u) {
+      const uint32_t q = q0 + (uint32_t)lane;
+      const int g = wave_owner(incl, q);
+      if (q < total) a.node_group[wbase - band0 + q] = base + (uint32_t)g;
+    }
+    // the left candidates, 64 at a time: item p is its group's (p - first)-th
+    // highest rank, copied out of the hash with its parent's child link
+    const uint32_t idlo = id0 - (uint32_t)lo, cfirst = cincl - nc;
+    for (uint32_t p0 = 0; p0 < ctotal; p0 += 64u) {
+      const uint32_t p = p0 + (uint32_t)lane;
+      const int g = wave_owner(cincl, p);
+      const uint64_t h0 = __shfl(mk0, g, 64), h1 = __shfl(mk1, g, 64);
+      const uint32_t gj = __shfl(jj, g, 64), gm = __shfl(m, g, 64), gidlo = __shfl(idlo, g, 64);
+      const uint32_t gfirst = __shfl(cfirst, g, 64);
+      if (p >= ctotal) continue;
+      const int k = mask_select_top(h1, h0, p - gfirst);
+      const uint32_t cs = cand_find<KW>(Cb, a.cmask, fkey(ftagb(a, (uint32_t)band), gj, gm, (uint32_t)k));
+      if (cs == UINT32_MAX) {
+        set_overflow(a, 16);  // cannot happen: the mask bit follows the insertion
+        continue;
       }
+      const FCand<KW>& e = Cb[cs];
+      const uint32_t par = e.parent, id = gidlo + (uint32_t)k;
+      if (par & kRootBit) a.root_node[par & ~kRootBit] = id;
+      else a.lchild[par] = id;
+      FCRec<KW> cr;
+#pragma unroll
+      for (int w = 0; w < KW; ++w) cr.fk[w] = e.fk[w];
+      cr.A = e.A;
+      cr.B = e.B;
+      cr.rank = (uint8_t)k;
+      CR[cwbase + p] = cr;
     }
   }
 }
