@@ -1002,18 +1002,28 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
         need_u = 4 * K_u * words_u + 32 * words_u
         by_u = np.argsort(inv, kind="stable")
         u_first = np.concatenate([[0], np.cumsum(np.bincount(inv, minlength=U))])
-        u0 = 0
+        batches, u0 = [], 0
         while u0 < U:
             u1, tot = u0, 0
             while u1 < U and (u1 == u0 or tot + need_u[u1] <= reach_budget_bytes):
                 tot += int(need_u[u1])
                 u1 += 1
+            batches.append((u0, u1))
+            u0 = u1
+        # one row-bitset and one lowest-rank buffer for every batch, sized to
+        # the largest (a fresh allocation of tens of GB per batch, and its
+        # release, idled the GPU for 0.1 s each)
+        kw_b = [int((K_u[b0:b1] * words_u[b0:b1]).sum()) for b0, b1 in batches]
+        lw_b = [int(32 * words_u[b0:b1].sum()) for b0, b1 in batches]
+        bits_all = torch.empty(max([1] + kw_b), dtype=torch.int32, device=dev)
+        lr_all = torch.empty(max([1] + lw_b), dtype=torch.uint8, device=dev)
+        for bi, (u0, u1) in enumerate(batches):
             nu = u1 - u0
             wb = words_u[u0:u1]
             off_u = np.concatenate([[0], np.cumsum(K_u[u0:u1] * wb)[:-1]]).astype(np.int64)
             lr_off = np.concatenate([[0], np.cumsum(32 * wb)[:-1]]).astype(np.int64)
-            bits = torch.empty(max(1, int((K_u[u0:u1] * wb).sum())), dtype=torch.int32, device=dev)
-            lr = torch.empty(max(1, int(32 * wb.sum())), dtype=torch.uint8, device=dev)
+            bits = bits_all[:max(1, kw_b[bi])]
+            lr = lr_all[:max(1, lw_b[bi])]
             alu_t = torch.as_tensor(uniq[u0:u1].view(np.int64), device=dev).contiguous()
             wu_t = torch.as_tensor(wb, device=dev)
             ou_t = torch.as_tensor(off_u, device=dev)
@@ -1024,9 +1034,8 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
             eng.check(L.sst_reach_lowest_device(h, alu_t.data_ptr(), wu_t.data_ptr(), ou_t.data_ptr(), nu,
                                                 bits.data_ptr(), lo_u_t.data_ptr(), lr.data_ptr()),
                       "sst_reach_lowest_device")
-            eng.synchronize()
-            del bits
-            torch.cuda.empty_cache()
+            if _PROGRESS:
+                eng.synchronize()
             t_reach = time.perf_counter() - t_batch
             lu_src = by_u[u_first[u0]:u_first[u1]]
             members = sel[lu_src]
@@ -1064,9 +1073,9 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
             if _PROGRESS:
                 print(f"[length] frontier batch {stats['batches']}: {n} spectra, {nu} alphabets, reach "
                       f"{t_reach:.3f}s, batch {time.perf_counter() - t_batch:.3f}s: {fd}", file=sys.stderr, flush=True)
-            del lr
             stats["batches"] += 1
-            u0 = u1
+        del bits_all, lr_all, bits, lr
+        torch.cuda.empty_cache()
 
     if engine == "frontier":
         frontier_pass(sel)
