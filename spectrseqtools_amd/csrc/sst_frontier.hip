@@ -411,8 +411,26 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
       return;
     }
     const uint32_t id0 = wbase + incl - n;
+    {  // per-query node counts: one atomic per run of one query's groups in the wave
+      // (a chunk of few queries otherwise sends every group's add to the same word)
+      const uint32_t jprev = __shfl_up(jj, 1, 64), jnext = __shfl_down(jj, 1, 64);  // every lane shuffles
+      const bool head = lane == 0 || jprev != jj;
+      const bool tail = lane == 63 || jnext != jj;
+      int seg = head ? lane : 0;
+      uint32_t run = n;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int ps = __shfl_up(seg, d, 64);
+        if (lane >= d && ps > seg) seg = ps;
+      }
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(run, d, 64);
+        if (lane - d >= seg) run += y;
+      }
+      if (tail && run) atomicAdd(&a.node_cnt[jj], run);
+    }
     if (act) {
-      if (n) atomicAdd(&a.node_cnt[jj], n);
       FGRec r;
       r.base = id0;
       r.j = jj;
