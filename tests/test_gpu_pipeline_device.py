@@ -242,6 +242,17 @@ def _mirror_run(dp, obs):
     frags, expl = pred.filter_by_explanation(f)
     sb = SkeletonBuilder(explanations=expl, dp_table=dp)
     out, sks = {"filter_masses": [m.mass for m in dp.masses], "filter_kept": frags.get_column("index").to_list()}, {}
+    # SU differences the final dict's queries hold more than once at different
+    # thresholds (the last writer's threshold is the one the walk must use)
+    cols = frags.to_dict()
+    su_f, ob_f = np.asarray(cols["standard_unit_mass"], np.float64), np.asarray(cols["observed_mass"], np.float64)
+    thr_of = {}
+    for side in ("START", "END"):
+        m = np.array([side in b for b in cols["breakage"]], bool)
+        keys, _, thr = pred._side_queries(su_f[m], ob_f[m])
+        for k_, t_ in zip(keys, thr.tolist()):
+            thr_of.setdefault(k_, set()).add(t_)
+    out["dup_thr_keys"] = sum(len(v) > 1 for v in thr_of.values())
     for side in ("START", "END"):
         sub = frags.filter_mask([side in b for b in frags.get_column("breakage").to_list()])
         sk, fs = sb._predict_skeleton(Frame(sub.to_dict()), [set() for _ in range(dp.seq.max_len)])
@@ -262,7 +273,8 @@ def _mirror_run(dp, obs):
     return out
 
 
-@pytest.mark.parametrize("variant", ["full_ladders", "short_fragments_missing", "low_modification_rate"])
+@pytest.mark.parametrize("variant", ["full_ladders", "short_fragments_missing", "low_modification_rate",
+                                     "noise_free", "noise_free_exact"])
 def test_device_skeleton_and_length_vs_mirror(engine, variant):
     """Stages 4-5 on the device over synthetic spectra against the
     per-spectrum host mirrors in this process (same interpreter, same hash
@@ -272,7 +284,12 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
     and re-queries against older bins (the masked explain, suspended lanes).
     At --modification_rate 0.05 (cli.py:35) the budgets bind on pair windows
     (max_modifications and caps < 2): every stage runs its spectra in exact
-    mode (sst_exact_io: the exact masked replay answers their windows)."""
+    mode (sst_exact_io: the exact masked replay answers their windows).
+    Noise-free spectra repeat SU differences exactly at different observed
+    masses, so the final dict's last writer often carries another threshold
+    than the bin the walk queries (skeleton_building.py:429-430): the walk
+    answers pair-class windows at the dict's threshold, and re-queries
+    exact-mode ones instead of taking stage 3's answer."""
     from spectrseqtools_amd import _native, pipeline, pipeline_device as PD
     from spectrseqtools_amd.mass_explanation import MASS_NAMES
     from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
@@ -280,12 +297,15 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
     from spectrseqtools_amd.synthetic import make_spectra
 
     n = 48
-    mod_rate = 0.05 if variant == "low_modification_rate" else 0.5
-    b = make_spectra(n, seed={"full_ladders": 41, "short_fragments_missing": 43}.get(variant, 47), len_range=(6, 14),
-                     mod_rate=0.3 if variant == "low_modification_rate" else 0.5)
+    exact = variant in ("low_modification_rate", "noise_free_exact")
+    clean = variant.startswith("noise_free")
+    mod_rate = 0.05 if exact else 0.5
+    b = make_spectra(n, seed={"full_ladders": 41, "short_fragments_missing": 43, "noise_free": 53,
+                              "noise_free_exact": 59}.get(variant, 47), len_range=(6, 14),
+                     mod_rate=0.3 if exact else 0.5, ppm=0.0 if clean else 3.0, noise_frac=0.0 if clean else 0.2)
     spec = np.repeat(np.arange(n), np.diff(b.offsets))
     keep = np.ones(len(b.observed), bool)
-    if variant != "full_ladders":
+    if variant in ("short_fragments_missing", "low_modification_rate"):
         keep = (spec % 3 == 0) | (b.observed > 1300.0)
     obs = b.observed[keep]
     offsets = np.concatenate([[0], np.cumsum(np.bincount(spec[keep], minlength=n))])
@@ -297,7 +317,7 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
     dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
                                  precision=TOLERANCE, seq=seq, engine=engine)
     max_len = pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:]))
-    if variant == "low_modification_rate":
+    if exact:
         assert not PD.budgets_pair_ok(dp, max_len).any()
     rows = PD.classify_device(dp, obs, offsets, su_seq, bd)
     fx = PD.fixpoint_device(dp, rows, max_len)
@@ -305,7 +325,7 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
     sk = PD.skeleton_device(dp, rows, fx.alpha, max_len, bins=bins)
     ln = PD.length_device(dp, sk, bins.alpha_dev, su_seq, b.seq_mass)
     names = [None] + [MASS_NAMES[m.mass][0] for m in dp.masses[1:]]
-    n_len = n_err = 0
+    n_len = n_err = n_dup = 0
     for g in range(n):
         want = _mirror_outcome(obs[offsets[g]:offsets[g + 1]], su_seq[g], b.seq_mass[g], max_len[g], engine,
                                mod_rate)
@@ -314,6 +334,7 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
         o4 = int(rows.peak_off[g].item()) * 4
         al = rows.alive[o4:o4 + int(rows.rows[g].item())].cpu().numpy().astype(bool)
         assert np.flatnonzero(al).tolist() == want["filter_kept"], g
+        n_dup += want["dup_thr_keys"] > 0
         assert (sk.status[2 * g:2 * g + 2] == _native.WALK_DONE).all(), (g, sk.status[2 * g:2 * g + 2])
         got = PD.skeleton_frames(dp, rows, sk, g)
         for side in ("START", "END"):
@@ -335,7 +356,9 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
             assert got_c == want["combined"], g
             n_len += 1
     assert n_len >= n // 2
-    if variant != "full_ladders":
+    if clean:
+        assert n_dup >= n // 4, n_dup  # the scenario is present, not just allowed
+    if variant in ("short_fragments_missing", "low_modification_rate"):
         assert sk.requeries > 0 or bins.deferred["queries"] > 0
         import torch
 
