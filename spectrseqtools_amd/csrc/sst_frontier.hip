@@ -32,7 +32,7 @@
 //   cands     one per left edge (child (query, mass, rank)): hash ring, entry
 //             {key, parent node, child budgets A B, the child's FV key}
 //   nodes     ids allocated per group (ranks lo..hv ascending): flags, left
-//             child id, lower / upper value
+//             child id, lower / upper value packed in 16 bits
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -628,15 +628,15 @@ __global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
             set_overflow(a, 32);
             c = x;
           }
-          const int l = (int)a.vlo[c] + 1;
+          const uint32_t p = a.val[c];
+          const int l = (int)(p & 0xFFu) + 1;
           cl = l > 255 ? 255 : l;
-          ch = (int)a.vhi[c] + 1;  // -1 + 1 = 0 (the reference's default feeds the max)
+          ch = (int)(p >> 8);  // upper + 1: -1 + 1 = 0 (the reference's default feeds the max)
         }
         vl = cl < vl ? cl : vl;
         vh = ch > vh ? ch : vh;
       }
-      a.vlo[x] = (uint8_t)vl;
-      a.vhi[x] = (int8_t)vh;
+      a.val[x] = (uint16_t)(vl | ((vh + 1) << 8));
       plo = vl;
       phi = vh;
     }
@@ -664,7 +664,8 @@ __global__ __launch_bounds__(256) void k_lbf_out(FrontierArgs a) {
       set_overflow(a, 32);
       return;
     }
-    const int l = a.vlo[id], h = a.vhi[id];
+    const uint32_t p = a.val[id];
+    const int l = (int)(p & 0xFFu), h = (int)(p >> 8) - 1;
     bl = l < bl ? l : bl;
     bh = h > bh ? h : bh;
   }

@@ -350,8 +350,7 @@ struct FrontierArgs {
   uint32_t* root_node;
   uint8_t* flags;
   uint32_t* lchild;
-  uint8_t* vlo;
-  int8_t* vhi;
+  uint16_t* val;  // per node: lower | (upper + 1) << 8 (one load per left child)
   uint64_t ncap;
   char* gtab;
   uint32_t gmask;
