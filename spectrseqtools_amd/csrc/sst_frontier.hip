@@ -598,48 +598,87 @@ __global__ void k_lbf_mark(FrontierArgs a, int band) {
   a.ctl->list_cnt[((uint32_t)band + (uint32_t)a.jump) & ((uint32_t)a.ring - 1u)] = 0;
 }
 
-// the memoised values of band b's nodes (mass_table.py:407-457): a lane per
-// group (its lowest rank, whose id starts the group), ranks ascending; lower
-// with 255 as "no path" (min(default, x) at the roots), upper from -1
+// the first group start (a node without kFUp) at or after x0 in [x0, s1], 64
+// flags per step
+__device__ __forceinline__ uint32_t next_group_start(const FrontierArgs& a, uint32_t x0, uint32_t s1) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t y = x0; y < s1; y += 64u) {
+    const uint32_t x = y + (uint32_t)lane;
+    const uint64_t b = __ballot(x >= s1 || !(a.flags[x] & kFUp));
+    if (b) return y + (uint32_t)__builtin_ctzll(b);
+  }
+  return s1;
+}
+
+// the memoised values of band b's nodes (mass_table.py:407-457).  Within a
+// group (ranks ascending) a node's values fold its left branch into the node
+// below's: lower = min, upper = max over the group's ranks up to it -- a
+// segmented prefix min / max over consecutive node ids.  A wave takes a range
+// of whole groups and runs it 64 nodes at a time (a lane per node: every
+// left child's value load in flight at once; the group open at a step's
+// start carried from the step before); lower with 255 as "no path" (min(default,
+// x) at the roots), upper from -1
 __global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
   if (__hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  const int lane = threadIdx.x & 63;
   const uint32_t s0 = a.band_start[band], s1 = a.band_start[band + 1];
   const uint32_t n_nodes = a.band_start[a.n_bands];  // every id below is a node of this chunk
-  const uint32_t nth = gridDim.x * blockDim.x;
-  for (uint32_t x0 = s0 + blockIdx.x * blockDim.x + threadIdx.x; x0 < s1; x0 += nth) {
-    uint8_t f = a.flags[x0];
-    if (f & kFUp) continue;  // not the lowest rank of its group
-    int plo = 255, phi = -1;
-    for (uint32_t x = x0; x < s1; ++x) {
-      if (x != x0) {
-        f = a.flags[x];
-        if (!(f & kFUp)) break;
-      }
-      int vl = 255, vh = -1;
-      if (f & kFUp) {  // (m, k - 1): the node below in this group
-        vl = plo;
-        vh = phi;
-      }
-      if (f & kFLeft) {
-        int cl = 1, ch = 1;  // a left move onto mass 0: 0 + 1
-        if (!(f & kFZero)) {
-          uint32_t c = a.lchild[x];
-          if (c >= n_nodes || c < s1) {  // a left child lies in a later band: never unset or stale
-            set_overflow(a, 32);
-            c = x;
-          }
-          const uint32_t p = a.val[c];
-          const int l = (int)(p & 0xFFu) + 1;
-          cl = l > 255 ? 255 : l;
-          ch = (int)(p >> 8);  // upper + 1: -1 + 1 = 0 (the reference's default feeds the max)
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t nn = s1 - s0;
+  const uint32_t per = ((nn + nwaves - 1u) / nwaves + 63u) & ~63u;
+  const uint64_t b0 = (uint64_t)wave * per, b1 = b0 + per;
+  if (b0 >= nn) return;
+  // whole groups: both ends moved to the next group start (the neighbours
+  // compute the same boundary)
+  const uint32_t r0 = wave ? next_group_start(a, s0 + (uint32_t)b0, s1) : s0;
+  const uint32_t r1 = b1 >= nn ? s1 : next_group_start(a, s0 + (uint32_t)b1, s1);
+  const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+  int clo = 255, chi = -1;  // the values of the group open at the step's start
+  for (uint32_t c0 = r0; c0 < r1; c0 += 64u) {
+    const uint32_t x = c0 + (uint32_t)lane;
+    const bool live = x < r1;
+    const uint8_t f = live ? a.flags[x] : (uint8_t)0;
+    int vl = 255, vh = -1;
+    if (f & kFLeft) {
+      vl = 1;  // a left move onto mass 0: 0 + 1
+      vh = 1;
+      if (!(f & kFZero)) {
+        uint32_t c = a.lchild[x];
+        if (c >= n_nodes || c < s1) {  // a left child lies in a later band: never unset or stale
+          set_overflow(a, 32);
+          c = x;
         }
-        vl = cl < vl ? cl : vl;
-        vh = ch > vh ? ch : vh;
+        const uint32_t p = a.val[c];
+        const int l = (int)(p & 0xFFu) + 1;
+        vl = l > 255 ? 255 : l;
+        vh = (int)(p >> 8);  // upper + 1: -1 + 1 = 0 (the reference's default feeds the max)
       }
-      a.val[x] = (uint16_t)(vl | ((vh + 1) << 8));
-      plo = vl;
-      phi = vh;
     }
+    // segmented inclusive min / max: a segment starts at each group's lowest rank
+    const bool head = live && !(f & kFUp);
+    int seg = head ? lane : 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int ps = __shfl_up(seg, d, 64);
+      if (lane >= d && ps > seg) seg = ps;
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int yl = __shfl_up(vl, d, 64), yh = __shfl_up(vh, d, 64);
+      if (lane - d >= seg) {
+        vl = yl < vl ? yl : vl;
+        vh = yh > vh ? yh : vh;
+      }
+    }
+    if (!(__ballot(head) & le)) {  // still in the group open at the step's start
+      vl = clo < vl ? clo : vl;
+      vh = chi > vh ? chi : vh;
+    }
+    if (live) a.val[x] = (uint16_t)(vl | ((vh + 1) << 8));
+    const int last = r1 - c0 >= 64u ? 63 : (int)(r1 - c0 - 1u);
+    clo = __shfl(vl, last, 64);
+    chi = __shfl(vh, last, 64);
   }
 }
 
