@@ -45,7 +45,8 @@ namespace {
 
 constexpr int kProbeMax = 4096;
 constexpr uint32_t kRootBit = 0x80000000u;
-constexpr uint8_t kFLeft = 1, kFUp = 2, kFZero = 4;
+constexpr uint32_t kNodeSeg = 512;  // k_lbf_nodes: ids per ticket
+constexpr uint8_t kFLeft = 1, kFUp = 2, kFZero = 4, kFCand = 8;  // kFCand: k_lbf_groups' mark, until k_lbf_nodes
 
 struct alignas(32) FGroup {
   uint64_t key;
@@ -447,7 +448,14 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
     for (uint32_t q0 = 0; q0 < total; q0 += 64u) {
       const uint32_t q = q0 + (uint32_t)lane;
       const int g = wave_owner(incl, q);
-      if (q < total) a.node_group[wbase - band0 + q] = base + (uint32_t)g;
+      const uint32_t gfirst = __shfl(incl - n, g, 64), glo = __shfl((uint32_t)lo, g, 64);
+      const uint64_t h0 = __shfl(mk0, g, 64), h1 = __shfl(mk1, g, 64);
+      if (q < total) {
+        a.node_group[wbase - band0 + q] = base + (uint32_t)g;
+        const uint32_t k = glo + (q - gfirst);  // its rank: a candidate of its own at rank k, a node below it
+        const bool has = ((k >= 64 ? h1 : h0) >> (k & 63)) & 1ull;
+        a.flags[wbase + q] = (uint8_t)((k > glo ? kFUp : 0) | (has ? kFCand : 0));
+      }
     }
     // the left candidates, 64 at a time: item p is its group's (p - first)-th
     // highest rank, copied out of the hash with its parent's child link
@@ -480,8 +488,20 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
   }
 }
 
+// the first group start (a node without kFUp) at or after x0 in [x0, s1], 64
+// flags per step
+__device__ __forceinline__ uint32_t next_group_start(const FrontierArgs& a, uint32_t x0, uint32_t s1) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t y = x0; y < s1; y += 64u) {
+    const uint32_t x = y + (uint32_t)lane;
+    const uint64_t b = __ballot(x >= s1 || !(a.flags[x] & kFUp));
+    if (b) return y + (uint32_t)__builtin_ctzll(b);
+  }
+  return s1;
+}
+
 template <int KW>
-__global__ __launch_bounds__(256) void k_lbf_nodes(FrontierArgs a, int band) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_lbf_nodes(FrontierArgs a, int band) {
   if (__hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int lane = threadIdx.x & 63;
   const uint32_t rmask = (uint32_t)a.ring - 1u;
@@ -492,42 +512,121 @@ __global__ __launch_bounds__(256) void k_lbf_nodes(FrontierArgs a, int band) {
   const FCRec<KW>* CR = (const FCRec<KW>*)a.crec;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-  for (uint32_t base = wave * 64u; base < nn; base += nwaves * 64u) {
-    const uint32_t x = base + lane;
-    const bool live = x < nn;
-    const uint32_t id = band0 + x;
-    uint32_t jj = 0, m = 0;
-    int k = 0, lo = 0;
-    uint64_t key[KW];
+  // a wave takes a range of whole groups and runs it 64 nodes at a time from
+  // the top: a node's first visit is the smallest candidate at its rank or
+  // above in its group -- a segmented suffix min over consecutive ids, each
+  // lane loading only its own rank's candidate record; the group open at a
+  // step's top carried from the step above
+  // (ranges of kNodeSeg ids, taken from a ticket, moved to group starts)
+  (void)wave;
+  (void)nwaves;
+  const uint32_t e_all = band0 + nn, nseg = (nn + kNodeSeg - 1u) / kNodeSeg;
+  for (;;) {
+  uint32_t sg = 0;
+  if (lane == 0) sg = atomicAdd(&a.ctl->node_ticket, 1u);
+  sg = __shfl(sg, 0, 64);
+  if (sg >= nseg) break;
+  const uint32_t r0 = sg ? next_group_start(a, band0 + sg * kNodeSeg, e_all) : band0;
+  const uint32_t r1 = sg + 1u >= nseg ? e_all : next_group_start(a, band0 + (sg + 1u) * kNodeSeg, e_all);
+  uint64_t cy_key[KW];
 #pragma unroll
-    for (int w = 0; w < KW; ++w) key[w] = 0;
-    int A = 0, B = 0;
+  for (int w = 0; w < KW; ++w) cy_key[w] = ~0ull;
+  int cy_A = 0, cy_B = 0, cy_win = -1;
+  uint32_t cy_cnt = 0;
+  for (uint32_t c1 = r1; c1 > r0;) {
+    const uint32_t c0 = c1 - r0 > 64u ? c1 - 64u : r0;
+    const uint32_t id = c0 + (uint32_t)lane;
+    const bool live = id < c1;
+    const uint32_t x = id - band0;
+    c1 = c0;
+    uint32_t jj = 0, m = 0, cbase = 0;
+    int k = 0, lo = 0, hv = 0;
     uint32_t rw = 0;
+    uint8_t f0 = 0;
     FQInfo q{};
     if (live) {
+      f0 = a.flags[id];
       const FGRec r = GR[a.node_group[x]];
       jj = r.j;
       m = r.m;
       lo = r.lo;
+      hv = r.hv;
+      cbase = r.cbase;
       k = lo + (int)(id - r.base);
       q = a.qi[jj];
       rw = a.qrow[(size_t)jj * 128 + k];
-      // the smallest left candidate at ranks >= k (ranks descending: stop below k)
-      int win = -1;
-      for (uint32_t t = 0; t < r.nc; ++t) {
-        const FCRec<KW>& c = CR[r.cbase + t];
-        if ((int)c.rank < k) break;
-        uint64_t ck[KW];
+    }
+    const bool has = live && (f0 & kFCand);
+    // the first group top (highest rank) at or above this lane; 64: the
+    // group continues past the step's top (dead lanes -- above a partial
+    // bottom step -- end nothing and add nothing)
+    int se = (live && k == hv) ? lane : 64;
 #pragma unroll
-        for (int w = 0; w < KW; ++w) ck[w] = c.fk[w];
-        if (win < 0 || key_less<KW>(ck, key)) {
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_down(se, d, 64);
+      if (lane + d < 64 && o < se) se = o;
+    }
+    const bool open = se == 64;
+    const int lim = open ? 63 : se;
+    // candidates at ranks >= k in the group (records are rank-descending:
+    // this rank's own sits after the ones above it)
+    uint32_t cnt = has ? 1u : 0u;
 #pragma unroll
-          for (int w = 0; w < KW; ++w) key[w] = ck[w];
-          A = c.A;
-          B = c.B;
-          win = c.rank;
-        }
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_down(cnt, d, 64);
+      if (lane + d <= lim) cnt += y;
+    }
+    if (open) cnt += cy_cnt;
+    uint64_t key[KW];
+#pragma unroll
+    for (int w = 0; w < KW; ++w) key[w] = ~0ull;
+    int A = 0, B = 0, win = -1;
+    if (has) {
+      const FCRec<KW>& c = CR[cbase + cnt - 1u];
+#pragma unroll
+      for (int w = 0; w < KW; ++w) key[w] = c.fk[w];
+      A = c.A;
+      B = c.B;
+      win = k;
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint64_t ok[KW];
+#pragma unroll
+      for (int w = 0; w < KW; ++w) ok[w] = __shfl_down(key[w], d, 64);
+      const int oA = __shfl_down(A, d, 64), oB = __shfl_down(B, d, 64), ow = __shfl_down(win, d, 64);
+      if (lane + d <= lim && ow >= 0 && (win < 0 || key_less<KW>(ok, key))) {
+#pragma unroll
+        for (int w = 0; w < KW; ++w) key[w] = ok[w];
+        A = oA;
+        B = oB;
+        win = ow;
       }
+    }
+    if (open && cy_win >= 0 && (win < 0 || key_less<KW>(cy_key, key))) {
+#pragma unroll
+      for (int w = 0; w < KW; ++w) key[w] = cy_key[w];
+      A = cy_A;
+      B = cy_B;
+      win = cy_win;
+    }
+    // the step below continues lane 0's group unless lane 0 is its lowest rank
+    if (__shfl(k > lo ? 1 : 0, 0, 64)) {
+#pragma unroll
+      for (int w = 0; w < KW; ++w) cy_key[w] = __shfl(key[w], 0, 64);
+      cy_A = __shfl(A, 0, 64);
+      cy_B = __shfl(B, 0, 64);
+      cy_win = __shfl(win, 0, 64);
+      cy_cnt = __shfl(cnt, 0, 64);
+    } else {
+#pragma unroll
+      for (int w = 0; w < KW; ++w) cy_key[w] = ~0ull;
+      cy_A = cy_B = 0;
+      cy_win = -1;
+      cy_cnt = 0;
+    }
+    if (live) {
+      if (win < 0) set_overflow(a, 8);  // cannot happen: the group's top rank holds a candidate
       if (win != k) B = qrow_cap(rw);  // reached by the up chain: B = cap of this row (mass_table.py:411-420)
     }
     const int64_t wk = qrow_w(rw);
@@ -588,6 +687,7 @@ __global__ __launch_bounds__(256) void k_lbf_nodes(FrontierArgs a, int band) {
       }
     }
   }
+  }
 }
 
 // between bands: record where band b's nodes start; free the list slot the
@@ -596,18 +696,7 @@ __global__ void k_lbf_mark(FrontierArgs a, int band) {
   a.band_start[band] = a.ctl->node_ctr;
   a.ctl->crec_ctr = 0;  // the candidate records are per band
   a.ctl->list_cnt[((uint32_t)band + (uint32_t)a.jump) & ((uint32_t)a.ring - 1u)] = 0;
-}
-
-// the first group start (a node without kFUp) at or after x0 in [x0, s1], 64
-// flags per step
-__device__ __forceinline__ uint32_t next_group_start(const FrontierArgs& a, uint32_t x0, uint32_t s1) {
-  const int lane = threadIdx.x & 63;
-  for (uint32_t y = x0; y < s1; y += 64u) {
-    const uint32_t x = y + (uint32_t)lane;
-    const uint64_t b = __ballot(x >= s1 || !(a.flags[x] & kFUp));
-    if (b) return y + (uint32_t)__builtin_ctzll(b);
-  }
-  return s1;
+  a.ctl->node_ticket = 0;
 }
 
 // the memoised values of band b's nodes (mass_table.py:407-457).  Within a

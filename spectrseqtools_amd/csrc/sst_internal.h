@@ -324,6 +324,7 @@ struct FCtl {
   uint32_t list_cnt[8];
   uint32_t max_band, max_win, max_k, crec_ctr;
   uint64_t max_hi;
+  uint32_t node_ticket;  // k_lbf_nodes' next id range (reset per band by k_lbf_mark)
 };
 struct FrontierArgs {
   const uint32_t* list;  // the list pass's live queries
