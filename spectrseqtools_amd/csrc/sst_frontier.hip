@@ -336,12 +336,13 @@ __global__ __launch_bounds__(256) void k_lbf_roots(FrontierArgs a) {
 // winner down; its budgets: A from the winning candidate, B = cap[k] unless
 // the winner is rank k's own).  Every node of the band is then independent:
 //   k_lbf_groups  a lane per group: the group's entry (its masks consumed),
-//                 lo, node ids (ranks lo .. hv ascending), its left
-//                 candidates copied out of the hash (rank descending) with
-//                 their parents' child links, node -> group for the band
-//   k_lbf_nodes   a lane per node: its first visit from the group's
-//                 candidates, the left attempt (mass_table.py:424-441), the
-//                 left child's group and candidate in the band it falls in
+//                 lo, node ids (ranks lo .. hv ascending), node -> group and
+//                 each node's flags (a rank below it, a candidate of its own)
+//   k_lbf_nodes   a lane per node: its own rank's candidate from the hash
+//                 (and its parent's child link), its first visit as a
+//                 segmented suffix min over the group, the left attempt
+//                 (mass_table.py:424-441), the left child's group and
+//                 candidate in the band it falls in
 template <int KW>
 struct FCRec {  // a group's left candidate, copied for the node lanes
   uint64_t fk[KW];
@@ -366,12 +367,10 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
     if (blockIdx.x == 0 && threadIdx.x == 0) set_overflow(a, 4);
     return;
   }
-  const size_t gstride = (size_t)a.gmask + 1, cstride = (size_t)a.cmask + 1;
+  const size_t gstride = (size_t)a.gmask + 1;
   FGroup* G = (FGroup*)a.gtab + slot * gstride;
-  const FCand<KW>* Cb = (const FCand<KW>*)a.ctab + slot * cstride;
   const uint32_t* Lst = a.glist + slot * gstride;
   FGRec* GR = (FGRec*)a.grec;
-  FCRec<KW>* CR = (FCRec<KW>*)a.crec;
   const uint32_t band0 = a.band_start[band];
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
@@ -396,18 +395,12 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
       else n = (uint32_t)(hv - lo + 1);
       nc = (uint32_t)(__builtin_popcountll(mk0) + __builtin_popcountll(mk1));
     }
-    // node ids and candidate records: one atomic each per wave
+    // node ids: one atomic per wave
     const uint32_t incl = wave_incl_u(n), total = __shfl(incl, 63, 64);
-    const uint32_t cincl = wave_incl_u(nc), ctotal = __shfl(cincl, 63, 64);
-    uint32_t wbase = 0, cwbase = 0;
-    if (lane == 0) {
-      wbase = atomicAdd(&a.ctl->node_ctr, total);
-      cwbase = atomicAdd(&a.ctl->crec_ctr, ctotal);
-    }
+    uint32_t wbase = 0;
+    if (lane == 0) wbase = atomicAdd(&a.ctl->node_ctr, total);
     wbase = __shfl(wbase, 0, 64);
-    cwbase = __shfl(cwbase, 0, 64);
-    if ((uint64_t)wbase + total > a.ncap || (uint64_t)wbase + total - band0 > a.ngrp_cap ||
-        (uint64_t)cwbase + ctotal > a.crec_cap) {
+    if ((uint64_t)wbase + total > a.ncap || (uint64_t)wbase + total - band0 > a.ngrp_cap) {
       if (lane == 0) set_overflow(a, 1);
       return;
     }
@@ -436,7 +429,7 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
       r.base = id0;
       r.j = jj;
       r.m = m;
-      r.cbase = cwbase + cincl - nc;
+      r.cbase = 0;  // (candidates are read from the hash by the node pass)
       r.lo = (uint8_t)lo;
       r.hv = (uint8_t)hv;
       r.nc = (uint8_t)nc;
@@ -456,34 +449,6 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
         const bool has = ((k >= 64 ? h1 : h0) >> (k & 63)) & 1ull;
         a.flags[wbase + q] = (uint8_t)((k > glo ? kFUp : 0) | (has ? kFCand : 0));
       }
-    }
-    // the left candidates, 64 at a time: item p is its group's (p - first)-th
-    // highest rank, copied out of the hash with its parent's child link
-    const uint32_t idlo = id0 - (uint32_t)lo, cfirst = cincl - nc;
-    for (uint32_t p0 = 0; p0 < ctotal; p0 += 64u) {
-      const uint32_t p = p0 + (uint32_t)lane;
-      const int g = wave_owner(cincl, p);
-      const uint64_t h0 = __shfl(mk0, g, 64), h1 = __shfl(mk1, g, 64);
-      const uint32_t gj = __shfl(jj, g, 64), gm = __shfl(m, g, 64), gidlo = __shfl(idlo, g, 64);
-      const uint32_t gfirst = __shfl(cfirst, g, 64);
-      if (p >= ctotal) continue;
-      const int k = mask_select_top(h1, h0, p - gfirst);
-      const uint32_t cs = cand_find<KW>(Cb, a.cmask, fkey(ftagb(a, (uint32_t)band), gj, gm, (uint32_t)k));
-      if (cs == UINT32_MAX) {
-        set_overflow(a, 16);  // cannot happen: the mask bit follows the insertion
-        continue;
-      }
-      const FCand<KW>& e = Cb[cs];
-      const uint32_t par = e.parent, id = gidlo + (uint32_t)k;
-      if (par & kRootBit) a.root_node[par & ~kRootBit] = id;
-      else a.lchild[par] = id;
-      FCRec<KW> cr;
-#pragma unroll
-      for (int w = 0; w < KW; ++w) cr.fk[w] = e.fk[w];
-      cr.A = e.A;
-      cr.B = e.B;
-      cr.rank = (uint8_t)k;
-      CR[cwbase + p] = cr;
     }
   }
 }
@@ -509,7 +474,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   const uint32_t nn = a.ctl->node_ctr - band0;  // this band's nodes (k_lbf_groups allocated them)
   const size_t gstride = (size_t)a.gmask + 1, cstride = (size_t)a.cmask + 1;
   const FGRec* GR = (const FGRec*)a.grec;
-  const FCRec<KW>* CR = (const FCRec<KW>*)a.crec;
+  const FCand<KW>* Cb = (const FCand<KW>*)a.ctab + ((uint32_t)band & rmask) * cstride;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   // a wave takes a range of whole groups and runs it 64 nodes at a time from
@@ -532,14 +497,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 #pragma unroll
   for (int w = 0; w < KW; ++w) cy_key[w] = ~0ull;
   int cy_A = 0, cy_B = 0, cy_win = -1;
-  uint32_t cy_cnt = 0;
   for (uint32_t c1 = r1; c1 > r0;) {
     const uint32_t c0 = c1 - r0 > 64u ? c1 - 64u : r0;
     const uint32_t id = c0 + (uint32_t)lane;
     const bool live = id < c1;
     const uint32_t x = id - band0;
     c1 = c0;
-    uint32_t jj = 0, m = 0, cbase = 0;
+    uint32_t jj = 0, m = 0;
     int k = 0, lo = 0, hv = 0;
     uint32_t rw = 0;
     uint8_t f0 = 0;
@@ -551,7 +515,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       m = r.m;
       lo = r.lo;
       hv = r.hv;
-      cbase = r.cbase;
       k = lo + (int)(id - r.base);
       q = a.qi[jj];
       rw = a.qrow[(size_t)jj * 128 + k];
@@ -568,26 +531,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     }
     const bool open = se == 64;
     const int lim = open ? 63 : se;
-    // candidates at ranks >= k in the group (records are rank-descending:
-    // this rank's own sits after the ones above it)
-    uint32_t cnt = has ? 1u : 0u;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_down(cnt, d, 64);
-      if (lane + d <= lim) cnt += y;
-    }
-    if (open) cnt += cy_cnt;
     uint64_t key[KW];
 #pragma unroll
     for (int w = 0; w < KW; ++w) key[w] = ~0ull;
     int A = 0, B = 0, win = -1;
-    if (has) {
-      const FCRec<KW>& c = CR[cbase + cnt - 1u];
+    if (has) {  // this rank's own candidate, straight from the hash, and its parent's child link
+      const uint32_t cs = cand_find<KW>(Cb, a.cmask, fkey(ftagb(a, (uint32_t)band), jj, m, (uint32_t)k));
+      if (cs == UINT32_MAX) {
+        set_overflow(a, 16);  // cannot happen: the mask bit follows the insertion
+      } else {
+        const FCand<KW>& c = Cb[cs];
 #pragma unroll
-      for (int w = 0; w < KW; ++w) key[w] = c.fk[w];
-      A = c.A;
-      B = c.B;
-      win = k;
+        for (int w = 0; w < KW; ++w) key[w] = c.fk[w];
+        A = c.A;
+        B = c.B;
+        win = k;
+        const uint32_t par = c.parent;
+        if (par & kRootBit) a.root_node[par & ~kRootBit] = id;
+        else a.lchild[par] = id;
+      }
     }
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -617,13 +579,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       cy_A = __shfl(A, 0, 64);
       cy_B = __shfl(B, 0, 64);
       cy_win = __shfl(win, 0, 64);
-      cy_cnt = __shfl(cnt, 0, 64);
     } else {
 #pragma unroll
       for (int w = 0; w < KW; ++w) cy_key[w] = ~0ull;
       cy_A = cy_B = 0;
       cy_win = -1;
-      cy_cnt = 0;
     }
     if (live) {
       if (win < 0) set_overflow(a, 8);  // cannot happen: the group's top rank holds a candidate
