@@ -358,7 +358,10 @@ struct FGRec {
 
 template <int KW>
 __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
-  if (__hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  __shared__ uint32_t s_ovf;  // one reading for the workgroup: its barriers below need every wave
+  if (threadIdx.x == 0) s_ovf = __hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_ovf) return;
   const int lane = threadIdx.x & 63;
   const uint32_t slot = (uint32_t)band & ((uint32_t)a.ring - 1u);
   const uint32_t ng = a.ctl->list_cnt[slot];
@@ -372,9 +375,10 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
   const uint32_t* Lst = a.glist + slot * gstride;
   FGRec* GR = (FGRec*)a.grec;
   const uint32_t band0 = a.band_start[band];
-  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
-  for (uint32_t base = wave * 64u; base < ng; base += nwaves * 64u) {
+  __shared__ uint32_t s_tot[4], s_base;
+  const int wib = (int)(threadIdx.x >> 6);
+  for (uint32_t bbase = blockIdx.x * 256u; bbase < ng; bbase += gridDim.x * 256u) {  // block-uniform trips
+    const uint32_t base = bbase + (uint32_t)wib * 64u;
     const uint32_t gi = base + lane;
     const bool act = gi < ng;
     uint32_t jj = 0, m = 0, n = 0, nc = 0;
@@ -395,14 +399,20 @@ __global__ __launch_bounds__(256) void k_lbf_groups(FrontierArgs a, int band) {
       else n = (uint32_t)(hv - lo + 1);
       nc = (uint32_t)(__builtin_popcountll(mk0) + __builtin_popcountll(mk1));
     }
-    // node ids: one atomic per wave
+    // node ids: one atomic per workgroup (the waves' totals through LDS)
     const uint32_t incl = wave_incl_u(n), total = __shfl(incl, 63, 64);
-    uint32_t wbase = 0;
-    if (lane == 0) wbase = atomicAdd(&a.ctl->node_ctr, total);
-    wbase = __shfl(wbase, 0, 64);
-    if ((uint64_t)wbase + total > a.ncap || (uint64_t)wbase + total - band0 > a.ngrp_cap) {
-      if (lane == 0) set_overflow(a, 1);
-      return;
+    if (lane == 0) s_tot[wib] = total;
+    __syncthreads();
+    const uint32_t btotal = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
+    if (threadIdx.x == 0) s_base = atomicAdd(&a.ctl->node_ctr, btotal);
+    __syncthreads();
+    const uint32_t bstart = s_base;
+    uint32_t wbase = bstart;
+    for (int w = 0; w < wib; ++w) wbase += s_tot[w];
+    __syncthreads();  // the next trip rewrites s_tot / s_base
+    if ((uint64_t)bstart + btotal > a.ncap || (uint64_t)bstart + btotal - band0 > a.ngrp_cap) {
+      if (threadIdx.x == 0) set_overflow(a, 1);
+      return;  // the whole workgroup
     }
     const uint32_t id0 = wbase + incl - n;
     {  // per-query node counts: one atomic per run of one query's groups in the wave
