@@ -46,6 +46,7 @@ namespace {
 constexpr int kProbeMax = 4096;
 constexpr uint32_t kRootBit = 0x80000000u;
 constexpr uint32_t kNodeSeg = 512;  // k_lbf_nodes: ids per ticket
+constexpr uint32_t kFreshBuf = 640;  // > kNodeSeg + 127: the nodes of a range moved to group starts
 constexpr uint8_t kFLeft = 1, kFUp = 2, kFZero = 4, kFCand = 8;  // kFCand: k_lbf_groups' mark, until k_lbf_nodes
 
 struct alignas(32) FGroup {
@@ -496,7 +497,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   (void)wave;
   (void)nwaves;
   const uint32_t e_all = band0 + nn, nseg = (nn + kNodeSeg - 1u) / kNodeSeg;
+  __shared__ uint32_t s_fresh[4][2][kFreshBuf];  // per wave: the range's fresh groups of bands b+1, b+2
+  const int wib = (int)(threadIdx.x >> 6);
   for (;;) {
+  uint32_t nf0 = 0, nf1 = 0;  // (wave-uniform) fresh groups buffered per band
   uint32_t sg = 0;
   if (lane == 0) sg = atomicAdd(&a.ctl->node_ticket, 1u);
   sg = __shfl(sg, 0, 64);
@@ -622,10 +626,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         atomicOr((unsigned long long*)&G2[gs2].mask[k >> 6], 1ull << (k & 63));
       }
     }
-    for (int d = 1; d <= a.jump; ++d) {  // fresh groups join their band's list: one atomic per wave and band
+    for (int d = 1; d <= a.jump; ++d) {  // fresh groups join their band's list
       const bool pd = fresh && band2 == (uint32_t)band + (uint32_t)d;
       const uint64_t bm = __ballot(pd);
-      if (bm) {
+      if (bm && d <= 2) {  // buffered for the range: one atomic per range and band
+        uint32_t& nf = d == 1 ? nf0 : nf1;
+        const uint32_t at = nf + (uint32_t)__builtin_popcountll(bm & lanemask_lt());
+        if (pd) {
+          if (at < kFreshBuf) s_fresh[wib][d - 1][at] = gs2;
+          else set_overflow(a, 4);  // cannot happen: a range holds < kFreshBuf nodes
+        }
+        nf += (uint32_t)__builtin_popcountll(bm);
+      } else if (bm) {
         const int leader = __builtin_ctzll(bm);
         const uint32_t sl = ((uint32_t)band + (uint32_t)d) & rmask;
         uint32_t b0 = 0;
@@ -657,6 +669,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       }
     }
   }
+  // the range's fresh groups into their bands' lists
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  for (int d = 1; d <= 2; ++d) {
+    const uint32_t nf = d == 1 ? nf0 : nf1;
+    if (!nf) continue;
+    const uint32_t sl = ((uint32_t)band + (uint32_t)d) & rmask;
+    uint32_t b0 = 0;
+    if (lane == 0) b0 = atomicAdd(&a.ctl->list_cnt[sl], nf);
+    b0 = __shfl(b0, 0, 64);
+    for (uint32_t t = (uint32_t)lane; t < nf && t < kFreshBuf; t += 64u) {
+      const uint32_t at = b0 + t;
+      if (at > a.gmask) set_overflow(a, 4);
+      else a.glist[sl * gstride + at] = s_fresh[wib][d - 1][t];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the buffer is refilled by the next range
   }
 }
 
