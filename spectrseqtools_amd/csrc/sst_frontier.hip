@@ -494,17 +494,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
   // lane loading only its own rank's candidate record; the group open at a
   // step's top carried from the step above
   // (ranges of kNodeSeg ids, taken from a ticket, moved to group starts)
-  (void)wave;
-  (void)nwaves;
   const uint32_t e_all = band0 + nn, nseg = (nn + kNodeSeg - 1u) / kNodeSeg;
   __shared__ uint32_t s_fresh[4][2][kFreshBuf];  // per wave: the range's fresh groups of bands b+1, b+2
   const int wib = (int)(threadIdx.x >> 6);
+  uint32_t next = wave;  // the first range: the wave's own; later ones from the ticket, past the grid's
   for (;;) {
   uint32_t nf0 = 0, nf1 = 0;  // (wave-uniform) fresh groups buffered per band
-  uint32_t sg = 0;
-  if (lane == 0) sg = atomicAdd(&a.ctl->node_ticket, 1u);
-  sg = __shfl(sg, 0, 64);
-  if (sg >= nseg) break;
+  const uint32_t sg = next;
+  if (sg >= nseg) break;  // (a wave past a small band's ranges leaves without touching the ticket)
   const uint32_t r0 = sg ? next_group_start(a, band0 + sg * kNodeSeg, e_all) : band0;
   const uint32_t r1 = sg + 1u >= nseg ? e_all : next_group_start(a, band0 + (sg + 1u) * kNodeSeg, e_all);
   uint64_t cy_key[KW];
@@ -685,6 +682,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the buffer is refilled by the next range
+  if (lane == 0) next = nwaves + atomicAdd(&a.ctl->node_ticket, 1u);
+  next = __shfl(next, 0, 64);
   }
 }
 
