@@ -70,6 +70,15 @@ void* sst_ctx_stream(sst_ctx* ctx);
 int sst_ctx_set_stream(sst_ctx* ctx, void* stream);
 /* Wait for all queued work of this ctx. */
 int sst_ctx_synchronize(sst_ctx* ctx);
+/* Release the ctx's cached work buffers: the first-visit frontier's
+ * workspaces that sst_length_bounds_frontier_device and
+ * sst_length_bound_batch keep across calls (up to min(96 GB, free / 2) and
+ * 4 GB), so that later stages, other allocators or another process on the
+ * same GPU get that HBM back.  Waits for the ctx's queued work first; the
+ * next frontier call allocates again.  No reference equivalent (the
+ * reference's memo dict is freed when compute_sequence_length_bound returns,
+ * mass_table.py:361). */
+int sst_ctx_trim(sst_ctx* ctx);
 
 /* Build the packed 2-bit DP reachability table on the GPU.
  * Replaces set_up_bit_table(integer_masses, max_mass, compression_rate)

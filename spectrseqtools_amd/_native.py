@@ -37,7 +37,7 @@ EXPORTS = (
     "sst_skel_walk_device", "sst_result_refs_device", "sst_dict_count_device", "sst_dict_build_device",
     "sst_reach_rows_device", "sst_length_bounds_reach_device", "sst_jaccard_device", "sst_skeleton_alpha_device",
     "sst_dict_list_device", "sst_fix_finish_device", "sst_pipe_reserve_rows", "sst_reach_lowest_device",
-    "sst_length_bounds_frontier_device", "sst_post_skeleton_device",
+    "sst_length_bounds_frontier_device", "sst_post_skeleton_device", "sst_ctx_trim",
 )
 
 # kernel ids of sst_profile_read
@@ -167,7 +167,8 @@ def load_library(path=LIB_PATH):
 
         why = build_record.check(path)
         if why:
-            raise ImportError(f"{path}: {why}; rebuild it (make -C spectrseqtools_amd/csrc)")
+            raise ImportError(f"{path}: {why}; rebuild it (make -B -C spectrseqtools_amd/csrc: -B also "
+                              "when the library looks up to date)")
     _share_hip_runtime_with_torch()
     lib = ctypes.CDLL(path)
     lib.sst_device_count.restype = _I
@@ -180,6 +181,8 @@ def load_library(path=LIB_PATH):
     lib.sst_ctx_stream.restype = _P
     lib.sst_ctx_set_stream.argtypes = [_P, _P]
     lib.sst_ctx_set_stream.restype = _I
+    lib.sst_ctx_trim.argtypes = [_P]
+    lib.sst_ctx_trim.restype = _I
     lib.sst_ctx_synchronize.argtypes = [_P]
     lib.sst_table_build.argtypes = [_P, _P, _I, _I64, _I, _PP]
     lib.sst_table_upload.argtypes = [_P, _P, _I, _P, _I64, _I, _PP]
@@ -451,6 +454,10 @@ class Engine:
 
     def synchronize(self):
         self.check(self._lib.sst_ctx_synchronize(self.handle), "sst_ctx_synchronize")
+
+    def trim(self):
+        """Release the cached frontier workspaces (sst_ctx_trim)."""
+        self.check(self._lib.sst_ctx_trim(self.handle), "sst_ctx_trim")
 
     def is_singleton(self, integer_masses, masses, thresholds, tolerance, precision):
         """fragment_classification.is_singleton for each mass: int8 {0, 1}."""

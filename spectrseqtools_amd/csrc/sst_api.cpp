@@ -553,6 +553,16 @@ int sst_ctx_synchronize(sst_ctx* c) {
   return SST_OK;
 }
 
+int sst_ctx_trim(sst_ctx* c) {
+  if (!c) return SST_E_ARG;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  HIP_OK(c, hipStreamSynchronize(c->stream));
+  c->lbf = sst_ctx::LbfWs{};  // DevBuf frees on destruction
+  c->lbf_small = sst_ctx::LbfWs{};
+  return SST_OK;
+}
+
 int sst_table_build(sst_ctx* c, const int64_t* masses, int n_rows, int64_t max_mass, int C, sst_table** out) {
   if (!c || !out) return SST_E_ARG;
   std::lock_guard<std::recursive_mutex> g(c->mu);
@@ -2536,31 +2546,51 @@ static int length_bound_batch(sst_table* t, const double* su, const double* obs,
   std::vector<int8_t> st(nn);
   DevBuf f_alpha, f_words, f_off, f_bits, f_lr, f_lro, f_spec, f_lo, f_hi, f_st;
   bool frontier_ok = t->closure && !alpha && !replay_only && t->args.w_min >= 1024;  // (the reach rows' LDS ring)
-  for (int r = 1; r < t->n_rows && frontier_ok; ++r) frontier_ok = t->masses[r] < (1 << 20);
+  int64_t w_top = 0;
+  for (int r = 1; r < t->n_rows && frontier_ok; ++r) {
+    frontier_ok = t->masses[r] < (1 << 20);
+    w_top = std::max<int64_t>(w_top, t->masses[r]);
+  }
+  // the frontier applies the reduced-alphabet extent ceil((w_top * 35 + 1) / C) * C
+  // (mass_table.py:116): only a table of exactly that extent (every table built
+  // here, the reference's cache) is answered by it; an uploaded table of another
+  // extent goes to the replay, which reads the table's own
+  frontier_ok = frontier_ok && (w_top * 35 + t->C) / t->C == t->n_cols;
   if (n_exact && frontier_ok) {
     // the first-visit frontier on the table's own rows, both
-    // directions for every query of the call (the fast path's answers are the
-    // same); a window in the table's last packed word, where the frontier's
-    // reachability cannot see the last-column mask (SST_ABORTED there), goes
-    // on to the replay below
+    // directions, for the queries the fast path left pending only (its own
+    // answers stay); a window in the table's last packed word, where the
+    // frontier's reachability cannot see the last-column mask (SST_ABORTED
+    // there), or one the frontier's layout cannot hold, goes on to the replay
+    const size_t m = n_exact;
+    std::vector<uint32_t> pend(m);
+    HIP_OK(c, hipMemcpyAsync(pend.data(), d_list.p, m * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    std::vector<double> psu(m), pob(m);
     int64_t hmax = 1;
-    for (int64_t i = 0; i < n; ++i)
-      hmax = std::max<int64_t>(hmax, (int64_t)((su[i] + tol * std::fabs(obs[i])) / prec) + 4);
+    for (size_t j = 0; j < m; ++j) {
+      psu[j] = su[pend[j]];
+      pob[j] = obs[pend[j]];
+      hmax = std::max<int64_t>(hmax, (int64_t)((psu[j] + tol * std::fabs(pob[j])) / prec) + 4);
+    }
     hmax = std::min<int64_t>(hmax, t->n_cols * t->C);
     const int64_t words = hmax / 32 + 2;
     uint64_t am[2] = {0, 0};
     for (int r = 1; r < t->n_rows; ++r) am[r >> 6] |= 1ull << (r & 63);
     const int64_t zero = 0;
     const size_t K = (size_t)(t->n_rows - 1);
+    DevBuf f_su, f_ob;
     if (!f_alpha.ensure(16) || !f_words.ensure(8) || !f_off.ensure(8) || !f_bits.ensure(K * words * 4) ||
-        !f_lr.ensure((size_t)words * 32) || !f_lro.ensure(8) || !f_spec.ensure(nn * 4) || !f_lo.ensure(nn * 8) ||
-        !f_hi.ensure(nn * 8) || !f_st.ensure(nn))
+        !f_lr.ensure((size_t)words * 32) || !f_lro.ensure(8) || !f_spec.ensure(m * 4) || !f_lo.ensure(m * 8) ||
+        !f_hi.ensure(m * 8) || !f_st.ensure(m) || !f_su.ensure(m * 8) || !f_ob.ensure(m * 8))
       return fail(c, SST_E_NOMEM, "device allocation failed (length bound, frontier)");
     HIP_OK(c, hipMemcpyAsync(f_alpha.p, am, 16, hipMemcpyHostToDevice, c->stream));
     HIP_OK(c, hipMemcpyAsync(f_words.p, &words, 8, hipMemcpyHostToDevice, c->stream));
     HIP_OK(c, hipMemcpyAsync(f_off.p, &zero, 8, hipMemcpyHostToDevice, c->stream));
     HIP_OK(c, hipMemcpyAsync(f_lro.p, &zero, 8, hipMemcpyHostToDevice, c->stream));
-    HIP_OK(c, hipMemsetAsync(f_spec.p, 0, nn * 4, c->stream));
+    HIP_OK(c, hipMemcpyAsync(f_su.p, psu.data(), m * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipMemcpyAsync(f_ob.p, pob.data(), m * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipMemsetAsync(f_spec.p, 0, m * 4, c->stream));
     if (int rc = sst_reach_rows_device(t, (const uint64_t*)f_alpha.p, (const int64_t*)f_words.p,
                                        (const uint64_t*)f_off.p, 1, (uint32_t*)f_bits.p))
       return rc;
@@ -2568,23 +2598,34 @@ static int length_bound_batch(sst_table* t, const double* su, const double* obs,
                                          (const uint64_t*)f_off.p, 1, (const uint32_t*)f_bits.p,
                                          (const uint64_t*)f_lro.p, (uint8_t*)f_lr.p))
       return rc;
-    if (int rc = lbf_frontier(t, c->lbf_small, q.su, q.obs, (const int32_t*)f_spec.p, (const uint64_t*)f_alpha.p,
-                              (const uint8_t*)f_lr.p, (const uint64_t*)f_lro.p, n, tol, prec, max_len, max_mods,
-                              (int64_t*)f_lo.p, (int64_t*)f_hi.p, (int8_t*)f_st.p, nullptr, nullptr, nullptr, nullptr,
-                              kBatchFrontierBytes, nullptr))
+    if (int rc = lbf_frontier(t, c->lbf_small, (const double*)f_su.p, (const double*)f_ob.p,
+                              (const int32_t*)f_spec.p, (const uint64_t*)f_alpha.p, (const uint8_t*)f_lr.p,
+                              (const uint64_t*)f_lro.p, (int64_t)m, tol, prec, max_len, max_mods, (int64_t*)f_lo.p,
+                              (int64_t*)f_hi.p, (int8_t*)f_st.p, nullptr, nullptr, nullptr, nullptr, kBatchFrontierBytes,
+                              nullptr))
       return rc;
-    HIP_OK(c, hipMemcpyAsync(d_out.p, direction ? f_hi.p : f_lo.p, nn * 8, hipMemcpyDeviceToDevice, c->stream));
-    HIP_OK(c, hipMemcpyAsync(d_st.p, f_st.p, nn, hipMemcpyDeviceToDevice, c->stream));
-    HIP_OK(c, hipMemcpyAsync(st.data(), f_st.p, nn, hipMemcpyDeviceToHost, c->stream));
+    // scatter the frontier's answers over the fast pass's (host copies: nn x 9 bytes)
+    std::vector<int64_t> fv(m), ov(nn);
+    std::vector<int8_t> fs(m);
+    HIP_OK(c, hipMemcpyAsync(fv.data(), direction ? f_hi.p : f_lo.p, m * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(fs.data(), f_st.p, m, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(ov.data(), d_out.p, nn * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipMemcpyAsync(st.data(), d_st.p, nn, hipMemcpyDeviceToHost, c->stream));
     HIP_OK(c, hipStreamSynchronize(c->stream));
     std::vector<uint32_t> rest;
-    for (size_t i = 0; i < nn; ++i)
-      if (st[i] == SST_ABORTED) rest.push_back((uint32_t)i);
+    for (size_t j = 0; j < m; ++j) {
+      ov[pend[j]] = fv[j];
+      st[pend[j]] = fs[j];
+      if (fs[j] == SST_ABORTED) rest.push_back(pend[j]);
+    }
+    HIP_OK(c, hipMemcpyAsync(d_out.p, ov.data(), nn * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipMemcpyAsync(d_st.p, st.data(), nn, hipMemcpyHostToDevice, c->stream));
     n_exact = (uint32_t)rest.size();
     if (n_exact) {
       HIP_OK(c, hipMemcpyAsync(d_list.p, rest.data(), rest.size() * 4, hipMemcpyHostToDevice, c->stream));
       HIP_OK(c, hipMemcpyAsync(d_cnt.p, &n_exact, 4, hipMemcpyHostToDevice, c->stream));
     }
+    HIP_OK(c, hipStreamSynchronize(c->stream));  // the host vectors above are read by the copies
   }
   if (n_exact) {
     // one 64-lane block per query in flight (k_length_exact<WAVE>), each with
@@ -3360,7 +3401,7 @@ static int lbf_frontier(sst_table* t, sst_ctx::LbfWs& W, const double* d_su, con
     if (h.max_hi >= (1ull << 25)) return fail(c, SST_E_ARG, "length bounds (frontier): a window at 2^25 or beyond");
     a.rb = bits_for(h.max_win > 0 ? h.max_win - 1 : 0);
     // unary keys: root bits, one zero per kept rank, one 1 per left move (<= hi / w_min)
-    const int need = a.rb + (int)h.max_k + (int)(h.max_hi / (uint64_t)wb);
+    const int need = a.rb + (int)h.max_need;  // (k_lbf_setup excluded every query beyond 256 bits)
     const int kw = need <= 64 ? 1 : need <= 128 ? 2 : need <= 256 ? 4 : 0;
     if (!kw || a.rb > 32) return fail(c, SST_E_ARG, "length bounds (frontier): first-visit keys beyond 256 bits");
     a.rstride = (int)std::max<uint32_t>(1, h.max_win);

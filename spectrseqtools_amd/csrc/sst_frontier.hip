@@ -250,15 +250,33 @@ __global__ __launch_bounds__(256) void k_lbf_setup(TableArgs t, FrontierArgs a) 
     }
   }
   if (lane == 0) {
+    // queries the engine's layout cannot hold are answered SST_ABORTED on
+    // their own (the batch's other queries are unaffected): a window wider
+    // than one band (its roots would fall in several bands, and a root's left
+    // child could land on another root's mass), a window top at 2^25 or
+    // beyond (the keys' mass field), or a first-visit key beyond 256 bits
+    // (root index bits -- at most bits(w_min - 1) once the window fits a
+    // band --, one bit per kept rank, one per left move <= hi / w_min)
+    int kb = 0;
+    while (kb < 32 && ((uint32_t)(a.wb - 1) >> kb)) ++kb;
+    const int64_t win0 = hi - lo + 1;
+    const bool fits = win0 <= (int64_t)a.wb && hi < (1ll << 25) &&
+                      kb + K + (int)((hi > 0 ? hi : 0) / a.wb) <= 256;
     FQInfo q;
-    q.hi = hi;
+    q.hi = fits ? hi : lo - 1;  // an excluded query has no window values: no roots, no nodes
     q.lo = lo;
     q.lr_off = a.lr_off[u];
     q.i = i;
-    q.K = (uint16_t)K;
+    q.K = (uint16_t)(fits ? K : 0);
     q.L = (uint16_t)(L > 65535 ? 65535 : L);
     q.A0 = (uint16_t)(A0 < 0 ? 0 : (A0 > 255 ? 255 : A0));
+    q.pad = fits ? 0 : 1;
     a.qi[jj] = q;
+    if (!fits) {
+      a.status[i] = SST_ABORTED;
+      return;
+    }
+    atomicMax(&a.ctl->max_need, (uint32_t)(K + (hi > 0 ? hi : 0) / a.wb));
     if (hi >= 1) {
       atomicMax(&a.ctl->max_band, (uint32_t)((hi - 1) / a.wb));
       atomicMax((unsigned long long*)&a.ctl->max_hi, (unsigned long long)hi);
@@ -775,6 +793,7 @@ __global__ __launch_bounds__(256) void k_lbf_out(FrontierArgs a) {
   const FQInfo q = a.qi[jj];
   const bool bad = __hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   if (bad) return;  // the host splits the chunk and runs it again
+  if (q.pad & 1) return;  // excluded by k_lbf_setup (SST_ABORTED already written)
   const int dl = (int)q.L + 1;
   int bl = dl, bh = -1;
   if (q.lo <= 0 && q.hi >= 0) {  // total_mass == 0 -> 0

@@ -316,7 +316,7 @@ struct FQInfo {       // per listed query of a chunk
   uint16_t K;         // kept rows (row 0 excluded)
   uint16_t L;         // max_len
   uint16_t A0;        // max_modifications (clamped to 255)
-  uint16_t pad;
+  uint16_t pad;       // bit 0: excluded by k_lbf_setup (answered SST_ABORTED)
 };
 struct FCtl {
   uint32_t node_ctr;
@@ -325,6 +325,7 @@ struct FCtl {
   uint32_t max_band, max_win, max_k, crec_ctr;
   uint64_t max_hi;
   uint32_t node_ticket;  // k_lbf_nodes' next id range (reset per band by k_lbf_mark)
+  uint32_t max_need;     // max over the chunk's queries of K + hi / w_min (key bits besides the root index)
 };
 struct FrontierArgs {
   const uint32_t* list;  // the list pass's live queries

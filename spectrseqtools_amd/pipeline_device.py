@@ -1098,7 +1098,7 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
 @_one_stream
 def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reach_budget_bytes=64 << 30,
                   share_alphabets=True, length_chunk=1 << 30, spectra=None, soft_nodes=1 << 20,
-                  heavy_memo=1 << 22, engine="frontier", frontier_workspace=0):
+                  heavy_memo=1 << 22, engine="frontier", frontier_workspace=0, trim=True):
     """Stage 5: each spectrum's skeleton alphabet (the canonical rows and the
     modifications its START / END skeletons name), both length bounds on it,
     then the Jaccard selection and the combined skeleton (k_jaccard).
@@ -1112,7 +1112,9 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     reference's DFS per spectrum (the round-4 engine, kept for comparison).
     spectra: the bounds for these spectra only (indices; the others get
     lb_status LB_NOT_RUN and Jaccard status SST_JAC_BOUNDS) -- a bounded
-    sample where the reference's DFS is too large to replay for all."""
+    sample where the reference's DFS is too large to replay for all.
+    trim: release the frontier's cached workspace (sst_ctx_trim) once the
+    bounds are done, so later stages and other allocators get that HBM."""
     import torch
 
     dt = dp_table.device_table
@@ -1144,6 +1146,8 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
         dp_table, alpha_sk, su, ob, ml, caps_len, a0_len, sel=sel, engine=engine,
         reach_budget_bytes=reach_budget_bytes, share_alphabets=share_alphabets, length_chunk=length_chunk,
         soft_nodes=soft_nodes, heavy_memo=heavy_memo, frontier_workspace=frontier_workspace)
+    if trim:
+        eng.trim()
     n_batches, U = stats["batches"], stats["distinct"]
     # Jaccard + combine
     comb_off = np.concatenate([[0], np.cumsum(ml)]).astype(np.int64)

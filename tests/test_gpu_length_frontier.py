@@ -197,3 +197,169 @@ def test_replay_heavy_pass_and_retries_vs_oracle(setup, cases, fused):
     assert (nodes[sel] > (1 << 12)).sum() >= 10  # the heavy pass ran
     skip = set(range(len(alphas))) - set(sel.tolist())
     assert _check(want, lower, upper, st, skip=skip) >= len(sel) - 2
+
+
+def _reference_cases(rows):
+    """length_cases.json.gz (tests/golden/make_length_golden.py): the
+    reference's own compute_sequence_length_bound on 40 alphabets it rebuilt
+    itself, windows of 6..20 nucleotides, binding budgets, one window past
+    each rebuilt table's end."""
+    g = load_golden("length_cases.json.gz")
+    cases = g["cases"]
+    masks = np.zeros((len(cases), 2), np.uint64)
+    for j, c in enumerate(cases):
+        a = g["alphabets"][c["alpha"]]
+        assert [rows[r] for r in a["rows"]] == a["masses"]
+        for r in a["rows"][1:]:
+            masks[j, r >> 6] |= np.uint64(1) << np.uint64(r & 63)
+    su = np.array([c["su_mass"] for c in cases])
+    ob = np.array([c["obs_mass"] for c in cases])
+    ml = np.array([c["max_len"] for c in cases])
+    return g, cases, masks, su, ob, ml
+
+
+@pytest.mark.parametrize("engine", ["frontier", "replay"])
+def test_length_bounds_vs_reference_fixtures(setup, engine):
+    """Both stage-5 engines (length_bounds_alpha_device: the first-visit
+    frontier config 5 runs, and the round-4 DFS replay) against the
+    REFERENCE's results directly, not the oracle: lower, upper and the raise
+    past the reduced table's end, with each case's per-row caps (rate
+    profile) and max_modifications, grouped into one call per (profile,
+    max_modifications)."""
+    from spectrseqtools_amd import pipeline_device as PD
+
+    dp, rows, _, _ = setup
+    g, cases, masks, su, ob, ml = _reference_cases(rows)
+    n_rows = len(rows)
+    groups = {}
+    for j, c in enumerate(cases):
+        groups.setdefault((c["profile"], c["max_modifications"]), []).append(j)
+    n_ok = n_raise = 0
+    for (p, A), idx in sorted(groups.items()):
+        prof = g["profiles"][p]
+        caps_len = np.zeros((21, _native.MAX_ROWS), np.int32)
+        for L in range(21):
+            caps_len[L, :n_rows] = [round(L * r) for r in prof]
+        for j in idx:  # the case's own caps are the profile's (as the generator asserted)
+            a = g["alphabets"][cases[j]["alpha"]]
+            assert [int(caps_len[cases[j]["max_len"], r]) for r in a["rows"][1:]] == cases[j]["caps"][1:]
+        lower, upper, st, _, _ = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, np.full(21, A),
+                                                               sel=np.array(idx), engine=engine)
+        for j in idx:
+            c = cases[j]
+            if c["lower"] is None:  # the reference raises NotImplementedError (mass_table.py:389-393)
+                assert int(st[j]) != 0, (j, int(st[j]))
+                n_raise += 1
+                continue
+            assert int(st[j]) == 0 and (int(lower[j]), int(upper[j])) == (c["lower"], c["upper"]), \
+                (j, engine, int(st[j]), int(lower[j]), int(upper[j]), c["lower"], c["upper"])
+            n_ok += 1
+    assert n_ok >= 240 and n_raise == len(g["alphabets"])
+
+
+def test_length_bound_mirror_vs_reference_fixtures(setup):
+    """The drop-in call itself: mass_table.compute_sequence_length_bound on a
+    DynamicProgrammingTable reduced by
+    adapt_individual_modification_rates_by_alphabet_reduction (a GPU rebuild
+    of the reference's SHA-256) with the case's per-row rates and
+    SequenceInformation -- the reference's call sequence at
+    skeleton_building.py:212-224 -- equals the reference, and raises its
+    NotImplementedError past the table."""
+    from spectrseqtools_amd import mass_table as MTm
+    from spectrseqtools_amd.mass_explanation import MASS_NAMES
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE
+
+    dp0, rows, _, _ = setup
+    g, cases, _, _, _, _ = _reference_cases(rows)
+    eng = _native.get_engine(0)
+    n_ok = 0
+    for ai, a in enumerate(g["alphabets"]):
+        seq = MTm.SequenceInformation(max_len=20, su_mass=0.0, obs_mass=0.0, modification_rate=1.0)
+        dp = MTm.DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                         precision=TOLERANCE, seq=seq, engine=eng)
+        try:
+            keep = {"A", "C", "G", "U"} | {MASS_NAMES[m][0] for m in a["masses"][1:]}
+            dp.adapt_individual_modification_rates_by_alphabet_reduction(keep)
+            assert [m.mass for m in dp.masses] == a["masses"]
+            import hashlib
+
+            assert hashlib.sha256(np.ascontiguousarray(dp.table).tobytes()).hexdigest() == a["table_sha256"], ai
+            for c in (c for c in cases if c["alpha"] == ai):
+                prof = g["profiles"][c["profile"]]
+                for i, m in enumerate(dp.masses):
+                    if m.is_modification:
+                        m.modification_rate = prof[a["rows"][i]]
+                dp.seq = MTm.SequenceInformation(max_len=c["max_len"], su_mass=c["su_mass"],
+                                                 obs_mass=c["obs_mass"], modification_rate=c["modification_rate"])
+                for d in ("lower", "upper"):
+                    if c[d] is None:
+                        with pytest.raises(NotImplementedError):
+                            MTm.compute_sequence_length_bound(dp, d)
+                    else:
+                        assert MTm.compute_sequence_length_bound(dp, d) == c[d], (ai, c["su_mass"], d)
+                        n_ok += 1
+        finally:
+            dp.close()
+    assert n_ok >= 480
+
+
+def test_wide_windows_vs_oracle():
+    """Windows wider than one band (w_min masses: a tolerance far above the
+    reference's 10 ppm) cannot be laid out by the frontier (their roots would
+    span bands): the frontier answers them SST_ABORTED on their own and the
+    drop-in compute_sequence_length_bound hands them to the DFS replay, equal
+    to the oracle; windows just inside one band stay on the frontier."""
+    from spectrseqtools_amd import mass_table as MTm
+    from spectrseqtools_amd import pipeline_device as PD
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, TOLERANCE
+
+    eng = _native.get_engine(0)
+    rng = np.random.default_rng(5)
+    for tol in (0.02, 0.2, 0.3):  # window widths 2 tol obs / 1e-3 masses: inside one band, then beyond w_min
+        seq = MTm.SequenceInformation(max_len=8, su_mass=1500.0, obs_mass=1500.0, modification_rate=0.25)
+        dp = MTm.DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=tol,
+                                         precision=TOLERANCE, seq=seq, engine=eng)
+        try:
+            dp.adapt_individual_modification_rates_by_alphabet_reduction({"A", "C", "G", "U", "2C", "71C"})
+            ms = [m.mass for m in dp.masses]
+            tab = oracle.build_table(ms, max(ms) * 35, 32)
+            alph = oracle.Alphabet(ms, [m.is_modification for m in dp.masses],
+                                   [round(8 * m.modification_rate) for m in dp.masses])
+            sus = [float(x) for x in rng.uniform(650.0, 800.0, 3)]
+            for su in sus:
+                dp.seq = MTm.SequenceInformation(max_len=8, su_mass=su, obs_mass=su, modification_rate=0.25)
+                for d in ("lower", "upper"):
+                    want = oracle.length_bound(tab, 32, alph, su, su, tol, 8, 2, d)
+                    assert MTm.compute_sequence_length_bound(dp, d) == want, (tol, su, d)
+        finally:
+            dp.close()
+    # length_bounds_alpha_device (config 5's path, no replay behind it) at a
+    # wide tolerance: the wide windows alone report SST_ABORTED
+    seq = MTm.SequenceInformation(max_len=8, su_mass=1500.0, obs_mass=1500.0, modification_rate=0.25)
+    dp = MTm.DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=0.09, precision=TOLERANCE,
+                                     seq=seq, engine=eng)
+    try:
+        rows_full = [m.mass for m in dp.masses]
+        keep = [r for r, m in enumerate(rows_full) if m in CANONICAL]
+        masks = np.zeros((4, 2), np.uint64)
+        for r in keep:
+            masks[:, 0] |= np.uint64(1) << np.uint64(r)
+        su = np.array([1200.0, 2600.0, 3500.0, 4100.0])
+        ob = np.array([1200.0, 2000.0, 3500.0, 4100.0])
+        wb = min(rows_full[1:])
+        wide = np.ceil(0.09 * ob / TOLERANCE) * 2 + 1 > wb
+        assert wide.any() and not wide.all()
+        caps_len = np.full((21, _native.MAX_ROWS), 4, np.int32)
+        lower, upper, st, _, _ = PD.length_bounds_alpha_device(dp, masks, su, ob, np.full(4, 8), caps_len,
+                                                               np.full(21, 4))
+        ms = [0] + [rows_full[r] for r in keep]
+        tab = oracle.build_table(ms, max(ms) * 35, 32)
+        alph = oracle.Alphabet(ms, [False] * len(ms), [4] * len(ms))
+        for g in range(4):
+            if wide[g]:
+                assert int(st[g]) == _native.SST_ABORTED, (g, int(st[g]))
+                continue
+            want = [oracle.length_bound(tab, 32, alph, su[g], ob[g], 0.09, 8, 4, d) for d in ("lower", "upper")]
+            assert int(st[g]) == 0 and [int(lower[g]), int(upper[g])] == want, (g, int(st[g]), want)
+    finally:
+        dp.close()

@@ -131,3 +131,42 @@ def test_is_singleton_restatement_vs_reference():
     want = np.array([x[2] for x in g["queries"]])
     got = oracle.is_singleton_batch(q[:, 0], q[:, 1], ctx["masses"], ctx["tolerance"], ctx["precision"])
     assert want.sum() > 1000 and np.array_equal(got, want)
+
+
+def test_length_bound_reference_depth():
+    """compute_sequence_length_bound at config 5's depth (length_cases.json.gz,
+    tests/golden/make_length_golden.py: the reference's own call on 40 reduced
+    alphabets it rebuilt itself, windows of 6..20 nucleotides, per-row rate
+    profiles and max_modifications of 0..3 or round(0.5 L)): the oracle's
+    rebuilt tables have the reference's SHA-256, and both directions equal the
+    reference on every window (None: the reference raised).  Budgets bind:
+    enough windows' bounds differ from the budget-free ones."""
+    import concurrent.futures as cf
+
+    g = load_golden("length_cases.json.gz")
+    tabs = {}
+    for ai, a in enumerate(g["alphabets"]):
+        t = oracle.build_table(a["masses"], max(a["masses"]) * 35, 32)
+        assert list(t.shape) == a["table_shape"] and sha(t) == a["table_sha256"], ai
+        tabs[ai] = t
+    cases = g["cases"]
+    assert len(cases) >= 280 and sum(c["lower"] is None for c in cases) == len(g["alphabets"])
+    assert sum(c["nucleotides"] >= 15 for c in cases) >= 20  # windows of 15..20 nucleotides
+
+    def one(c, free=False):
+        a = g["alphabets"][c["alpha"]]
+        caps = [255] * len(c["caps"]) if free else c["caps"]
+        alph = oracle.Alphabet(a["masses"], c["is_mod"], caps)
+        return tuple(oracle.length_bound(tabs[c["alpha"]], 32, alph, c["su_mass"], c["obs_mass"], c["tolerance"],
+                                         c["max_len"], 255 if free else c["max_modifications"], d)
+                     for d in ("lower", "upper"))
+
+    with cf.ThreadPoolExecutor(8) as ex:  # ctypes releases the GIL
+        got = list(ex.map(one, cases))
+    for c, (lo, up) in zip(cases, got):
+        assert (lo, up) == (c["lower"], c["upper"]), (c["alpha"], c["su_mass"], lo, up, c["lower"], c["upper"])
+    # budgets bind on these windows (the first 60 answered ones are enough to show it)
+    live = [c for c in cases if c["lower"] is not None][:60]
+    with cf.ThreadPoolExecutor(8) as ex:
+        free = list(ex.map(lambda c: one(c, True), live))
+    assert sum(f != (c["lower"], c["upper"]) for c, f in zip(live, free)) >= 20
