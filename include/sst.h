@@ -473,16 +473,18 @@ int64_t sst_su_diff_queries(const double* su, const double* obs, const uint8_t* 
  * 4 * d_peak_off[g] + i, i < d_rows[g] (d_rows_* arrays of 4 * n_peaks):
  * su, observed mass, meta = breakage | sides << 2 | is_singleton << 4 | peak
  * position << 8, alive.  Peaks in any order (ranked by mass on the device, equal
- * masses in their given order), <= 4096 per spectrum;
- * shifts / sides as sst_step_rows_device.  A spectrum of more than 2048 rows
- * is held in HBM slices the table's context reserves (sst_pipe_reserve_rows,
- * before the stages run); without them it is an error.  d_err collects | 1 a
- * spectrum over 4096 peaks, 2 over 2048 rows with no slices reserved (or over
+ * masses in their given order), <= 16383 per spectrum (above 4096 in the
+ * reserved HBM slices); shifts / sides as sst_step_rows_device.  A spectrum of
+ * more than 2048 rows is held in HBM slices the table's context reserves
+ * (sst_pipe_reserve_rows, before the stages run); without them it is an
+ * error.  d_err collects | 1 a spectrum over 16383 peaks (or over 4096 with
+ * no slices reserved), 2 over 2048 rows with no slices reserved (or over
  * the reserved rows), 4 a window outside the pair class, 8 a window past a
  * table's end (the reference raises), 16 a dict too large for its hash, 32
  * rows out of mass order; the caller checks it. */
-/* Reserve the context's slices for spectra of up to max_rows rows (<= 16384:
- * 4 breakages x 4096 peaks) in the row stages (fix rounds, final dict, bins);
+/* Reserve the context's slices for spectra of up to max_rows rows (<= 65532:
+ * 4 breakages x 16383 peaks) in the row stages (classify above 4096 peaks, fix
+ * rounds, final dict, bins);
  * a no-op for max_rows <= 2048 or at most what is reserved.  Synchronises the
  * context's stream when it grows. */
 int sst_pipe_reserve_rows(sst_table* t, int64_t max_rows);
@@ -681,6 +683,33 @@ typedef struct sst_walk_args {
  * sst_pyset_table_size). */
 uint64_t sst_walk_scratch_bytes(uint32_t pos_cap, uint32_t len_cap, uint32_t expl_cap, uint32_t cand_cap,
                                 uint32_t tset_cap);
+
+/* The walk's re-query answers merged over rounds (skeleton_device's round
+ * loop; skeleton_building.py:114-196 issues them one explain call at a time,
+ * the device walk suspends and resumes, so a side's k-th re-query answer must
+ * be entry k of its merged list).  Per side sid of n_sides: the earlier
+ * rounds' merged entries (o_block[sid] = start << 32 | count into o_ptr /
+ * o_n / o_st; o_block NULL for the first round), then this round's
+ * (block[sid] likewise into ptr / n / st) -> m_block[sid] = start << 32 |
+ * count into m_ptr / m_n / m_st, sides in order.  m_* must hold the earlier
+ * rounds' total plus this round's entries; tot (u32[n_sides]) and off
+ * (u64[n_sides + 1]) are device scratch.  Device pointers, the ctx's stream. */
+typedef struct sst_requery_merge_args {
+  const int64_t* o_block;
+  const uint64_t* o_ptr;
+  const uint32_t* o_n;
+  const int8_t* o_st;
+  const int64_t* block;
+  const uint64_t* ptr;
+  const uint32_t* n;
+  const int8_t* st;
+  int64_t n_sides;
+  int64_t* m_block;
+  uint64_t* m_ptr;
+  uint32_t* m_n;
+  int8_t* m_st;
+} sst_requery_merge_args;
+int sst_requery_merge_device(sst_table* t, const sst_requery_merge_args* args, uint32_t* d_tot, uint64_t* d_off);
 /* CPython's table size after n distinct additions to an empty set. */
 uint32_t sst_pyset_table_size(uint32_t n);
 int sst_skel_walk_device(sst_table* t, const sst_walk_args* a);
@@ -857,6 +886,8 @@ typedef struct sst_lbf_stats {
   int64_t table_slots;     /* slots per hash table of the ring */
   int64_t node_cap;        /* node capacity per chunk */
   int64_t overflow_bits;   /* why chunks were split: 1 nodes / a band's records, 2 a hash table, 4 a band list */
+  int64_t groups;          /* (query, mass) groups of the completed chunks (the memo's distinct masses) */
+  int64_t edges;           /* left moves onto a mass > 0 of the completed chunks (candidate inserts) */
 } sst_lbf_stats;
 int sst_reach_lowest_device(sst_table* t, const uint64_t* d_alpha, const int64_t* d_words, const uint64_t* d_off,
                             int64_t n_spec, const uint32_t* d_bits, const uint64_t* d_lr_off, uint8_t* d_lr);
@@ -901,6 +932,7 @@ int64_t sst_pyset_order(const int32_t* keys, const int64_t* hashes, int64_t n, i
 #define SST_K_LENGTH_BOUND 15 /* k_length_fast / k_length_exact (length-bound batches) */
 #define SST_K_JACCARD 16      /* k_jaccard (sst_jaccard_device) */
 #define SST_K_PAIRS_ALPHA 17  /* k_pairs_alpha (sst_explain_pairs_alpha*) */
+#define SST_K_REQUERY_MERGE 18 /* k_requery_count + k_scan_u32 + k_requery_copy (sst_requery_merge_device) */
 #define SST_K_COUNT 24
 /* When enabled, every kernel launch of this ctx is bracketed by hipEvents
  * recorded on the ctx stream; sst_profile_read synchronises and returns the

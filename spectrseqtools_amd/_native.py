@@ -37,14 +37,14 @@ EXPORTS = (
     "sst_skel_walk_device", "sst_result_refs_device", "sst_dict_count_device", "sst_dict_build_device",
     "sst_reach_rows_device", "sst_length_bounds_reach_device", "sst_jaccard_device", "sst_skeleton_alpha_device",
     "sst_dict_list_device", "sst_fix_finish_device", "sst_pipe_reserve_rows", "sst_reach_lowest_device",
-    "sst_length_bounds_frontier_device", "sst_post_skeleton_device", "sst_ctx_trim",
+    "sst_length_bounds_frontier_device", "sst_post_skeleton_device", "sst_ctx_trim", "sst_requery_merge_device",
 )
 
 # kernel ids of sst_profile_read
 K_IS_VALID, K_EXPLAIN_SCAN, K_EXPLAIN_DEEP, K_EXPLAIN_NOMEMO, K_EXPLAIN_EXACT, K_EXPLAIN_EXPAND = 0, 1, 2, 3, 4, 5
 K_RESULT_PACK = 6
 (K_CLASSIFY_ROWS, K_FIX_ROUND, K_VALID_ALPHA, K_BINS_COUNT, K_BINS_EMIT, K_DICT, K_SKEL_WALK, K_REACH_ROWS,
- K_LENGTH_BOUND, K_JACCARD, K_PAIRS_ALPHA) = range(7, 18)
+ K_LENGTH_BOUND, K_JACCARD, K_PAIRS_ALPHA, K_REQUERY_MERGE) = range(7, 19)
 K_COUNT = 24  # SST_K_COUNT
 KERNEL_NAMES = {K_IS_VALID: "k_is_valid", K_EXPLAIN_SCAN: "k_explain_scan", K_EXPLAIN_DEEP: "k_explain_deferred",
                 K_EXPLAIN_EXPAND: "k_explain_expand",
@@ -52,7 +52,7 @@ KERNEL_NAMES = {K_IS_VALID: "k_is_valid", K_EXPLAIN_SCAN: "k_explain_scan", K_EX
                 K_CLASSIFY_ROWS: "k_classify_rows", K_FIX_ROUND: "k_fix_round", K_VALID_ALPHA: "k_valid_alpha",
                 K_BINS_COUNT: "k_bins_count", K_BINS_EMIT: "k_bins_emit", K_DICT: "k_dict_build",
                 K_SKEL_WALK: "k_skel_walk", K_REACH_ROWS: "k_reach_rows", K_LENGTH_BOUND: "k_length_bound",
-                K_JACCARD: "k_jaccard", K_PAIRS_ALPHA: "k_pairs_alpha"}
+                K_JACCARD: "k_jaccard", K_PAIRS_ALPHA: "k_pairs_alpha", K_REQUERY_MERGE: "k_requery_merge"}
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -94,11 +94,17 @@ class PostArgs(ctypes.Structure):
                 ("max_end_out", ctypes.c_void_p), ("err", ctypes.c_void_p)]
 
 
+class RequeryMergeArgs(ctypes.Structure):
+    """sst_requery_merge_args (include/sst.h): the walk's re-query answers merged over rounds."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("o_block", "o_ptr", "o_n", "o_st", "block", "ptr", "n", "st")] + \
+        [("n_sides", ctypes.c_int64)] + [(n, ctypes.c_void_p) for n in ("m_block", "m_ptr", "m_n", "m_st")]
+
+
 class LbfStats(ctypes.Structure):
     """sst_lbf_stats (include/sst.h): the first-visit frontier's record."""
     _fields_ = [(n, ctypes.c_int64) for n in ("live", "nodes", "chunks", "splits", "aborted", "bands", "key_words",
                                              "max_band_groups", "max_band_nodes", "table_slots", "node_cap",
-                                             "overflow_bits")]
+                                             "overflow_bits", "groups", "edges")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -295,6 +301,8 @@ def load_library(path=LIB_PATH):
     lib.sst_length_bounds_frontier_device.restype = _I
     lib.sst_post_skeleton_device.argtypes = [_P, ctypes.POINTER(PostArgs)]
     lib.sst_post_skeleton_device.restype = _I
+    lib.sst_requery_merge_device.argtypes = [_P, ctypes.POINTER(RequeryMergeArgs), _P, _P]
+    lib.sst_requery_merge_device.restype = _I
     lib.sst_jaccard_device.argtypes = [_P, ctypes.POINTER(JaccardArgs)]
     lib.sst_jaccard_device.restype = _I
     lib.sst_skeleton_alpha_device.argtypes = [_P, _I64, _P, _P, _P, _P, _P]

@@ -2198,6 +2198,17 @@ static int pipe_args(sst_table* t, const double* d_obs, const int64_t* d_peak_of
   return SST_OK;
 }
 
+// the context's big-spectrum slices into the stage's arguments (none reserved:
+// a spectrum of more than kPipeMaxRows rows is reported, bit 2)
+static void big_args(sst_ctx* c, sst::PipeArgs& a) {
+  if (!c->pipe_big_rows) return;
+  a.big = (uint8_t*)c->pipe_big.p;
+  a.big_rows = c->pipe_big_rows;
+  a.big_slots = c->pipe_big_slots;
+  a.big_stride = sst::pipe_big_layout(a.big_rows, a.big_slots).stride;
+  a.big_wg = c->pipe_big_wg;
+}
+
 int sst_classify_rows_device(sst_table* t, const double* d_obs, const int64_t* d_peak_off, int64_t n_spec,
                              int64_t n_peaks, const double* d_intensity, double intensity_cutoff, double mass_cutoff,
                              const double* d_su_seq, const double* shifts, const uint8_t* sides, int n_shifts,
@@ -2224,6 +2235,7 @@ int sst_classify_rows_device(sst_table* t, const double* d_obs, const int64_t* d
   a.alive = d_alive;
   a.cnt = d_rows;
   a.err = d_err;
+  big_args(c, a);  // spectra of more than kPipeMaxPeaks peaks: k_classify_rows_big in the reserved slices
   Prof p(c, SST_K_CLASSIFY_ROWS);
   HIP_OK(c, launch_classify_rows(t->args, a, c->n_cu, c->stream));
   return SST_OK;
@@ -2248,15 +2260,16 @@ static int exact_io(sst_ctx* c, const sst_exact_io* x, sst::PipeArgs& a) {
   return SST_OK;
 }
 
-// the context's big-spectrum slices into the stage's arguments (none reserved:
-// a spectrum of more than kPipeMaxRows rows is reported, bit 2)
-static void big_args(sst_ctx* c, sst::PipeArgs& a) {
-  if (!c->pipe_big_rows) return;
-  a.big = (uint8_t*)c->pipe_big.p;
-  a.big_rows = c->pipe_big_rows;
-  a.big_slots = c->pipe_big_slots;
-  a.big_stride = sst::pipe_big_layout(a.big_rows, a.big_slots).stride;
-  a.big_wg = c->pipe_big_wg;
+
+int sst_requery_merge_device(sst_table* t, const sst_requery_merge_args* args, uint32_t* d_tot, uint64_t* d_off) {
+  if (!t || !args || args->n_sides < 0 || (args->n_sides > 0 && (!args->block || !args->m_block || !d_tot || !d_off)))
+    return SST_E_ARG;
+  sst_ctx* c = t->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (int rc = set_device(c)) return rc;
+  Prof p(c, SST_K_REQUERY_MERGE);
+  HIP_OK(c, sst::launch_requery_merge(*args, d_tot, d_off, c->stream));
+  return SST_OK;
 }
 
 int sst_pipe_reserve_rows(sst_table* t, int64_t max_rows) {
@@ -3402,7 +3415,14 @@ static int lbf_frontier(sst_table* t, sst_ctx::LbfWs& W, const double* d_su, con
     a.rb = bits_for(h.max_win > 0 ? h.max_win - 1 : 0);
     // unary keys: root bits, one zero per kept rank, one 1 per left move (<= hi / w_min)
     const int need = a.rb + (int)h.max_need;  // (k_lbf_setup excluded every query beyond 256 bits)
-    const int kw = need <= 64 ? 1 : need <= 128 ? 2 : need <= 256 ? 4 : 0;
+    int kw = need <= 64 ? 1 : need <= 128 ? 2 : need <= 256 ? 4 : 0;
+    // (tests: SST_LBF_MIN_KEY_WORDS=2|4 runs a batch with wider keys than it
+    // needs -- wide keys are otherwise reached only by windows whose memo no
+    // oracle could check; the results must not change)
+    if (const char* mk = getenv("SST_LBF_MIN_KEY_WORDS")) {
+      const int m = atoi(mk);
+      if (kw && (m == 2 || m == 4) && m > kw) kw = m;
+    }
     if (!kw || a.rb > 32) return fail(c, SST_E_ARG, "length bounds (frontier): first-visit keys beyond 256 bits");
     a.rstride = (int)std::max<uint32_t>(1, h.max_win);
     a.n_bands = n_bands;
@@ -3478,7 +3498,11 @@ static int lbf_frontier(sst_table* t, sst_ctx::LbfWs& W, const double* d_su, con
       stats->nodes += h.node_ctr;
       stats->bands = std::max<int64_t>(stats->bands, n_bands);
       stats->key_words = std::max<int64_t>(stats->key_words, kw);
-      for (uint32_t x : band_groups) stats->max_band_groups = std::max<int64_t>(stats->max_band_groups, x);
+      for (uint32_t x : band_groups) {
+        stats->max_band_groups = std::max<int64_t>(stats->max_band_groups, x);
+        stats->groups += x;
+      }
+      stats->edges += (int64_t)h.edges;
       for (int b = 0; b < n_bands; ++b)
         stats->max_band_nodes = std::max<int64_t>(stats->max_band_nodes, band_start[b + 1] - band_start[b]);
       stats->table_slots = (int64_t)S;

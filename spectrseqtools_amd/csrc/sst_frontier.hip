@@ -739,10 +739,12 @@ __global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
   const uint32_t r1 = b1 >= nn ? s1 : next_group_start(a, s0 + (uint32_t)b1, s1);
   const uint64_t le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
   int clo = 255, chi = -1;  // the values of the group open at the step's start
+  uint32_t n_edges = 0;     // (wave-uniform) left moves onto a mass > 0: the run's edge count
   for (uint32_t c0 = r0; c0 < r1; c0 += 64u) {
     const uint32_t x = c0 + (uint32_t)lane;
     const bool live = x < r1;
     const uint8_t f = live ? a.flags[x] : (uint8_t)0;
+    n_edges += (uint32_t)__builtin_popcountll(__ballot((f & kFLeft) && !(f & kFZero)));
     int vl = 255, vh = -1;
     if (f & kFLeft) {
       vl = 1;  // a left move onto mass 0: 0 + 1
@@ -784,6 +786,7 @@ __global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
     clo = __shfl(vl, last, 64);
     chi = __shfl(vh, last, 64);
   }
+  if (lane == 0 && n_edges) atomicAdd((unsigned long long*)&a.ctl->edges, (unsigned long long)n_edges);
 }
 
 // per query: min / max over the window's roots (mass_table.py:459-487)

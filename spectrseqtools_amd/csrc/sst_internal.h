@@ -326,6 +326,7 @@ struct FCtl {
   uint64_t max_hi;
   uint32_t node_ticket;  // k_lbf_nodes' next id range (reset per band by k_lbf_mark)
   uint32_t max_need;     // max over the chunk's queries of K + hi / w_min (key bits besides the root index)
+  uint64_t edges;        // left moves onto a mass > 0 (k_lbf_values: one add per wave and band)
 };
 struct FrontierArgs {
   const uint32_t* list;  // the list pass's live queries
@@ -511,7 +512,8 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
 // config 5 on the device (sst_pipe.hip)
 constexpr int kPipeMaxPeaks = 4096;  // peaks per spectrum the classify workgroup holds (77 KB of LDS)
 constexpr int kPipeMaxRows = 2048;   // rows per spectrum the LDS variants of the row kernels hold
-constexpr int kPipeBigRows = 4 * kPipeMaxPeaks;  // rows per spectrum in the HBM-scratch variants
+constexpr int kPipeMaxPeaksBig = 16383;  // peaks per spectrum k_classify_rows_big takes (u16 peak and row indices)
+constexpr int kPipeBigRows = 4 * kPipeMaxPeaksBig;  // rows per spectrum in the HBM-scratch variants (< 2^16)
 // A spectrum of more than kPipeMaxRows rows is handled by the *_big variants
 // of k_fix_round / k_dict / k_fix_finish / k_bins_*: the same code over a
 // workgroup's slice of HBM scratch (PipeArgs big*) instead of LDS arrays,
@@ -627,6 +629,7 @@ struct DictArgs {
 hipError_t launch_dict(const TableArgs& t, const PipeArgs& a, const DictArgs& d, int mode, int n_wg,
                        hipStream_t st);
 hipError_t launch_scan_u32(const uint32_t* in, uint64_t* out, int64_t n, hipStream_t st);
+hipError_t launch_requery_merge(const sst_requery_merge_args& a, uint32_t* tot, uint64_t* off, hipStream_t st);
 // the skeleton walk (sst_skel.hip, k_skel_walk): the public sst_walk_args
 constexpr int kWalkMaxRounds = SST_WALK_MAX_ROUNDS;
 enum { kWalkDone = SST_WALK_DONE, kWalkSuspended = SST_WALK_SUSPENDED, kWalkBig = SST_WALK_BIG,

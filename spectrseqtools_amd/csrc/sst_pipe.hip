@@ -105,119 +105,194 @@ struct ClsLds {
   uint16_t ord[kPipeMaxPeaks];      // peaks in (mass, position) order
   uint16_t kidx[4][kPipeMaxPeaks];
   uint8_t keep[kPipeMaxPeaks];
+};
+struct ClsSmall {  // both variants: the block scan's words, the row masses
   uint32_t kcnt[4];
   int64_t masses[kMaxRows];
   uint32_t w[16];
 };
+// one spectrum's peak arrays: the LDS ones (<= kPipeMaxPeaks peaks) or a
+// workgroup's slice of the pipeline's HBM scratch (k_classify_rows_big)
+struct ClsView {
+  double* obs;
+  uint16_t* ord;
+  uint16_t* kidx[4];
+  uint8_t* keep;
+};
+// the slice bytes the big variant needs for P peaks
+__device__ __forceinline__ uint64_t cls_slice_bytes(uint32_t P) { return 29ull * P + 4 * 256; }
+__device__ __forceinline__ ClsView cls_big_view(uint8_t* p, uint32_t P) {
+  auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
+  ClsView V;
+  uint64_t o = 0;
+  V.obs = (double*)(p + o);
+  o += up(8ull * P);
+  V.ord = (uint16_t*)(p + o);
+  o += up(2ull * P);
+  for (int k = 0; k < 4; ++k) {
+    V.kidx[k] = (uint16_t*)(p + o);
+    o += up(2ull * P);
+  }
+  V.keep = p + o;
+  return V;
+}
+
+// classify_fragments (fragment_classification.py:17-101) for spectrum g of P
+// peaks, one workgroup: A7 per peak and breakage, the filters, the SU order
+// of the kept rows (breakage streams merged), is_singleton
+__device__ __forceinline__ void classify_spec(const TableArgs& t, const PipeArgs& a, ClsSmall& S, const ClsView& V,
+                                              int64_t g, int64_t p0, uint32_t P) {
+  const double su_seq = a.su_seq[g];
+  for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) {
+    const double o = a.obs[p0 + p];
+    V.obs[p] = o;
+    uint8_t kp = 0;
+    for (int k = 0; k < a.n_shifts; ++k) {
+      const double su = o - a.shift[k];
+      double lof, hif;
+      quantise_lean(su, a.tol * o, a.prec, a.rprec, lof, hif);
+      const int8_t code =
+          valid_window(t.valid, t.limit, (int64_t)lof, (int64_t)hif, t.full_lo, t.full_hi, t.first_reach);
+      if (a.valid_out) a.valid_out[(int64_t)k * a.n_peaks + p0 + p] = code;
+      if (code < 0) atomicOr(a.err, 8u);  // is_valid_mass raises: the reference's classify would too
+      const bool inten = a.intensity ? a.intensity[p0 + p] > a.intensity_cutoff : true;
+      const bool full = (a.sides[k] & 3) == 3;
+      const bool keep = code == 1 && inten && o < a.mass_cutoff && su < su_seq + a.max_variance &&
+                        (su > su_seq - a.max_variance || !full);
+      kp |= (uint8_t)keep << k;
+    }
+    V.keep[p] = kp;
+  }
+  __syncthreads();
+  // the peaks in ascending mass order, equal masses in their given order (a
+  // peak list need not be sorted; a breakage's rows are then in SU order)
+  const bool sorted = peaks_sorted(V.obs, P);
+  for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) {
+    uint32_t rank = p;
+    if (!sorted) {
+      const double o = V.obs[p];
+      rank = 0;
+      for (uint32_t q = 0; q < P; ++q) {
+        const double v = V.obs[q];
+        rank += (v < o) | ((v == o) & (q < p));
+      }
+    }
+    V.ord[rank] = (uint16_t)p;
+  }
+  __syncthreads();
+  for (int k = 0; k < a.n_shifts; ++k) {
+    uint32_t carry = 0;
+    for (uint32_t q0 = 0; q0 < P; q0 += blockDim.x) {
+      const uint32_t i = q0 + threadIdx.x;
+      const uint32_t p = i < P ? V.ord[i] : 0u;
+      const uint32_t f = i < P ? (V.keep[p] >> k) & 1u : 0u;
+      uint32_t tot;
+      const uint32_t ex = block_excl(f, S.w, tot);
+      if (f) V.kidx[k][carry + ex] = (uint16_t)p;
+      carry += tot;
+    }
+    if (threadIdx.x == 0) S.kcnt[k] = carry;
+  }
+  __syncthreads();
+  // every kept row's place in the spectrum's SU order (all breakages)
+  uint32_t n = 0;
+  for (int k = 0; k < a.n_shifts; ++k) n += S.kcnt[k];
+  const int64_t base = 4 * p0;
+  for (int k = 0; k < a.n_shifts; ++k) {
+    const double sk = a.shift[k];
+    for (uint32_t j = threadIdx.x; j < S.kcnt[k]; j += blockDim.x) {
+      const uint32_t p = V.kidx[k][j];
+      const double su = V.obs[p] - sk;
+      uint32_t pos = j;
+      for (int k2 = 0; k2 < a.n_shifts; ++k2) {
+        if (k2 == k) continue;
+        const double s2 = a.shift[k2];
+        uint32_t lo = 0, hi = S.kcnt[k2];
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi) >> 1;
+          const double v = V.obs[V.kidx[k2][mid]] - s2;
+          if (v < su || (v == su && k2 < k)) lo = mid + 1;
+          else hi = mid;
+        }
+        pos += lo;
+      }
+      // is_singleton (:104-119): a table row mass (the sentinel 0 included) in the window
+      int64_t lo, hi;
+      quantise(su, a.tol * V.obs[p], false, a.tol, a.prec, a.rprec, lo, hi);
+      int l = 0, r = a.n_masses;
+      while (l < r) {
+        const int mid = (l + r) >> 1;
+        if (S.masses[mid] < lo) l = mid + 1;
+        else r = mid;
+      }
+      const bool single = lo <= hi && l < a.n_masses && S.masses[l] <= hi;
+      a.r_su[base + pos] = su;
+      a.r_ob[base + pos] = V.obs[p];
+      a.r_meta[base + pos] = (uint32_t)k | ((uint32_t)a.sides[k] << 2) | ((uint32_t)single << 4) | (p << 8);
+      a.alive[base + pos] = 1;
+    }
+  }
+  if (threadIdx.x == 0) a.cnt[g] = n;
+  __syncthreads();
+}
 
 }  // namespace
 
 __global__ __launch_bounds__(kPipeWG) void k_classify_rows(TableArgs t, PipeArgs a) {
   __shared__ ClsLds L;
-  for (int r = threadIdx.x; r < a.n_masses; r += blockDim.x) L.masses[r] = a.masses[r];
+  __shared__ ClsSmall S;
+  for (int r = threadIdx.x; r < a.n_masses; r += blockDim.x) S.masses[r] = a.masses[r];
   __syncthreads();
+  ClsView V;  // (assigned, not a constant initializer: LDS addresses are not constants)
+  V.obs = L.obs;
+  V.ord = L.ord;
+  for (int k = 0; k < 4; ++k) V.kidx[k] = L.kidx[k];
+  V.keep = L.keep;
   for (int64_t g = blockIdx.x; g < a.n_spec; g += gridDim.x) {
     const int64_t p0 = a.peak_off[g];
     const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
-    if (P > (uint32_t)kPipeMaxPeaks) {
-      if (threadIdx.x == 0) {
+    if (P > (uint32_t)kPipeMaxPeaks) {  // k_classify_rows_big's (or rejected there)
+      if (threadIdx.x == 0 && !a.big) {
         atomicOr(a.err, 1u);
         a.cnt[g] = 0;
       }
       continue;
     }
-    const double su_seq = a.su_seq[g];
-    for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) {
-      const double o = a.obs[p0 + p];
-      L.obs[p] = o;
-      uint8_t kp = 0;
-      for (int k = 0; k < a.n_shifts; ++k) {
-        const double su = o - a.shift[k];
-        double lof, hif;
-        quantise_lean(su, a.tol * o, a.prec, a.rprec, lof, hif);
-        const int8_t code =
-            valid_window(t.valid, t.limit, (int64_t)lof, (int64_t)hif, t.full_lo, t.full_hi, t.first_reach);
-        if (a.valid_out) a.valid_out[(int64_t)k * a.n_peaks + p0 + p] = code;
-        if (code < 0) atomicOr(a.err, 8u);  // is_valid_mass raises: the reference's classify would too
-        const bool inten = a.intensity ? a.intensity[p0 + p] > a.intensity_cutoff : true;
-        const bool full = (a.sides[k] & 3) == 3;
-        const bool keep = code == 1 && inten && o < a.mass_cutoff && su < su_seq + a.max_variance &&
-                          (su > su_seq - a.max_variance || !full);
-        kp |= (uint8_t)keep << k;
-      }
-      L.keep[p] = kp;
-    }
+    classify_spec(t, a, S, V, g, p0, P);
+  }
+}
+
+// spectra of more than kPipeMaxPeaks peaks: the same code over a workgroup's
+// slice of the pipeline's HBM scratch (sst_pipe_reserve_rows); spectrum g
+// goes to workgroup g % gridDim.x, found by a coalesced scan of the peak counts
+__global__ __launch_bounds__(kPipeWG) void k_classify_rows_big(TableArgs t, PipeArgs a) {
+  __shared__ ClsSmall S;
+  __shared__ uint32_t s_list[kPipeWG];
+  __shared__ uint32_t s_n;
+  for (int r = threadIdx.x; r < a.n_masses; r += blockDim.x) S.masses[r] = a.masses[r];
+  uint8_t* slice = a.big + (uint64_t)blockIdx.x * a.big_stride;
+  const int64_t G = gridDim.x;
+  for (int64_t c0 = 0; (int64_t)blockIdx.x + c0 * G < a.n_spec; c0 += blockDim.x) {
+    if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
-    // the peaks in ascending mass order, equal masses in their given order (a
-    // peak list need not be sorted; a breakage's rows are then in SU order)
-    const bool sorted = peaks_sorted(L.obs, P);
-    for (uint32_t p = threadIdx.x; p < P; p += blockDim.x) {
-      uint32_t rank = p;
-      if (!sorted) {
-        const double o = L.obs[p];
-        rank = 0;
-        for (uint32_t q = 0; q < P; ++q) {
-          const double v = L.obs[q];
-          rank += (v < o) | ((v == o) & (q < p));
+    const int64_t gi = (int64_t)blockIdx.x + (c0 + threadIdx.x) * G;
+    if (gi < a.n_spec && a.peak_off[gi + 1] - a.peak_off[gi] > kPipeMaxPeaks) s_list[atomicAdd(&s_n, 1u)] = threadIdx.x;
+    __syncthreads();
+    const uint32_t n = s_n;
+    for (uint32_t k = 0; k < n; ++k) {
+      const int64_t g = (int64_t)blockIdx.x + (c0 + s_list[k]) * G;
+      const int64_t p0 = a.peak_off[g];
+      const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
+      if (P > (uint32_t)kPipeMaxPeaksBig || (uint64_t)P * (uint64_t)a.n_shifts > a.big_rows ||
+          cls_slice_bytes(P) > a.big_stride) {
+        if (threadIdx.x == 0) {
+          atomicOr(a.err, 1u);
+          a.cnt[g] = 0;
         }
+        continue;
       }
-      L.ord[rank] = (uint16_t)p;
+      classify_spec(t, a, S, cls_big_view(slice, P), g, p0, P);
     }
-    __syncthreads();
-    for (int k = 0; k < a.n_shifts; ++k) {
-      uint32_t carry = 0;
-      for (uint32_t q0 = 0; q0 < P; q0 += blockDim.x) {
-        const uint32_t i = q0 + threadIdx.x;
-        const uint32_t p = i < P ? L.ord[i] : 0u;
-        const uint32_t f = i < P ? (L.keep[p] >> k) & 1u : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_excl(f, L.w, tot);
-        if (f) L.kidx[k][carry + ex] = (uint16_t)p;
-        carry += tot;
-      }
-      if (threadIdx.x == 0) L.kcnt[k] = carry;
-    }
-    __syncthreads();
-    // every kept row's place in the spectrum's SU order (all breakages)
-    uint32_t n = 0;
-    for (int k = 0; k < a.n_shifts; ++k) n += L.kcnt[k];
-    const int64_t base = 4 * p0;
-    for (int k = 0; k < a.n_shifts; ++k) {
-      const double sk = a.shift[k];
-      for (uint32_t j = threadIdx.x; j < L.kcnt[k]; j += blockDim.x) {
-        const uint32_t p = L.kidx[k][j];
-        const double su = L.obs[p] - sk;
-        uint32_t pos = j;
-        for (int k2 = 0; k2 < a.n_shifts; ++k2) {
-          if (k2 == k) continue;
-          const double s2 = a.shift[k2];
-          uint32_t lo = 0, hi = L.kcnt[k2];
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            const double v = L.obs[L.kidx[k2][mid]] - s2;
-            if (v < su || (v == su && k2 < k)) lo = mid + 1;
-            else hi = mid;
-          }
-          pos += lo;
-        }
-        // is_singleton (:104-119): a table row mass (the sentinel 0 included) in the window
-        int64_t lo, hi;
-        quantise(su, a.tol * L.obs[p], false, a.tol, a.prec, a.rprec, lo, hi);
-        int l = 0, r = a.n_masses;
-        while (l < r) {
-          const int mid = (l + r) >> 1;
-          if (L.masses[mid] < lo) l = mid + 1;
-          else r = mid;
-        }
-        const bool single = lo <= hi && l < a.n_masses && L.masses[l] <= hi;
-        a.r_su[base + pos] = su;
-        a.r_ob[base + pos] = L.obs[p];
-        a.r_meta[base + pos] = (uint32_t)k | ((uint32_t)a.sides[k] << 2) | ((uint32_t)single << 4) | (p << 8);
-        a.alive[base + pos] = 1;
-      }
-    }
-    if (threadIdx.x == 0) a.cnt[g] = n;
-    __syncthreads();
   }
 }
 
@@ -1111,6 +1186,7 @@ hipError_t launch_bins_emit(const TableArgs& t, const PipeArgs& a, int n_wg, hip
 hipError_t launch_classify_rows(const TableArgs& t, const PipeArgs& a, int n_wg, hipStream_t st) {
   if (a.n_spec <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_classify_rows, dim3(n_wg), dim3(kPipeWG), 0, st, t, a);
+  if (a.big) hipLaunchKernelGGL(k_classify_rows_big, dim3(a.big_wg), dim3(kPipeWG), 0, st, t, a);
   return hipGetLastError();
 }
 hipError_t launch_fix_finish(const PipeArgs& a, int n_wg, hipStream_t st) {

@@ -173,6 +173,7 @@ __device__ bool ref_candidates(Lane& L, uint32_t cand_cap, uint64_t ptr, uint32_
   const uint8_t* p = (const uint8_t*)ptr;
   for (uint32_t c = 0; c < n; ++c) {
     const int k = p[0];
+    if (k > 127) return false;  // a ref holds 7 length bits: a side with such an explanation ends SST_WALK_LIMIT
     L.cref[c] = ref_ptr(p, k);
     p += 1 + k;
   }
@@ -790,7 +791,7 @@ hipError_t launch_skel_alpha(int64_t n_spec, const int32_t* max_len, const uint6
 // (mass_table.py:94-100).  One workgroup per spectrum; the peaks of kept
 // terminal rows as an LDS bitmap.  The caller then runs is_valid on that
 // alphabet (sst_valid_rows_alpha_device) over alive_out.
-constexpr int kPostPeaks = 4096;
+constexpr int kPostPeaks = kPipeMaxPeaksBig + 1;  // the classify kernels' peak limit
 __global__ __launch_bounds__(256) void k_post_skel(sst_post_args a, uint64_t canon0, uint64_t canon1) {
   __shared__ uint32_t peaks[kPostPeaks / 32];
   __shared__ uint64_t names[2];
@@ -863,6 +864,47 @@ __global__ __launch_bounds__(256) void k_post_skel(sst_post_args a, uint64_t can
     __syncthreads();
   }
 }
+// the walk's re-query answers merged over rounds (skeleton_device's round
+// loop): per side, the merged view's entries of the earlier rounds, then this
+// round's block -- round-major per side, sides in order, as the walk's
+// resolved() reads a single round.  count: per side totals; copy: one lane
+// per side (its entries are few), at the exclusive scan of the totals.
+__global__ void k_requery_count(const int64_t* o_block, const int64_t* block, uint32_t* tot, int64_t n_sides) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_sides) return;
+  const uint32_t o = o_block ? (uint32_t)((uint64_t)o_block[i] & 0xFFFFFFFFull) : 0u;
+  tot[i] = o + (uint32_t)((uint64_t)block[i] & 0xFFFFFFFFull);
+}
+__global__ void k_requery_copy(sst_requery_merge_args a, const uint64_t* off) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_sides) return;
+  uint64_t at = off[i];
+  const uint64_t start = at;
+  if (a.o_block) {
+    const uint64_t b = (uint64_t)a.o_block[i];
+    for (uint64_t k = b >> 32, e = (b >> 32) + (b & 0xFFFFFFFFull); k < e; ++k, ++at) {
+      a.m_ptr[at] = a.o_ptr[k];
+      a.m_n[at] = a.o_n[k];
+      a.m_st[at] = a.o_st[k];
+    }
+  }
+  const uint64_t b = (uint64_t)a.block[i];
+  for (uint64_t k = b >> 32, e = (b >> 32) + (b & 0xFFFFFFFFull); k < e; ++k, ++at) {
+    a.m_ptr[at] = a.ptr[k];
+    a.m_n[at] = a.n[k];
+    a.m_st[at] = a.st[k];
+  }
+  a.m_block[i] = (int64_t)((start << 32) | (at - start));
+}
+hipError_t launch_requery_merge(const sst_requery_merge_args& a, uint32_t* tot, uint64_t* off, hipStream_t st) {
+  if (a.n_sides <= 0) return hipSuccess;
+  const unsigned g = (unsigned)((a.n_sides + 255) / 256);
+  hipLaunchKernelGGL(k_requery_count, dim3(g), dim3(256), 0, st, a.o_block, a.block, tot, a.n_sides);
+  if (hipError_t e = launch_scan_u32(tot, off, a.n_sides, st)) return e;
+  hipLaunchKernelGGL(k_requery_copy, dim3(g), dim3(256), 0, st, a, (const uint64_t*)off);
+  return hipGetLastError();
+}
+
 hipError_t launch_post_skel(const sst_post_args& a, uint64_t canon0, uint64_t canon1, int n_wg, hipStream_t st) {
   if (a.n_spec <= 0) return hipSuccess;
   const int64_t g = a.n_spec < (int64_t)n_wg ? a.n_spec : (int64_t)n_wg;

@@ -10,7 +10,9 @@ round: how many spectra are still reducing) and sizes the bin answers (one
 Rows of spectrum g sit in slots 4 * peak_off[g] + i (i < rows[g]), in the
 SU order of its classify_fragments frame, so a row's slot offset is the
 `index` Predictor.predict gives it (prediction.py:68-72).  PyTorch provides
-the device memory only; every computation is the library's.
+the device memory, plus the index gathers that set up a masked-explain pass's
+per-query budget rows (_lens_pass); every stage's computation -- the rounds'
+re-query merge included (sst_requery_merge_device) -- is the library's.
 """
 import ctypes
 import os
@@ -26,7 +28,8 @@ from .pipeline import mask_rows, row_masks
 
 _PROGRESS = os.environ.get("SST_PIPE_PROGRESS") == "1"  # per-launch lines of the long stages on stderr
 LB_NOT_RUN = -6  # length_device(spectra=...): the bounds of a spectrum outside the sample
-ERR_BITS = {1: "a spectrum has more than 4096 peaks", 2: "a spectrum has more rows than the reserved slices hold",
+MAX_PEAKS = 16383  # peaks per spectrum (sst_internal.h kPipeMaxPeaksBig: above 4096 in HBM slices)
+ERR_BITS = {1: f"a spectrum has more than {MAX_PEAKS} peaks", 2: "a spectrum has more rows than the reserved slices hold",
             4: "a window outside the pair class", 8: "is_valid_mass raised (a window past a table's end)",
             16: "an explanation dict too large for the LDS hash", 32: "rows out of mass order",
             64: "an exact-mode query list overflowed", 128: "an exact-mode answer raised or was capped"}
@@ -141,7 +144,8 @@ def classify_device(dp_table, obs, offsets, su_seq, breakage_dict, intensity=Non
     # spectra of more than 2048 rows run in the context's HBM slices (sst_pipe_reserve_rows)
     peaks = np.diff(np.asarray(offsets, dtype=np.int64))
     if len(peaks):
-        eng.check(eng._lib.sst_pipe_reserve_rows(dp_table.device_table.handle, min(int(peaks.max()), 4096) * len(shifts)),
+        eng.check(eng._lib.sst_pipe_reserve_rows(dp_table.device_table.handle,
+                                                 min(int(peaks.max()), MAX_PEAKS) * len(shifts)),
                   "sst_pipe_reserve_rows")
     su = torch.empty(max(1, 4 * P), dtype=torch.float64, device=dev)
     ob = torch.empty_like(su)
@@ -587,31 +591,34 @@ def _masked_explain_refs(dp_table, alpha_dev, mass, thr, spec, n, max_len, dst, 
     return [res]
 
 
-def merge_requery_round(m_sid, m_ptr, m_n, m_st, block, p_, n_, s_, n_sides):
+def merge_requery_round(dp_table, merged, n_merged, block, p_, n_, s_, n_sides):
     """Append one re-query round's answers to the merged per-side lists the
-    walk reads as a single round.  block[sid] = start << 32 | count: side
-    sid's entries of this round, contiguous in its lane's order, in p_ / n_ /
-    s_.  Returns the merged (sid, ptr, n, st) ordered by side and, per side,
-    round-major (a stable sort of the concatenation), and the walk's view
-    (start << 32 | count per side, ptr, n, st)."""
+    walk reads as a single round (sst_requery_merge_device: per side the
+    earlier rounds' entries, then this round's; sides in order).  merged:
+    the previous view (block, ptr, n, st) or None; n_merged its entries;
+    block[sid] = start << 32 | count: side sid's entries of this round in p_
+    / n_ / s_.  Returns the new view (start << 32 | count per side, ptr, n,
+    st) and its entry count -- known on the host, so no device read-back."""
     import torch
 
     dev = block.device
-    cnt_s = block & 0xFFFFFFFF
-    sides_nz = torch.nonzero(cnt_s).flatten()
-    c_nz = cnt_s[sides_nz]
-    first = torch.cumsum(c_nz, 0) - c_nz
-    idx = torch.repeat_interleave(block[sides_nz] >> 32, c_nz) + (
-        torch.arange(int(c_nz.sum().item()), device=dev) - torch.repeat_interleave(first, c_nz))
-    m_sid = torch.cat([m_sid, torch.repeat_interleave(sides_nz, c_nz)])
-    m_ptr = torch.cat([m_ptr, p_[idx]])
-    m_n = torch.cat([m_n, n_[idx]])
-    m_st = torch.cat([m_st, s_[idx]])
-    order = torch.sort(m_sid, stable=True).indices
-    m_sid, m_ptr, m_n, m_st = m_sid[order], m_ptr[order], m_n[order], m_st[order]
-    per = torch.bincount(m_sid, minlength=n_sides)
-    start = torch.cumsum(per, 0) - per
-    return m_sid, m_ptr, m_n, m_st, ((start << 32) | per, m_ptr, m_n, m_st)
+    n_new = n_merged + len(p_)
+    m_block = torch.empty(max(1, n_sides), dtype=torch.int64, device=dev)
+    m_ptr = torch.empty(max(1, n_new), dtype=torch.int64, device=dev)
+    m_n = torch.empty(max(1, n_new), dtype=torch.int32, device=dev)
+    m_st = torch.empty(max(1, n_new), dtype=torch.int8, device=dev)
+    tot = torch.empty(max(1, n_sides), dtype=torch.int32, device=dev)
+    off = torch.empty(n_sides + 1, dtype=torch.int64, device=dev)
+    a = _native.RequeryMergeArgs()
+    if merged is not None:
+        a.o_block, a.o_ptr, a.o_n, a.o_st = (t.data_ptr() for t in merged)
+    a.block, a.ptr, a.n, a.st = block.data_ptr(), p_.data_ptr(), n_.data_ptr(), s_.data_ptr()
+    a.n_sides = n_sides
+    a.m_block, a.m_ptr, a.m_n, a.m_st = m_block.data_ptr(), m_ptr.data_ptr(), m_n.data_ptr(), m_st.data_ptr()
+    dt = dp_table.device_table
+    dt.engine.check(dt.engine._lib.sst_requery_merge_device(dt.handle, ctypes.byref(a), tot.data_ptr(),
+                                                            off.data_ptr()), "sst_requery_merge_device")
+    return (m_block, m_ptr, m_n, m_st), n_new
 
 
 @dataclass
@@ -688,8 +695,8 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
     nh = torch.as_tensor(name_hashes(dp_table) if name_hash is None else np.asarray(name_hash, np.int64), device=dev)
     ml_max = int(max_len.max()) if S else 1
     len_cap = ml_max + 2
-    if len_cap > 128:
-        raise NotImplementedError("skeleton walk: max_len above 126")
+    if len_cap > 255:
+        raise NotImplementedError("skeleton walk: max_len above 253")
     pos_cap = _native.pyset_table_size(ml_max + 1)
     req_cap = max(1 << 16, Q)
     req_mass = torch.empty(req_cap, dtype=torch.float64, device=dev)
@@ -717,12 +724,8 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
     # round, so the number of re-query rounds is not bounded by the ABI's
     # SST_WALK_MAX_ROUNDS (exact-mode spectra re-query every bin whose
     # predecessor had no explanations through the host)
-    merged = None
+    merged, n_merged = None, 0
     keep_alive = []
-    m_sid = torch.zeros(0, dtype=torch.int64, device=dev)
-    m_ptr = torch.zeros(0, dtype=torch.int64, device=dev)
-    m_n = torch.zeros(0, dtype=torch.int32, device=dev)
-    m_st = torch.zeros(0, dtype=torch.int8, device=dev)
     n_rounds = 0
     run = np.arange(2 * S, dtype=np.int32)
     big = np.zeros(0, np.int32)
@@ -794,8 +797,7 @@ def skeleton_device(dp_table, rows: DeviceRows, alpha, max_len, bins=None, toler
             res = _masked_explain_refs(dp_table, alpha_dev, req_mass, req_thr, req_spec, n_req, max_len, dst, p_, n_,
                                        s_)
             results.extend(res)
-            m_sid, m_ptr, m_n, m_st, merged = merge_requery_round(m_sid, m_ptr, m_n, m_st, req_block[:2 * S], p_,
-                                                                  n_, s_, 2 * S)
+            merged, n_merged = merge_requery_round(dp_table, merged, n_merged, req_block[:2 * S], p_, n_, s_, 2 * S)
             n_rounds += 1
             n_req_total += n_req
     return DeviceSkeleton(max_len, skel_off, skel, min_end, max_end, kept, status.cpu().numpy()[:2 * S], launches,
@@ -1234,7 +1236,7 @@ def post_skeleton_device(dp_table, rows: DeviceRows, sk: DeviceSkeleton, ln: Dev
                                             err2.data_ptr()), "sst_valid_rows_alpha_device")
     eng.synchronize()
     if int(err.item()):
-        raise _native.EngineError("post-skeleton stage: a spectrum of more than 4096 peaks")
+        raise _native.EngineError(f"post-skeleton stage: a spectrum of more than {MAX_PEAKS} peaks")
     _check_err(err2)
     return DevicePost(alpha_out.cpu().numpy().view(np.uint64)[:S].copy(), active.cpu().numpy()[:S].copy(),
                       alive_out, alive_skel, min_out, max_out, before, int(alive_out.sum().item()))

@@ -137,3 +137,26 @@ def test_skeleton_vs_reference(tc):
                        capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert f"skeleton ok {tc}" in p.stdout
+
+
+@pytest.mark.parametrize("variant", ["full_ladders", "short_fragments_missing", "low_modification_rate",
+                                     "noise_free", "noise_free_exact"])
+def test_synthetic_mirrors_vs_reference(variant):
+    """The host mirrors of config 5's stages on synthetic spectra
+    (tests/_synth_cases.py) against the REFERENCE's own results
+    (synth_stages.json.gz, make_synth_golden.py): classify, the fixpoint's
+    final alphabet and fragments, the skeleton walk per side, the Jaccard
+    length with both length bounds, the combined skeleton and the
+    skeleton-based reduction -- the first 12 spectra of each variant on
+    oracle-backed tables (the GPU suite runs all 48 on the device), under the
+    reference run's hash seed (child process)."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PYTHONHASHSEED="0")
+    p = subprocess.run([sys.executable, os.path.join(here, "_synth_check.py"), variant, "cpu", "12"], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert f"synth ok {variant} cpu" in p.stdout

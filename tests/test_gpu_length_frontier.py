@@ -130,13 +130,23 @@ def test_frontier_vs_oracle_rebuilt_tables(setup, cases):
     lower, upper, st, nodes, stats = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len)
     fr = stats["frontier"]
     assert _check(want, lower, upper, st, nodes=nodes) >= 190
-    assert fr["key_words"] == 4 and fr["splits"] == 0 and fr["aborted"] == 0, fr  # 104 rows and 20-mers: > 128 bits
+    # keys: root bits + the query's kept ranks + its left moves (<= hi / w_min), the
+    # widest query of the batch: 104 rows and 6-mers need more than 64 bits
+    assert fr["key_words"] == 2 and fr["splits"] == 0 and fr["aborted"] == 0, fr
     assert fr["nodes"] == int(nodes.sum()) > 10 ** 6, fr  # memo entries, summed over the spectra
-    # the same spectra with narrower keys: the <= 12-row alphabets (64-bit
-    # keys) and the 41..64-row ones of <= 9 nucleotides (128-bit keys)
+    # the same spectra with other key widths: the <= 12-row alphabets alone
+    # (64-bit keys), and the whole batch forced to 256-bit keys (a width only
+    # windows with memos beyond any oracle's reach need: SST_LBF_MIN_KEY_WORDS)
+    import os
+
     K = np.array([len(a) for a in alphas])
-    for sel, kw in ((np.flatnonzero(K <= 12), 1), (np.flatnonzero((K > 40) & (K <= 64)), 2)):
-        lo1, up1, st1, nd1, s1 = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len, sel=sel)
+    for sel, kw, force in ((np.flatnonzero(K <= 12), 1, None), (np.arange(len(K)), 4, "4")):
+        if force:
+            os.environ["SST_LBF_MIN_KEY_WORDS"] = force
+        try:
+            lo1, up1, st1, nd1, s1 = PD.length_bounds_alpha_device(dp, masks, su, ob, ml, caps_len, a0_len, sel=sel)
+        finally:
+            os.environ.pop("SST_LBF_MIN_KEY_WORDS", None)
         assert np.array_equal(nd1[sel], nodes[sel])
         assert s1["frontier"]["key_words"] == kw and len(sel) >= 20, (kw, s1["frontier"])
         assert np.array_equal(lo1[sel], lower[sel]) and np.array_equal(up1[sel], upper[sel])

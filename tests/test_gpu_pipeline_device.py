@@ -294,29 +294,23 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
     from spectrseqtools_amd.mass_explanation import MASS_NAMES
     from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
     from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict
-    from spectrseqtools_amd.synthetic import make_spectra
+
+    import _synth_cases as SC
 
     n = 48
-    exact = variant in ("low_modification_rate", "noise_free_exact")
-    clean = variant.startswith("noise_free")
-    mod_rate = 0.05 if exact else 0.5
-    b = make_spectra(n, seed={"full_ladders": 41, "short_fragments_missing": 43, "noise_free": 53,
-                              "noise_free_exact": 59}.get(variant, 47), len_range=(6, 14),
-                     mod_rate=0.3 if exact else 0.5, ppm=0.0 if clean else 3.0, noise_frac=0.0 if clean else 0.2)
-    spec = np.repeat(np.arange(n), np.diff(b.offsets))
-    keep = np.ones(len(b.observed), bool)
-    if variant in ("short_fragments_missing", "low_modification_rate"):
-        keep = (spec % 3 == 0) | (b.observed > 1300.0)
-    obs = b.observed[keep]
-    offsets = np.concatenate([[0], np.cumsum(np.bincount(spec[keep], minlength=n))])
-    bd = build_breakage_dict(555.1294, 455.1491)
-    w_full = [k for k, v in bd.items() if "START_END" in v][0]
-    su_seq = b.seq_mass - w_full * TOLERANCE
+    d = SC.variant_inputs(variant, n)  # the inputs of the reference-run fixtures (test_device_synthetic_vs_reference)
+    exact, clean, mod_rate = d["exact"], d["clean"], d["mod_rate"]
+    obs, offsets, su_seq, max_len = d["obs"], d["offsets"], d["su_seq"], d["max_len"]
+
+    class b:  # noqa: N801 -- the sequence masses under the name the checks below use
+        seq_mass = d["seq_mass"]
+
+    bd = build_breakage_dict(*SC.TAGS)
     seq = SequenceInformation(max_len=20, su_mass=float(su_seq[0]), obs_mass=float(b.seq_mass[0]),
                               modification_rate=mod_rate)
     dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
                                  precision=TOLERANCE, seq=seq, engine=engine)
-    max_len = pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:]))
+    assert np.array_equal(max_len, pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:])))
     if exact:
         assert not PD.budgets_pair_ok(dp, max_len).any()
     rows = PD.classify_device(dp, obs, offsets, su_seq, bd)
@@ -370,6 +364,34 @@ def test_device_skeleton_and_length_vs_mirror(engine, variant):
         for x, y in ((sk.skel, sk2.skel), (sk.min_end, sk2.min_end), (sk.max_end, sk2.max_end),
                      (sk.kept, sk2.kept)):
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("variant", ["full_ladders", "short_fragments_missing", "low_modification_rate",
+                                     "noise_free", "noise_free_exact"])
+def test_device_synthetic_vs_reference(variant):
+    """Stages 2-5 and the skeleton-based reduction on the device over 48
+    synthetic spectra per variant against the REFERENCE's own results
+    (synth_stages.json.gz, tests/golden/make_synth_golden.py: classify_fragments,
+    Predictor.filter_by_explanation, SkeletonBuilder._predict_skeleton per
+    side, select_sequence_length_with_jaccard with both
+    compute_sequence_length_bound calls, combine_skeleton_sequences, and
+    Predictor.predict up to the skeleton-based _reduce_alphabet, all run
+    unmodified): final alphabet and kept fragments, each side's skeleton /
+    kept fragments / min_end / max_end, the skeleton alphabet, both bounds,
+    the length (or its exception), the combined skeleton, build_skeleton's
+    fragments and the reduction's alphabet and fragments.  Child process
+    under the reference run's hash seed (the walk orders explanations as
+    CPython's sets do)."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, PYTHONHASHSEED="0")
+    p = subprocess.run([sys.executable, os.path.join(here, "_synth_check.py"), variant, "device"], env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert f"synth ok {variant} device" in p.stdout
 
 
 def test_device_pipeline_big_spectra(engine):
@@ -452,6 +474,120 @@ def test_device_pipeline_big_spectra(engine):
             got_c = [sorted(names[r] for r in range(1, len(names)) if (int(c_[r >> 6]) >> (r & 63)) & 1)
                      for c_ in comb]
             assert got_c == want["combined"], g
+
+
+def test_device_pipeline_limits(engine):
+    """The reference has no peak or length limit (fragment_classification.py:
+    17-101, cli.py:161-172): a spectrum of ~6 000 peaks (more than the LDS
+    classify kernel's 4 096: k_classify_rows_big in the HBM slices, peaks in
+    random order) and one of max_len ~150 (a 140-nt sequence, peaks below
+    20 kDa; the walk's positions above 126) batched with ordinary spectra,
+    through every stage -- classify / fixpoint / bins against the host-driven
+    stages, the walk, the Jaccard stage (the long one's bounds leave the
+    reduced table: the reference raises there) and the skeleton-based
+    reduction against the per-spectrum host mirrors."""
+    from spectrseqtools_amd import _native, pipeline, pipeline_device as PD
+    from spectrseqtools_amd.fragment_classification import classify_fragments
+    from spectrseqtools_amd.frame import Frame
+    from spectrseqtools_amd.mass_explanation import MASS_NAMES
+    from spectrseqtools_amd.mass_table import DynamicProgrammingTable, SequenceInformation
+    from spectrseqtools_amd.masses import EXPLANATION_MASSES, MATCHING_THRESHOLD, TOLERANCE, build_breakage_dict
+    from spectrseqtools_amd.prediction import Predictor
+    from spectrseqtools_amd.synthetic import make_spectra
+
+    rng = np.random.default_rng(83)
+    small = make_spectra(10, seed=71, len_range=(6, 14))
+    wide = make_spectra(1, seed=73, len_range=(20, 20))
+    o_wide = wide.observed[:wide.offsets[1]]
+    # 6 000 peaks: mostly light noise (rarely a valid mass below 1.5 kDa), some heavy
+    o_wide = np.concatenate([o_wide, rng.uniform(300.0, 1500.0, 5200), rng.uniform(1500.0, 8000.0, 800)])
+    o_wide = o_wide[rng.permutation(len(o_wide))]
+    long_ = make_spectra(1, seed=79, len_range=(140, 140), internal_per_nt=1)
+    o_long = long_.observed[:long_.offsets[1]]
+    o_long = o_long[o_long < 20000.0]  # the full table ends at 22.16 kDa: is_valid_mass would raise above
+    parts = [small.observed[small.offsets[g]:small.offsets[g + 1]] for g in range(10)]
+    seq_mass = list(small.seq_mass)
+    parts.insert(3, o_wide)
+    seq_mass.insert(3, wide.seq_mass[0])
+    parts.insert(8, o_long)
+    seq_mass.insert(8, long_.seq_mass[0])
+    obs = np.concatenate(parts)
+    offsets = np.concatenate([[0], np.cumsum([len(x) for x in parts])])
+    seq_mass = np.asarray(seq_mass)
+    n = len(parts)
+    assert len(parts[3]) > 6000
+    bd = build_breakage_dict(555.1294, 455.1491)
+    w_full = [k for k, v in bd.items() if "START_END" in v][0]
+    su_seq = seq_mass - w_full * TOLERANCE
+    seq = SequenceInformation(max_len=20, su_mass=float(su_seq[0]), obs_mass=float(seq_mass[0]),
+                              modification_rate=0.5)
+    dp = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                 precision=TOLERANCE, seq=seq, engine=engine)
+    max_len = pipeline.max_len_of(su_seq, TOLERANCE, min(m.mass for m in dp.masses[1:]))
+    assert max_len[8] > 140
+    c = pipeline.classify(obs, offsets, su_seq, dp, bd)
+    rows = PD.classify_device(dp, obs, offsets, su_seq, bd)
+    cnt = rows.rows.cpu().numpy()
+    assert np.array_equal(cnt, np.diff(c.offsets))
+    slot = (4 * offsets[:-1])[c.spec] + (np.arange(len(c.spec)) - c.offsets[c.spec])
+    assert np.array_equal(rows.su.cpu().numpy()[slot], c.su)
+    assert np.array_equal(rows.obs.cpu().numpy()[slot], c.obs)
+    fx_h = pipeline.filter_fixpoint(c, dp, max_len, EXPLANATION_MASSES)
+    fx_d = PD.fixpoint_device(dp, rows, max_len)
+    assert np.array_equal(fx_d.alpha, fx_h.alpha)
+    assert np.array_equal(rows.alive.cpu().numpy()[slot].astype(bool), fx_h.alive)
+    alive_fx = rows.alive.cpu().numpy().copy()
+    bins = PD.bins_device(dp, rows, fx_d.alpha, max_len=max_len)
+    sk = PD.skeleton_device(dp, rows, fx_d.alpha, max_len, bins=bins)
+    ln = PD.length_device(dp, sk, bins.alpha_dev, su_seq, seq_mass)
+    post = PD.post_skeleton_device(dp, rows, sk, ln)
+    names = [None] + [MASS_NAMES[m.mass][0] for m in dp.masses[1:]]
+    for g in (3, 8, 0):
+        o = obs[offsets[g]:offsets[g + 1]]
+        want = _mirror_outcome(o, su_seq[g], seq_mass[g], max_len[g], engine)
+        o4 = int(rows.peak_off[g].item()) * 4
+        assert np.flatnonzero(alive_fx[o4:o4 + int(cnt[g])]).tolist() == want["filter_kept"], g
+        assert (sk.status[2 * g:2 * g + 2] == _native.WALK_DONE).all(), (g, sk.status[2 * g:2 * g + 2])
+        got = PD.skeleton_frames(dp, rows, sk, g)
+        for side in ("START", "END"):
+            assert got[side] == want[side], (g, side)
+        kept = pipeline.mask_rows(ln.alpha[g:g + 1], len(dp.masses))[0]
+        assert [0] + [dp.masses[r].mass for r in range(1, len(dp.masses)) if kept[r]] == want["masses"], g
+        st = int(ln.status[g])
+        if want["seq_len"] is None:  # the reference raised: no length fits, or a bound left the table
+            assert st in (_native.JAC_NO_LENGTH, _native.JAC_BOUNDS), (g, st)
+            if g == 8:
+                assert st == _native.JAC_BOUNDS and int(ln.lb_status[g]) == _native.SST_OUT_OF_TABLE, g
+        elif want["seq_len"] == "IndexError":
+            assert st == _native.JAC_INDEX, g
+        else:
+            assert st == _native.JAC_OK and int(ln.seq_len[g]) == want["seq_len"], g
+            L = int(ln.seq_len[g])
+            comb = ln.comb[int(ln.comb_off[g]):int(ln.comb_off[g]) + L].cpu().numpy().view(np.uint64)
+            got_c = [sorted(names[r] for r in range(1, len(names)) if (int(c_[r >> 6]) >> (r & 63)) & 1)
+                     for c_ in comb]
+            assert got_c == want["combined"], g
+        # Predictor.predict up to the skeleton-based reduction (mirror, fresh table)
+        seq_g = SequenceInformation(max_len=int(max_len[g]), su_mass=float(su_seq[g]), obs_mass=float(seq_mass[g]),
+                                    modification_rate=0.5)
+        dp_g = DynamicProgrammingTable(EXPLANATION_MASSES, compression_rate=32, tolerance=MATCHING_THRESHOLD,
+                                       precision=TOLERANCE, seq=seq_g, engine=engine)
+        try:
+            rec = {}
+            fr = classify_fragments(Frame({"observed_mass": list(map(float, o))}), dp_g, bd)
+            out = Predictor(dp_g, EXPLANATION_MASSES).predict_skeleton_stage(fr, record=rec)
+            if out is None:
+                assert int(post.active[g]) == 0, g
+                continue
+            assert int(post.active[g]) == 1, g
+            for key, frame, alive in (("build_skeleton", rec["build_skeleton"], post.alive_skeleton),
+                                      ("reduction", out[1], post.alive)):
+                idx = np.flatnonzero(alive[o4:o4 + int(cnt[g])].cpu().numpy())
+                assert idx.tolist() == frame.get_column("index").to_list(), (g, key)
+                assert post.min_end[o4 + idx].cpu().numpy().tolist() == frame.get_column("min_end").to_list()
+                assert post.max_end[o4 + idx].cpu().numpy().tolist() == frame.get_column("max_end").to_list()
+        finally:
+            dp_g.close()
 
 
 def test_device_fixpoint_rounds_vs_oracle_rebuilt_tables(engine):

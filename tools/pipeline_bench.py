@@ -133,6 +133,79 @@ def length_cpu_baseline(dp, ln, su_seq, obs_seq, max_len, n_len, budget_s):
             "mismatches_vs_gpu": int(mism)}
 
 
+CHASE_LINES_PER_S = 50e9  # tools/chase_probe.hip: random 64-B line fetches per second chip-wide (r3_chase_probe.txt)
+
+
+def frontier_roofline(fr, kernels):
+    """Stage 5's dominant kernels (the first-visit frontier: k_lbf_groups,
+    k_lbf_nodes, k_lbf_values, all under the k_length_bound profile id) against
+    the per-unit model of DESIGN.md §4: algorithmic bytes at their natural
+    sizes per node N, group G and edge E (a left move onto a mass > 0: one
+    candidate insert, find and link), and the random lines they touch -- the
+    kernels' real bound, priced against the chip's random-line rate."""
+    N, G, E, kw = fr["nodes"], fr.get("groups", 0), fr.get("edges", 0), max(1, fr.get("key_words", 1))
+    cand = {1: 24, 2: 32, 4: 48}[kw]
+    per_node, per_group, per_edge = 19, 97, 34 + 2 * cand
+    algo = per_node * N + per_group * G + per_edge * E
+    lines = N + G + 5 * E  # lowest-rank byte per node; group entry per group; per edge the child's group entry,
+    # its candidate slot (insert, then find), the parent's link and the child's value (DESIGN §4)
+    ms = kernels.get("k_length_bound", [0.0])[0]
+    s = ms / 1e3
+    achieved = algo / s / 1e9 if s > 0 else 0.0
+    return {"bound": "random lines (HBM / fabric)", "kernels": "k_lbf_* (profile id k_length_bound)",
+            "nodes": N, "groups": G, "edges": E, "key_words": kw,
+            "model_bytes_per": {"node": per_node, "group": per_group, "edge": per_edge},
+            "algorithmic_bytes": algo, "algorithmic_bytes_per_node": algo / N if N else 0.0,
+            "kernel_s": s, "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,
+            "random_lines": lines, "random_lines_per_node": lines / N if N else 0.0,
+            "random_lines_per_s": lines / s if s > 0 else 0.0,
+            "frac_random_line_rate": lines / s / CHASE_LINES_PER_S if s > 0 else 0.0,
+            "line_rate_peak": CHASE_LINES_PER_S, "nodes_per_s": N / s if s > 0 else 0.0}
+
+
+def stages_cpu_baseline(dp, rows, fx, sk, args, data_rank, budget_s):
+    """Stages 1-4 on the host (tools/cpu_stages_leg.py, a child process that
+    never touches the GPU): A7 on every peak x 4 breakages by the oracle
+    (OpenMP), then the host mirrors of classify_fragments /
+    filter_by_explanation / _predict_skeleton with the oracle answering every
+    query, one spectrum per process, spectra in order for about budget_s.
+    Every sampled spectrum's final alphabet and kept rows are compared with
+    the device's, and both sides' skeletons too when PYTHONHASHSEED is fixed
+    (the walk's set order is this interpreter's, the child's must equal it)."""
+    import subprocess
+
+    from spectrseqtools_amd import pipeline_device as pd
+    from spectrseqtools_amd.pipeline import mask_rows
+
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))  # the box's CPU share for one GPU
+    cmd = [sys.executable, os.path.join(REPO, "tools", "cpu_stages_leg.py"), "--spectra", str(args.spectra),
+           "--seed", str(args.seed), "--rank", str(data_rank), "--procs", str(threads), "--budget-s", str(budget_s)]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=budget_s + 600)
+    if p.returncode != 0:
+        return {"error": p.stderr[-2000:]}
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    outs = res.pop("outcomes")
+    seeded = os.environ.get("PYTHONHASHSEED") is not None and args.name_hashes is None
+    n_rows = len(dp.masses)
+    mism = {"alphabet": 0, "kept": 0, "skeleton": 0}
+    alive = rows.alive.cpu().numpy()
+    for o in outs:
+        g = o["g"]
+        kept = mask_rows(fx.alpha[g:g + 1], n_rows)[0]
+        mism["alphabet"] += [0] + [dp.masses[r].mass for r in range(1, n_rows) if kept[r]] != o["masses"]
+        o4 = int(rows.peak_off[g].item()) * 4
+        mism["kept"] += np.flatnonzero(alive[o4:o4 + int(rows.rows[g].item())]).tolist() != o["kept"]
+        if seeded:
+            got = pd.skeleton_frames(dp, rows, sk, g)
+            mism["skeleton"] += any(got[sd] != o[sd] for sd in ("START", "END"))
+    st = res["stages1to4"]
+    st["mismatches_vs_gpu"] = mism
+    st["skeletons_compared"] = seeded
+    res["stages1to4"] = st
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spectra", type=int, default=100000, help="spectra per GPU")
@@ -380,6 +453,8 @@ def main():
                                                                                    return_counts=True))},
                             "mean_seq_len": float(ln.seq_len[ln.status == 0].mean()) if (ln.status == 0).any() else 0,
                             "engine": ln.engine, "frontier": ln.frontier, "kernels": kernels()}
+        if ln.engine == "frontier" and ln.frontier.get("nodes"):
+            stages["length"]["roofline"] = frontier_roofline(ln.frontier, stages["length"]["kernels"])
         busy(stages["length"])
         progress("length")
         barrier()
@@ -415,6 +490,10 @@ def main():
     if rows is not None and rank == 0 and args.cpu_baseline_s > 0:
         stages["length"]["cpu_baseline"] = length_cpu_baseline(dp, ln, su_seq, batch.seq_mass, max_len, n_len,
                                                                args.cpu_baseline_s)
+    cpu_1to4 = None
+    if rows is not None and rank == 0 and args.cpu_baseline_s > 0 and args.as_rank is None:
+        cpu_1to4 = stages_cpu_baseline(dp, rows, fx, sk, args, data_rank, args.cpu_baseline_s)
+        stages["classify"]["cpu_baseline"] = cpu_1to4.pop("a7")
 
     # per-spectrum alphabet reduction = a table rebuild (canonical + 3 mods)
     keep = {m.names[0] for m in dp.masses[1:5]} | {m.names[0] for m in dp.masses[-3:]}
@@ -435,7 +514,7 @@ def main():
         peaks_all, spectra_all = (int(x) for x in t.tolist())
     else:
         peaks_all, spectra_all = peaks, args.spectra
-    ref_est = (n_valid_q + valid_q_rounds) / 70e3 + (explain_q + stages["bins"]["queries"]) / 4.0e3
+    ref_est = (n_valid_q + valid_q_rounds) / 70e3 + (explain_q + stages["bins"]["queries"]) / 4.0e3  # (an estimate)
     gpu_s = sum(sum(v[0] for v in st["kernels"].values()) / 1e3 for st in stages.values())
     if rank == 0 and args.dump_outcomes and outcome is not None:
         os.makedirs(args.dump_outcomes, exist_ok=True)
@@ -454,9 +533,11 @@ def main():
             "total_s_without_length": total_s - stages.get("length", {}).get("s", 0.0),
             "spectra_per_s": spectra_all / total_s, "peaks_per_s": peaks_all / total_s,
             "reduction_rebuild_ms": rebuild_ms, "generation_s": gen_s,
+            "cpu_baseline_stages1to4": cpu_1to4,
             "reference_estimate_s_per_gpu_share": ref_est,
-            "reference_estimate_basis": "BASELINE.md single-core rates: is_valid 70k/s, explain 4.0k/s "
-                                        "(queries of one GPU's share; 1 core)",
+            "reference_estimate_basis": "an ESTIMATE, not timed: BASELINE.md single-core rates of the reference "
+                                        "Python (is_valid 70k/s, explain 4.0k/s) times this GPU's query counts "
+                                        "(1 core); cpu_baseline_stages1to4 is the measured leg",
         }), flush=True)
     if dist:
         dist.destroy_process_group()
