@@ -664,7 +664,7 @@ typedef struct sst_walk_args {
   uint32_t n_sides;
   uint8_t* scratch;          /* scratch_stride bytes per slot (sst_walk_scratch_bytes) */
   uint64_t scratch_stride;
-  uint32_t pos_cap, len_cap, expl_cap, cand_cap, tset_cap;
+  uint32_t pos_cap, len_cap, expl_cap, cand_cap, tset_cap;  /* len_cap = max max_len + 2 <= 255 */
   uint16_t* side_rows;       /* [2 slots] */
   const uint64_t* skel_off;  /* [n_spec] exclusive prefix of 2 max_len */
   uint64_t* skel;            /* spectrum g, side sd, position i: masks at 2 (skel_off[g] + sd max_len[g] + i) */

@@ -3079,7 +3079,7 @@ extern "C" int sst_skel_walk_device(sst_table* t, const sst_walk_args* a) {
   for (int r = 0; r < a->n_rounds; ++r)
     if (!a->rq_block[r] || !a->rq_ptr[r] || !a->rq_n[r] || !a->rq_st[r]) return SST_E_ARG;
   if (a->pos_cap < sst::pyset::kMinSize || a->tset_cap < sst::pyset::kMinSize || (a->pos_cap & (a->pos_cap - 1)) ||
-      (a->tset_cap & (a->tset_cap - 1)) || a->len_cap < 2 || a->len_cap > 128 ||
+      (a->tset_cap & (a->tset_cap - 1)) || a->len_cap < 2 || a->len_cap > 255 ||
       a->scratch_stride < sst::walk_scratch_bytes(a->pos_cap, a->len_cap, a->expl_cap, a->cand_cap, a->tset_cap))
     return fail(t->ctx, SST_E_ARG, "skeleton walk: scratch capacities");
   if (!t->args.pairs_enabled) return fail(t->ctx, SST_E_ARG, "skeleton walk: the table has no pair list");

@@ -1211,7 +1211,14 @@ def post_skeleton_device(dp_table, rows: DeviceRows, sk: DeviceSkeleton, ln: Dev
     slots = int(rows.alive.numel())
     i32 = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.int32), device=dev)  # noqa: E731
     seq_len = i32(ln.seq_len)
-    jst = torch.as_tensor(np.ascontiguousarray(ln.status, dtype=np.int8), device=dev)
+    # build_skeleton first runs select_sequence_length_with_lp (skeleton_building.py:
+    # 45-57, 198-251): without a solver it only combines the skeletons at every
+    # candidate length in [lower, upper], which raises IndexError past max_len
+    # (:494-512) -- build_skeleton raises and predict returns its default
+    jac_post = np.array(ln.status, dtype=np.int8, copy=True)
+    lp_raises = (ln.lb_status == 0) & (ln.lower <= ln.upper) & (ln.upper > np.asarray(sk.max_len, np.int64))
+    jac_post[lp_raises & (jac_post == _native.JAC_OK)] = _native.JAC_INDEX
+    jst = torch.as_tensor(jac_post, device=dev)
     comb_off = torch.as_tensor(np.ascontiguousarray(ln.comb_off[:-1] if len(ln.comb_off) > S else ln.comb_off,
                                                     dtype=np.int64), device=dev)
     alpha = torch.as_tensor(np.ascontiguousarray(ln.alpha).view(np.int64), device=dev)

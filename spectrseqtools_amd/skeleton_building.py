@@ -25,6 +25,11 @@ is mirrored with the length the reference selects when no LP instance can be
 built -- determine_lp_score's `except Exception: return np.inf` (:279-286)
 for every candidate length, so select_sequence_length_with_lp returns -1 and
 the Jaccard selection decides (:52-57) -- which is config 5's MILP-free path.
+That path still runs select_sequence_length_with_lp's own steps before the LP
+(:198-251): the alphabet reduction, both length bounds, and
+combine_skeleton_sequences for every candidate length in [lower, upper],
+which raises IndexError for a length above the skeletons' max_len
+(:494-512); build_skeleton then raises and predict returns its default.
 """
 from dataclasses import dataclass, field
 from itertools import chain, groupby
@@ -63,6 +68,7 @@ class SkeletonBuilder:
             fragments.filter_mask(["END" in b for b in brk]),
             skeleton_seq=[set() for _ in range(self.dp_table.seq.max_len)])
         end_sk = end_sk[::-1]
+        self._lp_candidates_without_solver(start_skeleton=start_sk, end_skeleton=end_sk)
         seq_len = self.select_sequence_length_with_jaccard(start_skeleton=start_sk, end_skeleton=end_sk)
         skeleton_seq = combine_skeleton_sequences(seq_len=seq_len, start_skeleton=start_sk, end_skeleton=end_sk)
         n = len(skeleton_seq)
@@ -240,6 +246,20 @@ class SkeletonBuilder:
             min_mass += min([nuc_masses[nuc] for nuc in (start_nucs | end_nucs)], default=0)
             max_mass += max([nuc_masses[nuc] for nuc in (start_nucs | end_nucs)], default=0)
         return min_mass - MAX_VARIANCE <= self.dp_table.seq.su_mass <= max_mass + MAX_VARIANCE
+
+    def _lp_candidates_without_solver(self, start_skeleton, end_skeleton):
+        """select_sequence_length_with_lp (skeleton_building.py:198-251) where
+        no LP instance can be built (determine_lp_score -> np.inf, so it
+        returns -1): its alphabet reduction, both bounds, and
+        combine_skeleton_sequences per candidate length -- the only step
+        that can raise (IndexError past the skeletons' length)."""
+        nucleotides = {nuc for skeleton_pos in start_skeleton + end_skeleton for nuc in skeleton_pos}
+        self.dp_table.adapt_individual_modification_rates_by_alphabet_reduction(nucleotides)
+        min_len = compute_sequence_length_bound(dp_table=self.dp_table, dir="lower")
+        max_len = compute_sequence_length_bound(dp_table=self.dp_table, dir="upper")
+        for len_cand in range(min_len, max_len + 1):
+            combine_skeleton_sequences(seq_len=len_cand, start_skeleton=start_skeleton, end_skeleton=end_skeleton)
+        return -1
 
     def select_sequence_length_with_jaccard(self, start_skeleton, end_skeleton) -> int:
         """skeleton_building.py:315-370 (the two length bounds on the GPU)."""
