@@ -376,7 +376,9 @@ int sst_result_stats(const sst_result* r, uint64_t* stats_out /* [8] */);
  * uploaded as they are, SST_LB_REPLAY).  out[i] = the bound; status[i]: 0
  * ok, SST_OUT_OF_TABLE (the reference raises NotImplementedError),
  * SST_LB_EMPTY_WINDOW (its min([]) raises ValueError), SST_ABORTED (DFS node
- * budget exhausted: no bound).  Synchronous, host buffers. */
+ * budget exhausted: no bound).  max_len <= 253 (the frontier's u8 values);
+ * a window only the replay answers needs max_len <= 120 (SST_E_ARG with a
+ * message otherwise).  Synchronous, host buffers. */
 #define SST_LB_EMPTY_WINDOW (-5)
 /* sst_length_bound_batch on per-query reduced alphabets (the table
  * adapt_individual_modification_rates_by_alphabet_reduction would rebuild,

@@ -2482,7 +2482,7 @@ static int length_bound_batch(sst_table* t, const double* su, const double* obs,
   const bool replay_only = (direction & SST_LB_REPLAY) != 0;
   direction &= ~(SST_LB_EXACT_ONLY | SST_LB_REPLAY);
   if (!t || n < 0 || n > INT32_MAX || (n > 0 && (!su || !obs || !out || !status)) || (direction != 0 && direction != 1) ||
-      max_len < 0 || max_len > 120)
+      max_len < 0 || max_len > 253)
     return SST_E_ARG;
   sst_ctx* c = t->ctx;
   std::lock_guard<std::recursive_mutex> g(c->mu);
@@ -2640,6 +2640,10 @@ static int length_bound_batch(sst_table* t, const double* su, const double* obs,
     }
     HIP_OK(c, hipStreamSynchronize(c->stream));  // the host vectors above are read by the copies
   }
+  if (n_exact && max_len > 120)  // the frontier answers up to 253; the replay's int8 value slots hold 121
+    return fail(c, SST_E_ARG,
+                "length bound: max_len " + std::to_string(max_len) + " above 120 for a window only the DFS replay "
+                "answers (the table's last packed word, or beyond the frontier's layout)");
   if (n_exact) {
     // one 64-lane block per query in flight (k_length_exact<WAVE>), each with
     // its own memo slice: up to 1 024 at once (4 waves per CU; the memo slices

@@ -147,7 +147,7 @@ def test_synthetic_mirrors_vs_reference(variant):
     (synth_stages.json.gz, make_synth_golden.py): classify, the fixpoint's
     final alphabet and fragments, the skeleton walk per side, the Jaccard
     length with both length bounds, the combined skeleton and the
-    skeleton-based reduction -- the first 12 spectra of each variant on
+    skeleton-based reduction -- the first 6 spectra of each variant on
     oracle-backed tables (the GPU suite runs all 48 on the device), under the
     reference run's hash seed (child process)."""
     import os
@@ -156,7 +156,7 @@ def test_synthetic_mirrors_vs_reference(variant):
 
     here = os.path.dirname(os.path.abspath(__file__))
     env = dict(os.environ, PYTHONHASHSEED="0")
-    p = subprocess.run([sys.executable, os.path.join(here, "_synth_check.py"), variant, "cpu", "12"], env=env,
+    p = subprocess.run([sys.executable, os.path.join(here, "_synth_check.py"), variant, "cpu", "6"], env=env,
                        capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert f"synth ok {variant} cpu" in p.stdout

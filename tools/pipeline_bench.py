@@ -323,7 +323,9 @@ def main():
         sw = bw.status == 2
         int(sw.sum().item()), int((bw.status == -10).sum().item()), int(bw.count[sw].sum().item())
         kw = pd.skeleton_device(dp, rw, fw.alpha, m0, bins=bw, name_hash=nh)
-        lw = pd.length_device(dp, kw, bw.alpha_dev, su_seq[:S0], batch.seq_mass[:S0])
+        # (trim=False: a serving process keeps the frontier's workspace across
+        # batches; the timed stage reuses the warm-up's, as round 5 did)
+        lw = pd.length_device(dp, kw, bw.alpha_dev, su_seq[:S0], batch.seq_mass[:S0], trim=False)
         pd.post_skeleton_device(dp, rw, kw, lw)
     engine.synchronize()
     if rank == 0:
@@ -439,7 +441,7 @@ def main():
         ln = pd.length_device(dp, sk, db.alpha_dev, su_seq, batch.seq_mass,
                               spectra=None if n_len == len(max_len) else np.arange(n_len),
                               soft_nodes=args.length_soft_nodes, engine=args.length_engine,
-                              frontier_workspace=int(args.frontier_workspace_gb * (1 << 30)))
+                              frontier_workspace=int(args.frontier_workspace_gb * (1 << 30)), trim=False)
         barrier()
         stages["length"] = {"s": tmax(time.perf_counter() - t0), "bounds_spectra": n_len,
                             "bounds_sample": n_len < len(max_len), "reach_batches": ln.reach_batches,
@@ -487,6 +489,7 @@ def main():
                             "path": "pack_outcomes + one agreed-size gather to rank 0"
                                     + (f" ({'RCCL' if args.backend == 'nccl' else 'gloo'})" if dist else " (local)")}
     engine.profile(False)
+    engine.trim()  # the frontier's workspace back to the allocator (sst_ctx_trim), after the timed stages
     if rows is not None and rank == 0 and args.cpu_baseline_s > 0:
         stages["length"]["cpu_baseline"] = length_cpu_baseline(dp, ln, su_seq, batch.seq_mass, max_len, n_len,
                                                                args.cpu_baseline_s)
