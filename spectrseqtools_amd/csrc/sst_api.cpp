@@ -3329,6 +3329,15 @@ static int lbf_frontier(sst_table* t, sst_ctx::LbfWs& W, const double* d_su, con
   HIP_OK(c, hipStreamSynchronize(c->stream));
   if (stats) stats->live = n_live;
   if (n_live == 0) return SST_OK;
+  {  // the list pass appends with atomics: sorted, the chunks (and so every
+     // dispatch of a run) are the same from run to run (matched profiles)
+    std::vector<uint32_t> lst(n_live);
+    HIP_OK(c, hipMemcpyAsync(lst.data(), d_list.p, (size_t)n_live * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+    std::sort(lst.begin(), lst.end());
+    HIP_OK(c, hipMemcpyAsync(d_list.p, lst.data(), (size_t)n_live * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_OK(c, hipStreamSynchronize(c->stream));
+  }
   // workspace per "slot": 8 nodes of 7 B, a 4-B node -> group entry for the
   // band in hand, per ring table a group entry (32 B) + its list entry (4 B)
   // and a candidate entry (32 B: 128-bit keys), and the band's group record
