@@ -620,10 +620,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     }
     const int64_t wk = qrow_w(rw);
     const bool mod = qrow_mod(rw);
-    // the left branch (mass_table.py:424-441): bit1 <=> m - w_k in R_k
+    // the left branch (mass_table.py:424-441): attempted iff bit1 (m - w_k in
+    // R_k) and the budgets allow it; the budget test first, so a blocked
+    // modification row never fetches the lowest-rank byte (a random line)
     const int64_t m2 = (int64_t)m - wk;
-    const bool b1 = live && m2 >= 0 && (m2 == 0 || (int)a.lr[q.lr_off + m2] <= k);
-    const bool latt = b1 && (!mod || (A > 0 && B > 0));
+    const bool bud = !mod || (A > 0 && B > 0);
+    const bool latt = live && bud && m2 >= 0 && (m2 == 0 || (int)a.lr[q.lr_off + m2] <= k);
     if (live) a.flags[id] = (uint8_t)((latt ? kFLeft : 0) | (k > lo ? kFUp : 0) | (latt && m2 == 0 ? kFZero : 0));
     bool emit = latt && m2 > 0;
     const uint32_t band2 = emit ? (uint32_t)((q.hi - m2) / a.wb) : 0u;

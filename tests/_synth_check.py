@@ -1,8 +1,8 @@
 """Child-process check (run with PYTHONHASHSEED=0, the seed of the reference
 run in tests/golden/make_synth_golden.py): config 5's stages on synthetic
 spectra (tests/_synth_cases.py) against the REFERENCE's own results
-(synth_stages.json.gz) -- filter_by_explanation's final alphabet and kept
-fragments, _predict_skeleton per side (skeleton, kept fragments, min_end,
+(synth_stages.json.gz) -- filter_by_explanation's alphabet and kept
+fragments after every round (device) and at the end, _predict_skeleton per side (skeleton, kept fragments, min_end,
 max_end), select_sequence_length_with_jaccard (skeleton alphabet, both
 length bounds, the length or its exception, the combined skeleton) and
 Predictor.predict's skeleton-based reduction (build_skeleton's fragments,
@@ -53,7 +53,7 @@ def check_device(variant, want, d):
     bd = build_breakage_dict(*SC.TAGS)
     ml = d["max_len"]
     rows = PD.classify_device(dp, d["obs"], d["offsets"], d["su_seq"], bd)
-    fx = PD.fixpoint_device(dp, rows, ml)
+    fx = PD.fixpoint_device(dp, rows, ml, record=True)
     alive_fx = rows.alive.cpu().numpy().copy()
     bins = PD.bins_device(dp, rows, fx.alpha, max_len=ml)
     sk = PD.skeleton_device(dp, rows, fx.alpha, ml, bins=bins)
@@ -65,6 +65,13 @@ def check_device(variant, want, d):
         w = want[g]
         o4 = int(rows.peak_off[g].item()) * 4
         nr = int(rows.rows[g].item())
+        # every filter_by_explanation round of this spectrum: the alphabet after
+        # _reduce_alphabet and the kept fragments (the reference's rounds)
+        mine = [(a_, l_) for act, a_, l_ in fx.history if act[g]]
+        assert len(mine) == len(w["filter"]["rounds"]) == int(fx.rounds[g]), (g, len(mine), len(w["filter"]["rounds"]))
+        for k, ((a_, l_), rr) in enumerate(zip(mine, w["filter"]["rounds"])):
+            assert names_of(dp, a_[g]) == rr["masses"], (g, k, "round alphabet")
+            assert np.flatnonzero(l_[o4:o4 + nr]).tolist() == rr["kept_index"], (g, k, "round kept")
         assert names_of(dp, fx.alpha[g]) == w["filter"]["masses"], (g, "filter alphabet")
         assert np.flatnonzero(alive_fx[o4:o4 + nr]).tolist() == w["filter"]["kept_index"], (g, "filter kept")
         assert (sk.status[2 * g:2 * g + 2] == _native.WALK_DONE).all(), (g, sk.status[2 * g:2 * g + 2])

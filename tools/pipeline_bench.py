@@ -152,6 +152,15 @@ def frontier_roofline(fr, kernels):
     ms = kernels.get("k_length_bound", [0.0])[0]
     s = ms / 1e3
     achieved = algo / s / 1e9 if s > 0 else 0.0
+    # HBM bytes per node from the matched counter record (tools/gpu_frontier_record.sh, 16 k spectra)
+    rec_path = os.path.join(REPO, "profiles", "r6_frontier_16k_record.json")
+    traffic = None
+    if os.path.exists(rec_path):
+        rec = json.load(open(rec_path))["frontier_band_kernels"]
+        traffic = {"bytes_per_node": rec["hbm_bytes_per_node"], "bytes": rec["hbm_bytes_per_node"] * N,
+                   "GBps": rec["hbm_bytes_per_node"] * N / s / 1e9 if s > 0 else 0.0,
+                   "frac_hbm": rec["hbm_bytes_per_node"] * N / s / 8e12 if s > 0 else 0.0,
+                   "source": "profiles/r6_frontier_16k_record.json (2 FETCH_SIZE + WRITE_SIZE per node, gfx950)"}
     return {"bound": "random lines (HBM / fabric)", "kernels": "k_lbf_* (profile id k_length_bound)",
             "nodes": N, "groups": G, "edges": E, "key_words": kw,
             "model_bytes_per": {"node": per_node, "group": per_group, "edge": per_edge},
@@ -160,7 +169,7 @@ def frontier_roofline(fr, kernels):
             "random_lines": lines, "random_lines_per_node": lines / N if N else 0.0,
             "random_lines_per_s": lines / s if s > 0 else 0.0,
             "frac_random_line_rate": lines / s / CHASE_LINES_PER_S if s > 0 else 0.0,
-            "line_rate_peak": CHASE_LINES_PER_S, "nodes_per_s": N / s if s > 0 else 0.0}
+            "line_rate_peak": CHASE_LINES_PER_S, "nodes_per_s": N / s if s > 0 else 0.0, "traffic": traffic}
 
 
 def stages_cpu_baseline(dp, rows, fx, sk, args, data_rank, budget_s):
