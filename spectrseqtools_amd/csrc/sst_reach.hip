@@ -31,6 +31,7 @@ namespace {
 constexpr int kReachWG = 1024;
 constexpr int kReachRing = 1 << 15;  // words (128 KB)
 constexpr int kReachRingMask = kReachRing - 1;
+constexpr int kReachILP = 4;  // words per thread whose loads are in flight together
 }  // namespace
 
 __global__ __launch_bounds__(kReachWG) void k_reach_rows(ReachArgs a) {
@@ -50,18 +51,32 @@ __global__ __launch_bounds__(kReachWG) void k_reach_rows(ReachArgs a) {
       uint32_t* cur = out + (int64_t)k * W;
       for (int64_t s = 0; s < W; s += seg) {
         const int64_t e = s + seg < W ? s + seg : W;
-        for (int64_t j = s + threadIdx.x; j < e; j += blockDim.x) {
-          // R_{-1} = {0}: the sentinel row; R_{k-1} was written by this
-          // workgroup's previous pass: read at device scope (from L2)
-          uint32_t v = prev ? __hip_atomic_load(prev + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                            : (j == 0 ? 1u : 0u);
-          const int64_t j0 = j - q, j1 = j - q - 1;
-          uint32_t sft = 0;
-          if (j0 >= 0) sft = ring[j0 & kReachRingMask] << sh;
-          if (sh && j1 >= 0) sft |= ring[j1 & kReachRingMask] >> (32 - sh);
-          v |= sft;
-          ring[j & kReachRingMask] = v;
-          cur[j] = v;
+        // kReachILP words per thread per step, their R_{k-1} loads issued
+        // together (a segment's words only read the ring's earlier segments,
+        // so they are independent of each other)
+        for (int64_t j0w = s + threadIdx.x; j0w < e; j0w += (int64_t)kReachILP * blockDim.x) {
+          uint32_t pv[kReachILP];
+#pragma unroll
+          for (int u = 0; u < kReachILP; ++u) {
+            const int64_t j = j0w + (int64_t)u * blockDim.x;
+            // R_{-1} = {0}: the sentinel row; R_{k-1} was written by this
+            // workgroup's previous pass: read at device scope (from L2)
+            pv[u] = j < e ? (prev ? __hip_atomic_load(prev + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : (j == 0 ? 1u : 0u))
+                          : 0u;
+          }
+#pragma unroll
+          for (int u = 0; u < kReachILP; ++u) {
+            const int64_t j = j0w + (int64_t)u * blockDim.x;
+            if (j >= e) break;
+            const int64_t j0 = j - q, j1 = j - q - 1;
+            uint32_t sft = 0;
+            if (j0 >= 0) sft = ring[j0 & kReachRingMask] << sh;
+            if (sh && j1 >= 0) sft |= ring[j1 & kReachRingMask] >> (32 - sh);
+            const uint32_t v = pv[u] | sft;
+            ring[j & kReachRingMask] = v;
+            cur[j] = v;
+          }
         }
         __syncthreads();
       }
