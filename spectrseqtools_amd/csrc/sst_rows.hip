@@ -547,17 +547,17 @@ constexpr int kWavesPerWG = 1;  // one wave per workgroup: a finished spectrum f
                                  // (4-wave workgroups held theirs until the slowest of the four: 168 vs 140 us)
 
 struct WaveLds {
-  double obs[kWP];
-  double su[kWS];
-  double ob[kWS];
-  uint16_t qoff[kWS + 1];  // a side has < 2^16 pairs (kWS (kWS - 1) / 2)
-  uint16_t kidx[4][kWP];
-  uint8_t keep[kWP];
-  uint8_t ord[kWP];  // peaks in (mass, position) order when they do not come sorted
+  double obs[kWP];           // the spectrum's peaks in mass order (equal masses in their given order)
+  double su[kWS];            // the side's rows in SU order
+  uint8_t rp[kWS];           // each row's peak (its observed mass: the pair threshold)
+  uint16_t qoff[kWS + 1];    // a side has < 2^16 pairs (kWS (kWS - 1) / 2)
+  uint8_t kidx[4][kWP];      // peak of the j-th kept row of breakage k (mass order)
+  uint8_t keep[kWP];         // bit k: the row (k, p) is kept
   uint32_t kcnt[4];
   uint32_t sstar;
   uint32_t hist[64];  // wave_pair_window: starts per position of a 64-query window
 };
+static_assert(kWP < 256, "u8 peak indices and kept-row counts");
 
 // LDS written by some lanes of the wave, read by others: order the accesses
 __device__ __forceinline__ void wsync() {
@@ -566,15 +566,21 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// inclusive prefix sum over the wave's 64 lanes: DPP row shifts within each
+// 16-lane row, then row broadcasts of lanes 15 and 31 (VALU only, no LDS
+// round trip as a ds_bpermute-based shuffle would take)
+__device__ __forceinline__ uint32_t wave_incl(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
 __device__ __forceinline__ uint32_t wave_excl(uint32_t v, uint32_t& total) {
-  const int lane = threadIdx.x & 63;
-  uint32_t incl = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  total = __shfl(incl, 63, 64);
+  const uint32_t incl = wave_incl(v);
+  total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   return incl - v;
 }
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
@@ -586,64 +592,126 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
   return v;
 }
 
-// A7, filters and the kept rows of every breakage (peak order) of spectrum g
+// A7, filters and the kept rows of every breakage (mass order) of spectrum g.  A peak's bitset words are all loaded before any is tested
+// (valid_window, sst_quant.h, with its loads hoisted: the first and last word
+// of each breakage's window; the middle words of a wider window afterwards),
+// and the A7 codes are stored after, so no store orders the loads.
 __device__ void wave_load(WaveLds& L, const TableArgs& t, const RowsArgs& a, int64_t p0, uint32_t P, double su_seq,
                           bool write_a7) {
   const int lane = threadIdx.x & 63;
   for (uint32_t p = lane; p < P; p += 64) {
     const double o = a.obs[p0 + p];
-    L.obs[p] = o;
-    uint8_t kp = 0;
-    for (int k = 0; k < a.n_shifts; ++k) {
-      const double su = o - a.shift[k];
+    uint32_t wa[4], wb[4], bits[4];  // window words; bits: a & 63 | (b & 63) << 8 | load << 16 | code << 24
+    uint64_t x0[4], x1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      wa[k] = wb[k] = 0u;
+      bits[k] = 0u;  // code 0
+      if (k >= a.n_shifts) continue;
       double lof, hif;
-      quantise_lean(su, a.tol * o, a.prec, a.rprec, lof, hif);
-      const int8_t code =
-          valid_window(t.valid, t.limit, (int64_t)lof, (int64_t)hif, t.full_lo, t.full_hi, t.first_reach);
+      quantise_lean(o - a.shift[k], a.tol * o, a.prec, a.rprec, lof, hif);
+      const int64_t lo = (int64_t)lof, hi = (int64_t)hif;
+      const int64_t aa = lo < 1 ? 1 : lo, bb = hi < t.limit - 1 ? hi : t.limit - 1;
+      if (hi < lo || aa > hi) continue;
+      if (aa <= bb && bb >= t.full_lo && aa < t.full_hi) {
+        bits[k] = 1u << 24;  // meets the all-reachable run
+        continue;
+      }
+      bits[k] = (uint32_t)(uint8_t)(hi >= t.limit ? (int8_t)-1 : (int8_t)0) << 24;  // unless a bit of [aa, bb] is set
+      if (aa <= bb && bb >= t.first_reach) {
+        wa[k] = (uint32_t)(aa >> 6);
+        wb[k] = (uint32_t)(bb >> 6);
+        bits[k] |= (uint32_t)(aa & 63) | (uint32_t)(bb & 63) << 8 | 1u << 16;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x0[k] = x1[k] = 0;
+      if (bits[k] & (1u << 16)) {
+        x0[k] = t.valid[wa[k]];
+        if (wb[k] != wa[k]) x1[k] = t.valid[wb[k]];
+      }
+    }
+    uint8_t kp = 0;
+    const bool inten = a.intensity ? a.intensity[p0 + p] > a.intensity_cutoff : true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= a.n_shifts) continue;
+      int8_t code = (int8_t)(bits[k] >> 24);
+      if (bits[k] & (1u << 16)) {
+        const uint32_t ba = bits[k] & 63u, bb = (bits[k] >> 8) & 63u;
+        const uint64_t hm = ~0ull >> (63 - bb);
+        uint64_t m0 = x0[k] & (~0ull << ba);
+        if (wa[k] == wb[k]) m0 &= hm;
+        bool any = m0 != 0;
+        if (wb[k] != wa[k]) any |= (x1[k] & hm) != 0;
+        if (!any && wb[k] - wa[k] > 1u) any = any_bits(t.valid, ((int64_t)wa[k] + 1) << 6, ((int64_t)wb[k] << 6) - 1);
+        if (any) code = 1;
+      }
       if (write_a7) a.valid_out[(int64_t)k * a.n_peaks + p0 + p] = code;
-      const bool inten = a.intensity ? a.intensity[p0 + p] > a.intensity_cutoff : true;
+      const double su = o - a.shift[k];
       const bool full = (a.sides[k] & 3) == 3;
       const bool keep = code == 1 && inten && o < a.mass_cutoff && su < su_seq + a.max_variance &&
                         (su > su_seq - a.max_variance || !full);
       kp |= (uint8_t)keep << k;
     }
+    L.obs[p] = o;
     L.keep[p] = kp;
   }
   wsync();
   // a peak list need not be sorted: rank the peaks by mass (equal masses in
-  // their given order) so that each breakage's rows come in SU order
+  // their given order) and rewrite them in that order (the rows need only
+  // their masses, never the peak's position in the list)
   bool sorted = true;
   for (uint32_t p = lane; p + 1 < P; p += 64) sorted &= L.obs[p] <= L.obs[p + 1];
   sorted = __ballot(!sorted) == 0;
   if (!sorted) {
-    for (uint32_t p = lane; p < P; p += 64) {
+    double ov[(kWP + 63) / 64];
+    uint8_t kv[(kWP + 63) / 64];
+    uint32_t rv[(kWP + 63) / 64];
+#pragma unroll
+    for (int i = 0; i < (kWP + 63) / 64; ++i) {
+      const uint32_t p = lane + 64u * i;
+      rv[i] = 0xFFFFFFFFu;
+      if (p >= P) continue;
       const double o = L.obs[p];
       uint32_t rank = 0;
       for (uint32_t q = 0; q < P; ++q) {
         const double v = L.obs[q];
         rank += (v < o) | ((v == o) & (q < p));
       }
-      L.ord[rank] = (uint8_t)p;
+      ov[i] = o;
+      kv[i] = L.keep[p];
+      rv[i] = rank;
     }
+    wsync();
+#pragma unroll
+    for (int i = 0; i < (kWP + 63) / 64; ++i)
+      if (rv[i] != 0xFFFFFFFFu) {
+        L.obs[rv[i]] = ov[i];
+        L.keep[rv[i]] = kv[i];
+      }
     wsync();
   }
   for (int k = 0; k < a.n_shifts; ++k) {
     uint32_t carry = 0;
     for (uint32_t q0 = 0; q0 < P; q0 += 64) {
       const uint32_t i = q0 + lane;
-      const uint32_t p = i < P ? (sorted ? i : L.ord[i]) : 0u;
-      const bool f = i < P && ((L.keep[p] >> k) & 1u);
+      const bool f = i < P && ((L.keep[i] >> k) & 1u);
       const uint64_t bal = __ballot(f);
-      if (f) L.kidx[k][carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = (uint16_t)p;
+      if (f)
+        L.kidx[k][carry + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = (uint8_t)i;
       carry += (uint32_t)__builtin_popcountll(bal);
     }
     if (lane == 0) L.kcnt[k] = carry;
   }
 }
 
-// side sd's rows into L.su / L.ob (SU order) and its window pairs' prefix;
-// returns the row count (or ~0 when it does not fit) and the pair count
+// side sd's rows into L.su / L.rp (SU order) and its window pairs' prefix;
+// returns the row count (or ~0 when it does not fit) and the pair count.  Row
+// j of breakage k goes to j plus, for each other breakage k2 of the side, the
+// kept rows of k2 before it (binary search; ties: the earlier breakage first).
 __device__ uint32_t wave_side(WaveLds& L, const RowsArgs& a, int sd, uint32_t& Q) {
   const int lane = threadIdx.x & 63;
   uint32_t n = 0;
@@ -671,7 +739,7 @@ __device__ uint32_t wave_side(WaveLds& L, const RowsArgs& a, int sd, uint32_t& Q
         pos += lo;
       }
       L.su[pos] = su;
-      L.ob[pos] = L.obs[p];
+      L.rp[pos] = (uint8_t)p;
     }
   }
   wsync();
@@ -744,7 +812,7 @@ __device__ __forceinline__ uint32_t wave_pair_window(WaveLds& L, uint32_t n, uin
   uint32_t tot;
   const uint32_t cnt = wave_excl(L.hist[lane], tot) + L.hist[lane];  // starts at positions <= lane
   const uint64_t at64 = __ballot(pos == 64u);
-  const bool full = __shfl(pos, 63, 64) <= 64u;  // lane 63's start begins by q0 + 64: maybe more beyond it
+  const bool full = (uint32_t)__builtin_amdgcn_readlane((int)pos, 63) <= 64u;  // lane 63's start begins by q0 + 64: maybe more beyond it
   const uint32_t q = q0 + (uint32_t)lane;
   wsync();  // the histogram is rewritten by the next window
   if (!full) {
@@ -758,30 +826,45 @@ __device__ __forceinline__ uint32_t wave_pair_window(WaveLds& L, uint32_t n, uin
   return s1;
 }
 
-// the pair-list entries with sums in [a, hi] (1 <= a <= hi < pair_hi) from the census: two independent loads
-__device__ __forceinline__ uint32_t census_walk(const TableArgs& t, uint32_t a, uint32_t hi, uint32_t& first,
-                                                uint32_t& bytes) {
-  const uint32_t c0 = t.pair_base - 1u;
-  const uint32_t lo = a - 1u < c0 ? c0 : a - 1u, h = hi < c0 ? c0 : hi;
-  const uint32_t x = t.census[lo - c0], y = t.census[h - c0];
-  first = x & 0xFFFFu;
-  bytes = (y >> 16) - (x >> 16);
-  return (y & 0xFFFFu) - first;
-}
-
-__device__ __forceinline__ QAns wave_answer(const WaveLds& L, const TableArgs& t, const RowsArgs& a, uint32_t s,
-                                            uint32_t e) {
+// A pair's answer: wave_ask quantises the pair's window and loads its two
+// census words (the pair-list entries with sums <= each end: none for an
+// inactive lane or a window without a whole mass), wave_reply forms the
+// status, count, first entry and record bytes from them.
+struct QAsk {
+  uint32_t x, y;  // census words at the window's lower and upper end
+  uint32_t mode;  // bit0: the window holds 0 or more (lof <= hif, hif >= 0); bit1: census words; bit2: lof <= 0
+};
+__device__ __forceinline__ QAsk wave_ask(const WaveLds& L, const TableArgs& t, const RowsArgs& a, bool act,
+                                         uint32_t s, uint32_t e) {
+  QAsk k{0u, 0u, 0u};
+  if (!act) return k;
   const double diff = L.su[e] - L.su[s];
-  const double thr = a.tol * (L.ob[s] + L.ob[e]);
+  const double thr = a.tol * (L.obs[L.rp[s]] + L.obs[L.rp[e]]);
   double lof, hif;
   quantise_lean(diff, thr, a.prec, a.rprec, lof, hif);
-  QAns r{SST_NONE, 0, 0, 0};
   if (lof <= hif && hif >= 0.0) {
     const double af = lof < 1.0 ? 1.0 : lof;
-    if (af <= hif) r.cnt = census_walk(t, (uint32_t)af, (uint32_t)hif, r.first, r.bytes);
+    k.mode = 1u | (lof <= 0.0 ? 4u : 0u);
+    if (af <= hif) {  // census_walk's two loads
+      const uint32_t c0 = t.pair_base - 1u, lo = (uint32_t)af - 1u, hi = (uint32_t)hif;
+      k.x = t.census[(lo < c0 ? c0 : lo) - c0];
+      k.y = t.census[(hi < c0 ? c0 : hi) - c0];
+      k.mode |= 2u;
+    }
+  }
+  return k;
+}
+__device__ __forceinline__ QAns wave_reply(const RowsArgs& a, const QAsk& k) {
+  QAns r{SST_NONE, 0, 0, 0};
+  if (k.mode & 1u) {
+    if (k.mode & 2u) {
+      r.first = k.x & 0xFFFFu;
+      r.bytes = (k.y >> 16) - (k.x >> 16);
+      r.cnt = (k.y & 0xFFFFu) - r.first;
+    }
     if (r.cnt > a.cap) r.status = SST_OVERFLOW;
     else if (r.cnt) r.status = SST_SOME;
-    else if (lof <= 0.0) r.status = SST_EMPTY;
+    else if (k.mode & 4u) r.status = SST_EMPTY;
   }
   return r;
 }
@@ -844,7 +927,7 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
         double* ro = a.rows_ob + 4 * p0 + (sd ? 2 * (int64_t)P : 0);
         for (uint32_t r = lane; r < n; r += 64) {
           rs[r] = L.su[r];
-          ro[r] = L.ob[r];
+          ro[r] = L.obs[L.rp[r]];
         }
       }
       uint32_t s0 = 0;  // the start of query q0
@@ -853,7 +936,7 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
         uint32_t s, e;
         s0 = wave_pair_window(L, n, q0, s0, s, e);
         if (q >= Q) continue;
-        const QAns r = wave_answer(L, t, a, s, e);
+        const QAns r = wave_reply(a, wave_ask(L, t, a, true, s, e));
         nh += (r.status == SST_SOME || r.status == SST_OVERFLOW);
         nb += r.status == SST_SOME ? r.bytes + 2u : 0u;
         if (fits)
@@ -950,11 +1033,20 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, R
           a.hits[hb + xh] = make_uint4((uint32_t)(qb + q), r.cnt, (uint32_t)word, (uint32_t)(word >> 32));
           a.refs[hb + xh] = (uint16_t)(r.first | (r.status == SST_OVERFLOW ? 0x8000u : 0u));
           if (r.status == SST_SOME) {
+            // four records' loads in flight before their stores (a store
+            // through the byte pointer would otherwise order every load)
             uint8_t* dst = a.dense + o;
-            for (uint32_t k = r.first; k < r.first + r.cnt; ++k) {
-              const uint32_t rec = img.recs[k];
-              *(u32_unal*)dst = rec;
-              dst += (rec & 0xFFu) + 1u;
+            const uint32_t kend = r.first + r.cnt;
+            for (uint32_t k0 = r.first; k0 < kend; k0 += 4) {
+              uint32_t rec[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) rec[u] = k0 + u < kend ? img.recs[k0 + u] : 0u;
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                if (k0 + u < kend) {
+                  *(u32_unal*)dst = rec[u];
+                  dst += (rec[u] & 0xFFu) + 1u;
+                }
             }
           }
         }
