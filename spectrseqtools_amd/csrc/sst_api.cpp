@@ -172,6 +172,7 @@ struct sst_result {
   uint64_t region_bytes = 0, spill_bytes = 0;
   uint64_t pass_id = 0;
   uint64_t pack_seq = 0;  // k_result_pack launches of this result: the header carries the latest
+  uint32_t rows_tile_par = 0;  // the rows step's tile-sum parity of the last launched step (RowsArgs.tile_tot)
   bool tail_ran = false;   // the deferred-class launch ran for the current pass
   bool settled = true;     // the current pass has been checked (routed windows run, retries done)
   bool arrays_ready = false;  // count[] / offset[] built from the hit list for the current pass
@@ -1556,13 +1557,13 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   const bool fresh = !r->rows_ctl.p;
   if (!r->dense.ensure(std::max<uint64_t>(r->arena_bytes, (uint64_t)16 * r->cap_n + (1u << 20))) ||
       !r->rows_su.ensure(std::max<size_t>(1, 4 * P) * 8) || !r->rows_ob.ensure(std::max<size_t>(1, 4 * P) * 8) ||
-      !r->rows_side.ensure(2 * S * 4) || !r->rows_tot.ensure(3 * S * 4) || !r->rows_chunk.ensure(2 * 3 * NC * 8 + 4 * 16 * 8) ||
+      !r->rows_side.ensure(2 * S * 4) || !r->rows_tot.ensure(3 * S * 4) || !r->rows_chunk.ensure((6 * NC + 6 * (NC / kRowsTile + 1)) * 8) ||
       !r->rows_big.ensure(S * 4) || !r->rows_redo.ensure(S * 4) || !r->rows_ctl.ensure(64) ||
-      !r->rows_ans.ensure(std::max<size_t>(1, 2 * kRowsAnsPerPeak * P) * 8) || !r->rows_aq.ensure(2 * S * 4))
+      !r->rows_ans.ensure(std::max<size_t>(1, 2 * kRowsAnsPerPeak * P) * 4) || !r->rows_aq.ensure(2 * S * 4))
     return bail(fail(c, SST_E_NOMEM, "device allocation failed (rows step)"));
   if (fresh) {
     HIP_OK(c, hipMemsetAsync(r->rows_ctl.p, 0, 64, c->stream));
-    HIP_OK(c, hipMemsetAsync((uint64_t*)r->rows_chunk.p + 6 * NC, 0, 4 * 16 * 8, c->stream));  // scan flags: no pass id
+    HIP_OK(c, hipMemsetAsync((uint64_t*)r->rows_chunk.p + 6 * NC, 0, 6 * (NC / kRowsTile + 1) * 8, c->stream));  // tile sums
   }
   r->pass = {t, nullptr, nullptr, nullptr, max_mods_scalar, tol, prec, 1, cap_per_query, nullptr, nullptr};
   r->pass_stream = c->stream;
@@ -1600,13 +1601,14 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   a.rows_su = (double*)r->rows_su.p;
   a.rows_ob = (double*)r->rows_ob.p;
   a.side_rows = (uint32_t*)r->rows_side.p;
-  a.ans = (uint64_t*)r->rows_ans.p;
+  a.ans = (uint32_t*)r->rows_ans.p;
   a.ans_q = (uint32_t*)r->rows_aq.p;
   a.totals = (uint32_t*)r->rows_tot.p;
   a.chunk_tot = (unsigned long long*)r->rows_chunk.p;
   a.chunk_off = (uint64_t*)r->rows_chunk.p + 3 * NC;
+  a.tile_tot = (unsigned long long*)r->rows_chunk.p + 6 * NC;
+  a.n_tiles = (int64_t)(NC / kRowsTile + 1);
   a.chunk_cap = (int64_t)NC;
-  a.scan_agg = (uint64_t*)r->rows_chunk.p + 6 * NC;
   a.ctl = (uint64_t*)r->rows_ctl.p;
   a.err = (uint32_t*)((char*)r->rows_ctl.p + 32);
   a.done = (uint32_t*)((char*)r->rows_ctl.p + 40);
@@ -1622,10 +1624,12 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   a.hdr = (uint64_t*)r->hdr.p;
   a.hdr_host = r->hdr_host_dev;
   a.pass_id = ++r->pack_seq;
+  a.tile_par = r->rows_tile_par ^ 1u;  // the last step zeroed these tile sums
   {
     Prof p(c, SST_K_EXPLAIN_MAIN);
     HIP_OK(c, launch_rows_step(t->args, a, c->n_cu, scan_dyn_lds(t->args), c->stream));
   }
+  r->rows_tile_par = a.tile_par;
   *out = r;
   return SST_OK;
 }

@@ -463,6 +463,7 @@ constexpr int kRowsWaveMaxPeaks = 160;  // spectra up to this many peaks: one wa
 // answer slots per peak and side of the rows step's count pass (config 3:
 // 10 queries per peak over both sides)
 constexpr int kRowsAnsPerPeak = 24;
+constexpr int kRowsTile = 64;  // chunks per tile of the rows step's offsets
 struct RowsArgs {
   const double* obs;          // [n_peaks] sorted within each spectrum
   const int64_t* peak_off;    // [n_spec + 1]
@@ -479,17 +480,21 @@ struct RowsArgs {
   double* rows_su;            // scratch [4 * n_peaks]
   double* rows_ob;
   uint32_t* side_rows;        // [2 n_spec]
-  // the wave kernels' answers, written once by the count pass: one u64 per
-  // query (status | count << 8 | first entry << 24 | record bytes << 40),
-  // side sd of spectrum g at kRowsAnsPerPeak * (2 peak_off[g] + sd * P_g)
-  // when its queries fit there (kRowsAnsPerPeak * P_g slots; else the emit
-  // pass answers that side again from its scratch rows)
-  uint64_t* ans;              // [2 kRowsAnsPerPeak n_peaks]
+  // the wave kernels' answers, written once by the count pass: one u32 per
+  // query (count << 16 | first entry, or the status of a pair without
+  // entries; sst_rows.hip ans_word), side sd of spectrum g at
+  // kRowsAnsPerPeak * (2 peak_off[g] + sd * P_g) when its queries fit there
+  // (kRowsAnsPerPeak * P_g slots; else the emit pass answers that side again
+  // from its scratch rows)
+  uint32_t* ans;              // [2 kRowsAnsPerPeak n_peaks]
   uint32_t* ans_q;            // [2 n_spec] the side's queries, ~0: did not fit
   uint32_t* totals;           // [3 n_spec] queries, hits, payload bytes
   unsigned long long* chunk_tot;  // [3 n_chunks] totals of each wave's contiguous chunk of spectra
-  uint64_t* chunk_off;        // [3 n_chunks] their exclusive offsets (k_rows_scan)
-  uint64_t* scan_agg;         // [4 x 16] k_rows_scan's tile sums and their pass id (the look-back)
+  uint64_t* chunk_off;        // [3 n_chunks] their exclusive offsets (k_rows_emit_w)
+  unsigned long long* tile_tot;  // [2][3 n_tiles] sums of kRowsTile consecutive chunks, by step parity: the
+                              // count kernels add into tile_par's and zero the other's (zeroed at allocation)
+  int64_t n_tiles;
+  uint32_t tile_par;          // alternates between consecutive rows steps on one result
   int64_t chunk, n_chunks;    // spectra per chunk, chunks (= waves of the wave kernels' grid; set at launch)
   int64_t chunk_cap;          // chunk arrays' capacity (chunks)
   uint64_t* ctl;              // [4] totals

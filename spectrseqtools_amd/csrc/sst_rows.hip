@@ -28,16 +28,17 @@
 // Launches: k_rows_count_w (one wave per contiguous chunk of spectra, each
 // spectrum of <= 160 peaks in turn; larger spectra are listed for
 // k_rows_count, one workgroup each): A7, every window pair answered once
-// (8 B per query to scratch, the pass's one answer per pair), per-spectrum
+// (4 B per query to scratch, the pass's one answer per pair), per-spectrum
 // totals of queries / hits / payload bytes and each chunk's sums;
-// k_rows_scan: the chunks' exclusive offsets (one workgroup over one value per
-// wave); k_rows_emit_w: each spectrum's offsets (its chunk's plus the chunk's
-// earlier spectra's totals), then its answers streamed back into statuses,
-// the dense hit list with pair-list refs and the dense payload;
-// k_rows_count / k_rows_emit do the same for the big spectra (rows to
-// scratch, answered in both passes); the last workgroup writes the header.  The result is
-// sst_result's dense layout in query order (spectrum-major; START pairs, then
-// END pairs).
+// k_rows_emit_w: each chunk's exclusive offsets from the 64-chunk tiles' sums
+// (added up by the count kernels) and its own tile's earlier chunks (no scan
+// launch),
+// each spectrum's offsets (its chunk's plus the chunk's earlier spectra's
+// totals), then its answers streamed back into statuses, the dense hit list
+// with pair-list refs and the dense payload; k_rows_count / k_rows_emit do the
+// same for the big spectra (rows to scratch, answered in both passes); the
+// last workgroup writes the header.  The result is sst_result's dense layout
+// in query order (spectrum-major; START pairs, then END pairs).
 #include <hip/hip_runtime.h>
 #include <mutex>
 #include <stdint.h>
@@ -153,6 +154,37 @@ struct QAns {
   int8_t status;
   uint32_t cnt, first, bytes;
 };
+
+// A stored answer (the count pass's 4 B per query): count << 16 | first
+// entry; a pair without entries stores its status instead (0 NONE, 1 EMPTY).
+// SOME / OVERFLOW follow from the count and the cap; the record bytes from
+// the records themselves (ans_bytes), which the emit reads anyway.
+__device__ __forceinline__ uint32_t ans_word(const QAns& r) {
+  return r.cnt ? ((r.cnt & 0xFFFFu) << 16 | (r.first & 0xFFFFu)) : (r.status == SST_EMPTY ? 1u : 0u);
+}
+__device__ __forceinline__ QAns ans_read(uint32_t v, uint32_t cap) {
+  QAns r{SST_NONE, v >> 16, 0, 0};
+  if (r.cnt) {
+    r.first = v & 0xFFFFu;
+    r.status = r.cnt > cap ? SST_OVERFLOW : SST_SOME;
+  } else if (v & 1u) {
+    r.status = SST_EMPTY;
+  }
+  return r;
+}
+// the payload bytes of records [first, first + cnt): record k takes
+// (recs[k] & 0xFF) + 1 bytes
+__device__ __forceinline__ uint32_t ans_bytes(const uint32_t* recs, uint32_t first, uint32_t cnt) {
+  uint32_t nb = 0;
+  for (uint32_t k0 = first; k0 < first + cnt; k0 += 4) {
+    uint32_t rec[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) rec[x] = k0 + x < first + cnt ? recs[k0 + x] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) nb += rec[x] != 0xFFFFFFFFu ? (rec[x] & 0xFFu) + 1u : 0u;
+  }
+  return nb;
+}
 
 __device__ __forceinline__ QAns answer(const SpecLds& L, const PairImg& img, const RowsArgs& a, uint32_t s,
                                        uint32_t e) {
@@ -341,76 +373,15 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_count(TableArgs t, RowsArgs a)
       a.side_rows[2 * g + 1] = nside[1];
       // into its chunk's totals (the wave kernel wrote the chunk's other spectra's)
       unsigned long long* ct = a.chunk_tot + 3 * (g / a.chunk);
+      unsigned long long* tt = a.tile_tot + a.tile_par * 3 * a.n_tiles + 3 * (g / a.chunk / kRowsTile);
       if (nq) atomicAdd(ct, (unsigned long long)nq);
       if (s_acc[1]) atomicAdd(ct + 1, (unsigned long long)s_acc[1]);
       if (s_acc[2]) atomicAdd(ct + 2, (unsigned long long)s_acc[2]);
+      if (nq) atomicAdd(tt, (unsigned long long)nq);
+      if (s_acc[1]) atomicAdd(tt + 1, (unsigned long long)s_acc[1]);
+      if (s_acc[2]) atomicAdd(tt + 2, (unsigned long long)s_acc[2]);
     }
     __syncthreads();
-  }
-}
-
-// exclusive offsets of the wave kernels' chunks (the workgroup kernels add
-// the big spectra's totals to their chunk) and the pass totals: one thread per
-// chunk, a workgroup per 1 024 chunks, the tiles chained by a look-back over
-// the earlier tiles' published sums (<= kScanTiles workgroups, all resident).
-// A spectrum's own offset is its chunk's plus the totals of the chunk's
-// earlier spectra (the emitting wave walks them in order).
-constexpr int kScanTiles = 16;
-
-__device__ __forceinline__ uint64_t block_excl64(uint64_t v, uint64_t* s_w, uint64_t& total) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint64_t incl = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) s_w[wv] = incl;
-  __syncthreads();
-  uint64_t base = 0, tot = 0;
-  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-    const uint64_t x = s_w[w];
-    if (w < wv) base += x;
-    tot += x;
-  }
-  __syncthreads();
-  total = tot;
-  return base + incl - v;
-}
-
-__global__ __launch_bounds__(kRowsWG) void k_rows_scan(RowsArgs a) {
-  __shared__ uint64_t s_w[16];
-  __shared__ uint64_t s_pre[3];
-  const int64_t nb = a.n_chunks;
-  const int b = blockIdx.x;
-  const int64_t j = (int64_t)b * kRowsWG + threadIdx.x;
-  uint64_t v[3], ex[3], tot[3];
-  for (int c = 0; c < 3; ++c) v[c] = j < nb ? a.chunk_tot[3 * j + c] : 0ull;
-  for (int c = 0; c < 3; ++c) ex[c] = block_excl64(v[c], s_w, tot[c]);
-  if (threadIdx.x == 0) {  // publish the tile's sums
-    for (int c = 0; c < 3; ++c) a.scan_agg[4 * b + c] = tot[c];
-    __threadfence();
-    __hip_atomic_store(&a.scan_agg[4 * b + 3], a.pass_id, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (threadIdx.x < 3) {  // this tile's offset: the earlier tiles' sums
-    const int c = threadIdx.x;
-    uint64_t pre = 0;
-    for (int k = 0; k < b; ++k) {
-      while (__hip_atomic_load(&a.scan_agg[4 * k + 3], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != a.pass_id) {
-      }
-      pre += __hip_atomic_load(&a.scan_agg[4 * k + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_pre[c] = pre;
-  }
-  __syncthreads();
-  if (j < nb)
-    for (int c = 0; c < 3; ++c) a.chunk_off[3 * j + c] = s_pre[c] + ex[c];
-  if (b == (int)gridDim.x - 1 && threadIdx.x == 0) {  // the pass totals
-    const uint64_t q = s_pre[0] + tot[0], h = s_pre[1] + tot[1], by = s_pre[2] + tot[2];
-    a.ctl[0] = q;
-    a.ctl[1] = h;
-    a.ctl[2] = by;
-    if (q > a.cap_queries || h > a.cap_queries || by > a.cap_bytes) atomicOr(a.err, 4u);
   }
 }
 
@@ -443,7 +414,7 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
     for (int sd = 0; sd < 2; ++sd) {
       const uint32_t n = a.side_rows[2 * g + sd];
       const bool stored = redo && a.ans_q[2 * g + sd] != 0xFFFFFFFFu;  // the count pass's answers, in query order
-      const uint64_t* ans = a.ans + (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)a.peak_off[g] + (uint64_t)sd * P);
+      const uint32_t* ans = a.ans + (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)a.peak_off[g] + (uint64_t)sd * P);
       uint32_t Q;
       if (stored) {
         Q = a.ans_q[2 * g + sd];
@@ -462,11 +433,8 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
         QAns r{SST_NONE, 0, 0, 0};
         if (q < Q) {
           if (stored) {
-            const uint64_t v = ans[q];
-            r.status = (int8_t)(uint8_t)v;
-            r.cnt = (uint32_t)(v >> 8) & 0xFFFFu;
-            r.first = (uint32_t)(v >> 24) & 0xFFFFu;
-            r.bytes = (uint32_t)(v >> 40);
+            r = ans_read(ans[q], a.cap);
+            if (r.status == SST_SOME) r.bytes = ans_bytes(img.recs, r.first, r.cnt);
           } else {
             uint32_t s, e;
             pair_of(L, n, q, s, e);
@@ -876,7 +844,8 @@ __device__ __forceinline__ PairImg global_img(const TableArgs& t) {
 
 }  // namespace
 
-__global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, RowsArgs a) {
+// six waves per SIMD (80 VGPRs, two spilled: same-box A/B 179-180 against 186 us/step at the natural 90 VGPRs and five)
+__global__ __launch_bounds__(64 * kWavesPerWG) __attribute__((amdgpu_waves_per_eu(6))) void k_rows_count_w(TableArgs t, RowsArgs a) {
   __shared__ WaveLds Ls[kWavesPerWG];
   WaveLds& L = Ls[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
@@ -913,7 +882,7 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
       }
       if (sd) n1 = n;
       else n0 = n;
-      // every pair is answered here, once: the emit pass reads the answers
+      // every pair is answered here, once (4 B: ans_word): the emit pass reads the answers
       // back in query order instead of re-forming and re-answering the pairs
       // (the side's fixed slots; a side with more queries keeps its rows in
       // scratch and is answered again by the emit pass)
@@ -940,8 +909,7 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
         nh += (r.status == SST_SOME || r.status == SST_OVERFLOW);
         nb += r.status == SST_SOME ? r.bytes + 2u : 0u;
         if (fits)
-          a.ans[base + q] = (uint64_t)(uint8_t)r.status | (uint64_t)(r.cnt & 0xFFFFu) << 8 |
-                            (uint64_t)(r.first & 0xFFFFu) << 24 | (uint64_t)r.bytes << 40;
+          a.ans[base + q] = ans_word(r);
       }
       nq += Q;
       wsync();
@@ -974,29 +942,76 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_count_w(TableArgs t, 
     a.chunk_tot[3 * w] = cq;
     a.chunk_tot[3 * w + 1] = chh;
     a.chunk_tot[3 * w + 2] = cb;
+    unsigned long long* tt = a.tile_tot + a.tile_par * 3 * a.n_tiles + 3 * (w / kRowsTile);
+    if (cq) atomicAdd(tt, (unsigned long long)cq);
+    if (chh) atomicAdd(tt + 1, (unsigned long long)chh);
+    if (cb) atomicAdd(tt + 2, (unsigned long long)cb);
   }
+  if (w == 0)  // the next pass's tile sums start from zero
+    for (int64_t i = lane; i < 3 * a.n_tiles; i += 64) a.tile_tot[(a.tile_par ^ 1u) * 3 * a.n_tiles + i] = 0;
   RPROF_T(w1);
   RPROF_ADD(8, w1 - w0);
   RPROF_ADD(9, 1);
   if (threadIdx.x == 0 && blockIdx.x == 0) RPROF_ADD(10, gridDim.x);
 }
 
-__global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, RowsArgs a) {
+namespace {
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// Chunk w's exclusive offsets (queries, hits, payload bytes): the totals of
+// the 64-chunk tiles before its own (tile_tot, summed by the count kernels)
+// plus its own tile's earlier chunks -- at most five coalesced loads per lane
+// and a wave sum, no launch of its own and no wait on other waves.
+__device__ void chunk_prefix(const RowsArgs& a, int64_t w, uint64_t off[3]) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long* tt = a.tile_tot + a.tile_par * 3 * a.n_tiles;
+  const int64_t t = w / kRowsTile;
+  uint64_t v[3] = {0, 0, 0};
+  for (int64_t i = lane; i < t; i += 64)
+    for (int c = 0; c < 3; ++c) v[c] += tt[3 * i + c];
+  const int64_t j = t * kRowsTile + lane;
+  if (j < w)
+    for (int c = 0; c < 3; ++c) v[c] += a.chunk_tot[3 * j + c];
+  for (int c = 0; c < 3; ++c) off[c] = wave_sum64(v[c]);
+}
+
+constexpr int kEmitAhead = 4;  // answer windows in flight ahead of the one emitted
+
+}  // namespace
+
+// six waves per SIMD (80 VGPRs; the four windows' state would take 87 and five): the emit is latency-bound, waves count
+__global__ __launch_bounds__(64 * kWavesPerWG) __attribute__((amdgpu_waves_per_eu(6))) void k_rows_emit_w(TableArgs t, RowsArgs a) {
   // the answers the count pass stored, streamed back in query order (a
   // spectrum with a side past its slots, or over kWP peaks, is the workgroup
   // emit's): no LDS, so the waves per CU are set by registers alone
   const int lane = threadIdx.x & 63;
   const PairImg img = global_img(t);
-  const bool room = !(*(volatile uint32_t*)a.err & 4u);
   const int64_t w = (int64_t)blockIdx.x * kWavesPerWG + (threadIdx.x >> 6);
+  if (w >= a.n_chunks) return;
   const int64_t g_end = (w + 1) * a.chunk < a.n_spec ? (w + 1) * a.chunk : a.n_spec;
-  uint64_t off[3] = {0, 0, 0};
-  if (room && w < a.n_chunks) {
-    off[0] = a.chunk_off[3 * w];
-    off[1] = a.chunk_off[3 * w + 1];
-    off[2] = a.chunk_off[3 * w + 2];
+  uint64_t off[3];
+  chunk_prefix(a, w, off);
+  const uint64_t ct[3] = {a.chunk_tot[3 * w], a.chunk_tot[3 * w + 1], a.chunk_tot[3 * w + 2]};
+  if (lane == 0) {  // this chunk's offsets (the workgroup emit's big spectra); the last chunk's end: the pass totals
+    for (int c = 0; c < 3; ++c) a.chunk_off[3 * w + c] = off[c];
+    if (w == a.n_chunks - 1) {
+      a.ctl[0] = off[0] + ct[0];
+      a.ctl[1] = off[1] + ct[1];
+      a.ctl[2] = off[2] + ct[2];
+    }
   }
-  for (int64_t g = w * a.chunk; g < g_end && room; ++g) {
+  // past the result's capacity: nothing written (the header reports it)
+  const bool room = off[0] + ct[0] <= a.cap_queries && off[1] + ct[1] <= a.cap_queries && off[2] + ct[2] <= a.cap_bytes;
+  if (!room) {
+    if (lane == 0) atomicOr(a.err, 4u);
+    return;
+  }
+  for (int64_t g = w * a.chunk; g < g_end; ++g) {
     const int64_t p0 = a.peak_off[g];
     const uint32_t P = (uint32_t)(a.peak_off[g + 1] - p0);
     const uint32_t Q0 = a.ans_q[2 * g], Q1 = a.ans_q[2 * g + 1];
@@ -1008,50 +1023,84 @@ __global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, R
     if (P > (uint32_t)kWP || Q0 == 0xFFFFFFFFu || Q1 == 0xFFFFFFFFu) continue;  // the workgroup kernel's
     for (int sd = 0; sd < 2; ++sd) {
       const uint32_t Q = sd ? Q1 : Q0;
-      const uint64_t* ans = a.ans + (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P);
-      // one window ahead: its answers are in flight while this one is emitted
-      uint64_t nv = lane < (int)Q ? __builtin_nontemporal_load(&ans[lane]) : 0ull;
-      for (uint32_t q0 = 0; q0 < Q; q0 += 64) {
-        const uint32_t q = q0 + lane;
-        const uint64_t v = nv;
-        if (q0 + 64 < Q) nv = q + 64 < Q ? __builtin_nontemporal_load(&ans[q + 64]) : 0ull;
-        QAns r{SST_NONE, 0, 0, 0};
-        if (q < Q) {
-          r.status = (int8_t)(uint8_t)v;
-          r.cnt = (uint32_t)(v >> 8) & 0xFFFFu;
-          r.first = (uint32_t)(v >> 24) & 0xFFFFu;
-          r.bytes = (uint32_t)(v >> 40);
-          a.status[qb + q] = r.status;
-        }
-        const bool hit = r.status == SST_SOME || r.status == SST_OVERFLOW;
-        uint32_t th, tb;
-        const uint32_t xh = wave_excl(hit ? 1u : 0u, th);
-        const uint32_t xb = wave_excl(r.status == SST_SOME ? r.bytes + 2u : 0u, tb);
-        if (hit) {
-          const uint64_t o = bb + xb;
-          const uint64_t word = r.status == SST_SOME ? o : (uint64_t)r.cnt;
-          a.hits[hb + xh] = make_uint4((uint32_t)(qb + q), r.cnt, (uint32_t)word, (uint32_t)(word >> 32));
-          a.refs[hb + xh] = (uint16_t)(r.first | (r.status == SST_OVERFLOW ? 0x8000u : 0u));
-          if (r.status == SST_SOME) {
-            // four records' loads in flight before their stores (a store
-            // through the byte pointer would otherwise order every load)
-            uint8_t* dst = a.dense + o;
-            const uint32_t kend = r.first + r.cnt;
-            for (uint32_t k0 = r.first; k0 < kend; k0 += 4) {
-              uint32_t rec[4];
+      const uint32_t* ans = a.ans + (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P);
+      // kEmitAhead windows at a time, phase by phase so that their latencies
+      // overlap: the answers (loaded one group ahead), then every SOME
+      // answer's first two records (its bytes and payload), the wave prefix
+      // sums, and the stores in window order
+      uint32_t buf[kEmitAhead];
 #pragma unroll
-              for (int u = 0; u < 4; ++u) rec[u] = k0 + u < kend ? img.recs[k0 + u] : 0u;
+      for (int u = 0; u < kEmitAhead; ++u) {
+        const uint32_t q = (uint32_t)lane + 64u * u;
+        buf[u] = q < Q ? __builtin_nontemporal_load(&ans[q]) : 0u;
+      }
+      for (uint32_t q0 = 0; q0 < Q; q0 += 64u * kEmitAhead) {
+        QAns r[kEmitAhead];
+        uint32_t rec[kEmitAhead][2], xh[kEmitAhead], xb[kEmitAhead], th[kEmitAhead], tb[kEmitAhead];
 #pragma unroll
-              for (int u = 0; u < 4; ++u)
-                if (k0 + u < kend) {
-                  *(u32_unal*)dst = rec[u];
-                  dst += (rec[u] & 0xFFu) + 1u;
-                }
-            }
+        for (int u = 0; u < kEmitAhead; ++u) {
+          const uint32_t q = q0 + 64u * u + lane;
+          const uint32_t v = buf[u];
+          const uint32_t qn = q + 64u * kEmitAhead;
+          buf[u] = qn < Q ? __builtin_nontemporal_load(&ans[qn]) : 0u;
+          r[u] = QAns{SST_NONE, 0, 0, 0};
+          if (q < Q) {
+            r[u] = ans_read(v, a.cap);
+            a.status[qb + q] = r[u].status;
           }
         }
-        hb += th;
-        bb += tb;
+#pragma unroll
+        for (int u = 0; u < kEmitAhead; ++u) {
+          const bool some = r[u].status == SST_SOME;
+          rec[u][0] = some ? img.recs[r[u].first] : 0u;
+          rec[u][1] = some && r[u].cnt > 1 ? img.recs[r[u].first + 1] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kEmitAhead; ++u) {
+          const bool some = r[u].status == SST_SOME;
+          if (some) {
+            r[u].bytes = (rec[u][0] & 0xFFu) + 1u + (r[u].cnt > 1 ? (rec[u][1] & 0xFFu) + 1u : 0u);
+            if (r[u].cnt > 2) r[u].bytes += ans_bytes(img.recs, r[u].first + 2, r[u].cnt - 2);
+          }
+          const bool hit = some || r[u].status == SST_OVERFLOW;
+          xh[u] = wave_excl(hit ? 1u : 0u, th[u]);
+          xb[u] = wave_excl(some ? r[u].bytes + 2u : 0u, tb[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kEmitAhead; ++u) {
+          const uint32_t q = q0 + 64u * u + lane;
+          const bool some = r[u].status == SST_SOME;
+          if (some || r[u].status == SST_OVERFLOW) {
+            const uint64_t o = bb + xb[u];
+            const uint64_t word = some ? o : (uint64_t)r[u].cnt;
+            a.hits[hb + xh[u]] = make_uint4((uint32_t)(qb + q), r[u].cnt, (uint32_t)word, (uint32_t)(word >> 32));
+            a.refs[hb + xh[u]] = (uint16_t)(r[u].first | (r[u].status == SST_OVERFLOW ? 0x8000u : 0u));
+            if (some) {
+              // the 2 pad bytes after the query's last record take the overhang
+              uint8_t* dst = a.dense + o;
+              *(u32_unal*)dst = rec[u][0];
+              dst += (rec[u][0] & 0xFFu) + 1u;
+              if (r[u].cnt > 1) {
+                *(u32_unal*)dst = rec[u][1];
+                dst += (rec[u][1] & 0xFFu) + 1u;
+              }
+              const uint32_t kend = r[u].first + r[u].cnt;
+              for (uint32_t k0 = r[u].first + 2; k0 < kend; k0 += 4) {  // more than two records
+                uint32_t rr[4];
+#pragma unroll
+                for (int x = 0; x < 4; ++x) rr[x] = k0 + x < kend ? img.recs[k0 + x] : 0u;
+#pragma unroll
+                for (int x = 0; x < 4; ++x)
+                  if (k0 + x < kend) {
+                    *(u32_unal*)dst = rr[x];
+                    dst += (rr[x] & 0xFFu) + 1u;
+                  }
+              }
+            }
+          }
+          hb += th[u];
+          bb += tb[u];
+        }
       }
       qb += Q;
     }
@@ -1098,7 +1147,7 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
   b.n_chunks = a.n_spec < a.chunk_cap ? a.n_spec : a.chunk_cap;
   b.chunk = (a.n_spec + b.n_chunks - 1) / b.n_chunks;
   b.n_chunks = (a.n_spec + b.chunk - 1) / b.chunk;
-  if (b.n_chunks > a.chunk_cap || b.n_chunks > (int64_t)kScanTiles * kRowsWG) return hipErrorInvalidValue;
+  if (b.n_chunks > a.chunk_cap || b.n_chunks > a.n_tiles * kRowsTile) return hipErrorInvalidValue;
   const int wgrid = (int)((b.n_chunks + kWavesPerWG - 1) / kWavesPerWG);
   (void)wave_wg;
   hipLaunchKernelGGL(k_rows_count_w, dim3(wgrid), dim3(64 * kWavesPerWG), 0, st, t, b);
@@ -1106,7 +1155,6 @@ hipError_t launch_rows_step(const TableArgs& t, const RowsArgs& a, int n_wg, siz
   // batches: a small grid keeps their launches cheap when idle)
   const int big_wg = n_wg < 64 ? n_wg : 64;
   hipLaunchKernelGGL(k_rows_count, dim3(big_wg), dim3(kRowsWG), dyn, st, t, b);
-  hipLaunchKernelGGL(k_rows_scan, dim3((unsigned)((b.n_chunks + kRowsWG - 1) / kRowsWG)), dim3(kRowsWG), 0, st, b);
   hipLaunchKernelGGL(k_rows_emit_w, dim3(wgrid), dim3(64 * kWavesPerWG), wdyn, st, t, b);
   hipLaunchKernelGGL(k_rows_emit, dim3(big_wg), dim3(kRowsWG), dyn, st, t, b);  // last: writes the header
   return hipGetLastError();

@@ -32,7 +32,7 @@ def dp():
                                    precision=TOLERANCE, seq=seq, engine=_native.get_engine(0))
 
 
-def _run(dp, wl, intensity=None, cutoff=0.5e6, mass_cutoff=50000.0, reuse=None):
+def _run(dp, wl, intensity=None, cutoff=0.5e6, mass_cutoff=50000.0, reuse=None, max_q=None):
     import torch
 
     dev = torch.device("cuda", 0)
@@ -46,7 +46,7 @@ def _run(dp, wl, intensity=None, cutoff=0.5e6, mass_cutoff=50000.0, reuse=None):
     res = dp.device_table.step_rows_device(do.data_ptr(), dpo.data_ptr(), len(wl["peak_off"]) - 1, len(wl["obs"]),
                                            ds.data_ptr(), wl["shifts"], wl["sides"], out7.data_ptr(),
                                            wl["max_weight"], dp.tolerance, dp.precision, A,
-                                           max(1, int(len(wl["a8_mass"]) * 1.1) + 64),
+                                           max_q or max(1, int(len(wl["a8_mass"]) * 1.1) + 64),
                                            d_intensity=None if di is None else di.data_ptr(),
                                            intensity_cutoff=cutoff, mass_cutoff=mass_cutoff, reuse=reuse)
     res.fetch_device()
@@ -134,6 +134,20 @@ def test_rows_step_edge_spectra(dp):
         wl = bench.workload_from(obs, offs, seqm, dp, intensity=inten if with_int else None, mass_cutoff=cut)
         res, a7 = _run(dp, wl, intensity=inten if with_int else None, mass_cutoff=cut)
         _check(dp, wl, res, a7, sample=300, seed=2)
+
+
+def test_rows_step_capacity_overflow(dp):
+    """A result too small for the step's queries is reported, not overrun
+    (each chunk checks its own end against the result's capacity after its
+    look-back), and the next step on the same engine is answered in full."""
+    import bench
+    from spectrseqtools_amd import _native
+
+    wl = bench.build_workload(600, 31, dp)
+    with pytest.raises(_native.EngineError, match="more queries"):
+        _run(dp, wl, max_q=len(wl["a8_mass"]) // 2)
+    res, a7 = _run(dp, wl)
+    _check(dp, wl, res, a7, sample=200, seed=3)
 
 
 def test_rows_step_refuses_binding_budgets(dp):
