@@ -1559,7 +1559,7 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
       !r->rows_su.ensure(std::max<size_t>(1, 4 * P) * 8) || !r->rows_ob.ensure(std::max<size_t>(1, 4 * P) * 8) ||
       !r->rows_side.ensure(2 * S * 4) || !r->rows_tot.ensure(3 * S * 4) || !r->rows_chunk.ensure((6 * NC + 6 * (NC / kRowsTile + 1)) * 8) ||
       !r->rows_big.ensure(S * 4) || !r->rows_redo.ensure(S * 4) || !r->rows_ctl.ensure(64) ||
-      !r->rows_ans.ensure(std::max<size_t>(1, 2 * kRowsAnsPerPeak * P) * 4) || !r->rows_aq.ensure(2 * S * 4))
+      !r->rows_ans.ensure(128 * S * 8 + (2 * kRowsAnsPerPeak * P / 64 + 2 * S + 2) * 64 * 4) || !r->rows_aq.ensure(2 * S * 4))
     return bail(fail(c, SST_E_NOMEM, "device allocation failed (rows step)"));
   if (fresh) {
     HIP_OK(c, hipMemsetAsync(r->rows_ctl.p, 0, 64, c->stream));
@@ -1601,7 +1601,8 @@ int sst_step_rows_device(sst_table* t, const double* d_obs, const int64_t* d_pea
   a.rows_su = (double*)r->rows_su.p;
   a.rows_ob = (double*)r->rows_ob.p;
   a.side_rows = (uint32_t*)r->rows_side.p;
-  a.ans = (uint32_t*)r->rows_ans.p;
+  a.ans_mask = (uint64_t*)r->rows_ans.p;
+  a.ans_ent = (uint32_t*)(a.ans_mask + 128 * S);
   a.ans_q = (uint32_t*)r->rows_aq.p;
   a.totals = (uint32_t*)r->rows_tot.p;
   a.chunk_tot = (unsigned long long*)r->rows_chunk.p;

@@ -480,13 +480,15 @@ struct RowsArgs {
   double* rows_su;            // scratch [4 * n_peaks]
   double* rows_ob;
   uint32_t* side_rows;        // [2 n_spec]
-  // the wave kernels' answers, written once by the count pass: one u32 per
-  // query (count << 16 | first entry, or the status of a pair without
-  // entries; sst_rows.hip ans_word), side sd of spectrum g at
-  // kRowsAnsPerPeak * (2 peak_off[g] + sd * P_g) when its queries fit there
-  // (kRowsAnsPerPeak * P_g slots; else the emit pass answers that side again
-  // from its scratch rows)
-  uint32_t* ans;              // [2 kRowsAnsPerPeak n_peaks]
+  // the wave kernels' answers, written once by the count pass, per 64-query
+  // window of a side: the mask of queries with an answer other than NONE and
+  // those answers' words (count << 16 | first entry, or 1 for EMPTY;
+  // sst_rows.hip ans_word), side sd of spectrum g from window
+  // ans_win_base(peak_off[g], P_g, sd, g) on (masks at 128 g + 64 sd) when
+  // its queries fit its kRowsAnsPerPeak * P_g slots (else the emit pass
+  // answers that side again from its scratch rows)
+  uint64_t* ans_mask;         // [128 n_spec]
+  uint32_t* ans_ent;          // [64 (2 kRowsAnsPerPeak n_peaks / 64 + 2 n_spec + 2)]
   uint32_t* ans_q;            // [2 n_spec] the side's queries, ~0: did not fit
   uint32_t* totals;           // [3 n_spec] queries, hits, payload bytes
   unsigned long long* chunk_tot;  // [3 n_chunks] totals of each wave's contiguous chunk of spectra

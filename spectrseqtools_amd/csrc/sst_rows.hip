@@ -28,7 +28,8 @@
 // Launches: k_rows_count_w (one wave per contiguous chunk of spectra, each
 // spectrum of <= 160 peaks in turn; larger spectra are listed for
 // k_rows_count, one workgroup each): A7, every window pair answered once
-// (4 B per query to scratch, the pass's one answer per pair), per-spectrum
+// (each 64-query window's mask of answers other than NONE, and those
+// answers' 4-B words, to scratch: the pass's one answer per pair), per-spectrum
 // totals of queries / hits / payload bytes and each chunk's sums;
 // k_rows_emit_w: each chunk's exclusive offsets from the 64-chunk tiles' sums
 // (added up by the count kernels) and its own tile's earlier chunks (no scan
@@ -172,6 +173,20 @@ __device__ __forceinline__ QAns ans_read(uint32_t v, uint32_t cap) {
   }
   return r;
 }
+// The count pass's stored answers: per 64-query window of a side, the mask
+// of its queries with an answer other than NONE (ans_mask, 8 B at 128 g +
+// 64 sd + window: a stored side has <= 60 windows), and the side's answers
+// other than NONE, in query order (ans_ent, 4-B words from 64 ans_win_base
+// on).  Side sd of spectrum g owns ceil(kRowsAnsPerPeak P / 64) 64-word
+// blocks from ans_win_base on, which never reach the next side's first
+// (floor(x + y) - floor(x) >= floor(y), plus one per side).
+__device__ __forceinline__ uint64_t ans_win_base(int64_t p0, uint32_t P, int sd, int64_t g) {
+  return (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P) / 64 + 2 * (uint64_t)g + (uint64_t)sd;
+}
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // the payload bytes of records [first, first + cnt): record k takes
 // (recs[k] & 0xFF) + 1 bytes
 __device__ __forceinline__ uint32_t ans_bytes(const uint32_t* recs, uint32_t first, uint32_t cnt) {
@@ -414,7 +429,7 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
     for (int sd = 0; sd < 2; ++sd) {
       const uint32_t n = a.side_rows[2 * g + sd];
       const bool stored = redo && a.ans_q[2 * g + sd] != 0xFFFFFFFFu;  // the count pass's answers, in query order
-      const uint32_t* ans = a.ans + (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)a.peak_off[g] + (uint64_t)sd * P);
+      const uint64_t wb = ans_win_base(a.peak_off[g], (uint32_t)P, sd, g);
       uint32_t Q;
       if (stored) {
         Q = a.ans_q[2 * g + sd];
@@ -433,7 +448,13 @@ __global__ __launch_bounds__(kRowsWG) void k_rows_emit(TableArgs t, RowsArgs a) 
         QAns r{SST_NONE, 0, 0, 0};
         if (q < Q) {
           if (stored) {
-            r = ans_read(ans[q], a.cap);
+            const uint64_t* mk = a.ans_mask + 128 * g + 64 * sd;
+            const uint64_t m = mk[q / 64], below = (1ull << (q & 63)) - 1ull;
+            if ((m >> (q & 63)) & 1ull) {
+              uint32_t e = (uint32_t)__builtin_popcountll(m & below);  // the side's answers before q
+              for (uint32_t w = 0; w < q / 64; ++w) e += (uint32_t)__builtin_popcountll(mk[w]);
+              r = ans_read(a.ans_ent[wb * 64 + e], a.cap);
+            }
             if (r.status == SST_SOME) r.bytes = ans_bytes(img.recs, r.first, r.cnt);
           } else {
             uint32_t s, e;
@@ -560,64 +581,24 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
   return v;
 }
 
-// A7, filters and the kept rows of every breakage (mass order) of spectrum g.  A peak's bitset words are all loaded before any is tested
-// (valid_window, sst_quant.h, with its loads hoisted: the first and last word
-// of each breakage's window; the middle words of a wider window afterwards),
-// and the A7 codes are stored after, so no store orders the loads.
+// A7, filters and the kept rows of every breakage (mass order) of spectrum g.
+// (Hoisting every breakage's bitset loads ahead of the code stores measured
+// no faster: most windows meet the all-reachable run and load nothing, and
+// the hoisted form took 17 more VGPRs.)
 __device__ void wave_load(WaveLds& L, const TableArgs& t, const RowsArgs& a, int64_t p0, uint32_t P, double su_seq,
                           bool write_a7) {
   const int lane = threadIdx.x & 63;
   for (uint32_t p = lane; p < P; p += 64) {
     const double o = a.obs[p0 + p];
-    uint32_t wa[4], wb[4], bits[4];  // window words; bits: a & 63 | (b & 63) << 8 | load << 16 | code << 24
-    uint64_t x0[4], x1[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      wa[k] = wb[k] = 0u;
-      bits[k] = 0u;  // code 0
-      if (k >= a.n_shifts) continue;
-      double lof, hif;
-      quantise_lean(o - a.shift[k], a.tol * o, a.prec, a.rprec, lof, hif);
-      const int64_t lo = (int64_t)lof, hi = (int64_t)hif;
-      const int64_t aa = lo < 1 ? 1 : lo, bb = hi < t.limit - 1 ? hi : t.limit - 1;
-      if (hi < lo || aa > hi) continue;
-      if (aa <= bb && bb >= t.full_lo && aa < t.full_hi) {
-        bits[k] = 1u << 24;  // meets the all-reachable run
-        continue;
-      }
-      bits[k] = (uint32_t)(uint8_t)(hi >= t.limit ? (int8_t)-1 : (int8_t)0) << 24;  // unless a bit of [aa, bb] is set
-      if (aa <= bb && bb >= t.first_reach) {
-        wa[k] = (uint32_t)(aa >> 6);
-        wb[k] = (uint32_t)(bb >> 6);
-        bits[k] |= (uint32_t)(aa & 63) | (uint32_t)(bb & 63) << 8 | 1u << 16;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      x0[k] = x1[k] = 0;
-      if (bits[k] & (1u << 16)) {
-        x0[k] = t.valid[wa[k]];
-        if (wb[k] != wa[k]) x1[k] = t.valid[wb[k]];
-      }
-    }
     uint8_t kp = 0;
-    const bool inten = a.intensity ? a.intensity[p0 + p] > a.intensity_cutoff : true;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (k >= a.n_shifts) continue;
-      int8_t code = (int8_t)(bits[k] >> 24);
-      if (bits[k] & (1u << 16)) {
-        const uint32_t ba = bits[k] & 63u, bb = (bits[k] >> 8) & 63u;
-        const uint64_t hm = ~0ull >> (63 - bb);
-        uint64_t m0 = x0[k] & (~0ull << ba);
-        if (wa[k] == wb[k]) m0 &= hm;
-        bool any = m0 != 0;
-        if (wb[k] != wa[k]) any |= (x1[k] & hm) != 0;
-        if (!any && wb[k] - wa[k] > 1u) any = any_bits(t.valid, ((int64_t)wa[k] + 1) << 6, ((int64_t)wb[k] << 6) - 1);
-        if (any) code = 1;
-      }
-      if (write_a7) a.valid_out[(int64_t)k * a.n_peaks + p0 + p] = code;
+    for (int k = 0; k < a.n_shifts; ++k) {
       const double su = o - a.shift[k];
+      double lof, hif;
+      quantise_lean(su, a.tol * o, a.prec, a.rprec, lof, hif);
+      const int8_t code =
+          valid_window(t.valid, t.limit, (int64_t)lof, (int64_t)hif, t.full_lo, t.full_hi, t.first_reach);
+      if (write_a7) a.valid_out[(int64_t)k * a.n_peaks + p0 + p] = code;
+      const bool inten = a.intensity ? a.intensity[p0 + p] > a.intensity_cutoff : true;
       const bool full = (a.sides[k] & 3) == 3;
       const bool keep = code == 1 && inten && o < a.mass_cutoff && su < su_seq + a.max_variance &&
                         (su > su_seq - a.max_variance || !full);
@@ -844,7 +825,7 @@ __device__ __forceinline__ PairImg global_img(const TableArgs& t) {
 
 }  // namespace
 
-// six waves per SIMD (80 VGPRs, two spilled: same-box A/B 179-180 against 186 us/step at the natural 90 VGPRs and five)
+// six waves per SIMD (<= 80 VGPRs: same-box A/B 179-180 against 186 us/step at 90 VGPRs and five)
 __global__ __launch_bounds__(64 * kWavesPerWG) __attribute__((amdgpu_waves_per_eu(6))) void k_rows_count_w(TableArgs t, RowsArgs a) {
   __shared__ WaveLds Ls[kWavesPerWG];
   WaveLds& L = Ls[threadIdx.x >> 6];
@@ -886,7 +867,7 @@ __global__ __launch_bounds__(64 * kWavesPerWG) __attribute__((amdgpu_waves_per_e
       // back in query order instead of re-forming and re-answering the pairs
       // (the side's fixed slots; a side with more queries keeps its rows in
       // scratch and is answered again by the emit pass)
-      const uint64_t base = (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P);
+      const uint64_t wb = ans_win_base(p0, P, sd, g);
       const bool fits = Q <= (uint32_t)kRowsAnsPerPeak * P;
       if (lane == 0) a.ans_q[2 * g + sd] = fits ? Q : 0xFFFFFFFFu;
       // a side past its slots: the workgroup emit answers it again (listed once per spectrum)
@@ -900,17 +881,23 @@ __global__ __launch_bounds__(64 * kWavesPerWG) __attribute__((amdgpu_waves_per_e
         }
       }
       uint32_t s0 = 0;  // the start of query q0
+      uint64_t mka = 0;   // lane w: window w's mask (stored once, after the side)
+      uint32_t ne = 0;    // the side's answers other than NONE so far
       for (uint32_t q0 = 0; q0 < Q; q0 += 64) {
         const uint32_t q = q0 + lane;
         uint32_t s, e;
         s0 = wave_pair_window(L, n, q0, s0, s, e);
-        if (q >= Q) continue;
-        const QAns r = wave_reply(a, wave_ask(L, t, a, true, s, e));
+        QAns r{SST_NONE, 0, 0, 0};
+        if (q < Q) r = wave_reply(a, wave_ask(L, t, a, true, s, e));
         nh += (r.status == SST_SOME || r.status == SST_OVERFLOW);
         nb += r.status == SST_SOME ? r.bytes + 2u : 0u;
-        if (fits)
-          a.ans[base + q] = ans_word(r);
+        const bool kept = r.status != SST_NONE;  // NONE (most pairs) is stored as a clear mask bit only
+        const uint64_t m = __ballot(kept);
+        if ((uint32_t)lane == q0 / 64) mka = m;
+        if (fits && kept) a.ans_ent[wb * 64 + ne + mbcnt64(m)] = ans_word(r);
+        ne += (uint32_t)__builtin_popcountll(m);
       }
+      if (fits && (uint32_t)lane < (Q + 63) / 64) a.ans_mask[128 * g + 64 * sd + lane] = mka;
       nq += Q;
       wsync();
       RPROF_T(c5);
@@ -980,15 +967,22 @@ __device__ void chunk_prefix(const RowsArgs& a, int64_t w, uint64_t off[3]) {
   for (int c = 0; c < 3; ++c) off[c] = wave_sum64(v[c]);
 }
 
-constexpr int kEmitAhead = 4;  // answer windows in flight ahead of the one emitted
+struct EmitLds {
+  uint64_t mask[2][64];   // each side's window masks
+  uint32_t ebase[2][64];  // the side's answers before each window
+  uint32_t ne[2];         // the side's answers other than NONE
+  uint16_t qring[128];    // the queries of answers [64 c, 64 c + 128), at answer & 127
+};
 
 }  // namespace
 
-// six waves per SIMD (80 VGPRs; the four windows' state would take 87 and five): the emit is latency-bound, waves count
-__global__ __launch_bounds__(64 * kWavesPerWG) __attribute__((amdgpu_waves_per_eu(6))) void k_rows_emit_w(TableArgs t, RowsArgs a) {
+__global__ __launch_bounds__(64 * kWavesPerWG) void k_rows_emit_w(TableArgs t, RowsArgs a) {
   // the answers the count pass stored, streamed back in query order (a
   // spectrum with a side past its slots, or over kWP peaks, is the workgroup
-  // emit's): no LDS, so the waves per CU are set by registers alone
+  // emit's); 1.5 KB of LDS per wave for the spectrum's window masks, so the
+  // waves per CU are set by registers
+  __shared__ EmitLds Es[kWavesPerWG];
+  EmitLds& E = Es[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
   const PairImg img = global_img(t);
   const int64_t w = (int64_t)blockIdx.x * kWavesPerWG + (threadIdx.x >> 6);
@@ -1021,86 +1015,118 @@ __global__ __launch_bounds__(64 * kWavesPerWG) __attribute__((amdgpu_waves_per_e
     off[1] += a.totals[3 * g + 1];
     off[2] += a.totals[3 * g + 2];
     if (P > (uint32_t)kWP || Q0 == 0xFFFFFFFFu || Q1 == 0xFFFFFFFFu) continue;  // the workgroup kernel's
+    // both sides' window masks and each window's first answer (the answers
+    // before it: a wave prefix of the masks' popcounts) to LDS, and each
+    // side's first 64 answer words, in one round trip
+    {
+      const uint64_t m0 = (uint32_t)lane < (Q0 + 63) / 64 ? __builtin_nontemporal_load(&a.ans_mask[128 * g + lane]) : 0ull;
+      const uint64_t m1 = (uint32_t)lane < (Q1 + 63) / 64 ? __builtin_nontemporal_load(&a.ans_mask[128 * g + 64 + lane]) : 0ull;
+      uint32_t n0, n1;
+      const uint32_t e0 = wave_excl((uint32_t)__builtin_popcountll(m0), n0);
+      const uint32_t e1 = wave_excl((uint32_t)__builtin_popcountll(m1), n1);
+      E.mask[0][lane] = m0;
+      E.mask[1][lane] = m1;
+      E.ebase[0][lane] = e0;
+      E.ebase[1][lane] = e1;
+      if (lane == 0) {
+        E.ne[0] = n0;
+        E.ne[1] = n1;
+      }
+      wsync();
+    }
+    const uint32_t* ent0 = a.ans_ent + ans_win_base(p0, P, 0, g) * 64;
+    const uint32_t* ent1 = a.ans_ent + ans_win_base(p0, P, 1, g) * 64;
+    uint32_t cur = Q0 ? __builtin_nontemporal_load(&ent0[lane]) : 0u;
+    const uint32_t pre1 = Q1 ? __builtin_nontemporal_load(&ent1[lane]) : 0u;
     for (int sd = 0; sd < 2; ++sd) {
       const uint32_t Q = sd ? Q1 : Q0;
-      const uint32_t* ans = a.ans + (uint64_t)kRowsAnsPerPeak * (2 * (uint64_t)p0 + (uint64_t)sd * P);
-      // kEmitAhead windows at a time, phase by phase so that their latencies
-      // overlap: the answers (loaded one group ahead), then every SOME
-      // answer's first two records (its bytes and payload), the wave prefix
-      // sums, and the stores in window order
-      uint32_t buf[kEmitAhead];
+      const uint32_t nwin = (Q + 63) / 64;
+      const uint32_t* ent = sd ? ent1 : ent0;
+      const uint32_t ne = E.ne[sd];
+      if (sd) cur = pre1;
+      // The side's answers other than NONE stream through two 64-word
+      // registers (answers [64 c, 64 c + 128)), the next block loaded as
+      // the stream enters the last.  A pass over the windows writes every
+      // status byte (an answer reaches its query's lane by ds_bpermute) and
+      // each answer's query to an LDS ring; each block of 64 answers, once
+      // the windows have passed it, is emitted in one go: one lane per
+      // answer, its first records loaded together, one pair of wave prefix
+      // sums per 64 answers (hit records, refs and payload in query order).
+      uint32_t c = 0;
+      uint32_t nxt = 64u < ne ? __builtin_nontemporal_load(&ent[64 + lane]) : 0u;
+      auto emit_block = [&](uint32_t words, uint32_t k) {
+        const uint32_t e = 64u * k + lane;
+        wsync();  // the ring's query indices
+        const QAns r = e < ne ? ans_read(words, a.cap) : QAns{SST_NONE, 0, 0, 0};
+        const uint32_t q = E.qring[e & 127u];
+        const bool some = r.status == SST_SOME;
+        uint32_t rec[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int u = 0; u < kEmitAhead; ++u) {
-        const uint32_t q = (uint32_t)lane + 64u * u;
-        buf[u] = q < Q ? __builtin_nontemporal_load(&ans[q]) : 0u;
-      }
-      for (uint32_t q0 = 0; q0 < Q; q0 += 64u * kEmitAhead) {
-        QAns r[kEmitAhead];
-        uint32_t rec[kEmitAhead][2], xh[kEmitAhead], xb[kEmitAhead], th[kEmitAhead], tb[kEmitAhead];
+        for (int x = 0; x < 4; ++x)
+          if (some && (uint32_t)x < r.cnt) rec[x] = img.recs[r.first + x];
+        uint32_t nb = 0;
+        if (some) {
 #pragma unroll
-        for (int u = 0; u < kEmitAhead; ++u) {
-          const uint32_t q = q0 + 64u * u + lane;
-          const uint32_t v = buf[u];
-          const uint32_t qn = q + 64u * kEmitAhead;
-          buf[u] = qn < Q ? __builtin_nontemporal_load(&ans[qn]) : 0u;
-          r[u] = QAns{SST_NONE, 0, 0, 0};
-          if (q < Q) {
-            r[u] = ans_read(v, a.cap);
-            a.status[qb + q] = r[u].status;
-          }
+          for (int x = 0; x < 4; ++x) nb += (uint32_t)x < r.cnt ? (rec[x] & 0xFFu) + 1u : 0u;
+          if (r.cnt > 4) nb += ans_bytes(img.recs, r.first + 4, r.cnt - 4);
         }
-#pragma unroll
-        for (int u = 0; u < kEmitAhead; ++u) {
-          const bool some = r[u].status == SST_SOME;
-          rec[u][0] = some ? img.recs[r[u].first] : 0u;
-          rec[u][1] = some && r[u].cnt > 1 ? img.recs[r[u].first + 1] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kEmitAhead; ++u) {
-          const bool some = r[u].status == SST_SOME;
+        uint32_t th, tb;
+        const bool hit = some || r.status == SST_OVERFLOW;
+        const uint32_t xh = wave_excl(hit ? 1u : 0u, th);
+        const uint32_t xb = wave_excl(some ? nb + 2u : 0u, tb);
+        if (hit) {
+          const uint64_t o = bb + xb;
+          const uint64_t word = some ? o : (uint64_t)r.cnt;
+          a.hits[hb + xh] = make_uint4((uint32_t)(qb + q), r.cnt, (uint32_t)word, (uint32_t)(word >> 32));
+          a.refs[hb + xh] = (uint16_t)(r.first | (r.status == SST_OVERFLOW ? 0x8000u : 0u));
           if (some) {
-            r[u].bytes = (rec[u][0] & 0xFFu) + 1u + (r[u].cnt > 1 ? (rec[u][1] & 0xFFu) + 1u : 0u);
-            if (r[u].cnt > 2) r[u].bytes += ans_bytes(img.recs, r[u].first + 2, r[u].cnt - 2);
-          }
-          const bool hit = some || r[u].status == SST_OVERFLOW;
-          xh[u] = wave_excl(hit ? 1u : 0u, th[u]);
-          xb[u] = wave_excl(some ? r[u].bytes + 2u : 0u, tb[u]);
-        }
+            // the 2 pad bytes after the query's last record take the overhang
+            uint8_t* dst = a.dense + o;
 #pragma unroll
-        for (int u = 0; u < kEmitAhead; ++u) {
-          const uint32_t q = q0 + 64u * u + lane;
-          const bool some = r[u].status == SST_SOME;
-          if (some || r[u].status == SST_OVERFLOW) {
-            const uint64_t o = bb + xb[u];
-            const uint64_t word = some ? o : (uint64_t)r[u].cnt;
-            a.hits[hb + xh[u]] = make_uint4((uint32_t)(qb + q), r[u].cnt, (uint32_t)word, (uint32_t)(word >> 32));
-            a.refs[hb + xh[u]] = (uint16_t)(r[u].first | (r[u].status == SST_OVERFLOW ? 0x8000u : 0u));
-            if (some) {
-              // the 2 pad bytes after the query's last record take the overhang
-              uint8_t* dst = a.dense + o;
-              *(u32_unal*)dst = rec[u][0];
-              dst += (rec[u][0] & 0xFFu) + 1u;
-              if (r[u].cnt > 1) {
-                *(u32_unal*)dst = rec[u][1];
-                dst += (rec[u][1] & 0xFFu) + 1u;
+            for (int x = 0; x < 4; ++x)
+              if ((uint32_t)x < r.cnt) {
+                *(u32_unal*)dst = rec[x];
+                dst += (rec[x] & 0xFFu) + 1u;
               }
-              const uint32_t kend = r[u].first + r[u].cnt;
-              for (uint32_t k0 = r[u].first + 2; k0 < kend; k0 += 4) {  // more than two records
-                uint32_t rr[4];
+            const uint32_t kend = r.first + r.cnt;
+            for (uint32_t k0 = r.first + 4; k0 < kend; k0 += 4) {  // more than four records
+              uint32_t rr[4];
 #pragma unroll
-                for (int x = 0; x < 4; ++x) rr[x] = k0 + x < kend ? img.recs[k0 + x] : 0u;
+              for (int x = 0; x < 4; ++x) rr[x] = k0 + x < kend ? img.recs[k0 + x] : 0u;
 #pragma unroll
-                for (int x = 0; x < 4; ++x)
-                  if (k0 + x < kend) {
-                    *(u32_unal*)dst = rr[x];
-                    dst += (rr[x] & 0xFFu) + 1u;
-                  }
-              }
+              for (int x = 0; x < 4; ++x)
+                if (k0 + x < kend) {
+                  *(u32_unal*)dst = rr[x];
+                  dst += (rr[x] & 0xFFu) + 1u;
+                }
             }
           }
-          hb += th[u];
-          bb += tb[u];
         }
+        hb += th;
+        bb += tb;
+        wsync();  // the ring's slots are rewritten
+      };
+      for (uint32_t wi = 0; wi < nwin; ++wi) {
+        const uint64_t m = E.mask[sd][wi];
+        const uint32_t base = E.ebase[sd][wi];
+        if (base >= 64u * (c + 1)) {  // block c is complete: emit it, the stream enters the next
+          emit_block(cur, c);
+          ++c;
+          cur = nxt;
+          nxt = 64u * (c + 1) < ne ? __builtin_nontemporal_load(&ent[64u * (c + 1) + lane]) : 0u;
+        }
+        const uint32_t q = 64u * wi + lane;
+        const uint32_t e = base + mbcnt64(m);
+        const uint32_t v0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((e & 63u) << 2), (int)cur);
+        const uint32_t v1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((e & 63u) << 2), (int)nxt);
+        const bool has = (m >> lane) & 1ull;
+        const uint32_t v = has ? ((e >> 6) > c ? v1 : v0) : 0u;
+        if (q < Q) a.status[qb + q] = ans_read(v, a.cap).status;
+        if (has) E.qring[e & 127u] = (uint16_t)q;
+      }
+      if (ne > 64u * c) {  // the last blocks
+        emit_block(cur, c);
+        if (ne > 64u * (c + 1)) emit_block(nxt, c + 1);
       }
       qb += Q;
     }
