@@ -599,9 +599,12 @@ def main():
         if rows_mode:
             # the step from the peaks: each peak (8) read once, its A7 codes and
             # bitset words, every side row written to scratch and read back
-            # (16 + 16), then per query its status byte and per hit the dense
-            # record (16), the pair-list ref (2) and the candidate bytes; the
-            # queries themselves never touch HBM
+            # (16 + 16: the round-3 model, kept so that fractions compare
+            # across rounds -- the kernels now keep the rows in LDS and move
+            # the compact answer scratch instead), then
+            # per query its status byte and per hit the dense record (16), the
+            # pair-list ref (2) and the candidate bytes; the queries themselves
+            # never touch HBM
             bk["k_explain_scan"] = float(8 * P + n7 + bits7 + 32 * w_["side_rows"] + n8 +
                                          18 * rf["n_hits"] + cand_bytes)
             l2["k_explain_scan"] = float(bits7)
@@ -699,7 +702,8 @@ def main():
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": ("k_rows_count + k_rows_scan + k_rows_emit (the step from the peaks)" if rows_mode else
+            "kernel": ("k_rows_count_w + k_rows_emit_w (+ k_rows_count / k_rows_emit for spectra over 160 peaks: "
+                       "the step from the peaks)" if rows_mode else
                        "k_step (k_is_valid_peaks + k_explain_scan in one launch)" if args.fused_step and
                        dom == "k_explain_scan" else dom),
             "achieved": achieved,
@@ -727,7 +731,7 @@ def main():
                          "nomemo": int(stats[3]), "index_loads": int(stats[4]),
                          "candidates": int(res.count[some].sum()), "payload_bytes": int(stats[5] + stats[7]),
                          "hits": n_hits0, "dense_payload_bytes": int(len(res.payload))},
-        "step": ("k_rows_count + k_rows_scan + k_rows_emit (from the peaks)" if rows_mode else
+        "step": ("k_rows_count_w + k_rows_count + k_rows_emit_w + k_rows_emit (from the peaks)" if rows_mode else
                  "k_is_valid + k_explain_scan (packing its own dense result)" if fused else
                  "k_is_valid + k_explain_scan + k_result_pack") +
                 " per step: status bytes, dense hit list and dense payload of every query (the complete "
