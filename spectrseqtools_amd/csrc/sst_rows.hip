@@ -547,6 +547,7 @@ struct WaveLds {
   uint32_t hist[64];  // wave_pair_window: starts per position of a 64-query window
 };
 static_assert(kWP < 256, "u8 peak indices and kept-row counts");
+static_assert(kRowsAnsPerPeak * kWP <= 64 * 64, "a stored side's window masks: one per lane of a wave (<= 64 windows)");
 
 // LDS written by some lanes of the wave, read by others: order the accesses
 __device__ __forceinline__ void wsync() {
