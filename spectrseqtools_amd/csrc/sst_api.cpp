@@ -88,7 +88,7 @@ struct sst_ctx {
   // allocating tens of GB per call costs seconds), with its hash epoch and the
   // memo entries per query seen so far (the next call's first chunk size)
   struct LbfWs {
-    DevBuf flags, lchild, vlo, gtab, ctab, glist, ctl, bstart, bgroups, qi, qrow, roots, ncnt, grec, crec, ngrp;
+    DevBuf flags, lpar, lval, gtab, ctab, glist, ctl, bstart, bgroups, qi, qrow, roots, ncnt, grec, crec, ngrp;
     uint64_t S = 0, ncap = 0, budget = 0;
     bool by_default = false;
     int epoch = 0;
@@ -3370,10 +3370,10 @@ static int lbf_frontier(sst_table* t, sst_ctx::LbfWs& W, const double* d_su, con
     W.ncap = std::min<uint64_t>(kNodesPerSlot * W.S, 0xFFFFFFF0ull);
   }
   const uint64_t S = W.S, ncap = W.ncap;
-  DevBuf &flags = W.flags, &lchild = W.lchild, &vlo = W.vlo, &gtab = W.gtab, &ctab = W.ctab,
+  DevBuf &flags = W.flags, &lpar = W.lpar, &lval = W.lval, &gtab = W.gtab, &ctab = W.ctab,
          &glist = W.glist, &ctl = W.ctl, &bstart = W.bstart, &bgroups = W.bgroups, &qi = W.qi, &qrow = W.qrow,
          &roots = W.roots, &ncnt = W.ncnt, &grec = W.grec, &crec = W.crec, &ngrp = W.ngrp;
-  if (!flags.ensure(ncap) || !lchild.ensure(ncap * 4) || !vlo.ensure(ncap * 2) ||
+  if (!flags.ensure(ncap) || !lpar.ensure(ncap * 4) || !lval.ensure(ncap * 2) ||
       !gtab.ensure((size_t)ring * S * lbf_group_bytes()) || !ctab.ensure((size_t)ring * S * lbf_cand_bytes(2)) ||
       !glist.ensure((size_t)ring * S * 4) || !ctl.ensure(sizeof(FCtl)) || !grec.ensure(S * lbf_grec_bytes()) ||
       !crec.ensure(S * lbf_crec_bytes(2)) || !ngrp.ensure(S * 4)) {
@@ -3448,8 +3448,8 @@ static int lbf_frontier(sst_table* t, sst_ctx::LbfWs& W, const double* d_su, con
       return fail(c, SST_E_NOMEM, "device allocation failed (length-bound frontier roots)");
     a.root_node = (uint32_t*)roots.p;
     a.flags = (uint8_t*)flags.p;
-    a.lchild = (uint32_t*)lchild.p;
-    a.val = (uint16_t*)vlo.p;
+    a.lpar = (uint32_t*)lpar.p;
+    a.lval = (uint16_t*)lval.p;
     a.ncap = ncap;
     a.gtab = (char*)gtab.p;
     a.gmask = (uint32_t)(S - 1);

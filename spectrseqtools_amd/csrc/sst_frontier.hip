@@ -32,7 +32,10 @@
 //   cands     one per left edge (child (query, mass, rank)): hash ring, entry
 //             {key, parent node, child budgets A B, the child's FV key}
 //   nodes     ids allocated per group (ranks lo..hv ascending): flags, left
-//             child id, lower / upper value packed in 16 bits
+//             parent id (a node with a left parent, or its root slot), and
+//             its left child's lower / upper value packed in 16 bits, pushed
+//             there by the child (values run bands in reverse: the child's
+//             first); a root's value goes to its root slot the same way
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -45,9 +48,11 @@ namespace {
 
 constexpr int kProbeMax = 4096;
 constexpr uint32_t kRootBit = 0x80000000u;
+constexpr uint32_t kRootUnset = 0xFFFFFFFFu;  // a root slot whose node has not pushed its value
 constexpr uint32_t kNodeSeg = 512;  // k_lbf_nodes: ids per ticket
 constexpr uint32_t kFreshBuf = 640;  // > kNodeSeg + 127: the nodes of a range moved to group starts
 constexpr uint8_t kFLeft = 1, kFUp = 2, kFZero = 4, kFCand = 8;  // kFCand: k_lbf_groups' mark, until k_lbf_nodes
+constexpr uint8_t kFPar = 16;  // k_lbf_nodes: the node has a left parent or is a root (lpar)
 
 struct alignas(32) FGroup {
   uint64_t key;
@@ -339,6 +344,7 @@ __global__ __launch_bounds__(256) void k_lbf_roots(FrontierArgs a) {
       } else {
         FCand<KW>& e = C[cs];
         e.parent = kRootBit | (uint32_t)(jj * a.rstride + s);
+        a.root_node[(size_t)jj * a.rstride + s] = kRootUnset;  // its value, once band 0's values run
         e.A = (uint8_t)q.A0;
         e.B = (uint8_t)qrow_cap(rtop);
 #pragma unroll
@@ -564,7 +570,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
 #pragma unroll
     for (int w = 0; w < KW; ++w) key[w] = ~0ull;
     int A = 0, B = 0, win = -1;
-    if (has) {  // this rank's own candidate, straight from the hash, and its parent's child link
+    bool hpar = false;  // a left parent (or a root slot): its id to lpar (this node's own slot), the value pushed later
+    if (has) {  // this rank's own candidate, straight from the hash
       const uint32_t cs = cand_find<KW>(Cb, a.cmask, fkey(ftagb(a, (uint32_t)band), jj, m, (uint32_t)k));
       if (cs == UINT32_MAX) {
         set_overflow(a, 16);  // cannot happen: the mask bit follows the insertion
@@ -575,9 +582,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
         A = c.A;
         B = c.B;
         win = k;
-        const uint32_t par = c.parent;
-        if (par & kRootBit) a.root_node[par & ~kRootBit] = id;
-        else a.lchild[par] = id;
+        a.lpar[id] = c.parent;
+        hpar = true;
       }
     }
 #pragma unroll
@@ -626,7 +632,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     const int64_t m2 = (int64_t)m - wk;
     const bool bud = !mod || (A > 0 && B > 0);
     const bool latt = live && bud && m2 >= 0 && (m2 == 0 || (int)a.lr[q.lr_off + m2] <= k);
-    if (live) a.flags[id] = (uint8_t)((latt ? kFLeft : 0) | (k > lo ? kFUp : 0) | (latt && m2 == 0 ? kFZero : 0));
+    if (live)
+      a.flags[id] = (uint8_t)((latt ? kFLeft : 0) | (k > lo ? kFUp : 0) | (latt && m2 == 0 ? kFZero : 0) |
+                              (hpar ? kFPar : 0));
     bool emit = latt && m2 > 0;
     const uint32_t band2 = emit ? (uint32_t)((q.hi - m2) / a.wb) : 0u;
     const uint32_t slot2 = band2 & rmask;
@@ -720,15 +728,17 @@ __global__ void k_lbf_mark(FrontierArgs a, int band) {
 // group (ranks ascending) a node's values fold its left branch into the node
 // below's: lower = min, upper = max over the group's ranks up to it -- a
 // segmented prefix min / max over consecutive node ids.  A wave takes a range
-// of whole groups and runs it 64 nodes at a time (a lane per node: every
-// left child's value load in flight at once; the group open at a step's
-// start carried from the step before); lower with 255 as "no path" (min(default,
-// x) at the roots), upper from -1
+// of whole groups and runs it 64 nodes at a time (a lane per node; the group
+// open at a step's start carried from the step before); lower with 255 as "no
+// path" (min(default, x) at the roots), upper from -1.  A node's left child
+// pushed its value into the node's lval slot when the child's (later) band
+// ran, so the node reads its own slot; it pushes its own value to its left
+// parent the same way (one random write per edge instead of the parent's
+// random read of the child's value and the child's random write of a link).
 __global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
   if (__hip_atomic_load(&a.ctl->overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
   const int lane = threadIdx.x & 63;
   const uint32_t s0 = a.band_start[band], s1 = a.band_start[band + 1];
-  const uint32_t n_nodes = a.band_start[a.n_bands];  // every id below is a node of this chunk
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   const uint32_t nn = s1 - s0;
@@ -746,18 +756,14 @@ __global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
     const uint32_t x = c0 + (uint32_t)lane;
     const bool live = x < r1;
     const uint8_t f = live ? a.flags[x] : (uint8_t)0;
+    const uint32_t par = (f & kFPar) ? a.lpar[x] : 0u;
     n_edges += (uint32_t)__builtin_popcountll(__ballot((f & kFLeft) && !(f & kFZero)));
     int vl = 255, vh = -1;
     if (f & kFLeft) {
       vl = 1;  // a left move onto mass 0: 0 + 1
       vh = 1;
       if (!(f & kFZero)) {
-        uint32_t c = a.lchild[x];
-        if (c >= n_nodes || c < s1) {  // a left child lies in a later band: never unset or stale
-          set_overflow(a, 32);
-          c = x;
-        }
-        const uint32_t p = a.val[c];
+        const uint32_t p = a.lval[x];  // the left child's value, pushed by the child's band
         const int l = (int)(p & 0xFFu) + 1;
         vl = l > 255 ? 255 : l;
         vh = (int)(p >> 8);  // upper + 1: -1 + 1 = 0 (the reference's default feeds the max)
@@ -783,7 +789,12 @@ __global__ __launch_bounds__(256) void k_lbf_values(FrontierArgs a, int band) {
       vl = clo < vl ? clo : vl;
       vh = chi > vh ? chi : vh;
     }
-    if (live) a.val[x] = (uint16_t)(vl | ((vh + 1) << 8));
+    const uint16_t pk = (uint16_t)(vl | ((vh + 1) << 8));
+    if (f & kFPar) {  // to the left parent, in an earlier band (a heavier mass) whose run comes later, or the root slot
+      if (par & kRootBit) a.root_node[par & ~kRootBit] = pk;
+      else if (par >= s0) set_overflow(a, 32);  // cannot happen
+      else a.lval[par] = pk;
+    }
     const int last = r1 - c0 >= 64u ? 63 : (int)(r1 - c0 - 1u);
     clo = __shfl(vl, last, 64);
     chi = __shfl(vh, last, 64);
@@ -808,12 +819,11 @@ __global__ __launch_bounds__(256) void k_lbf_out(FrontierArgs a) {
   const int top = (int)q.K - 1;
   for (int64_t v = q.lo < 1 ? 1 : q.lo; v <= q.hi; ++v) {
     if (top < 0 || (int)a.lr[q.lr_off + v] > top) continue;  // pair(top, v) == 0: the default
-    uint32_t id = a.root_node[(size_t)jj * a.rstride + (size_t)(v - q.lo)];
-    if (id >= a.band_start[a.n_bands]) {  // every reachable root is a band-0 node
+    const uint32_t p = a.root_node[(size_t)jj * a.rstride + (size_t)(v - q.lo)];  // the root's value
+    if (p == kRootUnset) {  // cannot happen: every reachable root is a band-0 node
       set_overflow(a, 32);
       return;
     }
-    const uint32_t p = a.val[id];
     const int l = (int)(p & 0xFFu), h = (int)(p >> 8) - 1;
     bl = l < bl ? l : bl;
     bh = h > bh ? h : bh;

@@ -350,10 +350,11 @@ struct FrontierArgs {
   int n_bands;     // band_start[n_bands] = the chunk's node count (after the last band)
   FQInfo* qi;
   uint32_t* qrow;  // [n_chunk][128]: rank -> w | cap << 20 | is_mod << 28
-  uint32_t* root_node;
+  uint32_t* root_node;  // per root slot: the root node's packed value (pushed by k_lbf_values)
   uint8_t* flags;
-  uint32_t* lchild;
-  uint16_t* val;  // per node: lower | (upper + 1) << 8 (one load per left child)
+  uint32_t* lpar;  // per node with a left parent: the parent's id, or kRootBit | its root slot (kFPar)
+  uint16_t* lval;  // per node with a left move onto a mass > 0: its left child's lower | (upper + 1) << 8,
+                   // pushed by the child
   uint64_t ncap;
   char* gtab;
   uint32_t gmask;
