@@ -51,7 +51,11 @@ def main():
     fr = [r["stages"]["length"]["frontier"] for r in runs.values()]
     assert all(f["nodes"] == fr[0]["nodes"] and f["chunks"] == fr[0]["chunks"] for f in fr), fr
     N, G, E = fr[0]["nodes"], fr[0]["groups"], fr[0]["edges"]
-    model = runs["trace"]["stages"]["length"]["roofline"]
+    # DESIGN §4's per-unit model for these counts, as pipeline_bench computes it now (not the copy in the run's
+    # JSON: a re-join after a model change uses the current model); the trace run's kernel time
+    sys.path.insert(0, "tools")
+    from pipeline_bench import frontier_roofline
+    model = frontier_roofline(fr[0], runs["trace"]["stages"]["length"]["kernels"])
     out = {"tag": tag, "spectra": runs["trace"]["spectra"], "nodes": N, "groups": G, "edges": E,
            "key_words": fr[0]["key_words"], "chunks": fr[0]["chunks"], "model": model, "kernels": {}}
     tot = {"s": 0.0, "hbm": 0.0, "algo": model["algorithmic_bytes"]}

@@ -141,14 +141,15 @@ def frontier_roofline(fr, kernels):
     k_lbf_nodes, k_lbf_values, all under the k_length_bound profile id) against
     the per-unit model of DESIGN.md §4: algorithmic bytes at their natural
     sizes per node N, group G and edge E (a left move onto a mass > 0: one
-    candidate insert, find and link), and the random lines they touch -- the
-    kernels' real bound, priced against the chip's random-line rate."""
+    candidate insert and find, the child's value pushed to the parent), and
+    the random lines they touch -- the kernels' real bound, priced against the
+    chip's random-line rate."""
     N, G, E, kw = fr["nodes"], fr.get("groups", 0), fr.get("edges", 0), max(1, fr.get("key_words", 1))
     cand = {1: 24, 2: 32, 4: 48}[kw]
-    per_node, per_group, per_edge = 19, 97, 34 + 2 * cand
+    per_node, per_group, per_edge = 17, 97, 36 + 2 * cand
     algo = per_node * N + per_group * G + per_edge * E
-    lines = N + G + 5 * E  # lowest-rank byte per node; group entry per group; per edge the child's group entry,
-    # its candidate slot (insert, then find), the parent's link and the child's value (DESIGN §4)
+    lines = N + G + 4 * E  # lowest-rank byte per node; group entry per group; per edge the child's group entry,
+    # its candidate slot (insert, then find) and the value pushed into the parent's slot (DESIGN §4)
     ms = kernels.get("k_length_bound", [0.0])[0]
     s = ms / 1e3
     achieved = algo / s / 1e9 if s > 0 else 0.0
