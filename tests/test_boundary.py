@@ -4,6 +4,7 @@ HIP device is visible.  CPU only."""
 import ctypes
 import os
 import re
+import shutil
 import subprocess
 
 import numpy as np
@@ -34,9 +35,13 @@ def test_library_exports_every_header_symbol():
     assert set(header_functions()) <= exported
 
 
-def test_library_targets_gfx950():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _native.LIB_PATH],
-                         capture_output=True, text=True)
+def test_library_targets_gfx950(tmp_path):
+    # llvm-objdump --offloading writes the code objects it lists next to its
+    # input: run it on a copy in a scratch directory, not on the in-tree library
+    lib = tmp_path / "libsstgpu.so"
+    shutil.copyfile(_native.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
+                         capture_output=True, text=True, cwd=tmp_path)
     text = out.stdout + out.stderr
     if "gfx" not in text:  # older objdump: fall back to the raw bundle id string
         text = open(_native.LIB_PATH, "rb").read().decode("latin-1")
