@@ -554,6 +554,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
       q = a.qi[jj];
       rw = a.qrow[(size_t)jj * 128 + k];
     }
+    // the left child's lowest-rank byte, loaded now (before this rank's
+    // candidate and the wave's scans) so the two random lines are in flight
+    // together; only the budget test (rarely false) could have spared it
+    const int64_t m2e = (int64_t)m - qrow_w(rw);
+    const int lrv = live && m2e > 0 ? (int)a.lr[q.lr_off + m2e] : 0;
     const bool has = live && (f0 & kFCand);
     // the first group top (highest rank) at or above this lane; 64: the
     // group continues past the step's top (dead lanes -- above a partial
@@ -627,11 +632,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) voi
     const int64_t wk = qrow_w(rw);
     const bool mod = qrow_mod(rw);
     // the left branch (mass_table.py:424-441): attempted iff bit1 (m - w_k in
-    // R_k) and the budgets allow it; the budget test first, so a blocked
-    // modification row never fetches the lowest-rank byte (a random line)
+    // R_k, the lowest-rank byte loaded above) and the budgets allow it
     const int64_t m2 = (int64_t)m - wk;
     const bool bud = !mod || (A > 0 && B > 0);
-    const bool latt = live && bud && m2 >= 0 && (m2 == 0 || (int)a.lr[q.lr_off + m2] <= k);
+    const bool latt = live && bud && m2 >= 0 && (m2 == 0 || lrv <= k);
     if (live)
       a.flags[id] = (uint8_t)((latt ? kFLeft : 0) | (k > lo ? kFUp : 0) | (latt && m2 == 0 ? kFZero : 0) |
                               (hpar ? kFPar : 0));
