@@ -27,6 +27,52 @@ from .masses import PHOSPHATE_LINK_MASS
 from .pipeline import mask_rows, row_masks
 
 _PROGRESS = os.environ.get("SST_PIPE_PROGRESS") == "1"  # per-launch lines of the long stages on stderr
+
+# Stage 5's one device buffer per GPU for a pass's reach bitsets and
+# lowest-rank bytes (tens of GB at 100 k spectra): kept between length passes
+# unless the pass trims (allocating and releasing it per call put up to a few
+# seconds of hipMalloc / hipFree into the stage, from run to run).
+_LEN_BUF = {}
+
+
+def _length_buffer(dev, nbytes):
+    import torch
+
+    key = dev.index if dev.index is not None else 0
+    b = _LEN_BUF.get(key)
+    if b is None or b.numel() < nbytes:
+        _LEN_BUF.pop(key, None)
+        b = None
+        torch.cuda.empty_cache()
+        b = torch.empty(max(256, int(nbytes)), dtype=torch.uint8, device=dev)
+        _LEN_BUF[key] = b
+    return b
+
+
+def reserve_length_buffer(dev, nbytes=64 << 30):
+    """Allocate stage 5's reach buffer ahead (a serving process's warm-up):
+    passes whose batches fit it (length_device's reach_budget_bytes is the
+    default size) then allocate nothing.  At most a quarter of the device's
+    free memory (ranks sharing a GPU, the frontier's own workspace); a pass
+    that needs more allocates it then, as without a reservation."""
+    import torch
+
+    free, _ = torch.cuda.mem_get_info(dev)
+    try:
+        _length_buffer(dev, min(int(nbytes), int(free) // 4))
+    except torch.OutOfMemoryError:
+        release_length_buffer(dev)
+
+
+def release_length_buffer(dev=None):
+    """Free stage 5's reach buffer (every GPU's when dev is None)."""
+    import torch
+
+    if dev is None:
+        _LEN_BUF.clear()
+    else:
+        _LEN_BUF.pop(dev.index if dev.index is not None else 0, None)
+    torch.cuda.empty_cache()
 LB_NOT_RUN = -6  # length_device(spectra=...): the bounds of a spectrum outside the sample
 MAX_PEAKS = 16383  # peaks per spectrum (sst_internal.h kPipeMaxPeaksBig: above 4096 in HBM slices)
 ERR_BITS = {1: f"a spectrum has more than {MAX_PEAKS} peaks", 2: "a spectrum has more rows than the reserved slices hold",
@@ -859,7 +905,7 @@ class DeviceLength:
 @_one_stream
 def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0_len, sel=None, engine="frontier",
                                reach_budget_bytes=64 << 30, share_alphabets=True, length_chunk=1 << 30,
-                               soft_nodes=1 << 20, heavy_memo=1 << 22, frontier_workspace=0):
+                               soft_nodes=1 << 20, heavy_memo=1 << 22, frontier_workspace=0, keep_buffers=False):
     """compute_sequence_length_bound(dir="lower") and (dir="upper")
     (mass_table.py:343-487) for spectra on reduced alphabets (alpha_sk [S, 2]
     u64 row masks; su / ob the SequenceInformation masses; max_len [S]), with
@@ -1012,20 +1058,22 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
                 u1 += 1
             batches.append((u0, u1))
             u0 = u1
-        # one row-bitset and one lowest-rank buffer for every batch, sized to
-        # the largest (a fresh allocation of tens of GB per batch, and its
-        # release, idled the GPU for 0.1 s each)
+        # one buffer for every batch's row bitsets and lowest-rank bytes, sized
+        # to the largest (a fresh allocation of tens of GB per batch, and its
+        # release, idled the GPU for 0.1 s each), kept across passes unless
+        # keep_buffers is False (_length_buffer)
         kw_b = [int((K_u[b0:b1] * words_u[b0:b1]).sum()) for b0, b1 in batches]
         lw_b = [int(32 * words_u[b0:b1].sum()) for b0, b1 in batches]
-        bits_all = torch.empty(max([1] + kw_b), dtype=torch.int32, device=dev)
-        lr_all = torch.empty(max([1] + lw_b), dtype=torch.uint8, device=dev)
+        lr_at = [(4 * max(1, kw) + 255) // 256 * 256 for kw in kw_b]  # the lowest-rank bytes after the bitsets
+        buf = _length_buffer(dev, max([256] + [a_ + max(1, lw) for a_, lw in zip(lr_at, lw_b)]))
+        bits = lr = None
         for bi, (u0, u1) in enumerate(batches):
             nu = u1 - u0
             wb = words_u[u0:u1]
             off_u = np.concatenate([[0], np.cumsum(K_u[u0:u1] * wb)[:-1]]).astype(np.int64)
             lr_off = np.concatenate([[0], np.cumsum(32 * wb)[:-1]]).astype(np.int64)
-            bits = bits_all[:max(1, kw_b[bi])]
-            lr = lr_all[:max(1, lw_b[bi])]
+            bits = buf[:4 * max(1, kw_b[bi])].view(torch.int32)
+            lr = buf[lr_at[bi]:lr_at[bi] + max(1, lw_b[bi])]
             alu_t = torch.as_tensor(uniq[u0:u1].view(np.int64), device=dev).contiguous()
             wu_t = torch.as_tensor(wb, device=dev)
             ou_t = torch.as_tensor(off_u, device=dev)
@@ -1076,8 +1124,9 @@ def length_bounds_alpha_device(dp_table, alpha_sk, su, ob, max_len, caps_len, a0
                 print(f"[length] frontier batch {stats['batches']}: {n} spectra, {nu} alphabets, reach "
                       f"{t_reach:.3f}s, batch {time.perf_counter() - t_batch:.3f}s: {fd}", file=sys.stderr, flush=True)
             stats["batches"] += 1
-        del bits_all, lr_all, bits, lr
-        torch.cuda.empty_cache()
+        buf = bits = lr = None  # (views of the cached buffer)
+        if not keep_buffers:
+            release_length_buffer(dev)
 
     if engine == "frontier":
         frontier_pass(sel)
@@ -1115,8 +1164,11 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     spectra: the bounds for these spectra only (indices; the others get
     lb_status LB_NOT_RUN and Jaccard status SST_JAC_BOUNDS) -- a bounded
     sample where the reference's DFS is too large to replay for all.
-    trim: release the frontier's cached workspace (sst_ctx_trim) once the
-    bounds are done, so later stages and other allocators get that HBM."""
+    trim: release the frontier's cached workspace (sst_ctx_trim) and the
+    reach buffer once the bounds are done, so later stages and other
+    allocators get that HBM (trim=False keeps both for the next call, as a
+    serving process would; reserve_length_buffer sizes the reach buffer
+    ahead)."""
     import torch
 
     dt = dp_table.device_table
@@ -1147,7 +1199,7 @@ def length_device(dp_table, sk: DeviceSkeleton, alpha_dev, su_seq, obs_seq, reac
     lower, upper, lb_st, nodes, stats = length_bounds_alpha_device(
         dp_table, alpha_sk, su, ob, ml, caps_len, a0_len, sel=sel, engine=engine,
         reach_budget_bytes=reach_budget_bytes, share_alphabets=share_alphabets, length_chunk=length_chunk,
-        soft_nodes=soft_nodes, heavy_memo=heavy_memo, frontier_workspace=frontier_workspace)
+        soft_nodes=soft_nodes, heavy_memo=heavy_memo, frontier_workspace=frontier_workspace, keep_buffers=not trim)
     if trim:
         eng.trim()
     n_batches, U = stats["batches"], stats["distinct"]

