@@ -52,14 +52,15 @@ def _length_buffer(dev, nbytes):
 def reserve_length_buffer(dev, nbytes=64 << 30):
     """Allocate stage 5's reach buffer ahead (a serving process's warm-up):
     passes whose batches fit it (length_device's reach_budget_bytes is the
-    default size) then allocate nothing.  At most a quarter of the device's
-    free memory (ranks sharing a GPU, the frontier's own workspace); a pass
-    that needs more allocates it then, as without a reservation."""
+    default size) then allocate nothing.  At most half of the device's free
+    memory (ranks sharing a GPU; the frontier's own workspace is allocated in
+    the warm-up's pass before this); a pass that needs more allocates it
+    then, as without a reservation."""
     import torch
 
     free, _ = torch.cuda.mem_get_info(dev)
     try:
-        _length_buffer(dev, min(int(nbytes), int(free) // 4))
+        _length_buffer(dev, min(int(nbytes), int(free) // 2))
     except torch.OutOfMemoryError:
         release_length_buffer(dev)
 
