@@ -136,6 +136,18 @@ def test_rows_step_edge_spectra(dp):
         _check(dp, wl, res, a7, sample=300, seed=2)
 
 
+def test_rows_step_chunked(dp):
+    """More spectra than the wave kernels' chunk arrays hold one per wave (64
+    per CU: 16 384 on MI355X), so each wave takes a contiguous chunk of two
+    spectra: the chunk totals, the 64-chunk tile sums and each spectrum's
+    offsets within its chunk."""
+    import bench
+
+    wl = bench.build_workload(17000, 4711, dp)
+    res, a7 = _run(dp, wl)
+    _check(dp, wl, res, a7, sample=200, seed=4)
+
+
 def test_rows_step_capacity_overflow(dp):
     """A result too small for the step's queries is reported, not overrun
     (each chunk checks its own end against the result's capacity after its
