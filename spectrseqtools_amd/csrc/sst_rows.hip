@@ -33,12 +33,12 @@
 // totals of queries / hits / payload bytes and each chunk's sums;
 // k_rows_emit_w: each chunk's exclusive offsets from the 64-chunk tiles' sums
 // (added up by the count kernels) and its own tile's earlier chunks (no scan
-// launch),
-// each spectrum's offsets (its chunk's plus the chunk's earlier spectra's
-// totals), then its answers streamed back into statuses, the dense hit list
-// with pair-list refs and the dense payload; k_rows_count / k_rows_emit do the
-// same for the big spectra (rows to scratch, answered in both passes); the
-// last workgroup writes the header.  The result is sst_result's dense layout
+// launch), each spectrum's offsets (its chunk's plus the chunk's earlier
+// spectra's totals), then a pass over its windows writing every status byte,
+// and per block of 64 stored answers the dense hit records with pair-list
+// refs and the dense payload; k_rows_count / k_rows_emit do the same for the
+// big spectra (rows to scratch, answered in both passes); the last workgroup
+// writes the header.  The result is sst_result's dense layout
 // in query order (spectrum-major; START pairs, then END pairs).
 #include <hip/hip_runtime.h>
 #include <mutex>
